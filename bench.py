@@ -1,0 +1,240 @@
+"""RANSAC hypotheses/s for the 8-point F hot path on MI355X (BASELINE.json metric).
+
+One step = one full RANSAC run over one synthetic correspondence set already resident in
+HBM (config C2: N = 2000 correspondences, 30 % outliers, 100 000 hypotheses): sample,
+8-point solve, inlier count, select c*, reference-order re-score of the candidates, the
+fun.py:320-328 replay, S_RANSAC extraction, and the result copied back to the host.
+
+Multi-GPU (weak scaling): one process per GPU, each owning its own image pair (pairs shard
+with no data-path collective); after the timed steps the per-pair best models are exchanged
+with one RCCL all-gather over xGMI (inside the timed region).  Timing: barrier +
+device sync on both sides, max over ranks.
+
+Extra fields: roofline of the dominant kernel (k_f8_count) from HIP events on its stream,
+the numpy-exact parity mode measured on the same workload, and the oracle CPU baseline.
+"""
+import os
+
+os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")  # CPU baseline is single-core numpy
+os.environ.setdefault("OMP_NUM_THREADS", "1")
+
+import argparse  # noqa: E402
+import ctypes  # noqa: E402
+import json  # noqa: E402
+import sys  # noqa: E402
+import time  # noqa: E402
+
+import numpy as np  # noqa: E402
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "tsbb15-3d-reconstruction-project_amd"))
+sys.path.insert(0, REPO)
+
+from tsbb15_amd import _ffi, synth  # noqa: E402
+
+METRIC = "RANSAC hypotheses/sec (8-pt F, 2k corr) at 1/2/4/8 GPUs; % HBM roofline"
+N_CORR = 2000
+OUTLIERS = 0.30
+HYPS = 100_000
+PEAK_FP64_VALU_TFLOPS = 78.6   # 256 CU x 4 SIMD x 16 fp64 FMA lanes x 2 x 2.4 GHz
+PEAK_HBM_GBS = 8000.0
+FLOP_PER_CORR = 42             # score work per (hypothesis, correspondence)
+FLOP_SOLVE = 15000             # minimal solve per hypothesis
+
+
+def dist_env():
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")),
+            int(os.environ.get("WORLD_SIZE", "1")))
+
+
+class Dist:
+    """Barrier / max-reduce / broadcast for the harness (gloo on the host); the data-path
+    exchange uses RCCL through librsamd."""
+
+    def __init__(self, world):
+        self.world = world
+        self.pg = None
+        if world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max(self, x):
+        if self.world == 1:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def bcast_bytes(self, b, src=0):
+        if self.world == 1:
+            return b
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=src)
+        return obj[0]
+
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
+
+
+def cpu_baseline(p1, p2, budget_s):
+    """Oracle (numpy restatement of fun.py:303-328) on one host core, bounded sample."""
+    from oracle import ransac_ref
+    rs = np.random.RandomState(0)
+    done, t0 = 0, time.perf_counter()
+    chunk = 250
+    while True:
+        ransac_ref.ransac_f(p1, p2, r=chunk, rng=rs)
+        done += chunk
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": done / el, "unit": "hypotheses/s", "cores": 1, "kind": "port",
+            "sample": f"{done} hypotheses of the same C2 pair (N={p1.shape[1]}) through "
+                      f"oracle/ransac_ref.ransac_f (numpy, OpenBLAS 1 thread) in {el:.1f} s"}
+
+
+def load_pmc(n_corr, hyps):
+    path = os.path.join(REPO, "profiles", "r01_pmc_k_f8_count.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("n_corr") == n_corr and d.get("hypotheses") == hyps:
+            return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--hyps", type=int, default=HYPS)
+    ap.add_argument("--n", type=int, default=N_CORR)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity-mode", action="store_true")
+    args = ap.parse_args()
+
+    rank, local_rank, world = dist_env()
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
+    dist = Dist(world)
+    ctx = _ffi.Context(local_rank)
+
+    # one synthetic pair per rank (weak scaling: per-GPU work fixed)
+    p1, p2, _ = synth.two_view(args.n, OUTLIERS, seed=1 + rank)
+    H = args.hyps
+    plan = _ffi.F8Plan(ctx, args.n, H)
+    plan.set_points(p1, p2)
+
+    comm = world > 1
+    if comm:
+        uid = np.zeros(_ffi.COMM_ID_BYTES, np.uint8)
+        if rank == 0:
+            _ffi.check(_ffi.lib().rs_comm_unique_id(_ffi.ptr(uid, ctypes.c_uint8)))
+        uid = np.frombuffer(dist.bcast_bytes(uid.tobytes()), np.uint8).copy()
+        _ffi.check(_ffi.lib().rs_comm_init(ctx.handle, world, rank, _ffi.ptr(uid, ctypes.c_uint8)))
+
+    def step(i):
+        plan.run(H, mode=_ffi.SAMPLER_PHILOX, seed=0xC2, hyp_offset=i * H)
+        return plan.result()
+
+    for i in range(args.warmup):
+        step(i)
+    ctx.synchronize()
+    dist.barrier()
+    count_ms, solve_ms = [], []
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        r, _ = step(args.warmup + i)
+        km = plan.kernel_ms()
+        count_ms.append(km["count_ms"])
+        solve_ms.append(km["solve_ms"])
+    if comm:  # RCCL all-gather of the per-pair best models (F, count, index)
+        rec = np.zeros(12, np.float64)
+        rec[:9] = r.F[:]
+        rec[9], rec[10], rec[11] = r.best_count, r.best_index, rank
+        out = np.zeros(12 * world, np.float64)
+        _ffi.check(_ffi.lib().rs_comm_allgather(ctx.handle, rec.ctypes.data_as(ctypes.c_void_p),
+                                                out.ctypes.data_as(ctypes.c_void_p), rec.nbytes))
+        assert int(out.reshape(world, 12)[rank, 11]) == rank
+    ctx.synchronize()
+    el = time.perf_counter() - t0
+    dist.barrier()
+    el = dist.max(el)
+    total_hyps = H * args.steps * world
+    value = total_hyps / el
+
+    c_ms = float(np.mean(count_ms))
+    achieved = H * FLOP_PER_CORR * args.n / (c_ms * 1e-3) / 1e12
+    pmc = load_pmc(args.n, H)
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "hypotheses/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (tsbb15_amd.synth.two_view, SURVEY.md 8(d) scene; one pair per GPU)",
+        "config": {"workload": "C2: synthetic two-view pair, N=2000 correspondences, 30% "
+                               "outliers, 100000 hypotheses per RANSAC run, 8-point F, "
+                               "threshold 1.5 px",
+                   "n_corr": args.n, "hypotheses_per_step": H, "sampler": "philox (throughput)",
+                   "parallelism": f"pairs sharded, {world} pair(s) on {world} GPU(s)"},
+        "roofline": {"bound": "valu", "kernel": "k_f8_count",
+                     "achieved": achieved, "peak": PEAK_FP64_VALU_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / PEAK_FP64_VALU_TFLOPS,
+                     "traffic": pmc,
+                     "per_launch": {"hypotheses": H, "flop": H * FLOP_PER_CORR * args.n,
+                                    "avg_ms": c_ms},
+                     "note": "FP64 vector-ALU bound (SURVEY.md 8(d)); HBM traffic per launch "
+                             "from rocprofv3 PMC in profiles/ (traffic, bytes)"},
+        "kernels_ms": {"k_f8_count": c_ms, "k_f8_solve": float(np.mean(solve_ms))},
+    }
+    if pmc:
+        line["hbm_roofline"] = {"bound": "hbm", "achieved": pmc / (c_ms * 1e-3) / 1e9,
+                                "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                                "frac": pmc / (c_ms * 1e-3) / 1e9 / PEAK_HBM_GBS}
+
+    if rank == 0 and world == 1 and not args.no_parity_mode:
+        # numpy-exact sampling (host MT19937 replay) + the same GPU pipeline
+        key, pos = _ffi.np_seed(0)
+        ts = []
+        for _ in range(2):
+            t = time.perf_counter()
+            tup, key, pos = _ffi.np_choice_tuples(key, pos, args.n, 8, H)
+            plan.run(H, mode=_ffi.SAMPLER_TUPLES, tuples=tup)
+            plan.result()
+            ts.append(time.perf_counter() - t)
+        line["parity_mode"] = {"value": H / min(ts), "unit": "hypotheses/s",
+                               "note": "np.random legacy stream replayed bit-exactly on one "
+                                       "host core, then the GPU pipeline; host-sampler bound"}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(p1, p2, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if comm:
+        _ffi.lib().rs_comm_destroy(ctx.handle)
+    plan.close()
+    dist.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,182 @@
+/*
+ * rsamd.h -- C ABI of the MI355X-native RANSAC-F / PnP hot path.
+ *
+ * Drop-in boundary for bioengstrom/tsbb15-3d-reconstruction-project (snapshot v0).  The
+ * reference has no FFI: its boundary is the Python module surface.  Each
+ * entry point below names the reference function it replaces; the Python shims in
+ * tsbb15_amd/ (lab3.py, fun.py, ransac.py, pnp.py, cv.py) bind these through ctypes with the
+ * reference's names, argument meaning and ValueError behaviour.
+ *
+ * Conventions
+ *   - every function returns int status: RS_OK (0) or a negative RS_E* code; the message of
+ *     the last failure on the calling thread is rs_last_error();
+ *   - host pointers are caller-owned; the library never frees or keeps them;
+ *   - point sets are row-major (2, n) float64 arrays: row 0 = x (column), row 1 = y (row);
+ *   - a context owns one HIP device, one HIP stream and its device buffers; calls on one
+ *     context are synchronous (except the *_plan_run launches, which are stream-ordered and
+ *     completed by *_plan_result) and must not be issued concurrently from two threads.
+ */
+#ifndef RSAMD_H
+#define RSAMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RS_OK 0
+#define RS_EINVAL (-1)   /* shape / argument error  -> ValueError   */
+#define RS_EDEVICE (-2)  /* HIP runtime failure     -> RuntimeError */
+#define RS_ENODEV (-3)   /* no GPU visible          -> RuntimeError */
+#define RS_ECOMM (-4)    /* RCCL failure            -> RuntimeError */
+#define RS_ENOMEM (-5)   /* allocation failure      -> MemoryError  */
+
+#define RS_MT_N 624      /* MT19937 state words */
+
+const char *rs_last_error(void);
+int rs_version(void);
+
+/* ------------------------------------------------------------------------------------------
+ * Host samplers (no device).  Bit-exact replays of the reference's random streams.
+ * ---------------------------------------------------------------------------------------- */
+
+/* numpy legacy RandomState: init_genrand(seed) -> key[624], pos = 624 (np.random.seed). */
+int rs_np_seed(uint32_t seed, uint32_t *mt_key, int32_t *mt_pos);
+
+/* `count` draws of np.random.choice(np.arange(n), k, replace=False) (fun.py:305-306), i.e.
+ * permutation(n)[:k] by Fisher-Yates with masked-rejection random_interval.  Advances the
+ * (key, pos) state in place exactly as numpy does.  out: (count, k) int32. */
+int rs_np_choice_tuples(uint32_t *mt_key, int32_t *mt_pos, int64_t n, int32_t k, int64_t count,
+                        int32_t *out);
+
+/* CPython random.seed(int) with the int given as 32-bit little-endian words
+ * (init_by_array) -> key[624], pos = 624. */
+int rs_py_seed(const uint32_t *words, int32_t n_words, uint32_t *mt_key, int32_t *mt_pos);
+
+/* `count` draws of ransac.gen_rnd_indices(n, k) (ransac.py:12-19): random.shuffle(
+ * list(range(n)))[:k] with CPython's getrandbits rejection.  out: (count, k) int32. */
+int rs_py_shuffle_tuples(uint32_t *mt_key, int32_t *mt_pos, int64_t n, int32_t k, int64_t count,
+                         int32_t *out);
+
+/* ------------------------------------------------------------------------------------------
+ * Context
+ * ---------------------------------------------------------------------------------------- */
+typedef struct rs_ctx rs_ctx;
+
+int rs_device_count(int *n);
+int rs_ctx_create(int device, rs_ctx **out);
+int rs_ctx_destroy(rs_ctx *ctx);
+int rs_ctx_synchronize(rs_ctx *ctx);
+
+/* ------------------------------------------------------------------------------------------
+ * lab3 primitives on the GPU
+ * ---------------------------------------------------------------------------------------- */
+
+/* lab3.fmatrix_stls(pl, pr) (lab3.py:269-329): pl, pr (2, n), n >= 8; F_out (3,3) row-major,
+ * pl^T F pr = 0.  n == 8 uses the batched minimal kernel, n > 8 the least-squares kernel. */
+int rs_fmatrix_stls(rs_ctx *ctx, const double *pl, const double *pr, int64_t n, double *F_out);
+
+/* Batched minimal solves: tuples (count, 8) index (2, n) point sets; F_out (count, 9). */
+int rs_fmatrix_stls_batch(rs_ctx *ctx, const double *pl, const double *pr, int64_t n,
+                          const int32_t *tuples, int64_t count, double *F_out);
+
+/* lab3.fmatrix_residuals(F, x, y) (lab3.py:188-227): res_out (2, n). */
+int rs_fmatrix_residuals(rs_ctx *ctx, const double *F, const double *x, const double *y,
+                         int64_t n, double *res_out);
+
+/* ------------------------------------------------------------------------------------------
+ * RANSAC-F (fun.getFFromLabCode hypothesis loop, fun.py:298-328)
+ * ---------------------------------------------------------------------------------------- */
+#define RS_SAMPLER_PHILOX 0   /* throughput mode: counter-based Philox4x32-10 + Floyd   */
+#define RS_SAMPLER_TUPLES 1   /* parity mode: host tuples (rs_np_choice_tuples stream)  */
+
+typedef struct rs_f8_result {
+  double F[9];            /* F_RANSAC, row-major (fun.py:322)                          */
+  int64_t best_index;     /* hypothesis index within the run, -1 if none               */
+  int64_t best_count;     /* len(S_RANSAC)                                             */
+  double best_std;        /* d_RANSAC = np.std(d) of the winner (fun.py:323)           */
+  double best_norm;       /* np.linalg.norm(d) of the winner                           */
+  int64_t max_count_fast; /* c* of the counting kernel                                 */
+  int64_t n_candidates;   /* hypotheses re-scored in float64 reference order           */
+  int64_t guard_mismatch; /* candidates whose re-scored count differs from the fast one */
+} rs_f8_result;
+
+typedef struct rs_f8_candidate {
+  int64_t index;          /* hypothesis index (run-local + hyp_offset)                 */
+  int64_t count;          /* reference-order inlier count                              */
+  double std_d;           /* np.std(d)                                                 */
+  double norm_d;          /* np.linalg.norm(d)                                         */
+  double F[9];
+} rs_f8_candidate;
+
+typedef struct rs_f8_plan rs_f8_plan;
+
+/* A plan holds one correspondence set (n points) resident in HBM plus buffers for up to
+ * max_hyp hypotheses per run. */
+int rs_f8_plan_create(rs_ctx *ctx, int64_t n, int64_t max_hyp, rs_f8_plan **out);
+int rs_f8_plan_destroy(rs_f8_plan *plan);
+/* H2D upload of p1, p2 (2, n) row-major float64. */
+int rs_f8_plan_set_points(rs_f8_plan *plan, const double *p1, const double *p2);
+/* Enqueue one RANSAC run of H hypotheses: sample (mode), solve, count, select, re-score,
+ * replay the fun.py:320-328 rule, extract inliers.  Philox mode draws hypothesis i from
+ * counter (seed, hyp_offset + i); tuple mode reads host_tuples (H, 8) int32. */
+int rs_f8_plan_run(rs_f8_plan *plan, int64_t H, int32_t mode, uint64_t seed, uint64_t hyp_offset,
+                   const int32_t *host_tuples, double thresh);
+/* Wait for the last run and copy its result; inliers (S_RANSAC, ascending) up to cap. */
+int rs_f8_plan_result(rs_f8_plan *plan, rs_f8_result *out, int64_t *inliers, int64_t cap,
+                      int64_t *n_inliers);
+/* Candidates (count == max re-scored count) of the last run, ascending index, up to cap. */
+int rs_f8_plan_candidates(rs_f8_plan *plan, rs_f8_candidate *out, int64_t cap, int64_t *n_out);
+/* Per-hypothesis fast counts / models of the last run (test & diagnostics). */
+int rs_f8_plan_counts(rs_f8_plan *plan, int32_t *counts, int64_t H);
+int rs_f8_plan_models(rs_f8_plan *plan, double *F_out, int64_t H);
+/* Average device time (ms) of the counting kernel over the last run (HIP events). */
+int rs_f8_plan_kernel_ms(rs_f8_plan *plan, double *score_ms, double *solve_ms, double *total_ms);
+
+/* One call: numpy-exact sampling (advancing mt_key/mt_pos in place) + GPU evaluation. */
+int rs_f8_ransac_np(rs_ctx *ctx, const double *p1, const double *p2, int64_t n, int64_t H,
+                    uint32_t *mt_key, int32_t *mt_pos, double thresh, rs_f8_result *out,
+                    int64_t *inliers, int64_t cap, int64_t *n_inliers);
+
+/* ------------------------------------------------------------------------------------------
+ * PnP (pnp.py:132-160 DLT; ransac.py:37-113 consensus semantics)
+ * ---------------------------------------------------------------------------------------- */
+typedef struct rs_pnp_result {
+  double R[9];
+  double t[3];
+  int64_t best_index;
+  int64_t best_count;     /* D_med consensus size (ransac.py:104,108)                  */
+} rs_pnp_result;
+
+/* DLT pose from m >= 6 correspondences: X (m,3) world points, y (m,3) C-normalised
+ * homogeneous image points (pnp.py:132-160).  R_out (3,3), t_out (3). */
+int rs_pnp_dlt(rs_ctx *ctx, const double *X, const double *y, int64_t m, double *R_out,
+               double *t_out);
+
+/* RANSAC over DLT minimal samples.  Tuples (H, k) index the `high` set; consensus
+ * e = |pi(y) - pi(R x + t)|^2 <= thresh is counted on the `med` set.  mode as for F;
+ * in tuple mode host_tuples come from rs_py_shuffle_tuples. */
+int rs_pnp_ransac(rs_ctx *ctx, const double *X_med, const double *y_med, int64_t m_med,
+                  const double *X_high, const double *y_high, int64_t m_high, int32_t k,
+                  int64_t H, int32_t mode, uint64_t seed, const int32_t *host_tuples,
+                  double thresh, rs_pnp_result *out, int64_t *inl_med, int64_t *n_inl_med,
+                  int64_t *inl_high, int64_t *n_inl_high);
+
+/* ------------------------------------------------------------------------------------------
+ * Multi-GPU (RCCL over xGMI).  One process per GPU; the unique id travels out of band.
+ * ---------------------------------------------------------------------------------------- */
+#define RS_COMM_ID_BYTES 128
+int rs_comm_unique_id(uint8_t *id_out);
+int rs_comm_init(rs_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t *id);
+int rs_comm_destroy(rs_ctx *ctx);
+/* All-gather of `bytes` per rank (host buffers; staged through HBM). */
+int rs_comm_allgather(rs_ctx *ctx, const void *send, void *recv, int64_t bytes);
+/* Max-all-reduce of one int64 (c* across hypothesis shards). */
+int rs_comm_allreduce_max_i64(rs_ctx *ctx, int64_t *value);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RSAMD_H */

@@ -1,0 +1,109 @@
+"""Host C++ stream replays vs numpy / CPython themselves and vs the reference goldens.
+
+These run on the CPU: the samplers are host code inside librsamd.so (no device needed)."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden
+from tsbb15_amd import _ffi
+
+
+def _np_state(seed):
+    st = np.random.RandomState(seed).get_state()
+    return np.asarray(st[1], np.uint32), int(st[2])
+
+
+def test_np_seed_matches_randomstate():
+    for seed in (0, 1, 12345, 2**32 - 1):
+        key, pos = _ffi.np_seed(seed)
+        k2, p2 = _np_state(seed)
+        assert np.array_equal(key, k2) and pos == p2
+
+
+@pytest.mark.parametrize("n,count", [(8, 50), (9, 50), (37, 200), (257, 100), (1000, 20),
+                                     (2000, 10), (4096, 5), (10000, 3)])
+@pytest.mark.parametrize("seed", [0, 7])
+def test_np_choice_tuples_match_numpy(n, count, seed):
+    key, pos = _np_state(seed)
+    tup, key2, pos2 = _ffi.np_choice_tuples(key, pos, n, 8, count)
+    rs = np.random.RandomState(seed)
+    ref = np.array([rs.choice(np.arange(n), 8, replace=False) for _ in range(count)])
+    assert np.array_equal(tup, ref)
+    st = rs.get_state()
+    assert np.array_equal(key2, np.asarray(st[1], np.uint32)) and pos2 == st[2]
+
+
+def test_np_choice_other_k_and_midstream_state():
+    rs = np.random.RandomState(3)
+    rs.random_sample(1001)  # arbitrary position inside the 624-word block
+    st = rs.get_state()
+    tup, key2, pos2 = _ffi.np_choice_tuples(st[1], st[2], 300, 5, 40)
+    ref = np.array([rs.choice(np.arange(300), 5, replace=False) for _ in range(40)])
+    assert np.array_equal(tup, ref)
+    assert pos2 == rs.get_state()[2]
+
+
+def test_np_choice_errors():
+    key, pos = _np_state(0)
+    with pytest.raises(ValueError, match="larger sample"):
+        _ffi.np_choice_tuples(key, pos, 7, 8, 1)
+
+
+def test_np_choice_matches_reference_goldens():
+    z = golden("synth_c2.npz")
+    tup, key, pos = _ffi.np_choice_tuples(z["mt_key_in"], z["mt_pos_in"], 2000, 8,
+                                          len(z["tuples"]))
+    assert np.array_equal(tup, z["tuples"].astype(np.int32))
+    assert np.array_equal(key, z["mt_key_out"]) and pos == int(z["mt_pos_out"])
+    c1 = golden("dino_c1.npz")
+    for tag in ("clean", "noisy"):
+        n = c1[f"{tag}_p1"].shape[1]
+        tup, key, pos = _ffi.np_choice_tuples(c1[f"{tag}_mt_key_in"], c1[f"{tag}_mt_pos_in"], n,
+                                              8, 1000)
+        assert np.array_equal(tup, c1[f"{tag}_tuples"])
+        assert np.array_equal(key, c1[f"{tag}_mt_key_out"])
+        assert pos == int(c1[f"{tag}_mt_pos_out"])
+
+
+def _py_state(seed):
+    r = random.Random(seed)
+    st = r.getstate()[1]
+    return np.array(st[:624], np.uint32), int(st[624]), r
+
+
+@pytest.mark.parametrize("seed", [0, 1, 5, 12345, 2**40 + 17])
+def test_py_seed_matches_cpython(seed):
+    key, pos = _ffi.py_seed(seed)
+    k2, p2, _ = _py_state(seed)
+    assert np.array_equal(key, k2) and pos == p2
+
+
+@pytest.mark.parametrize("n,k,count", [(6, 6, 30), (37, 6, 100), (500, 6, 50), (1000, 8, 20)])
+def test_py_shuffle_matches_cpython(n, k, count):
+    key, pos, r = _py_state(42)
+    tup, key2, pos2 = _ffi.py_shuffle_tuples(key, pos, n, k, count)
+    ref = []
+    for _ in range(count):
+        x = list(range(n))
+        r.shuffle(x)
+        ref.append(x[:k])
+    assert np.array_equal(tup, np.array(ref))
+    st = r.getstate()[1]
+    assert np.array_equal(key2, np.array(st[:624], np.uint32)) and pos2 == st[624]
+
+
+def test_py_shuffle_matches_reference_gen_rnd_indices():
+    with open(os.path.join(GOLDEN, "ransac_misc.json")) as f:
+        misc = json.load(f)
+    key, pos = _ffi.py_seed(0)
+    tup, _, _ = _ffi.py_shuffle_tuples(key, pos, 500, 6, 50)
+    assert tup.tolist() == misc["gen_rnd_indices_seed0_500_6"]
+    key, pos = _ffi.py_seed(12345)
+    tup, _, _ = _ffi.py_shuffle_tuples(key, pos, 37, 6, 50)
+    assert tup.tolist() == misc["gen_rnd_indices_seed12345_37_6"]
+    with pytest.raises(ValueError, match="Cannot generate more indices"):
+        _ffi.py_shuffle_tuples(key, pos, 5, 6, 1)

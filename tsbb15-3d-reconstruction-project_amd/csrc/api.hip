@@ -1,0 +1,474 @@
+// C ABI (include/rsamd.h): contexts, F plans, single-shot lab3 ops.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "ctx.h"
+#include "device_math.h"
+#include "f8_kernels.h"
+
+namespace rs {
+
+static thread_local std::string g_err;
+
+void set_error(const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+
+int hip_fail(hipError_t e, const char *what) {
+  set_error("%s: %s", what, hipGetErrorString(e));
+  return e == hipErrorOutOfMemory ? RS_ENOMEM : RS_EDEVICE;
+}
+
+int ensure_scratch(rs_ctx *c, size_t bytes) {
+  if (c->scratch_bytes >= bytes) return RS_OK;
+  if (c->scratch) (void)hipFree(c->scratch);
+  c->scratch = nullptr;
+  c->scratch_bytes = 0;
+  size_t want = std::max<size_t>(bytes, 1 << 20);
+  hipError_t e = hipMalloc(&c->scratch, want);
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc(scratch)");
+  c->scratch_bytes = want;
+  return RS_OK;
+}
+
+}  // namespace rs
+
+using rs::fail;
+using rs::hip_fail;
+
+#define HIP_TRY(expr)                                     \
+  do {                                                    \
+    hipError_t e_ = (expr);                               \
+    if (e_ != hipSuccess) return hip_fail(e_, #expr);     \
+  } while (0)
+
+extern "C" const char *rs_last_error(void) { return rs::g_err.c_str(); }
+extern "C" int rs_version(void) { return 100; }
+
+extern "C" int rs_device_count(int *n) {
+  if (!n) return fail(RS_EINVAL, "null pointer");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) {
+    *n = 0;
+    if (e == hipErrorNoDevice) return RS_OK;
+    return hip_fail(e, "hipGetDeviceCount");
+  }
+  *n = c;
+  return RS_OK;
+}
+
+extern "C" int rs_ctx_create(int device, rs_ctx **out) {
+  if (!out) return fail(RS_EINVAL, "null pointer");
+  *out = nullptr;
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count == 0)
+    return fail(RS_ENODEV, "no HIP device visible (the MI355X path needs a GPU)");
+  if (device < 0 || device >= count) return fail(RS_EINVAL, "device index out of range");
+  HIP_TRY(hipSetDevice(device));
+  rs_ctx *c = new rs_ctx();
+  c->device = device;
+  e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return hip_fail(e, "hipStreamCreate");
+  }
+  *out = c;
+  return RS_OK;
+}
+
+extern "C" int rs_ctx_destroy(rs_ctx *c) {
+  if (!c) return RS_OK;
+  (void)hipSetDevice(c->device);
+  (void)rs_comm_destroy(c);
+  if (c->np_plan) rs_f8_plan_destroy(c->np_plan);
+  if (c->scratch) (void)hipFree(c->scratch);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return RS_OK;
+}
+
+extern "C" int rs_ctx_synchronize(rs_ctx *c) {
+  if (!c) return fail(RS_EINVAL, "null context");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return RS_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// F plans
+// ------------------------------------------------------------------------------------------
+struct rs_f8_plan {
+  rs_ctx *ctx = nullptr;
+  int64_t n = 0, max_hyp = 0, ld = 0;
+  double *d_p12 = nullptr;     // staging (2,n) p1 then (2,n) p2
+  rsd::Pt *d_pts = nullptr;    // AoS points
+  double *d_F = nullptr;       // 9 x ld SoA models
+  int *d_counts = nullptr;     // fast counts
+  int *d_tuples = nullptr;     // host tuples (parity mode)
+  int *d_cand = nullptr;       // ordered candidate hypothesis ids
+  int *d_status = nullptr;     // [c*, n_candidates]
+  int *d_ccount = nullptr;
+  double *d_cstd = nullptr, *d_cnorm = nullptr;
+  rsd::F8DevResult *d_res = nullptr;
+  rsd::F8DevResult *h_res = nullptr;  // pinned
+  size_t res_bytes = 0;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  int64_t last_H = 0;
+  bool pending = false, have_result = false;
+  int chunk_override = 0;
+};
+
+static void plan_free(rs_f8_plan *p) {
+  (void)hipFree(p->d_p12);
+  (void)hipFree(p->d_pts);
+  (void)hipFree(p->d_F);
+  (void)hipFree(p->d_counts);
+  (void)hipFree(p->d_tuples);
+  (void)hipFree(p->d_cand);
+  (void)hipFree(p->d_status);
+  (void)hipFree(p->d_ccount);
+  (void)hipFree(p->d_cstd);
+  (void)hipFree(p->d_cnorm);
+  (void)hipFree(p->d_res);
+  if (p->h_res) (void)hipHostFree(p->h_res);
+  for (auto &e : p->ev)
+    if (e) (void)hipEventDestroy(e);
+}
+
+extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_plan **out) {
+  if (!c || !out) return fail(RS_EINVAL, "null pointer");
+  *out = nullptr;
+  if (n < 8) return fail(RS_EINVAL, "Cannot take a larger sample than population when 'replace=False'");
+  if (n > (1LL << 30) || max_hyp < 1 || max_hyp > (1LL << 30))
+    return fail(RS_EINVAL, "plan dimensions out of range");
+  HIP_TRY(hipSetDevice(c->device));
+  auto *p = new rs_f8_plan();
+  p->ctx = c;
+  p->n = n;
+  p->max_hyp = max_hyp;
+  p->ld = (max_hyp + 63) / 64 * 64;
+  p->res_bytes = sizeof(rsd::F8DevResult) + sizeof(int64_t) * static_cast<size_t>(n);
+  if (const char *ch = std::getenv("RSAMD_CHUNK")) p->chunk_override = std::atoi(ch);
+  hipError_t e = hipSuccess;
+#define ALLOC(ptr, bytes)                                  \
+  if (e == hipSuccess) e = hipMalloc(&(ptr), (bytes));
+  ALLOC(p->d_p12, sizeof(double) * 4 * n);
+  ALLOC(p->d_pts, sizeof(rsd::Pt) * n);
+  ALLOC(p->d_F, sizeof(double) * 9 * p->ld);
+  ALLOC(p->d_counts, sizeof(int) * p->ld);
+  ALLOC(p->d_tuples, sizeof(int) * 8 * p->ld);
+  ALLOC(p->d_cand, sizeof(int) * p->ld);
+  ALLOC(p->d_status, sizeof(int) * 4);
+  ALLOC(p->d_ccount, sizeof(int) * p->ld);
+  ALLOC(p->d_cstd, sizeof(double) * p->ld);
+  ALLOC(p->d_cnorm, sizeof(double) * p->ld);
+  ALLOC(p->d_res, p->res_bytes);
+#undef ALLOC
+  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&p->h_res), p->res_bytes);
+  for (auto &ev : p->ev)
+    if (e == hipSuccess) e = hipEventCreate(&ev);
+  if (e != hipSuccess) {
+    plan_free(p);
+    delete p;
+    return hip_fail(e, "rs_f8_plan_create");
+  }
+  *out = p;
+  return RS_OK;
+}
+
+extern "C" int rs_f8_plan_destroy(rs_f8_plan *p) {
+  if (!p) return RS_OK;
+  (void)hipSetDevice(p->ctx->device);
+  (void)hipStreamSynchronize(p->ctx->stream);
+  plan_free(p);
+  delete p;
+  return RS_OK;
+}
+
+extern "C" int rs_f8_plan_set_points(rs_f8_plan *p, const double *p1, const double *p2) {
+  if (!p || !p1 || !p2) return fail(RS_EINVAL, "null pointer");
+  rs_ctx *c = p->ctx;
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t b = sizeof(double) * 2 * p->n;
+  HIP_TRY(hipMemcpyAsync(p->d_p12, p1, b, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(p->d_p12 + 2 * p->n, p2, b, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(rsd::launch_pack_points(p->d_p12, p->d_p12 + 2 * p->n, static_cast<int>(p->n),
+                                  p->d_pts, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return RS_OK;
+}
+
+static int choose_chunk(const rs_f8_plan *p, int64_t H) {
+  if (p->chunk_override > 0) return p->chunk_override;
+  const int64_t groups = (H + 63) / 64;
+  // aim for >= 8 units of work per SIMD (1024 SIMDs) without chunks below 64 points
+  int64_t nchunks = (8192 + groups - 1) / groups;
+  nchunks = std::max<int64_t>(1, std::min<int64_t>(nchunks, (p->n + 63) / 64));
+  return static_cast<int>((p->n + nchunks - 1) / nchunks);
+}
+
+extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t seed,
+                              uint64_t hyp_offset, const int32_t *host_tuples, double thresh) {
+  if (!p) return fail(RS_EINVAL, "null plan");
+  if (H < 1 || H > p->max_hyp) return fail(RS_EINVAL, "hypothesis count out of plan range");
+  if (mode != RS_SAMPLER_PHILOX && mode != RS_SAMPLER_TUPLES)
+    return fail(RS_EINVAL, "unknown sampler mode");
+  if (mode == RS_SAMPLER_TUPLES && !host_tuples) return fail(RS_EINVAL, "tuples required");
+  if (!(thresh == thresh)) return fail(RS_EINVAL, "threshold is NaN");
+  rs_ctx *c = p->ctx;
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const int n = static_cast<int>(p->n), h = static_cast<int>(H);
+  if (mode == RS_SAMPLER_TUPLES) {
+    for (int64_t i = 0; i < 8 * H; ++i)
+      if (host_tuples[i] < 0 || host_tuples[i] >= p->n)
+        return fail(RS_EINVAL, "tuple index out of range");
+    HIP_TRY(hipMemcpyAsync(p->d_tuples, host_tuples, sizeof(int) * 8 * H,
+                           hipMemcpyHostToDevice, s));
+  }
+  HIP_TRY(hipEventRecord(p->ev[0], s));
+  HIP_TRY(hipMemsetAsync(p->d_counts, 0, sizeof(int) * H, s));
+  HIP_TRY(rsd::launch_f8_solve(p->d_pts, n, h, mode, seed, hyp_offset, p->d_tuples, p->d_F,
+                               p->ld, s));
+  HIP_TRY(hipEventRecord(p->ev[1], s));
+  HIP_TRY(rsd::launch_f8_count(p->d_pts, n, h, p->d_F, p->ld, choose_chunk(p, H),
+                               thresh * thresh, p->d_counts, s));
+  HIP_TRY(hipEventRecord(p->ev[2], s));
+  HIP_TRY(rsd::launch_f8_select(p->d_counts, h, 1, p->d_cand, p->d_status, s));
+  const int sgrid = static_cast<int>(std::min<int64_t>((H + 3) / 4, 2048));
+  HIP_TRY(rsd::launch_f8_stats(p->d_pts, n, p->d_F, p->ld, p->d_cand, p->d_status, thresh,
+                               p->d_ccount, p->d_cstd, p->d_cnorm, sgrid, s));
+  HIP_TRY(rsd::launch_f8_replay(p->d_cand, p->d_status, p->d_counts, p->d_ccount, p->d_cstd,
+                                p->d_cnorm, p->d_F, p->ld, p->d_res, s));
+  HIP_TRY(rsd::launch_f8_inliers(p->d_pts, n, thresh, p->d_res, s));
+  HIP_TRY(hipEventRecord(p->ev[3], s));
+  HIP_TRY(hipMemcpyAsync(p->h_res, p->d_res, p->res_bytes, hipMemcpyDeviceToHost, s));
+  p->last_H = H;
+  p->pending = true;
+  p->have_result = true;
+  return RS_OK;
+}
+
+static int plan_wait(rs_f8_plan *p) {
+  if (!p->have_result) return fail(RS_EINVAL, "no run has been issued on this plan");
+  if (p->pending) {
+    HIP_TRY(hipSetDevice(p->ctx->device));
+    HIP_TRY(hipStreamSynchronize(p->ctx->stream));
+    p->pending = false;
+  }
+  return RS_OK;
+}
+
+extern "C" int rs_f8_plan_result(rs_f8_plan *p, rs_f8_result *out, int64_t *inliers, int64_t cap,
+                                 int64_t *n_inliers) {
+  if (!p || !out) return fail(RS_EINVAL, "null pointer");
+  int st = plan_wait(p);
+  if (st) return st;
+  const rsd::F8DevResult *r = p->h_res;
+  std::memcpy(out->F, r->F, sizeof(out->F));
+  out->best_index = r->best_index;
+  out->best_count = r->best_count;
+  out->best_std = r->best_std;
+  out->best_norm = r->best_norm;
+  out->max_count_fast = r->max_count_fast;
+  out->n_candidates = r->n_candidates;
+  out->guard_mismatch = r->guard_mismatch;
+  if (n_inliers) *n_inliers = r->n_inliers;
+  if (inliers && cap > 0)
+    std::memcpy(inliers, r->inliers, sizeof(int64_t) * std::min<int64_t>(cap, r->n_inliers));
+  return RS_OK;
+}
+
+extern "C" int rs_f8_plan_candidates(rs_f8_plan *p, rs_f8_candidate *out, int64_t cap,
+                                     int64_t *n_out) {
+  if (!p || !n_out) return fail(RS_EINVAL, "null pointer");
+  int st = plan_wait(p);
+  if (st) return st;
+  HIP_TRY(hipSetDevice(p->ctx->device));
+  int status[2];
+  HIP_TRY(hipMemcpy(status, p->d_status, sizeof(status), hipMemcpyDeviceToHost));
+  const int nc = status[1];
+  std::vector<int> cand(nc), cc(nc);
+  std::vector<double> cs(nc), cn(nc);
+  if (nc > 0) {
+    HIP_TRY(hipMemcpy(cand.data(), p->d_cand, sizeof(int) * nc, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(cc.data(), p->d_ccount, sizeof(int) * nc, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(cs.data(), p->d_cstd, sizeof(double) * nc, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(cn.data(), p->d_cnorm, sizeof(double) * nc, hipMemcpyDeviceToHost));
+  }
+  int cmax = 0;
+  for (int i = 0; i < nc; ++i) cmax = std::max(cmax, cc[i]);
+  int64_t k = 0;
+  for (int i = 0; i < nc; ++i) {
+    if (cc[i] != cmax || cmax == 0) continue;
+    if (out && k < cap) {
+      rs_f8_candidate &o = out[k];
+      o.index = cand[i];
+      o.count = cc[i];
+      o.std_d = cs[i];
+      o.norm_d = cn[i];
+      for (int q = 0; q < 9; ++q)
+        HIP_TRY(hipMemcpy(&o.F[q], p->d_F + q * p->ld + cand[i], sizeof(double),
+                          hipMemcpyDeviceToHost));
+    }
+    ++k;
+  }
+  *n_out = k;
+  return RS_OK;
+}
+
+extern "C" int rs_f8_plan_counts(rs_f8_plan *p, int32_t *counts, int64_t H) {
+  if (!p || !counts) return fail(RS_EINVAL, "null pointer");
+  int st = plan_wait(p);
+  if (st) return st;
+  if (H > p->last_H) return fail(RS_EINVAL, "H exceeds the last run");
+  HIP_TRY(hipSetDevice(p->ctx->device));
+  HIP_TRY(hipMemcpy(counts, p->d_counts, sizeof(int) * H, hipMemcpyDeviceToHost));
+  return RS_OK;
+}
+
+extern "C" int rs_f8_plan_models(rs_f8_plan *p, double *F_out, int64_t H) {
+  if (!p || !F_out) return fail(RS_EINVAL, "null pointer");
+  int st = plan_wait(p);
+  if (st) return st;
+  if (H > p->last_H) return fail(RS_EINVAL, "H exceeds the last run");
+  HIP_TRY(hipSetDevice(p->ctx->device));
+  std::vector<double> soa(static_cast<size_t>(9 * H));
+  for (int k = 0; k < 9; ++k)
+    HIP_TRY(hipMemcpy(soa.data() + k * H, p->d_F + k * p->ld, sizeof(double) * H,
+                      hipMemcpyDeviceToHost));
+  for (int64_t h = 0; h < H; ++h)
+    for (int k = 0; k < 9; ++k) F_out[h * 9 + k] = soa[k * H + h];
+  return RS_OK;
+}
+
+extern "C" int rs_f8_plan_kernel_ms(rs_f8_plan *p, double *score_ms, double *solve_ms,
+                                    double *total_ms) {
+  if (!p) return fail(RS_EINVAL, "null plan");
+  int st = plan_wait(p);
+  if (st) return st;
+  float a = 0, b = 0, t = 0;
+  HIP_TRY(hipEventElapsedTime(&a, p->ev[0], p->ev[1]));
+  HIP_TRY(hipEventElapsedTime(&b, p->ev[1], p->ev[2]));
+  HIP_TRY(hipEventElapsedTime(&t, p->ev[0], p->ev[3]));
+  if (solve_ms) *solve_ms = a;
+  if (score_ms) *score_ms = b;
+  if (total_ms) *total_ms = t;
+  return RS_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// numpy-exact one call (fun.getFFromLabCode loop)
+// ------------------------------------------------------------------------------------------
+extern "C" int rs_f8_ransac_np(rs_ctx *c, const double *p1, const double *p2, int64_t n,
+                               int64_t H, uint32_t *mt_key, int32_t *mt_pos, double thresh,
+                               rs_f8_result *out, int64_t *inliers, int64_t cap,
+                               int64_t *n_inliers) {
+  if (!c || !p1 || !p2 || !mt_key || !mt_pos || !out) return fail(RS_EINVAL, "null pointer");
+  if (n < 8)
+    return fail(RS_EINVAL, "Cannot take a larger sample than population when 'replace=False'");
+  if (H < 1) return fail(RS_EINVAL, "hypothesis count must be positive");
+  if (c->np_plan && (c->np_plan->n != n || c->np_plan->max_hyp < H)) {
+    rs_f8_plan_destroy(c->np_plan);
+    c->np_plan = nullptr;
+  }
+  int st;
+  if (!c->np_plan && (st = rs_f8_plan_create(c, n, H, &c->np_plan))) return st;
+  if ((st = rs_f8_plan_set_points(c->np_plan, p1, p2))) return st;
+  std::vector<int32_t> tuples(static_cast<size_t>(8 * H));
+  uint32_t key[RS_MT_N];
+  int32_t pos = *mt_pos;
+  std::memcpy(key, mt_key, sizeof(key));
+  if ((st = rs_np_choice_tuples(key, &pos, n, 8, H, tuples.data()))) return st;
+  if ((st = rs_f8_plan_run(c->np_plan, H, RS_SAMPLER_TUPLES, 0, 0, tuples.data(), thresh)))
+    return st;
+  if ((st = rs_f8_plan_result(c->np_plan, out, inliers, cap, n_inliers))) return st;
+  std::memcpy(mt_key, key, sizeof(key));
+  *mt_pos = pos;
+  return RS_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// lab3 primitives
+// ------------------------------------------------------------------------------------------
+extern "C" int rs_fmatrix_residuals(rs_ctx *c, const double *F, const double *x, const double *y,
+                                    int64_t n, double *res_out) {
+  if (!c || !F || !res_out || (n > 0 && (!x || !y))) return fail(RS_EINVAL, "null pointer");
+  if (n < 0 || n > (1LL << 30)) return fail(RS_EINVAL, "bad point count");
+  if (n == 0) return RS_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t bpts = sizeof(double) * 4 * n, bpt = sizeof(rsd::Pt) * n, bout = sizeof(double) * 2 * n;
+  int st = rs::ensure_scratch(c, bpts + bpt + bout + 128);
+  if (st) return st;
+  char *base = static_cast<char *>(c->scratch);
+  double *d_xy = reinterpret_cast<double *>(base);
+  rsd::Pt *d_pts = reinterpret_cast<rsd::Pt *>(base + bpts);
+  double *d_out = reinterpret_cast<double *>(base + bpts + bpt);
+  double *d_F = reinterpret_cast<double *>(base + bpts + bpt + bout);
+  HIP_TRY(hipMemcpyAsync(d_xy, x, sizeof(double) * 2 * n, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(d_xy + 2 * n, y, sizeof(double) * 2 * n, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(d_F, F, sizeof(double) * 9, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(rsd::launch_pack_points(d_xy, d_xy + 2 * n, static_cast<int>(n), d_pts, c->stream));
+  HIP_TRY(rsd::launch_residuals(d_pts, static_cast<int>(n), d_F, d_out, c->stream));
+  HIP_TRY(hipMemcpyAsync(res_out, d_out, bout, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return RS_OK;
+}
+
+extern "C" int rs_fmatrix_stls_batch(rs_ctx *c, const double *pl, const double *pr, int64_t n,
+                                     const int32_t *tuples, int64_t count, double *F_out) {
+  if (!c || !pl || !pr || !tuples || !F_out) return fail(RS_EINVAL, "null pointer");
+  if (n < 8 || count < 1 || count > (1LL << 28)) return fail(RS_EINVAL, "bad dimensions");
+  for (int64_t i = 0; i < 8 * count; ++i)
+    if (tuples[i] < 0 || tuples[i] >= n) return fail(RS_EINVAL, "tuple index out of range");
+  HIP_TRY(hipSetDevice(c->device));
+  const int64_t ld = (count + 63) / 64 * 64;
+  const size_t bpts = sizeof(double) * 4 * n, bpt = sizeof(rsd::Pt) * n;
+  const size_t btup = sizeof(int) * 8 * count, bF = sizeof(double) * 9 * ld;
+  int st = rs::ensure_scratch(c, bpts + bpt + btup + bF + 256);
+  if (st) return st;
+  char *base = static_cast<char *>(c->scratch);
+  double *d_xy = reinterpret_cast<double *>(base);
+  rsd::Pt *d_pts = reinterpret_cast<rsd::Pt *>(base + bpts);
+  int *d_tup = reinterpret_cast<int *>(base + bpts + bpt);
+  double *d_F = reinterpret_cast<double *>(base + ((bpts + bpt + btup + 63) / 64) * 64);
+  HIP_TRY(hipMemcpyAsync(d_xy, pl, sizeof(double) * 2 * n, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(d_xy + 2 * n, pr, sizeof(double) * 2 * n, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(d_tup, tuples, btup, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(rsd::launch_pack_points(d_xy, d_xy + 2 * n, static_cast<int>(n), d_pts, c->stream));
+  HIP_TRY(rsd::launch_f8_solve(d_pts, static_cast<int>(n), static_cast<int>(count),
+                               RS_SAMPLER_TUPLES, 0, 0, d_tup, d_F, ld, c->stream));
+  std::vector<double> soa(static_cast<size_t>(9 * ld));
+  HIP_TRY(hipMemcpyAsync(soa.data(), d_F, bF, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  for (int64_t h = 0; h < count; ++h)
+    for (int k = 0; k < 9; ++k) F_out[h * 9 + k] = soa[k * ld + h];
+  return RS_OK;
+}
+
+extern "C" int rs_fmatrix_stls(rs_ctx *c, const double *pl, const double *pr, int64_t n,
+                               double *F_out) {
+  if (!c || !pl || !pr || !F_out) return fail(RS_EINVAL, "null pointer");
+  if (n < 8) return fail(RS_EINVAL, "the 8-point algorithm needs at least 8 correspondences");
+  if (n == 8) {
+    const int32_t t[8] = {0, 1, 2, 3, 4, 5, 6, 7};
+    return rs_fmatrix_stls_batch(c, pl, pr, n, t, 1, F_out);
+  }
+  return rs::fmatrix_stls_lsq(c, pl, pr, n, F_out);
+}

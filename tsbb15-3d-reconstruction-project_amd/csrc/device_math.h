@@ -1,0 +1,276 @@
+// Device-side numerics shared by the F and PnP kernels (gfx950, float64).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rsd {
+
+// One correspondence, AoS 32 B: left image (x1, y1) = p1 column, right image (x2, y2) = p2
+// column (fun.getFFromLabCode(p1, p2), convention p1^T F p2 = 0, lab3.py:195-196).
+struct Pt {
+  double x1, y1, x2, y2;
+};
+
+// ----------------------------------------------------------------------------------------
+// Philox4x32-10 counter-based generator (throughput-mode sampler).
+// ----------------------------------------------------------------------------------------
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    k.x += 0x9E3779B9u;
+    k.y += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// Uniform k-subset of [0, n) by Floyd's algorithm with unbiased (Lemire) bounded draws.
+// Hypothesis `h` of stream `seed` uses Philox counters (h, 0..); every k-subset is equally
+// likely, as for np.random.choice(arange(n), k, replace=False).
+template <int K>
+__device__ __forceinline__ void floyd_sample(uint64_t seed, uint64_t h, int n, int (&idx)[K]) {
+  const uint2 key = make_uint2(static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
+  uint32_t ctr = 0;
+  uint4 blk = philox4x32_10(
+      make_uint4(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), ctr++, 0x5a17u), key);
+  int used = 0;
+  auto next = [&]() -> uint32_t {
+    if (used == 4) {
+      blk = philox4x32_10(
+          make_uint4(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), ctr++, 0x5a17u),
+          key);
+      used = 0;
+    }
+    const uint32_t w = used == 0 ? blk.x : used == 1 ? blk.y : used == 2 ? blk.z : blk.w;
+    ++used;
+    return w;
+  };
+#pragma unroll
+  for (int m = 0; m < K; ++m) {
+    const uint32_t j = static_cast<uint32_t>(n - K + m);
+    const uint32_t range = j + 1u;
+    uint64_t prod = static_cast<uint64_t>(next()) * range;
+    uint32_t low = static_cast<uint32_t>(prod);
+    if (low < range) {
+      const uint32_t thresh = (0u - range) % range;
+      while (low < thresh) {
+        prod = static_cast<uint64_t>(next()) * range;
+        low = static_cast<uint32_t>(prod);
+      }
+    }
+    const int t = static_cast<int>(prod >> 32);
+    bool dup = false;
+#pragma unroll
+    for (int q = 0; q < m; ++q) dup |= (idx[q] == t);
+    idx[m] = dup ? static_cast<int>(j) : t;
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// One-sided Jacobi SVD of a 3x3 matrix (row-major M).  On exit the columns of B = M V are
+// mutually orthogonal (their norms are the singular values) and V holds the right
+// singular vectors as columns.
+// ----------------------------------------------------------------------------------------
+__device__ __forceinline__ void jacobi_rot(double (&B)[9], double (&V)[9], int p, int q,
+                                           bool &rotated) {
+  const double a = B[p] * B[p] + B[3 + p] * B[3 + p] + B[6 + p] * B[6 + p];
+  const double b = B[q] * B[q] + B[3 + q] * B[3 + q] + B[6 + q] * B[6 + q];
+  const double g = B[p] * B[q] + B[3 + p] * B[3 + q] + B[6 + p] * B[6 + q];
+  if (fabs(g) > 1e-15 * sqrt(a * b)) {
+    rotated = true;
+    const double zeta = (b - a) / (2.0 * g);
+    const double t = copysign(1.0, zeta) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+    const double c = 1.0 / sqrt(1.0 + t * t);
+    const double s = c * t;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const double bp = B[3 * r + p], bq = B[3 * r + q];
+      B[3 * r + p] = c * bp - s * bq;
+      B[3 * r + q] = s * bp + c * bq;
+      const double vp = V[3 * r + p], vq = V[3 * r + q];
+      V[3 * r + p] = c * vp - s * vq;
+      V[3 * r + q] = s * vp + c * vq;
+    }
+  }
+}
+
+__device__ __forceinline__ void svd3_jacobi(double (&B)[9], double (&V)[9]) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) V[i] = (i % 4 == 0) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 12; ++sweep) {
+    bool rotated = false;
+    jacobi_rot(B, V, 0, 1, rotated);
+    jacobi_rot(B, V, 0, 2, rotated);
+    jacobi_rot(B, V, 1, 2, rotated);
+    if (!rotated) break;
+  }
+}
+
+// Nearest rank-2 matrix (lab3.py:321-324: U diag(s0, s1, 0) V): drop the term of the
+// smallest singular value, F2 = sum_{j != min} b_j v_j^T.
+__device__ __forceinline__ void enforce_rank2(const double (&Fs)[9], double (&F2)[9]) {
+  double B[9], V[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) B[i] = Fs[i];
+  svd3_jacobi(B, V);
+  double s[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) s[j] = B[j] * B[j] + B[3 + j] * B[3 + j] + B[6 + j] * B[6 + j];
+  const int m = (s[0] <= s[1] && s[0] <= s[2]) ? 0 : (s[1] <= s[2] ? 1 : 2);
+  const double w0 = m == 0 ? 0.0 : 1.0, w1 = m == 1 ? 0.0 : 1.0, w2 = m == 2 ? 0.0 : 1.0;
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      F2[3 * r + c] = w0 * B[3 * r + 0] * V[3 * c + 0] + w1 * B[3 * r + 1] * V[3 * c + 1] +
+                      w2 * B[3 * r + 2] * V[3 * c + 2];
+}
+
+// ----------------------------------------------------------------------------------------
+// Null vector of an R x C (R < C) matrix by Householder LQ: A Q = [L 0], null = Q e_{C-1}.
+// The reflector of row k is stored in place of row k (entries k..C-1).  For R = C-1 and
+// rank R this is the (unique up to sign) unit null vector, i.e. numpy svd's V[-1].
+// ----------------------------------------------------------------------------------------
+template <int R, int C>
+__device__ __forceinline__ void lq_null_vector(double (&A)[R][C], double (&q)[C]) {
+  double tau[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    double ss = 0.0;
+#pragma unroll
+    for (int j = k; j < C; ++j) ss = fma(A[k][j], A[k][j], ss);
+    const double nrm = sqrt(ss);
+    const double akk = A[k][k];
+    const double alpha = akk >= 0.0 ? -nrm : nrm;
+    const double denom = nrm * (nrm + fabs(akk));  // = v.v / 2
+    const double tk = denom > 0.0 ? 1.0 / denom : 0.0;
+    A[k][k] = akk - alpha;
+    tau[k] = tk;
+#pragma unroll
+    for (int i = k + 1; i < R; ++i) {
+      double w = 0.0;
+#pragma unroll
+      for (int j = k; j < C; ++j) w = fma(A[i][j], A[k][j], w);
+      w *= tk;
+#pragma unroll
+      for (int j = k; j < C; ++j) A[i][j] = fma(-w, A[k][j], A[i][j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < C; ++j) q[j] = (j == C - 1) ? 1.0 : 0.0;
+#pragma unroll
+  for (int k = R - 1; k >= 0; --k) {
+    double w = 0.0;
+#pragma unroll
+    for (int j = k; j < C; ++j) w = fma(A[k][j], q[j], w);
+    w *= tau[k];
+#pragma unroll
+    for (int j = k; j < C; ++j) q[j] = fma(-w, A[k][j], q[j]);
+  }
+}
+
+// numpy pairwise_sum order for exactly 8 contiguous values.
+__device__ __forceinline__ double sum8(const double (&a)[8]) {
+  return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+
+// lab3.py:288-295 for N = 8: H = [[s, 0, ox], [0, s, oy], [0, 0, 1]], s = 1/L, o = -m/L.
+__device__ __forceinline__ void scaling8(const double (&x)[8], const double (&y)[8], double &s,
+                                         double &ox, double &oy) {
+  const double xm = sum8(x) / 8.0;
+  const double ym = sum8(y) / 8.0;
+  double r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const double dx = x[j] - xm, dy = y[j] - ym;
+    r[j] = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
+  }
+  const double L = sqrt(0.0625 * sum8(r));  // 1./2./N with N = 8
+  s = 1.0 / L;
+  ox = -xm / L;
+  oy = -ym / L;
+}
+
+// The 8-point algorithm of lab3.fmatrix_stls (lab3.py:269-329) on one minimal sample.
+// xl, yl: left points (p1), xr, yr: right points (p2).  F row-major, pl^T F pr = 0.
+__device__ __forceinline__ void fmatrix8(const double (&xl)[8], const double (&yl)[8],
+                                         const double (&xr)[8], const double (&yr)[8],
+                                         double (&F)[9]) {
+  double s1, ox1, oy1, s2, ox2, oy2;
+  scaling8(xl, yl, s1, ox1, oy1);
+  scaling8(xr, yr, s2, ox2, oy2);
+  double A[8][9];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    // map_homography (lab3.py:301-306): x*H00 + y*H01 + H02 with H01 = 0
+    const double X = __dadd_rn(__dmul_rn(xl[k], s1), ox1);
+    const double Y = __dadd_rn(__dmul_rn(yl[k], s1), oy1);
+    const double x = __dadd_rn(__dmul_rn(xr[k], s2), ox2);
+    const double y = __dadd_rn(__dmul_rn(yr[k], s2), oy2);
+    // lab3.py:314: [X x, X y, X, Y x, Y y, Y, x, y, 1]
+    A[k][0] = X * x;
+    A[k][1] = X * y;
+    A[k][2] = X;
+    A[k][3] = Y * x;
+    A[k][4] = Y * y;
+    A[k][5] = Y;
+    A[k][6] = x;
+    A[k][7] = y;
+    A[k][8] = 1.0;
+  }
+  double fs[9];
+  lq_null_vector<8, 9>(A, fs);  // lab3.py:317-318: V[-1] of svd(A)
+  double F2[9];
+  enforce_rank2(fs, F2);
+  // lab3.py:327: F = S^T (F2 T); S = H(s1, ox1, oy1), T = H(s2, ox2, oy2)
+  double M[9];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    M[3 * r + 0] = F2[3 * r + 0] * s2;
+    M[3 * r + 1] = F2[3 * r + 1] * s2;
+    M[3 * r + 2] = (F2[3 * r + 0] * ox2 + F2[3 * r + 1] * oy2) + F2[3 * r + 2];
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    F[0 + c] = s1 * M[0 + c];
+    F[3 + c] = s1 * M[3 + c];
+    F[6 + c] = (ox1 * M[0 + c] + oy1 * M[3 + c]) + M[6 + c];
+  }
+}
+
+// Reference-order distance d = max(|res1|, |res2|) of lab3.fmatrix_residuals (lab3.py:
+// 210-227) followed by fun.py:316 (NaN-propagating max).  No FMA contraction.
+__device__ __forceinline__ double dist_ref(const double (&f)[9], const Pt &p) {
+#pragma clang fp contract(off)
+  const double l10 = (f[0] * p.x2 + f[1] * p.y2) + f[2];
+  const double l11 = (f[3] * p.x2 + f[4] * p.y2) + f[5];
+  const double l12 = (f[6] * p.x2 + f[7] * p.y2) + f[8];
+  const double l20 = (f[0] * p.x1 + f[3] * p.y1) + f[6];
+  const double l21 = (f[1] * p.x1 + f[4] * p.y1) + f[7];
+  const double l22 = (f[2] * p.x1 + f[5] * p.y1) + f[8];
+  const double l1s = sqrt(l10 * l10 + l11 * l11);
+  const double l2s = sqrt(l20 * l20 + l21 * l21);
+  const double r1 = ((l10 * p.x1 + l11 * p.y1) + l12) / l1s;
+  const double r2 = ((l20 * p.x2 + l21 * p.y2) + l22) / l2s;
+  const double a1 = fabs(r1), a2 = fabs(r2);
+  return (a1 != a1 || a2 != a2) ? __longlong_as_double(0x7ff8000000000000LL)
+                                : (a1 > a2 ? a1 : a2);
+}
+
+__device__ __forceinline__ void residuals_ref(const double (&f)[9], const Pt &p, double &r1,
+                                              double &r2) {
+#pragma clang fp contract(off)
+  const double l10 = (f[0] * p.x2 + f[1] * p.y2) + f[2];
+  const double l11 = (f[3] * p.x2 + f[4] * p.y2) + f[5];
+  const double l12 = (f[6] * p.x2 + f[7] * p.y2) + f[8];
+  const double l20 = (f[0] * p.x1 + f[3] * p.y1) + f[6];
+  const double l21 = (f[1] * p.x1 + f[4] * p.y1) + f[7];
+  const double l22 = (f[2] * p.x1 + f[5] * p.y1) + f[8];
+  r1 = ((l10 * p.x1 + l11 * p.y1) + l12) / sqrt(l10 * l10 + l11 * l11);
+  r2 = ((l20 * p.x2 + l21 * p.y2) + l22) / sqrt(l20 * l20 + l21 * l21);
+}
+
+}  // namespace rsd

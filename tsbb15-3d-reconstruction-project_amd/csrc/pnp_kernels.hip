@@ -1,0 +1,491 @@
+// PnP-RANSAC with the algebraic DLT of pnp.py:132-160, consensus of ransac.py:93-111.
+//
+//   k_pnp_solve   lane per hypothesis: sample k >= 6 points of the `high` set (Philox/Floyd or
+//                 host tuples from rs_py_shuffle_tuples), stream the 2k DLT rows
+//                 vec(r_l x^T) (rows 0,1 of [y]_x) through Givens rotations into a 12x12
+//                 upper-triangular R (78 doubles in VGPRs), smallest right singular vector by
+//                 inverse iteration on R^T R, C0 = (A|b), tau = sign det A, polar factor of
+//                 tau A by 3x3 Jacobi SVD, lambda = 3 tau / tr S, t = lambda b.
+//   k_pnp_count   lane per hypothesis x chunk of `med` points (wave-uniform scalar loads):
+//                 e = |pi(y) - pi(R x + t)|^2 <= thresh, evaluated division-free.
+//   k_pnp_select  one workgroup: first hypothesis with the largest count (strict ">").
+//   k_pnp_inliers consensus sets of the winner on `med` and `high` (reference order).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+#include "ctx.h"
+#include "device_math.h"
+#include "f8_kernels.h"
+
+namespace rsd {
+
+// A 3D<->2D correspondence: world point (X, Y, Z) and pi(y) = (y0/y2, y1/y2).
+struct PPt {
+  double X, Y, Z, u, v, y0, y1, y2;
+};
+
+constexpr int ridx(int j, int l) { return j * 12 - (j * (j - 1)) / 2 + (l - j); }
+
+__device__ __forceinline__ void givens_row(double (&R)[78], double (&a)[12]) {
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    const double r = R[ridx(j, j)];
+    const double rho = sqrt(r * r + a[j] * a[j]);
+    const double inv = rho > 0.0 ? 1.0 / rho : 0.0;
+    const double c = rho > 0.0 ? r * inv : 1.0;
+    const double s = a[j] * inv;
+    R[ridx(j, j)] = rho;
+#pragma unroll
+    for (int l = j + 1; l < 12; ++l) {
+      const double rl = R[ridx(j, l)];
+      R[ridx(j, l)] = c * rl + s * a[l];
+      a[l] = c * a[l] - s * rl;
+    }
+  }
+}
+
+__device__ __forceinline__ void dlt_rows(const PPt &p, double (&a0)[12], double (&a1)[12]) {
+  // [y]_x rows 0 and 1 (lab3.cross_matrix): r0 = (0, -y2, y1), r1 = (y2, 0, -y0)
+  const double r0[3] = {0.0, -p.y2, p.y1};
+  const double r1[3] = {p.y2, 0.0, -p.y0};
+  const double xh[4] = {p.X, p.Y, p.Z, 1.0};
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      a0[4 * i + j] = r0[i] * xh[j];
+      a1[4 * i + j] = r1[i] * xh[j];
+    }
+}
+
+// Smallest right singular vector of the matrix whose R factor is given.
+__device__ __forceinline__ void smallest_right_sv(const double (&R)[78], double (&x)[12]) {
+  double dinv[12];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) dinv[j] = 1.0 / R[ridx(j, j)];
+  // start: R^-1 e_11
+#pragma unroll
+  for (int j = 11; j >= 0; --j) {
+    double acc = (j == 11) ? 1.0 : 0.0;
+#pragma unroll
+    for (int l = j + 1; l < 12; ++l) acc -= R[ridx(j, l)] * x[l];
+    x[j] = acc * dinv[j];
+  }
+  for (int it = 0; it < 8; ++it) {
+    double nn = 0.0;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) nn += x[j] * x[j];
+    const double inv = 1.0 / sqrt(nn);
+    double z[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {  // R^T z = x
+      double acc = x[j] * inv;
+#pragma unroll
+      for (int i = 0; i < j; ++i) acc -= R[ridx(i, j)] * z[i];
+      z[j] = acc * dinv[j];
+    }
+#pragma unroll
+    for (int j = 11; j >= 0; --j) {  // R x = z
+      double acc = z[j];
+#pragma unroll
+      for (int l = j + 1; l < 12; ++l) acc -= R[ridx(j, l)] * x[l];
+      x[j] = acc * dinv[j];
+    }
+  }
+  double nn = 0.0;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) nn += x[j] * x[j];
+  const double inv = 1.0 / sqrt(nn);
+#pragma unroll
+  for (int j = 0; j < 12; ++j) x[j] *= inv;
+}
+
+// Constraint enforcement (pnp.py:141-145): C0 = (A | b) -> (R, t).
+__device__ __forceinline__ void enforce_pose(const double (&c0)[12], double (&Rm)[9],
+                                             double (&t)[3]) {
+  double A[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) A[3 * i + j] = c0[4 * i + j];
+  const double det = A[0] * (A[4] * A[8] - A[5] * A[7]) - A[1] * (A[3] * A[8] - A[5] * A[6]) +
+                     A[2] * (A[3] * A[7] - A[4] * A[6]);
+  const double tau = det > 0.0 ? 1.0 : (det < 0.0 ? -1.0 : (det == 0.0 ? 0.0 : det));
+  double B[9], V[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) B[i] = tau * A[i];
+  svd3_jacobi(B, V);
+  double s[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) s[j] = sqrt(B[j] * B[j] + B[3 + j] * B[3 + j] + B[6 + j] * B[6 + j]);
+  const double is0 = 1.0 / s[0], is1 = 1.0 / s[1], is2 = 1.0 / s[2];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      Rm[3 * r + c] = B[3 * r + 0] * is0 * V[3 * c + 0] + B[3 * r + 1] * is1 * V[3 * c + 1] +
+                      B[3 * r + 2] * is2 * V[3 * c + 2];
+  const double lam = 3.0 * tau / ((s[0] + s[1]) + s[2]);
+  t[0] = lam * c0[3];
+  t[1] = lam * c0[7];
+  t[2] = lam * c0[11];
+}
+
+template <class IndexAt>
+__device__ __forceinline__ void pnp_solve_points(const PPt *pts, int k, IndexAt index_at,
+                                                 double (&Rm)[9], double (&t)[3]) {
+  double R[78];
+#pragma unroll
+  for (int i = 0; i < 78; ++i) R[i] = 0.0;
+  for (int q = 0; q < k; ++q) {
+    double a0[12], a1[12];
+    dlt_rows(pts[index_at(q)], a0, a1);
+    givens_row(R, a0);
+    givens_row(R, a1);
+  }
+  double c0[12];
+  smallest_right_sv(R, c0);
+  enforce_pose(c0, Rm, t);
+}
+
+constexpr int kMaxK = 16;
+
+__global__ __launch_bounds__(256) void k_pnp_solve(const PPt *__restrict__ pts, int m, int H,
+                                                   int k, int mode, uint64_t seed,
+                                                   const int *__restrict__ tuples,
+                                                   double *__restrict__ Psoa, int64_t ld) {
+  const int h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= H) return;
+  double Rm[9], t[3];
+  if (mode == RSD_SAMPLER_PHILOX) {
+    int s6[6];
+    floyd_sample<6>(seed, static_cast<uint64_t>(h), m, s6);
+    // select from the 6 registers without dynamic indexing
+    pnp_solve_points(pts, 6, [&](int q) {
+      return q == 0 ? s6[0] : q == 1 ? s6[1] : q == 2 ? s6[2] : q == 3 ? s6[3] : q == 4 ? s6[4] : s6[5];
+    }, Rm, t);
+  } else {
+    const int *tup = tuples + static_cast<int64_t>(h) * k;
+    pnp_solve_points(pts, k, [&](int q) { return tup[q]; }, Rm, t);
+  }
+#pragma unroll
+  for (int q = 0; q < 9; ++q) Psoa[q * ld + h] = Rm[q];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) Psoa[(9 + q) * ld + h] = t[q];
+}
+
+// One-point DLT over all m correspondences (rs_pnp_dlt): single lane.
+__global__ void k_pnp_dlt_all(const PPt *__restrict__ pts, int m, double *__restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double R[78];
+  for (int i = 0; i < 78; ++i) R[i] = 0.0;
+  for (int q = 0; q < m; ++q) {
+    double a0[12], a1[12];
+    dlt_rows(pts[q], a0, a1);
+    givens_row(R, a0);
+    givens_row(R, a1);
+  }
+  double c0[12], Rm[9], t[3];
+  smallest_right_sv(R, c0);
+  enforce_pose(c0, Rm, t);
+  for (int q = 0; q < 9; ++q) out[q] = Rm[q];
+  for (int q = 0; q < 3; ++q) out[9 + q] = t[q];
+}
+
+__global__ __launch_bounds__(256) void k_pnp_count(const PPt *__restrict__ pts, int m, int H,
+                                                   const double *__restrict__ Psoa, int64_t ld,
+                                                   int chunk, int nchunks, double thresh,
+                                                   int *__restrict__ counts) {
+  const int lane = threadIdx.x & 63;
+  const int u = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int ngroups = (H + 63) >> 6;
+  if (u >= ngroups * nchunks) return;
+  const int g = u / nchunks, c = u - g * nchunks;
+  const int p0 = c * chunk, p1 = min(m, p0 + chunk);
+  const int h = g * 64 + lane;
+  const int hl = h < H ? h : H - 1;
+  double P[12];
+#pragma unroll
+  for (int q = 0; q < 12; ++q) P[q] = Psoa[q * ld + hl];
+  int cnt = 0;
+  for (int i = p0; i < p1; ++i) {
+    const PPt p = pts[i];
+    const double q0 = fma(P[0], p.X, fma(P[1], p.Y, fma(P[2], p.Z, P[9])));
+    const double q1 = fma(P[3], p.X, fma(P[4], p.Y, fma(P[5], p.Z, P[10])));
+    const double q2 = fma(P[6], p.X, fma(P[7], p.Y, fma(P[8], p.Z, P[11])));
+    // |pi(y) - pi(q)|^2 <= thr  <=>  (u q2 - q0)^2 + (v q2 - q1)^2 <= thr q2^2, q2 != 0
+    const double du = fma(p.u, q2, -q0), dv = fma(p.v, q2, -q1);
+    const double lhs = fma(du, du, dv * dv);
+    cnt += (q2 != 0.0 && lhs <= thresh * (q2 * q2)) ? 1 : 0;
+  }
+  if (h < H) atomicAdd(&counts[h], cnt);
+}
+
+struct PnpDevResult {
+  double R[9];
+  double t[3];
+  int64_t best_index, best_count, n_med, n_high;
+  int64_t inliers[];  // med then high
+};
+
+__global__ __launch_bounds__(1024) void k_pnp_select(const int *__restrict__ counts, int H,
+                                                     const double *__restrict__ Psoa,
+                                                     int64_t ld, PnpDevResult *res) {
+  __shared__ int sm[16], si[16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int bm = 0, bi = 0x7fffffff;
+  for (int i = tid; i < H; i += 1024) {
+    const int c = counts[i];
+    if (c > bm || (c == bm && i < bi)) {
+      bm = c;
+      bi = i;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int om = __shfl_xor(bm, o), oi = __shfl_xor(bi, o);
+    if (om > bm || (om == bm && oi < bi)) {
+      bm = om;
+      bi = oi;
+    }
+  }
+  if (lane == 0) {
+    sm[w] = bm;
+    si[w] = bi;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int q = 1; q < 16; ++q)
+      if (sm[q] > bm || (sm[q] == bm && si[q] < bi)) {
+        bm = sm[q];
+        bi = si[q];
+      }
+    // strict ">" against an initial best of 0 (ransac.py:108): zero consensus never wins
+    if (bm > 0) {
+      res->best_index = bi;
+      res->best_count = bm;
+      for (int q = 0; q < 9; ++q) res->R[q] = Psoa[q * ld + bi];
+      for (int q = 0; q < 3; ++q) res->t[q] = Psoa[(9 + q) * ld + bi];
+    } else {
+      res->best_index = -1;
+      res->best_count = 0;
+      for (int q = 0; q < 9; ++q) res->R[q] = 0.0;
+      for (int q = 0; q < 3; ++q) res->t[q] = 0.0;
+    }
+  }
+}
+
+// e = dpp_squared(y, R x + t) in the reference's order (ransac.py:21-35): pi, diff, dot.
+__device__ __forceinline__ bool pnp_inlier_ref(const double (&Rm)[9], const double (&t)[3],
+                                               const PPt &p, double thresh) {
+#pragma clang fp contract(off)
+  const double q0 = ((Rm[0] * p.X + Rm[1] * p.Y) + Rm[2] * p.Z) + t[0];
+  const double q1 = ((Rm[3] * p.X + Rm[4] * p.Y) + Rm[5] * p.Z) + t[1];
+  const double q2 = ((Rm[6] * p.X + Rm[7] * p.Y) + Rm[8] * p.Z) + t[2];
+  const double a0 = p.u - q0 / q2, a1 = p.v - q1 / q2;
+  const double a2 = p.y2 / p.y2 - q2 / q2;
+  const double e = (a0 * a0 + a1 * a1) + a2 * a2;
+  return thresh >= e;
+}
+
+__device__ void ordered_compact(const PPt *pts, int m, const double (&Rm)[9],
+                                const double (&t)[3], double thresh, bool have, int64_t *out,
+                                int64_t *n_out, int *woff, int *base_s) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid == 0) *base_s = 0;
+  __syncthreads();
+  for (int b = 0; b < m; b += 1024) {
+    const int i = b + tid;
+    const bool take = have && i < m && pnp_inlier_ref(Rm, t, pts[i], thresh);
+    const unsigned long long bal = __ballot(take);
+    const int before = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) woff[w] = __popcll(bal);
+    __syncthreads();
+    if (tid == 0) {
+      int acc = *base_s;
+      for (int q = 0; q < 16; ++q) {
+        const int tq = woff[q];
+        woff[q] = acc;
+        acc += tq;
+      }
+      *base_s = acc;
+    }
+    __syncthreads();
+    if (take) out[woff[w] + before] = i;
+    __syncthreads();
+  }
+  if (tid == 0) *n_out = *base_s;
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(1024) void k_pnp_inliers(const PPt *__restrict__ med, int m_med,
+                                                      const PPt *__restrict__ high, int m_high,
+                                                      double thresh, PnpDevResult *res) {
+  __shared__ int woff[16];
+  __shared__ int base_s;
+  const bool have = res->best_index >= 0;
+  double Rm[9], t[3];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) Rm[q] = res->R[q];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) t[q] = res->t[q];
+  ordered_compact(med, m_med, Rm, t, thresh, have, res->inliers, &res->n_med, woff, &base_s);
+  ordered_compact(high, m_high, Rm, t, thresh, have, res->inliers + m_med, &res->n_high, woff,
+                  &base_s);
+}
+
+__global__ __launch_bounds__(256) void k_pack_ppts(const double *__restrict__ X,
+                                                   const double *__restrict__ y, int m,
+                                                   PPt *__restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  PPt p;
+  p.X = X[3 * i];
+  p.Y = X[3 * i + 1];
+  p.Z = X[3 * i + 2];
+  p.y0 = y[3 * i];
+  p.y1 = y[3 * i + 1];
+  p.y2 = y[3 * i + 2];
+  p.u = p.y0 / p.y2;  // norm_p (ransac.py:21-23)
+  p.v = p.y1 / p.y2;
+  out[i] = p;
+}
+
+}  // namespace rsd
+
+// ------------------------------------------------------------------------------------------
+using rs::fail;
+using rs::hip_fail;
+
+#define HIP_TRY(expr)                                 \
+  do {                                                \
+    hipError_t e_ = (expr);                           \
+    if (e_ != hipSuccess) return hip_fail(e_, #expr); \
+  } while (0)
+
+static size_t align256(size_t b) { return (b + 255) / 256 * 256; }
+
+extern "C" int rs_pnp_dlt(rs_ctx *c, const double *X, const double *y, int64_t m, double *R_out,
+                          double *t_out) {
+  if (!c || !X || !y || !R_out || !t_out) return fail(RS_EINVAL, "null pointer");
+  if (m < 6) return fail(RS_EINVAL, "the DLT needs m >= 6 correspondences (pnp.py:134)");
+  if (m > (1 << 24)) return fail(RS_EINVAL, "too many correspondences");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t bin = align256(sizeof(double) * 3 * m), bp = align256(sizeof(rsd::PPt) * m);
+  int st = rs::ensure_scratch(c, 2 * bin + bp + 256);
+  if (st) return st;
+  char *base = static_cast<char *>(c->scratch);
+  double *dX = reinterpret_cast<double *>(base), *dy = reinterpret_cast<double *>(base + bin);
+  auto *dp = reinterpret_cast<rsd::PPt *>(base + 2 * bin);
+  double *dout = reinterpret_cast<double *>(base + 2 * bin + bp);
+  HIP_TRY(hipMemcpyAsync(dX, X, sizeof(double) * 3 * m, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(dy, y, sizeof(double) * 3 * m, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(rsd::k_pack_ppts, dim3((m + 255) / 256), dim3(256), 0, c->stream, dX, dy,
+                     static_cast<int>(m), dp);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(rsd::k_pnp_dlt_all, dim3(1), dim3(64), 0, c->stream, dp,
+                     static_cast<int>(m), dout);
+  HIP_TRY(hipGetLastError());
+  double out[12];
+  HIP_TRY(hipMemcpyAsync(out, dout, sizeof(out), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  std::memcpy(R_out, out, sizeof(double) * 9);
+  std::memcpy(t_out, out + 9, sizeof(double) * 3);
+  return RS_OK;
+}
+
+extern "C" int rs_pnp_ransac(rs_ctx *c, const double *X_med, const double *y_med, int64_t m_med,
+                             const double *X_high, const double *y_high, int64_t m_high,
+                             int32_t k, int64_t H, int32_t mode, uint64_t seed,
+                             const int32_t *host_tuples, double thresh, rs_pnp_result *out,
+                             int64_t *inl_med, int64_t *n_inl_med, int64_t *inl_high,
+                             int64_t *n_inl_high) {
+  if (!c || !X_med || !y_med || !X_high || !y_high || !out) return fail(RS_EINVAL, "null pointer");
+  if (k < 6 || k > rsd::kMaxK) return fail(RS_EINVAL, "sample size must be in [6, 16] for the DLT");
+  if (mode == RS_SAMPLER_PHILOX && k != 6) return fail(RS_EINVAL, "Philox sampler draws k = 6");
+  if (mode != RS_SAMPLER_PHILOX && mode != RS_SAMPLER_TUPLES) return fail(RS_EINVAL, "bad mode");
+  if (m_high < k)
+    return fail(RS_EINVAL,
+                "Cannot generate more indices than the amount of values in the set from which "
+                "they are extracted. n should therefore be smaller or equal to set_length");
+  if (m_med < 1 || H < 1 || H > (1LL << 28) || m_med > (1 << 26) || m_high > (1 << 26))
+    return fail(RS_EINVAL, "bad dimensions");
+  if (mode == RS_SAMPLER_TUPLES) {
+    if (!host_tuples) return fail(RS_EINVAL, "tuples required");
+    for (int64_t i = 0; i < H * k; ++i)
+      if (host_tuples[i] < 0 || host_tuples[i] >= m_high)
+        return fail(RS_EINVAL, "tuple index out of range");
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  const int64_t ld = (H + 63) / 64 * 64;
+  const size_t b_in_m = align256(sizeof(double) * 3 * m_med), b_in_h = align256(sizeof(double) * 3 * m_high);
+  const size_t b_pm = align256(sizeof(rsd::PPt) * m_med), b_ph = align256(sizeof(rsd::PPt) * m_high);
+  const size_t b_tup = align256(sizeof(int) * (mode == RS_SAMPLER_TUPLES ? H * k : 1));
+  const size_t b_P = align256(sizeof(double) * 12 * ld), b_cnt = align256(sizeof(int) * ld);
+  const size_t b_res = align256(sizeof(rsd::PnpDevResult) + sizeof(int64_t) * (m_med + m_high));
+  int st = rs::ensure_scratch(c, 2 * b_in_m + 2 * b_in_h + b_pm + b_ph + b_tup + b_P + b_cnt + b_res);
+  if (st) return st;
+  char *p = static_cast<char *>(c->scratch);
+  auto take = [&p](size_t b) {
+    char *q = p;
+    p += b;
+    return q;
+  };
+  double *dXm = reinterpret_cast<double *>(take(b_in_m));
+  double *dym = reinterpret_cast<double *>(take(b_in_m));
+  double *dXh = reinterpret_cast<double *>(take(b_in_h));
+  double *dyh = reinterpret_cast<double *>(take(b_in_h));
+  auto *pm = reinterpret_cast<rsd::PPt *>(take(b_pm));
+  auto *ph = reinterpret_cast<rsd::PPt *>(take(b_ph));
+  int *dtup = reinterpret_cast<int *>(take(b_tup));
+  double *dP = reinterpret_cast<double *>(take(b_P));
+  int *dcnt = reinterpret_cast<int *>(take(b_cnt));
+  auto *dres = reinterpret_cast<rsd::PnpDevResult *>(take(b_res));
+  hipStream_t s = c->stream;
+  HIP_TRY(hipMemcpyAsync(dXm, X_med, sizeof(double) * 3 * m_med, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(dym, y_med, sizeof(double) * 3 * m_med, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(dXh, X_high, sizeof(double) * 3 * m_high, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(dyh, y_high, sizeof(double) * 3 * m_high, hipMemcpyHostToDevice, s));
+  if (mode == RS_SAMPLER_TUPLES)
+    HIP_TRY(hipMemcpyAsync(dtup, host_tuples, sizeof(int) * H * k, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(rsd::k_pack_ppts, dim3((m_med + 255) / 256), dim3(256), 0, s, dXm, dym,
+                     static_cast<int>(m_med), pm);
+  hipLaunchKernelGGL(rsd::k_pack_ppts, dim3((m_high + 255) / 256), dim3(256), 0, s, dXh, dyh,
+                     static_cast<int>(m_high), ph);
+  HIP_TRY(hipMemsetAsync(dcnt, 0, sizeof(int) * H, s));
+  hipLaunchKernelGGL(rsd::k_pnp_solve, dim3((H + 255) / 256), dim3(256), 0, s, ph,
+                     static_cast<int>(m_high), static_cast<int>(H), k, mode, seed, dtup, dP, ld);
+  HIP_TRY(hipGetLastError());
+  const int64_t groups = (H + 63) / 64;
+  int64_t nch = std::max<int64_t>(1, std::min<int64_t>((8192 + groups - 1) / groups, (m_med + 63) / 64));
+  const int chunk = static_cast<int>((m_med + nch - 1) / nch);
+  nch = (m_med + chunk - 1) / chunk;
+  const int64_t units = groups * nch;
+  hipLaunchKernelGGL(rsd::k_pnp_count, dim3((units + 3) / 4), dim3(256), 0, s, pm,
+                     static_cast<int>(m_med), static_cast<int>(H), dP, ld, chunk,
+                     static_cast<int>(nch), thresh, dcnt);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(rsd::k_pnp_select, dim3(1), dim3(1024), 0, s, dcnt, static_cast<int>(H), dP,
+                     ld, dres);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(rsd::k_pnp_inliers, dim3(1), dim3(1024), 0, s, pm, static_cast<int>(m_med),
+                     ph, static_cast<int>(m_high), thresh, dres);
+  HIP_TRY(hipGetLastError());
+  std::vector<char> host(sizeof(rsd::PnpDevResult) + sizeof(int64_t) * (m_med + m_high));
+  HIP_TRY(hipMemcpyAsync(host.data(), dres, host.size(), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  const auto *r = reinterpret_cast<const rsd::PnpDevResult *>(host.data());
+  std::memcpy(out->R, r->R, sizeof(out->R));
+  std::memcpy(out->t, r->t, sizeof(out->t));
+  out->best_index = r->best_index;
+  out->best_count = r->best_count;
+  if (n_inl_med) *n_inl_med = r->n_med;
+  if (n_inl_high) *n_inl_high = r->n_high;
+  if (inl_med) std::memcpy(inl_med, r->inliers, sizeof(int64_t) * r->n_med);
+  if (inl_high) std::memcpy(inl_high, r->inliers + m_med, sizeof(int64_t) * r->n_high);
+  return RS_OK;
+}

@@ -1,0 +1,197 @@
+// Host replays of the reference's random streams (bit-exact).
+//
+//  * numpy legacy RandomState (fun.py:306 np.random.choice(arange(N), 8, replace=False)):
+//    MT19937 init_genrand seeding; choice(replace=False) == permutation(N)[:k], a
+//    Fisher-Yates sweep i = N-1..1 with j = random_interval(i) (u32 & smear-mask, retry
+//    while > i).  SURVEY.md 8(a) row a-R.
+//  * CPython random (ransac.py:17 random.shuffle): init_by_array seeding; shuffle sweep
+//    i = N-1..1 with j = randbelow(i+1), randbelow(n) = getrandbits(bitlen(n)) retried
+//    while >= n, getrandbits(k) = u32 >> (32-k).  SURVEY.md 8(a) row a-8.
+//
+// The state (key[624], pos) is the one np.random.get_state() / random.getstate() expose,
+// so the Python shims hand it in and write the advanced state back (drop-in fidelity).
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+
+namespace {
+
+constexpr int kN = 624;
+constexpr int kM = 397;
+constexpr uint32_t kMatrixA = 0x9908b0dfu;
+constexpr uint32_t kUpper = 0x80000000u;
+constexpr uint32_t kLower = 0x7fffffffu;
+
+struct Mt {
+  uint32_t key[kN];
+  int pos;
+
+  void load(const uint32_t *k, int32_t p) {
+    std::memcpy(key, k, sizeof(key));
+    pos = p;
+  }
+  void store(uint32_t *k, int32_t *p) const {
+    std::memcpy(k, key, sizeof(key));
+    *p = pos;
+  }
+  // The classic mt19937 twist (numpy mt19937_gen == CPython genrand_uint32 refill).
+  void twist() {
+    int i = 0;
+    for (; i < kN - kM; ++i) {
+      uint32_t y = (key[i] & kUpper) | (key[i + 1] & kLower);
+      key[i] = key[i + kM] ^ (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
+    }
+    for (; i < kN - 1; ++i) {
+      uint32_t y = (key[i] & kUpper) | (key[i + 1] & kLower);
+      key[i] = key[i + (kM - kN)] ^ (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
+    }
+    uint32_t y = (key[kN - 1] & kUpper) | (key[0] & kLower);
+    key[kN - 1] = key[kM - 1] ^ (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
+    pos = 0;
+  }
+  inline uint32_t next() {
+    if (pos >= kN) twist();
+    uint32_t y = key[pos++];
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+  }
+};
+
+void init_genrand(uint32_t *key, uint32_t s) {
+  key[0] = s;
+  for (int i = 1; i < kN; ++i)
+    key[i] = 1812433253u * (key[i - 1] ^ (key[i - 1] >> 30)) + static_cast<uint32_t>(i);
+}
+
+inline uint32_t smear_mask(uint32_t v) {
+  v |= v >> 1;
+  v |= v >> 2;
+  v |= v >> 4;
+  v |= v >> 8;
+  v |= v >> 16;
+  return v;
+}
+
+inline int bit_length(uint32_t v) { return v ? 32 - __builtin_clz(v) : 0; }
+
+}  // namespace
+
+extern "C" int rs_np_seed(uint32_t seed, uint32_t *mt_key, int32_t *mt_pos) {
+  if (!mt_key || !mt_pos) return rs::fail(RS_EINVAL, "rs_np_seed: null pointer");
+  init_genrand(mt_key, seed);
+  *mt_pos = kN;
+  return RS_OK;
+}
+
+extern "C" int rs_py_seed(const uint32_t *words, int32_t n_words, uint32_t *mt_key,
+                          int32_t *mt_pos) {
+  if (!mt_key || !mt_pos || n_words < 0 || (n_words > 0 && !words))
+    return rs::fail(RS_EINVAL, "rs_py_seed: bad arguments");
+  // CPython random_seed(): an int seed 0 is the key [0]; init_by_array (mt19937ar.c).
+  uint32_t zero = 0;
+  const uint32_t *key = n_words ? words : &zero;
+  const int len = n_words ? n_words : 1;
+  uint32_t *mt = mt_key;
+  init_genrand(mt, 19650218u);
+  int i = 1, j = 0;
+  for (int k = (kN > len ? kN : len); k; --k) {
+    mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1664525u)) + key[j] +
+            static_cast<uint32_t>(j);
+    ++i;
+    ++j;
+    if (i >= kN) {
+      mt[0] = mt[kN - 1];
+      i = 1;
+    }
+    if (j >= len) j = 0;
+  }
+  for (int k = kN - 1; k; --k) {
+    mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1566083941u)) - static_cast<uint32_t>(i);
+    ++i;
+    if (i >= kN) {
+      mt[0] = mt[kN - 1];
+      i = 1;
+    }
+  }
+  mt[0] = 0x80000000u;
+  *mt_pos = kN;
+  return RS_OK;
+}
+
+namespace {
+
+// One Fisher-Yates hypothesis over a scratch identity permutation; writes x[0:k].
+template <class Draw>
+inline void fisher_yates_prefix(std::vector<int32_t> &perm, const std::vector<int32_t> &iota,
+                                int64_t n, int32_t k, int32_t *out, Draw draw) {
+  std::memcpy(perm.data(), iota.data(), sizeof(int32_t) * static_cast<size_t>(n));
+  int32_t *x = perm.data();
+  for (int64_t i = n - 1; i >= 1; --i) {
+    const int64_t j = draw(static_cast<uint32_t>(i));
+    const int32_t t = x[i];
+    x[i] = x[j];
+    x[j] = t;
+  }
+  std::memcpy(out, x, sizeof(int32_t) * static_cast<size_t>(k));
+}
+
+}  // namespace
+
+extern "C" int rs_np_choice_tuples(uint32_t *mt_key, int32_t *mt_pos, int64_t n, int32_t k,
+                                   int64_t count, int32_t *out) {
+  if (!mt_key || !mt_pos || (count > 0 && !out))
+    return rs::fail(RS_EINVAL, "rs_np_choice_tuples: null pointer");
+  if (k < 0 || count < 0) return rs::fail(RS_EINVAL, "negative dimensions are not allowed");
+  if (k > n)  // numpy: "Cannot take a larger sample than population when 'replace=False'"
+    return rs::fail(RS_EINVAL,
+                    "Cannot take a larger sample than population when 'replace=False'");
+  if (n > 0x7fffffffLL) return rs::fail(RS_EINVAL, "population too large");
+  if (*mt_pos < 0 || *mt_pos > kN) return rs::fail(RS_EINVAL, "bad MT19937 position");
+  Mt mt;
+  mt.load(mt_key, *mt_pos);
+  std::vector<int32_t> perm(static_cast<size_t>(n > 0 ? n : 1)), iota(perm.size());
+  for (int64_t i = 0; i < n; ++i) iota[static_cast<size_t>(i)] = static_cast<int32_t>(i);
+  auto draw = [&mt](uint32_t max) -> int64_t {  // numpy random_interval(max), max < 2^32
+    const uint32_t mask = smear_mask(max);
+    uint32_t v;
+    while ((v = (mt.next() & mask)) > max) {
+    }
+    return v;
+  };
+  for (int64_t h = 0; h < count; ++h) fisher_yates_prefix(perm, iota, n, k, out + h * k, draw);
+  mt.store(mt_key, mt_pos);
+  return RS_OK;
+}
+
+extern "C" int rs_py_shuffle_tuples(uint32_t *mt_key, int32_t *mt_pos, int64_t n, int32_t k,
+                                    int64_t count, int32_t *out) {
+  if (!mt_key || !mt_pos || (count > 0 && !out))
+    return rs::fail(RS_EINVAL, "rs_py_shuffle_tuples: null pointer");
+  if (n < k)  // ransac.py:13-14
+    return rs::fail(RS_EINVAL,
+                    "Cannot generate more indices than the amount of values in the set from "
+                    "which they are extracted. n should therefore be smaller or equal to "
+                    "set_length");
+  if (k < 0 || count < 0 || n > 0x7fffffffLL) return rs::fail(RS_EINVAL, "bad dimensions");
+  if (*mt_pos < 0 || *mt_pos > kN) return rs::fail(RS_EINVAL, "bad MT19937 position");
+  Mt mt;
+  mt.load(mt_key, *mt_pos);
+  std::vector<int32_t> perm(static_cast<size_t>(n > 0 ? n : 1)), iota(perm.size());
+  for (int64_t i = 0; i < n; ++i) iota[static_cast<size_t>(i)] = static_cast<int32_t>(i);
+  auto draw = [&mt](uint32_t i) -> int64_t {  // randbelow(i + 1)
+    const uint32_t lim = i + 1;
+    const int kb = bit_length(lim);
+    uint32_t r;
+    while ((r = (mt.next() >> (32 - kb))) >= lim) {
+    }
+    return r;
+  };
+  for (int64_t h = 0; h < count; ++h) fisher_yates_prefix(perm, iota, n, k, out + h * k, draw);
+  mt.store(mt_key, mt_pos);
+  return RS_OK;
+}

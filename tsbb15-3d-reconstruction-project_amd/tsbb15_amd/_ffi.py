@@ -1,0 +1,296 @@
+"""ctypes binding of lib/librsamd.so (C ABI declared in include/rsamd.h).
+
+The library is built in-tree (``make -C csrc``, or ``__graft_entry__.build()``).  There is no
+fallback: if the shared object is missing or no GPU is visible, the compute entry points
+raise.  Status codes map to the reference's exception types (ValueError for shape/argument
+errors, as lab3.py:207-208 / lab3.py:283-284 / ransac.py:13-14 raise).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("RSAMD_LIB", os.path.join(_PKG_ROOT, "lib", "librsamd.so"))
+HEADER_PATH = os.path.join(os.path.dirname(_PKG_ROOT), "include", "rsamd.h")
+
+RS_OK, RS_EINVAL, RS_EDEVICE, RS_ENODEV, RS_ECOMM, RS_ENOMEM = 0, -1, -2, -3, -4, -5
+SAMPLER_PHILOX, SAMPLER_TUPLES = 0, 1
+MT_N = 624
+COMM_ID_BYTES = 128
+
+_dp = C.POINTER(C.c_double)
+_i32p = C.POINTER(C.c_int32)
+_i64p = C.POINTER(C.c_int64)
+_u32p = C.POINTER(C.c_uint32)
+_u8p = C.POINTER(C.c_uint8)
+
+
+class F8Result(C.Structure):
+    _fields_ = [("F", C.c_double * 9), ("best_index", C.c_int64), ("best_count", C.c_int64),
+                ("best_std", C.c_double), ("best_norm", C.c_double),
+                ("max_count_fast", C.c_int64), ("n_candidates", C.c_int64),
+                ("guard_mismatch", C.c_int64)]
+
+
+class F8Candidate(C.Structure):
+    _fields_ = [("index", C.c_int64), ("count", C.c_int64), ("std_d", C.c_double),
+                ("norm_d", C.c_double), ("F", C.c_double * 9)]
+
+
+class PnpResult(C.Structure):
+    _fields_ = [("R", C.c_double * 9), ("t", C.c_double * 3), ("best_index", C.c_int64),
+                ("best_count", C.c_int64)]
+
+
+_SIGS = {
+    "rs_last_error": (C.c_char_p, []),
+    "rs_version": (C.c_int, []),
+    "rs_np_seed": (C.c_int, [C.c_uint32, _u32p, _i32p]),
+    "rs_np_choice_tuples": (C.c_int, [_u32p, _i32p, C.c_int64, C.c_int32, C.c_int64, _i32p]),
+    "rs_py_seed": (C.c_int, [_u32p, C.c_int32, _u32p, _i32p]),
+    "rs_py_shuffle_tuples": (C.c_int, [_u32p, _i32p, C.c_int64, C.c_int32, C.c_int64, _i32p]),
+    "rs_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "rs_ctx_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    "rs_ctx_destroy": (C.c_int, [C.c_void_p]),
+    "rs_ctx_synchronize": (C.c_int, [C.c_void_p]),
+    "rs_fmatrix_stls": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp]),
+    "rs_fmatrix_stls_batch": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _i32p, C.c_int64, _dp]),
+    "rs_fmatrix_residuals": (C.c_int, [C.c_void_p, _dp, _dp, _dp, C.c_int64, _dp]),
+    "rs_f8_plan_create": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.POINTER(C.c_void_p)]),
+    "rs_f8_plan_destroy": (C.c_int, [C.c_void_p]),
+    "rs_f8_plan_set_points": (C.c_int, [C.c_void_p, _dp, _dp]),
+    "rs_f8_plan_run": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.c_uint64, C.c_uint64,
+                                 _i32p, C.c_double]),
+    "rs_f8_plan_result": (C.c_int, [C.c_void_p, C.POINTER(F8Result), _i64p, C.c_int64, _i64p]),
+    "rs_f8_plan_candidates": (C.c_int, [C.c_void_p, C.POINTER(F8Candidate), C.c_int64, _i64p]),
+    "rs_f8_plan_counts": (C.c_int, [C.c_void_p, _i32p, C.c_int64]),
+    "rs_f8_plan_models": (C.c_int, [C.c_void_p, _dp, C.c_int64]),
+    "rs_f8_plan_kernel_ms": (C.c_int, [C.c_void_p, _dp, _dp, _dp]),
+    "rs_f8_ransac_np": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, C.c_int64, _u32p, _i32p,
+                                  C.c_double, C.POINTER(F8Result), _i64p, C.c_int64, _i64p]),
+    "rs_pnp_dlt": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, _dp]),
+    "rs_pnp_ransac": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, _dp, C.c_int64, C.c_int32,
+                                C.c_int64, C.c_int32, C.c_uint64, _i32p, C.c_double,
+                                C.POINTER(PnpResult), _i64p, _i64p, _i64p, _i64p]),
+    "rs_comm_unique_id": (C.c_int, [_u8p]),
+    "rs_comm_init": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, _u8p]),
+    "rs_comm_destroy": (C.c_int, [C.c_void_p]),
+    "rs_comm_allgather": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]),
+    "rs_comm_allreduce_max_i64": (C.c_int, [C.c_void_p, _i64p]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib():
+    """Load librsamd.so once; raise loudly if it was not built."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise ImportError(
+                        f"{LIB_PATH} is missing: build the HIP extension first "
+                        "(make -C tsbb15-3d-reconstruction-project_amd/csrc or "
+                        "__graft_entry__.build()); there is no CPU fallback")
+                L = C.CDLL(LIB_PATH)
+                for name, (res, args) in _SIGS.items():
+                    fn = getattr(L, name)
+                    fn.restype = res
+                    fn.argtypes = args
+                _lib = L
+    return _lib
+
+
+def check(status):
+    if status == RS_OK:
+        return
+    msg = lib().rs_last_error().decode(errors="replace")
+    if status == RS_EINVAL:
+        raise ValueError(msg)
+    if status == RS_ENOMEM:
+        raise MemoryError(msg)
+    raise RuntimeError(f"rsamd error {status}: {msg}")
+
+
+def ptr(a, ctype):
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+def f64c(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def device_count():
+    n = C.c_int(0)
+    check(lib().rs_device_count(C.byref(n)))
+    return n.value
+
+
+class Context:
+    """One HIP device + stream (rs_ctx)."""
+
+    def __init__(self, device=0):
+        h = C.c_void_p()
+        check(lib().rs_ctx_create(int(device), C.byref(h)))
+        self._h = h
+        self.device = int(device)
+
+    @property
+    def handle(self):
+        if self._h is None:
+            raise RuntimeError("context destroyed")
+        return self._h
+
+    def close(self):
+        if self._h is not None:
+            lib().rs_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def synchronize(self):
+        check(lib().rs_ctx_synchronize(self.handle))
+
+
+_default = {}
+
+
+def default_context():
+    """Process-wide context on the device named by RSAMD_DEVICE / LOCAL_RANK (default 0)."""
+    dev = int(os.environ.get("RSAMD_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+    ctx = _default.get(dev)
+    if ctx is None:
+        ctx = Context(dev)
+        _default[dev] = ctx
+    return ctx
+
+
+# ------------------------------------------------------------------------------------------
+# host samplers
+# ------------------------------------------------------------------------------------------
+def np_choice_tuples(key, pos, n, k, count):
+    """Replay ``count`` x np.random.choice(arange(n), k, replace=False); returns
+    (tuples (count,k) int32, key', pos')."""
+    key = np.array(key, dtype=np.uint32, copy=True)
+    if key.shape != (MT_N,):
+        raise ValueError("MT19937 key must have 624 words")
+    p = C.c_int32(int(pos))
+    out = np.empty((int(count), int(k)), dtype=np.int32)
+    check(lib().rs_np_choice_tuples(ptr(key, C.c_uint32), C.byref(p), int(n), int(k),
+                                    int(count), ptr(out, C.c_int32)))
+    return out, key, p.value
+
+
+def py_shuffle_tuples(key, pos, n, k, count):
+    """Replay ``count`` x ransac.gen_rnd_indices(n, k) on a CPython MT state."""
+    key = np.array(key, dtype=np.uint32, copy=True)
+    if key.shape != (MT_N,):
+        raise ValueError("MT19937 key must have 624 words")
+    p = C.c_int32(int(pos))
+    out = np.empty((int(count), int(k)), dtype=np.int32)
+    check(lib().rs_py_shuffle_tuples(ptr(key, C.c_uint32), C.byref(p), int(n), int(k),
+                                     int(count), ptr(out, C.c_int32)))
+    return out, key, p.value
+
+
+def np_seed(seed):
+    key = np.empty(MT_N, dtype=np.uint32)
+    p = C.c_int32(0)
+    check(lib().rs_np_seed(int(seed) & 0xFFFFFFFF, ptr(key, C.c_uint32), C.byref(p)))
+    return key, p.value
+
+
+def py_seed(seed):
+    n = abs(int(seed))
+    words = []
+    while n:
+        words.append(n & 0xFFFFFFFF)
+        n >>= 32
+    w = np.array(words or [0], dtype=np.uint32)
+    key = np.empty(MT_N, dtype=np.uint32)
+    p = C.c_int32(0)
+    check(lib().rs_py_seed(ptr(w, C.c_uint32), len(words), ptr(key, C.c_uint32), C.byref(p)))
+    return key, p.value
+
+
+# ------------------------------------------------------------------------------------------
+# RANSAC-F plan
+# ------------------------------------------------------------------------------------------
+class F8Plan:
+    """Correspondences resident in HBM + buffers for up to ``max_hyp`` hypotheses."""
+
+    def __init__(self, ctx, n, max_hyp):
+        self.ctx = ctx
+        self.n = int(n)
+        self.max_hyp = int(max_hyp)
+        h = C.c_void_p()
+        check(lib().rs_f8_plan_create(ctx.handle, self.n, self.max_hyp, C.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None:
+            lib().rs_f8_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_points(self, p1, p2):
+        p1, p2 = f64c(p1), f64c(p2)
+        if p1.shape != (2, self.n) or p2.shape != (2, self.n):
+            raise ValueError("points must be (2, n) matching the plan")
+        check(lib().rs_f8_plan_set_points(self._h, ptr(p1, C.c_double), ptr(p2, C.c_double)))
+
+    def run(self, H, mode=SAMPLER_PHILOX, seed=0, hyp_offset=0, tuples=None, thresh=1.5):
+        tp = None
+        if mode == SAMPLER_TUPLES:
+            tuples = np.ascontiguousarray(tuples, dtype=np.int32)
+            if tuples.shape != (int(H), 8):
+                raise ValueError("tuples must be (H, 8)")
+            self._tuples = tuples  # keep alive until the copy is issued
+            tp = ptr(tuples, C.c_int32)
+        check(lib().rs_f8_plan_run(self._h, int(H), int(mode), int(seed) & (2**64 - 1),
+                                   int(hyp_offset), tp, float(thresh)))
+
+    def result(self):
+        r = F8Result()
+        inl = np.empty(self.n, dtype=np.int64)
+        k = C.c_int64(0)
+        check(lib().rs_f8_plan_result(self._h, C.byref(r), ptr(inl, C.c_int64), self.n,
+                                      C.byref(k)))
+        return r, inl[:k.value].copy()
+
+    def candidates(self):
+        k = C.c_int64(0)
+        check(lib().rs_f8_plan_candidates(self._h, None, 0, C.byref(k)))
+        arr = (F8Candidate * max(1, k.value))()
+        check(lib().rs_f8_plan_candidates(self._h, arr, k.value, C.byref(k)))
+        return [arr[i] for i in range(k.value)]
+
+    def counts(self, H):
+        out = np.empty(int(H), dtype=np.int32)
+        check(lib().rs_f8_plan_counts(self._h, ptr(out, C.c_int32), int(H)))
+        return out
+
+    def models(self, H):
+        out = np.empty((int(H), 9), dtype=np.float64)
+        check(lib().rs_f8_plan_models(self._h, ptr(out, C.c_double), int(H)))
+        return out.reshape(-1, 3, 3)
+
+    def kernel_ms(self):
+        a, b, t = C.c_double(), C.c_double(), C.c_double()
+        check(lib().rs_f8_plan_kernel_ms(self._h, C.byref(a), C.byref(b), C.byref(t)))
+        return {"count_ms": a.value, "solve_ms": b.value, "total_ms": t.value}
