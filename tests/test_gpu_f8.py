@@ -182,6 +182,7 @@ def test_degenerate_and_edge_inputs(ctx):
     # minimal population
     p1, p2, _ = synth.two_view(8, 0.0, seed=4)
     res = fun.ransac_f(p1, p2, r=5, rng=np.random.RandomState(0))
-    assert res.count == 8
+    F, S, _, best, _ = ransac_ref.ransac_f(p1, p2, r=5, rng=np.random.RandomState(0))
+    assert res.count == len(S) and np.array_equal(res.inliers, S)
     with pytest.raises(ValueError, match="larger sample"):
         fun.ransac_f(p1[:, :7], p2[:, :7], r=5, rng=np.random.RandomState(0))

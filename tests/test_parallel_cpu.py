@@ -1,0 +1,143 @@
+"""Multi-rank logic of tsbb15_amd.parallel on the CPU (gloo, world_size 2 and 3): hypothesis
+sharding + candidate merge must reproduce the single-process fun.py:320-328 decision, and the
+pair table assembled after the all-gather must equal a single-process run."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import ransac_ref
+from tsbb15_amd import parallel, synth
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _oracle_trace(p1, p2, H):
+    return ransac_ref.ransac_f(p1, p2, r=H, rng=np.random.RandomState(0), trace=True)
+
+
+def _records(tr, F_of, lo, hi):
+    rec = np.zeros(hi - lo, dtype=parallel.CAND_DTYPE)
+    rec["index"] = np.arange(lo, hi)
+    rec["count"] = tr.counts[lo:hi]
+    rec["std"] = tr.stds[lo:hi]
+    rec["norm"] = tr.norms[lo:hi]
+    for k, h in enumerate(range(lo, hi)):
+        rec["F"][k] = F_of(h).ravel()
+    return rec
+
+
+def _worker(rank, world, port, case, q):
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    comm = parallel.TorchComm()
+    try:
+        if case["kind"] == "shard":
+            p1, p2, H = case["p1"], case["p2"], case["H"]
+            F, S, _, best, tr = _oracle_trace(p1, p2, H)
+            lo, n = parallel.shard_range(H, world, rank)
+            F_of = lambda h: ransac_ref.fmatrix_stls(p1[:, tr.tuples[h]], p2[:, tr.tuples[h]])
+            local = _records(tr, F_of, lo, lo + n)
+            lmax = local["count"].max() if n else 0
+            win = parallel.merge_shard_candidates(comm, local[local["count"] == lmax])
+            q.put((rank, int(win["index"]), best))
+        else:
+            pairs = case["pairs"]
+
+            def solve(i, p1, p2):
+                F, S, d, best, _ = ransac_ref.ransac_f(p1, p2, r=case["H"],
+                                                       rng=np.random.RandomState(i))
+                return (1, best, len(S), float(d), F.ravel())
+            tab = parallel.run_pairs(comm, pairs, case["H"], solve)
+            q.put((rank, tab.tobytes(), None))
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(world, case):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return sorted(out, key=lambda t: t[0])
+
+
+def test_shard_range_partitions():
+    for H in (1, 7, 100, 100_000):
+        for w in (1, 2, 3, 8):
+            spans = [parallel.shard_range(H, w, r) for r in range(w)]
+            assert spans[0][0] == 0
+            assert all(a[0] + a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            assert spans[-1][0] + spans[-1][1] == H
+            assert max(s[1] for s in spans) - min(s[1] for s in spans) <= 1
+
+
+def test_lpt_assign_balances():
+    rng = np.random.RandomState(0)
+    costs = list(rng.randint(8, 446, size=231) * 1000)
+    parts = parallel.lpt_assign(costs, 8)
+    assert sorted(i for p in parts for i in p) == list(range(231))
+    loads = [sum(costs[i] for i in p) for p in parts]
+    assert max(loads) <= sum(costs) / 8 + max(costs)
+    assert parts == parallel.lpt_assign(costs, 8)
+
+
+def test_replay_rule_matches_oracle_selection():
+    rng = np.random.RandomState(1)
+    for _ in range(200):
+        n = rng.randint(1, 40)
+        counts = rng.randint(0, 4, size=n)
+        stds = rng.choice([0.5, 1.0, 2.0, 50.0, np.nan], size=n)
+        norms = rng.choice([0.4, 1.5, 3.0, 60.0, np.nan], size=n)
+        best = ransac_ref.select_replay(counts, stds, norms)
+        rec = np.zeros(n, dtype=parallel.CAND_DTYPE)
+        rec["index"], rec["count"], rec["std"], rec["norm"] = np.arange(n), counts, stds, norms
+        cmax = counts.max()
+        win = parallel.replay_rule(rec[rec["count"] == cmax])
+        assert (win is None and best == -1) or int(win["index"]) == best
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_hypothesis_sharding_equals_single_process(world):
+    p1, p2, _ = synth.two_view(150, 0.3, seed=21)
+    out = _spawn(world, {"kind": "shard", "p1": p1, "p2": p2, "H": 240})
+    for rank, idx, best in out:
+        assert idx == best
+
+
+def test_gloo_hypothesis_sharding_all_ties():
+    # noise-free data: every hypothesis ties at c* = N and the std/norm rule decides
+    p1, p2, _ = synth.two_view(40, 0.0, seed=22, sigma=0.0)
+    out = _spawn(2, {"kind": "shard", "p1": p1, "p2": p2, "H": 60})
+    for rank, idx, best in out:
+        assert idx == best
+
+
+def test_gloo_pair_table_equals_single_process():
+    pairs = [synth.two_view(n, 0.2, seed=30 + i)[:2] for i, n in enumerate([40, 9, 7, 120, 60])]
+    out = _spawn(2, {"kind": "pairs", "pairs": pairs, "H": 50})
+    tabs = [np.frombuffer(b, dtype=parallel.PAIR_DTYPE) for _, b, _ in out]
+    assert tabs[0].tobytes() == tabs[1].tobytes()
+    for i, (p1, p2) in enumerate(pairs):
+        row = tabs[0][i]
+        if p1.shape[1] < 8:
+            assert row["valid"] == 0 and row["best_index"] == -1
+            continue
+        F, S, d, best, _ = ransac_ref.ransac_f(p1, p2, r=50, rng=np.random.RandomState(i))
+        assert row["valid"] == 1 and row["best_index"] == best and row["count"] == len(S)
+        np.testing.assert_array_equal(row["F"], F.ravel())

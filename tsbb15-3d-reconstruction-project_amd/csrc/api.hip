@@ -174,7 +174,7 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
   ALLOC(p->d_counts, sizeof(int) * p->ld);
   ALLOC(p->d_tuples, sizeof(int) * 8 * p->ld);
   ALLOC(p->d_cand, sizeof(int) * p->ld);
-  ALLOC(p->d_status, sizeof(int) * 4);
+  ALLOC(p->d_status, sizeof(int) * rsd::kStatusWords);
   ALLOC(p->d_ccount, sizeof(int) * p->ld);
   ALLOC(p->d_cstd, sizeof(double) * p->ld);
   ALLOC(p->d_cnorm, sizeof(double) * p->ld);
@@ -243,15 +243,14 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
                            hipMemcpyHostToDevice, s));
   }
   HIP_TRY(hipEventRecord(p->ev[0], s));
-  HIP_TRY(hipMemsetAsync(p->d_counts, 0, sizeof(int) * H, s));
   HIP_TRY(rsd::launch_f8_solve(p->d_pts, n, h, mode, seed, hyp_offset, p->d_tuples, p->d_F,
-                               p->ld, s));
+                               p->ld, p->d_counts, p->d_status, s));
   HIP_TRY(hipEventRecord(p->ev[1], s));
   HIP_TRY(rsd::launch_f8_count(p->d_pts, n, h, p->d_F, p->ld, choose_chunk(p, H),
                                thresh * thresh, p->d_counts, s));
   HIP_TRY(hipEventRecord(p->ev[2], s));
   HIP_TRY(rsd::launch_f8_select(p->d_counts, h, 1, p->d_cand, p->d_status, s));
-  const int sgrid = static_cast<int>(std::min<int64_t>((H + 3) / 4, 2048));
+  const int sgrid = static_cast<int>(std::min<int64_t>(H, 1024));
   HIP_TRY(rsd::launch_f8_stats(p->d_pts, n, p->d_F, p->ld, p->d_cand, p->d_status, thresh,
                                p->d_ccount, p->d_cstd, p->d_cnorm, sgrid, s));
   HIP_TRY(rsd::launch_f8_replay(p->d_cand, p->d_status, p->d_counts, p->d_ccount, p->d_cstd,
@@ -453,7 +452,8 @@ extern "C" int rs_fmatrix_stls_batch(rs_ctx *c, const double *pl, const double *
   HIP_TRY(hipMemcpyAsync(d_tup, tuples, btup, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(rsd::launch_pack_points(d_xy, d_xy + 2 * n, static_cast<int>(n), d_pts, c->stream));
   HIP_TRY(rsd::launch_f8_solve(d_pts, static_cast<int>(n), static_cast<int>(count),
-                               RS_SAMPLER_TUPLES, 0, 0, d_tup, d_F, ld, c->stream));
+                               RS_SAMPLER_TUPLES, 0, 0, d_tup, d_F, ld, nullptr, nullptr,
+                               c->stream));
   std::vector<double> soa(static_cast<size_t>(9 * ld));
   HIP_TRY(hipMemcpyAsync(soa.data(), d_F, bF, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));

@@ -11,6 +11,10 @@ namespace rsd {
 
 struct Pt;
 
+// Grid of the selection passes; the status buffer holds 4 words + kSelectBlocks counts.
+constexpr int kSelectBlocks = 256;
+constexpr int kStatusWords = 4 + kSelectBlocks;
+
 // Device-resident result of one F run; copied back to the host in one transfer together
 // with the first n_inliers entries of `inliers`.
 struct F8DevResult {
@@ -32,7 +36,7 @@ hipError_t launch_pack_points(const double *p1, const double *p2, int n, Pt *pts
                               hipStream_t s);
 hipError_t launch_f8_solve(const Pt *pts, int n, int H, int mode, uint64_t seed,
                            uint64_t hyp_offset, const int *tuples, double *Fsoa, int64_t ld,
-                           hipStream_t s);
+                           int *counts, int *status, hipStream_t s);
 hipError_t launch_f8_count(const Pt *pts, int n, int H, const double *Fsoa, int64_t ld,
                            int chunk, double thr2, int *counts, hipStream_t s);
 hipError_t launch_f8_select(const int *counts, int H, int slack, int *cand, int *status,

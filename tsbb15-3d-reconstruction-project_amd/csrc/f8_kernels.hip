@@ -13,6 +13,8 @@
 //   k_f8_inliers  one workgroup: S_RANSAC = flatnonzero(d < t) of the winner, in order
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "device_math.h"
 #include "f8_kernels.h"
 
@@ -24,9 +26,13 @@ __device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_rea
 __global__ __launch_bounds__(256) void k_f8_solve(const Pt *__restrict__ pts, int n, int H,
                                                   int mode, uint64_t seed, uint64_t hyp_offset,
                                                   const int *__restrict__ tuples,
-                                                  double *__restrict__ Fsoa, int64_t ld) {
+                                                  double *__restrict__ Fsoa, int64_t ld,
+                                                  int *__restrict__ counts,
+                                                  int *__restrict__ status) {
   const int h = blockIdx.x * blockDim.x + threadIdx.x;
   if (h >= H) return;
+  if (counts) counts[h] = 0;  // the counting kernel accumulates into it
+  if (status && h < 2) status[h] = 0;  // c*, n_candidates
   int idx[8];
   if (mode == RSD_SAMPLER_PHILOX) {
     floyd_sample<8>(seed, hyp_offset + static_cast<uint64_t>(h), n, idx);
@@ -92,55 +98,87 @@ __global__ __launch_bounds__(256) void k_f8_count(const Pt *__restrict__ pts, in
 }
 
 // ----------------------------------------------------------------------------------------
-// Selection: one 1024-thread workgroup.  max count, then ordered compaction of every
-// hypothesis whose fast count >= max(c* - slack, 1).
+// Selection over H counts in three grid-wide passes (no single-workgroup scan):
+//   k_f8_max        c* = max count (block max -> one atomicMax per block)
+//   k_f8_blockcount per block slice: number of hypotheses with count >= max(c* - slack, 1)
+//   k_f8_compact    ordered compaction: block offset = sum of earlier block counts, then
+//                   ballot/popcount prefix inside the block; the last block writes the total
 // ----------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_f8_select(const int *__restrict__ counts, int H,
-                                                    int slack, int *__restrict__ cand,
-                                                    int *__restrict__ status) {
-  __shared__ int red[16];
-  __shared__ int woff[16];
-  __shared__ int base_s;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  int m = 0;
-  for (int i = tid; i < H; i += 1024) m = max(m, counts[i]);
+__device__ __forceinline__ int block_reduce_max(int v, int *sh) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o));
-  if (lane == 0) red[w] = m;
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
   __syncthreads();
-  if (tid == 0) {
-    int mm = 0;
-    for (int i = 0; i < 16; ++i) mm = max(mm, red[i]);
-    red[0] = mm;
-    base_s = 0;
-  }
+  int r = sh[0];
+  for (int q = 1; q < (int)(blockDim.x >> 6); ++q) r = max(r, sh[q]);
   __syncthreads();
-  const int cmax = red[0];
+  return r;
+}
+__device__ __forceinline__ int block_reduce_sum(int v, int *sh) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  int r = 0;
+  for (int q = 0; q < (int)(blockDim.x >> 6); ++q) r += sh[q];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(256) void k_f8_max(const int *__restrict__ counts, int H,
+                                                int *__restrict__ status) {
+  __shared__ int sh[4];
+  int m = 0;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < H; i += gridDim.x * 256) m = max(m, counts[i]);
+  m = block_reduce_max(m, sh);
+  if (threadIdx.x == 0 && m > 0) atomicMax(&status[0], m);
+}
+
+__global__ __launch_bounds__(256) void k_f8_blockcount(const int *__restrict__ counts, int H,
+                                                       int slack, int per_block,
+                                                       const int *__restrict__ status,
+                                                       int *__restrict__ bc) {
+  __shared__ int sh[4];
+  const int cmax = status[0];
   const int thr = max(cmax - slack, 1);
-  for (int b = 0; b < H; b += 1024) {
-    const int i = b + tid;
-    const bool take = (cmax > 0) && (i < H) && (counts[i] >= thr);
-    const unsigned long long bal = __ballot(take);
-    const int before = __popcll(bal & ((1ull << lane) - 1ull));
-    if (lane == 0) woff[w] = __popcll(bal);
-    __syncthreads();
-    if (tid == 0) {
-      int acc = base_s;
-      for (int q = 0; q < 16; ++q) {
-        const int t = woff[q];
-        woff[q] = acc;
-        acc += t;
-      }
-      base_s = acc;
+  const int b0 = blockIdx.x * per_block, b1 = min(H, b0 + per_block);
+  int c = 0;
+  if (cmax > 0)
+    for (int i = b0 + threadIdx.x; i < b1; i += 256) c += counts[i] >= thr ? 1 : 0;
+  c = block_reduce_sum(c, sh);
+  if (threadIdx.x == 0) bc[blockIdx.x] = c;
+}
+
+__global__ __launch_bounds__(256) void k_f8_compact(const int *__restrict__ counts, int H,
+                                                    int slack, int per_block,
+                                                    int *__restrict__ status,
+                                                    const int *__restrict__ bc,
+                                                    int *__restrict__ cand) {
+  __shared__ int sh[4];
+  __shared__ int woff[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int off = 0;
+  for (int j = tid; j < (int)blockIdx.x; j += 256) off += bc[j];
+  off = block_reduce_sum(off, sh);
+  const int cmax = status[0];
+  const int thr = max(cmax - slack, 1);
+  const int b0 = blockIdx.x * per_block, b1 = min(H, b0 + per_block);
+  if (cmax > 0 && bc[blockIdx.x] > 0) {
+    for (int b = b0; b < b1; b += 256) {
+      const int i = b + tid;
+      const bool take = i < b1 && counts[i] >= thr;
+      const unsigned long long bal = __ballot(take);
+      if (lane == 0) woff[w] = __popcll(bal);
+      __syncthreads();
+      int base = off;
+      for (int q = 0; q < w; ++q) base += woff[q];
+      const int tot = woff[0] + woff[1] + woff[2] + woff[3];
+      if (take) cand[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
+      off += tot;
+      __syncthreads();
     }
-    __syncthreads();
-    if (take) cand[woff[w] + before] = i;
-    __syncthreads();
   }
-  if (tid == 0) {
-    status[0] = cmax;
-    status[1] = base_s;
-  }
+  if (blockIdx.x == gridDim.x - 1 && tid == 0) status[1] = off + (cmax > 0 ? 0 : 0);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -157,6 +195,17 @@ __device__ __forceinline__ int wave_sum_i(int v) {
   return v;
 }
 
+__device__ __forceinline__ double block_sum_d(double v, double *sh) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double r = 0.0;
+  for (int q = 0; q < (int)(blockDim.x >> 6); ++q) r += sh[q];
+  __syncthreads();
+  return r;
+}
+
+// Workgroup (256 threads) per candidate, grid-stride over the device-side candidate count.
 __global__ __launch_bounds__(256) void k_f8_stats(const Pt *__restrict__ pts, int n,
                                                   const double *__restrict__ Fsoa, int64_t ld,
                                                   const int *__restrict__ cand,
@@ -164,34 +213,34 @@ __global__ __launch_bounds__(256) void k_f8_stats(const Pt *__restrict__ pts, in
                                                   int *__restrict__ ccount,
                                                   double *__restrict__ cstd,
                                                   double *__restrict__ cnorm) {
-  const int lane = threadIdx.x & 63;
+  __shared__ double shd[4];
+  __shared__ int shi[4];
+  const int tid = threadIdx.x;
   const int nc = status[1];
-  const int wpg = wave_uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
-  const int nw = gridDim.x * 4;
-  for (int c = wpg; c < nc; c += nw) {
+  for (int c = blockIdx.x; c < nc; c += gridDim.x) {
     const int h = cand[c];
     double f[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) f[k] = Fsoa[k * ld + h];
     double s1 = 0.0, s2 = 0.0;
     int cnt = 0;
-    for (int i = lane; i < n; i += 64) {
+    for (int i = tid; i < n; i += 256) {
       const double d = dist_ref(f, pts[i]);
       cnt += d < thresh ? 1 : 0;
       s1 += d;
       s2 += d * d;
     }
-    s1 = wave_sum(s1);
-    s2 = wave_sum(s2);
-    cnt = wave_sum_i(cnt);
+    s1 = block_sum_d(s1, shd);
+    s2 = block_sum_d(s2, shd);
+    cnt = block_reduce_sum(cnt, shi);
     const double mean = s1 / static_cast<double>(n);
     double s3 = 0.0;
-    for (int i = lane; i < n; i += 64) {
+    for (int i = tid; i < n; i += 256) {
       const double v = dist_ref(f, pts[i]) - mean;
       s3 += v * v;
     }
-    s3 = wave_sum(s3);
-    if (lane == 0) {
+    s3 = block_sum_d(s3, shd);
+    if (tid == 0) {
       ccount[c] = cnt;
       cstd[c] = sqrt(s3 / static_cast<double>(n));
       cnorm[c] = sqrt(s2);
@@ -355,9 +404,9 @@ hipError_t launch_pack_points(const double *p1, const double *p2, int n, Pt *pts
 
 hipError_t launch_f8_solve(const Pt *pts, int n, int H, int mode, uint64_t seed,
                            uint64_t hyp_offset, const int *tuples, double *Fsoa, int64_t ld,
-                           hipStream_t s) {
+                           int *counts, int *status, hipStream_t s) {
   hipLaunchKernelGGL(k_f8_solve, dim3((H + 255) / 256), dim3(256), 0, s, pts, n, H, mode, seed,
-                     hyp_offset, tuples, Fsoa, ld);
+                     hyp_offset, tuples, Fsoa, ld, counts, status);
   return hipGetLastError();
 }
 
@@ -372,7 +421,14 @@ hipError_t launch_f8_count(const Pt *pts, int n, int H, const double *Fsoa, int6
 
 hipError_t launch_f8_select(const int *counts, int H, int slack, int *cand, int *status,
                             hipStream_t s) {
-  hipLaunchKernelGGL(k_f8_select, dim3(1), dim3(1024), 0, s, counts, H, slack, cand, status);
+  int *bc = status + 4;  // kSelectBlocks block counts live behind the status words
+  const int per_block = (H + kSelectBlocks - 1) / kSelectBlocks;
+  const int nb = (H + per_block - 1) / per_block;
+  hipLaunchKernelGGL(k_f8_max, dim3(std::min(nb, 256)), dim3(256), 0, s, counts, H, status);
+  hipLaunchKernelGGL(k_f8_blockcount, dim3(nb), dim3(256), 0, s, counts, H, slack, per_block,
+                     status, bc);
+  hipLaunchKernelGGL(k_f8_compact, dim3(nb), dim3(256), 0, s, counts, H, slack, per_block,
+                     status, bc, cand);
   return hipGetLastError();
 }
 

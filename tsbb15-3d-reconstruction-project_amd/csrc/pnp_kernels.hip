@@ -75,33 +75,47 @@ __device__ __forceinline__ void smallest_right_sv(const double (&R)[78], double 
     for (int l = j + 1; l < 12; ++l) acc -= R[ridx(j, l)] * x[l];
     x[j] = acc * dinv[j];
   }
-  for (int it = 0; it < 8; ++it) {
-    double nn = 0.0;
+  // Inverse iteration on R^T R: converges at (s12/s11)^2 per step; a noisy minimal sample can
+  // have s12/s11 ~ 0.5, so iterate to a fixed point (|dx| <= 1e-15) rather than a fixed count.
+  double nn = 0.0;
 #pragma unroll
-    for (int j = 0; j < 12; ++j) nn += x[j] * x[j];
-    const double inv = 1.0 / sqrt(nn);
-    double z[12];
+  for (int j = 0; j < 12; ++j) nn += x[j] * x[j];
+  double inv = 1.0 / sqrt(nn);
+#pragma unroll
+  for (int j = 0; j < 12; ++j) x[j] *= inv;
+  for (int it = 0; it < 400; ++it) {
+    double z[12], w[12];
 #pragma unroll
     for (int j = 0; j < 12; ++j) {  // R^T z = x
-      double acc = x[j] * inv;
+      double acc = x[j];
 #pragma unroll
       for (int i = 0; i < j; ++i) acc -= R[ridx(i, j)] * z[i];
       z[j] = acc * dinv[j];
     }
 #pragma unroll
-    for (int j = 11; j >= 0; --j) {  // R x = z
+    for (int j = 11; j >= 0; --j) {  // R w = z
       double acc = z[j];
 #pragma unroll
-      for (int l = j + 1; l < 12; ++l) acc -= R[ridx(j, l)] * x[l];
-      x[j] = acc * dinv[j];
+      for (int l = j + 1; l < 12; ++l) acc -= R[ridx(j, l)] * w[l];
+      w[j] = acc * dinv[j];
     }
+    double ww = 0.0, dot = 0.0;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      ww += w[j] * w[j];
+      dot += w[j] * x[j];
+    }
+    const double sgn = dot < 0.0 ? -1.0 : 1.0;
+    const double iw = sgn / sqrt(ww);
+    double delta = 0.0;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      const double v = w[j] * iw;
+      delta = fmax(delta, fabs(v - x[j]));
+      x[j] = v;
+    }
+    if (!(delta > 1e-15)) break;  // converged (or NaN: give up, the model scores zero)
   }
-  double nn = 0.0;
-#pragma unroll
-  for (int j = 0; j < 12; ++j) nn += x[j] * x[j];
-  const double inv = 1.0 / sqrt(nn);
-#pragma unroll
-  for (int j = 0; j < 12; ++j) x[j] *= inv;
 }
 
 // Constraint enforcement (pnp.py:141-145): C0 = (A | b) -> (R, t).

@@ -1,0 +1,237 @@
+"""Multi-GPU layer: one process per GPU, RCCL over xGMI.
+
+Two shardings:
+
+  * pairs (config C4): independent image pairs are assigned to ranks by longest-processing-
+    time greedy on N x H; each rank runs its pairs with no collective; one all-gather of fixed
+    size per-pair records (F, count, index, pair id) at the end.
+  * hypotheses of one pair (C2/C5 weak scaling): rank r evaluates the contiguous hypothesis
+    range [start_r, start_r + n_r) (Philox counters are global hypothesis indices, so the
+    union is exactly the single-GPU run); then one max-all-reduce of c* and one all-gather of
+    the candidates with count == c*, which every rank replays in global index order with the
+    fun.py:320-328 rule (first c* hypothesis, then std/norm tie replacements).
+
+Communicators: :class:`RcclComm` (librsamd, device buffers, xGMI) on GPUs and
+:class:`TorchComm` (torch.distributed, e.g. gloo on the CPU) for tests; both expose
+``allgather_bytes`` and ``allreduce_max_int``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _ffi
+
+CAND_DTYPE = np.dtype([("index", "<i8"), ("count", "<i8"), ("std", "<f8"), ("norm", "<f8"),
+                       ("F", "<f8", (9,))])
+PAIR_DTYPE = np.dtype([("pair", "<i8"), ("valid", "<i8"), ("best_index", "<i8"),
+                       ("count", "<i8"), ("std", "<f8"), ("F", "<f8", (9,))])
+
+
+# ------------------------------------------------------------------------------------------
+# communicators
+# ------------------------------------------------------------------------------------------
+class TorchComm:
+    """torch.distributed process group (gloo on the host, for tests and bootstrap)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+
+    def allgather_bytes(self, b: bytes):
+        out = [None] * self.world
+        self.dist.all_gather_object(out, b, group=self.group)
+        return out
+
+    def allreduce_max_int(self, v: int) -> int:
+        import torch
+        t = torch.tensor([int(v)], dtype=torch.int64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+        return int(t.item())
+
+    def broadcast_bytes(self, b, src=0):
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=src, group=self.group)
+        return obj[0]
+
+
+class RcclComm:
+    """RCCL communicator owned by a librsamd context (bootstrapped through ``boot``, any
+    object with ``broadcast_bytes``; a TorchComm over gloo works)."""
+
+    def __init__(self, ctx, rank, world, boot):
+        self.ctx, self.rank, self.world = ctx, int(rank), int(world)
+        uid = np.zeros(_ffi.COMM_ID_BYTES, np.uint8)
+        if self.rank == 0:
+            _ffi.check(_ffi.lib().rs_comm_unique_id(_ffi.ptr(uid, C.c_uint8)))
+        uid = np.frombuffer(boot.broadcast_bytes(uid.tobytes(), 0), np.uint8).copy()
+        _ffi.check(_ffi.lib().rs_comm_init(ctx.handle, self.world, self.rank,
+                                           _ffi.ptr(uid, C.c_uint8)))
+
+    def allgather_bytes(self, b: bytes):
+        n = len(b)
+        send = np.frombuffer(b, np.uint8).copy()
+        recv = np.zeros(n * self.world, np.uint8)
+        _ffi.check(_ffi.lib().rs_comm_allgather(self.ctx.handle,
+                                                send.ctypes.data_as(C.c_void_p),
+                                                recv.ctypes.data_as(C.c_void_p), n))
+        return [recv[i * n:(i + 1) * n].tobytes() for i in range(self.world)]
+
+    def allreduce_max_int(self, v: int) -> int:
+        x = C.c_int64(int(v))
+        _ffi.check(_ffi.lib().rs_comm_allreduce_max_i64(self.ctx.handle, C.byref(x)))
+        return int(x.value)
+
+    def close(self):
+        _ffi.lib().rs_comm_destroy(self.ctx.handle)
+
+
+# ------------------------------------------------------------------------------------------
+# sharding and merging (host logic shared by every communicator)
+# ------------------------------------------------------------------------------------------
+def shard_range(H, world, rank):
+    """Contiguous hypothesis range of ``rank``: sizes differ by at most one."""
+    base, extra = divmod(int(H), int(world))
+    start = rank * base + min(rank, extra)
+    return start, base + (1 if rank < extra else 0)
+
+
+def lpt_assign(costs, world):
+    """Longest-processing-time greedy: list of item indices per rank (deterministic)."""
+    order = sorted(range(len(costs)), key=lambda i: (-costs[i], i))
+    load = [0.0] * world
+    out = [[] for _ in range(world)]
+    for i in order:
+        r = min(range(world), key=lambda q: (load[q], q))
+        out[r].append(i)
+        load[r] += costs[i]
+    return [sorted(v) for v in out]
+
+
+def replay_rule(cands):
+    """fun.py:320-328 over candidate records sorted by global hypothesis index.
+
+    ``cands`` must hold every hypothesis whose count equals the global maximum.  Returns the
+    winning record (or None when no hypothesis has a non-empty consensus)."""
+    if len(cands) == 0:
+        return None
+    cands = np.sort(cands, order="index")
+    best = None
+    for c in cands:
+        if best is None:
+            if c["count"] > 0:
+                best = c
+        elif c["count"] > best["count"]:
+            best = c
+        elif c["count"] == best["count"] and abs(best["std"]) > c["norm"]:
+            best = c
+    return best
+
+
+def merge_shard_candidates(comm, local):
+    """All-reduce c*, all-gather the local candidates with count == c*, replay globally."""
+    local = np.asarray(local, dtype=CAND_DTYPE)
+    lmax = int(local["count"].max()) if len(local) else 0
+    cstar = comm.allreduce_max_int(lmax)
+    mine = local[local["count"] == cstar] if cstar > 0 else local[:0]
+    width = comm.allreduce_max_int(len(mine))
+    buf = np.zeros(width + 1, dtype=CAND_DTYPE)
+    buf[0]["index"] = len(mine)          # header record: number of valid entries
+    buf[1:1 + len(mine)] = mine
+    parts = comm.allgather_bytes(buf.tobytes())
+    allc = []
+    for p in parts:
+        a = np.frombuffer(p, dtype=CAND_DTYPE)
+        allc.append(a[1:1 + int(a[0]["index"])])
+    return replay_rule(np.concatenate(allc) if allc else np.zeros(0, CAND_DTYPE))
+
+
+def candidates_from_plan(plan, hyp_offset):
+    recs = plan.candidates()
+    out = np.zeros(len(recs), dtype=CAND_DTYPE)
+    for i, c in enumerate(recs):
+        out[i] = (c.index + hyp_offset, c.count, c.std_d, c.norm_d, np.array(c.F[:]))
+    return out
+
+
+def ransac_f_sharded(comm, ctx, p1, p2, H, seed=0, thresh=1.5, plan=None):
+    """Hypotheses [0, H) of one pair split over the ranks of ``comm`` (Philox sampler).
+
+    Returns (winner record, inliers) -- identical on every rank and identical to the
+    single-GPU run with the same seed."""
+    p1 = _ffi.f64c(p1)
+    p2 = _ffi.f64c(p2)
+    start, cnt = shard_range(H, comm.world, comm.rank)
+    own = plan is None
+    if own:
+        plan = _ffi.F8Plan(ctx, p1.shape[1], max(cnt, 1))
+        plan.set_points(p1, p2)
+    local = np.zeros(0, CAND_DTYPE)
+    if cnt > 0:
+        plan.run(cnt, mode=_ffi.SAMPLER_PHILOX, seed=seed, hyp_offset=start, thresh=thresh)
+        plan.result()
+        local = candidates_from_plan(plan, start)
+    best = merge_shard_candidates(comm, local)
+    if own:
+        plan.close()
+    if best is None:
+        return None, np.zeros(0, np.int64)
+    from . import lab3
+    F = best["F"].reshape(3, 3)
+    r = np.abs(lab3.fmatrix_residuals(F, p1, p2))
+    d = np.where(np.isnan(r).any(axis=0), np.nan, r.max(axis=0))
+    return best, np.flatnonzero(d < thresh)
+
+
+class GpuPairSolver:
+    """Runs one pair's RANSAC on this rank's GPU (plans cached per correspondence count)."""
+
+    def __init__(self, ctx, H, seed_base=1000, thresh=1.5):
+        self.ctx, self.H, self.seed_base, self.thresh = ctx, int(H), seed_base, thresh
+        self.plans = {}
+
+    def __call__(self, i, p1, p2):
+        n = p1.shape[1]
+        plan = self.plans.get(n)
+        if plan is None:
+            plan = self.plans[n] = _ffi.F8Plan(self.ctx, n, self.H)
+        plan.set_points(p1, p2)
+        plan.run(self.H, mode=_ffi.SAMPLER_PHILOX, seed=self.seed_base + i, thresh=self.thresh)
+        r, _ = plan.result()
+        return (1 if r.best_index >= 0 else 0, r.best_index, r.best_count, r.best_std,
+                np.array(r.F[:]))
+
+    def close(self):
+        for p in self.plans.values():
+            p.close()
+        self.plans = {}
+
+
+def run_pairs(comm, pairs, H, solve):
+    """Config C4: ``pairs`` = list of (p1, p2); ``solve(i, p1, p2)`` -> (valid, best_index,
+    count, std, F[9]) runs one pair on this rank (GpuPairSolver on a GPU).  Pairs with N < 8
+    are skipped (valid = 0).  Returns the PAIR_DTYPE table of every pair, identical on every
+    rank, after one all-gather of fixed-size records."""
+    costs = [p1.shape[1] * H if p1.shape[1] >= 8 else 0 for p1, _ in pairs]
+    owners = lpt_assign(costs, comm.world)
+    recs = np.zeros(len(pairs), dtype=PAIR_DTYPE)
+    recs["pair"] = np.arange(len(pairs))
+    recs["best_index"] = -1
+    for i in owners[comm.rank]:
+        p1, p2 = pairs[i]
+        if p1.shape[1] < 8:
+            continue
+        valid, best, count, std, F = solve(i, p1, p2)
+        recs[i] = (i, valid, best, count, std, F)
+    parts = comm.allgather_bytes(recs.tobytes())
+    table = np.zeros(len(pairs), dtype=PAIR_DTYPE)
+    for r, p in enumerate(parts):
+        a = np.frombuffer(p, dtype=PAIR_DTYPE)
+        table[owners[r]] = a[owners[r]]
+    table["pair"] = np.arange(len(pairs))
+    table["best_index"][table["valid"] == 0] = -1
+    return table
