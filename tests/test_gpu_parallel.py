@@ -1,0 +1,97 @@
+"""Sharded execution on the GPU: hypothesis shards (Philox counters are global hypothesis
+indices, so shards reproduce the single run), the RCCL communicator at world size 1, and the
+36-view Dino ring (config C4: all C(36,2) pairs of BAdino2.mat)."""
+import itertools
+
+import numpy as np
+import pytest
+
+from conftest import golden
+from oracle import ransac_ref
+from tsbb15_amd import _ffi, parallel, synth
+
+pytestmark = pytest.mark.gpu
+
+
+class _Boot:
+    def broadcast_bytes(self, b, src=0):
+        return b
+
+
+class _Solo:
+    rank, world = 0, 1
+
+    def allgather_bytes(self, b):
+        return [b]
+
+    def allreduce_max_int(self, v):
+        return int(v)
+
+
+def test_hypothesis_shards_reproduce_single_run(ctx):
+    p1, p2, _ = synth.two_view(2000, 0.3, seed=1)
+    H, seed = 20_000, 77
+    plan = _ffi.F8Plan(ctx, 2000, H)
+    plan.set_points(p1, p2)
+    plan.run(H, mode=_ffi.SAMPLER_PHILOX, seed=seed)
+    ref, ref_inl = plan.result()
+    ref_counts = plan.counts(H)
+    parts = []
+    for w in range(4):
+        lo, n = parallel.shard_range(H, 4, w)
+        plan.run(n, mode=_ffi.SAMPLER_PHILOX, seed=seed, hyp_offset=lo)
+        plan.result()
+        assert np.array_equal(plan.counts(n), ref_counts[lo:lo + n])
+        parts.append(parallel.candidates_from_plan(plan, lo))
+    allc = np.concatenate(parts)
+    cstar = allc["count"].max()
+    win = parallel.replay_rule(allc[allc["count"] == cstar])
+    assert int(win["index"]) == ref.best_index and int(win["count"]) == ref.best_count
+
+
+def test_rccl_world_one_sharded_api(ctx):
+    p1, p2, _ = synth.two_view(500, 0.3, seed=2)
+    comm = parallel.RcclComm(ctx, 0, 1, _Boot())
+    try:
+        assert comm.allreduce_max_int(17) == 17
+        assert comm.allgather_bytes(b"abcdefgh") == [b"abcdefgh"]
+        best, inl = parallel.ransac_f_sharded(comm, ctx, p1, p2, 5000, seed=3)
+    finally:
+        comm.close()
+    plan = _ffi.F8Plan(ctx, 500, 5000)
+    plan.set_points(p1, p2)
+    plan.run(5000, mode=_ffi.SAMPLER_PHILOX, seed=3)
+    r, rinl = plan.result()
+    assert int(best["index"]) == r.best_index
+    assert np.array_equal(inl, rinl)
+
+
+def _dino_pairs():
+    z = golden("dino_pnp_kat.npz")
+    P = z["points2d"]
+    pairs = []
+    for i, j in itertools.combinations(range(36), 2):
+        vis = np.flatnonzero(np.any(P[i] != -1, axis=0) & np.any(P[j] != -1, axis=0))
+        pairs.append((np.ascontiguousarray(P[i][:, vis]), np.ascontiguousarray(P[j][:, vis])))
+    return pairs
+
+
+def test_dino_ring_all_pairs(ctx):
+    pairs = _dino_pairs()
+    assert len(pairs) == 630
+    solver = parallel.GpuPairSolver(ctx, 1000)
+    try:
+        tab = parallel.run_pairs(_Solo(), pairs, 1000, solver)
+    finally:
+        solver.close()
+    n = np.array([p1.shape[1] for p1, _ in pairs])
+    # correspondences.py:37-42 filter; 284 non-empty pairs, 203 with N >= 8
+    assert int((n > 0).sum()) == 284 and int((n >= 8).sum()) == 203
+    assert int(n[n >= 8].sum()) == 11257
+    assert np.array_equal(tab["valid"] == 1, n >= 8)
+    # noise-free scene: every valid pair's winner explains all of its correspondences
+    for i in np.flatnonzero(n >= 8)[::10]:
+        p1, p2 = pairs[i]
+        F = tab["F"][i].reshape(3, 3)
+        d = ransac_ref.inlier_distance(F, p1, p2)
+        assert tab["count"][i] == np.count_nonzero(d < 1.5) == p1.shape[1]

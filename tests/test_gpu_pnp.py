@@ -73,13 +73,21 @@ def test_gen_rnd_indices_advances_global_stream(ctx):
 
 
 def test_ransac_robust_surface(ctx):
+    # The reference's unnormalised 6-point DLT is poorly conditioned on noisy data
+    # (s11/s12 ~ 4 here), so minimal-sample poses are rough and consensus sets small; the
+    # drop-in must reproduce the oracle exactly, not an idealised estimator.
     X, _, y, _, _, truth = synth.pnp_scene(120, 0.2, seed=5)
     D = np.stack([y, X], axis=1)            # (N, 2, 3): D[:,0] = y, D[:,1] = x
+    thr = (8.0 / 800) ** 2
     random.seed(0)
-    R_est, t_est, C_est = ransac.ransac_robust(D, D, 200, (2.0 / 800) ** 2, 6)
+    R_est, t_est, C_est = ransac.ransac_robust(D, D, 200, thr, 6)
+    Ro, to, imo, iho, besto, _ = pnp_ref.ransac_pnp(y, X, y, X, 200, thr, 6,
+                                                    rng=random.Random(0))
     assert len(R_est) == 1 and R_est[0].shape == (3, 3)
     assert np.allclose(R_est[0] @ R_est[0].T, np.eye(3), atol=1e-9)
-    assert C_est[0][0].shape[1:] == (2, 3) and len(C_est[0][0]) >= 0.9 * truth.sum()
+    np.testing.assert_allclose(R_est[0], Ro, atol=1e-6)
+    np.testing.assert_allclose(t_est[0], to, rtol=1e-6, atol=1e-6)
+    assert np.array_equal(C_est[0][0], D[imo]) and np.array_equal(C_est[0][1], D[iho])
     with pytest.raises(ValueError, match="Not implemented yet"):
         ransac.ransac_robust(D, D, 10, 1e-5, 4)
     with pytest.raises(ValueError, match="No PnP algorithm"):

@@ -1,0 +1,72 @@
+"""Summarise a gpu_round.sh output directory into profiles/: rocprofv3 --stats kernel table
+and per-launch PMC counters of the dominant kernel.
+
+  python tools/pmc_summary.py gpurun_out/<tag> <round-tag>
+
+HBM bytes follow MI355X_MICROARCH.md "HBM": FETCH_SIZE and WRITE_SIZE are in KiB; FETCH_SIZE
+reads half the bytes only for 16-B-per-lane streaming reads.  The count kernel's HBM-side
+reads are 8-B-per-lane model loads (uncalibrated width), so both the raw sum and the
+2x-corrected upper bound are recorded; `hbm_bytes_per_launch` is the raw (FETCH+WRITE)*1024.
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+KERNEL = "k_f8_count"
+
+
+def per_launch(path, kernel):
+    vals = defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if kernel in r["Kernel_Name"]:
+            vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
+
+
+def main():
+    src, tag = sys.argv[1], sys.argv[2]
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prof = os.path.join(repo, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    shutil.copy(os.path.join(src, "prof", "bench_kernel_stats.csv"),
+                os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    bench = json.load(open(os.path.join(src, "bench.json")))
+    counters, launches = {}, {}
+    for sub in ("pmc_fetch", "pmc_write", "pmc_sq"):
+        p = os.path.join(src, sub, "pmc_counter_collection.csv")
+        if os.path.exists(p):
+            c, n = per_launch(p, KERNEL)
+            counters.update(c)
+            launches.update(n)
+    stats = {r["Name"].split("(")[0]: {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                                       "pct": float(r["Percentage"])}
+             for r in csv.DictReader(open(os.path.join(src, "prof", "bench_kernel_stats.csv")))}
+    fetch = counters.get("FETCH_SIZE", 0.0) * 1024
+    write = counters.get("WRITE_SIZE", 0.0) * 1024
+    out = {
+        "kernel": KERNEL,
+        "n_corr": bench["config"]["n_corr"],
+        "hypotheses": bench["config"]["hypotheses_per_step"],
+        "counters_per_launch": counters,
+        "launches_sampled": launches,
+        "hbm_bytes_per_launch": fetch + write,
+        "hbm_bytes_per_launch_fetch_x2_upper": 2 * fetch + write,
+        "kernel_stats_avg_ns": stats.get(f"rsd::{KERNEL}", {}).get("avg_ns"),
+        "bench_hip_event_avg_ms": bench["kernels_ms"][KERNEL],
+        "valu_insts_per_wave_point": (counters.get("SQ_INSTS_VALU", 0.0) /
+                                      (bench["config"]["hypotheses_per_step"] *
+                                       bench["config"]["n_corr"] / 64.0)),
+        "source": f"rocprofv3 --pmc passes of bench.py (tools/gpu_round.sh), {src}",
+    }
+    with open(os.path.join(prof, f"{tag}_pmc_{KERNEL}.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    with open(os.path.join(prof, f"{tag}_bench.json"), "w") as f:
+        json.dump(bench, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
