@@ -186,3 +186,75 @@ def test_degenerate_and_edge_inputs(ctx):
     assert res.count == len(S) and np.array_equal(res.inliers, S)
     with pytest.raises(ValueError, match="larger sample"):
         fun.ransac_f(p1[:, :7], p2[:, :7], r=5, rng=np.random.RandomState(0))
+
+
+def _near_threshold_points(F, p1, p2, deltas, rng, keep):
+    """Move right-image points (except ``keep``) along a random direction until the reference
+    distance d = max(|r1|, |r2|) equals 1.5 * (1 +/- delta) (bisection on the oracle's d)."""
+    p2 = p2.copy()
+    k = 0
+    for i in range(p1.shape[1]):
+        if i in keep:
+            continue
+        delta = deltas[k % len(deltas)] * (1 if k % 2 == 0 else -1)
+        k += 1
+        target = 1.5 * (1.0 + delta)
+        dirn = rng.randn(2)
+        dirn /= np.linalg.norm(dirn)
+        d = lambda t: ransac_ref.inlier_distance(
+            F, p1[:, i:i + 1], p2[:, i:i + 1] + t * dirn[:, None])[0]
+        lo, hi = 0.0, 1.0
+        while d(hi) < target and hi < 1e4:
+            hi *= 2
+        if not (d(lo) <= target <= d(hi)):
+            continue
+        for _ in range(200):
+            mid = 0.5 * (lo + hi)
+            if d(mid) < target:
+                lo = mid
+            else:
+                hi = mid
+        p2[:, i] += lo * dirn
+    return p2
+
+
+def test_fp32_guard_band_exact_near_threshold(ctx, monkeypatch):
+    """Points placed at d = 1.5 (1 +/- delta), delta down to 1e-12: the fp32 counting kernel
+    must agree bit for bit with the fp64 kernel and with the oracle's reference-order test."""
+    rng = np.random.RandomState(5)
+    p1, p2, _ = synth.two_view(512, 0.1, seed=8)
+    tup = np.array([np.arange(8) * 7 + s for s in range(4)], np.int32)
+    F = lab3.fmatrix_stls_batch(p1, p2, tup)
+    p2n = _near_threshold_points(F[0], p1, p2, [1e-12, 1e-9, 1e-7, 1e-6, 1e-5, 1e-4, 1e-3], rng,
+                                 set(tup.ravel().tolist()))
+    res = {}
+    for mode in ("fp32", "fp64"):
+        monkeypatch.setenv("RSAMD_COUNT", mode)
+        plan = _ffi.F8Plan(ctx, 512, 4)
+        plan.set_points(p1, p2n)
+        plan.run(4, mode=_ffi.SAMPLER_TUPLES, tuples=tup)
+        plan.result()
+        res[mode] = plan.counts(4)
+        plan.close()
+    Fm = lab3.fmatrix_stls_batch(p1, p2n, tup)
+    oracle = [np.count_nonzero(ransac_ref.inlier_distance(f, p1, p2n) < 1.5) for f in Fm]
+    assert np.array_equal(res["fp32"], res["fp64"])
+    assert res["fp64"][0] == oracle[0]  # model 0 is the one the points were placed around
+    np.testing.assert_array_equal(Fm[0], F[0])
+
+
+@pytest.mark.parametrize("name", ["synth_c2.npz", "synth_c5.npz"])
+def test_fp32_and_fp64_counting_identical_full_size(ctx, monkeypatch, name):
+    z = golden(name)
+    n = z["p1"].shape[1]
+    H = 20_000
+    counts = {}
+    for mode in ("fp32", "fp64"):
+        monkeypatch.setenv("RSAMD_COUNT", mode)
+        plan = _ffi.F8Plan(ctx, n, H)
+        plan.set_points(z["p1"], z["p2"])
+        plan.run(H, mode=_ffi.SAMPLER_PHILOX, seed=99)
+        plan.result()
+        counts[mode] = plan.counts(H)
+        plan.close()
+    assert np.array_equal(counts["fp32"], counts["fp64"])

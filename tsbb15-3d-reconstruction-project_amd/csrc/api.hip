@@ -132,7 +132,37 @@ struct rs_f8_plan {
   int64_t last_H = 0;
   bool pending = false, have_result = false;
   int chunk_override = 0;
+  // fp32 counting (k_f8_count32): frame, fp32 points and models
+  float4 *d_pts32 = nullptr;
+  float *d_F32 = nullptr;
+  rsd::Frame frame{1.0, 0.0, 0.0, 0.0, 0.0};
+  bool fp32_ok = false;   // finite points and a non-degenerate frame
+  bool use_fp32 = true;   // RSAMD_COUNT=fp64 selects the float64 kernel
+  int resident_waves = 8192;  // CUs x 4 SIMDs x 8 waves (RSAMD_WAVES overrides)
+  int count_block = 4;        // points per scalar-load block (RSAMD_BLOCK = 4 | 8)
 };
+
+namespace {
+
+// Absolute error bounds of the fp32 test in the unit frame (|x~| <= R); derivation in
+// f8_kernels.hip above k_f8_count32.  Dl: a line component, De: e, Dn: a squared length.
+rsd::Guard32 guard_constants(const rsd::Frame &fr, double thresh) {
+  const double u = std::ldexp(1.0, -24), R = 1.0 + 1e-6, Lm = 2.0 * R + 1.0;
+  const double Dl = 1.1 * u * (7.0 * R + 3.0);
+  const double De =
+      1.1 * (2.0 * (Dl * R * 1.001 + Lm * u * R) + Dl + u * (Lm + Dl) * (3.0 * R + 2.0) * 1.001);
+  const double Dn = 1.1 * (2.0 * Dl * (2.0 * Lm + Dl) + 3.0 * u * (Lm + Dl) * (Lm + Dl) * 1.001);
+  const double thr2 = (thresh / fr.s) * (thresh / fr.s);
+  rsd::Guard32 g;
+  g.thr2 = static_cast<float>(thr2);
+  g.K1 = static_cast<float>(1.02 * 2.0 * De);
+  g.Ku = static_cast<float>(1.02 * u);
+  g.K0 = static_cast<float>(1.02 * (De * De + thr2 * (1.0 + 1e-6) * Dn));
+  g.thr2_px = thresh * thresh;
+  return g;
+}
+
+}  // namespace
 
 static void plan_free(rs_f8_plan *p) {
   (void)hipFree(p->d_p12);
@@ -146,6 +176,8 @@ static void plan_free(rs_f8_plan *p) {
   (void)hipFree(p->d_cstd);
   (void)hipFree(p->d_cnorm);
   (void)hipFree(p->d_res);
+  (void)hipFree(p->d_pts32);
+  (void)hipFree(p->d_F32);
   if (p->h_res) (void)hipHostFree(p->h_res);
   for (auto &e : p->ev)
     if (e) (void)hipEventDestroy(e);
@@ -165,6 +197,15 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
   p->ld = (max_hyp + 63) / 64 * 64;
   p->res_bytes = sizeof(rsd::F8DevResult) + sizeof(int64_t) * static_cast<size_t>(n);
   if (const char *ch = std::getenv("RSAMD_CHUNK")) p->chunk_override = std::atoi(ch);
+  if (const char *cm = std::getenv("RSAMD_COUNT")) p->use_fp32 = std::strcmp(cm, "fp64") != 0;
+  {
+    int cus = 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
+      cus = 256;
+    p->resident_waves = cus * 4 * 8;
+    if (const char *wv = std::getenv("RSAMD_WAVES")) p->resident_waves = std::max(1, std::atoi(wv));
+    if (const char *bk = std::getenv("RSAMD_BLOCK")) p->count_block = std::atoi(bk) == 8 ? 8 : 4;
+  }
   hipError_t e = hipSuccess;
 #define ALLOC(ptr, bytes)                                  \
   if (e == hipSuccess) e = hipMalloc(&(ptr), (bytes));
@@ -179,6 +220,8 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
   ALLOC(p->d_cstd, sizeof(double) * p->ld);
   ALLOC(p->d_cnorm, sizeof(double) * p->ld);
   ALLOC(p->d_res, p->res_bytes);
+  ALLOC(p->d_pts32, sizeof(float4) * ((n + 7) & ~7LL));
+  ALLOC(p->d_F32, sizeof(float) * 9 * p->ld);
 #undef ALLOC
   if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&p->h_res), p->res_bytes);
   for (auto &ev : p->ev)
@@ -210,6 +253,35 @@ extern "C" int rs_f8_plan_set_points(rs_f8_plan *p, const double *p1, const doub
   HIP_TRY(hipMemcpyAsync(p->d_p12 + 2 * p->n, p2, b, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(rsd::launch_pack_points(p->d_p12, p->d_p12 + 2 * p->n, static_cast<int>(p->n),
                                   p->d_pts, c->stream));
+  // unit frame of the fp32 counting kernel: per-image centres, one common scale
+  const int64_t n = p->n;
+  double lo[4], hi[4];
+  bool finite = true;
+  for (int k = 0; k < 4; ++k) {
+    lo[k] = INFINITY;
+    hi[k] = -INFINITY;
+  }
+  for (int64_t i = 0; i < n; ++i) {
+    const double v[4] = {p1[i], p1[n + i], p2[i], p2[n + i]};
+    for (int k = 0; k < 4; ++k) {
+      finite &= std::isfinite(v[k]);
+      lo[k] = std::min(lo[k], v[k]);
+      hi[k] = std::max(hi[k], v[k]);
+    }
+  }
+  rsd::Frame fr{0.0, 0.5 * (lo[0] + hi[0]), 0.5 * (lo[1] + hi[1]), 0.5 * (lo[2] + hi[2]),
+                0.5 * (lo[3] + hi[3])};
+  const double cen[4] = {fr.cx1, fr.cy1, fr.cx2, fr.cy2};
+  for (int64_t i = 0; finite && i < n; ++i) {
+    const double v[4] = {p1[i], p1[n + i], p2[i], p2[n + i]};
+    for (int k = 0; k < 4; ++k) fr.s = std::max(fr.s, std::fabs(v[k] - cen[k]));
+  }
+  p->fp32_ok = finite && fr.s > 0.0 && std::isfinite(fr.s);
+  if (p->fp32_ok) {
+    fr.s *= 1.0 + 1e-12;  // |x~| <= 1 after the fp64 division
+    p->frame = fr;
+    HIP_TRY(rsd::launch_pack_points32(p->d_pts, static_cast<int>(n), fr, p->d_pts32, c->stream));
+  }
   HIP_TRY(hipStreamSynchronize(c->stream));
   return RS_OK;
 }
@@ -243,19 +315,22 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
                            hipMemcpyHostToDevice, s));
   }
   HIP_TRY(hipEventRecord(p->ev[0], s));
+  const bool fp32 = p->use_fp32 && p->fp32_ok;
   HIP_TRY(rsd::launch_f8_solve(p->d_pts, n, h, mode, seed, hyp_offset, p->d_tuples, p->d_F,
-                               p->ld, p->d_counts, p->d_status, s));
+                               p->ld, p->d_counts, p->d_status, s, p->d_F32,
+                               fp32 ? &p->frame : nullptr));
   HIP_TRY(hipEventRecord(p->ev[1], s));
-  HIP_TRY(rsd::launch_f8_count(p->d_pts, n, h, p->d_F, p->ld, choose_chunk(p, H),
-                               thresh * thresh, p->d_counts, s));
+  if (fp32)
+    HIP_TRY(rsd::launch_f8_count32(p->d_pts32, p->d_pts, n, h, p->d_F32, p->d_F, p->ld,
+                                   p->resident_waves, guard_constants(p->frame, thresh),
+                                   p->d_counts, s, p->count_block));
+  else
+    HIP_TRY(rsd::launch_f8_count(p->d_pts, n, h, p->d_F, p->ld, choose_chunk(p, H),
+                                 thresh * thresh, p->d_counts, s));
   HIP_TRY(hipEventRecord(p->ev[2], s));
-  HIP_TRY(rsd::launch_f8_select(p->d_counts, h, 1, p->d_cand, p->d_status, s));
-  const int sgrid = static_cast<int>(std::min<int64_t>(H, 1024));
-  HIP_TRY(rsd::launch_f8_stats(p->d_pts, n, p->d_F, p->ld, p->d_cand, p->d_status, thresh,
-                               p->d_ccount, p->d_cstd, p->d_cnorm, sgrid, s));
-  HIP_TRY(rsd::launch_f8_replay(p->d_cand, p->d_status, p->d_counts, p->d_ccount, p->d_cstd,
-                                p->d_cnorm, p->d_F, p->ld, p->d_res, s));
-  HIP_TRY(rsd::launch_f8_inliers(p->d_pts, n, thresh, p->d_res, s));
+  HIP_TRY(rsd::launch_f8_tail(p->d_pts, n, h, p->d_F, p->ld, p->d_counts, 1, thresh,
+                              p->d_status, p->d_cand, p->d_ccount, p->d_cstd, p->d_cnorm,
+                              p->d_res, s));
   HIP_TRY(hipEventRecord(p->ev[3], s));
   HIP_TRY(hipMemcpyAsync(p->h_res, p->d_res, p->res_bytes, hipMemcpyDeviceToHost, s));
   p->last_H = H;
@@ -300,17 +375,26 @@ extern "C" int rs_f8_plan_candidates(rs_f8_plan *p, rs_f8_candidate *out, int64_
   int st = plan_wait(p);
   if (st) return st;
   HIP_TRY(hipSetDevice(p->ctx->device));
-  int status[2];
-  HIP_TRY(hipMemcpy(status, p->d_status, sizeof(status), hipMemcpyDeviceToHost));
-  const int nc = status[1];
-  std::vector<int> cand(nc), cc(nc);
-  std::vector<double> cs(nc), cn(nc);
-  if (nc > 0) {
-    HIP_TRY(hipMemcpy(cand.data(), p->d_cand, sizeof(int) * nc, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(cc.data(), p->d_ccount, sizeof(int) * nc, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(cs.data(), p->d_cstd, sizeof(double) * nc, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(cn.data(), p->d_cnorm, sizeof(double) * nc, hipMemcpyDeviceToHost));
+  const int H = static_cast<int>(p->last_H);
+  const int nb = rsd::select_blocks(H), pb = rsd::select_per_block(H);
+  std::vector<int> bc(nb);
+  HIP_TRY(hipMemcpy(bc.data(), p->d_status + 4, sizeof(int) * nb, hipMemcpyDeviceToHost));
+  std::vector<int> cand, cc;
+  std::vector<double> cs, cn;
+  for (int b = 0; b < nb; ++b) {
+    if (bc[b] == 0) continue;
+    const size_t o = cand.size(), k = static_cast<size_t>(bc[b]);
+    const int64_t slot = static_cast<int64_t>(b) * pb;
+    cand.resize(o + k);
+    cc.resize(o + k);
+    cs.resize(o + k);
+    cn.resize(o + k);
+    HIP_TRY(hipMemcpy(&cand[o], p->d_cand + slot, sizeof(int) * k, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&cc[o], p->d_ccount + slot, sizeof(int) * k, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&cs[o], p->d_cstd + slot, sizeof(double) * k, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&cn[o], p->d_cnorm + slot, sizeof(double) * k, hipMemcpyDeviceToHost));
   }
+  const int nc = static_cast<int>(cand.size());
   int cmax = 0;
   for (int i = 0; i < nc; ++i) cmax = std::max(cmax, cc[i]);
   int64_t k = 0;

@@ -12,6 +12,19 @@ struct Pt {
   double x1, y1, x2, y2;
 };
 
+// Similarity frame of the fp32 counting kernel: x~ = (x - c_i) / s per image i, one common
+// scale s so both line-length terms scale by s^2 and the min() test is frame invariant.
+struct Frame {
+  double s, cx1, cy1, cx2, cy2;
+};
+
+// Rigorous error bounds of the fp32 test (see f8_kernels.hip, k_f8_count32).
+struct Guard32 {
+  float thr2;  // (t / s)^2 rounded to fp32
+  float K0, K1, Ku;
+  double thr2_px;  // t^2 for the fp64 re-test in pixel units
+};
+
 // ----------------------------------------------------------------------------------------
 // Philox4x32-10 counter-based generator (throughput-mode sampler).
 // ----------------------------------------------------------------------------------------

@@ -10,6 +10,8 @@
 namespace rsd {
 
 struct Pt;
+struct Frame;
+struct Guard32;
 
 // Grid of the selection passes; the status buffer holds 4 words + kSelectBlocks counts.
 constexpr int kSelectBlocks = 256;
@@ -36,19 +38,23 @@ hipError_t launch_pack_points(const double *p1, const double *p2, int n, Pt *pts
                               hipStream_t s);
 hipError_t launch_f8_solve(const Pt *pts, int n, int H, int mode, uint64_t seed,
                            uint64_t hyp_offset, const int *tuples, double *Fsoa, int64_t ld,
-                           int *counts, int *status, hipStream_t s);
+                           int *counts, int *status, hipStream_t s, float *F32soa = nullptr,
+                           const Frame *frame = nullptr);
+hipError_t launch_pack_points32(const Pt *pts, int n, const Frame &fr, float4 *pts32,
+                                hipStream_t s);
+hipError_t launch_f8_count32(const float4 *pts32, const Pt *pts, int n, int H,
+                             const float *F32soa, const double *Fsoa, int64_t ld, int waves,
+                             const Guard32 &g, int *counts, hipStream_t s, int blk = 4);
 hipError_t launch_f8_count(const Pt *pts, int n, int H, const double *Fsoa, int64_t ld,
                            int chunk, double thr2, int *counts, hipStream_t s);
-hipError_t launch_f8_select(const int *counts, int H, int slack, int *cand, int *status,
-                            hipStream_t s);
-hipError_t launch_f8_stats(const Pt *pts, int n, const double *Fsoa, int64_t ld,
-                           const int *cand, const int *status, double thresh, int *ccount,
-                           double *cstd, double *cnorm, int grid, hipStream_t s);
-hipError_t launch_f8_replay(const int *cand, const int *status, const int *counts,
-                            const int *ccount, const double *cstd, const double *cnorm,
-                            const double *Fsoa, int64_t ld, F8DevResult *res, hipStream_t s);
-hipError_t launch_f8_inliers(const Pt *pts, int n, double thresh, F8DevResult *res,
-                             hipStream_t s);
+// Selection tail: c* (k_f8_max), candidates + reference statistics (k_f8_cand_stats), replay
+// + S_RANSAC (k_f8_replay_inliers).  Candidates live in per-block segments of `cand`.
+int select_per_block(int H);
+int select_blocks(int H);
+hipError_t launch_f8_tail(const Pt *pts, int n, int H, const double *Fsoa, int64_t ld,
+                          const int *counts, int slack, double thresh, int *status, int *cand,
+                          int *ccount, double *cstd, double *cnorm, F8DevResult *res,
+                          hipStream_t s);
 hipError_t launch_residuals(const Pt *pts, int n, const double *F, double *out, hipStream_t s);
 
 }  // namespace rsd

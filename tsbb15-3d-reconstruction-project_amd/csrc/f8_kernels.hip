@@ -28,7 +28,8 @@ __global__ __launch_bounds__(256) void k_f8_solve(const Pt *__restrict__ pts, in
                                                   const int *__restrict__ tuples,
                                                   double *__restrict__ Fsoa, int64_t ld,
                                                   int *__restrict__ counts,
-                                                  int *__restrict__ status) {
+                                                  int *__restrict__ status,
+                                                  float *__restrict__ F32soa, Frame fr) {
   const int h = blockIdx.x * blockDim.x + threadIdx.x;
   if (h >= H) return;
   if (counts) counts[h] = 0;  // the counting kernel accumulates into it
@@ -53,6 +54,29 @@ __global__ __launch_bounds__(256) void k_f8_solve(const Pt *__restrict__ pts, in
   fmatrix8(xl, yl, xr, yr, F);
 #pragma unroll
   for (int k = 0; k < 9; ++k) Fsoa[k * ld + h] = F[k];
+  if (F32soa) {
+    // F~ = T1^T F T2 (T_i = [[s,0,cx_i],[0,s,cy_i],[0,0,1]]), scaled to max |F~_ij| = 1
+    double G[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      G[3 * r + 0] = F[3 * r + 0] * fr.s;
+      G[3 * r + 1] = F[3 * r + 1] * fr.s;
+      G[3 * r + 2] = F[3 * r + 0] * fr.cx2 + F[3 * r + 1] * fr.cy2 + F[3 * r + 2];
+    }
+    double Ft[9];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      Ft[0 + c] = fr.s * G[0 + c];
+      Ft[3 + c] = fr.s * G[3 + c];
+      Ft[6 + c] = fr.cx1 * G[0 + c] + fr.cy1 * G[3 + c] + G[6 + c];
+    }
+    double mx = 0.0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) mx = fmax(mx, fabs(Ft[k]));
+    const double kap = 1.0 / mx;  // F = 0 or non-finite -> NaN model, counts 0 on both paths
+#pragma unroll
+    for (int k = 0; k < 9; ++k) F32soa[k * ld + h] = static_cast<float>(Ft[k] * kap);
+  }
 }
 
 // ----------------------------------------------------------------------------------------
@@ -98,6 +122,135 @@ __global__ __launch_bounds__(256) void k_f8_count(const Pt *__restrict__ pts, in
 }
 
 // ----------------------------------------------------------------------------------------
+// fp32 counting with a rigorous fp64 guard band.
+//
+// In the frame x~ = (x - c_i)/s (|x~| <= R = 1) with F~ = T1^T F T2 / max|.| the test
+// e^2 < t^2 min(n1, n2) becomes e~^2 < (t/s)^2 min(n~1, n~2) exactly (e scales with the
+// model scale, n with its square, both line lengths with s^2).  Each fp32 operation and the
+// fp64->fp32 rounding of F~ and of the points is bounded absolutely (Dl for a line
+// component, De for e, Dn for a squared length; constants from the host, api.hip
+// guard_constants), giving a per-point bound
+//     B = 2 De |e| + De^2 + u (e^2 + 2 rhs) + (t/s)^2 Dn     (x 1.02 slack)
+// on |fl(e^2 - rhs) - (e^2 - rhs)_exact|.  Outside |d| <= B the fp32 sign is the exact one;
+// inside, the lane re-runs the fp64 test of k_f8_count (pixel units) -- bit-identical counts.
+// 26 fp32 VALU ops per (hypothesis, point) instead of 21 fp64 ones.
+// ----------------------------------------------------------------------------------------
+// One point of the fp32 test: returns d = e^2 - t~^2 m and its error bound B.
+__device__ __forceinline__ void test32(const float (&f)[9], const float4 &p, const Guard32 &g,
+                                       float &d, float &B) {
+  const float l10 = fmaf(f[0], p.z, fmaf(f[1], p.w, f[2]));
+  const float l11 = fmaf(f[3], p.z, fmaf(f[4], p.w, f[5]));
+  const float l12 = fmaf(f[6], p.z, fmaf(f[7], p.w, f[8]));
+  const float l20 = fmaf(f[0], p.x, fmaf(f[3], p.y, f[6]));
+  const float l21 = fmaf(f[1], p.x, fmaf(f[4], p.y, f[7]));
+  const float e = fmaf(l10, p.x, fmaf(l11, p.y, l12));
+  const float n1 = fmaf(l10, l10, l11 * l11);
+  const float n2 = fmaf(l20, l20, l21 * l21);
+  const float ee = e * e;
+  const float rhs = g.thr2 * fminf(n1, n2);
+  d = ee - rhs;
+  B = fmaf(fabsf(e), g.K1, fmaf(fmaf(rhs, 2.0f, ee), g.Ku, g.K0));
+}
+
+// The float64 test of k_f8_count (pixel units) for one (hypothesis, point).
+__device__ __forceinline__ bool test64(const double (&fd)[9], const Pt &q, double thr2) {
+  const double a10 = fma(fd[0], q.x2, fma(fd[1], q.y2, fd[2]));
+  const double a11 = fma(fd[3], q.x2, fma(fd[4], q.y2, fd[5]));
+  const double a12 = fma(fd[6], q.x2, fma(fd[7], q.y2, fd[8]));
+  const double a20 = fma(fd[0], q.x1, fma(fd[3], q.y1, fd[6]));
+  const double a21 = fma(fd[1], q.x1, fma(fd[4], q.y1, fd[7]));
+  const double ed = fma(a10, q.x1, fma(a11, q.y1, a12));
+  const double m1 = fma(a10, a10, a11 * a11);
+  const double m2 = fma(a20, a20, a21 * a21);
+  return ed * ed < thr2 * fmin(m1, m2);
+}
+
+// Work partition: the (group of 64 hypotheses) x (point) plane, flattened group-major, is cut
+// into W equal contiguous slices, one per wave, W = the number of waves the chip holds at
+// once (all resident, no tail round).  A slice covers the end of one group and the start of
+// the next (two segments, each with its own model load and one coalesced atomic).
+//
+// Points are processed in blocks of 4 (one s_load_dwordx16; the point arrays are padded with
+// NaN points, which are neither inliers nor ambiguous).  The main path counts only sure
+// inliers, d < -B; each point's ambiguity ballot |d| <= B stays in SGPRs and, once per block,
+// the flagged (lane, point) pairs are re-tested in float64.
+template <int BLK>
+__global__ __launch_bounds__(256) void k_f8_count32(const float4 *__restrict__ pts32,
+                                                    const Pt *__restrict__ pts, int n, int H,
+                                                    const float *__restrict__ F32soa,
+                                                    const double *__restrict__ Fsoa, int64_t ld,
+                                                    int64_t per_wave, Guard32 g,
+                                                    int *__restrict__ counts) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = wave_uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int64_t npad = (n + BLK - 1) / BLK * BLK;
+  const int64_t total = static_cast<int64_t>((H + 63) >> 6) * npad;
+  int64_t pos = w * per_wave;
+  const int64_t end = min(total, pos + per_wave);
+  while (pos < end) {
+    const int grp = static_cast<int>(pos / npad);
+    const int p0 = static_cast<int>(pos - grp * npad);
+    const int p1 = static_cast<int>(min(npad, p0 + (end - pos)));
+    pos += p1 - p0;
+    const int h = grp * 64 + lane;
+    const int hl = h < H ? h : H - 1;
+    float f[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) f[k] = F32soa[k * ld + hl];
+    int cnt = 0;
+    float4 cur[BLK];
+#pragma unroll
+    for (int k = 0; k < BLK; ++k) cur[k] = pts32[p0 + k];
+    for (int i = p0; i < p1; i += BLK) {
+      // prefetch the next block (software pipelining of the scalar loads)
+      float4 nxt[BLK];
+      const int j = (i + BLK < p1) ? i + BLK : i;
+#pragma unroll
+      for (int k = 0; k < BLK; ++k) nxt[k] = pts32[j + k];
+      unsigned long long amb[BLK];
+#pragma unroll
+      for (int k = 0; k < BLK; ++k) {
+        float d, B;
+        test32(f, cur[k], g, d, B);
+        cnt += (d < -B) ? 1 : 0;  // sure inlier
+        amb[k] = __ballot(fabsf(d) <= B);
+      }
+      unsigned long long any = 0ull;
+#pragma unroll
+      for (int k = 0; k < BLK; ++k) any |= amb[k];
+      if (any != 0ull) {
+        double fd[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) fd[k] = Fsoa[k * ld + hl];
+#pragma unroll
+        for (int k = 0; k < BLK; ++k)
+          if ((amb[k] >> lane) & 1ull) cnt += test64(fd, pts[i + k], g.thr2_px) ? 1 : 0;
+      }
+#pragma unroll
+      for (int k = 0; k < BLK; ++k) cur[k] = nxt[k];
+    }
+    if (h < H) atomicAdd(&counts[h], cnt);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pack_points32(const Pt *__restrict__ pts, int n,
+                                                       Frame fr, float4 *__restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ((n + 7) & ~7)) return;
+  if (i >= n) {  // padding: NaN points are never inliers and never ambiguous
+    const float qn = __builtin_nanf("");
+    out[i] = make_float4(qn, qn, qn, qn);
+    return;
+  }
+  const Pt p = pts[i];
+  const double is = 1.0 / fr.s;
+  out[i] = make_float4(static_cast<float>((p.x1 - fr.cx1) * is),
+                       static_cast<float>((p.y1 - fr.cy1) * is),
+                       static_cast<float>((p.x2 - fr.cx2) * is),
+                       static_cast<float>((p.y2 - fr.cy2) * is));
+}
+
+// ----------------------------------------------------------------------------------------
 // Selection over H counts in three grid-wide passes (no single-workgroup scan):
 //   k_f8_max        c* = max count (block max -> one atomicMax per block)
 //   k_f8_blockcount per block slice: number of hypotheses with count >= max(c* - slack, 1)
@@ -134,53 +287,6 @@ __global__ __launch_bounds__(256) void k_f8_max(const int *__restrict__ counts, 
   if (threadIdx.x == 0 && m > 0) atomicMax(&status[0], m);
 }
 
-__global__ __launch_bounds__(256) void k_f8_blockcount(const int *__restrict__ counts, int H,
-                                                       int slack, int per_block,
-                                                       const int *__restrict__ status,
-                                                       int *__restrict__ bc) {
-  __shared__ int sh[4];
-  const int cmax = status[0];
-  const int thr = max(cmax - slack, 1);
-  const int b0 = blockIdx.x * per_block, b1 = min(H, b0 + per_block);
-  int c = 0;
-  if (cmax > 0)
-    for (int i = b0 + threadIdx.x; i < b1; i += 256) c += counts[i] >= thr ? 1 : 0;
-  c = block_reduce_sum(c, sh);
-  if (threadIdx.x == 0) bc[blockIdx.x] = c;
-}
-
-__global__ __launch_bounds__(256) void k_f8_compact(const int *__restrict__ counts, int H,
-                                                    int slack, int per_block,
-                                                    int *__restrict__ status,
-                                                    const int *__restrict__ bc,
-                                                    int *__restrict__ cand) {
-  __shared__ int sh[4];
-  __shared__ int woff[4];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  int off = 0;
-  for (int j = tid; j < (int)blockIdx.x; j += 256) off += bc[j];
-  off = block_reduce_sum(off, sh);
-  const int cmax = status[0];
-  const int thr = max(cmax - slack, 1);
-  const int b0 = blockIdx.x * per_block, b1 = min(H, b0 + per_block);
-  if (cmax > 0 && bc[blockIdx.x] > 0) {
-    for (int b = b0; b < b1; b += 256) {
-      const int i = b + tid;
-      const bool take = i < b1 && counts[i] >= thr;
-      const unsigned long long bal = __ballot(take);
-      if (lane == 0) woff[w] = __popcll(bal);
-      __syncthreads();
-      int base = off;
-      for (int q = 0; q < w; ++q) base += woff[q];
-      const int tot = woff[0] + woff[1] + woff[2] + woff[3];
-      if (take) cand[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
-      off += tot;
-      __syncthreads();
-    }
-  }
-  if (blockIdx.x == gridDim.x - 1 && tid == 0) status[1] = off + (cmax > 0 ? 0 : 0);
-}
-
 // ----------------------------------------------------------------------------------------
 // Reference-order statistics, wave per candidate (grid-stride).
 // ----------------------------------------------------------------------------------------
@@ -205,20 +311,47 @@ __device__ __forceinline__ double block_sum_d(double v, double *sh) {
   return r;
 }
 
-// Workgroup (256 threads) per candidate, grid-stride over the device-side candidate count.
-__global__ __launch_bounds__(256) void k_f8_stats(const Pt *__restrict__ pts, int n,
-                                                  const double *__restrict__ Fsoa, int64_t ld,
-                                                  const int *__restrict__ cand,
-                                                  const int *__restrict__ status, double thresh,
-                                                  int *__restrict__ ccount,
-                                                  double *__restrict__ cstd,
-                                                  double *__restrict__ cnorm) {
+// Candidates + their reference-order statistics, one block per slice of hypotheses:
+// every hypothesis of the slice with fast count >= max(c* - slack, 1) is appended in index
+// order to the block's own segment cand[b * per_block + j] (bc[b] entries), then the block
+// re-scores each of them with dist_ref: count, np.std(d) (two-pass), np.linalg.norm(d).
+__global__ __launch_bounds__(256) void k_f8_cand_stats(const Pt *__restrict__ pts, int n,
+                                                       const double *__restrict__ Fsoa,
+                                                       int64_t ld, const int *__restrict__ counts,
+                                                       int H, int slack, int per_block,
+                                                       const int *__restrict__ status,
+                                                       double thresh, int *__restrict__ bc,
+                                                       int *__restrict__ cand,
+                                                       int *__restrict__ ccount,
+                                                       double *__restrict__ cstd,
+                                                       double *__restrict__ cnorm) {
   __shared__ double shd[4];
   __shared__ int shi[4];
-  const int tid = threadIdx.x;
-  const int nc = status[1];
-  for (int c = blockIdx.x; c < nc; c += gridDim.x) {
-    const int h = cand[c];
+  __shared__ int woff[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int cmax = status[0];
+  const int thr = max(cmax - slack, 1);
+  const int b0 = blockIdx.x * per_block, b1 = min(H, b0 + per_block);
+  int *seg = cand + static_cast<int64_t>(blockIdx.x) * per_block;
+  int nloc = 0;
+  if (cmax > 0) {
+    for (int b = b0; b < b1; b += 256) {
+      const int i = b + tid;
+      const bool take = i < b1 && counts[i] >= thr;
+      const unsigned long long bal = __ballot(take);
+      if (lane == 0) woff[w] = __popcll(bal);
+      __syncthreads();
+      int base = nloc;
+      for (int q = 0; q < w; ++q) base += woff[q];
+      if (take) seg[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
+      nloc += woff[0] + woff[1] + woff[2] + woff[3];
+      __syncthreads();
+    }
+  }
+  if (tid == 0) bc[blockIdx.x] = nloc;
+  __syncthreads();  // seg[] written by this block is visible to all its threads
+  for (int j = 0; j < nloc; ++j) {
+    const int h = seg[j];
     double f[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) f[k] = Fsoa[k * ld + h];
@@ -241,9 +374,10 @@ __global__ __launch_bounds__(256) void k_f8_stats(const Pt *__restrict__ pts, in
     }
     s3 = block_sum_d(s3, shd);
     if (tid == 0) {
-      ccount[c] = cnt;
-      cstd[c] = sqrt(s3 / static_cast<double>(n));
-      cnorm[c] = sqrt(s2);
+      const int64_t slot = static_cast<int64_t>(blockIdx.x) * per_block + j;
+      ccount[slot] = cnt;
+      cstd[slot] = sqrt(s3 / static_cast<double>(n));
+      cnorm[slot] = sqrt(s2);
     }
   }
 }
@@ -260,83 +394,111 @@ __device__ __forceinline__ uint64_t key_norm(double v) {  // "y > norm" is false
   return (v != v) ? ~0ull : static_cast<uint64_t>(__double_as_longlong(v));
 }
 
-__global__ __launch_bounds__(64) void k_f8_replay(const int *__restrict__ cand,
-                                                  const int *__restrict__ status,
-                                                  const int *__restrict__ counts,
-                                                  const int *__restrict__ ccount,
-                                                  const double *__restrict__ cstd,
-                                                  const double *__restrict__ cnorm,
-                                                  const double *__restrict__ Fsoa, int64_t ld,
-                                                  F8DevResult *__restrict__ res) {
-  const int lane = threadIdx.x;
-  const int nc = status[1];
-  int best = -1, bcount = 0;
-  uint64_t bstd = 0ull;  // S_RANSAC = [], norm([]) = 0
-  int mismatch = 0;
-  for (int b = 0; b < nc; b += 64) {
-    const int c = b + lane;
-    int cc = 0;
-    uint64_t ks = 0, kn = 0;
-    if (c < nc) {
-      cc = ccount[c];
-      ks = key_std(cstd[c]);
-      kn = key_norm(cnorm[c]);
-      mismatch += (cc != counts[cand[c]]) ? 1 : 0;
-    }
-    const int lim = min(64, nc - b);
-    for (int q = 0; q < lim; ++q) {
-      const int qc = __shfl(cc, q);
-      const uint64_t qs = __shfl(ks, q);
-      const uint64_t qn = __shfl(kn, q);
-      if (qc > bcount) {
-        best = b + q;
-        bcount = qc;
-        bstd = qs;
-      } else if (qc == bcount && bcount > 0 && bstd > qn) {
-        best = b + q;
-        bstd = qs;
-      }
-    }
-  }
-  mismatch = wave_sum_i(mismatch);
-  if (lane == 0) {
-    res->n_candidates = nc;
-    res->max_count_fast = status[0];
-    res->guard_mismatch = mismatch;
-    if (best >= 0) {
-      const int h = cand[best];
-      res->best_index = h;
-      res->best_count = bcount;
-      res->best_std = cstd[best];
-      res->best_norm = cnorm[best];
-      res->best_cand = best;
-      for (int k = 0; k < 9; ++k) res->F[k] = Fsoa[k * ld + h];
-    } else {
-      res->best_index = -1;
-      res->best_count = 0;
-      res->best_std = 0.0;
-      res->best_norm = 0.0;
-      res->best_cand = -1;
-      for (int k = 0; k < 9; ++k) res->F[k] = 0.0;
-    }
-  }
-}
-
-// ----------------------------------------------------------------------------------------
-// S_RANSAC of the winner: ascending indices with d < thresh (np.flatnonzero order).
-// ----------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_f8_inliers(const Pt *__restrict__ pts, int n,
-                                                     double thresh,
-                                                     F8DevResult *__restrict__ res) {
+// One 1024-thread workgroup: wave 0 replays fun.py:320-328 over the candidates in global
+// index order (segments of k_f8_cand_stats in block order), 64 per coalesced load; then the
+// whole workgroup extracts S_RANSAC = flatnonzero(d < t) of the winner in order.
+__global__ __launch_bounds__(1024) void k_f8_replay_inliers(
+    const Pt *__restrict__ pts, int n, const int *__restrict__ counts, int nb, int per_block,
+    const int *__restrict__ bc, const int *__restrict__ cand, const int *__restrict__ ccount,
+    const double *__restrict__ cstd, const double *__restrict__ cnorm,
+    const double *__restrict__ Fsoa, int64_t ld, const int *__restrict__ status,
+    double thresh, int *__restrict__ status_out, F8DevResult *__restrict__ res) {
+  __shared__ int pref[kSelectBlocks + 1];
   __shared__ int woff[16];
   __shared__ int base_s;
+  __shared__ double fsh[9];
+  __shared__ int have_s;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const bool have = res->best_index >= 0;
+  if (tid == 0) {
+    int acc = 0;
+    for (int q = 0; q < nb; ++q) {
+      pref[q] = acc;
+      acc += bc[q];
+    }
+    pref[nb] = acc;
+  }
+  __syncthreads();
+  const int nc = pref[nb];
+  if (w == 0) {
+    int best = -1, bcount = 0;
+    uint64_t bstd = 0ull;  // S_RANSAC = [], norm([]) = 0
+    int mismatch = 0;
+    for (int b = 0; b < nc; b += 64) {
+      const int c = b + lane;
+      int cc = 0;
+      uint64_t ks = 0, kn = 0;
+      if (c < nc) {
+        int lo = 0, hi = nb - 1;  // block q with pref[q] <= c < pref[q+1]
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (pref[mid] <= c) lo = mid; else hi = mid - 1;
+        }
+        const int64_t slot = static_cast<int64_t>(lo) * per_block + (c - pref[lo]);
+        cc = ccount[slot];
+        ks = key_std(cstd[slot]);
+        kn = key_norm(cnorm[slot]);
+        mismatch += (cc != counts[cand[slot]]) ? 1 : 0;
+      }
+      const int lim = min(64, nc - b);
+      for (int q = 0; q < lim; ++q) {
+        const int qc = __shfl(cc, q);
+        const uint64_t qs = __shfl(ks, q);
+        const uint64_t qn = __shfl(kn, q);
+        if (qc > bcount) {
+          best = b + q;
+          bcount = qc;
+          bstd = qs;
+        } else if (qc == bcount && bcount > 0 && bstd > qn) {
+          best = b + q;
+          bstd = qs;
+        }
+      }
+    }
+    mismatch = wave_sum_i(mismatch);
+    if (lane == 0) {
+      res->n_candidates = nc;
+      res->max_count_fast = status[0];
+      res->guard_mismatch = mismatch;
+      status_out[1] = nc;
+      if (best >= 0) {
+        int lo = 0, hi = nb - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (pref[mid] <= best) lo = mid; else hi = mid - 1;
+        }
+        const int64_t slot = static_cast<int64_t>(lo) * per_block + (best - pref[lo]);
+        const int h = cand[slot];
+        res->best_index = h;
+        res->best_count = bcount;
+        res->best_std = cstd[slot];
+        res->best_norm = cnorm[slot];
+        res->best_cand = best;
+        for (int k = 0; k < 9; ++k) {
+          const double v = Fsoa[k * ld + h];
+          res->F[k] = v;
+          fsh[k] = v;
+        }
+        have_s = 1;
+      } else {
+        res->best_index = -1;
+        res->best_count = 0;
+        res->best_std = 0.0;
+        res->best_norm = 0.0;
+        res->best_cand = -1;
+        for (int k = 0; k < 9; ++k) {
+          res->F[k] = 0.0;
+          fsh[k] = 0.0;
+        }
+        have_s = 0;
+      }
+      base_s = 0;
+    }
+  }
+  __syncthreads();
+  const bool have = have_s != 0;
   double f[9];
 #pragma unroll
-  for (int k = 0; k < 9; ++k) f[k] = res->F[k];
-  if (tid == 0) base_s = 0;
-  __syncthreads();
+  for (int k = 0; k < 9; ++k) f[k] = fsh[k];
   for (int b = 0; b < n; b += 1024) {
     const int i = b + tid;
     const bool take = have && i < n && dist_ref(f, pts[i]) < thresh;
@@ -404,9 +566,12 @@ hipError_t launch_pack_points(const double *p1, const double *p2, int n, Pt *pts
 
 hipError_t launch_f8_solve(const Pt *pts, int n, int H, int mode, uint64_t seed,
                            uint64_t hyp_offset, const int *tuples, double *Fsoa, int64_t ld,
-                           int *counts, int *status, hipStream_t s) {
+                           int *counts, int *status, hipStream_t s, float *F32soa,
+                           const Frame *frame) {
+  const Frame fr = frame ? *frame : Frame{1.0, 0.0, 0.0, 0.0, 0.0};
   hipLaunchKernelGGL(k_f8_solve, dim3((H + 255) / 256), dim3(256), 0, s, pts, n, H, mode, seed,
-                     hyp_offset, tuples, Fsoa, ld, counts, status);
+                     hyp_offset, tuples, Fsoa, ld, counts, status, frame ? F32soa : nullptr,
+                     fr);
   return hipGetLastError();
 }
 
@@ -419,38 +584,51 @@ hipError_t launch_f8_count(const Pt *pts, int n, int H, const double *Fsoa, int6
   return hipGetLastError();
 }
 
-hipError_t launch_f8_select(const int *counts, int H, int slack, int *cand, int *status,
-                            hipStream_t s) {
-  int *bc = status + 4;  // kSelectBlocks block counts live behind the status words
-  const int per_block = (H + kSelectBlocks - 1) / kSelectBlocks;
-  const int nb = (H + per_block - 1) / per_block;
-  hipLaunchKernelGGL(k_f8_max, dim3(std::min(nb, 256)), dim3(256), 0, s, counts, H, status);
-  hipLaunchKernelGGL(k_f8_blockcount, dim3(nb), dim3(256), 0, s, counts, H, slack, per_block,
-                     status, bc);
-  hipLaunchKernelGGL(k_f8_compact, dim3(nb), dim3(256), 0, s, counts, H, slack, per_block,
-                     status, bc, cand);
+hipError_t launch_pack_points32(const Pt *pts, int n, const Frame &fr, float4 *pts32,
+                                hipStream_t s) {
+  hipLaunchKernelGGL(k_pack_points32, dim3((n + 7 + 255) / 256), dim3(256), 0, s, pts, n, fr,
+                     pts32);
   return hipGetLastError();
 }
 
-hipError_t launch_f8_stats(const Pt *pts, int n, const double *Fsoa, int64_t ld,
-                           const int *cand, const int *status, double thresh, int *ccount,
-                           double *cstd, double *cnorm, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(k_f8_stats, dim3(grid), dim3(256), 0, s, pts, n, Fsoa, ld, cand, status,
-                     thresh, ccount, cstd, cnorm);
+hipError_t launch_f8_count32(const float4 *pts32, const Pt *pts, int n, int H,
+                             const float *F32soa, const double *Fsoa, int64_t ld, int waves,
+                             const Guard32 &g, int *counts, hipStream_t s, int blk) {
+  blk = blk == 8 ? 8 : 4;
+  const int64_t npad = (n + blk - 1) / blk * blk;
+  const int64_t total = static_cast<int64_t>((H + 63) / 64) * npad;
+  // at least 64 points per slice; slices are multiples of the point block
+  int64_t W = std::max<int64_t>(1, std::min<int64_t>(waves, total / 64));
+  int64_t per = (total + W - 1) / W;
+  per = (per + blk - 1) / blk * blk;
+  W = (total + per - 1) / per;
+  const dim3 grid(static_cast<unsigned>((W + 3) / 4));
+  if (blk == 8)
+    hipLaunchKernelGGL(k_f8_count32<8>, grid, dim3(256), 0, s, pts32, pts, n, H, F32soa, Fsoa,
+                       ld, per, g, counts);
+  else
+    hipLaunchKernelGGL(k_f8_count32<4>, grid, dim3(256), 0, s, pts32, pts, n, H, F32soa, Fsoa,
+                       ld, per, g, counts);
   return hipGetLastError();
 }
 
-hipError_t launch_f8_replay(const int *cand, const int *status, const int *counts,
-                            const int *ccount, const double *cstd, const double *cnorm,
-                            const double *Fsoa, int64_t ld, F8DevResult *res, hipStream_t s) {
-  hipLaunchKernelGGL(k_f8_replay, dim3(1), dim3(64), 0, s, cand, status, counts, ccount, cstd,
-                     cnorm, Fsoa, ld, res);
-  return hipGetLastError();
+int select_per_block(int H) { return (H + kSelectBlocks - 1) / kSelectBlocks; }
+int select_blocks(int H) {
+  const int pb = select_per_block(H);
+  return (H + pb - 1) / pb;
 }
 
-hipError_t launch_f8_inliers(const Pt *pts, int n, double thresh, F8DevResult *res,
-                             hipStream_t s) {
-  hipLaunchKernelGGL(k_f8_inliers, dim3(1), dim3(1024), 0, s, pts, n, thresh, res);
+hipError_t launch_f8_tail(const Pt *pts, int n, int H, const double *Fsoa, int64_t ld,
+                          const int *counts, int slack, double thresh, int *status, int *cand,
+                          int *ccount, double *cstd, double *cnorm, F8DevResult *res,
+                          hipStream_t s) {
+  int *bc = status + 4;  // per-block candidate counts live behind the status words
+  const int pb = select_per_block(H), nb = select_blocks(H);
+  hipLaunchKernelGGL(k_f8_max, dim3(nb), dim3(256), 0, s, counts, H, status);
+  hipLaunchKernelGGL(k_f8_cand_stats, dim3(nb), dim3(256), 0, s, pts, n, Fsoa, ld, counts, H,
+                     slack, pb, status, thresh, bc, cand, ccount, cstd, cnorm);
+  hipLaunchKernelGGL(k_f8_replay_inliers, dim3(1), dim3(1024), 0, s, pts, n, counts, nb, pb, bc,
+                     cand, ccount, cstd, cnorm, Fsoa, ld, status, thresh, status, res);
   return hipGetLastError();
 }
 

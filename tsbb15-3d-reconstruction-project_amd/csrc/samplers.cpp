@@ -125,16 +125,71 @@ extern "C" int rs_py_seed(const uint32_t *words, int32_t n_words, uint32_t *mt_k
 
 namespace {
 
-// One Fisher-Yates hypothesis over a scratch identity permutation; writes x[0:k].
+// Block-tempered MT19937 stream: after each twist all 624 words are tempered at once (two
+// vectorisable loops), so a draw is a buffer read.  (key, pos) keep numpy's / CPython's exact
+// meaning: `out[j]` is the tempered `key[j]`, the next draw is out[pos].
+struct MtStream {
+  uint32_t key[kN];
+  uint32_t out[kN];
+  int pos;
+
+  __attribute__((target_clones("avx2", "default"))) static void temper_all(const uint32_t *k,
+                                                                           uint32_t *o) {
+    for (int i = 0; i < kN; ++i) {
+      uint32_t y = k[i];
+      y ^= (y >> 11);
+      y ^= (y << 7) & 0x9d2c5680u;
+      y ^= (y << 15) & 0xefc60000u;
+      y ^= (y >> 18);
+      o[i] = y;
+    }
+  }
+  __attribute__((target_clones("avx2", "default"))) static void twist_all(uint32_t *k) {
+    for (int i = 0; i < kN - kM; ++i) {
+      const uint32_t y = (k[i] & kUpper) | (k[i + 1] & kLower);
+      k[i] = k[i + kM] ^ (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
+    }
+    for (int i = kN - kM; i < kN - 1; ++i) {
+      const uint32_t y = (k[i] & kUpper) | (k[i + 1] & kLower);
+      k[i] = k[i + (kM - kN)] ^ (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
+    }
+    const uint32_t y = (k[kN - 1] & kUpper) | (k[0] & kLower);
+    k[kN - 1] = k[kM - 1] ^ (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
+  }
+  void load(const uint32_t *k, int32_t p) {
+    std::memcpy(key, k, sizeof(key));
+    pos = p;
+    temper_all(key, out);  // valid for the words at pos..623 of the current block
+  }
+  void store(uint32_t *k, int32_t *p) const {
+    std::memcpy(k, key, sizeof(key));
+    *p = pos;
+  }
+  inline uint32_t next() {
+    if (__builtin_expect(pos >= kN, 0)) {
+      twist_all(key);
+      temper_all(key, out);
+      pos = 0;
+    }
+    return out[pos++];
+  }
+};
+
+// One Fisher-Yates hypothesis x = arange(n); for i = n-1..1: swap(x[i], x[draw(i)]) and the
+// k-prefix of the result.  Position i is final after step i, so x[i] is only written back
+// while i < k (the prefix); x[j] always receives the old x[i].
 template <class Draw>
 inline void fisher_yates_prefix(std::vector<int32_t> &perm, const std::vector<int32_t> &iota,
                                 int64_t n, int32_t k, int32_t *out, Draw draw) {
   std::memcpy(perm.data(), iota.data(), sizeof(int32_t) * static_cast<size_t>(n));
   int32_t *x = perm.data();
+  uint32_t mask = smear_mask(static_cast<uint32_t>(n > 1 ? n - 1 : 0));
   for (int64_t i = n - 1; i >= 1; --i) {
-    const int64_t j = draw(static_cast<uint32_t>(i));
+    const uint32_t iu = static_cast<uint32_t>(i);
+    if (iu <= (mask >> 1)) mask >>= 1;  // mask == smear_mask(i)
+    const int64_t j = draw(iu, mask);
     const int32_t t = x[i];
-    x[i] = x[j];
+    if (i < k) x[i] = x[j];
     x[j] = t;
   }
   std::memcpy(out, x, sizeof(int32_t) * static_cast<size_t>(k));
@@ -152,12 +207,12 @@ extern "C" int rs_np_choice_tuples(uint32_t *mt_key, int32_t *mt_pos, int64_t n,
                     "Cannot take a larger sample than population when 'replace=False'");
   if (n > 0x7fffffffLL) return rs::fail(RS_EINVAL, "population too large");
   if (*mt_pos < 0 || *mt_pos > kN) return rs::fail(RS_EINVAL, "bad MT19937 position");
-  Mt mt;
+  MtStream mt;
   mt.load(mt_key, *mt_pos);
   std::vector<int32_t> perm(static_cast<size_t>(n > 0 ? n : 1)), iota(perm.size());
   for (int64_t i = 0; i < n; ++i) iota[static_cast<size_t>(i)] = static_cast<int32_t>(i);
-  auto draw = [&mt](uint32_t max) -> int64_t {  // numpy random_interval(max), max < 2^32
-    const uint32_t mask = smear_mask(max);
+  // numpy random_interval(max): draws u32 & smear(max) until <= max
+  auto draw = [&mt](uint32_t max, uint32_t mask) -> int64_t {
     uint32_t v;
     while ((v = (mt.next() & mask)) > max) {
     }
@@ -179,11 +234,11 @@ extern "C" int rs_py_shuffle_tuples(uint32_t *mt_key, int32_t *mt_pos, int64_t n
                     "set_length");
   if (k < 0 || count < 0 || n > 0x7fffffffLL) return rs::fail(RS_EINVAL, "bad dimensions");
   if (*mt_pos < 0 || *mt_pos > kN) return rs::fail(RS_EINVAL, "bad MT19937 position");
-  Mt mt;
+  MtStream mt;
   mt.load(mt_key, *mt_pos);
   std::vector<int32_t> perm(static_cast<size_t>(n > 0 ? n : 1)), iota(perm.size());
   for (int64_t i = 0; i < n; ++i) iota[static_cast<size_t>(i)] = static_cast<int32_t>(i);
-  auto draw = [&mt](uint32_t i) -> int64_t {  // randbelow(i + 1)
+  auto draw = [&mt](uint32_t i, uint32_t) -> int64_t {  // randbelow(i + 1)
     const uint32_t lim = i + 1;
     const int kb = bit_length(lim);
     uint32_t r;
