@@ -148,20 +148,20 @@ def main():
         _ffi.check(_ffi.lib().rs_comm_init(ctx.handle, world, rank, _ffi.ptr(uid, ctypes.c_uint8)))
 
     def step(i):
+        # one full RANSAC run; runs are stream-ordered and issued back to back (each run
+        # copies its own result record + S_RANSAC into its own pinned slot)
         plan.run(H, mode=_ffi.SAMPLER_PHILOX, seed=0xC2, hyp_offset=i * H)
-        return plan.result()
 
     for i in range(args.warmup):
         step(i)
+    plan.result()
     ctx.synchronize()
     dist.barrier()
-    count_ms, solve_ms = [], []
     t0 = time.perf_counter()
     for i in range(args.steps):
-        r, _ = step(args.warmup + i)
-        km = plan.kernel_ms()
-        count_ms.append(km["count_ms"])
-        solve_ms.append(km["solve_ms"])
+        step(args.warmup + i)
+    r, inl = plan.result()          # waits for the last run
+    assert r.best_count > 0 and len(inl) == r.best_count
     if comm:  # RCCL all-gather of the per-pair best models (F, count, index)
         rec = np.zeros(12, np.float64)
         rec[:9] = r.F[:]
@@ -177,7 +177,8 @@ def main():
     total_hyps = H * args.steps * world
     value = total_hyps / el
 
-    c_ms = float(np.mean(count_ms))
+    km = plan.kernel_ms(last_n=args.steps)   # HIP events of the timed runs (<= 64)
+    c_ms = km["count_ms"]
     achieved = H * FLOP_PER_CORR * args.n / (c_ms * 1e-3) / 1e12
     pmc = load_pmc(args.n, H)
     line = {
@@ -206,7 +207,8 @@ def main():
                                     "avg_ms": c_ms},
                      "note": "FP64 vector-ALU bound (SURVEY.md 8(d)); HBM traffic per launch "
                              "from rocprofv3 PMC in profiles/ (traffic, bytes)"},
-        "kernels_ms": {"k_f8_count": c_ms, "k_f8_solve": float(np.mean(solve_ms))},
+        "kernels_ms": {"k_f8_count": c_ms, "k_f8_solve": km["solve_ms"],
+                       "run_device_total": km["total_ms"]},
     }
     if pmc:
         line["hbm_roofline"] = {"bound": "hbm", "achieved": pmc / (c_ms * 1e-3) / 1e9,

@@ -131,8 +131,12 @@ int rs_f8_plan_candidates(rs_f8_plan *plan, rs_f8_candidate *out, int64_t cap, i
 /* Per-hypothesis fast counts / models of the last run (test & diagnostics). */
 int rs_f8_plan_counts(rs_f8_plan *plan, int32_t *counts, int64_t H);
 int rs_f8_plan_models(rs_f8_plan *plan, double *F_out, int64_t H);
-/* Average device time (ms) of the counting kernel over the last run (HIP events). */
+/* Device time (ms, HIP events on the plan's stream) of the counting kernel, the solve kernel
+ * and the whole run: of the last run, or averaged over the last `last_n` runs (<= 64).  Runs
+ * may be issued back to back (each owns a result slot); rs_f8_plan_result waits for the last. */
 int rs_f8_plan_kernel_ms(rs_f8_plan *plan, double *score_ms, double *solve_ms, double *total_ms);
+int rs_f8_plan_kernel_avg(rs_f8_plan *plan, int64_t last_n, double *score_ms, double *solve_ms,
+                          double *total_ms);
 
 /* One call: numpy-exact sampling (advancing mt_key/mt_pos in place) + GPU evaluation. */
 int rs_f8_ransac_np(rs_ctx *ctx, const double *p1, const double *p2, int64_t n, int64_t H,

@@ -15,7 +15,7 @@ import shutil
 import sys
 from collections import defaultdict
 
-KERNEL = "k_f8_count"
+KERNEL = "k_f8_count32"
 
 
 def per_launch(path, kernel):
@@ -54,14 +54,14 @@ def main():
         "launches_sampled": launches,
         "hbm_bytes_per_launch": fetch + write,
         "hbm_bytes_per_launch_fetch_x2_upper": 2 * fetch + write,
-        "kernel_stats_avg_ns": stats.get(f"rsd::{KERNEL}", {}).get("avg_ns"),
-        "bench_hip_event_avg_ms": bench["kernels_ms"][KERNEL],
+        "kernel_stats_avg_ns": next((v["avg_ns"] for k, v in stats.items() if KERNEL in k), None),
+        "bench_hip_event_avg_ms": bench["kernels_ms"]["k_f8_count"],
         "valu_insts_per_wave_point": (counters.get("SQ_INSTS_VALU", 0.0) /
                                       (bench["config"]["hypotheses_per_step"] *
                                        bench["config"]["n_corr"] / 64.0)),
         "source": f"rocprofv3 --pmc passes of bench.py (tools/gpu_round.sh), {src}",
     }
-    with open(os.path.join(prof, f"{tag}_pmc_{KERNEL}.json"), "w") as f:
+    with open(os.path.join(prof, f"{tag}_pmc_k_f8_count.json"), "w") as f:
         json.dump(out, f, indent=1)
     with open(os.path.join(prof, f"{tag}_bench.json"), "w") as f:
         json.dump(bench, f, indent=1)

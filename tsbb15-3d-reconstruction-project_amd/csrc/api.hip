@@ -126,9 +126,15 @@ struct rs_f8_plan {
   int *d_ccount = nullptr;
   double *d_cstd = nullptr, *d_cnorm = nullptr;
   rsd::F8DevResult *d_res = nullptr;
-  rsd::F8DevResult *h_res = nullptr;  // pinned
+  // Runs are stream-ordered and may be issued back to back without a host round trip: each
+  // run copies its result into its own pinned slot and records its own events.
+  static constexpr int kSlots = 4, kEvRing = 64;
+  rsd::F8DevResult *h_slot[kSlots] = {};  // pinned result slots
+  rsd::F8DevResult *h_res = nullptr;      // slot of the last run
+  hipEvent_t done[kSlots] = {};           // D2H of a slot complete
   size_t res_bytes = 0;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ring[kEvRing][4] = {};       // per-run kernel events (solve, count, tail)
+  int64_t runs = 0;                       // runs issued on this plan
   int64_t last_H = 0;
   bool pending = false, have_result = false;
   int chunk_override = 0;
@@ -139,7 +145,11 @@ struct rs_f8_plan {
   bool fp32_ok = false;   // finite points and a non-degenerate frame
   bool use_fp32 = true;   // RSAMD_COUNT=fp64 selects the float64 kernel
   int resident_waves = 8192;  // CUs x 4 SIMDs x 8 waves (RSAMD_WAVES overrides)
-  int count_block = 4;        // points per scalar-load block (RSAMD_BLOCK = 4 | 8)
+  int count_block = 8;        // points per scalar-load block (RSAMD_BLOCK = 4 | 8)
+  bool prefetch = true;       // software-pipelined point loads (RSAMD_PREFETCH=0 off)
+  bool packed = false;        // two hypotheses per lane, v_pk_fma_f32 (RSAMD_COUNT=pk)
+  int pk_variant = 0;         // RSAMD_PKVAR: 0 (2-pt blocks, 8 waves/SIMD), 1 (6), 2 (4), 3
+  int pk_waves = 8192;        // resident waves of the chosen variant
 };
 
 namespace {
@@ -162,6 +172,23 @@ rsd::Guard32 guard_constants(const rsd::Frame &fr, double thresh) {
   return g;
 }
 
+rsd::GuardPk guard_packed(const rsd::Frame &fr, double thresh) {
+  const double u = std::ldexp(1.0, -24), R = 1.0 + 1e-6, Lm = 2.0 * R + 1.0;
+  const double Dl = 1.1 * u * (7.0 * R + 3.0);
+  const double De =
+      1.1 * (2.0 * (Dl * R * 1.001 + Lm * u * R) + Dl + u * (Lm + Dl) * (3.0 * R + 2.0) * 1.001);
+  const double Dn = 1.1 * (2.0 * Dl * (2.0 * Lm + Dl) + 3.0 * u * (Lm + Dl) * (Lm + Dl) * 1.001);
+  const double thr2 = (thresh / fr.s) * (thresh / fr.s);
+  const double c = std::sqrt(thr2);  // AM-GM split point for 2 De |e| <= De (e^2 / c + c)
+  rsd::GuardPk g;
+  g.thr2 = static_cast<float>(thr2);
+  g.Ka = static_cast<float>(1.02 * (De / c * (1.0 + 2.0 * u) + u));
+  g.Kb = static_cast<float>(1.02 * 2.0 * u);
+  g.K0 = static_cast<float>(1.02 * (De * c + De * De + thr2 * (1.0 + 1e-6) * Dn));
+  g.thr2_px = thresh * thresh;
+  return g;
+}
+
 }  // namespace
 
 static void plan_free(rs_f8_plan *p) {
@@ -178,9 +205,13 @@ static void plan_free(rs_f8_plan *p) {
   (void)hipFree(p->d_res);
   (void)hipFree(p->d_pts32);
   (void)hipFree(p->d_F32);
-  if (p->h_res) (void)hipHostFree(p->h_res);
-  for (auto &e : p->ev)
+  for (auto &h : p->h_slot)
+    if (h) (void)hipHostFree(h);
+  for (auto &e : p->done)
     if (e) (void)hipEventDestroy(e);
+  for (auto &r : p->ring)
+    for (auto &e : r)
+      if (e) (void)hipEventDestroy(e);
 }
 
 extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_plan **out) {
@@ -197,14 +228,22 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
   p->ld = (max_hyp + 63) / 64 * 64;
   p->res_bytes = sizeof(rsd::F8DevResult) + sizeof(int64_t) * static_cast<size_t>(n);
   if (const char *ch = std::getenv("RSAMD_CHUNK")) p->chunk_override = std::atoi(ch);
-  if (const char *cm = std::getenv("RSAMD_COUNT")) p->use_fp32 = std::strcmp(cm, "fp64") != 0;
+  if (const char *cm = std::getenv("RSAMD_COUNT")) {
+    p->use_fp32 = std::strcmp(cm, "fp64") != 0;
+    p->packed = std::strcmp(cm, "pk") == 0;  // "fp32" (default), "pk", "fp64"
+  }
   {
     int cus = 256;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
       cus = 256;
-    p->resident_waves = cus * 4 * 8;
+    p->resident_waves = cus * 4 * 8 * 4;  // 4 slices per resident wave slot (sweep r01)
     if (const char *wv = std::getenv("RSAMD_WAVES")) p->resident_waves = std::max(1, std::atoi(wv));
     if (const char *bk = std::getenv("RSAMD_BLOCK")) p->count_block = std::atoi(bk) == 8 ? 8 : 4;
+    if (const char *pf = std::getenv("RSAMD_PREFETCH")) p->prefetch = std::atoi(pf) != 0;
+    if (const char *pv = std::getenv("RSAMD_PKVAR")) p->pk_variant = std::atoi(pv);
+    const int minw = p->pk_variant == 1 || p->pk_variant == 3 ? 6 : (p->pk_variant == 2 ? 4 : 8);
+    p->pk_waves = cus * 4 * minw;
+    if (const char *wv = std::getenv("RSAMD_WAVES")) p->pk_waves = std::max(1, std::atoi(wv));
   }
   hipError_t e = hipSuccess;
 #define ALLOC(ptr, bytes)                                  \
@@ -223,9 +262,13 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
   ALLOC(p->d_pts32, sizeof(float4) * ((n + 7) & ~7LL));
   ALLOC(p->d_F32, sizeof(float) * 9 * p->ld);
 #undef ALLOC
-  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&p->h_res), p->res_bytes);
-  for (auto &ev : p->ev)
-    if (e == hipSuccess) e = hipEventCreate(&ev);
+  for (auto &h : p->h_slot)
+    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&h), p->res_bytes);
+  for (auto &ev : p->done)
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  for (auto &r : p->ring)
+    for (auto &ev : r)
+      if (e == hipSuccess) e = hipEventCreate(&ev);
   if (e != hipSuccess) {
     plan_free(p);
     delete p;
@@ -314,25 +357,34 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
     HIP_TRY(hipMemcpyAsync(p->d_tuples, host_tuples, sizeof(int) * 8 * H,
                            hipMemcpyHostToDevice, s));
   }
-  HIP_TRY(hipEventRecord(p->ev[0], s));
+  hipEvent_t *ev = p->ring[p->runs % rs_f8_plan::kEvRing];
+  const int slot = static_cast<int>(p->runs % rs_f8_plan::kSlots);
+  HIP_TRY(hipEventRecord(ev[0], s));
   const bool fp32 = p->use_fp32 && p->fp32_ok;
   HIP_TRY(rsd::launch_f8_solve(p->d_pts, n, h, mode, seed, hyp_offset, p->d_tuples, p->d_F,
                                p->ld, p->d_counts, p->d_status, s, p->d_F32,
                                fp32 ? &p->frame : nullptr));
-  HIP_TRY(hipEventRecord(p->ev[1], s));
-  if (fp32)
+  HIP_TRY(hipEventRecord(ev[1], s));
+  if (fp32 && p->packed)
+    HIP_TRY(rsd::launch_f8_count32p(p->d_pts32, p->d_pts, n, h, p->d_F32, p->d_F, p->ld,
+                                    p->pk_waves, guard_packed(p->frame, thresh),
+                                    p->d_counts, s, p->pk_variant));
+  else if (fp32)
     HIP_TRY(rsd::launch_f8_count32(p->d_pts32, p->d_pts, n, h, p->d_F32, p->d_F, p->ld,
                                    p->resident_waves, guard_constants(p->frame, thresh),
-                                   p->d_counts, s, p->count_block));
+                                   p->d_counts, s, p->count_block, p->prefetch));
   else
     HIP_TRY(rsd::launch_f8_count(p->d_pts, n, h, p->d_F, p->ld, choose_chunk(p, H),
                                  thresh * thresh, p->d_counts, s));
-  HIP_TRY(hipEventRecord(p->ev[2], s));
+  HIP_TRY(hipEventRecord(ev[2], s));
   HIP_TRY(rsd::launch_f8_tail(p->d_pts, n, h, p->d_F, p->ld, p->d_counts, 1, thresh,
                               p->d_status, p->d_cand, p->d_ccount, p->d_cstd, p->d_cnorm,
                               p->d_res, s));
-  HIP_TRY(hipEventRecord(p->ev[3], s));
-  HIP_TRY(hipMemcpyAsync(p->h_res, p->d_res, p->res_bytes, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipEventRecord(ev[3], s));
+  HIP_TRY(hipMemcpyAsync(p->h_slot[slot], p->d_res, p->res_bytes, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipEventRecord(p->done[slot], s));
+  p->h_res = p->h_slot[slot];
+  ++p->runs;
   p->last_H = H;
   p->pending = true;
   p->have_result = true;
@@ -343,6 +395,7 @@ static int plan_wait(rs_f8_plan *p) {
   if (!p->have_result) return fail(RS_EINVAL, "no run has been issued on this plan");
   if (p->pending) {
     HIP_TRY(hipSetDevice(p->ctx->device));
+    HIP_TRY(hipEventSynchronize(p->done[(p->runs - 1) % rs_f8_plan::kSlots]));
     HIP_TRY(hipStreamSynchronize(p->ctx->stream));
     p->pending = false;
   }
@@ -443,16 +496,30 @@ extern "C" int rs_f8_plan_models(rs_f8_plan *p, double *F_out, int64_t H) {
 
 extern "C" int rs_f8_plan_kernel_ms(rs_f8_plan *p, double *score_ms, double *solve_ms,
                                     double *total_ms) {
+  return rs_f8_plan_kernel_avg(p, 1, score_ms, solve_ms, total_ms);
+}
+
+extern "C" int rs_f8_plan_kernel_avg(rs_f8_plan *p, int64_t last_n, double *score_ms,
+                                     double *solve_ms, double *total_ms) {
   if (!p) return fail(RS_EINVAL, "null plan");
   int st = plan_wait(p);
   if (st) return st;
-  float a = 0, b = 0, t = 0;
-  HIP_TRY(hipEventElapsedTime(&a, p->ev[0], p->ev[1]));
-  HIP_TRY(hipEventElapsedTime(&b, p->ev[1], p->ev[2]));
-  HIP_TRY(hipEventElapsedTime(&t, p->ev[0], p->ev[3]));
-  if (solve_ms) *solve_ms = a;
-  if (score_ms) *score_ms = b;
-  if (total_ms) *total_ms = t;
+  const int64_t k = std::max<int64_t>(1, std::min<int64_t>({last_n, p->runs,
+                                                            (int64_t)rs_f8_plan::kEvRing}));
+  double sa = 0, sb = 0, st_ = 0;
+  for (int64_t r = p->runs - k; r < p->runs; ++r) {
+    hipEvent_t *ev = p->ring[r % rs_f8_plan::kEvRing];
+    float a = 0, b = 0, t = 0;
+    HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));
+    HIP_TRY(hipEventElapsedTime(&b, ev[1], ev[2]));
+    HIP_TRY(hipEventElapsedTime(&t, ev[0], ev[3]));
+    sa += a;
+    sb += b;
+    st_ += t;
+  }
+  if (solve_ms) *solve_ms = sa / k;
+  if (score_ms) *score_ms = sb / k;
+  if (total_ms) *total_ms = st_ / k;
   return RS_OK;
 }
 

@@ -25,6 +25,12 @@ struct Guard32 {
   double thr2_px;  // t^2 for the fp64 re-test in pixel units
 };
 
+// Bound constants of the packed fp32 test (k_f8_count32p): B = Ka e^2 + Kb rhs + K0.
+struct GuardPk {
+  float thr2, Ka, Kb, K0;
+  double thr2_px;
+};
+
 // ----------------------------------------------------------------------------------------
 // Philox4x32-10 counter-based generator (throughput-mode sampler).
 // ----------------------------------------------------------------------------------------

@@ -12,6 +12,7 @@ namespace rsd {
 struct Pt;
 struct Frame;
 struct Guard32;
+struct GuardPk;
 
 // Grid of the selection passes; the status buffer holds 4 words + kSelectBlocks counts.
 constexpr int kSelectBlocks = 256;
@@ -42,9 +43,13 @@ hipError_t launch_f8_solve(const Pt *pts, int n, int H, int mode, uint64_t seed,
                            const Frame *frame = nullptr);
 hipError_t launch_pack_points32(const Pt *pts, int n, const Frame &fr, float4 *pts32,
                                 hipStream_t s);
+hipError_t launch_f8_count32p(const float4 *pts32, const Pt *pts, int n, int H,
+                              const float *F32soa, const double *Fsoa, int64_t ld, int waves,
+                              const GuardPk &g, int *counts, hipStream_t s, int variant = 0);
 hipError_t launch_f8_count32(const float4 *pts32, const Pt *pts, int n, int H,
                              const float *F32soa, const double *Fsoa, int64_t ld, int waves,
-                             const Guard32 &g, int *counts, hipStream_t s, int blk = 4);
+                             const Guard32 &g, int *counts, hipStream_t s, int blk = 8,
+                             bool prefetch = false);
 hipError_t launch_f8_count(const Pt *pts, int n, int H, const double *Fsoa, int64_t ld,
                            int chunk, double thr2, int *counts, hipStream_t s);
 // Selection tail: c* (k_f8_max), candidates + reference statistics (k_f8_cand_stats), replay

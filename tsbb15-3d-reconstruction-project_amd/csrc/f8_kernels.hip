@@ -174,7 +174,7 @@ __device__ __forceinline__ bool test64(const double (&fd)[9], const Pt &q, doubl
 // NaN points, which are neither inliers nor ambiguous).  The main path counts only sure
 // inliers, d < -B; each point's ambiguity ballot |d| <= B stays in SGPRs and, once per block,
 // the flagged (lane, point) pairs are re-tested in float64.
-template <int BLK>
+template <int BLK, bool PREFETCH>
 __global__ __launch_bounds__(256) void k_f8_count32(const float4 *__restrict__ pts32,
                                                     const Pt *__restrict__ pts, int n, int H,
                                                     const float *__restrict__ F32soa,
@@ -199,14 +199,21 @@ __global__ __launch_bounds__(256) void k_f8_count32(const float4 *__restrict__ p
     for (int k = 0; k < 9; ++k) f[k] = F32soa[k * ld + hl];
     int cnt = 0;
     float4 cur[BLK];
+    if (PREFETCH) {
 #pragma unroll
-    for (int k = 0; k < BLK; ++k) cur[k] = pts32[p0 + k];
+      for (int k = 0; k < BLK; ++k) cur[k] = pts32[p0 + k];
+    }
     for (int i = p0; i < p1; i += BLK) {
-      // prefetch the next block (software pipelining of the scalar loads)
+      // optional software pipelining of the scalar loads (prefetch the next block)
       float4 nxt[BLK];
-      const int j = (i + BLK < p1) ? i + BLK : i;
+      if (PREFETCH) {
+        const int j = (i + BLK < p1) ? i + BLK : i;
 #pragma unroll
-      for (int k = 0; k < BLK; ++k) nxt[k] = pts32[j + k];
+        for (int k = 0; k < BLK; ++k) nxt[k] = pts32[j + k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < BLK; ++k) cur[k] = pts32[i + k];
+      }
       unsigned long long amb[BLK];
 #pragma unroll
       for (int k = 0; k < BLK; ++k) {
@@ -226,10 +233,96 @@ __global__ __launch_bounds__(256) void k_f8_count32(const float4 *__restrict__ p
         for (int k = 0; k < BLK; ++k)
           if ((amb[k] >> lane) & 1ull) cnt += test64(fd, pts[i + k], g.thr2_px) ? 1 : 0;
       }
+      if (PREFETCH) {
 #pragma unroll
-      for (int k = 0; k < BLK; ++k) cur[k] = nxt[k];
+        for (int k = 0; k < BLK; ++k) cur[k] = nxt[k];
+      }
     }
     if (h < H) atomicAdd(&counts[h], cnt);
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// Packed variant: on gfx950 a wave64 v_fma_f32 issues at the float64 rate (4 cycles); only
+// v_pk_fma_f32 doubles fp32 throughput (tools/ubench/valu_rate.hip: 77 vs 154 TFLOP/s).  So
+// each lane carries TWO hypotheses (g*128 + lane and g*128 + 64 + lane) as a float2 and every
+// FMA is packed; the wave-uniform point coordinate is an SGPR broadcast to both halves
+// (op_sel_hi).  The |e| term of the bound uses 2|e| <= e^2/c + c (c = t~, any c > 0 is
+// rigorous) because packed FMAs take no abs modifier:
+//     B = Ka e^2 + Kb rhs + K0,  Ka = 1.02 (De/c (1+2u) + u), Kb = 1.02 (2u),
+//                                K0 = 1.02 (De c + De^2 + t~^2 Dn).
+// 29 VALU per lane and point for two hypotheses (14.5 per hypothesis-point).
+// ----------------------------------------------------------------------------------------
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+template <int BLK, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_f8_count32p(const float4 *__restrict__ pts32,
+                                                     const Pt *__restrict__ pts, int n, int H,
+                                                     const float *__restrict__ F32soa,
+                                                     const double *__restrict__ Fsoa,
+                                                     int64_t ld, int64_t per_wave,
+                                                     GuardPk g, int *__restrict__ counts) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = wave_uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int64_t npad = (n + BLK - 1) / BLK * BLK;
+  const int64_t total = static_cast<int64_t>((H + 127) >> 7) * npad;
+  int64_t pos = w * per_wave;
+  const int64_t end = min(total, pos + per_wave);
+  const f2v thr2 = g.thr2, ka = g.Ka, kb = g.Kb, k0 = g.K0;
+  while (pos < end) {
+    const int grp = static_cast<int>(pos / npad);
+    const int p0 = static_cast<int>(pos - grp * npad);
+    const int p1 = static_cast<int>(min(npad, p0 + (end - pos)));
+    pos += p1 - p0;
+    const int hlo = grp * 128 + lane, hhi = hlo + 64;
+    const int llo = hlo < H ? hlo : H - 1, lhi = hhi < H ? hhi : H - 1;
+    f2v f[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) f[k] = f2v{F32soa[k * ld + llo], F32soa[k * ld + lhi]};
+    int clo = 0, chi = 0;
+    for (int i = p0; i < p1; i += BLK) {
+      unsigned long long alo[BLK], ahi[BLK];
+#pragma unroll
+      for (int k = 0; k < BLK; ++k) {
+        const float4 p = pts32[i + k];
+        const f2v x1 = p.x, y1 = p.y, x2 = p.z, y2 = p.w;
+        const f2v l10 = __builtin_elementwise_fma(f[0], x2, __builtin_elementwise_fma(f[1], y2, f[2]));
+        const f2v l11 = __builtin_elementwise_fma(f[3], x2, __builtin_elementwise_fma(f[4], y2, f[5]));
+        const f2v l12 = __builtin_elementwise_fma(f[6], x2, __builtin_elementwise_fma(f[7], y2, f[8]));
+        const f2v l20 = __builtin_elementwise_fma(f[0], x1, __builtin_elementwise_fma(f[3], y1, f[6]));
+        const f2v l21 = __builtin_elementwise_fma(f[1], x1, __builtin_elementwise_fma(f[4], y1, f[7]));
+        const f2v e = __builtin_elementwise_fma(l10, x1, __builtin_elementwise_fma(l11, y1, l12));
+        const f2v n1 = __builtin_elementwise_fma(l10, l10, l11 * l11);
+        const f2v n2 = __builtin_elementwise_fma(l20, l20, l21 * l21);
+        const f2v m = f2v{fminf(n1.x, n2.x), fminf(n1.y, n2.y)};
+        const f2v ee = e * e;
+        const f2v rhs = thr2 * m;
+        const f2v d = ee - rhs;
+        const f2v B = __builtin_elementwise_fma(ee, ka, __builtin_elementwise_fma(rhs, kb, k0));
+        clo += (d.x < -B.x) ? 1 : 0;  // sure inliers
+        chi += (d.y < -B.y) ? 1 : 0;
+        alo[k] = __ballot(fabsf(d.x) <= B.x);
+        ahi[k] = __ballot(fabsf(d.y) <= B.y);
+      }
+      unsigned long long any = 0ull;
+#pragma unroll
+      for (int k = 0; k < BLK; ++k) any |= alo[k] | ahi[k];
+      if (any != 0ull) {
+        double fd[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) fd[k] = Fsoa[k * ld + llo];
+#pragma unroll
+        for (int k = 0; k < BLK; ++k)
+          if ((alo[k] >> lane) & 1ull) clo += test64(fd, pts[i + k], g.thr2_px) ? 1 : 0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) fd[k] = Fsoa[k * ld + lhi];
+#pragma unroll
+        for (int k = 0; k < BLK; ++k)
+          if ((ahi[k] >> lane) & 1ull) chi += test64(fd, pts[i + k], g.thr2_px) ? 1 : 0;
+      }
+    }
+    if (hlo < H) atomicAdd(&counts[hlo], clo);
+    if (hhi < H) atomicAdd(&counts[hhi], chi);
   }
 }
 
@@ -591,9 +684,41 @@ hipError_t launch_pack_points32(const Pt *pts, int n, const Frame &fr, float4 *p
   return hipGetLastError();
 }
 
+hipError_t launch_f8_count32p(const float4 *pts32, const Pt *pts, int n, int H,
+                              const float *F32soa, const double *Fsoa, int64_t ld, int waves,
+                              const GuardPk &g, int *counts, hipStream_t s, int variant) {
+  const int blk = variant == 3 ? 4 : 2;
+  const int64_t npad = (n + blk - 1) / blk * blk;
+  const int64_t total = static_cast<int64_t>((H + 127) / 128) * npad;
+  int64_t W = std::max<int64_t>(1, std::min<int64_t>(waves, total / 32));
+  int64_t per = (total + W - 1) / W;
+  per = (per + blk - 1) / blk * blk;
+  W = (total + per - 1) / per;
+  const dim3 grid(static_cast<unsigned>((W + 3) / 4));
+  switch (variant) {
+    case 1:
+      hipLaunchKernelGGL((k_f8_count32p<2, 6>), grid, dim3(256), 0, s, pts32, pts, n, H, F32soa,
+                         Fsoa, ld, per, g, counts);
+      break;
+    case 2:
+      hipLaunchKernelGGL((k_f8_count32p<2, 4>), grid, dim3(256), 0, s, pts32, pts, n, H, F32soa,
+                         Fsoa, ld, per, g, counts);
+      break;
+    case 3:
+      hipLaunchKernelGGL((k_f8_count32p<4, 6>), grid, dim3(256), 0, s, pts32, pts, n, H, F32soa,
+                         Fsoa, ld, per, g, counts);
+      break;
+    default:
+      hipLaunchKernelGGL((k_f8_count32p<2, 8>), grid, dim3(256), 0, s, pts32, pts, n, H, F32soa,
+                         Fsoa, ld, per, g, counts);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_f8_count32(const float4 *pts32, const Pt *pts, int n, int H,
                              const float *F32soa, const double *Fsoa, int64_t ld, int waves,
-                             const Guard32 &g, int *counts, hipStream_t s, int blk) {
+                             const Guard32 &g, int *counts, hipStream_t s, int blk,
+                             bool prefetch) {
   blk = blk == 8 ? 8 : 4;
   const int64_t npad = (n + blk - 1) / blk * blk;
   const int64_t total = static_cast<int64_t>((H + 63) / 64) * npad;
@@ -603,12 +728,18 @@ hipError_t launch_f8_count32(const float4 *pts32, const Pt *pts, int n, int H,
   per = (per + blk - 1) / blk * blk;
   W = (total + per - 1) / per;
   const dim3 grid(static_cast<unsigned>((W + 3) / 4));
-  if (blk == 8)
-    hipLaunchKernelGGL(k_f8_count32<8>, grid, dim3(256), 0, s, pts32, pts, n, H, F32soa, Fsoa,
-                       ld, per, g, counts);
+  if (blk == 8 && prefetch)
+    hipLaunchKernelGGL((k_f8_count32<8, true>), grid, dim3(256), 0, s, pts32, pts, n, H, F32soa,
+                       Fsoa, ld, per, g, counts);
+  else if (blk == 8)
+    hipLaunchKernelGGL((k_f8_count32<8, false>), grid, dim3(256), 0, s, pts32, pts, n, H,
+                       F32soa, Fsoa, ld, per, g, counts);
+  else if (prefetch)
+    hipLaunchKernelGGL((k_f8_count32<4, true>), grid, dim3(256), 0, s, pts32, pts, n, H, F32soa,
+                       Fsoa, ld, per, g, counts);
   else
-    hipLaunchKernelGGL(k_f8_count32<4>, grid, dim3(256), 0, s, pts32, pts, n, H, F32soa, Fsoa,
-                       ld, per, g, counts);
+    hipLaunchKernelGGL((k_f8_count32<4, false>), grid, dim3(256), 0, s, pts32, pts, n, H,
+                       F32soa, Fsoa, ld, per, g, counts);
   return hipGetLastError();
 }
 

@@ -70,6 +70,7 @@ _SIGS = {
     "rs_f8_plan_counts": (C.c_int, [C.c_void_p, _i32p, C.c_int64]),
     "rs_f8_plan_models": (C.c_int, [C.c_void_p, _dp, C.c_int64]),
     "rs_f8_plan_kernel_ms": (C.c_int, [C.c_void_p, _dp, _dp, _dp]),
+    "rs_f8_plan_kernel_avg": (C.c_int, [C.c_void_p, C.c_int64, _dp, _dp, _dp]),
     "rs_f8_ransac_np": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, C.c_int64, _u32p, _i32p,
                                   C.c_double, C.POINTER(F8Result), _i64p, C.c_int64, _i64p]),
     "rs_pnp_dlt": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, _dp]),
@@ -290,7 +291,9 @@ class F8Plan:
         check(lib().rs_f8_plan_models(self._h, ptr(out, C.c_double), int(H)))
         return out.reshape(-1, 3, 3)
 
-    def kernel_ms(self):
+    def kernel_ms(self, last_n=1):
+        """Device times of the last run, or averaged over the last ``last_n`` runs."""
         a, b, t = C.c_double(), C.c_double(), C.c_double()
-        check(lib().rs_f8_plan_kernel_ms(self._h, C.byref(a), C.byref(b), C.byref(t)))
+        check(lib().rs_f8_plan_kernel_avg(self._h, int(last_n), C.byref(a), C.byref(b),
+                                          C.byref(t)))
         return {"count_ms": a.value, "solve_ms": b.value, "total_ms": t.value}
