@@ -408,7 +408,7 @@ __device__ __forceinline__ double block_sum_d(double v, double *sh) {
 // every hypothesis of the slice with fast count >= max(c* - slack, 1) is appended in index
 // order to the block's own segment cand[b * per_block + j] (bc[b] entries), then the block
 // re-scores each of them with dist_ref: count, np.std(d) (two-pass), np.linalg.norm(d).
-__global__ __launch_bounds__(256) void k_f8_cand_stats(const Pt *__restrict__ pts, int n,
+__global__ __launch_bounds__(1024) void k_f8_cand_stats(const Pt *__restrict__ pts, int n,
                                                        const double *__restrict__ Fsoa,
                                                        int64_t ld, const int *__restrict__ counts,
                                                        int H, int slack, int per_block,
@@ -418,9 +418,9 @@ __global__ __launch_bounds__(256) void k_f8_cand_stats(const Pt *__restrict__ pt
                                                        int *__restrict__ ccount,
                                                        double *__restrict__ cstd,
                                                        double *__restrict__ cnorm) {
-  __shared__ double shd[4];
-  __shared__ int shi[4];
-  __shared__ int woff[4];
+  __shared__ double shd[16];
+  __shared__ int shi[16];
+  __shared__ int woff[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int cmax = status[0];
   const int thr = max(cmax - slack, 1);
@@ -428,16 +428,19 @@ __global__ __launch_bounds__(256) void k_f8_cand_stats(const Pt *__restrict__ pt
   int *seg = cand + static_cast<int64_t>(blockIdx.x) * per_block;
   int nloc = 0;
   if (cmax > 0) {
-    for (int b = b0; b < b1; b += 256) {
+    for (int b = b0; b < b1; b += 1024) {
       const int i = b + tid;
       const bool take = i < b1 && counts[i] >= thr;
       const unsigned long long bal = __ballot(take);
       if (lane == 0) woff[w] = __popcll(bal);
       __syncthreads();
-      int base = nloc;
-      for (int q = 0; q < w; ++q) base += woff[q];
+      int base = nloc, tot = 0;
+      for (int q = 0; q < 16; ++q) {
+        if (q < w) base += woff[q];
+        tot += woff[q];
+      }
       if (take) seg[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
-      nloc += woff[0] + woff[1] + woff[2] + woff[3];
+      nloc += tot;
       __syncthreads();
     }
   }
@@ -450,7 +453,7 @@ __global__ __launch_bounds__(256) void k_f8_cand_stats(const Pt *__restrict__ pt
     for (int k = 0; k < 9; ++k) f[k] = Fsoa[k * ld + h];
     double s1 = 0.0, s2 = 0.0;
     int cnt = 0;
-    for (int i = tid; i < n; i += 256) {
+    for (int i = tid; i < n; i += 1024) {
       const double d = dist_ref(f, pts[i]);
       cnt += d < thresh ? 1 : 0;
       s1 += d;
@@ -461,7 +464,7 @@ __global__ __launch_bounds__(256) void k_f8_cand_stats(const Pt *__restrict__ pt
     cnt = block_reduce_sum(cnt, shi);
     const double mean = s1 / static_cast<double>(n);
     double s3 = 0.0;
-    for (int i = tid; i < n; i += 256) {
+    for (int i = tid; i < n; i += 1024) {
       const double v = dist_ref(f, pts[i]) - mean;
       s3 += v * v;
     }
@@ -502,16 +505,32 @@ __global__ __launch_bounds__(1024) void k_f8_replay_inliers(
   __shared__ double fsh[9];
   __shared__ int have_s;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (tid == 0) {
-    int acc = 0;
-    for (int q = 0; q < nb; ++q) {
-      pref[q] = acc;
-      acc += bc[q];
+  // exclusive prefix of the per-block candidate counts (nb <= 256): one wave per 64 blocks,
+  // then the 4 wave totals
+  {
+    const int v = tid < nb ? bc[tid] : 0;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o);
+      if (lane >= o) x += y;
     }
-    pref[nb] = acc;
+    if (tid < kSelectBlocks) pref[tid] = x - v;   // wave-local exclusive
+    if (lane == 63 && w < kSelectBlocks / 64) woff[w] = x;
+    __syncthreads();
+    if (tid < kSelectBlocks) {
+      int add = 0;
+      for (int q = 0; q < (tid >> 6); ++q) add += woff[q];
+      pref[tid] += add;
+    }
+    if (tid == 0) {
+      int tot = 0;
+      for (int q = 0; q < kSelectBlocks / 64; ++q) tot += woff[q];
+      pref[kSelectBlocks] = tot;
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  const int nc = pref[nb];
+  const int nc = pref[kSelectBlocks];
   if (w == 0) {
     int best = -1, bcount = 0;
     uint64_t bstd = 0ull;  // S_RANSAC = [], norm([]) = 0
@@ -756,7 +775,7 @@ hipError_t launch_f8_tail(const Pt *pts, int n, int H, const double *Fsoa, int64
   int *bc = status + 4;  // per-block candidate counts live behind the status words
   const int pb = select_per_block(H), nb = select_blocks(H);
   hipLaunchKernelGGL(k_f8_max, dim3(nb), dim3(256), 0, s, counts, H, status);
-  hipLaunchKernelGGL(k_f8_cand_stats, dim3(nb), dim3(256), 0, s, pts, n, Fsoa, ld, counts, H,
+  hipLaunchKernelGGL(k_f8_cand_stats, dim3(nb), dim3(1024), 0, s, pts, n, Fsoa, ld, counts, H,
                      slack, pb, status, thresh, bc, cand, ccount, cstd, cnorm);
   hipLaunchKernelGGL(k_f8_replay_inliers, dim3(1), dim3(1024), 0, s, pts, n, counts, nb, pb, bc,
                      cand, ccount, cstd, cnorm, Fsoa, ld, status, thresh, status, res);
