@@ -218,6 +218,11 @@ def _near_threshold_points(F, p1, p2, deltas, rng, keep):
     return p2
 
 
+# counting kernels: x / y = packed-pair fp32 with packed / plain decision, fp32 = scalar fp32, pk = two hypotheses
+# per lane, fp64 = the float64 reference-order kernel every fp32 variant must match exactly
+COUNT_MODES = ("x", "y", "z", "fp32", "pk", "fp64")
+
+
 def test_fp32_guard_band_exact_near_threshold(ctx, monkeypatch):
     """Points placed at d = 1.5 (1 +/- delta), delta down to 1e-12: the fp32 counting kernel
     must agree bit for bit with the fp64 kernel and with the oracle's reference-order test."""
@@ -228,7 +233,7 @@ def test_fp32_guard_band_exact_near_threshold(ctx, monkeypatch):
     p2n = _near_threshold_points(F[0], p1, p2, [1e-12, 1e-9, 1e-7, 1e-6, 1e-5, 1e-4, 1e-3], rng,
                                  set(tup.ravel().tolist()))
     res = {}
-    for mode in ("fp32", "fp64"):
+    for mode in COUNT_MODES:
         monkeypatch.setenv("RSAMD_COUNT", mode)
         plan = _ffi.F8Plan(ctx, 512, 4)
         plan.set_points(p1, p2n)
@@ -238,7 +243,8 @@ def test_fp32_guard_band_exact_near_threshold(ctx, monkeypatch):
         plan.close()
     Fm = lab3.fmatrix_stls_batch(p1, p2n, tup)
     oracle = [np.count_nonzero(ransac_ref.inlier_distance(f, p1, p2n) < 1.5) for f in Fm]
-    assert np.array_equal(res["fp32"], res["fp64"])
+    for mode in COUNT_MODES:
+        assert np.array_equal(res[mode], res["fp64"]), mode
     assert res["fp64"][0] == oracle[0]  # model 0 is the one the points were placed around
     np.testing.assert_array_equal(Fm[0], F[0])
 
@@ -249,7 +255,7 @@ def test_fp32_and_fp64_counting_identical_full_size(ctx, monkeypatch, name):
     n = z["p1"].shape[1]
     H = 20_000
     counts = {}
-    for mode in ("fp32", "fp64"):
+    for mode in COUNT_MODES:
         monkeypatch.setenv("RSAMD_COUNT", mode)
         plan = _ffi.F8Plan(ctx, n, H)
         plan.set_points(z["p1"], z["p2"])
@@ -257,4 +263,5 @@ def test_fp32_and_fp64_counting_identical_full_size(ctx, monkeypatch, name):
         plan.result()
         counts[mode] = plan.counts(H)
         plan.close()
-    assert np.array_equal(counts["fp32"], counts["fp64"])
+    for mode in COUNT_MODES:
+        assert np.array_equal(counts[mode], counts["fp64"]), mode

@@ -31,6 +31,31 @@ struct GuardPk {
   double thr2_px;
 };
 
+// Decision constants of the packed-pair test (k_f8_count32x, derivation above it):
+//   sure inlier   (|e| + K1i) |e| + K0i  <  alpha m
+//   sure outlier  (|e| - K1o) |e| - K0o  >  beta  m
+// each side evaluated as one half of a v_pk_* pair.
+struct GuardX {
+  float K1i, K1o_neg;  // ( K1i, -K1o)
+  float K0i, K0o_neg;  // ( K0i, -K0o)
+  float alpha, beta;
+  double thr2_px;
+};
+
+// Decision constants of the plain-op decision (k_f8_count32x, DEC = 1):
+//   G = fl(e^2 - fl(alpha m)),  h = fl(K1 |e| + K0)
+//   sure inlier  G < -h;   sure outlier  G > fl(delta m + h)
+struct GuardY {
+  float K1, K0, alpha, delta;
+  double thr2_px;
+};
+
+// Folded plain decision (k_f8_count32x, DEC = 2): sure inlier G < -h, ambiguous |G| <= h.
+struct GuardF {
+  float K1, K0, alpha, pad_;
+  double thr2_px;
+};
+
 // ----------------------------------------------------------------------------------------
 // Philox4x32-10 counter-based generator (throughput-mode sampler).
 // ----------------------------------------------------------------------------------------

@@ -40,7 +40,7 @@ hipError_t launch_pack_points(const double *p1, const double *p2, int n, Pt *pts
 hipError_t launch_f8_solve(const Pt *pts, int n, int H, int mode, uint64_t seed,
                            uint64_t hyp_offset, const int *tuples, double *Fsoa, int64_t ld,
                            int *counts, int *status, hipStream_t s, float *F32soa = nullptr,
-                           const Frame *frame = nullptr);
+                           const Frame *frame = nullptr, int *gdone = nullptr);
 hipError_t launch_pack_points32(const Pt *pts, int n, const Frame &fr, float4 *pts32,
                                 hipStream_t s);
 hipError_t launch_f8_count32p(const float4 *pts32, const Pt *pts, int n, int H,
@@ -50,16 +50,23 @@ hipError_t launch_f8_count32(const float4 *pts32, const Pt *pts, int n, int H,
                              const float *F32soa, const double *Fsoa, int64_t ld, int waves,
                              const Guard32 &g, int *counts, hipStream_t s, int blk = 8,
                              bool prefetch = false);
+// Packed-pair fp32 counting; Guard = GuardX (packed decision) or GuardY (plain decision).
+template <class Guard>
+hipError_t launch_f8_count32x(const float4 *pts32, const Pt *pts, int n, int H,
+                              const float *F32soa, const double *Fsoa, int64_t ld, int waves,
+                              const Guard &g, int *counts, hipStream_t s, int blk = 8,
+                              bool prefetch = true, int *gdone = nullptr,
+                              int *status = nullptr);
 hipError_t launch_f8_count(const Pt *pts, int n, int H, const double *Fsoa, int64_t ld,
                            int chunk, double thr2, int *counts, hipStream_t s);
-// Selection tail: c* (k_f8_max), candidates + reference statistics (k_f8_cand_stats), replay
-// + S_RANSAC (k_f8_replay_inliers).  Candidates live in per-block segments of `cand`.
+// Selection tail: c* (k_f8_max, unless the counting kernel fused it), candidates + reference
+// statistics + (last block) replay and S_RANSAC (k_f8_cand_stats).  Candidates live in per-block segments of `cand`.
 int select_per_block(int H);
 int select_blocks(int H);
 hipError_t launch_f8_tail(const Pt *pts, int n, int H, const double *Fsoa, int64_t ld,
                           const int *counts, int slack, double thresh, int *status, int *cand,
                           int *ccount, double *cstd, double *cnorm, F8DevResult *res,
-                          hipStream_t s);
+                          hipStream_t s, bool need_max = true, F8DevResult *hres = nullptr);
 hipError_t launch_residuals(const Pt *pts, int n, const double *F, double *out, hipStream_t s);
 
 }  // namespace rsd

@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "device_math.h"
 #include "f8_kernels.h"
@@ -22,6 +23,53 @@ namespace rsd {
 
 __device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// cnt + (this lane's bit of a wave mask): one v_addc_co_u32 with the SGPR mask as carry-in.
+__device__ __forceinline__ int add_lane_bit(int cnt, unsigned long long mask) {
+  int r;
+  unsigned long long co;
+  asm("v_addc_co_u32_e64 %0, %1, 0, %2, %3" : "=v"(r), "=s"(co) : "v"(cnt), "s"(mask));
+  return r;
+}
+
+// Cross-workgroup hand-off inside one launch.  Each XCD has its own L2, so an agent-scope
+// fence (__threadfence) writes back / invalidates L2 -- far too slow per segment.  Instead the
+// shared values travel as agent-scope atomics (coherent across XCDs), each wave waits for its
+// own to complete (vmcnt) before publishing with the counter atomic, and readers use
+// agent-scope atomic loads.
+template <class T>
+__device__ __forceinline__ void st_agent(T *p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ T ld_agent(const T *p) {
+  return __hip_atomic_load(const_cast<T *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void wait_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Per-lane sum of 8 wave masks (0..8) added to cnt: the masks are summed as bit planes by
+// scalar full adders (SALU, wave-uniform), then 5 VALU add the planes' lane bits.
+__device__ __forceinline__ int add_block_count8(int cnt, const unsigned long long (&b)[8]) {
+  const unsigned long long s01 = b[0] ^ b[1], c01 = b[0] & b[1];
+  const unsigned long long s23 = b[2] ^ b[3], c23 = b[2] & b[3];
+  const unsigned long long s45 = b[4] ^ b[5], c45 = b[4] & b[5];
+  const unsigned long long s67 = b[6] ^ b[7], c67 = b[6] & b[7];
+  const unsigned long long q0 = s01 ^ s23, kq = s01 & s23, tq = c01 ^ c23;
+  const unsigned long long q1 = tq ^ kq, q2 = (c01 & c23) | (kq & tq);
+  const unsigned long long r0 = s45 ^ s67, kr = s45 & s67, tr = c45 ^ c67;
+  const unsigned long long r1 = tr ^ kr, r2 = (c45 & c67) | (kr & tr);
+  const unsigned long long o0 = q0 ^ r0, k0 = q0 & r0, t1 = q1 ^ r1;
+  const unsigned long long o1 = t1 ^ k0, k1 = (q1 & r1) | (k0 & t1), t2 = q2 ^ r2;
+  const unsigned long long o2 = t2 ^ k1, o3 = (q2 & r2) | (k1 & t2);
+  int a, c, d, r;
+  unsigned long long co;
+  asm("v_cndmask_b32_e64 %0, 0, 2, %1" : "=v"(a) : "s"(o1));
+  asm("v_cndmask_b32_e64 %0, 0, 4, %1" : "=v"(c) : "s"(o2));
+  asm("v_cndmask_b32_e64 %0, 0, 8, %1" : "=v"(d) : "s"(o3));
+  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(cnt), "v"(a), "v"(c));
+  asm("v_addc_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(cnt), "=s"(co) : "v"(r), "v"(d), "s"(o0));
+  return cnt;
+}
+
 // ----------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_f8_solve(const Pt *__restrict__ pts, int n, int H,
                                                   int mode, uint64_t seed, uint64_t hyp_offset,
@@ -29,11 +77,16 @@ __global__ __launch_bounds__(256) void k_f8_solve(const Pt *__restrict__ pts, in
                                                   double *__restrict__ Fsoa, int64_t ld,
                                                   int *__restrict__ counts,
                                                   int *__restrict__ status,
-                                                  float *__restrict__ F32soa, Frame fr) {
+                                                  float *__restrict__ F32soa, Frame fr,
+                                                  int *__restrict__ gdone) {
   const int h = blockIdx.x * blockDim.x + threadIdx.x;
   if (h >= H) return;
   if (counts) counts[h] = 0;  // the counting kernel accumulates into it
-  if (status && h < 2) status[h] = 0;  // c*, n_candidates
+  if (status && h == 0) {  // c*, n_candidates, tail done-counter, spare
+#pragma unroll
+    for (int k = 0; k < 4; ++k) status[k] = 0;
+  }
+  if (gdone && (h & 63) == 0) gdone[h >> 6] = 0;  // fused c*: per-group finish counters
   int idx[8];
   if (mode == RSD_SAMPLER_PHILOX) {
     floyd_sample<8>(seed, hyp_offset + static_cast<uint64_t>(h), n, idx);
@@ -138,12 +191,13 @@ __global__ __launch_bounds__(256) void k_f8_count(const Pt *__restrict__ pts, in
 // One point of the fp32 test: returns d = e^2 - t~^2 m and its error bound B.
 __device__ __forceinline__ void test32(const float (&f)[9], const float4 &p, const Guard32 &g,
                                        float &d, float &B) {
-  const float l10 = fmaf(f[0], p.z, fmaf(f[1], p.w, f[2]));
-  const float l11 = fmaf(f[3], p.z, fmaf(f[4], p.w, f[5]));
-  const float l12 = fmaf(f[6], p.z, fmaf(f[7], p.w, f[8]));
-  const float l20 = fmaf(f[0], p.x, fmaf(f[3], p.y, f[6]));
-  const float l21 = fmaf(f[1], p.x, fmaf(f[4], p.y, f[7]));
-  const float e = fmaf(l10, p.x, fmaf(l11, p.y, l12));
+  const float x2 = p.x, x1 = p.y, y2 = p.z, y1 = p.w;  // k_pack_points32 layout
+  const float l10 = fmaf(f[0], x2, fmaf(f[1], y2, f[2]));
+  const float l11 = fmaf(f[3], x2, fmaf(f[4], y2, f[5]));
+  const float l12 = fmaf(f[6], x2, fmaf(f[7], y2, f[8]));
+  const float l20 = fmaf(f[0], x1, fmaf(f[3], y1, f[6]));
+  const float l21 = fmaf(f[1], x1, fmaf(f[4], y1, f[7]));
+  const float e = fmaf(l10, x1, fmaf(l11, y1, l12));
   const float n1 = fmaf(l10, l10, l11 * l11);
   const float n2 = fmaf(l20, l20, l21 * l21);
   const float ee = e * e;
@@ -242,6 +296,201 @@ __global__ __launch_bounds__(256) void k_f8_count32(const float4 *__restrict__ p
   }
 }
 
+// Last-finisher reduction of one hypothesis group (64 lanes): the wave whose segment brings
+// gdone[grp] to npad reads the group's final counts and folds their max into status[0].  Every
+// segment's count atomics complete (vmcnt) before its gdone atomic, and the reader's atomic
+// loads issue after its gdone atomic returned, so they see all of them.
+__device__ __forceinline__ void group_done_max(int *counts, int *gdone, int *status, int grp,
+                                               int len, int npad, int h, int H) {
+  wait_vmem();
+  int last = 0;
+  if ((threadIdx.x & 63) == 0) last = (atomicAdd(&gdone[grp], len) + len == npad) ? 1 : 0;
+  last = __shfl(last, 0);
+  if (!last) return;
+  int v = h < H ? ld_agent(&counts[h]) : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+  if ((threadIdx.x & 63) == 0 && v > 0) atomicMax(&status[0], v);
+}
+
+// ----------------------------------------------------------------------------------------
+// Packed-pair variant (default).  On gfx950 a wave64 v_fma_f32 issues at the float64 rate
+// and only v_pk_fma_f32 doubles fp32 throughput, so the two epipolar lines of ONE hypothesis
+// travel as pairs:  A = (l10, l20),  Bv = (l11, l21),  N = A*A + Bv*Bv = (n1, n2),
+//   A  = pk_fma((f0, f0), (x2, x1), pk_fma((f1, f3), (y2, y1), (f2, f6)))
+//   Bv = pk_fma((f3, f1), (x2, x1), pk_fma((f4, f4), (y2, y1), (f5, f7)))
+// with the point pairs (x2, x1), (y2, y1) straight from SGPRs (k_pack_points32 layout).  Every
+// value is the same IEEE expression as in test32, so De and Dn hold unchanged.
+//
+// The decision folds the guard band into the two compared sides.  With T = (t/s)^2,
+// |e_c - e| <= De, |m_c - m| <= Dn (m = min(n1, n2)) and u = 2^-24:
+//   sure inlier   P = fl(fl(|e_c| + K1i)|e_c| + K0i) < fl(alpha m_c)
+//     P >= (1-u)^2 (e_c^2 + K1i|e_c| + K0i) and fl(alpha m_c) <= alpha m_c (1+u); with
+//     K1i >= 2De, K0i >= De^2 + T Dn, alpha <= T (1-u)^2/(1+u) this gives
+//     e^2 <= e_c^2 + 2De|e_c| + De^2 < T m_c - T Dn <= T m    (exact inlier);
+//   sure outlier  Q = fl(fl(|e_c| - K1o)|e_c| - K0o) > fl(beta m_c)  (>= 0, so |e_c| > K1o)
+//     Q <= (1+u)^2 (e_c^2 - K1o|e_c|) - (1+u) K0o; with K1o >= 2De, K0o >= (1+u) T Dn,
+//     beta >= T (1+u)^2/(1-u) this gives e^2 >= e_c^2 - 2De|e_c| > T m_c + T Dn >= T m.
+// Neither side -> the lane re-tests in float64 (test64).  NaN (padding points, NaN models)
+// fails both compares and the ambiguity compare (Q <= beta m), as the float64 test fails.
+// Per (hypothesis, point): 6 pk + 1 pk-mul + 2 pk (P, Q) + 4 fma (l12, e) + min + abs
+// + 2 cmp + 1 add = 18 VALU instead of test32's 26.
+// ----------------------------------------------------------------------------------------
+//
+// Variant DEC = 1 keeps the packed lines and decides with plain ops (GuardY):
+//   R = fl(alpha m), G = fl(e^2 - R) (one fma), h = fl(K1|e| + K0), h2 = fl(delta m + h)
+//   sure inlier  G < -h:  e_c^2 - R <= G/(1+u) < -c1 (K1|e_c| + K0), c1 = (1-u)/(1+u), so
+//     with c1 K1 >= 2De, c1 K0 >= De^2 + T Dn, alpha (1+u) <= T: e^2 < T m_c - T Dn <= T m;
+//   sure outlier G > h2 (>= 0):  e_c^2 > R + c1 (delta m_c + (1-u)(K1|e_c| + K0)); with
+//     alpha (1-u) + c1 delta >= T and c1 (1-u) K1 >= 2De, c1 (1-u) K0 >= T Dn this gives
+//     e^2 >= e_c^2 - 2De|e_c| > T m_c + T Dn >= T m.
+//   Ambiguous = (G <= h2) XOR (G < -h)  (h2 >= 0 > -h, NaN fails both).
+// 6 pk + 4 fma + min + 4 (R, G, h, h2) + 2 cmp + 1 add = 18 VALU, 6 of them packed.
+//
+// Variant DEC = 2 folds delta m into K0: |F~_ij| <= 1 and |x~| <= 1 bound every line
+// component by 3 and m_c by M = 18 (1 + 1e-5), so (T - alpha (1-u)) m_c <= D0 =
+// (T - alpha (1-u)) M and one h serves both sides (K0 >= (De^2 + T Dn + D0)/c1):
+//   sure inlier  G < -h,   ambiguous |G| <= h  (disjoint; NaN fails both),
+// and the per-point inlier add becomes a SALU bit-plane sum per block (add_block_count8):
+// 6 pk + 4 fma + min + 3 (R, G, h) + 2 cmp + 5/8 = 16.6 VALU.
+//
+// c* is fused in (gdone != nullptr): every segment adds its length to its group's counter
+// gdone[grp] after its count atomics; the segment that completes the group (total npad)
+// reads the 64 final counts and issues one atomicMax(status[0]) -- no k_f8_max pass.
+template <int BLK, bool PREFETCH, int DEC, class Guard>
+__global__ __launch_bounds__(256) void k_f8_count32x(const float4 *__restrict__ pts32,
+                                                     const Pt *__restrict__ pts, int n, int H,
+                                                     const float *__restrict__ F32soa,
+                                                     const double *__restrict__ Fsoa,
+                                                     int64_t ld, int64_t per_wave, Guard g,
+                                                     int *__restrict__ counts,
+                                                     int *__restrict__ gdone,
+                                                     int *__restrict__ status) {
+#pragma clang fp contract(off)
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const int lane = threadIdx.x & 63;
+  const int64_t w = wave_uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int64_t npad = (n + BLK - 1) / BLK * BLK;
+  const int64_t total = static_cast<int64_t>((H + 63) >> 6) * npad;
+  int64_t pos = w * per_wave;
+  const int64_t end = min(total, pos + per_wave);
+  f2 k1 = {0.f, 0.f}, k0 = {0.f, 0.f}, ab = {0.f, 0.f};
+  if constexpr (DEC == 0) {
+    k1 = f2{g.K1i, g.K1o_neg};
+    k0 = f2{g.K0i, g.K0o_neg};
+    ab = f2{g.alpha, g.beta};
+  }
+  while (pos < end) {
+    const int grp = static_cast<int>(pos / npad);
+    const int p0 = static_cast<int>(pos - grp * npad);
+    const int p1 = static_cast<int>(min(npad, p0 + (end - pos)));
+    pos += p1 - p0;
+    const int h = grp * 64 + lane;
+    const int hl = h < H ? h : H - 1;
+    float f[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) f[k] = F32soa[k * ld + hl];
+    const f2 fa = {f[0], f[0]}, fb = {f[1], f[3]}, fc = {f[2], f[6]};
+    const f2 fd = {f[3], f[1]}, fe = {f[4], f[4]}, ff = {f[5], f[7]};
+    // one block of BLK points starting at i: fast fp32 decisions, then the float64 re-test of
+    // the ambiguous (lane, point) pairs
+    auto block = [&](const float4 (&cur)[BLK], int i, int cnt) -> int {
+      unsigned long long amb[BLK], inl[BLK];
+#pragma unroll
+      for (int k = 0; k < BLK; ++k) {
+        const f2 X = {cur[k].x, cur[k].y}, Y = {cur[k].z, cur[k].w};  // (x2, x1), (y2, y1)
+        const f2 A = __builtin_elementwise_fma(fa, X, __builtin_elementwise_fma(fb, Y, fc));
+        const f2 Bv = __builtin_elementwise_fma(fd, X, __builtin_elementwise_fma(fe, Y, ff));
+        const f2 N = __builtin_elementwise_fma(A, A, Bv * Bv);
+        const float l12 = fmaf(f[6], cur[k].x, fmaf(f[7], cur[k].z, f[8]));
+        const float e = fmaf(A.x, cur[k].y, fmaf(Bv.x, cur[k].w, l12));
+        const float m = fminf(N.x, N.y);
+        unsigned long long bi, bl;
+        if constexpr (DEC == 0) {
+          const float ae = fabsf(e);
+          const f2 AE = {ae, ae};
+          const f2 PQ = __builtin_elementwise_fma(AE + k1, AE, k0);
+          const f2 RS = f2{m, m} * ab;
+          // P >= Q and alpha m <= beta m survive rounding (monotone), so a sure inlier
+          // always has Q <= beta m: the ambiguous lanes are the XOR of the two ballots.
+          bi = __ballot(PQ.x < RS.x);
+          bl = __ballot(PQ.y <= RS.y);
+        } else if constexpr (DEC == 1) {
+          const float R = g.alpha * m;
+          const float G = fmaf(e, e, -R);
+          const float h = fmaf(fabsf(e), g.K1, g.K0);
+          const float h2 = fmaf(g.delta, m, h);
+          bi = __ballot(G < -h);
+          bl = __ballot(G <= h2);
+        } else {
+          const float R = g.alpha * m;
+          const float G = fmaf(e, e, -R);
+          const float h = fmaf(fabsf(e), g.K1, g.K0);
+          bi = __ballot(G < -h);
+          bl = __ballot(fabsf(G) <= h);
+        }
+        if constexpr (DEC == 2) {
+          amb[k] = bl;
+          inl[k] = bi;
+        } else {
+          amb[k] = bi ^ bl;
+          cnt = add_lane_bit(cnt, bi);  // sure inlier
+        }
+      }
+      if constexpr (DEC == 2) {
+        if constexpr (BLK == 8) {
+          cnt = add_block_count8(cnt, inl);
+        } else {
+#pragma unroll
+          for (int k = 0; k < BLK; ++k) cnt = add_lane_bit(cnt, inl[k]);
+        }
+      }
+      unsigned long long any = 0ull;
+#pragma unroll
+      for (int k = 0; k < BLK; ++k) any |= amb[k];
+      if (any != 0ull) {
+        double fdd[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) fdd[k] = Fsoa[k * ld + hl];
+#pragma unroll
+        for (int k = 0; k < BLK; ++k)
+          if ((amb[k] >> lane) & 1ull) cnt += test64(fdd, pts[i + k], g.thr2_px) ? 1 : 0;
+      }
+      return cnt;
+    };
+    int cnt = 0;
+    float4 ba[BLK], bb[BLK];
+#pragma unroll
+    for (int k = 0; k < BLK; ++k) ba[k] = pts32[p0 + k];
+    if (PREFETCH) {
+      // ping-pong: the next block's scalar loads land in the other buffer while this one is
+      // tested (no register rotation; the last prefetch re-reads the current block)
+      for (int i = p0;;) {
+        const int ja = (i + BLK < p1) ? i + BLK : i;
+#pragma unroll
+        for (int k = 0; k < BLK; ++k) bb[k] = pts32[ja + k];
+        cnt = block(ba, i, cnt);
+        i += BLK;
+        if (i >= p1) break;
+        const int jb = (i + BLK < p1) ? i + BLK : i;
+#pragma unroll
+        for (int k = 0; k < BLK; ++k) ba[k] = pts32[jb + k];
+        cnt = block(bb, i, cnt);
+        i += BLK;
+        if (i >= p1) break;
+      }
+    } else {
+      for (int i = p0; i < p1; i += BLK) {
+#pragma unroll
+        for (int k = 0; k < BLK; ++k) ba[k] = pts32[i + k];
+        cnt = block(ba, i, cnt);
+      }
+    }
+    if (h < H) atomicAdd(&counts[h], cnt);
+    if (gdone) group_done_max(counts, gdone, status, grp, p1 - p0, static_cast<int>(npad), h, H);
+  }
+}
+
 // ----------------------------------------------------------------------------------------
 // Packed variant: on gfx950 a wave64 v_fma_f32 issues at the float64 rate (4 cycles); only
 // v_pk_fma_f32 doubles fp32 throughput (tools/ubench/valu_rate.hip: 77 vs 154 TFLOP/s).  So
@@ -285,7 +534,7 @@ __global__ __launch_bounds__(256, MINW) void k_f8_count32p(const float4 *__restr
 #pragma unroll
       for (int k = 0; k < BLK; ++k) {
         const float4 p = pts32[i + k];
-        const f2v x1 = p.x, y1 = p.y, x2 = p.z, y2 = p.w;
+        const f2v x2 = p.x, x1 = p.y, y2 = p.z, y1 = p.w;
         const f2v l10 = __builtin_elementwise_fma(f[0], x2, __builtin_elementwise_fma(f[1], y2, f[2]));
         const f2v l11 = __builtin_elementwise_fma(f[3], x2, __builtin_elementwise_fma(f[4], y2, f[5]));
         const f2v l12 = __builtin_elementwise_fma(f[6], x2, __builtin_elementwise_fma(f[7], y2, f[8]));
@@ -337,10 +586,11 @@ __global__ __launch_bounds__(256) void k_pack_points32(const Pt *__restrict__ pt
   }
   const Pt p = pts[i];
   const double is = 1.0 / fr.s;
-  out[i] = make_float4(static_cast<float>((p.x1 - fr.cx1) * is),
-                       static_cast<float>((p.y1 - fr.cy1) * is),
-                       static_cast<float>((p.x2 - fr.cx2) * is),
-                       static_cast<float>((p.y2 - fr.cy2) * is));
+  // layout (x2, x1, y2, y1): the SGPR pairs (x2, x1) and (y2, y1) feed v_pk_fma_f32
+  out[i] = make_float4(static_cast<float>((p.x2 - fr.cx2) * is),
+                       static_cast<float>((p.x1 - fr.cx1) * is),
+                       static_cast<float>((p.y2 - fr.cy2) * is),
+                       static_cast<float>((p.y1 - fr.cy1) * is));
 }
 
 // ----------------------------------------------------------------------------------------
@@ -404,6 +654,13 @@ __device__ __forceinline__ double block_sum_d(double v, double *sh) {
   return r;
 }
 
+__device__ void replay_inliers(const Pt *__restrict__ pts, int n, const int *counts, int nb,
+                               int per_block, const int *bc, const int *cand, const int *ccount,
+                               const double *cstd, const double *cnorm,
+                               const double *__restrict__ Fsoa, int64_t ld, int *status,
+                               double thresh, F8DevResult *__restrict__ res,
+                               F8DevResult *__restrict__ hres);
+
 // Candidates + their reference-order statistics, one block per slice of hypotheses:
 // every hypothesis of the slice with fast count >= max(c* - slack, 1) is appended in index
 // order to the block's own segment cand[b * per_block + j] (bc[b] entries), then the block
@@ -417,8 +674,12 @@ __global__ __launch_bounds__(1024) void k_f8_cand_stats(const Pt *__restrict__ p
                                                        int *__restrict__ cand,
                                                        int *__restrict__ ccount,
                                                        double *__restrict__ cstd,
-                                                       double *__restrict__ cnorm) {
+                                                       double *__restrict__ cnorm,
+                                                       int *__restrict__ status_rw,
+                                                       F8DevResult *__restrict__ res,
+                                                       F8DevResult *__restrict__ hres) {
   __shared__ double shd[16];
+  __shared__ int last_s;
   __shared__ int shi[16];
   __shared__ int woff[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -439,15 +700,16 @@ __global__ __launch_bounds__(1024) void k_f8_cand_stats(const Pt *__restrict__ p
         if (q < w) base += woff[q];
         tot += woff[q];
       }
-      if (take) seg[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
+      if (take) st_agent(&seg[base + __popcll(bal & ((1ull << lane) - 1ull))], i);
       nloc += tot;
       __syncthreads();
     }
   }
-  if (tid == 0) bc[blockIdx.x] = nloc;
+  if (tid == 0) st_agent(&bc[blockIdx.x], nloc);
+  wait_vmem();
   __syncthreads();  // seg[] written by this block is visible to all its threads
   for (int j = 0; j < nloc; ++j) {
-    const int h = seg[j];
+    const int h = ld_agent(&seg[j]);
     double f[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) f[k] = Fsoa[k * ld + h];
@@ -471,11 +733,20 @@ __global__ __launch_bounds__(1024) void k_f8_cand_stats(const Pt *__restrict__ p
     s3 = block_sum_d(s3, shd);
     if (tid == 0) {
       const int64_t slot = static_cast<int64_t>(blockIdx.x) * per_block + j;
-      ccount[slot] = cnt;
-      cstd[slot] = sqrt(s3 / static_cast<double>(n));
-      cnorm[slot] = sqrt(s2);
+      st_agent(&ccount[slot], cnt);
+      st_agent(&cstd[slot], sqrt(s3 / static_cast<double>(n)));
+      st_agent(&cnorm[slot], sqrt(s2));
     }
   }
+  // the last block to finish runs the replay: every block's segment, counts and statistics
+  // are agent-scope stores completed (vmcnt) before its done-counter increment
+  wait_vmem();
+  __syncthreads();
+  if (tid == 0) last_s = atomicAdd(&status_rw[2], 1) == static_cast<int>(gridDim.x) - 1;
+  __syncthreads();
+  if (!last_s) return;
+  replay_inliers(pts, n, counts, gridDim.x, per_block, bc, cand, ccount, cstd, cnorm, Fsoa, ld,
+                 status_rw, thresh, res, hres);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -490,15 +761,19 @@ __device__ __forceinline__ uint64_t key_norm(double v) {  // "y > norm" is false
   return (v != v) ? ~0ull : static_cast<uint64_t>(__double_as_longlong(v));
 }
 
-// One 1024-thread workgroup: wave 0 replays fun.py:320-328 over the candidates in global
-// index order (segments of k_f8_cand_stats in block order), 64 per coalesced load; then the
-// whole workgroup extracts S_RANSAC = flatnonzero(d < t) of the winner in order.
-__global__ __launch_bounds__(1024) void k_f8_replay_inliers(
-    const Pt *__restrict__ pts, int n, const int *__restrict__ counts, int nb, int per_block,
-    const int *__restrict__ bc, const int *__restrict__ cand, const int *__restrict__ ccount,
-    const double *__restrict__ cstd, const double *__restrict__ cnorm,
-    const double *__restrict__ Fsoa, int64_t ld, const int *__restrict__ status,
-    double thresh, int *__restrict__ status_out, F8DevResult *__restrict__ res) {
+// One 1024-thread workgroup (the last k_f8_cand_stats block to finish): wave 0 replays
+// fun.py:320-328 over the candidates in global index order (segments in block order), 64 per
+// coalesced load; then the whole workgroup extracts S_RANSAC = flatnonzero(d < t) of the
+// winner in order.  The result header goes to res (HBM) and, when given, to hres (the run's
+// pinned host slot, written through the host mapping: no copy pass); the inlier list stays
+// in res->inliers (HBM).
+__device__ void replay_inliers(const Pt *__restrict__ pts, int n, const int *counts, int nb,
+                               int per_block, const int *bc, const int *cand, const int *ccount,
+                               const double *cstd, const double *cnorm,
+                               const double *__restrict__ Fsoa, int64_t ld, int *status,
+                               double thresh, F8DevResult *__restrict__ res,
+                               F8DevResult *__restrict__ hres) {
+  int *status_out = status;
   __shared__ int pref[kSelectBlocks + 1];
   __shared__ int woff[16];
   __shared__ int base_s;
@@ -508,7 +783,7 @@ __global__ __launch_bounds__(1024) void k_f8_replay_inliers(
   // exclusive prefix of the per-block candidate counts (nb <= 256): one wave per 64 blocks,
   // then the 4 wave totals
   {
-    const int v = tid < nb ? bc[tid] : 0;
+    const int v = tid < nb ? ld_agent(&bc[tid]) : 0;
     int x = v;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -546,10 +821,10 @@ __global__ __launch_bounds__(1024) void k_f8_replay_inliers(
           if (pref[mid] <= c) lo = mid; else hi = mid - 1;
         }
         const int64_t slot = static_cast<int64_t>(lo) * per_block + (c - pref[lo]);
-        cc = ccount[slot];
-        ks = key_std(cstd[slot]);
-        kn = key_norm(cnorm[slot]);
-        mismatch += (cc != counts[cand[slot]]) ? 1 : 0;
+        cc = ld_agent(&ccount[slot]);
+        ks = key_std(ld_agent(&cstd[slot]));
+        kn = key_norm(ld_agent(&cnorm[slot]));
+        mismatch += (cc != counts[ld_agent(&cand[slot])]) ? 1 : 0;
       }
       const int lim = min(64, nc - b);
       for (int q = 0; q < lim; ++q) {
@@ -571,6 +846,11 @@ __global__ __launch_bounds__(1024) void k_f8_replay_inliers(
       res->n_candidates = nc;
       res->max_count_fast = status[0];
       res->guard_mismatch = mismatch;
+      if (hres) {
+        hres->n_candidates = nc;
+        hres->max_count_fast = status[0];
+        hres->guard_mismatch = mismatch;
+      }
       status_out[1] = nc;
       if (best >= 0) {
         int lo = 0, hi = nb - 1;
@@ -579,17 +859,13 @@ __global__ __launch_bounds__(1024) void k_f8_replay_inliers(
           if (pref[mid] <= best) lo = mid; else hi = mid - 1;
         }
         const int64_t slot = static_cast<int64_t>(lo) * per_block + (best - pref[lo]);
-        const int h = cand[slot];
+        const int h = ld_agent(&cand[slot]);
         res->best_index = h;
         res->best_count = bcount;
-        res->best_std = cstd[slot];
-        res->best_norm = cnorm[slot];
+        res->best_std = ld_agent(&cstd[slot]);
+        res->best_norm = ld_agent(&cnorm[slot]);
         res->best_cand = best;
-        for (int k = 0; k < 9; ++k) {
-          const double v = Fsoa[k * ld + h];
-          res->F[k] = v;
-          fsh[k] = v;
-        }
+        for (int k = 0; k < 9; ++k) fsh[k] = Fsoa[k * ld + h];
         have_s = 1;
       } else {
         res->best_index = -1;
@@ -597,11 +873,17 @@ __global__ __launch_bounds__(1024) void k_f8_replay_inliers(
         res->best_std = 0.0;
         res->best_norm = 0.0;
         res->best_cand = -1;
-        for (int k = 0; k < 9; ++k) {
-          res->F[k] = 0.0;
-          fsh[k] = 0.0;
-        }
+        for (int k = 0; k < 9; ++k) fsh[k] = 0.0;
         have_s = 0;
+      }
+      for (int k = 0; k < 9; ++k) res->F[k] = fsh[k];
+      if (hres) {
+        hres->best_index = res->best_index;
+        hres->best_count = res->best_count;
+        hres->best_std = res->best_std;
+        hres->best_norm = res->best_norm;
+        hres->best_cand = res->best_cand;
+        for (int k = 0; k < 9; ++k) hres->F[k] = fsh[k];
       }
       base_s = 0;
     }
@@ -631,7 +913,10 @@ __global__ __launch_bounds__(1024) void k_f8_replay_inliers(
     if (take) res->inliers[woff[w] + before] = i;
     __syncthreads();
   }
-  if (tid == 0) res->n_inliers = base_s;
+  if (tid == 0) {
+    res->n_inliers = base_s;
+    if (hres) hres->n_inliers = base_s;
+  }
 }
 
 // ----------------------------------------------------------------------------------------
@@ -679,11 +964,11 @@ hipError_t launch_pack_points(const double *p1, const double *p2, int n, Pt *pts
 hipError_t launch_f8_solve(const Pt *pts, int n, int H, int mode, uint64_t seed,
                            uint64_t hyp_offset, const int *tuples, double *Fsoa, int64_t ld,
                            int *counts, int *status, hipStream_t s, float *F32soa,
-                           const Frame *frame) {
+                           const Frame *frame, int *gdone) {
   const Frame fr = frame ? *frame : Frame{1.0, 0.0, 0.0, 0.0, 0.0};
   hipLaunchKernelGGL(k_f8_solve, dim3((H + 255) / 256), dim3(256), 0, s, pts, n, H, mode, seed,
                      hyp_offset, tuples, Fsoa, ld, counts, status, frame ? F32soa : nullptr,
-                     fr);
+                     fr, gdone);
   return hipGetLastError();
 }
 
@@ -762,6 +1047,49 @@ hipError_t launch_f8_count32(const float4 *pts32, const Pt *pts, int n, int H,
   return hipGetLastError();
 }
 
+template <class Guard>
+hipError_t launch_f8_count32x(const float4 *pts32, const Pt *pts, int n, int H,
+                              const float *F32soa, const double *Fsoa, int64_t ld, int waves,
+                              const Guard &g, int *counts, hipStream_t s, int blk,
+                              bool prefetch, int *gdone, int *status) {
+  constexpr int D = std::is_same<Guard, GuardX>::value ? 0
+                   : std::is_same<Guard, GuardY>::value ? 1 : 2;
+  blk = blk == 8 ? 8 : 4;
+  const int64_t npad = (n + blk - 1) / blk * blk;
+  const int64_t total = static_cast<int64_t>((H + 63) / 64) * npad;
+  int64_t W = std::max<int64_t>(1, std::min<int64_t>(waves, total / 64));
+  int64_t per = (total + W - 1) / W;
+  per = (per + blk - 1) / blk * blk;
+  W = (total + per - 1) / per;
+  const dim3 grid(static_cast<unsigned>((W + 3) / 4));
+  if (blk == 8 && prefetch)
+    hipLaunchKernelGGL((k_f8_count32x<8, true, D, Guard>), grid, dim3(256), 0, s, pts32, pts, n, H,
+                       F32soa, Fsoa, ld, per, g, counts, gdone, status);
+  else if (blk == 8)
+    hipLaunchKernelGGL((k_f8_count32x<8, false, D, Guard>), grid, dim3(256), 0, s, pts32, pts, n, H,
+                       F32soa, Fsoa, ld, per, g, counts, gdone, status);
+  else if (prefetch)
+    hipLaunchKernelGGL((k_f8_count32x<4, true, D, Guard>), grid, dim3(256), 0, s, pts32, pts, n, H,
+                       F32soa, Fsoa, ld, per, g, counts, gdone, status);
+  else
+    hipLaunchKernelGGL((k_f8_count32x<4, false, D, Guard>), grid, dim3(256), 0, s, pts32, pts, n, H,
+                       F32soa, Fsoa, ld, per, g, counts, gdone, status);
+  return hipGetLastError();
+}
+
+template hipError_t launch_f8_count32x<GuardX>(const float4 *, const Pt *, int, int,
+                                               const float *, const double *, int64_t, int,
+                                               const GuardX &, int *, hipStream_t, int, bool,
+                                               int *, int *);
+template hipError_t launch_f8_count32x<GuardY>(const float4 *, const Pt *, int, int,
+                                               const float *, const double *, int64_t, int,
+                                               const GuardY &, int *, hipStream_t, int, bool,
+                                               int *, int *);
+template hipError_t launch_f8_count32x<GuardF>(const float4 *, const Pt *, int, int,
+                                               const float *, const double *, int64_t, int,
+                                               const GuardF &, int *, hipStream_t, int, bool,
+                                               int *, int *);
+
 int select_per_block(int H) { return (H + kSelectBlocks - 1) / kSelectBlocks; }
 int select_blocks(int H) {
   const int pb = select_per_block(H);
@@ -771,14 +1099,12 @@ int select_blocks(int H) {
 hipError_t launch_f8_tail(const Pt *pts, int n, int H, const double *Fsoa, int64_t ld,
                           const int *counts, int slack, double thresh, int *status, int *cand,
                           int *ccount, double *cstd, double *cnorm, F8DevResult *res,
-                          hipStream_t s) {
+                          hipStream_t s, bool need_max, F8DevResult *hres) {
   int *bc = status + 4;  // per-block candidate counts live behind the status words
   const int pb = select_per_block(H), nb = select_blocks(H);
-  hipLaunchKernelGGL(k_f8_max, dim3(nb), dim3(256), 0, s, counts, H, status);
+  if (need_max) hipLaunchKernelGGL(k_f8_max, dim3(nb), dim3(256), 0, s, counts, H, status);
   hipLaunchKernelGGL(k_f8_cand_stats, dim3(nb), dim3(1024), 0, s, pts, n, Fsoa, ld, counts, H,
-                     slack, pb, status, thresh, bc, cand, ccount, cstd, cnorm);
-  hipLaunchKernelGGL(k_f8_replay_inliers, dim3(1), dim3(1024), 0, s, pts, n, counts, nb, pb, bc,
-                     cand, ccount, cstd, cnorm, Fsoa, ld, status, thresh, status, res);
+                     slack, pb, status, thresh, bc, cand, ccount, cstd, cnorm, status, res, hres);
   return hipGetLastError();
 }
 

@@ -1,0 +1,624 @@
+// F plans (include/rsamd.h "RANSAC-F"): one correspondence set resident in HBM, runs of H
+// hypotheses issued back to back.  Replaces the fun.getFFromLabCode hypothesis loop
+// (fun.py:298-328).
+//
+// Pipeline of one run (two HIP streams, double-buffered per-run buffers):
+//
+//   side stream:  [wait slot free] -> tuples H2D (parity mode) -> k_f8_solve -> (solved)
+//   main stream:  [wait solved]    -> k_f8_count32x (+ fused c*) -> k_f8_cand_stats (+ replay
+//                                  in its last block; header -> pinned host slot) -> (slot free)
+//
+// The solve of run k+1 (latency bound, ~1.5 waves per SIMD) writes buffer set (k+1)%2 while
+// the counting kernel of run k (VALU bound) reads set k%2, so in a back-to-back sequence the
+// solve hides under the previous run's count + selection tail.  The side stream has the
+// higher priority so its workgroups are dispatched ahead of queued count slices.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+#include "ctx.h"
+#include "device_math.h"
+#include "f8_kernels.h"
+
+using rs::fail;
+using rs::hip_fail;
+
+namespace {
+
+// Per-run device buffers; two sets alternate between consecutive runs.
+struct RunBufs {
+  double *d_F = nullptr;       // 9 x ld SoA models (float64)
+  float *d_F32 = nullptr;      // 9 x ld SoA models in the unit frame (fp32 counting)
+  int *d_counts = nullptr;     // fast counts
+  int *d_tuples = nullptr;     // host tuples (parity mode)
+  int *d_cand = nullptr;       // candidate hypothesis ids, per-block segments
+  int *d_status = nullptr;     // [c*, n_candidates, ., ., per-block candidate counts]
+  int *d_ccount = nullptr;
+  double *d_cstd = nullptr, *d_cnorm = nullptr;
+  rsd::F8DevResult *d_res = nullptr;
+  int *d_gdone = nullptr;      // per-group finish counters (fused c* in k_f8_count32x)
+  hipEvent_t solved = nullptr;  // side stream: models of the run using this set written
+  hipEvent_t freed = nullptr;   // main stream: last reader of this set finished
+};
+
+// Absolute error bounds of the fp32 test in the unit frame (|x~| <= R); derivation in
+// f8_kernels.hip above k_f8_count32.  Dl: a line component, De: e, Dn: a squared length.
+struct Bounds {
+  double u, De, Dn, thr2;
+};
+
+Bounds fp32_bounds(const rsd::Frame &fr, double thresh) {
+  const double u = std::ldexp(1.0, -24), R = 1.0 + 1e-6, Lm = 2.0 * R + 1.0;
+  const double Dl = 1.1 * u * (7.0 * R + 3.0);
+  const double De =
+      1.1 * (2.0 * (Dl * R * 1.001 + Lm * u * R) + Dl + u * (Lm + Dl) * (3.0 * R + 2.0) * 1.001);
+  const double Dn = 1.1 * (2.0 * Dl * (2.0 * Lm + Dl) + 3.0 * u * (Lm + Dl) * (Lm + Dl) * 1.001);
+  return {u, De, Dn, (thresh / fr.s) * (thresh / fr.s)};
+}
+
+rsd::Guard32 guard_constants(const rsd::Frame &fr, double thresh) {
+  const Bounds b = fp32_bounds(fr, thresh);
+  rsd::Guard32 g;
+  g.thr2 = static_cast<float>(b.thr2);
+  g.K1 = static_cast<float>(1.02 * 2.0 * b.De);
+  g.Ku = static_cast<float>(1.02 * b.u);
+  g.K0 = static_cast<float>(1.02 * (b.De * b.De + b.thr2 * (1.0 + 1e-6) * b.Dn));
+  g.thr2_px = thresh * thresh;
+  return g;
+}
+
+rsd::GuardPk guard_packed(const rsd::Frame &fr, double thresh) {
+  const Bounds b = fp32_bounds(fr, thresh);
+  const double c = std::sqrt(b.thr2);  // AM-GM split point for 2 De |e| <= De (e^2 / c + c)
+  rsd::GuardPk g;
+  g.thr2 = static_cast<float>(b.thr2);
+  g.Ka = static_cast<float>(1.02 * (b.De / c * (1.0 + 2.0 * b.u) + b.u));
+  g.Kb = static_cast<float>(1.02 * 2.0 * b.u);
+  g.K0 = static_cast<float>(1.02 * (b.De * c + b.De * b.De + b.thr2 * (1.0 + 1e-6) * b.Dn));
+  g.thr2_px = thresh * thresh;
+  return g;
+}
+
+// k_f8_count32x decision constants (derivation above the kernel in f8_kernels.hip).  The
+// 1.02 and 1 -/+ 4u factors absorb the fp64 -> fp32 rounding of the constants themselves.
+rsd::GuardX guard_pair(const rsd::Frame &fr, double thresh) {
+  const Bounds b = fp32_bounds(fr, thresh);
+  const double T = b.thr2, u = b.u, tiny = 1e-30;  // tiny: denormal flushing headroom
+  rsd::GuardX g;
+  g.K1i = static_cast<float>(1.02 * 2.0 * b.De);
+  g.K1o_neg = -g.K1i;
+  g.K0i = static_cast<float>(1.02 * (b.De * b.De + T * b.Dn) + tiny);
+  g.K0o_neg = -static_cast<float>(1.02 * (1.0 + u) * T * b.Dn + tiny);
+  g.alpha = static_cast<float>(T * (1.0 - u) * (1.0 - u) / (1.0 + u) * (1.0 - 4.0 * u));
+  g.beta = static_cast<float>(T * (1.0 + u) * (1.0 + u) / (1.0 - u) * (1.0 + 4.0 * u));
+  g.thr2_px = thresh * thresh;
+  return g;
+}
+
+// Plain-op decision constants (derivation above k_f8_count32x, DEC = 1).
+rsd::GuardY guard_plain(const rsd::Frame &fr, double thresh) {
+  const Bounds b = fp32_bounds(fr, thresh);
+  const double T = b.thr2, u = b.u, tiny = 1e-30;
+  const double c1 = (1.0 - u) / (1.0 + u);
+  rsd::GuardY g;
+  g.K1 = static_cast<float>(1.02 * 2.0 * b.De / (c1 * (1.0 - u)));
+  g.K0 = static_cast<float>(1.02 * (b.De * b.De + T * b.Dn) / (c1 * (1.0 - u)) + tiny);
+  g.alpha = static_cast<float>(T * (1.0 - 4.0 * u) / (1.0 + u));
+  const double alpha = g.alpha;  // the fp32 value the kernel multiplies with
+  g.delta = static_cast<float>(1.02 * (T - alpha * (1.0 - u)) / c1 + tiny);
+  g.thr2_px = thresh * thresh;
+  return g;
+}
+
+// Folded plain-op decision constants (derivation above k_f8_count32x, DEC = 2).
+rsd::GuardF guard_folded(const rsd::Frame &fr, double thresh) {
+  const Bounds b = fp32_bounds(fr, thresh);
+  const double T = b.thr2, u = b.u, tiny = 1e-30;
+  const double c1 = (1.0 - u) / (1.0 + u), M = 18.0 * (1.0 + 1e-5);
+  rsd::GuardF g;
+  g.alpha = static_cast<float>(T * (1.0 - 4.0 * u) / (1.0 + u));
+  const double alpha = g.alpha;
+  const double D0 = (T - alpha * (1.0 - u)) * M;
+  g.K1 = static_cast<float>(1.02 * 2.0 * b.De / (c1 * (1.0 - u)));
+  g.K0 = static_cast<float>(1.02 * (b.De * b.De + T * b.Dn + D0) / (c1 * (1.0 - u)) + tiny);
+  g.pad_ = 0.f;
+  g.thr2_px = thresh * thresh;
+  return g;
+}
+
+int env_int(const char *name, int dflt) {
+  const char *v = std::getenv(name);
+  return v ? std::atoi(v) : dflt;
+}
+
+}  // namespace
+
+struct rs_f8_plan {
+  rs_ctx *ctx = nullptr;
+  int64_t n = 0, max_hyp = 0, ld = 0;
+  hipStream_t side = nullptr;  // solve stream (main stream = ctx->stream)
+  double *d_p12 = nullptr;     // staging (2,n) p1 then (2,n) p2
+  rsd::Pt *d_pts = nullptr;    // AoS float64 points
+  float4 *d_pts32 = nullptr;   // unit-frame fp32 points, NaN-padded to a multiple of 8
+  static constexpr int kBufs = 2, kSlots = 4, kEvRing = 64;
+  RunBufs buf[kBufs];
+  // Each run copies its result into its own pinned slot and records its own events, so runs
+  // are issued without a host round trip; rs_f8_plan_result waits for the last one.
+  rsd::F8DevResult *h_slot[kSlots] = {};  // pinned result headers (inliers stay in HBM)
+  rsd::F8DevResult *h_slot_dev[kSlots] = {};  // their device mappings (written by the tail)
+  hipEvent_t done[kSlots] = {};     // tail of the run owning a slot complete
+  hipEvent_t ring[kEvRing][5] = {}; // solve start/end (side), count start/end, tail end (main)
+  size_t res_bytes = 0;
+  int64_t runs = 0, last_H = 0;
+  bool pending = false;
+  // counting kernel selection (environment knobs for A/B sweeps, tools/sweep.py)
+  rsd::Frame frame{1.0, 0.0, 0.0, 0.0, 0.0};
+  bool fp32_ok = false;       // finite points and a non-degenerate frame
+  bool use_fp32 = true;       // RSAMD_COUNT=fp64 selects the float64 kernel
+  bool packed = false;        // RSAMD_COUNT=pk: two hypotheses per lane (v_pk_fma_f32)
+  bool pair = true;           // k_f8_count32x (default); RSAMD_COUNT=fp32: k_f8_count32
+  bool plain_dec = true;      // k_f8_count32x with the plain-op decision (default, "y")
+  bool folded = false;        // RSAMD_COUNT=z: folded plain decision + SALU bit-plane counts
+  // RSAMD_OVERLAP=1: solve on the side stream, overlapping the previous run's count.  Off by
+  // default: the count kernel is issue bound and the solve's waves slow it by as much as
+  // they hide (r01 A/B: 162.2 vs 159.5 us per run).
+  bool overlap = false;
+  // HIP timing events per run (each is a marker packet between kernels): 0 none, 1 around the
+  // counting kernel (default; the bench's roofline timing), 2 also solve and whole run
+  int timing = 1;
+  int timing_every = 1;       // RSAMD_TIMING_EVERY / rs_f8_plan_set_timing: time every k-th run
+  bool timed[kEvRing] = {};   // whether run r % kEvRing recorded its events
+  bool fuse_max = true;       // RSAMD_FUSEMAX=0: separate k_f8_max pass instead of the fused c*
+  int resident_waves = 8192;  // slices of the fp32 kernel (RSAMD_WAVES)
+  int count_block = 8;        // points per scalar-load block (RSAMD_BLOCK = 4 | 8)
+  bool prefetch = false;      // ping-pong point prefetch (RSAMD_PREFETCH=1; spills SGPRs at 8)
+  int pk_variant = 0, pk_waves = 8192;
+  int chunk_override = 0;     // fp64 kernel point chunk (RSAMD_CHUNK)
+
+  const RunBufs &last() const { return buf[(runs - 1) % kBufs]; }
+};
+
+#define HIP_TRY(expr)                                   \
+  do {                                                  \
+    hipError_t e_ = (expr);                             \
+    if (e_ != hipSuccess) return hip_fail(e_, #expr);   \
+  } while (0)
+
+static void plan_free(rs_f8_plan *p) {
+  (void)hipFree(p->d_p12);
+  (void)hipFree(p->d_pts);
+  (void)hipFree(p->d_pts32);
+  for (RunBufs &b : p->buf) {
+    (void)hipFree(b.d_F);
+    (void)hipFree(b.d_F32);
+    (void)hipFree(b.d_counts);
+    (void)hipFree(b.d_tuples);
+    (void)hipFree(b.d_cand);
+    (void)hipFree(b.d_status);
+    (void)hipFree(b.d_ccount);
+    (void)hipFree(b.d_cstd);
+    (void)hipFree(b.d_cnorm);
+    (void)hipFree(b.d_res);
+    (void)hipFree(b.d_gdone);
+    if (b.solved) (void)hipEventDestroy(b.solved);
+    if (b.freed) (void)hipEventDestroy(b.freed);
+  }
+  for (auto &h : p->h_slot)
+    if (h) (void)hipHostFree(h);
+  for (auto &e : p->done)
+    if (e) (void)hipEventDestroy(e);
+  for (auto &r : p->ring)
+    for (auto &e : r)
+      if (e) (void)hipEventDestroy(e);
+  if (p->side) (void)hipStreamDestroy(p->side);
+}
+
+extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_plan **out) {
+  if (!c || !out) return fail(RS_EINVAL, "null pointer");
+  *out = nullptr;
+  if (n < 8) return fail(RS_EINVAL, "Cannot take a larger sample than population when 'replace=False'");
+  if (n > (1LL << 30) || max_hyp < 1 || max_hyp > (1LL << 30))
+    return fail(RS_EINVAL, "plan dimensions out of range");
+  HIP_TRY(hipSetDevice(c->device));
+  auto *p = new rs_f8_plan();
+  p->ctx = c;
+  p->n = n;
+  p->max_hyp = max_hyp;
+  p->ld = (max_hyp + 63) / 64 * 64;
+  p->res_bytes = sizeof(rsd::F8DevResult) + sizeof(int64_t) * static_cast<size_t>(n);
+  p->chunk_override = env_int("RSAMD_CHUNK", 0);
+  if (const char *cm = std::getenv("RSAMD_COUNT")) {
+    p->use_fp32 = std::strcmp(cm, "fp64") != 0;
+    p->packed = std::strcmp(cm, "pk") == 0;  // "y" (default), "x", "z", "fp32", "pk", "fp64"
+    p->pair = std::strcmp(cm, "x") == 0 || std::strcmp(cm, "y") == 0 ||
+              std::strcmp(cm, "z") == 0;
+    p->plain_dec = std::strcmp(cm, "y") == 0;
+    p->folded = std::strcmp(cm, "z") == 0;
+  }
+  p->overlap = env_int("RSAMD_OVERLAP", 0) != 0;
+  p->timing = env_int("RSAMD_TIMING", 1);
+  p->timing_every = std::max(1, env_int("RSAMD_TIMING_EVERY", 1));
+  p->fuse_max = env_int("RSAMD_FUSEMAX", 1) != 0;
+  {
+    int cus = 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
+      cus = 256;
+    p->resident_waves = std::max(1, env_int("RSAMD_WAVES", cus * 4 * 8 * 4));  // 4 slices per
+    p->count_block = env_int("RSAMD_BLOCK", 8) == 4 ? 4 : 8;                  // resident wave
+    p->prefetch = env_int("RSAMD_PREFETCH", 0) != 0;
+    p->pk_variant = env_int("RSAMD_PKVAR", 0);
+    const int minw = p->pk_variant == 1 || p->pk_variant == 3 ? 6 : (p->pk_variant == 2 ? 4 : 8);
+    p->pk_waves = std::max(1, env_int("RSAMD_WAVES", cus * 4 * minw));
+  }
+  hipError_t e = hipSuccess;
+  int lo = 0, hi = 0;
+  if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+  if (e == hipSuccess) e = hipStreamCreateWithPriority(&p->side, hipStreamNonBlocking, hi);
+#define ALLOC(ptr, bytes) \
+  if (e == hipSuccess) e = hipMalloc(&(ptr), (bytes));
+  ALLOC(p->d_p12, sizeof(double) * 4 * n);
+  ALLOC(p->d_pts, sizeof(rsd::Pt) * n);
+  ALLOC(p->d_pts32, sizeof(float4) * ((n + 7) & ~7LL));
+  for (RunBufs &b : p->buf) {
+    ALLOC(b.d_F, sizeof(double) * 9 * p->ld);
+    ALLOC(b.d_F32, sizeof(float) * 9 * p->ld);
+    ALLOC(b.d_counts, sizeof(int) * p->ld);
+    ALLOC(b.d_tuples, sizeof(int) * 8 * p->ld);
+    ALLOC(b.d_cand, sizeof(int) * p->ld);
+    ALLOC(b.d_status, sizeof(int) * rsd::kStatusWords);
+    ALLOC(b.d_ccount, sizeof(int) * p->ld);
+    ALLOC(b.d_cstd, sizeof(double) * p->ld);
+    ALLOC(b.d_cnorm, sizeof(double) * p->ld);
+    ALLOC(b.d_res, p->res_bytes);
+    ALLOC(b.d_gdone, sizeof(int) * (p->ld / 64));
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&b.solved, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&b.freed, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(b.freed, c->stream);
+  }
+#undef ALLOC
+  for (int k = 0; k < rs_f8_plan::kSlots; ++k) {
+    if (e == hipSuccess)
+      e = hipHostMalloc(reinterpret_cast<void **>(&p->h_slot[k]), sizeof(rsd::F8DevResult));
+    if (e == hipSuccess)
+      e = hipHostGetDevicePointer(reinterpret_cast<void **>(&p->h_slot_dev[k]), p->h_slot[k], 0);
+  }
+  for (auto &ev : p->done)
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  for (auto &r : p->ring)
+    for (auto &ev : r)
+      if (e == hipSuccess) e = hipEventCreate(&ev);
+  if (e != hipSuccess) {
+    plan_free(p);
+    delete p;
+    return hip_fail(e, "rs_f8_plan_create");
+  }
+  *out = p;
+  return RS_OK;
+}
+
+static int plan_sync(rs_f8_plan *p) {
+  HIP_TRY(hipSetDevice(p->ctx->device));
+  HIP_TRY(hipStreamSynchronize(p->side));
+  HIP_TRY(hipStreamSynchronize(p->ctx->stream));
+  p->pending = false;
+  return RS_OK;
+}
+
+extern "C" int rs_f8_plan_destroy(rs_f8_plan *p) {
+  if (!p) return RS_OK;
+  (void)plan_sync(p);
+  plan_free(p);
+  delete p;
+  return RS_OK;
+}
+
+extern "C" int rs_f8_plan_set_points(rs_f8_plan *p, const double *p1, const double *p2) {
+  if (!p || !p1 || !p2) return fail(RS_EINVAL, "null pointer");
+  int st = plan_sync(p);  // runs in flight read the resident points
+  if (st) return st;
+  rs_ctx *c = p->ctx;
+  const int64_t n = p->n;
+  const size_t b = sizeof(double) * 2 * n;
+  HIP_TRY(hipMemcpyAsync(p->d_p12, p1, b, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(p->d_p12 + 2 * n, p2, b, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(rsd::launch_pack_points(p->d_p12, p->d_p12 + 2 * n, static_cast<int>(n), p->d_pts,
+                                  c->stream));
+  // unit frame of the fp32 counting kernel: per-image centres, one common scale
+  double lo[4], hi[4];
+  bool finite = true;
+  for (int k = 0; k < 4; ++k) {
+    lo[k] = INFINITY;
+    hi[k] = -INFINITY;
+  }
+  for (int64_t i = 0; i < n; ++i) {
+    const double v[4] = {p1[i], p1[n + i], p2[i], p2[n + i]};
+    for (int k = 0; k < 4; ++k) {
+      finite &= std::isfinite(v[k]);
+      lo[k] = std::min(lo[k], v[k]);
+      hi[k] = std::max(hi[k], v[k]);
+    }
+  }
+  rsd::Frame fr{0.0, 0.5 * (lo[0] + hi[0]), 0.5 * (lo[1] + hi[1]), 0.5 * (lo[2] + hi[2]),
+                0.5 * (lo[3] + hi[3])};
+  const double cen[4] = {fr.cx1, fr.cy1, fr.cx2, fr.cy2};
+  for (int64_t i = 0; finite && i < n; ++i) {
+    const double v[4] = {p1[i], p1[n + i], p2[i], p2[n + i]};
+    for (int k = 0; k < 4; ++k) fr.s = std::max(fr.s, std::fabs(v[k] - cen[k]));
+  }
+  p->fp32_ok = finite && fr.s > 0.0 && std::isfinite(fr.s);
+  if (p->fp32_ok) {
+    fr.s *= 1.0 + 1e-12;  // |x~| <= 1 after the fp64 division
+    p->frame = fr;
+    HIP_TRY(rsd::launch_pack_points32(p->d_pts, static_cast<int>(n), fr, p->d_pts32, c->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return RS_OK;
+}
+
+static int choose_chunk(const rs_f8_plan *p, int64_t H) {
+  if (p->chunk_override > 0) return p->chunk_override;
+  const int64_t groups = (H + 63) / 64;
+  // aim for >= 8 units of work per SIMD (1024 SIMDs) without chunks below 64 points
+  int64_t nchunks = (8192 + groups - 1) / groups;
+  nchunks = std::max<int64_t>(1, std::min<int64_t>(nchunks, (p->n + 63) / 64));
+  return static_cast<int>((p->n + nchunks - 1) / nchunks);
+}
+
+extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t seed,
+                              uint64_t hyp_offset, const int32_t *host_tuples, double thresh) {
+  if (!p) return fail(RS_EINVAL, "null plan");
+  if (H < 1 || H > p->max_hyp) return fail(RS_EINVAL, "hypothesis count out of plan range");
+  if (mode != RS_SAMPLER_PHILOX && mode != RS_SAMPLER_TUPLES)
+    return fail(RS_EINVAL, "unknown sampler mode");
+  if (mode == RS_SAMPLER_TUPLES && !host_tuples) return fail(RS_EINVAL, "tuples required");
+  if (!(thresh == thresh)) return fail(RS_EINVAL, "threshold is NaN");
+  if (mode == RS_SAMPLER_TUPLES)
+    for (int64_t i = 0; i < 8 * H; ++i)
+      if (host_tuples[i] < 0 || host_tuples[i] >= p->n)
+        return fail(RS_EINVAL, "tuple index out of range");
+  rs_ctx *c = p->ctx;
+  HIP_TRY(hipSetDevice(c->device));
+  const int n = static_cast<int>(p->n), h = static_cast<int>(H);
+  RunBufs &b = p->buf[p->runs % rs_f8_plan::kBufs];
+  hipEvent_t *ev = p->ring[p->runs % rs_f8_plan::kEvRing];
+  const int tl = (p->runs % p->timing_every == 0) ? p->timing : 0;  // this run's timing level
+  p->timed[p->runs % rs_f8_plan::kEvRing] = tl >= 1;
+  const int slot = static_cast<int>(p->runs % rs_f8_plan::kSlots);
+  const bool fp32 = p->use_fp32 && p->fp32_ok;
+  hipStream_t ms = c->stream, ss = p->overlap ? p->side : c->stream;
+
+  // side stream: models of this run into buffer set b once its previous reader is done
+  if (ss != ms) HIP_TRY(hipStreamWaitEvent(ss, b.freed, 0));
+  if (mode == RS_SAMPLER_TUPLES)
+    HIP_TRY(hipMemcpyAsync(b.d_tuples, host_tuples, sizeof(int) * 8 * H, hipMemcpyHostToDevice,
+                           ss));
+  if (tl >= 2) HIP_TRY(hipEventRecord(ev[0], ss));
+  HIP_TRY(rsd::launch_f8_solve(p->d_pts, n, h, mode, seed, hyp_offset, b.d_tuples, b.d_F, p->ld,
+                               b.d_counts, b.d_status, ss, b.d_F32, fp32 ? &p->frame : nullptr,
+                               b.d_gdone));
+  if (tl >= 2) HIP_TRY(hipEventRecord(ev[1], ss));
+  if (ss != ms) {
+    HIP_TRY(hipEventRecord(b.solved, ss));
+    HIP_TRY(hipStreamWaitEvent(ms, b.solved, 0));
+  }
+
+  // main stream: count, select, replay, result D2H
+  if (tl >= 1) HIP_TRY(hipEventRecord(ev[2], ms));
+  if (fp32 && p->packed)
+    HIP_TRY(rsd::launch_f8_count32p(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
+                                    p->pk_waves, guard_packed(p->frame, thresh), b.d_counts, ms,
+                                    p->pk_variant));
+  else if (fp32 && p->pair && p->folded)
+    HIP_TRY(rsd::launch_f8_count32x(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
+                                    p->resident_waves, guard_folded(p->frame, thresh),
+                                    b.d_counts, ms, p->count_block, p->prefetch,
+                                    p->fuse_max ? b.d_gdone : nullptr, b.d_status));
+  else if (fp32 && p->pair && p->plain_dec)
+    HIP_TRY(rsd::launch_f8_count32x(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
+                                    p->resident_waves, guard_plain(p->frame, thresh),
+                                    b.d_counts, ms, p->count_block, p->prefetch,
+                                    p->fuse_max ? b.d_gdone : nullptr, b.d_status));
+  else if (fp32 && p->pair)
+    HIP_TRY(rsd::launch_f8_count32x(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
+                                    p->resident_waves, guard_pair(p->frame, thresh),
+                                    b.d_counts, ms, p->count_block, p->prefetch,
+                                    p->fuse_max ? b.d_gdone : nullptr, b.d_status));
+  else if (fp32)
+    HIP_TRY(rsd::launch_f8_count32(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
+                                   p->resident_waves, guard_constants(p->frame, thresh),
+                                   b.d_counts, ms, p->count_block, p->prefetch));
+  else
+    HIP_TRY(rsd::launch_f8_count(p->d_pts, n, h, b.d_F, p->ld, choose_chunk(p, H),
+                                 thresh * thresh, b.d_counts, ms));
+  if (tl >= 1) HIP_TRY(hipEventRecord(ev[3], ms));
+  // k_f8_count32x folds c* in (gdone given)
+  const bool fused_max = fp32 && p->pair && !p->packed && p->fuse_max;
+  HIP_TRY(rsd::launch_f8_tail(p->d_pts, n, h, b.d_F, p->ld, b.d_counts, 1, thresh, b.d_status,
+                              b.d_cand, b.d_ccount, b.d_cstd, b.d_cnorm, b.d_res, ms,
+                              !fused_max, p->h_slot_dev[slot]));
+  if (tl >= 2) HIP_TRY(hipEventRecord(ev[4], ms));
+  // buffer set b is free once the tail is done (the only cross-stream edge besides solved)
+  if (ss != ms) HIP_TRY(hipEventRecord(b.freed, ms));
+  ++p->runs;
+  p->last_H = H;
+  p->pending = true;
+  return RS_OK;
+}
+
+// Wait for the last run.  Accessors below then read its buffer set synchronously.
+static int plan_wait(rs_f8_plan *p) {
+  if (p->runs == 0) return fail(RS_EINVAL, "no run has been issued on this plan");
+  return p->pending ? plan_sync(p) : RS_OK;
+}
+
+extern "C" int rs_f8_plan_result(rs_f8_plan *p, rs_f8_result *out, int64_t *inliers, int64_t cap,
+                                 int64_t *n_inliers) {
+  if (!p || !out) return fail(RS_EINVAL, "null pointer");
+  int st = plan_wait(p);
+  if (st) return st;
+  const rsd::F8DevResult *r = p->h_slot[(p->runs - 1) % rs_f8_plan::kSlots];
+  std::memcpy(out->F, r->F, sizeof(out->F));
+  out->best_index = r->best_index;
+  out->best_count = r->best_count;
+  out->best_std = r->best_std;
+  out->best_norm = r->best_norm;
+  out->max_count_fast = r->max_count_fast;
+  out->n_candidates = r->n_candidates;
+  out->guard_mismatch = r->guard_mismatch;
+  if (n_inliers) *n_inliers = r->n_inliers;
+  const int64_t k = std::min<int64_t>(cap, r->n_inliers);
+  if (inliers && k > 0)  // S_RANSAC stays in HBM until asked for
+    HIP_TRY(hipMemcpy(inliers, p->last().d_res->inliers, sizeof(int64_t) * k,
+                      hipMemcpyDeviceToHost));
+  return RS_OK;
+}
+
+extern "C" int rs_f8_plan_candidates(rs_f8_plan *p, rs_f8_candidate *out, int64_t cap,
+                                     int64_t *n_out) {
+  if (!p || !n_out) return fail(RS_EINVAL, "null pointer");
+  int st = plan_wait(p);
+  if (st) return st;
+  const RunBufs &b = p->last();
+  const int H = static_cast<int>(p->last_H);
+  const int nb = rsd::select_blocks(H), pb = rsd::select_per_block(H);
+  std::vector<int> bc(nb);
+  HIP_TRY(hipMemcpy(bc.data(), b.d_status + 4, sizeof(int) * nb, hipMemcpyDeviceToHost));
+  std::vector<int> cand, cc;
+  std::vector<double> cs, cn;
+  for (int k = 0; k < nb; ++k) {
+    if (bc[k] == 0) continue;
+    const size_t o = cand.size(), m = static_cast<size_t>(bc[k]);
+    const int64_t seg = static_cast<int64_t>(k) * pb;
+    cand.resize(o + m);
+    cc.resize(o + m);
+    cs.resize(o + m);
+    cn.resize(o + m);
+    HIP_TRY(hipMemcpy(&cand[o], b.d_cand + seg, sizeof(int) * m, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&cc[o], b.d_ccount + seg, sizeof(int) * m, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&cs[o], b.d_cstd + seg, sizeof(double) * m, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&cn[o], b.d_cnorm + seg, sizeof(double) * m, hipMemcpyDeviceToHost));
+  }
+  int cmax = 0;
+  for (int v : cc) cmax = std::max(cmax, v);
+  int64_t k = 0;
+  for (size_t i = 0; i < cand.size(); ++i) {
+    if (cc[i] != cmax || cmax == 0) continue;
+    if (out && k < cap) {
+      rs_f8_candidate &o = out[k];
+      o.index = cand[i];
+      o.count = cc[i];
+      o.std_d = cs[i];
+      o.norm_d = cn[i];
+      for (int q = 0; q < 9; ++q)
+        HIP_TRY(hipMemcpy(&o.F[q], b.d_F + q * p->ld + cand[i], sizeof(double),
+                          hipMemcpyDeviceToHost));
+    }
+    ++k;
+  }
+  *n_out = k;
+  return RS_OK;
+}
+
+extern "C" int rs_f8_plan_counts(rs_f8_plan *p, int32_t *counts, int64_t H) {
+  if (!p || !counts) return fail(RS_EINVAL, "null pointer");
+  int st = plan_wait(p);
+  if (st) return st;
+  if (H > p->last_H) return fail(RS_EINVAL, "H exceeds the last run");
+  HIP_TRY(hipMemcpy(counts, p->last().d_counts, sizeof(int) * H, hipMemcpyDeviceToHost));
+  return RS_OK;
+}
+
+extern "C" int rs_f8_plan_models(rs_f8_plan *p, double *F_out, int64_t H) {
+  if (!p || !F_out) return fail(RS_EINVAL, "null pointer");
+  int st = plan_wait(p);
+  if (st) return st;
+  if (H > p->last_H) return fail(RS_EINVAL, "H exceeds the last run");
+  std::vector<double> soa(static_cast<size_t>(9 * H));
+  for (int k = 0; k < 9; ++k)
+    HIP_TRY(hipMemcpy(soa.data() + k * H, p->last().d_F + k * p->ld, sizeof(double) * H,
+                      hipMemcpyDeviceToHost));
+  for (int64_t h = 0; h < H; ++h)
+    for (int k = 0; k < 9; ++k) F_out[h * 9 + k] = soa[k * H + h];
+  return RS_OK;
+}
+
+extern "C" int rs_f8_plan_kernel_avg(rs_f8_plan *p, int64_t last_n, double *score_ms,
+                                     double *solve_ms, double *total_ms) {
+  if (!p) return fail(RS_EINVAL, "null plan");
+  int st = plan_wait(p);
+  if (st) return st;
+  const int64_t k = std::max<int64_t>(
+      1, std::min<int64_t>({last_n, p->runs, static_cast<int64_t>(rs_f8_plan::kEvRing)}));
+  if (p->timing < 1) return fail(RS_EINVAL, "timing events are disabled (RSAMD_TIMING=0)");
+  double sa = 0, sb = 0, sc = 0;
+  int64_t nt = 0;
+  for (int64_t r = p->runs - k; r < p->runs; ++r) {
+    if (!p->timed[r % rs_f8_plan::kEvRing]) continue;
+    ++nt;
+    hipEvent_t *ev = p->ring[r % rs_f8_plan::kEvRing];
+    float a = 0, b = 0, t = 0;
+    HIP_TRY(hipEventElapsedTime(&b, ev[2], ev[3]));  // count (main stream)
+    if (p->timing >= 2) {
+      HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));  // solve (side stream)
+      HIP_TRY(hipEventElapsedTime(&t, ev[0], ev[4]));  // solve start .. tail end
+    }
+    sa += a;
+    sb += b;
+    sc += t;
+  }
+  // solve / whole-run times need RSAMD_TIMING=2; reported as -1 otherwise
+  if (nt == 0) return fail(RS_EINVAL, "no timed run among the requested ones");
+  if (solve_ms) *solve_ms = p->timing >= 2 ? sa / nt : -1.0;
+  if (score_ms) *score_ms = sb / nt;
+  if (total_ms) *total_ms = p->timing >= 2 ? sc / nt : -1.0;
+  return RS_OK;
+}
+
+extern "C" int rs_f8_plan_set_timing(rs_f8_plan *p, int32_t level, int32_t every) {
+  if (!p) return fail(RS_EINVAL, "null plan");
+  if (level < 0 || level > 2 || every < 1) return fail(RS_EINVAL, "bad timing level / period");
+  p->timing = level;
+  p->timing_every = every;
+  return RS_OK;
+}
+
+extern "C" int rs_f8_plan_kernel_ms(rs_f8_plan *p, double *score_ms, double *solve_ms,
+                                    double *total_ms) {
+  return rs_f8_plan_kernel_avg(p, 1, score_ms, solve_ms, total_ms);
+}
+
+// ------------------------------------------------------------------------------------------
+// numpy-exact one call (fun.getFFromLabCode loop)
+// ------------------------------------------------------------------------------------------
+extern "C" int rs_f8_ransac_np(rs_ctx *c, const double *p1, const double *p2, int64_t n,
+                               int64_t H, uint32_t *mt_key, int32_t *mt_pos, double thresh,
+                               rs_f8_result *out, int64_t *inliers, int64_t cap,
+                               int64_t *n_inliers) {
+  if (!c || !p1 || !p2 || !mt_key || !mt_pos || !out) return fail(RS_EINVAL, "null pointer");
+  if (n < 8)
+    return fail(RS_EINVAL, "Cannot take a larger sample than population when 'replace=False'");
+  if (H < 1) return fail(RS_EINVAL, "hypothesis count must be positive");
+  if (c->np_plan && (c->np_plan->n != n || c->np_plan->max_hyp < H)) {
+    rs_f8_plan_destroy(c->np_plan);
+    c->np_plan = nullptr;
+  }
+  int st;
+  if (!c->np_plan && (st = rs_f8_plan_create(c, n, H, &c->np_plan))) return st;
+  if ((st = rs_f8_plan_set_points(c->np_plan, p1, p2))) return st;
+  std::vector<int32_t> tuples(static_cast<size_t>(8 * H));
+  uint32_t key[RS_MT_N];
+  int32_t pos = *mt_pos;
+  std::memcpy(key, mt_key, sizeof(key));
+  if ((st = rs_np_choice_tuples(key, &pos, n, 8, H, tuples.data()))) return st;
+  if ((st = rs_f8_plan_run(c->np_plan, H, RS_SAMPLER_TUPLES, 0, 0, tuples.data(), thresh)))
+    return st;
+  if ((st = rs_f8_plan_result(c->np_plan, out, inliers, cap, n_inliers))) return st;
+  std::memcpy(mt_key, key, sizeof(key));
+  *mt_pos = pos;
+  return RS_OK;
+}

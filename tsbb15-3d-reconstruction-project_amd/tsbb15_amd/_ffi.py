@@ -71,6 +71,7 @@ _SIGS = {
     "rs_f8_plan_models": (C.c_int, [C.c_void_p, _dp, C.c_int64]),
     "rs_f8_plan_kernel_ms": (C.c_int, [C.c_void_p, _dp, _dp, _dp]),
     "rs_f8_plan_kernel_avg": (C.c_int, [C.c_void_p, C.c_int64, _dp, _dp, _dp]),
+    "rs_f8_plan_set_timing": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     "rs_f8_ransac_np": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, C.c_int64, _u32p, _i32p,
                                   C.c_double, C.POINTER(F8Result), _i64p, C.c_int64, _i64p]),
     "rs_pnp_dlt": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, _dp]),
@@ -290,6 +291,11 @@ class F8Plan:
         out = np.empty((int(H), 9), dtype=np.float64)
         check(lib().rs_f8_plan_models(self._h, ptr(out, C.c_double), int(H)))
         return out.reshape(-1, 3, 3)
+
+    def set_timing(self, level=1, every=1):
+        """HIP timing events per run: level 0 none, 1 counting kernel, 2 also solve / run;
+        recorded on every ``every``-th run (each event is a marker packet between kernels)."""
+        check(lib().rs_f8_plan_set_timing(self._h, int(level), int(every)))
 
     def kernel_ms(self, last_n=1):
         """Device times of the last run, or averaged over the last ``last_n`` runs."""
