@@ -4,19 +4,18 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "device_math.h"
+
 #define RSD_SAMPLER_PHILOX 0
 #define RSD_SAMPLER_TUPLES 1
 
 namespace rsd {
 
-struct Pt;
-struct Frame;
-struct Guard32;
-struct GuardPk;
 
 // Grid of the selection passes; the status buffer holds 4 words + kSelectBlocks counts.
 constexpr int kSelectBlocks = 256;
 constexpr int kStatusWords = 4 + kSelectBlocks;
+constexpr int kTailThreads = 512;  // workgroup of the fused tail + solve launch
 
 // Device-resident result of one F run; copied back to the host in one transfer together
 // with the first n_inliers entries of `inliers`.
@@ -33,6 +32,36 @@ struct F8DevResult {
   int64_t best_cand;
   int64_t pad_;
   int64_t inliers[];
+};
+
+// One run's solve (k_f8_solve / the solve half of k_f8_tail_solve).
+struct SolveArgs {
+  const Pt *pts;
+  int n, H, mode, pad_;
+  uint64_t seed, hyp_offset;
+  const int *tuples;
+  double *Fsoa;
+  int64_t ld;
+  int *counts;   // zeroed per hypothesis
+  int *status;   // status words 0..3 zeroed
+  float *F32soa; // unit-frame fp32 models (null: fp64 counting)
+  Frame frame;
+  int *gdone;    // per-group finish counters zeroed (fused c*)
+};
+
+// One run's selection tail (candidates, reference statistics, replay, S_RANSAC).
+struct TailArgs {
+  const Pt *pts;
+  int n, H, slack, per_block;
+  const double *Fsoa;
+  int64_t ld;
+  const int *counts;
+  int *status;   // [c*, n_candidates, done counter, spare, per-block candidate counts]
+  double thresh;
+  int *cand, *ccount;
+  double *cstd, *cnorm;
+  F8DevResult *res;   // HBM result (header + S_RANSAC)
+  F8DevResult *hres;  // pinned host header slot (device mapping), may be null
 };
 
 hipError_t launch_pack_points(const double *p1, const double *p2, int n, Pt *pts,
@@ -60,13 +89,13 @@ hipError_t launch_f8_count32x(const float4 *pts32, const Pt *pts, int n, int H,
 hipError_t launch_f8_count(const Pt *pts, int n, int H, const double *Fsoa, int64_t ld,
                            int chunk, double thr2, int *counts, hipStream_t s);
 // Selection tail: c* (k_f8_max, unless the counting kernel fused it), candidates + reference
-// statistics + (last block) replay and S_RANSAC (k_f8_cand_stats).  Candidates live in per-block segments of `cand`.
+// statistics + (last block) replay and S_RANSAC.  Candidates live in per-block segments of
+// `cand`.
 int select_per_block(int H);
 int select_blocks(int H);
-hipError_t launch_f8_tail(const Pt *pts, int n, int H, const double *Fsoa, int64_t ld,
-                          const int *counts, int slack, double thresh, int *status, int *cand,
-                          int *ccount, double *cstd, double *cnorm, F8DevResult *res,
-                          hipStream_t s, bool need_max = true, F8DevResult *hres = nullptr);
+hipError_t launch_f8_max(const int *counts, int H, int *status, hipStream_t s);
+// Tail of one run and/or solve of the next in one launch (either may be null).
+hipError_t launch_f8_tail_solve(TailArgs *ta, SolveArgs *sa, hipStream_t s);
 hipError_t launch_residuals(const Pt *pts, int n, const double *F, double *out, hipStream_t s);
 
 }  // namespace rsd

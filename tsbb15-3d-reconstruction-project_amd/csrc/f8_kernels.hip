@@ -71,16 +71,20 @@ __device__ __forceinline__ int add_block_count8(int cnt, const unsigned long lon
 }
 
 // ----------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_f8_solve(const Pt *__restrict__ pts, int n, int H,
-                                                  int mode, uint64_t seed, uint64_t hyp_offset,
-                                                  const int *__restrict__ tuples,
-                                                  double *__restrict__ Fsoa, int64_t ld,
-                                                  int *__restrict__ counts,
-                                                  int *__restrict__ status,
-                                                  float *__restrict__ F32soa, Frame fr,
-                                                  int *__restrict__ gdone) {
-  const int h = blockIdx.x * blockDim.x + threadIdx.x;
-  if (h >= H) return;
+// One hypothesis h of a run: sample, 8-point F (float64), its unit-frame fp32 copy, and the
+// per-run zeroing the counting kernel and the selection tail rely on.
+__device__ __forceinline__ void solve_one(const SolveArgs &a, int h) {
+  const Pt *__restrict__ pts = a.pts;
+  const int n = a.n, mode = a.mode;
+  const uint64_t seed = a.seed, hyp_offset = a.hyp_offset;
+  const int *__restrict__ tuples = a.tuples;
+  double *__restrict__ Fsoa = a.Fsoa;
+  const int64_t ld = a.ld;
+  int *__restrict__ counts = a.counts;
+  int *__restrict__ status = a.status;
+  float *__restrict__ F32soa = a.F32soa;
+  const Frame fr = a.frame;
+  int *__restrict__ gdone = a.gdone;
   if (counts) counts[h] = 0;  // the counting kernel accumulates into it
   if (status && h == 0) {  // c*, n_candidates, tail done-counter, spare
 #pragma unroll
@@ -130,6 +134,11 @@ __global__ __launch_bounds__(256) void k_f8_solve(const Pt *__restrict__ pts, in
 #pragma unroll
     for (int k = 0; k < 9; ++k) F32soa[k * ld + h] = static_cast<float>(Ft[k] * kap);
   }
+}
+
+__global__ __launch_bounds__(256) void k_f8_solve(SolveArgs a) {
+  const int h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h < a.H) solve_one(a, h);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -665,38 +674,40 @@ __device__ void replay_inliers(const Pt *__restrict__ pts, int n, const int *cou
 // every hypothesis of the slice with fast count >= max(c* - slack, 1) is appended in index
 // order to the block's own segment cand[b * per_block + j] (bc[b] entries), then the block
 // re-scores each of them with dist_ref: count, np.std(d) (two-pass), np.linalg.norm(d).
-__global__ __launch_bounds__(1024) void k_f8_cand_stats(const Pt *__restrict__ pts, int n,
-                                                       const double *__restrict__ Fsoa,
-                                                       int64_t ld, const int *__restrict__ counts,
-                                                       int H, int slack, int per_block,
-                                                       const int *__restrict__ status,
-                                                       double thresh, int *__restrict__ bc,
-                                                       int *__restrict__ cand,
-                                                       int *__restrict__ ccount,
-                                                       double *__restrict__ cstd,
-                                                       double *__restrict__ cnorm,
-                                                       int *__restrict__ status_rw,
-                                                       F8DevResult *__restrict__ res,
-                                                       F8DevResult *__restrict__ hres) {
-  __shared__ double shd[16];
+__device__ void cand_stats_block(const TailArgs &a, int bid, int nblocks) {
+  const Pt *__restrict__ pts = a.pts;
+  const int n = a.n, H = a.H, slack = a.slack, per_block = a.per_block;
+  const double *__restrict__ Fsoa = a.Fsoa;
+  const int64_t ld = a.ld;
+  const int *__restrict__ counts = a.counts;
+  const int *__restrict__ status = a.status;
+  int *__restrict__ status_rw = a.status;
+  const double thresh = a.thresh;
+  int *__restrict__ bc = a.status + 4;
+  int *__restrict__ cand = a.cand;
+  int *__restrict__ ccount = a.ccount;
+  double *__restrict__ cstd = a.cstd;
+  double *__restrict__ cnorm = a.cnorm;
+  constexpr int NW = kTailThreads / 64;
+  __shared__ double shd[NW];
   __shared__ int last_s;
-  __shared__ int shi[16];
-  __shared__ int woff[16];
+  __shared__ int shi[NW];
+  __shared__ int woff[NW];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int cmax = status[0];
   const int thr = max(cmax - slack, 1);
-  const int b0 = blockIdx.x * per_block, b1 = min(H, b0 + per_block);
-  int *seg = cand + static_cast<int64_t>(blockIdx.x) * per_block;
+  const int b0 = bid * per_block, b1 = min(H, b0 + per_block);
+  int *seg = cand + static_cast<int64_t>(bid) * per_block;
   int nloc = 0;
   if (cmax > 0) {
-    for (int b = b0; b < b1; b += 1024) {
+    for (int b = b0; b < b1; b += kTailThreads) {
       const int i = b + tid;
       const bool take = i < b1 && counts[i] >= thr;
       const unsigned long long bal = __ballot(take);
       if (lane == 0) woff[w] = __popcll(bal);
       __syncthreads();
       int base = nloc, tot = 0;
-      for (int q = 0; q < 16; ++q) {
+      for (int q = 0; q < NW; ++q) {
         if (q < w) base += woff[q];
         tot += woff[q];
       }
@@ -705,7 +716,7 @@ __global__ __launch_bounds__(1024) void k_f8_cand_stats(const Pt *__restrict__ p
       __syncthreads();
     }
   }
-  if (tid == 0) st_agent(&bc[blockIdx.x], nloc);
+  if (tid == 0) st_agent(&bc[bid], nloc);
   wait_vmem();
   __syncthreads();  // seg[] written by this block is visible to all its threads
   for (int j = 0; j < nloc; ++j) {
@@ -715,7 +726,7 @@ __global__ __launch_bounds__(1024) void k_f8_cand_stats(const Pt *__restrict__ p
     for (int k = 0; k < 9; ++k) f[k] = Fsoa[k * ld + h];
     double s1 = 0.0, s2 = 0.0;
     int cnt = 0;
-    for (int i = tid; i < n; i += 1024) {
+    for (int i = tid; i < n; i += kTailThreads) {
       const double d = dist_ref(f, pts[i]);
       cnt += d < thresh ? 1 : 0;
       s1 += d;
@@ -726,13 +737,13 @@ __global__ __launch_bounds__(1024) void k_f8_cand_stats(const Pt *__restrict__ p
     cnt = block_reduce_sum(cnt, shi);
     const double mean = s1 / static_cast<double>(n);
     double s3 = 0.0;
-    for (int i = tid; i < n; i += 1024) {
+    for (int i = tid; i < n; i += kTailThreads) {
       const double v = dist_ref(f, pts[i]) - mean;
       s3 += v * v;
     }
     s3 = block_sum_d(s3, shd);
     if (tid == 0) {
-      const int64_t slot = static_cast<int64_t>(blockIdx.x) * per_block + j;
+      const int64_t slot = static_cast<int64_t>(bid) * per_block + j;
       st_agent(&ccount[slot], cnt);
       st_agent(&cstd[slot], sqrt(s3 / static_cast<double>(n)));
       st_agent(&cnorm[slot], sqrt(s2));
@@ -742,11 +753,11 @@ __global__ __launch_bounds__(1024) void k_f8_cand_stats(const Pt *__restrict__ p
   // are agent-scope stores completed (vmcnt) before its done-counter increment
   wait_vmem();
   __syncthreads();
-  if (tid == 0) last_s = atomicAdd(&status_rw[2], 1) == static_cast<int>(gridDim.x) - 1;
+  if (tid == 0) last_s = atomicAdd(&status_rw[2], 1) == static_cast<int>(nblocks) - 1;
   __syncthreads();
   if (!last_s) return;
-  replay_inliers(pts, n, counts, gridDim.x, per_block, bc, cand, ccount, cstd, cnorm, Fsoa, ld,
-                 status_rw, thresh, res, hres);
+  replay_inliers(pts, n, counts, nblocks, per_block, bc, cand, ccount, cstd, cnorm, Fsoa, ld,
+                 status_rw, thresh, a.res, a.hres);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -761,7 +772,7 @@ __device__ __forceinline__ uint64_t key_norm(double v) {  // "y > norm" is false
   return (v != v) ? ~0ull : static_cast<uint64_t>(__double_as_longlong(v));
 }
 
-// One 1024-thread workgroup (the last k_f8_cand_stats block to finish): wave 0 replays
+// One kTailThreads workgroup (the last cand_stats block to finish): wave 0 replays
 // fun.py:320-328 over the candidates in global index order (segments in block order), 64 per
 // coalesced load; then the whole workgroup extracts S_RANSAC = flatnonzero(d < t) of the
 // winner in order.  The result header goes to res (HBM) and, when given, to hres (the run's
@@ -775,7 +786,7 @@ __device__ void replay_inliers(const Pt *__restrict__ pts, int n, const int *cou
                                F8DevResult *__restrict__ hres) {
   int *status_out = status;
   __shared__ int pref[kSelectBlocks + 1];
-  __shared__ int woff[16];
+  __shared__ int woff[kTailThreads / 64];
   __shared__ int base_s;
   __shared__ double fsh[9];
   __shared__ int have_s;
@@ -893,7 +904,7 @@ __device__ void replay_inliers(const Pt *__restrict__ pts, int n, const int *cou
   double f[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) f[k] = fsh[k];
-  for (int b = 0; b < n; b += 1024) {
+  for (int b = 0; b < n; b += kTailThreads) {
     const int i = b + tid;
     const bool take = have && i < n && dist_ref(f, pts[i]) < thresh;
     const unsigned long long bal = __ballot(take);
@@ -902,7 +913,7 @@ __device__ void replay_inliers(const Pt *__restrict__ pts, int n, const int *cou
     __syncthreads();
     if (tid == 0) {
       int acc = base_s;
-      for (int q = 0; q < 16; ++q) {
+      for (int q = 0; q < kTailThreads / 64; ++q) {
         const int t = woff[q];
         woff[q] = acc;
         acc += t;
@@ -965,10 +976,22 @@ hipError_t launch_f8_solve(const Pt *pts, int n, int H, int mode, uint64_t seed,
                            uint64_t hyp_offset, const int *tuples, double *Fsoa, int64_t ld,
                            int *counts, int *status, hipStream_t s, float *F32soa,
                            const Frame *frame, int *gdone) {
-  const Frame fr = frame ? *frame : Frame{1.0, 0.0, 0.0, 0.0, 0.0};
-  hipLaunchKernelGGL(k_f8_solve, dim3((H + 255) / 256), dim3(256), 0, s, pts, n, H, mode, seed,
-                     hyp_offset, tuples, Fsoa, ld, counts, status, frame ? F32soa : nullptr,
-                     fr, gdone);
+  SolveArgs a{};
+  a.pts = pts;
+  a.n = n;
+  a.H = H;
+  a.mode = mode;
+  a.seed = seed;
+  a.hyp_offset = hyp_offset;
+  a.tuples = tuples;
+  a.Fsoa = Fsoa;
+  a.ld = ld;
+  a.counts = counts;
+  a.status = status;
+  a.F32soa = frame ? F32soa : nullptr;
+  a.frame = frame ? *frame : Frame{1.0, 0.0, 0.0, 0.0, 0.0};
+  a.gdone = gdone;
+  hipLaunchKernelGGL(k_f8_solve, dim3((H + 255) / 256), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
@@ -1096,15 +1119,40 @@ int select_blocks(int H) {
   return (H + pb - 1) / pb;
 }
 
-hipError_t launch_f8_tail(const Pt *pts, int n, int H, const double *Fsoa, int64_t ld,
-                          const int *counts, int slack, double thresh, int *status, int *cand,
-                          int *ccount, double *cstd, double *cnorm, F8DevResult *res,
-                          hipStream_t s, bool need_max, F8DevResult *hres) {
-  int *bc = status + 4;  // per-block candidate counts live behind the status words
-  const int pb = select_per_block(H), nb = select_blocks(H);
-  if (need_max) hipLaunchKernelGGL(k_f8_max, dim3(nb), dim3(256), 0, s, counts, H, status);
-  hipLaunchKernelGGL(k_f8_cand_stats, dim3(nb), dim3(1024), 0, s, pts, n, Fsoa, ld, counts, H,
-                     slack, pb, status, thresh, bc, cand, ccount, cstd, cnorm, status, res, hres);
+hipError_t launch_f8_max(const int *counts, int H, int *status, hipStream_t s) {
+  hipLaunchKernelGGL(k_f8_max, dim3(select_blocks(H)), dim3(256), 0, s, counts, H, status);
+  return hipGetLastError();
+}
+
+// The selection tail of run k-1 (blocks [0, ntail)) and the solve of run k (the rest) in one
+// launch: both are latency bound and touch disjoint buffer sets, so they share the machine
+// instead of running back to back.
+__global__ __launch_bounds__(kTailThreads) void k_f8_tail_solve(TailArgs ta, int ntail,
+                                                               SolveArgs sa) {
+  if (static_cast<int>(blockIdx.x) < ntail) {
+    cand_stats_block(ta, blockIdx.x, ntail);
+  } else {
+    const int h = (blockIdx.x - ntail) * kTailThreads + threadIdx.x;
+    if (h < sa.H) solve_one(sa, h);
+  }
+}
+
+hipError_t launch_f8_tail_solve(TailArgs *ta, SolveArgs *sa, hipStream_t s) {
+  int ntail = 0, nsolve = 0;
+  TailArgs t{};
+  SolveArgs v{};
+  if (ta) {
+    t = *ta;
+    t.per_block = select_per_block(t.H);
+    ntail = select_blocks(t.H);
+  }
+  if (sa) {
+    v = *sa;
+    nsolve = (v.H + kTailThreads - 1) / kTailThreads;
+  }
+  if (ntail + nsolve == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_f8_tail_solve, dim3(ntail + nsolve), dim3(kTailThreads), 0, s, t, ntail,
+                     v);
   return hipGetLastError();
 }
 

@@ -2,16 +2,17 @@
 // hypotheses issued back to back.  Replaces the fun.getFFromLabCode hypothesis loop
 // (fun.py:298-328).
 //
-// Pipeline of one run (two HIP streams, double-buffered per-run buffers):
+// One HIP stream, two alternating per-run buffer sets.  rs_f8_plan_run(k) enqueues
 //
-//   side stream:  [wait slot free] -> tuples H2D (parity mode) -> k_f8_solve -> (solved)
-//   main stream:  [wait solved]    -> k_f8_count32x (+ fused c*) -> k_f8_cand_stats (+ replay
-//                                  in its last block; header -> pinned host slot) -> (slot free)
+//   k_f8_tail_solve  [selection tail of run k-1 | solve of run k]   (one launch)
+//   k_f8_count32x    counts of run k (+ fused c*)
 //
-// The solve of run k+1 (latency bound, ~1.5 waves per SIMD) writes buffer set (k+1)%2 while
-// the counting kernel of run k (VALU bound) reads set k%2, so in a back-to-back sequence the
-// solve hides under the previous run's count + selection tail.  The side stream has the
-// higher priority so its workgroups are dispatched ahead of queued count slices.
+// and leaves run k's tail pending: it rides along with run k+1's solve, or is flushed alone
+// by rs_f8_plan_result / set_points / destroy.  The tail (candidates, reference statistics,
+// replay, S_RANSAC; latency bound, a few busy workgroups) and the solve (latency bound,
+// ~1.5 waves per SIMD) thus share the machine instead of running back to back, with no
+// cross-stream events (each event or wait is a packet the command processor retires
+// between kernels; r01: ~3.5 us each).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -42,8 +43,6 @@ struct RunBufs {
   double *d_cstd = nullptr, *d_cnorm = nullptr;
   rsd::F8DevResult *d_res = nullptr;
   int *d_gdone = nullptr;      // per-group finish counters (fused c* in k_f8_count32x)
-  hipEvent_t solved = nullptr;  // side stream: models of the run using this set written
-  hipEvent_t freed = nullptr;   // main stream: last reader of this set finished
 };
 
 // Absolute error bounds of the fp32 test in the unit frame (|x~| <= R); derivation in
@@ -141,21 +140,22 @@ int env_int(const char *name, int dflt) {
 struct rs_f8_plan {
   rs_ctx *ctx = nullptr;
   int64_t n = 0, max_hyp = 0, ld = 0;
-  hipStream_t side = nullptr;  // solve stream (main stream = ctx->stream)
   double *d_p12 = nullptr;     // staging (2,n) p1 then (2,n) p2
   rsd::Pt *d_pts = nullptr;    // AoS float64 points
   float4 *d_pts32 = nullptr;   // unit-frame fp32 points, NaN-padded to a multiple of 8
   static constexpr int kBufs = 2, kSlots = 4, kEvRing = 64;
   RunBufs buf[kBufs];
-  // Each run copies its result into its own pinned slot and records its own events, so runs
-  // are issued without a host round trip; rs_f8_plan_result waits for the last one.
-  rsd::F8DevResult *h_slot[kSlots] = {};  // pinned result headers (inliers stay in HBM)
-  rsd::F8DevResult *h_slot_dev[kSlots] = {};  // their device mappings (written by the tail)
-  hipEvent_t done[kSlots] = {};     // tail of the run owning a slot complete
-  hipEvent_t ring[kEvRing][5] = {}; // solve start/end (side), count start/end, tail end (main)
-  size_t res_bytes = 0;
+  // Each run's tail writes its result header into its own pinned slot (through the host
+  // mapping) and S_RANSAC into its buffer set's HBM result; rs_f8_plan_result waits for the
+  // last run and copies S_RANSAC on demand.
+  rsd::F8DevResult *h_slot[kSlots] = {};
+  rsd::F8DevResult *h_slot_dev[kSlots] = {};
+  hipEvent_t ring[kEvRing][4] = {};  // count start/end; tail+solve launch start/end
+  bool timed[kEvRing] = {};          // whether run r % kEvRing recorded its events
   int64_t runs = 0, last_H = 0;
-  bool pending = false;
+  bool pending = false;              // stream work not yet waited for
+  bool tail_pending = false;         // the last run's tail is not enqueued yet
+  rsd::TailArgs tail{};              // ... its arguments
   // counting kernel selection (environment knobs for A/B sweeps, tools/sweep.py)
   rsd::Frame frame{1.0, 0.0, 0.0, 0.0, 0.0};
   bool fp32_ok = false;       // finite points and a non-degenerate frame
@@ -164,16 +164,11 @@ struct rs_f8_plan {
   bool pair = true;           // k_f8_count32x (default); RSAMD_COUNT=fp32: k_f8_count32
   bool plain_dec = true;      // k_f8_count32x with the plain-op decision (default, "y")
   bool folded = false;        // RSAMD_COUNT=z: folded plain decision + SALU bit-plane counts
-  // RSAMD_OVERLAP=1: solve on the side stream, overlapping the previous run's count.  Off by
-  // default: the count kernel is issue bound and the solve's waves slow it by as much as
-  // they hide (r01 A/B: 162.2 vs 159.5 us per run).
-  bool overlap = false;
+  bool fuse_max = true;       // RSAMD_FUSEMAX=0: separate k_f8_max pass instead of the fused c*
   // HIP timing events per run (each is a marker packet between kernels): 0 none, 1 around the
-  // counting kernel (default; the bench's roofline timing), 2 also solve and whole run
+  // counting kernel (default; the bench's roofline timing), 2 also the tail+solve launch
   int timing = 1;
   int timing_every = 1;       // RSAMD_TIMING_EVERY / rs_f8_plan_set_timing: time every k-th run
-  bool timed[kEvRing] = {};   // whether run r % kEvRing recorded its events
-  bool fuse_max = true;       // RSAMD_FUSEMAX=0: separate k_f8_max pass instead of the fused c*
   int resident_waves = 8192;  // slices of the fp32 kernel (RSAMD_WAVES)
   int count_block = 8;        // points per scalar-load block (RSAMD_BLOCK = 4 | 8)
   bool prefetch = false;      // ping-pong point prefetch (RSAMD_PREFETCH=1; spills SGPRs at 8)
@@ -205,17 +200,12 @@ static void plan_free(rs_f8_plan *p) {
     (void)hipFree(b.d_cnorm);
     (void)hipFree(b.d_res);
     (void)hipFree(b.d_gdone);
-    if (b.solved) (void)hipEventDestroy(b.solved);
-    if (b.freed) (void)hipEventDestroy(b.freed);
   }
   for (auto &h : p->h_slot)
     if (h) (void)hipHostFree(h);
-  for (auto &e : p->done)
-    if (e) (void)hipEventDestroy(e);
   for (auto &r : p->ring)
     for (auto &e : r)
       if (e) (void)hipEventDestroy(e);
-  if (p->side) (void)hipStreamDestroy(p->side);
 }
 
 extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_plan **out) {
@@ -230,7 +220,7 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
   p->n = n;
   p->max_hyp = max_hyp;
   p->ld = (max_hyp + 63) / 64 * 64;
-  p->res_bytes = sizeof(rsd::F8DevResult) + sizeof(int64_t) * static_cast<size_t>(n);
+  const size_t res_bytes = sizeof(rsd::F8DevResult) + sizeof(int64_t) * static_cast<size_t>(n);
   p->chunk_override = env_int("RSAMD_CHUNK", 0);
   if (const char *cm = std::getenv("RSAMD_COUNT")) {
     p->use_fp32 = std::strcmp(cm, "fp64") != 0;
@@ -240,10 +230,9 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
     p->plain_dec = std::strcmp(cm, "y") == 0;
     p->folded = std::strcmp(cm, "z") == 0;
   }
-  p->overlap = env_int("RSAMD_OVERLAP", 0) != 0;
+  p->fuse_max = env_int("RSAMD_FUSEMAX", 1) != 0;
   p->timing = env_int("RSAMD_TIMING", 1);
   p->timing_every = std::max(1, env_int("RSAMD_TIMING_EVERY", 1));
-  p->fuse_max = env_int("RSAMD_FUSEMAX", 1) != 0;
   {
     int cus = 256;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
@@ -256,9 +245,6 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
     p->pk_waves = std::max(1, env_int("RSAMD_WAVES", cus * 4 * minw));
   }
   hipError_t e = hipSuccess;
-  int lo = 0, hi = 0;
-  if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&lo, &hi);
-  if (e == hipSuccess) e = hipStreamCreateWithPriority(&p->side, hipStreamNonBlocking, hi);
 #define ALLOC(ptr, bytes) \
   if (e == hipSuccess) e = hipMalloc(&(ptr), (bytes));
   ALLOC(p->d_p12, sizeof(double) * 4 * n);
@@ -274,11 +260,8 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
     ALLOC(b.d_ccount, sizeof(int) * p->ld);
     ALLOC(b.d_cstd, sizeof(double) * p->ld);
     ALLOC(b.d_cnorm, sizeof(double) * p->ld);
-    ALLOC(b.d_res, p->res_bytes);
+    ALLOC(b.d_res, res_bytes);
     ALLOC(b.d_gdone, sizeof(int) * (p->ld / 64));
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&b.solved, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&b.freed, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventRecord(b.freed, c->stream);
   }
 #undef ALLOC
   for (int k = 0; k < rs_f8_plan::kSlots; ++k) {
@@ -287,8 +270,6 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
     if (e == hipSuccess)
       e = hipHostGetDevicePointer(reinterpret_cast<void **>(&p->h_slot_dev[k]), p->h_slot[k], 0);
   }
-  for (auto &ev : p->done)
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
   for (auto &r : p->ring)
     for (auto &ev : r)
       if (e == hipSuccess) e = hipEventCreate(&ev);
@@ -301,9 +282,13 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
   return RS_OK;
 }
 
-static int plan_sync(rs_f8_plan *p) {
+// Enqueue the pending tail alone (no next run to ride along with), then wait for the stream.
+static int plan_flush(rs_f8_plan *p) {
   HIP_TRY(hipSetDevice(p->ctx->device));
-  HIP_TRY(hipStreamSynchronize(p->side));
+  if (p->tail_pending) {
+    HIP_TRY(rsd::launch_f8_tail_solve(&p->tail, nullptr, p->ctx->stream));
+    p->tail_pending = false;
+  }
   HIP_TRY(hipStreamSynchronize(p->ctx->stream));
   p->pending = false;
   return RS_OK;
@@ -311,7 +296,7 @@ static int plan_sync(rs_f8_plan *p) {
 
 extern "C" int rs_f8_plan_destroy(rs_f8_plan *p) {
   if (!p) return RS_OK;
-  (void)plan_sync(p);
+  (void)plan_flush(p);
   plan_free(p);
   delete p;
   return RS_OK;
@@ -319,7 +304,7 @@ extern "C" int rs_f8_plan_destroy(rs_f8_plan *p) {
 
 extern "C" int rs_f8_plan_set_points(rs_f8_plan *p, const double *p1, const double *p2) {
   if (!p || !p1 || !p2) return fail(RS_EINVAL, "null pointer");
-  int st = plan_sync(p);  // runs in flight read the resident points
+  int st = plan_flush(p);  // runs in flight read the resident points
   if (st) return st;
   rs_ctx *c = p->ctx;
   const int64_t n = p->n;
@@ -390,25 +375,36 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
   p->timed[p->runs % rs_f8_plan::kEvRing] = tl >= 1;
   const int slot = static_cast<int>(p->runs % rs_f8_plan::kSlots);
   const bool fp32 = p->use_fp32 && p->fp32_ok;
-  hipStream_t ms = c->stream, ss = p->overlap ? p->side : c->stream;
+  const bool fused_max = fp32 && p->pair && !p->packed && p->fuse_max;
+  hipStream_t ms = c->stream;
 
-  // side stream: models of this run into buffer set b once its previous reader is done
-  if (ss != ms) HIP_TRY(hipStreamWaitEvent(ss, b.freed, 0));
   if (mode == RS_SAMPLER_TUPLES)
     HIP_TRY(hipMemcpyAsync(b.d_tuples, host_tuples, sizeof(int) * 8 * H, hipMemcpyHostToDevice,
-                           ss));
-  if (tl >= 2) HIP_TRY(hipEventRecord(ev[0], ss));
-  HIP_TRY(rsd::launch_f8_solve(p->d_pts, n, h, mode, seed, hyp_offset, b.d_tuples, b.d_F, p->ld,
-                               b.d_counts, b.d_status, ss, b.d_F32, fp32 ? &p->frame : nullptr,
-                               b.d_gdone));
-  if (tl >= 2) HIP_TRY(hipEventRecord(ev[1], ss));
-  if (ss != ms) {
-    HIP_TRY(hipEventRecord(b.solved, ss));
-    HIP_TRY(hipStreamWaitEvent(ms, b.solved, 0));
-  }
+                           ms));
+  // [tail of the previous run | solve of this run]: buffer set b was last read by run k-2,
+  // whose tail is complete (stream order)
+  rsd::SolveArgs sa{};
+  sa.pts = p->d_pts;
+  sa.n = n;
+  sa.H = h;
+  sa.mode = mode;
+  sa.seed = seed;
+  sa.hyp_offset = hyp_offset;
+  sa.tuples = b.d_tuples;
+  sa.Fsoa = b.d_F;
+  sa.ld = p->ld;
+  sa.counts = b.d_counts;
+  sa.status = b.d_status;
+  sa.F32soa = fp32 ? b.d_F32 : nullptr;
+  sa.frame = fp32 ? p->frame : rsd::Frame{1.0, 0.0, 0.0, 0.0, 0.0};
+  sa.gdone = b.d_gdone;
+  if (tl >= 2) HIP_TRY(hipEventRecord(ev[2], ms));
+  HIP_TRY(rsd::launch_f8_tail_solve(p->tail_pending ? &p->tail : nullptr, &sa, ms));
+  p->tail_pending = false;
+  if (tl >= 2) HIP_TRY(hipEventRecord(ev[3], ms));
 
-  // main stream: count, select, replay, result D2H
-  if (tl >= 1) HIP_TRY(hipEventRecord(ev[2], ms));
+  // counts of this run
+  if (tl >= 1) HIP_TRY(hipEventRecord(ev[0], ms));
   if (fp32 && p->packed)
     HIP_TRY(rsd::launch_f8_count32p(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
                                     p->pk_waves, guard_packed(p->frame, thresh), b.d_counts, ms,
@@ -417,17 +413,17 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
     HIP_TRY(rsd::launch_f8_count32x(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
                                     p->resident_waves, guard_folded(p->frame, thresh),
                                     b.d_counts, ms, p->count_block, p->prefetch,
-                                    p->fuse_max ? b.d_gdone : nullptr, b.d_status));
+                                    fused_max ? b.d_gdone : nullptr, b.d_status));
   else if (fp32 && p->pair && p->plain_dec)
     HIP_TRY(rsd::launch_f8_count32x(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
                                     p->resident_waves, guard_plain(p->frame, thresh),
                                     b.d_counts, ms, p->count_block, p->prefetch,
-                                    p->fuse_max ? b.d_gdone : nullptr, b.d_status));
+                                    fused_max ? b.d_gdone : nullptr, b.d_status));
   else if (fp32 && p->pair)
     HIP_TRY(rsd::launch_f8_count32x(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
                                     p->resident_waves, guard_pair(p->frame, thresh),
                                     b.d_counts, ms, p->count_block, p->prefetch,
-                                    p->fuse_max ? b.d_gdone : nullptr, b.d_status));
+                                    fused_max ? b.d_gdone : nullptr, b.d_status));
   else if (fp32)
     HIP_TRY(rsd::launch_f8_count32(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
                                    p->resident_waves, guard_constants(p->frame, thresh),
@@ -435,25 +431,39 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
   else
     HIP_TRY(rsd::launch_f8_count(p->d_pts, n, h, b.d_F, p->ld, choose_chunk(p, H),
                                  thresh * thresh, b.d_counts, ms));
-  if (tl >= 1) HIP_TRY(hipEventRecord(ev[3], ms));
-  // k_f8_count32x folds c* in (gdone given)
-  const bool fused_max = fp32 && p->pair && !p->packed && p->fuse_max;
-  HIP_TRY(rsd::launch_f8_tail(p->d_pts, n, h, b.d_F, p->ld, b.d_counts, 1, thresh, b.d_status,
-                              b.d_cand, b.d_ccount, b.d_cstd, b.d_cnorm, b.d_res, ms,
-                              !fused_max, p->h_slot_dev[slot]));
-  if (tl >= 2) HIP_TRY(hipEventRecord(ev[4], ms));
-  // buffer set b is free once the tail is done (the only cross-stream edge besides solved)
-  if (ss != ms) HIP_TRY(hipEventRecord(b.freed, ms));
+  if (!fused_max) HIP_TRY(rsd::launch_f8_max(b.d_counts, h, b.d_status, ms));
+  if (tl >= 1) HIP_TRY(hipEventRecord(ev[1], ms));
+
+  // this run's tail rides along with the next run's solve (or plan_flush)
+  rsd::TailArgs &ta = p->tail;
+  ta = rsd::TailArgs{};
+  ta.pts = p->d_pts;
+  ta.n = n;
+  ta.H = h;
+  ta.slack = 1;
+  ta.Fsoa = b.d_F;
+  ta.ld = p->ld;
+  ta.counts = b.d_counts;
+  ta.status = b.d_status;
+  ta.thresh = thresh;
+  ta.cand = b.d_cand;
+  ta.ccount = b.d_ccount;
+  ta.cstd = b.d_cstd;
+  ta.cnorm = b.d_cnorm;
+  ta.res = b.d_res;
+  ta.hres = p->h_slot_dev[slot];
+  p->tail_pending = true;
   ++p->runs;
   p->last_H = H;
   p->pending = true;
   return RS_OK;
 }
 
-// Wait for the last run.  Accessors below then read its buffer set synchronously.
+// Complete the last run (its pending tail) and wait.  Accessors below then read its buffer
+// set synchronously.
 static int plan_wait(rs_f8_plan *p) {
   if (p->runs == 0) return fail(RS_EINVAL, "no run has been issued on this plan");
-  return p->pending ? plan_sync(p) : RS_OK;
+  return p->pending ? plan_flush(p) : RS_OK;
 }
 
 extern "C" int rs_f8_plan_result(rs_f8_plan *p, rs_f8_result *out, int64_t *inliers, int64_t cap,
@@ -552,9 +562,9 @@ extern "C" int rs_f8_plan_kernel_avg(rs_f8_plan *p, int64_t last_n, double *scor
   if (!p) return fail(RS_EINVAL, "null plan");
   int st = plan_wait(p);
   if (st) return st;
+  if (p->timing < 1) return fail(RS_EINVAL, "timing events are disabled (RSAMD_TIMING=0)");
   const int64_t k = std::max<int64_t>(
       1, std::min<int64_t>({last_n, p->runs, static_cast<int64_t>(rs_f8_plan::kEvRing)}));
-  if (p->timing < 1) return fail(RS_EINVAL, "timing events are disabled (RSAMD_TIMING=0)");
   double sa = 0, sb = 0, sc = 0;
   int64_t nt = 0;
   for (int64_t r = p->runs - k; r < p->runs; ++r) {
@@ -562,17 +572,17 @@ extern "C" int rs_f8_plan_kernel_avg(rs_f8_plan *p, int64_t last_n, double *scor
     ++nt;
     hipEvent_t *ev = p->ring[r % rs_f8_plan::kEvRing];
     float a = 0, b = 0, t = 0;
-    HIP_TRY(hipEventElapsedTime(&b, ev[2], ev[3]));  // count (main stream)
+    HIP_TRY(hipEventElapsedTime(&b, ev[0], ev[1]));  // counting kernel
     if (p->timing >= 2) {
-      HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));  // solve (side stream)
-      HIP_TRY(hipEventElapsedTime(&t, ev[0], ev[4]));  // solve start .. tail end
+      HIP_TRY(hipEventElapsedTime(&a, ev[2], ev[3]));  // previous tail + this solve
+      HIP_TRY(hipEventElapsedTime(&t, ev[2], ev[1]));  // tail+solve start .. count end
     }
     sa += a;
     sb += b;
     sc += t;
   }
-  // solve / whole-run times need RSAMD_TIMING=2; reported as -1 otherwise
   if (nt == 0) return fail(RS_EINVAL, "no timed run among the requested ones");
+  // the solve / whole-run times need timing level 2; reported as -1 otherwise
   if (solve_ms) *solve_ms = p->timing >= 2 ? sa / nt : -1.0;
   if (score_ms) *score_ms = sb / nt;
   if (total_ms) *total_ms = p->timing >= 2 ? sc / nt : -1.0;
