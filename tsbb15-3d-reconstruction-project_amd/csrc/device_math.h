@@ -50,6 +50,12 @@ struct GuardY {
   double thr2_px;
 };
 
+// Per-hypothesis decision (k_f8_count32x, DEC = 3): constants live with each model (G4,
+// written by the solve); only the float64 re-test threshold is global.
+struct GuardW {
+  double thr2_px;
+};
+
 // Folded plain decision (k_f8_count32x, DEC = 2): sure inlier G < -h, ambiguous |G| <= h.
 struct GuardF {
   float K1, K0, alpha, pad_;

@@ -47,6 +47,8 @@ struct SolveArgs {
   float *F32soa; // unit-frame fp32 models (null: fp64 counting)
   Frame frame;
   int *gdone;    // per-group finish counters zeroed (fused c*)
+  float4 *G4;    // per-hypothesis decision constants (k_f8_count32x DEC 3), may be null
+  double gT, gDe, gDn;  // their inputs: (t/s)^2 and the fp32 error bounds of e and m
 };
 
 // One run's selection tail (candidates, reference statistics, replay, S_RANSAC).
@@ -85,7 +87,7 @@ hipError_t launch_f8_count32x(const float4 *pts32, const Pt *pts, int n, int H,
                               const float *F32soa, const double *Fsoa, int64_t ld, int waves,
                               const Guard &g, int *counts, hipStream_t s, int blk = 8,
                               bool prefetch = true, int *gdone = nullptr,
-                              int *status = nullptr);
+                              int *status = nullptr, const float4 *G4 = nullptr);
 hipError_t launch_f8_count(const Pt *pts, int n, int H, const double *Fsoa, int64_t ld,
                            int chunk, double thr2, int *counts, hipStream_t s);
 // Selection tail: c* (k_f8_max, unless the counting kernel fused it), candidates + reference

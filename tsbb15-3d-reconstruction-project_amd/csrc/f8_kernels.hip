@@ -133,6 +133,21 @@ __device__ __forceinline__ void solve_one(const SolveArgs &a, int h) {
     const double kap = 1.0 / mx;  // F = 0 or non-finite -> NaN model, counts 0 on both paths
 #pragma unroll
     for (int k = 0; k < 9; ++k) F32soa[k * ld + h] = static_cast<float>(Ft[k] * kap);
+    if (a.G4) {
+      // k_f8_count32x DEC 3 constants, AM-GM split point c = t~ sqrt(m at the frame centre)
+      // (any c > 0 is rigorous; this one keeps the band near the exact-|e| band)
+      const double u = 0x1p-24, T = a.gT, De = a.gDe, Dn = a.gDn;
+      const double f02 = Ft[2] * kap, f12 = Ft[5] * kap, f20 = Ft[6] * kap, f21 = Ft[7] * kap;
+      const double mc = fmin(f02 * f02 + f12 * f12, f20 * f20 + f21 * f21);
+      const double c = fmax(sqrt(T * fmax(mc, 1e-12)), 100.0 * De);
+      const double r = De / c;
+      const double alpha = T * (1.0 - u) / ((1.0 + u) * (1.0 + r)) * (1.0 - 4.0 * u);
+      const double beta = T * (1.0 + u) / ((1.0 - u) * (1.0 - r)) * (1.0 + 4.0 * u);
+      const double ki = 1.02 * (De * c + De * De + T * Dn) / (1.0 + r) + 1e-30;
+      const double ko = 1.02 * (T * Dn + De * c) / (1.0 - r) + 1e-30;
+      a.G4[h] = make_float4(static_cast<float>(ki), -static_cast<float>(ko),
+                            static_cast<float>(alpha), static_cast<float>(beta));
+    }
   }
 }
 
@@ -366,6 +381,19 @@ __device__ __forceinline__ void group_done_max(int *counts, int *gdone, int *sta
 // c* is fused in (gdone != nullptr): every segment adds its length to its group's counter
 // gdone[grp] after its count atomics; the segment that completes the group (total npad)
 // reads the 64 final counts and issues one atomicMax(status[0]) -- no k_f8_max pass.
+//
+// Variant DEC = 3 (default) bounds 2De|e_c| <= De (e_c^2/c + c) (AM-GM, any c > 0) with a
+// per-hypothesis c (k_f8_solve: c = t~ sqrt(m at the frame centre), r = De/c), so both sides
+// are one packed fma of the broadcast e and one packed multiply of the broadcast m:
+//   sure inlier  fl(e^2 + ki) < fl(alpha m):  e_c^2 + ki < alpha m_c (1+u)/(1-u), and with
+//     alpha <= T (1-u)/((1+u)(1+r)), ki >= (De c + De^2 + T Dn)/(1+r):
+//     e^2 <= e_c^2 (1+r) + De c + De^2 < T m_c - T Dn <= T m;
+//   sure outlier fl(e^2 - ko) > fl(beta m) (>= 0):  e_c^2 > ko + beta m_c (1-u)/(1+u), and
+//     with beta >= T (1+u)/((1-u)(1-r)), ko >= (T Dn + De c)/(1-r):
+//     e^2 >= e_c^2 (1-r) - De c > T m_c + T Dn >= T m.
+// (ki, -ko, alpha, beta) are one float4 per hypothesis (G4); ambiguous = XOR of the ballots
+// (fl(e^2 - ko) <= fl(e^2 + ki) and alpha <= beta).  6 pk + 4 fma + min + 2 pk + 2 cmp + 1 add
+// = 16 VALU.
 template <int BLK, bool PREFETCH, int DEC, class Guard>
 __global__ __launch_bounds__(256) void k_f8_count32x(const float4 *__restrict__ pts32,
                                                      const Pt *__restrict__ pts, int n, int H,
@@ -374,7 +402,8 @@ __global__ __launch_bounds__(256) void k_f8_count32x(const float4 *__restrict__ 
                                                      int64_t ld, int64_t per_wave, Guard g,
                                                      int *__restrict__ counts,
                                                      int *__restrict__ gdone,
-                                                     int *__restrict__ status) {
+                                                     int *__restrict__ status,
+                                                     const float4 *__restrict__ G4) {
 #pragma clang fp contract(off)
   typedef float f2 __attribute__((ext_vector_type(2)));
   const int lane = threadIdx.x & 63;
@@ -401,6 +430,12 @@ __global__ __launch_bounds__(256) void k_f8_count32x(const float4 *__restrict__ 
     for (int k = 0; k < 9; ++k) f[k] = F32soa[k * ld + hl];
     const f2 fa = {f[0], f[0]}, fb = {f[1], f[3]}, fc = {f[2], f[6]};
     const f2 fd = {f[3], f[1]}, fe = {f[4], f[4]}, ff = {f[5], f[7]};
+    f2 kw = {0.f, 0.f}, abw = {0.f, 0.f};
+    if constexpr (DEC == 3) {
+      const float4 q = G4[hl];
+      kw = f2{q.x, q.y};
+      abw = f2{q.z, q.w};
+    }
     // one block of BLK points starting at i: fast fp32 decisions, then the float64 re-test of
     // the ambiguous (lane, point) pairs
     auto block = [&](const float4 (&cur)[BLK], int i, int cnt) -> int {
@@ -431,12 +466,17 @@ __global__ __launch_bounds__(256) void k_f8_count32x(const float4 *__restrict__ 
           const float h2 = fmaf(g.delta, m, h);
           bi = __ballot(G < -h);
           bl = __ballot(G <= h2);
-        } else {
+        } else if constexpr (DEC == 2) {
           const float R = g.alpha * m;
           const float G = fmaf(e, e, -R);
           const float h = fmaf(fabsf(e), g.K1, g.K0);
           bi = __ballot(G < -h);
           bl = __ballot(fabsf(G) <= h);
+        } else {
+          const f2 PQ = __builtin_elementwise_fma(f2{e, e}, f2{e, e}, kw);
+          const f2 RS = f2{m, m} * abw;
+          bi = __ballot(PQ.x < RS.x);
+          bl = __ballot(PQ.y <= RS.y);
         }
         if constexpr (DEC == 2) {
           amb[k] = bl;
@@ -457,6 +497,7 @@ __global__ __launch_bounds__(256) void k_f8_count32x(const float4 *__restrict__ 
       unsigned long long any = 0ull;
 #pragma unroll
       for (int k = 0; k < BLK; ++k) any |= amb[k];
+      if (g.thr2_px < 0.0) any = 0ull;  // diagnostic only (RSAMD_NORECHECK): counts wrong
       if (any != 0ull) {
         double fdd[9];
 #pragma unroll
@@ -1074,9 +1115,11 @@ template <class Guard>
 hipError_t launch_f8_count32x(const float4 *pts32, const Pt *pts, int n, int H,
                               const float *F32soa, const double *Fsoa, int64_t ld, int waves,
                               const Guard &g, int *counts, hipStream_t s, int blk,
-                              bool prefetch, int *gdone, int *status) {
-  constexpr int D = std::is_same<Guard, GuardX>::value ? 0
-                   : std::is_same<Guard, GuardY>::value ? 1 : 2;
+                              bool prefetch, int *gdone, int *status, const float4 *G4) {
+  constexpr int D = std::is_same<Guard, GuardX>::value   ? 0
+                    : std::is_same<Guard, GuardY>::value ? 1
+                    : std::is_same<Guard, GuardF>::value ? 2
+                                                         : 3;
   blk = blk == 8 ? 8 : 4;
   const int64_t npad = (n + blk - 1) / blk * blk;
   const int64_t total = static_cast<int64_t>((H + 63) / 64) * npad;
@@ -1087,31 +1130,35 @@ hipError_t launch_f8_count32x(const float4 *pts32, const Pt *pts, int n, int H,
   const dim3 grid(static_cast<unsigned>((W + 3) / 4));
   if (blk == 8 && prefetch)
     hipLaunchKernelGGL((k_f8_count32x<8, true, D, Guard>), grid, dim3(256), 0, s, pts32, pts, n, H,
-                       F32soa, Fsoa, ld, per, g, counts, gdone, status);
+                       F32soa, Fsoa, ld, per, g, counts, gdone, status, G4);
   else if (blk == 8)
     hipLaunchKernelGGL((k_f8_count32x<8, false, D, Guard>), grid, dim3(256), 0, s, pts32, pts, n, H,
-                       F32soa, Fsoa, ld, per, g, counts, gdone, status);
+                       F32soa, Fsoa, ld, per, g, counts, gdone, status, G4);
   else if (prefetch)
     hipLaunchKernelGGL((k_f8_count32x<4, true, D, Guard>), grid, dim3(256), 0, s, pts32, pts, n, H,
-                       F32soa, Fsoa, ld, per, g, counts, gdone, status);
+                       F32soa, Fsoa, ld, per, g, counts, gdone, status, G4);
   else
     hipLaunchKernelGGL((k_f8_count32x<4, false, D, Guard>), grid, dim3(256), 0, s, pts32, pts, n, H,
-                       F32soa, Fsoa, ld, per, g, counts, gdone, status);
+                       F32soa, Fsoa, ld, per, g, counts, gdone, status, G4);
   return hipGetLastError();
 }
 
 template hipError_t launch_f8_count32x<GuardX>(const float4 *, const Pt *, int, int,
                                                const float *, const double *, int64_t, int,
                                                const GuardX &, int *, hipStream_t, int, bool,
-                                               int *, int *);
+                                               int *, int *, const float4 *);
 template hipError_t launch_f8_count32x<GuardY>(const float4 *, const Pt *, int, int,
                                                const float *, const double *, int64_t, int,
                                                const GuardY &, int *, hipStream_t, int, bool,
-                                               int *, int *);
+                                               int *, int *, const float4 *);
+template hipError_t launch_f8_count32x<GuardW>(const float4 *, const Pt *, int, int,
+                                               const float *, const double *, int64_t, int,
+                                               const GuardW &, int *, hipStream_t, int, bool,
+                                               int *, int *, const float4 *);
 template hipError_t launch_f8_count32x<GuardF>(const float4 *, const Pt *, int, int,
                                                const float *, const double *, int64_t, int,
                                                const GuardF &, int *, hipStream_t, int, bool,
-                                               int *, int *);
+                                               int *, int *, const float4 *);
 
 int select_per_block(int H) { return (H + kSelectBlocks - 1) / kSelectBlocks; }
 int select_blocks(int H) {

@@ -43,6 +43,7 @@ struct RunBufs {
   double *d_cstd = nullptr, *d_cnorm = nullptr;
   rsd::F8DevResult *d_res = nullptr;
   int *d_gdone = nullptr;      // per-group finish counters (fused c* in k_f8_count32x)
+  float4 *d_G4 = nullptr;      // per-hypothesis decision constants (k_f8_count32x DEC 3)
 };
 
 // Absolute error bounds of the fp32 test in the unit frame (|x~| <= R); derivation in
@@ -99,6 +100,8 @@ rsd::GuardX guard_pair(const rsd::Frame &fr, double thresh) {
   return g;
 }
 
+int env_int(const char *name, int dflt);
+
 // Plain-op decision constants (derivation above k_f8_count32x, DEC = 1).
 rsd::GuardY guard_plain(const rsd::Frame &fr, double thresh) {
   const Bounds b = fp32_bounds(fr, thresh);
@@ -111,6 +114,7 @@ rsd::GuardY guard_plain(const rsd::Frame &fr, double thresh) {
   const double alpha = g.alpha;  // the fp32 value the kernel multiplies with
   g.delta = static_cast<float>(1.02 * (T - alpha * (1.0 - u)) / c1 + tiny);
   g.thr2_px = thresh * thresh;
+  if (env_int("RSAMD_NORECHECK", 0)) g.thr2_px = -1.0;  // timing diagnostic: no fp64 re-test
   return g;
 }
 
@@ -162,8 +166,9 @@ struct rs_f8_plan {
   bool use_fp32 = true;       // RSAMD_COUNT=fp64 selects the float64 kernel
   bool packed = false;        // RSAMD_COUNT=pk: two hypotheses per lane (v_pk_fma_f32)
   bool pair = true;           // k_f8_count32x (default); RSAMD_COUNT=fp32: k_f8_count32
-  bool plain_dec = true;      // k_f8_count32x with the plain-op decision (default, "y")
+  bool plain_dec = false;     // RSAMD_COUNT=y: k_f8_count32x with the plain-op decision
   bool folded = false;        // RSAMD_COUNT=z: folded plain decision + SALU bit-plane counts
+  bool per_hyp = true;        // per-hypothesis AM-GM decision constants (default, "w")
   bool fuse_max = true;       // RSAMD_FUSEMAX=0: separate k_f8_max pass instead of the fused c*
   // HIP timing events per run (each is a marker packet between kernels): 0 none, 1 around the
   // counting kernel (default; the bench's roofline timing), 2 also the tail+solve launch
@@ -200,6 +205,7 @@ static void plan_free(rs_f8_plan *p) {
     (void)hipFree(b.d_cnorm);
     (void)hipFree(b.d_res);
     (void)hipFree(b.d_gdone);
+    (void)hipFree(b.d_G4);
   }
   for (auto &h : p->h_slot)
     if (h) (void)hipHostFree(h);
@@ -224,11 +230,13 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
   p->chunk_override = env_int("RSAMD_CHUNK", 0);
   if (const char *cm = std::getenv("RSAMD_COUNT")) {
     p->use_fp32 = std::strcmp(cm, "fp64") != 0;
-    p->packed = std::strcmp(cm, "pk") == 0;  // "y" (default), "x", "z", "fp32", "pk", "fp64"
+    p->packed = std::strcmp(cm, "pk") == 0;  // "w" (default), "x", "y", "z", "fp32", "pk", "fp64"
     p->pair = std::strcmp(cm, "x") == 0 || std::strcmp(cm, "y") == 0 ||
               std::strcmp(cm, "z") == 0;
+    p->pair = p->pair || std::strcmp(cm, "w") == 0;
     p->plain_dec = std::strcmp(cm, "y") == 0;
     p->folded = std::strcmp(cm, "z") == 0;
+    p->per_hyp = std::strcmp(cm, "w") == 0;
   }
   p->fuse_max = env_int("RSAMD_FUSEMAX", 1) != 0;
   p->timing = env_int("RSAMD_TIMING", 1);
@@ -262,6 +270,7 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
     ALLOC(b.d_cnorm, sizeof(double) * p->ld);
     ALLOC(b.d_res, res_bytes);
     ALLOC(b.d_gdone, sizeof(int) * (p->ld / 64));
+    ALLOC(b.d_G4, sizeof(float4) * p->ld);
   }
 #undef ALLOC
   for (int k = 0; k < rs_f8_plan::kSlots; ++k) {
@@ -398,6 +407,13 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
   sa.F32soa = fp32 ? b.d_F32 : nullptr;
   sa.frame = fp32 ? p->frame : rsd::Frame{1.0, 0.0, 0.0, 0.0, 0.0};
   sa.gdone = b.d_gdone;
+  if (fp32 && p->pair && p->per_hyp) {
+    const Bounds gb = fp32_bounds(p->frame, thresh);
+    sa.G4 = b.d_G4;
+    sa.gT = gb.thr2;
+    sa.gDe = gb.De;
+    sa.gDn = gb.Dn;
+  }
   if (tl >= 2) HIP_TRY(hipEventRecord(ev[2], ms));
   HIP_TRY(rsd::launch_f8_tail_solve(p->tail_pending ? &p->tail : nullptr, &sa, ms));
   p->tail_pending = false;
@@ -409,7 +425,14 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
     HIP_TRY(rsd::launch_f8_count32p(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
                                     p->pk_waves, guard_packed(p->frame, thresh), b.d_counts, ms,
                                     p->pk_variant));
-  else if (fp32 && p->pair && p->folded)
+  else if (fp32 && p->pair && p->per_hyp) {
+    rsd::GuardW gw{thresh * thresh};
+    if (env_int("RSAMD_NORECHECK", 0)) gw.thr2_px = -1.0;  // timing diagnostic only
+    HIP_TRY(rsd::launch_f8_count32x(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
+                                    p->resident_waves, gw, b.d_counts, ms, p->count_block,
+                                    p->prefetch, fused_max ? b.d_gdone : nullptr, b.d_status,
+                                    b.d_G4));
+  } else if (fp32 && p->pair && p->folded)
     HIP_TRY(rsd::launch_f8_count32x(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
                                     p->resident_waves, guard_folded(p->frame, thresh),
                                     b.d_counts, ms, p->count_block, p->prefetch,
