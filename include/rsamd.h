@@ -174,6 +174,58 @@ int rs_pnp_ransac(rs_ctx *ctx, const double *X_med, const double *y_med, int64_t
                   int64_t *inl_high, int64_t *n_inl_high);
 
 /* ------------------------------------------------------------------------------------------
+ * Two-view geometry after RANSAC (fun.py:91-102, 209-280, 336-369; lab3.py:331-475)
+ * ---------------------------------------------------------------------------------------- */
+
+/* lab3.triangulate_optimal (lab3.py:382-475), batched.  C1, C2: (n_cam, 3, 4) camera pairs;
+ * x1, x2: (2, n) point sets (row 0 = x); cam: (n) int32 pair index per point, or NULL for
+ * pair 0; X_out: (n, 3). */
+int rs_triangulate_optimal(rs_ctx *ctx, const double *C1, const double *C2, int64_t n_cam,
+                           const double *x1, const double *x2, const int32_t *cam, int64_t n,
+                           double *X_out);
+
+/* fun.camera_resectioning (fun.py:260-280, specRQ 181-188), batched: P (B, 3, 4) ->
+ * K (B, 3, 3) upper triangular with K[2,2] = 1, R (B, 3, 3) rotation, t (B, 3). */
+int rs_camera_resectioning(rs_ctx *ctx, const double *P, int64_t B, double *K, double *R,
+                           double *t);
+
+/* E = K^T F K of fun.getEAndK (fun.py:101), batched: F (B, 3, 3); K (B, 3, 3), or a single
+ * (3, 3) K for all when one_k != 0. */
+int rs_essential_from_f(rs_ctx *ctx, const double *K, int32_t one_k, const double *F, int64_t B,
+                        double *E);
+
+/* fun.relative_camera_pose (fun.py:209-258), batched: E (B, 3, 3); y1, y2 (B, 2) the
+ * C-normalised first correspondence (main.py:63).  R (B, 3, 3), t (B, 3); found (B) = 1..4,
+ * the candidate taken, or 0 where the reference returns None (R, t NaN). */
+int rs_relative_camera_pose(rs_ctx *ctx, const double *E, const double *y1, const double *y2,
+                            int64_t B, double *R, double *t, int32_t *found);
+
+/* lab3.fmatrix_cameras (lab3.py:353-380): F (B, 3, 3) -> C1 (B, 3, 4); C2 = [I | 0]. */
+int rs_fmatrix_cameras(rs_ctx *ctx, const double *F, int64_t B, double *C1);
+
+/* lab3.fmatrix_from_cameras (lab3.py:331-351): C1, C2 (B, 3, 4) -> F (B, 3, 3). */
+int rs_fmatrix_from_cameras(rs_ctx *ctx, const double *C1, const double *C2, int64_t B,
+                            double *F);
+
+typedef struct rs_gs_info {
+  double cost_init;       /* 0.5 |r|^2 at the start (cameras of F_RANSAC, optimal points)  */
+  double cost;            /* 0.5 |r|^2 at the end                                          */
+  int32_t iterations;     /* linearisations                                                */
+  int32_t accepted;       /* accepted LM steps                                             */
+  int32_t status;         /* 0 max_iter, 1 converged (ftol/xtol 1e-15), 2 no further decrease */
+  int32_t n;              /* inliers of the pair                                           */
+} rs_gs_info;
+
+/* The gold-standard tail of fun.getFFromLabCode (fun.py:336-369), batched over pairs:
+ * F (B, 3, 3) = F_RANSAC per pair; pl, pr (2, total) the inlier points of all pairs
+ * concatenated, pair b = columns off[b] .. off[b+1]-1 (off has B+1 entries, off[0] = 0).
+ * Minimises lab3.fmatrix_residuals_gs over (C1, X) to convergence (LM, Schur complement).
+ * F_gold (B, 3, 3); optional C1_out (B, 3, 4) and X_out (total, 3); info (B). */
+int rs_gold_standard(rs_ctx *ctx, const double *F, const double *pl, const double *pr,
+                     const int64_t *off, int64_t B, int32_t max_iter, double *F_gold,
+                     double *C1_out, double *X_out, rs_gs_info *info);
+
+/* ------------------------------------------------------------------------------------------
  * Multi-GPU (RCCL over xGMI).  One process per GPU; the unique id travels out of band.
  * ---------------------------------------------------------------------------------------- */
 #define RS_COMM_ID_BYTES 128

@@ -38,6 +38,7 @@ def test_struct_layouts():
     assert ctypes.sizeof(_ffi.F8Result) == 9 * 8 + 2 * 8 + 2 * 8 + 3 * 8
     assert ctypes.sizeof(_ffi.F8Candidate) == 4 * 8 + 9 * 8
     assert ctypes.sizeof(_ffi.PnpResult) == 12 * 8 + 2 * 8
+    assert ctypes.sizeof(_ffi.GsInfo) == 2 * 8 + 4 * 4
 
 
 def test_version_and_errors_without_gpu():

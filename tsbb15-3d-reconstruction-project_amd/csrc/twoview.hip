@@ -1,0 +1,806 @@
+// Two-view geometry after the RANSAC loop, batched on the GPU:
+//
+//   k_triangulate_optimal  lane per point: lab3.triangulate_optimal (lab3.py:382-475)
+//   k_resection            lane per camera: fun.camera_resectioning (fun.py:260-280)
+//   k_essential            lane per pair: E = K^T F K (fun.getEAndK, fun.py:101)
+//   k_relative_pose        lane per pair: fun.relative_camera_pose (fun.py:209-258)
+//   k_fmatrix_cameras / k_fmatrix_from_cameras: lab3.py:353-380 / 331-351
+//   k_gold_standard        workgroup per pair: the gold-standard tail of fun.getFFromLabCode
+//                          (fun.py:336-369) -- cameras from F_RANSAC, optimal triangulation of
+//                          the inliers, least squares on lab3.fmatrix_residuals_gs
+//                          (lab3.py:228-266) over (C1, X), F from the refined cameras.  The
+//                          least-squares step is Levenberg-Marquardt run to convergence with
+//                          the 3x3 point blocks eliminated (Schur complement on the 12 camera
+//                          parameters); see oracle/twoview_ref.gold_standard_lm for why the
+//                          reference's scipy TRF end point is not the target.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <initializer_list>
+#include <vector>
+
+#include "common.h"
+#include "ctx.h"
+#include "device_math.h"
+#include "twoview_math.h"
+
+namespace rsd {
+
+__global__ void k_triangulate_optimal(const double *__restrict__ C1s,
+                                      const double *__restrict__ C2s,
+                                      const double *__restrict__ x1, const double *__restrict__ x2,
+                                      const int32_t *__restrict__ cam, int64_t n,
+                                      double *__restrict__ X) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int k = cam ? cam[i] : 0;
+  double C1[12], C2[12], Y[3];
+#pragma unroll
+  for (int q = 0; q < 12; ++q) {
+    C1[q] = C1s[12 * k + q];
+    C2[q] = C2s[12 * k + q];
+  }
+  triangulate_optimal(C1, C2, x1[i], x1[n + i], x2[i], x2[n + i], Y);
+  X[3 * i + 0] = Y[0];
+  X[3 * i + 1] = Y[1];
+  X[3 * i + 2] = Y[2];
+}
+
+// fun.camera_resectioning: P = lambda K [R | t], K upper triangular with positive diagonal
+// and K[2,2] = 1, R a rotation.  The decomposition is unique, so it is computed directly
+// (RQ by twice-applied Gram-Schmidt from the last row, then the sign of det A), without the
+// LAPACK sign conventions specRQ (fun.py:181-188) and the D fix-up (fun.py:267-279) undo.
+__global__ void k_resection(const double *__restrict__ P, int64_t B, double *__restrict__ K,
+                            double *__restrict__ R, double *__restrict__ t) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  double a[3][3], b[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) a[r][c] = P[12 * i + 4 * r + c];
+    b[r] = P[12 * i + 4 * r + 3];
+  }
+  double U[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}}, Q[3][3];
+  for (int r = 2; r >= 0; --r) {
+    double w[3] = {a[r][0], a[r][1], a[r][2]};
+    for (int pass = 0; pass < 2; ++pass)
+      for (int k = r + 1; k < 3; ++k) {
+        const double p = w[0] * Q[k][0] + w[1] * Q[k][1] + w[2] * Q[k][2];
+        U[r][k] += p;
+        w[0] -= p * Q[k][0];
+        w[1] -= p * Q[k][1];
+        w[2] -= p * Q[k][2];
+      }
+    const double nrm = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    U[r][r] = nrm;
+    Q[r][0] = w[0] / nrm;
+    Q[r][1] = w[1] / nrm;
+    Q[r][2] = w[2] / nrm;
+  }
+  const double detA = a[0][0] * (a[1][1] * a[2][2] - a[1][2] * a[2][1]) -
+                      a[0][1] * (a[1][0] * a[2][2] - a[1][2] * a[2][0]) +
+                      a[0][2] * (a[1][0] * a[2][1] - a[1][1] * a[2][0]);
+  const double s = detA < 0.0 ? -1.0 : 1.0;
+  // t = s U^-1 b (back substitution)
+  double y[3];
+  y[2] = b[2] / U[2][2];
+  y[1] = (b[1] - U[1][2] * y[2]) / U[1][1];
+  y[0] = (b[0] - U[0][1] * y[1] - U[0][2] * y[2]) / U[0][0];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      K[9 * i + 3 * r + c] = U[r][c] / U[2][2];
+      R[9 * i + 3 * r + c] = s * Q[r][c];
+    }
+    t[3 * i + r] = s * y[r];
+  }
+}
+
+__global__ void k_essential(const double *__restrict__ K, int k_stride,
+                            const double *__restrict__ F, int64_t B, double *__restrict__ E) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  double k[9], f[9], kt[9], T[9], e[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) {
+    k[q] = K[k_stride * i + q];
+    f[q] = F[9 * i + q];
+  }
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) kt[3 * r + c] = k[3 * c + r];
+  mul33(kt, f, T);
+  mul33(T, k, e);
+#pragma unroll
+  for (int q = 0; q < 9; ++q) E[9 * i + q] = e[q];
+}
+
+// fun.relative_camera_pose: specSVD(E) (U, V with det +1), candidates
+// (V W U^T, v3), (V W^T U^T, v3), (V W U^T, -v3), (V W^T U^T, -v3), W = [[0,1,0],[-1,0,0],
+// [0,0,1]]; the first whose optimally triangulated first correspondence has positive depth
+// in both cameras wins (found = 1..4), else found = 0 (the reference returns None).  The
+// candidate set does not depend on the SVD's sign / ordering freedom of the two equal
+// singular values, so the pose is the reference's whenever exactly one candidate passes.
+__global__ void k_relative_pose(const double *__restrict__ Es, const double *__restrict__ y1,
+                                const double *__restrict__ y2, int64_t Bn,
+                                double *__restrict__ Rout, double *__restrict__ tout,
+                                int32_t *__restrict__ found) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= Bn) return;
+  double B[9], V[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) B[q] = Es[9 * i + q];
+  svd3_jacobi(B, V);
+  double s[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) s[j] = B[j] * B[j] + B[3 + j] * B[3 + j] + B[6 + j] * B[6 + j];
+  const int m = (s[0] <= s[1] && s[0] <= s[2]) ? 0 : (s[1] <= s[2] ? 1 : 2);
+  int p = m == 0 ? 1 : 0, q = m == 2 ? 1 : 2;
+  if (s[q] > s[p]) {  // descending, as LAPACK
+    const int tmp = p;
+    p = q;
+    q = tmp;
+  }
+  double u1[3], u2[3], u3[3], v1[3], v2[3], v3[3];
+  const double i1 = 1.0 / sqrt(s[p]), i2 = 1.0 / sqrt(s[q]);
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    u1[r] = B[3 * r + p] * i1;
+    u2[r] = B[3 * r + q] * i2;
+    v1[r] = V[3 * r + p];
+    v2[r] = V[3 * r + q];
+  }
+  cross3(u1, u2, u3);
+  cross3(v1, v2, v3);
+  // V W U^T = -v2 u1^T + v1 u2^T + v3 u3^T;  V W^T U^T = v2 u1^T - v1 u2^T + v3 u3^T
+  double Ra[9], Rb[9];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const double base = v3[r] * u3[c];
+      const double x = v1[r] * u2[c] - v2[r] * u1[c];
+      Ra[3 * r + c] = base + x;
+      Rb[3 * r + c] = base - x;
+    }
+  const double I34[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+  int which = 0;
+  double Rw[9], tw[3];
+  for (int k = 0; k < 4 && !which; ++k) {
+    const double *Rk = (k & 1) ? Rb : Ra;
+    const double sg = k < 2 ? 1.0 : -1.0;
+    double C2[12];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      C2[4 * r + 0] = Rk[3 * r + 0];
+      C2[4 * r + 1] = Rk[3 * r + 1];
+      C2[4 * r + 2] = Rk[3 * r + 2];
+      C2[4 * r + 3] = sg * v3[r];
+    }
+    double X[3];
+    triangulate_optimal(I34, C2, y1[2 * i], y1[2 * i + 1], y2[2 * i], y2[2 * i + 1], X);
+    const double z2 = Rk[6] * X[0] + Rk[7] * X[1] + Rk[8] * X[2] + sg * v3[2];
+    if (X[2] > 0.0 && z2 > 0.0) {
+      which = k + 1;
+#pragma unroll
+      for (int q2 = 0; q2 < 9; ++q2) Rw[q2] = Rk[q2];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) tw[r] = sg * v3[r];
+    }
+  }
+  found[i] = which;
+#pragma unroll
+  for (int q2 = 0; q2 < 9; ++q2) Rout[9 * i + q2] = which ? Rw[q2] : __builtin_nan("");
+#pragma unroll
+  for (int r = 0; r < 3; ++r) tout[3 * i + r] = which ? tw[r] : __builtin_nan("");
+}
+
+__global__ void k_fmatrix_cameras(const double *__restrict__ F, int64_t B,
+                                  double *__restrict__ C1) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  double f[9], c[12];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) f[q] = F[9 * i + q];
+  fmatrix_cameras(f, c);
+#pragma unroll
+  for (int q = 0; q < 12; ++q) C1[12 * i + q] = c[q];
+}
+
+__global__ void k_fmatrix_from_cameras(const double *__restrict__ C1s,
+                                       const double *__restrict__ C2s, int64_t B,
+                                       double *__restrict__ F) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  double a[12], b[12], f[9];
+#pragma unroll
+  for (int q = 0; q < 12; ++q) {
+    a[q] = C1s[12 * i + q];
+    b[q] = C2s[12 * i + q];
+  }
+  fmatrix_from_cameras(a, b, f);
+#pragma unroll
+  for (int q = 0; q < 9; ++q) F[9 * i + q] = f[q];
+}
+
+// ----------------------------------------------------------------------------------------
+// Gold standard (fun.py:336-369), one workgroup per pair.
+// ----------------------------------------------------------------------------------------
+constexpr int kGsT = 256;
+constexpr int kGsW = kGsT / 64;
+constexpr int kPerPt = 45;  // W (12x3), V (3x3 upper: 6), gx (3)
+
+// Index of (r, c), r <= c, in a packed upper-triangular 12x12.
+__device__ __forceinline__ int up12(int r, int c) { return r * 12 - (r * (r - 1)) / 2 + (c - r); }
+
+template <int K>
+__device__ __forceinline__ void block_reduce(double (&v)[K], double *scratch, double *out) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    double x = v[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    if (lane == 0) scratch[w * K + k] = x;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < K; k += kGsT) {
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < kGsW; ++q) s += scratch[q * K + k];
+    out[k] = s;
+  }
+  __syncthreads();
+}
+
+// Residuals of lab3.fmatrix_residuals_gs for one point and their Jacobians:
+// a0 / a1 (12) = d r0 / d C1, d r1 / d C1;  Bj (4x3) = d r / d X.
+__device__ __forceinline__ void gs_point(const double (&C)[12], const double *X, double plx,
+                                         double ply, double prx, double pry, double (&r)[4],
+                                         double (&a0)[12], double (&a1)[12], double (&Bj)[12]) {
+  const double xh[4] = {X[0], X[1], X[2], 1.0};
+  const double u = C[0] * xh[0] + C[1] * xh[1] + C[2] * xh[2] + C[3];
+  const double v = C[4] * xh[0] + C[5] * xh[1] + C[6] * xh[2] + C[7];
+  const double w = C[8] * xh[0] + C[9] * xh[1] + C[10] * xh[2] + C[11];
+  const double iw = 1.0 / w, iw2 = iw * iw;
+  r[0] = plx - u * iw;
+  r[1] = ply - v * iw;
+  r[2] = prx - X[0] / X[2];
+  r[3] = pry - X[1] / X[2];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    a0[k] = -xh[k] * iw;
+    a0[4 + k] = 0.0;
+    a0[8 + k] = xh[k] * u * iw2;
+    a1[k] = 0.0;
+    a1[4 + k] = -xh[k] * iw;
+    a1[8 + k] = xh[k] * v * iw2;
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    Bj[k] = -(C[k] * w - u * C[8 + k]) * iw2;
+    Bj[3 + k] = -(C[4 + k] * w - v * C[8 + k]) * iw2;
+  }
+  const double iz = 1.0 / X[2];
+  Bj[6] = -iz;
+  Bj[7] = 0.0;
+  Bj[8] = X[0] * iz * iz;
+  Bj[9] = 0.0;
+  Bj[10] = -iz;
+  Bj[11] = X[1] * iz * iz;
+}
+
+__device__ __forceinline__ double gs_cost_point(const double (&C)[12], const double *X, double plx,
+                                                double ply, double prx, double pry) {
+  const double u = C[0] * X[0] + C[1] * X[1] + C[2] * X[2] + C[3];
+  const double v = C[4] * X[0] + C[5] * X[1] + C[6] * X[2] + C[7];
+  const double w = C[8] * X[0] + C[9] * X[1] + C[10] * X[2] + C[11];
+  const double r0 = plx - u / w, r1 = ply - v / w;
+  const double r2 = prx - X[0] / X[2], r3 = pry - X[1] / X[2];
+  return r0 * r0 + r1 * r1 + r2 * r2 + r3 * r3;
+}
+
+// Inverse of the damped point block V + lam diag(V) (packed upper 6) -> packed upper 6.
+__device__ __forceinline__ void inv_sym3(const double *V, double lam, double (&Vi)[6]) {
+  const double a = V[0] * (1 + lam), b = V[1], c = V[2], d = V[3] * (1 + lam), e = V[4],
+               f = V[5] * (1 + lam);
+  const double c00 = d * f - e * e, c01 = c * e - b * f, c02 = b * e - c * d;
+  const double c11 = a * f - c * c, c12 = b * c - a * e, c22 = a * d - b * b;
+  const double id = 1.0 / (a * c00 + b * c01 + c * c02);
+  Vi[0] = c00 * id;
+  Vi[1] = c01 * id;
+  Vi[2] = c02 * id;
+  Vi[3] = c11 * id;
+  Vi[4] = c12 * id;
+  Vi[5] = c22 * id;
+}
+
+__device__ __forceinline__ void symv3(const double (&S)[6], const double *x, double *y) {
+  y[0] = S[0] * x[0] + S[1] * x[1] + S[2] * x[2];
+  y[1] = S[1] * x[0] + S[3] * x[1] + S[4] * x[2];
+  y[2] = S[2] * x[0] + S[4] * x[1] + S[5] * x[2];
+}
+
+struct GsInfo {  // == rs_gs_info
+  double cost_init;
+  double cost;
+  int32_t iterations;
+  int32_t accepted;
+  int32_t status;
+  int32_t n;
+};
+
+__global__ __launch_bounds__(kGsT) void k_gold_standard(
+    const double *__restrict__ Fin, const double *__restrict__ pl, const double *__restrict__ pr,
+    int64_t total, const int64_t *__restrict__ off, int max_iter, double *__restrict__ Xb,
+    double *__restrict__ Xc, double *__restrict__ Wb, double *__restrict__ Fout,
+    double *__restrict__ C1out, GsInfo *__restrict__ info) {
+  __shared__ double red[kGsW * 94];
+  __shared__ double sU[78], sgc[12], sres[94], sC[12], sdc[12];
+  __shared__ double s_lam, s_nu, s_cost, s_cost0;
+  __shared__ int s_state, s_it, s_acc, s_status;
+  const int tid = threadIdx.x;
+  const int64_t j0 = off[blockIdx.x];
+  const int n = static_cast<int>(off[blockIdx.x + 1] - j0);
+  const double *plx = pl + j0, *ply = pl + total + j0;
+  const double *prx = pr + j0, *pry = pr + total + j0;
+  double *X = Xb + 3 * j0, *XN = Xc + 3 * j0, *W = Wb + kPerPt * j0;
+  const double I34[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+
+  if (tid == 0) {
+    double f[9], c[12];
+    for (int q = 0; q < 9; ++q) f[q] = Fin[9 * blockIdx.x + q];
+    fmatrix_cameras(f, c);
+    for (int q = 0; q < 12; ++q) sC[q] = c[q];
+    s_lam = 1e-3;
+    s_nu = 2.0;
+    s_it = 0;
+    s_acc = 0;
+    s_status = 0;
+  }
+  __syncthreads();
+  double C[12];
+#pragma unroll
+  for (int q = 0; q < 12; ++q) C[q] = sC[q];
+  for (int j = tid; j < n; j += kGsT)
+    triangulate_optimal(C, I34, plx[j], ply[j], prx[j], pry[j], X + 3 * j);
+  __syncthreads();
+
+  bool relinearize = true;
+  for (;;) {
+    if (relinearize) {
+      // ---- linearisation at (C, X): U (78), gc (12), cost; W, V, gx per point ----
+      double acc[91];
+#pragma unroll
+      for (int k = 0; k < 91; ++k) acc[k] = 0.0;
+      for (int j = tid; j < n; j += kGsT) {
+        double r[4], a0[12], a1[12], Bj[12];
+        gs_point(C, X + 3 * j, plx[j], ply[j], prx[j], pry[j], r, a0, a1, Bj);
+#pragma unroll
+        for (int p = 0; p < 12; ++p)
+#pragma unroll
+          for (int q = p; q < 12; ++q) acc[up12(p, q)] += a0[p] * a0[q] + a1[p] * a1[q];
+#pragma unroll
+        for (int p = 0; p < 12; ++p) acc[78 + p] += a0[p] * r[0] + a1[p] * r[1];
+        acc[90] += r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
+        double *w = W + kPerPt * j;
+#pragma unroll
+        for (int p = 0; p < 12; ++p)
+#pragma unroll
+          for (int k = 0; k < 3; ++k) w[3 * p + k] = a0[p] * Bj[k] + a1[p] * Bj[3 + k];
+        int q = 36;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+          for (int l = k; l < 3; ++l)
+            w[q++] = Bj[k] * Bj[l] + Bj[3 + k] * Bj[3 + l] + Bj[6 + k] * Bj[6 + l] +
+                     Bj[9 + k] * Bj[9 + l];
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          w[42 + k] = Bj[k] * r[0] + Bj[3 + k] * r[1] + Bj[6 + k] * r[2] + Bj[9 + k] * r[3];
+      }
+      block_reduce<91>(acc, red, sres);
+      if (tid == 0) {
+        for (int k = 0; k < 78; ++k) sU[k] = sres[k];
+        for (int k = 0; k < 12; ++k) sgc[k] = sres[78 + k];
+        s_cost = 0.5 * sres[90];
+        if (s_it == 0) s_cost0 = s_cost;
+        s_it += 1;
+      }
+      __syncthreads();
+      relinearize = false;
+    }
+    const double lam = s_lam;
+    // ---- Schur complement on the camera block ----
+    {
+      double acc[90];
+#pragma unroll
+      for (int k = 0; k < 90; ++k) acc[k] = 0.0;
+      for (int j = tid; j < n; j += kGsT) {
+        const double *w = W + kPerPt * j;
+        double Vi[6];
+        inv_sym3(w + 36, lam, Vi);
+        double wv[12][3];
+#pragma unroll
+        for (int p = 0; p < 12; ++p) symv3(Vi, w + 3 * p, wv[p]);
+#pragma unroll
+        for (int p = 0; p < 12; ++p) {
+#pragma unroll
+          for (int q = p; q < 12; ++q)
+            acc[up12(p, q)] += wv[p][0] * w[3 * q] + wv[p][1] * w[3 * q + 1] + wv[p][2] * w[3 * q + 2];
+          acc[78 + p] += wv[p][0] * w[42] + wv[p][1] * w[43] + wv[p][2] * w[44];
+        }
+      }
+      block_reduce<90>(acc, red, sres);
+    }
+    if (tid == 0) {
+      // S = U + lam diag(U) - sum W Vi W^T;  rhs = -gc + sum W Vi gx;  Cholesky
+      double S[12][12], y[12];
+      for (int p = 0; p < 12; ++p)
+        for (int q = p; q < 12; ++q) {
+          double v = sU[up12(p, q)] - sres[up12(p, q)];
+          if (p == q) v += lam * sU[up12(p, p)];
+          S[p][q] = v;
+          S[q][p] = v;
+        }
+      for (int p = 0; p < 12; ++p) y[p] = -sgc[p] + sres[78 + p];
+      bool ok = true;
+      for (int k = 0; k < 12 && ok; ++k) {
+        double d = S[k][k];
+        for (int m = 0; m < k; ++m) d -= S[k][m] * S[k][m];
+        if (!(d > 0.0)) {
+          ok = false;
+          break;
+        }
+        d = sqrt(d);
+        S[k][k] = d;
+        for (int i = k + 1; i < 12; ++i) {
+          double v = S[i][k];
+          for (int m = 0; m < k; ++m) v -= S[i][m] * S[k][m];
+          S[i][k] = v / d;
+        }
+      }
+      if (ok) {
+        for (int i = 0; i < 12; ++i) {
+          double v = y[i];
+          for (int m = 0; m < i; ++m) v -= S[i][m] * y[m];
+          y[i] = v / S[i][i];
+        }
+        for (int i = 11; i >= 0; --i) {
+          double v = y[i];
+          for (int m = i + 1; m < 12; ++m) v -= S[m][i] * y[m];
+          y[i] = v / S[i][i];
+        }
+      }
+      for (int p = 0; p < 12; ++p) sdc[p] = ok ? y[p] : 0.0;
+      s_state = ok ? 0 : 1;
+    }
+    __syncthreads();
+    bool accepted = false, stop = false;
+    if (s_state == 0) {
+      // ---- point steps, candidate cost, predicted reduction, step / parameter norms ----
+      double dc[12], Cn[12];
+#pragma unroll
+      for (int p = 0; p < 12; ++p) {
+        dc[p] = sdc[p];
+        Cn[p] = C[p] + dc[p];
+      }
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};  // cost_n*2, x-part of pred*2, |dx|^2, |X|^2
+      for (int j = tid; j < n; j += kGsT) {
+        const double *w = W + kPerPt * j;
+        double Vi[6];
+        inv_sym3(w + 36, lam, Vi);
+        double g[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          double v = -w[42 + k];
+#pragma unroll
+          for (int p = 0; p < 12; ++p) v -= w[3 * p + k] * dc[p];
+          g[k] = v;
+        }
+        double dx[3];
+        symv3(Vi, g, dx);
+        const double *x = X + 3 * j;
+        double xn[3] = {x[0] + dx[0], x[1] + dx[1], x[2] + dx[2]};
+        XN[3 * j + 0] = xn[0];
+        XN[3 * j + 1] = xn[1];
+        XN[3 * j + 2] = xn[2];
+        acc[0] += gs_cost_point(Cn, xn, plx[j], ply[j], prx[j], pry[j]);
+        const double dv0 = w[36], dv1 = w[39], dv2 = w[41];
+        acc[1] += lam * (dx[0] * dv0 * dx[0] + dx[1] * dv1 * dx[1] + dx[2] * dv2 * dx[2]) -
+                  (dx[0] * w[42] + dx[1] * w[43] + dx[2] * w[44]);
+        acc[2] += dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2];
+        acc[3] += x[0] * x[0] + x[1] * x[1] + x[2] * x[2];
+      }
+      block_reduce<4>(acc, red, sres);
+      if (tid == 0) {
+        double pc = 0.0, dn = 0.0, cn = 0.0;
+        for (int p = 0; p < 12; ++p) {
+          pc += lam * dc[p] * sU[up12(p, p)] * dc[p] - dc[p] * sgc[p];
+          dn += dc[p] * dc[p];
+          cn += C[p] * C[p];
+        }
+        const double pred = 0.5 * (pc + sres[1]);
+        const double cost_n = 0.5 * sres[0];
+        const double cost = s_cost;
+        const double rho = pred > 0.0 ? (cost - cost_n) / pred : -1.0;
+        if (cost_n < cost && rho > 0.0) {
+          const bool small_f = (cost - cost_n) <= 1e-15 * cost;
+          const bool small_x = sqrt(dn + sres[2]) <= 1e-15 * (sqrt(cn + sres[3]) + 1e-15);
+          s_state = (small_f || small_x) ? 3 : 2;
+          s_acc += 1;
+          s_cost = cost_n;
+          const double t = 2.0 * rho - 1.0;
+          const double f = 1.0 - t * t * t;
+          s_lam = lam * (f > 1.0 / 3.0 ? f : 1.0 / 3.0);
+          s_nu = 2.0;
+          if (s_state == 3) s_status = 1;
+        } else {
+          s_state = 1;
+        }
+      }
+      __syncthreads();
+    }
+    if (s_state >= 2) {
+      accepted = true;
+      stop = s_state == 3;
+#pragma unroll
+      for (int p = 0; p < 12; ++p) C[p] += sdc[p];
+      for (int j = tid; j < n; j += kGsT) {
+        X[3 * j + 0] = XN[3 * j + 0];
+        X[3 * j + 1] = XN[3 * j + 1];
+        X[3 * j + 2] = XN[3 * j + 2];
+      }
+    } else {  // rejected (or S not positive definite): more damping
+      if (tid == 0) {
+        s_lam = lam * s_nu;
+        s_nu *= 2.0;
+        if (s_lam > 1e32) s_status = 2;
+      }
+    }
+    __syncthreads();
+    if (stop || s_status == 2) break;
+    if (accepted) {
+      if (s_it >= max_iter) break;
+      relinearize = true;
+    }
+  }
+  if (tid == 0) {
+    double f[9];
+    fmatrix_from_cameras(C, I34, f);
+    for (int q = 0; q < 9; ++q) Fout[9 * blockIdx.x + q] = f[q];
+    if (C1out)
+      for (int q = 0; q < 12; ++q) C1out[12 * blockIdx.x + q] = C[q];
+    GsInfo g;
+    g.cost_init = s_cost0;
+    g.cost = s_cost;
+    g.iterations = s_it;
+    g.accepted = s_acc;
+    g.status = s_status;
+    g.n = n;
+    info[blockIdx.x] = g;
+  }
+}
+
+}  // namespace rsd
+
+// ------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------
+using rs::fail;
+using rs::hip_fail;
+
+#define HIP_TRY(expr)                                 \
+  do {                                                \
+    hipError_t e_ = (expr);                           \
+    if (e_ != hipSuccess) return hip_fail(e_, #expr); \
+  } while (0)
+
+namespace {
+
+size_t al(size_t b) { return (b + 255) / 256 * 256; }
+
+// Carve `count` device buffers of the given byte sizes out of the context scratch.
+int carve(rs_ctx *c, std::initializer_list<size_t> sizes, std::vector<char *> &out) {
+  size_t tot = 0;
+  for (size_t s : sizes) tot += al(s);
+  int st = rs::ensure_scratch(c, tot + 256);
+  if (st) return st;
+  char *p = static_cast<char *>(c->scratch);
+  out.clear();
+  for (size_t s : sizes) {
+    out.push_back(p);
+    p += al(s);
+  }
+  return RS_OK;
+}
+
+int grid(int64_t n) { return static_cast<int>((n + 127) / 128); }
+
+}  // namespace
+
+static_assert(sizeof(rsd::GsInfo) == sizeof(rs_gs_info), "rs_gs_info layout");
+
+extern "C" int rs_triangulate_optimal(rs_ctx *c, const double *C1, const double *C2,
+                                      int64_t n_cam, const double *x1, const double *x2,
+                                      const int32_t *cam, int64_t n, double *X_out) {
+  if (!c || !C1 || !C2 || !x1 || !x2 || !X_out) return fail(RS_EINVAL, "null pointer");
+  if (n_cam < 1) return fail(RS_EINVAL, "need at least one camera pair");
+  if (n < 0 || n > (1LL << 28)) return fail(RS_EINVAL, "bad point count");
+  if (n == 0) return RS_OK;
+  if (cam)
+    for (int64_t i = 0; i < n; ++i)
+      if (cam[i] < 0 || cam[i] >= n_cam) return fail(RS_EINVAL, "camera index out of range");
+  HIP_TRY(hipSetDevice(c->device));
+  std::vector<char *> b;
+  const size_t bc = sizeof(double) * 12 * n_cam, bx = sizeof(double) * 2 * n;
+  int st = carve(c, {bc, bc, bx, bx, cam ? sizeof(int32_t) * n : 0, sizeof(double) * 3 * n}, b);
+  if (st) return st;
+  HIP_TRY(hipMemcpyAsync(b[0], C1, bc, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(b[1], C2, bc, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(b[2], x1, bx, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(b[3], x2, bx, hipMemcpyHostToDevice, c->stream));
+  if (cam) HIP_TRY(hipMemcpyAsync(b[4], cam, sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(rsd::k_triangulate_optimal, dim3(grid(n)), dim3(128), 0, c->stream,
+                     reinterpret_cast<double *>(b[0]), reinterpret_cast<double *>(b[1]),
+                     reinterpret_cast<double *>(b[2]), reinterpret_cast<double *>(b[3]),
+                     cam ? reinterpret_cast<int32_t *>(b[4]) : nullptr, n,
+                     reinterpret_cast<double *>(b[5]));
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(X_out, b[5], sizeof(double) * 3 * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return RS_OK;
+}
+
+extern "C" int rs_camera_resectioning(rs_ctx *c, const double *P, int64_t B, double *K,
+                                      double *R, double *t) {
+  if (!c || !P || !K || !R || !t) return fail(RS_EINVAL, "null pointer");
+  if (B < 0 || B > (1LL << 26)) return fail(RS_EINVAL, "bad camera count");
+  if (B == 0) return RS_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  std::vector<char *> b;
+  int st = carve(c, {sizeof(double) * 12 * B, sizeof(double) * 9 * B, sizeof(double) * 9 * B,
+                     sizeof(double) * 3 * B}, b);
+  if (st) return st;
+  HIP_TRY(hipMemcpyAsync(b[0], P, sizeof(double) * 12 * B, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(rsd::k_resection, dim3(grid(B)), dim3(128), 0, c->stream,
+                     reinterpret_cast<double *>(b[0]), B, reinterpret_cast<double *>(b[1]),
+                     reinterpret_cast<double *>(b[2]), reinterpret_cast<double *>(b[3]));
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(K, b[1], sizeof(double) * 9 * B, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(R, b[2], sizeof(double) * 9 * B, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(t, b[3], sizeof(double) * 3 * B, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return RS_OK;
+}
+
+extern "C" int rs_essential_from_f(rs_ctx *c, const double *K, int32_t one_k, const double *F,
+                                   int64_t B, double *E) {
+  if (!c || !K || !F || !E) return fail(RS_EINVAL, "null pointer");
+  if (B < 0 || B > (1LL << 26)) return fail(RS_EINVAL, "bad batch size");
+  if (B == 0) return RS_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  const int64_t nk = one_k ? 1 : B;
+  std::vector<char *> b;
+  int st = carve(c, {sizeof(double) * 9 * nk, sizeof(double) * 9 * B, sizeof(double) * 9 * B}, b);
+  if (st) return st;
+  HIP_TRY(hipMemcpyAsync(b[0], K, sizeof(double) * 9 * nk, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(b[1], F, sizeof(double) * 9 * B, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(rsd::k_essential, dim3(grid(B)), dim3(128), 0, c->stream,
+                     reinterpret_cast<double *>(b[0]), one_k ? 0 : 9,
+                     reinterpret_cast<double *>(b[1]), B, reinterpret_cast<double *>(b[2]));
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(E, b[2], sizeof(double) * 9 * B, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return RS_OK;
+}
+
+extern "C" int rs_relative_camera_pose(rs_ctx *c, const double *E, const double *y1,
+                                       const double *y2, int64_t B, double *R, double *t,
+                                       int32_t *found) {
+  if (!c || !E || !y1 || !y2 || !R || !t || !found) return fail(RS_EINVAL, "null pointer");
+  if (B < 0 || B > (1LL << 26)) return fail(RS_EINVAL, "bad batch size");
+  if (B == 0) return RS_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  std::vector<char *> b;
+  int st = carve(c, {sizeof(double) * 9 * B, sizeof(double) * 2 * B, sizeof(double) * 2 * B,
+                     sizeof(double) * 9 * B, sizeof(double) * 3 * B, sizeof(int32_t) * B}, b);
+  if (st) return st;
+  HIP_TRY(hipMemcpyAsync(b[0], E, sizeof(double) * 9 * B, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(b[1], y1, sizeof(double) * 2 * B, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(b[2], y2, sizeof(double) * 2 * B, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(rsd::k_relative_pose, dim3(grid(B)), dim3(128), 0, c->stream,
+                     reinterpret_cast<double *>(b[0]), reinterpret_cast<double *>(b[1]),
+                     reinterpret_cast<double *>(b[2]), B, reinterpret_cast<double *>(b[3]),
+                     reinterpret_cast<double *>(b[4]), reinterpret_cast<int32_t *>(b[5]));
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(R, b[3], sizeof(double) * 9 * B, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(t, b[4], sizeof(double) * 3 * B, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(found, b[5], sizeof(int32_t) * B, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return RS_OK;
+}
+
+extern "C" int rs_fmatrix_cameras(rs_ctx *c, const double *F, int64_t B, double *C1) {
+  if (!c || !F || !C1) return fail(RS_EINVAL, "null pointer");
+  if (B < 0 || B > (1LL << 26)) return fail(RS_EINVAL, "bad batch size");
+  if (B == 0) return RS_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  std::vector<char *> b;
+  int st = carve(c, {sizeof(double) * 9 * B, sizeof(double) * 12 * B}, b);
+  if (st) return st;
+  HIP_TRY(hipMemcpyAsync(b[0], F, sizeof(double) * 9 * B, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(rsd::k_fmatrix_cameras, dim3(grid(B)), dim3(128), 0, c->stream,
+                     reinterpret_cast<double *>(b[0]), B, reinterpret_cast<double *>(b[1]));
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(C1, b[1], sizeof(double) * 12 * B, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return RS_OK;
+}
+
+extern "C" int rs_fmatrix_from_cameras(rs_ctx *c, const double *C1, const double *C2, int64_t B,
+                                       double *F) {
+  if (!c || !C1 || !C2 || !F) return fail(RS_EINVAL, "null pointer");
+  if (B < 0 || B > (1LL << 26)) return fail(RS_EINVAL, "bad batch size");
+  if (B == 0) return RS_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  std::vector<char *> b;
+  int st = carve(c, {sizeof(double) * 12 * B, sizeof(double) * 12 * B, sizeof(double) * 9 * B}, b);
+  if (st) return st;
+  HIP_TRY(hipMemcpyAsync(b[0], C1, sizeof(double) * 12 * B, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(b[1], C2, sizeof(double) * 12 * B, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(rsd::k_fmatrix_from_cameras, dim3(grid(B)), dim3(128), 0, c->stream,
+                     reinterpret_cast<double *>(b[0]), reinterpret_cast<double *>(b[1]), B,
+                     reinterpret_cast<double *>(b[2]));
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(F, b[2], sizeof(double) * 9 * B, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return RS_OK;
+}
+
+extern "C" int rs_gold_standard(rs_ctx *c, const double *F, const double *pl, const double *pr,
+                                const int64_t *off, int64_t B, int32_t max_iter, double *F_gold,
+                                double *C1_out, double *X_out, rs_gs_info *info) {
+  if (!c || !F || !off || !F_gold || !info) return fail(RS_EINVAL, "null pointer");
+  if (B < 1 || B > (1 << 24)) return fail(RS_EINVAL, "bad pair count");
+  if (off[0] != 0) return fail(RS_EINVAL, "offsets must start at 0");
+  for (int64_t b = 0; b < B; ++b)
+    if (off[b + 1] < off[b] || off[b + 1] - off[b] > (1 << 24))
+      return fail(RS_EINVAL, "offsets must be non-decreasing");
+  const int64_t total = off[B];
+  if (total > 0 && (!pl || !pr)) return fail(RS_EINVAL, "null point arrays");
+  if (max_iter < 1 || max_iter > 100000) return fail(RS_EINVAL, "max_iter must be in [1, 1e5]");
+  HIP_TRY(hipSetDevice(c->device));
+  const int64_t tp = total > 0 ? total : 1;
+  std::vector<char *> b;
+  int st = carve(c, {sizeof(double) * 9 * B, sizeof(double) * 2 * tp, sizeof(double) * 2 * tp,
+                     sizeof(int64_t) * (B + 1), sizeof(double) * 3 * tp, sizeof(double) * 3 * tp,
+                     sizeof(double) * rsd::kPerPt * tp, sizeof(double) * 9 * B,
+                     sizeof(double) * 12 * B, sizeof(rs_gs_info) * B}, b);
+  if (st) return st;
+  HIP_TRY(hipMemcpyAsync(b[0], F, sizeof(double) * 9 * B, hipMemcpyHostToDevice, c->stream));
+  if (total > 0) {
+    HIP_TRY(hipMemcpyAsync(b[1], pl, sizeof(double) * 2 * total, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(b[2], pr, sizeof(double) * 2 * total, hipMemcpyHostToDevice, c->stream));
+  }
+  HIP_TRY(hipMemcpyAsync(b[3], off, sizeof(int64_t) * (B + 1), hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(rsd::k_gold_standard, dim3(static_cast<unsigned>(B)), dim3(rsd::kGsT), 0,
+                     c->stream, reinterpret_cast<double *>(b[0]),
+                     reinterpret_cast<double *>(b[1]), reinterpret_cast<double *>(b[2]), tp,
+                     reinterpret_cast<int64_t *>(b[3]), max_iter, reinterpret_cast<double *>(b[4]),
+                     reinterpret_cast<double *>(b[5]), reinterpret_cast<double *>(b[6]),
+                     reinterpret_cast<double *>(b[7]), reinterpret_cast<double *>(b[8]),
+                     reinterpret_cast<rsd::GsInfo *>(b[9]));
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(F_gold, b[7], sizeof(double) * 9 * B, hipMemcpyDeviceToHost, c->stream));
+  if (C1_out)
+    HIP_TRY(hipMemcpyAsync(C1_out, b[8], sizeof(double) * 12 * B, hipMemcpyDeviceToHost, c->stream));
+  if (X_out && total > 0)
+    HIP_TRY(hipMemcpyAsync(X_out, b[4], sizeof(double) * 3 * total, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(info, b[9], sizeof(rs_gs_info) * B, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return RS_OK;
+}

@@ -46,6 +46,11 @@ class PnpResult(C.Structure):
                 ("best_count", C.c_int64)]
 
 
+class GsInfo(C.Structure):
+    _fields_ = [("cost_init", C.c_double), ("cost", C.c_double), ("iterations", C.c_int32),
+                ("accepted", C.c_int32), ("status", C.c_int32), ("n", C.c_int32)]
+
+
 _SIGS = {
     "rs_last_error": (C.c_char_p, []),
     "rs_version": (C.c_int, []),
@@ -78,6 +83,16 @@ _SIGS = {
     "rs_pnp_ransac": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, _dp, C.c_int64, C.c_int32,
                                 C.c_int64, C.c_int32, C.c_uint64, _i32p, C.c_double,
                                 C.POINTER(PnpResult), _i64p, _i64p, _i64p, _i64p]),
+    "rs_triangulate_optimal": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, _dp, _i32p,
+                                         C.c_int64, _dp]),
+    "rs_camera_resectioning": (C.c_int, [C.c_void_p, _dp, C.c_int64, _dp, _dp, _dp]),
+    "rs_essential_from_f": (C.c_int, [C.c_void_p, _dp, C.c_int32, _dp, C.c_int64, _dp]),
+    "rs_relative_camera_pose": (C.c_int, [C.c_void_p, _dp, _dp, _dp, C.c_int64, _dp, _dp,
+                                          _i32p]),
+    "rs_fmatrix_cameras": (C.c_int, [C.c_void_p, _dp, C.c_int64, _dp]),
+    "rs_fmatrix_from_cameras": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp]),
+    "rs_gold_standard": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _i64p, C.c_int64, C.c_int32, _dp,
+                                   _dp, _dp, C.POINTER(GsInfo)]),
     "rs_comm_unique_id": (C.c_int, [_u8p]),
     "rs_comm_init": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, _u8p]),
     "rs_comm_destroy": (C.c_int, [C.c_void_p]),

@@ -7,8 +7,12 @@
     ``np.random.choice(arange(N), 8, replace=False)`` would consume, fun.py:305-306), every
     hypothesis is solved, counted and selected by the HIP kernels of librsamd, and the
     advanced MT state is written back into ``np.random`` exactly as the reference leaves it;
-  * the gold-standard refinement (fun.py:343-369) follows on the host
-    (:func:`tsbb15_amd.twoview.gold_standard`), as SURVEY.md 8(f) ranks it the next row.
+  * the gold-standard refinement (fun.py:336-369) follows on the GPU
+    (:func:`tsbb15_amd.twoview.gold_standard`: optimal triangulation of the inliers and a
+    converged Levenberg-Marquardt on the reference's objective, one workgroup per pair).
+
+The E / pose functions of fun.py (camera_resectioning, getEAndK, MakeHomogenous,
+relative_camera_pose) are re-exported from :mod:`tsbb15_amd.twoview` (HIP kernels).
 
 ``ransac_f`` exposes the loop alone with its knobs (iterations, threshold, RNG, sampler).
 """
@@ -19,6 +23,8 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _ffi
+from .twoview import (MakeHomogenous, camera_resectioning, getEAndK,  # noqa: F401
+                      relative_camera_pose)
 
 REFERENCE_ITERATIONS = 10000   # fun.py:302
 INLIER_THRESHOLD = 1.5         # fun.py:317 (strict "<")
@@ -76,7 +82,7 @@ def ransac_f(p1, p2, r=REFERENCE_ITERATIONS, thresh=INLIER_THRESHOLD, rng=None, 
 
 
 def getFFromLabCode(p1, p2):
-    """RANSAC (GPU) + gold-standard ML refinement (host); returns F_gold (fun.py:291-369)."""
+    """RANSAC (GPU) + gold-standard ML refinement (GPU); returns F_gold (fun.py:291-369)."""
     from . import twoview
     res = ransac_f(p1, p2)
     if res.F is None:

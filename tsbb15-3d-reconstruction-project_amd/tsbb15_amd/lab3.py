@@ -7,15 +7,18 @@ Same names, argument layout and errors as the reference toolbox
   * ``fmatrix_residuals(F, x, y)`` lab3.py:188-227 -> rs_fmatrix_residuals (HIP)
   * ``homog(x)``                   lab3.py:30-50 (host helper, no arithmetic)
 
-The two-view helpers used after RANSAC (fmatrix_cameras, fmatrix_from_cameras,
-triangulate_*, fmatrix_residuals_gs) live in :mod:`tsbb15_amd.twoview` (host code, SURVEY.md
-8(f) "next" rows).
+  * ``fmatrix_cameras(F)``                 lab3.py:353-380 -> rs_fmatrix_cameras (HIP)
+  * ``fmatrix_from_cameras(C1, C2)``       lab3.py:331-351 -> rs_fmatrix_from_cameras (HIP)
+  * ``triangulate_optimal(C1, C2, x1, x2)`` lab3.py:382-475 -> rs_triangulate_optimal (HIP)
+
+(implemented in :mod:`tsbb15_amd.twoview`, which also holds the batched forms).
 """
 from __future__ import annotations
 
 import numpy as np
 
 from . import _ffi
+from .twoview import fmatrix_cameras, fmatrix_from_cameras, triangulate_optimal  # noqa: F401
 
 
 def homog(x):

@@ -1,128 +1,218 @@
-"""Two-view geometry after RANSAC: the gold-standard (ML) refinement of fun.py:343-369.
+"""Two-view geometry after RANSAC on the GPU.
 
-Host numpy/scipy stage (the "next" row; not yet on the GPU).  The
-formulas are the textbook ones the reference toolbox uses:
+Every function here runs in librsamd's HIP kernels (twoview.hip); the reference functions
+they replace:
 
-  * cameras from F with C2 = [I | 0]: C1 = [[e1]_x F | e1], e1 the left null vector of F
-    (lab3.fmatrix_cameras, lab3.py:353-380);
-  * F from cameras: F = [C1 n]_x C1 C2^+, n the camera centre of C2 (lab3.py:331-351);
-  * optimal triangulation (Hartley & Zisserman, Alg. 12.1) with both epipoles rotated onto the
-    x axis and f = f' = 1: roots of g(t) = t P(t)^2 - (ad - bc)(1 + t^2)^2 (at + b)(ct + d),
-    P(t) = (at + b)^2 + (ct + d)^2, cost s(t) = t^2/(1 + t^2) + (ct + d)^2 / P(t), plus the
-    value at t = inf (lab3.py:382-475); real parts of all roots are evaluated, as there;
-  * linear triangulation by the null vector of [[x1]_x C1; [x2]_x C2] (lab3.py:477-503);
-  * reprojection residuals (lab3.py:230-266) minimised by scipy's TRF with lsmr and
-    xtol = 2.22e-14 (fun.py:358).
+  * ``fmatrix_cameras(F)``                     lab3.py:353-380   (rs_fmatrix_cameras)
+  * ``fmatrix_from_cameras(C1, C2)``           lab3.py:331-351   (rs_fmatrix_from_cameras)
+  * ``triangulate_optimal(C1, C2, x1, x2)``    lab3.py:382-475   (rs_triangulate_optimal)
+  * ``triangulate_optimal_batch``              the same over many points / camera pairs
+  * ``camera_resectioning(C)``                 fun.py:260-280    (rs_camera_resectioning)
+  * ``getEAndK(C, F)``                         fun.py:91-102     (+ rs_essential_from_f)
+  * ``relative_camera_pose(E, y1, y2)``        fun.py:209-258    (rs_relative_camera_pose)
+  * ``gold_standard(F, pl, pr)``               fun.py:336-369    (rs_gold_standard)
+  * ``gold_standard_batch(Fs, pls, prs)``      the same, one workgroup per pair
+
+``MakeHomogenous`` (fun.py:48-55) and ``project`` are input / output formatting helpers.
+The gold standard minimises the reference's objective (lab3.fmatrix_residuals_gs) to
+convergence; the reference's scipy TRF stops on ftol = 1e-8 at a path-dependent point with a
+higher objective (see oracle/twoview_ref.py and DESIGN.md).
 """
 from __future__ import annotations
 
+from dataclasses import dataclass
+
 import numpy as np
-from scipy.optimize import least_squares
+
+from . import _ffi
 
 I34 = np.hstack([np.eye(3), np.zeros((3, 1))])
+_d = _ffi.C.c_double
 
 
-def cross_matrix(v):
-    v = np.asarray(v, dtype=np.float64).ravel()
-    if v.size != 3:
-        raise ValueError('Can only handle 3D vectors')
-    return np.array([[0.0, -v[2], v[1]], [v[2], 0.0, -v[0]], [-v[1], v[0], 0.0]])
+def _ctx(ctx):
+    return (ctx or _ffi.default_context()).handle
 
 
-def project(X, C):
-    """Pinhole projection of (3,) or (3,N) points through a 3x4 camera -> (2,) or (2,N)."""
-    if C.shape != (3, 4):
+def _cam(C):
+    C = _ffi.f64c(C)
+    if C.shape[-2:] != (3, 4):
         raise ValueError('C is not a valid camera matrix')
-    X = np.asarray(X, dtype=np.float64)
-    one_d = X.ndim == 1
-    Xh = np.vstack([X.reshape(3, -1), np.ones((1, X.reshape(3, -1).shape[1]))])
-    y = C @ Xh
-    y = y[:2] / y[2]
-    return y.ravel() if one_d else y
+    return C
 
 
-def fmatrix_from_cameras(C1, C2):
-    _, _, Vt = np.linalg.svd(C2)
-    e = C1 @ Vt[3]
-    return cross_matrix(e) @ (C1 @ np.linalg.pinv(C2))
-
-
-def fmatrix_cameras(F):
-    U, _, _ = np.linalg.svd(F)
-    e1 = U[:, -1]
-    C1 = np.hstack([cross_matrix(e1) @ F, e1.reshape(3, 1)])
+def fmatrix_cameras(F, ctx=None):
+    """lab3.fmatrix_cameras: (C1, C2) with C2 = [I | 0] and C1 = [[e1]_x F | e1]."""
+    Fc = _ffi.f64c(F)
+    if Fc.shape != (3, 3):
+        raise ValueError('F must be (3, 3)')
+    C1 = np.empty((3, 4))
+    _ffi.check(_ffi.lib().rs_fmatrix_cameras(_ctx(ctx), _ffi.ptr(Fc, _d), 1, _ffi.ptr(C1, _d)))
     return C1, I34.copy()
 
 
-def fmatrix_epipoles(F):
-    U, _, Vt = np.linalg.svd(F)
-    e1 = U[:, -1] / U[-1, -1]
-    e2 = Vt[-1] / Vt[-1, -1]
-    return e1[:2], e2[:2]
+def fmatrix_from_cameras(C1, C2, ctx=None):
+    """lab3.fmatrix_from_cameras: F = [C1 n]_x C1 C2^+ (n the centre of C2)."""
+    a, b = _cam(C1), _cam(C2)
+    F = np.empty((3, 3))
+    _ffi.check(_ffi.lib().rs_fmatrix_from_cameras(_ctx(ctx), _ffi.ptr(a, _d), _ffi.ptr(b, _d), 1,
+                                                  _ffi.ptr(F, _d)))
+    return F
 
 
-def triangulate_linear(C1, C2, x1, x2):
-    x1 = np.append(x1, 1.0) if np.size(x1) == 2 else np.asarray(x1, float).ravel()
-    x2 = np.append(x2, 1.0) if np.size(x2) == 2 else np.asarray(x2, float).ravel()
-    M = np.vstack([cross_matrix(x1) @ C1, cross_matrix(x2) @ C2])
-    X = np.linalg.svd(M)[2][-1]
-    return X[:3] / X[3]
+def triangulate_optimal_batch(C1, C2, x1, x2, cam=None, ctx=None):
+    """Optimal triangulation of many correspondences.  C1, C2: (3,4) or (k,3,4); x1, x2:
+    (2, n); cam: (n,) camera-pair index per point (None: pair 0).  Returns X (n, 3)."""
+    a = _cam(C1).reshape(-1, 3, 4)
+    b = _cam(C2).reshape(-1, 3, 4)
+    if a.shape != b.shape:
+        raise ValueError('C1 and C2 batches differ')
+    x1, x2 = _ffi.f64c(x1), _ffi.f64c(x2)
+    if x1.shape != x2.shape or x1.ndim != 2 or x1.shape[0] != 2:
+        raise ValueError('x1 and x2 must both be (2, n)')
+    n = x1.shape[1]
+    cp = None
+    if cam is not None:
+        cam = np.ascontiguousarray(cam, dtype=np.int32)
+        if cam.shape != (n,):
+            raise ValueError('cam must be (n,)')
+        cp = _ffi.ptr(cam, _ffi.C.c_int32)
+    X = np.empty((n, 3))
+    _ffi.check(_ffi.lib().rs_triangulate_optimal(_ctx(ctx), _ffi.ptr(a, _d), _ffi.ptr(b, _d),
+                                                 a.shape[0], _ffi.ptr(x1, _d), _ffi.ptr(x2, _d),
+                                                 cp, n, _ffi.ptr(X, _d)))
+    return X
 
 
-def _rot_to_x_axis(e):
-    return np.array([[e[0], e[1], 0.0], [-e[1], e[0], 0.0], [0.0, 0.0, 1.0]])
+def triangulate_optimal(C1, C2, x1, x2, ctx=None):
+    """lab3.triangulate_optimal for one correspondence: x1, x2 (2,) -> X (3,)."""
+    x1 = np.asarray(x1, dtype=np.float64).reshape(2, 1)
+    x2 = np.asarray(x2, dtype=np.float64).reshape(2, 1)
+    return triangulate_optimal_batch(C1, C2, x1, x2, ctx=ctx)[0]
 
 
-def triangulate_optimal(C1, C2, x1, x2):
-    """Hartley-Zisserman optimal triangulation (f = f' = 1 form) of one correspondence."""
-    T1 = np.array([[1.0, 0.0, x1[0]], [0.0, 1.0, x1[1]], [0.0, 0.0, 1.0]])
-    T2 = np.array([[1.0, 0.0, x2[0]], [0.0, 1.0, x2[1]], [0.0, 0.0, 1.0]])
-    F = T1.T @ (fmatrix_from_cameras(C1, C2) @ T2)
-    e1, e2 = fmatrix_epipoles(F)
-    e1 = e1 / np.linalg.norm(e1)
-    e2 = e2 / np.linalg.norm(e2)
-    R1, R2 = _rot_to_x_axis(e1), _rot_to_x_axis(e2)
-    F = R1 @ (F @ R2.T)
-    a, b, c, d = F[1, 1], F[1, 2], F[2, 1], F[2, 2]
-    P = np.polyadd(np.polymul([a, b], [a, b]), np.polymul([c, d], [c, d]))
-    g = np.polysub(np.polymul([1.0, 0.0], np.polymul(P, P)),
-                   (a * d - b * c) * np.polymul([1.0, 0.0, 2.0, 0.0, 1.0],
-                                                np.polymul([a, b], [c, d])))
-    t = np.real(np.roots(g))
-    cost = [ti ** 2 / (1 + ti ** 2) + (c * ti + d) ** 2 / ((a * ti + b) ** 2 + (c * ti + d) ** 2)
-            for ti in t]
-    cost.append(1.0 + c ** 2 / (a ** 2 + c ** 2))
-    k = int(np.argmin(cost))
-    if k < t.size:
-        tm = t[k]
-        l1 = np.array([-(c * tm + d), a * tm + b, c * tm + d])
-        l2 = np.array([tm, 1.0, -tm])
-    else:
-        l1 = np.array([-c, a, c])
-        l2 = np.array([1.0, 0.0, -1.0])
-
-    def foot(l):  # closest point of line l to the origin (homogeneous)
-        return np.array([-l[0] * l[2], -l[1] * l[2], l[0] ** 2 + l[1] ** 2])
-
-    y1 = T1 @ (R1.T @ foot(l1))
-    y2 = T2 @ (R2.T @ foot(l2))
-    return triangulate_linear(C1, C2, y1, y2)
+def camera_resectioning_batch(P, ctx=None):
+    """fun.camera_resectioning over (B,3,4) cameras -> K, R (B,3,3), t (B,3)."""
+    P = _cam(P).reshape(-1, 3, 4)
+    B = P.shape[0]
+    K, R, t = np.empty((B, 3, 3)), np.empty((B, 3, 3)), np.empty((B, 3))
+    _ffi.check(_ffi.lib().rs_camera_resectioning(_ctx(ctx), _ffi.ptr(P, _d), B, _ffi.ptr(K, _d),
+                                                 _ffi.ptr(R, _d), _ffi.ptr(t, _d)))
+    return K, R, t
 
 
-def fmatrix_residuals_gs(params, pl, pr):
-    """Reprojection residuals [left x, left y, right x, right y] (lab3.py:230-266)."""
-    C1 = params[:12].reshape(3, 4)
-    X = params[12:].reshape(-1, 3).T
-    if X.shape[1] != pl.shape[1]:
-        raise ValueError('Wrong size of parameter vector')
-    return np.concatenate([(pl - project(X, C1)).ravel(), (pr - project(X, I34)).ravel()])
+def camera_resectioning(C, ctx=None):
+    """fun.camera_resectioning: C = lambda K [R | t] -> (K, R, t)."""
+    K, R, t = camera_resectioning_batch(np.asarray(C).reshape(1, 3, 4), ctx)
+    return K[0], R[0], t[0]
 
 
-def gold_standard(F, pl, pr):
-    """ML refinement of F on the consensus set (fun.py:343-369); returns F_gold."""
-    C1, C2 = fmatrix_cameras(F)
-    X = np.array([triangulate_optimal(C1, C2, a, b) for a, b in zip(pl.T, pr.T)])
-    params = np.hstack([C1.ravel(), X.ravel()])
-    sol = least_squares(fmatrix_residuals_gs, params, xtol=2.22e-14, tr_solver='lsmr',
-                        args=(pl, pr)).x
-    return fmatrix_from_cameras(sol[:12].reshape(3, 4), I34.copy())
+def essential_batch(K, F, ctx=None):
+    """E = K^T F K for F (B,3,3) and K (3,3) or (B,3,3)."""
+    F = _ffi.f64c(F).reshape(-1, 3, 3)
+    K = _ffi.f64c(K)
+    one = K.shape == (3, 3)
+    if not one and K.shape != F.shape:
+        raise ValueError('K must be (3, 3) or match F')
+    E = np.empty_like(F)
+    _ffi.check(_ffi.lib().rs_essential_from_f(_ctx(ctx), _ffi.ptr(K, _d), int(one),
+                                              _ffi.ptr(F, _d), F.shape[0], _ffi.ptr(E, _d)))
+    return E
+
+
+def getEAndK(C, F, ctx=None):
+    """fun.getEAndK: resection every camera of C (1, n, 3, 4) on the GPU; K of the LAST one
+    (the reference overwrites K in its loop, fun.py:96-98); E = K^T F K."""
+    C = np.asarray(C, dtype=np.float64)
+    K, _, _ = camera_resectioning_batch(C[0], ctx)
+    Kl = np.ascontiguousarray(K[-1])
+    return essential_batch(Kl, np.asarray(F).reshape(1, 3, 3), ctx)[0], Kl
+
+
+def MakeHomogenous(K, coord):
+    """fun.MakeHomogenous: (n, 2) pixels -> (n, 3) C-normalised K^-1 [u, v, 1] (formatting)."""
+    coord = np.asarray(coord, dtype=np.float64)
+    h = np.vstack([coord.T[:2], np.ones((1, coord.shape[0]))])
+    return np.linalg.solve(np.asarray(K, dtype=np.float64), h).T
+
+
+def relative_camera_pose_batch(E, y1, y2, ctx=None):
+    """fun.relative_camera_pose over pairs: E (B,3,3), y1, y2 (B,2).  Returns R (B,3,3),
+    t (B,3), found (B,) int32 (0 where the reference returns None)."""
+    E = _ffi.f64c(E).reshape(-1, 3, 3)
+    B = E.shape[0]
+    y1 = _ffi.f64c(y1).reshape(B, 2)
+    y2 = _ffi.f64c(y2).reshape(B, 2)
+    R, t = np.empty((B, 3, 3)), np.empty((B, 3))
+    found = np.empty(B, dtype=np.int32)
+    _ffi.check(_ffi.lib().rs_relative_camera_pose(
+        _ctx(ctx), _ffi.ptr(E, _d), _ffi.ptr(y1, _d), _ffi.ptr(y2, _d), B, _ffi.ptr(R, _d),
+        _ffi.ptr(t, _d), _ffi.ptr(found, _ffi.C.c_int32)))
+    return R, t, found
+
+
+def relative_camera_pose(E, y1, y2, ctx=None):
+    """fun.relative_camera_pose: (R, t) of the first chirality-valid candidate, or None."""
+    R, t, f = relative_camera_pose_batch(E, np.asarray(y1)[:2], np.asarray(y2)[:2], ctx)
+    if f[0] == 0:
+        return None
+    return R[0], t[0]
+
+
+def project(X, C):
+    """Pinhole projection of (3,) or (3,N) points through a 3x4 camera (formatting helper)."""
+    X = np.asarray(X, dtype=np.float64)
+    one = X.ndim == 1
+    Xr = X.reshape(3, -1)
+    y = C @ np.vstack([Xr, np.ones((1, Xr.shape[1]))])
+    y = y[:2] / y[2]
+    return y.ravel() if one else y
+
+
+@dataclass
+class GoldStandard:
+    F: np.ndarray          # F_gold (3,3)
+    C1: np.ndarray         # refined first camera (3,4); C2 = [I | 0]
+    X: np.ndarray          # refined 3D points (n,3)
+    cost_init: float       # 0.5 |r|^2 at the reference's start (fun.py:343-356)
+    cost: float            # 0.5 |r|^2 at the end
+    iterations: int
+    status: int            # 0 max_iter, 1 converged, 2 no further decrease
+
+
+MAX_ITER = 500
+
+
+def gold_standard_batch(Fs, pls, prs, max_iter=MAX_ITER, ctx=None):
+    """fun.py:336-369 for many pairs at once: Fs (B,3,3) F_RANSAC; pls, prs lists of (2, n_b)
+    inlier point sets.  Returns a list of :class:`GoldStandard`."""
+    Fs = _ffi.f64c(Fs).reshape(-1, 3, 3)
+    B = Fs.shape[0]
+    if len(pls) != B or len(prs) != B:
+        raise ValueError('one point set per F')
+    ns = []
+    for a, b in zip(pls, prs):
+        a, b = np.asarray(a), np.asarray(b)
+        if a.shape != b.shape or a.ndim != 2 or a.shape[0] != 2:
+            raise ValueError('point sets must be (2, n) pairs')
+        ns.append(a.shape[1])
+    off = np.zeros(B + 1, dtype=np.int64)
+    off[1:] = np.cumsum(ns)
+    total = int(off[-1])
+    pl = _ffi.f64c(np.hstack([np.asarray(a, np.float64) for a in pls]) if total else np.zeros((2, 0)))
+    pr = _ffi.f64c(np.hstack([np.asarray(b, np.float64) for b in prs]) if total else np.zeros((2, 0)))
+    Fg = np.empty((B, 3, 3))
+    C1 = np.empty((B, 3, 4))
+    X = np.empty((max(total, 1), 3))
+    info = (_ffi.GsInfo * B)()
+    _ffi.check(_ffi.lib().rs_gold_standard(
+        _ctx(ctx), _ffi.ptr(Fs, _d), _ffi.ptr(pl, _d), _ffi.ptr(pr, _d),
+        _ffi.ptr(off, _ffi.C.c_int64), B, int(max_iter), _ffi.ptr(Fg, _d), _ffi.ptr(C1, _d),
+        _ffi.ptr(X, _d), info))
+    return [GoldStandard(Fg[b], C1[b], X[off[b]:off[b + 1]].copy(), info[b].cost_init,
+                         info[b].cost, info[b].iterations, info[b].status) for b in range(B)]
+
+
+def gold_standard(F, pl, pr, max_iter=MAX_ITER, ctx=None):
+    """F_gold of fun.py:336-369 from F_RANSAC and the inlier points pl, pr (2, n)."""
+    return gold_standard_batch(np.asarray(F).reshape(1, 3, 3), [pl], [pr], max_iter, ctx)[0].F
