@@ -95,3 +95,33 @@ def test_dino_ring_all_pairs(ctx):
         F = tab["F"][i].reshape(3, 3)
         d = ransac_ref.inlier_distance(F, p1, p2)
         assert tab["count"][i] == np.count_nonzero(d < 1.5) == p1.shape[1]
+
+
+def test_dino_ring_pipeline_poses(ctx):
+    """C4 end to end on the GPU: RANSAC per pair, then one batched gold-standard launch and
+    one batched E / relative-pose launch over all 203 valid pairs.  The BAdino2 scene is
+    noise-free, so every pair's pose must be the true relative pose of its two resectioned
+    cameras (fun.camera_resectioning goldens): R = R_j R_i^T, and t = -unit(t_j - R t_i) --
+    the reference's chirality convention, pinned by clean_data_eval / twoview.npz pose_t."""
+    z = golden("dino_pnp_kat.npz")
+    pairs = _dino_pairs()
+    solver = parallel.GpuPairSolver(ctx, 1000)
+    refiner = parallel.GpuPairRefiner(ctx, z["K_last"])
+    try:
+        tab = parallel.run_pairs(_Solo(), pairs, 1000, solver, refine=refiner)
+    finally:
+        solver.close()
+    ij = list(itertools.combinations(range(36), 2))
+    valid = np.flatnonzero(tab["valid"] == 1)
+    assert len(valid) == 203 and np.all(tab["refined"][valid] == 1)
+    assert np.all(tab["pose"][valid] > 0)
+    Rs, ts = z["R"], z["t"]
+    worst_R = worst_t = 0.0
+    for k in valid:
+        i, j = ij[k]
+        Rt = Rs[j] @ Rs[i].T
+        tt = ts[j] - Rt @ ts[i]
+        worst_R = max(worst_R, np.abs(tab["R"][k].reshape(3, 3) - Rt).max())
+        worst_t = max(worst_t, np.abs(tab["t"][k] + tt / np.linalg.norm(tt)).max())
+        assert tab["gs_cost"][k] < 1e-12
+    assert worst_R < 1e-6 and worst_t < 1e-6, (worst_R, worst_t)

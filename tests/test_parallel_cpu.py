@@ -36,6 +36,26 @@ def _records(tr, F_of, lo, hi):
     return rec
 
 
+def _oracle_refiner(K):
+    """CPU stand-in for GpuPairRefiner (same item / result layout) built on the oracle."""
+    from oracle import twoview_ref as tvr
+
+    def refine(items):
+        out = []
+        for i, F, a, b, f1, f2 in items:
+            Fg, info = tvr.gold_standard_lm(np.asarray(F).reshape(3, 3), a, b)
+            E = K.T @ Fg @ K
+            y1 = tvr.MakeHomogenous(K, f1[None])[0, :2]
+            y2 = tvr.MakeHomogenous(K, f2[None])[0, :2]
+            r = tvr.relative_camera_pose(E, y1, y2)
+            if r is None:
+                out.append((Fg.ravel(), info["cost"], 0, np.full(9, np.nan), np.full(3, np.nan)))
+            else:
+                out.append((Fg.ravel(), info["cost"], 1, r[0].ravel(), r[1]))
+        return out
+    return refine
+
+
 def _worker(rank, world, port, case, q):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
@@ -56,8 +76,9 @@ def _worker(rank, world, port, case, q):
             def solve(i, p1, p2):
                 F, S, d, best, _ = ransac_ref.ransac_f(p1, p2, r=case["H"],
                                                        rng=np.random.RandomState(i))
-                return (1, best, len(S), float(d), F.ravel())
-            tab = parallel.run_pairs(comm, pairs, case["H"], solve)
+                return (1, best, len(S), float(d), F.ravel(), S)
+            refine = _oracle_refiner(case["K"]) if case.get("K") is not None else None
+            tab = parallel.run_pairs(comm, pairs, case["H"], solve, refine=refine)
             q.put((rank, tab.tobytes(), None))
     finally:
         dist.destroy_process_group()
@@ -141,3 +162,24 @@ def test_gloo_pair_table_equals_single_process():
         F, S, d, best, _ = ransac_ref.ransac_f(p1, p2, r=50, rng=np.random.RandomState(i))
         assert row["valid"] == 1 and row["best_index"] == best and row["count"] == len(S)
         np.testing.assert_array_equal(row["F"], F.ravel())
+
+
+def test_gloo_pair_pipeline_refined_equals_single_process():
+    """RANSAC + gold standard + E / pose per pair, sharded over 2 ranks, one all-gather: the
+    refined table equals the single-process refinement of every pair."""
+    K = np.array([[800.0, 0, 320], [0, 800, 240], [0, 0, 1]])
+    pairs = [synth.two_view(n, 0.2, seed=40 + i)[:2] for i, n in enumerate([60, 7, 90, 45])]
+    out = _spawn(2, {"kind": "pairs", "pairs": pairs, "H": 60, "K": K})
+    tabs = [np.frombuffer(b, dtype=parallel.PAIR_DTYPE) for _, b, _ in out]
+    assert tabs[0].tobytes() == tabs[1].tobytes()
+    ref = _oracle_refiner(K)
+    for i, (p1, p2) in enumerate(pairs):
+        row = tabs[0][i]
+        if p1.shape[1] < 8:
+            assert row["valid"] == 0 and row["refined"] == 0
+            continue
+        F, S, d, best, _ = ransac_ref.ransac_f(p1, p2, r=60, rng=np.random.RandomState(i))
+        (Fg, cost, found, R, t), = ref([(i, F, p1[:, S], p2[:, S], p1[:, 0], p2[:, 0])])
+        assert row["refined"] == 1 and row["pose"] == found
+        np.testing.assert_array_equal(row["F_gold"], Fg)
+        np.testing.assert_array_equal(row["R"], R)

@@ -3,8 +3,10 @@
 Two shardings:
 
   * pairs (config C4): independent image pairs are assigned to ranks by longest-processing-
-    time greedy on N x H; each rank runs its pairs with no collective; one all-gather of fixed
-    size per-pair records (F, count, index, pair id) at the end.
+    time greedy on N x H; each rank runs its pairs with no collective -- RANSAC per pair, then
+    (optionally) one batched launch of the gold-standard refinement and of E / relative pose
+    over all of its pairs -- and one all-gather of fixed-size per-pair records (F_RANSAC,
+    count, index, F_gold, R, t, pair id) at the end.
   * hypotheses of one pair (C2/C5 weak scaling): rank r evaluates the contiguous hypothesis
     range [start_r, start_r + n_r) (Philox counters are global hypothesis indices, so the
     union is exactly the single-GPU run); then one max-all-reduce of c* and one all-gather of
@@ -26,7 +28,9 @@ from . import _ffi
 CAND_DTYPE = np.dtype([("index", "<i8"), ("count", "<i8"), ("std", "<f8"), ("norm", "<f8"),
                        ("F", "<f8", (9,))])
 PAIR_DTYPE = np.dtype([("pair", "<i8"), ("valid", "<i8"), ("best_index", "<i8"),
-                       ("count", "<i8"), ("std", "<f8"), ("F", "<f8", (9,))])
+                       ("count", "<i8"), ("std", "<f8"), ("F", "<f8", (9,)),
+                       ("refined", "<i8"), ("F_gold", "<f8", (9,)), ("gs_cost", "<f8"),
+                       ("pose", "<i8"), ("R", "<f8", (9,)), ("t", "<f8", (3,))])
 
 
 # ------------------------------------------------------------------------------------------
@@ -201,9 +205,9 @@ class GpuPairSolver:
             plan = self.plans[n] = _ffi.F8Plan(self.ctx, n, self.H)
         plan.set_points(p1, p2)
         plan.run(self.H, mode=_ffi.SAMPLER_PHILOX, seed=self.seed_base + i, thresh=self.thresh)
-        r, _ = plan.result()
+        r, inl = plan.result()
         return (1 if r.best_index >= 0 else 0, r.best_index, r.best_count, r.best_std,
-                np.array(r.F[:]))
+                np.array(r.F[:]), inl)
 
     def close(self):
         for p in self.plans.values():
@@ -211,22 +215,68 @@ class GpuPairSolver:
         self.plans = {}
 
 
-def run_pairs(comm, pairs, H, solve):
+class GpuPairRefiner:
+    """After RANSAC, for all of this rank's pairs in one launch each: the gold standard
+    (fun.py:336-369) on the inliers, then -- given the calibration K -- E = K^T F_gold K and
+    the relative pose from the pair's first correspondence (fun.py:91-102, 209-258, as
+    main.py:50-63 does for the initial pair)."""
+
+    def __init__(self, ctx, K=None):
+        self.ctx = ctx
+        self.K = None if K is None else np.ascontiguousarray(K, dtype=np.float64)
+
+    def __call__(self, items):
+        from . import twoview
+        if not items:
+            return []
+        Fs = np.stack([np.asarray(it[1]).reshape(3, 3) for it in items])
+        gs = twoview.gold_standard_batch(Fs, [it[2] for it in items], [it[3] for it in items],
+                                         ctx=self.ctx)
+        Fg = np.stack([g.F for g in gs])
+        nan9, nan3 = np.full(9, np.nan), np.full(3, np.nan)
+        if self.K is None:
+            return [(g.F.ravel(), g.cost, 0, nan9, nan3) for g in gs]
+        E = twoview.essential_batch(self.K, Fg, ctx=self.ctx)
+        y1 = twoview.MakeHomogenous(self.K, np.stack([it[4] for it in items]))[:, :2]
+        y2 = twoview.MakeHomogenous(self.K, np.stack([it[5] for it in items]))[:, :2]
+        R, t, found = twoview.relative_camera_pose_batch(E, y1, y2, ctx=self.ctx)
+        return [(g.F.ravel(), g.cost, int(f), R[k].ravel(), t[k])
+                for k, (g, f) in enumerate(zip(gs, found))]
+
+
+def run_pairs(comm, pairs, H, solve, refine=None):
     """Config C4: ``pairs`` = list of (p1, p2); ``solve(i, p1, p2)`` -> (valid, best_index,
-    count, std, F[9]) runs one pair on this rank (GpuPairSolver on a GPU).  Pairs with N < 8
-    are skipped (valid = 0).  Returns the PAIR_DTYPE table of every pair, identical on every
-    rank, after one all-gather of fixed-size records."""
+    count, std, F[9][, inliers]) runs one pair on this rank (GpuPairSolver on a GPU).  Pairs
+    with N < 8 are skipped (valid = 0).  ``refine(items)`` (GpuPairRefiner on a GPU), with
+    items = [(i, F, pl_inliers, pr_inliers, first p1 point, first p2 point)], returns per item
+    (F_gold[9], gs_cost, pose found, R[9], t[3]) for all of the rank's valid pairs at once.
+    Returns the PAIR_DTYPE table of every pair, identical on every rank, after one
+    all-gather of fixed-size records."""
     costs = [p1.shape[1] * H if p1.shape[1] >= 8 else 0 for p1, _ in pairs]
     owners = lpt_assign(costs, comm.world)
     recs = np.zeros(len(pairs), dtype=PAIR_DTYPE)
     recs["pair"] = np.arange(len(pairs))
     recs["best_index"] = -1
+    for f in ("F_gold", "gs_cost", "R", "t"):
+        recs[f] = np.nan
+    items = []
     for i in owners[comm.rank]:
         p1, p2 = pairs[i]
         if p1.shape[1] < 8:
             continue
-        valid, best, count, std, F = solve(i, p1, p2)
-        recs[i] = (i, valid, best, count, std, F)
+        out = solve(i, p1, p2)
+        valid, best, count, std, F = out[:5]
+        recs[i]["pair"], recs[i]["valid"], recs[i]["best_index"] = i, valid, best
+        recs[i]["count"], recs[i]["std"], recs[i]["F"] = count, std, F
+        if refine is not None and valid and len(out) > 5 and len(out[5]) > 0:
+            S = np.asarray(out[5])
+            items.append((i, np.asarray(F), p1[:, S], p2[:, S], p1[:, 0], p2[:, 0]))
+    if refine is not None:
+        for it, (Fg, cost, found, R, t) in zip(items, refine(items)):
+            r = recs[it[0]]
+            r["refined"], r["F_gold"], r["gs_cost"] = 1, Fg, cost
+            r["pose"], r["R"], r["t"] = found, R, t
+            recs[it[0]] = r
     parts = comm.allgather_bytes(recs.tobytes())
     table = np.zeros(len(pairs), dtype=PAIR_DTYPE)
     for r, p in enumerate(parts):
