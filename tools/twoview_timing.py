@@ -1,0 +1,62 @@
+"""Timing of the two-view stages on one GPU (diagnostic; bench.py reports the headline)."""
+import itertools
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tsbb15-3d-reconstruction-project_amd"))
+sys.path.insert(0, REPO)
+from tsbb15_amd import _ffi, fun, parallel, synth, twoview  # noqa: E402
+
+
+class Solo:
+    rank, world = 0, 1
+
+    def allgather_bytes(self, b):
+        return [b]
+
+
+def t(f, reps=3):
+    best = 1e9
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        out = f()
+        best = min(best, time.perf_counter() - t0)
+    return best, out
+
+
+ctx = _ffi.default_context()
+z = np.load(os.path.join(REPO, "tests/golden/dino_pnp_kat.npz"))
+P = z["points2d"]
+pairs = []
+for i, j in itertools.combinations(range(36), 2):
+    vis = np.flatnonzero(np.any(P[i] != -1, axis=0) & np.any(P[j] != -1, axis=0))
+    pairs.append((np.ascontiguousarray(P[i][:, vis]), np.ascontiguousarray(P[j][:, vis])))
+solver = parallel.GpuPairSolver(ctx, 1000)
+refiner = parallel.GpuPairRefiner(ctx, z["K_last"])
+dt0, _ = t(lambda: parallel.run_pairs(Solo(), pairs, 1000, solver))
+dt1, tab = t(lambda: parallel.run_pairs(Solo(), pairs, 1000, solver, refine=refiner))
+print(f"C4 ransac only: {dt0*1e3:.1f} ms; ransac+gold+pose: {dt1*1e3:.1f} ms "
+      f"(203 valid pairs)")
+
+p1, p2, _ = synth.two_view(2000, 0.3, seed=1)
+res = fun.ransac_f(p1, p2, r=10000, rng=np.random.RandomState(0))
+a, b = p1[:, res.inliers], p2[:, res.inliers]
+dt, g = t(lambda: twoview.gold_standard_batch(res.F[None], [a], [b])[0])
+print(f"gold standard C2 winner: n={a.shape[1]} {dt*1e3:.2f} ms iters={g.iterations} "
+      f"cost {g.cost_init:.4f}->{g.cost:.4f} status={g.status}")
+c = np.load(os.path.join(REPO, "tests/golden/dino_c1.npz"))
+for tag in ("clean", "noisy"):
+    def full():
+        np.random.seed(0)
+        return fun.getFFromLabCode(c[f"{tag}_p1"], c[f"{tag}_p2"])
+    dt, _ = t(full)
+    print(f"getFFromLabCode {tag} (N={c[f'{tag}_p1'].shape[1]}): {dt*1e3:.1f} ms "
+          f"(reference {float(c[f'{tag}_full_seconds']):.1f} s in the build container)")
+X = np.ascontiguousarray(np.tile(a, 8)), np.ascontiguousarray(np.tile(b, 8))
+C1, C2 = twoview.fmatrix_cameras(res.F)
+dt, _ = t(lambda: twoview.triangulate_optimal_batch(C1, C2, X[0], X[1]))
+print(f"triangulate_optimal batch n={X[0].shape[1]}: {dt*1e3:.2f} ms")

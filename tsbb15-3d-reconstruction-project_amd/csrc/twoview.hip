@@ -26,7 +26,7 @@
 
 namespace rsd {
 
-__global__ void k_triangulate_optimal(const double *__restrict__ C1s,
+__global__ __launch_bounds__(128) void k_triangulate_optimal(const double *__restrict__ C1s,
                                       const double *__restrict__ C2s,
                                       const double *__restrict__ x1, const double *__restrict__ x2,
                                       const int32_t *__restrict__ cam, int64_t n,
@@ -50,7 +50,7 @@ __global__ void k_triangulate_optimal(const double *__restrict__ C1s,
 // and K[2,2] = 1, R a rotation.  The decomposition is unique, so it is computed directly
 // (RQ by twice-applied Gram-Schmidt from the last row, then the sign of det A), without the
 // LAPACK sign conventions specRQ (fun.py:181-188) and the D fix-up (fun.py:267-279) undo.
-__global__ void k_resection(const double *__restrict__ P, int64_t B, double *__restrict__ K,
+__global__ __launch_bounds__(128) void k_resection(const double *__restrict__ P, int64_t B, double *__restrict__ K,
                             double *__restrict__ R, double *__restrict__ t) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= B) return;
@@ -98,7 +98,7 @@ __global__ void k_resection(const double *__restrict__ P, int64_t B, double *__r
   }
 }
 
-__global__ void k_essential(const double *__restrict__ K, int k_stride,
+__global__ __launch_bounds__(128) void k_essential(const double *__restrict__ K, int k_stride,
                             const double *__restrict__ F, int64_t B, double *__restrict__ E) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= B) return;
@@ -124,7 +124,7 @@ __global__ void k_essential(const double *__restrict__ K, int k_stride,
 // in both cameras wins (found = 1..4), else found = 0 (the reference returns None).  The
 // candidate set does not depend on the SVD's sign / ordering freedom of the two equal
 // singular values, so the pose is the reference's whenever exactly one candidate passes.
-__global__ void k_relative_pose(const double *__restrict__ Es, const double *__restrict__ y1,
+__global__ __launch_bounds__(128) void k_relative_pose(const double *__restrict__ Es, const double *__restrict__ y1,
                                 const double *__restrict__ y2, int64_t Bn,
                                 double *__restrict__ Rout, double *__restrict__ tout,
                                 int32_t *__restrict__ found) {
@@ -198,7 +198,7 @@ __global__ void k_relative_pose(const double *__restrict__ Es, const double *__r
   for (int r = 0; r < 3; ++r) tout[3 * i + r] = which ? tw[r] : __builtin_nan("");
 }
 
-__global__ void k_fmatrix_cameras(const double *__restrict__ F, int64_t B,
+__global__ __launch_bounds__(128) void k_fmatrix_cameras(const double *__restrict__ F, int64_t B,
                                   double *__restrict__ C1) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= B) return;
@@ -210,7 +210,7 @@ __global__ void k_fmatrix_cameras(const double *__restrict__ F, int64_t B,
   for (int q = 0; q < 12; ++q) C1[12 * i + q] = c[q];
 }
 
-__global__ void k_fmatrix_from_cameras(const double *__restrict__ C1s,
+__global__ __launch_bounds__(128) void k_fmatrix_from_cameras(const double *__restrict__ C1s,
                                        const double *__restrict__ C2s, int64_t B,
                                        double *__restrict__ F) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -340,6 +340,7 @@ __global__ __launch_bounds__(kGsT) void k_gold_standard(
     double *__restrict__ C1out, GsInfo *__restrict__ info) {
   __shared__ double red[kGsW * 94];
   __shared__ double sU[78], sgc[12], sres[94], sC[12], sdc[12];
+  __shared__ double S[12][13];  // damped Schur complement, Cholesky in place (thread 0)
   __shared__ double s_lam, s_nu, s_cost, s_cost0;
   __shared__ int s_state, s_it, s_acc, s_status;
   const int tid = threadIdx.x;
@@ -438,7 +439,7 @@ __global__ __launch_bounds__(kGsT) void k_gold_standard(
     }
     if (tid == 0) {
       // S = U + lam diag(U) - sum W Vi W^T;  rhs = -gc + sum W Vi gx;  Cholesky
-      double S[12][12], y[12];
+      double y[12];
       for (int p = 0; p < 12; ++p)
         for (int q = p; q < 12; ++q) {
           double v = sU[up12(p, q)] - sres[up12(p, q)];

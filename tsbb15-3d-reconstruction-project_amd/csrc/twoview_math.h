@@ -226,6 +226,12 @@ __device__ __forceinline__ void triangulate_linear(const double *C1, const doubl
 // zeros are stripped, trailing zeros give zero roots (appended last); the other roots by
 // Aberth-Ehrlich iteration in complex float64.  Writes the real parts (lab3.py:442 takes
 // np.real of every root) and returns how many there are.
+//
+// Start points: per edge of the Newton polygon (upper convex hull of (k, log|b_k|), b the
+// ascending coefficients) m = k2 - k1 points on the circle |z| = (|b_k1| / |b_k2|)^(1/m), so
+// roots of very different magnitude (here ~1e-12 .. ~1e8) each start near their own circle.
+// A root is frozen once |p(z)| is within the rounding error of its Horner evaluation
+// (8 eps sum |a_j| |z|^j) or its correction is below 2 eps |z|; 4-11 sweeps on the goldens.
 // ----------------------------------------------------------------------------------------
 __device__ __forceinline__ int roots_real_parts(const double (&g)[7], double (&out)[6]) {
   int lo = 0;
@@ -235,76 +241,90 @@ __device__ __forceinline__ int roots_real_parts(const double (&g)[7], double (&o
   while (g[hi] == 0.0) --hi;
   const int trailing = 6 - hi;
   const int deg = hi - lo;
-  double a[7];  // monic: t^deg + a[1] t^(deg-1) + ... + a[deg]
+  double a[7];  // monic, descending: z^deg + a[1] z^(deg-1) + ... + a[deg]
   for (int k = 0; k <= deg; ++k) a[k] = g[lo + k] / g[lo];
   double zr[6], zi[6];
   if (deg > 0) {
-    // initial guesses on a circle of radius 2 max |a_k|^(1/k) (Fujiwara bound)
-    double rad = 0.0;
+    double lg[7];  // log |b_k|, b_k = a[deg - k] (ascending)
+    for (int k = 0; k <= deg; ++k) {
+      const double v = fabs(a[deg - k]);
+      lg[k] = v > 0.0 ? log(v) : -1.0e300;
+    }
+    int hull[7], nh = 0;
+    hull[nh++] = 0;
     for (int k = 1; k <= deg; ++k) {
-      const double v = pow(fabs(a[k]), 1.0 / k);
-      rad = v > rad ? v : rad;
+      if (lg[k] == -1.0e300) continue;
+      while (nh >= 2) {
+        const int k1 = hull[nh - 2], k2 = hull[nh - 1];
+        if ((lg[k2] - lg[k1]) * (k - k1) <= (lg[k] - lg[k1]) * (k2 - k1))
+          --nh;
+        else
+          break;
+      }
+      hull[nh++] = k;
     }
-    rad = rad > 0.0 ? 2.0 * rad : 1.0;
-    for (int k = 0; k < deg; ++k) {
-      const double ang = 6.283185307179586 * k / deg + 0.4;
-      zr[k] = rad * cos(ang);
-      zi[k] = rad * sin(ang);
+    int q = 0;
+    for (int e = 0; e + 1 < nh; ++e) {
+      const int m = hull[e + 1] - hull[e];
+      const double rad = exp((lg[hull[e]] - lg[hull[e + 1]]) / m);
+      for (int u = 0; u < m; ++u) {
+        const double ang = 6.283185307179586 * u / m + 6.283185307179586 * e / deg + 0.4;
+        zr[q] = rad * cos(ang);
+        zi[q] = rad * sin(ang);
+        ++q;
+      }
     }
-    for (int it = 0; it < 500; ++it) {
-      bool done = true;
+    unsigned conv = 0, all = (1u << deg) - 1u;
+    for (int it = 0; it < 100 && conv != all; ++it) {
       for (int k = 0; k < deg; ++k) {
-        // p(z), p'(z) by Horner
-        double pr = 1.0, pi = 0.0, dr = 0.0, di = 0.0;
+        if (conv & (1u << k)) continue;
+        const double xr = zr[k], xi = zi[k];
+        const double az = sqrt(xr * xr + xi * xi);
+        double pr = 1.0, pi = 0.0, dr = 0.0, di = 0.0, S = 1.0;
         for (int j = 1; j <= deg; ++j) {
-          const double ndr = dr * zr[k] - di * zi[k] + pr, ndi = dr * zi[k] + di * zr[k] + pi;
+          const double ndr = dr * xr - di * xi + pr, ndi = dr * xi + di * xr + pi;
           dr = ndr;
           di = ndi;
-          const double npr = pr * zr[k] - pi * zi[k] + a[j], npi = pr * zi[k] + pi * zr[k];
+          const double npr = pr * xr - pi * xi + a[j], npi = pr * xi + pi * xr;
           pr = npr;
           pi = npi;
+          S = S * az + fabs(a[j]);
         }
-        if (pr == 0.0 && pi == 0.0) continue;
-        // ratio = p / p'
-        double rr, ri;
-        {
-          const double den = dr * dr + di * di;
-          if (den == 0.0) {
-            rr = pr;
-            ri = pi;
-          } else {
-            rr = (pr * dr + pi * di) / den;
-            ri = (pi * dr - pr * di) / den;
-          }
+        if (sqrt(pr * pr + pi * pi) <= 8.0 * 2.220446049250313e-16 * S) {
+          conv |= 1u << k;
+          continue;
         }
-        // s = sum_{j != k} 1 / (z_k - z_j)
-        double sr = 0.0, si = 0.0;
+        double rr, ri;  // p / p'
+        const double den = dr * dr + di * di;
+        if (den == 0.0) {
+          rr = pr;
+          ri = pi;
+        } else {
+          rr = (pr * dr + pi * di) / den;
+          ri = (pi * dr - pr * di) / den;
+        }
+        double sr = 0.0, si = 0.0;  // sum_{j != k} 1 / (z_k - z_j)
         for (int j = 0; j < deg; ++j) {
           if (j == k) continue;
-          const double xr = zr[k] - zr[j], xi = zi[k] - zi[j];
-          const double den = xr * xr + xi * xi;
-          if (den > 0.0) {
-            sr += xr / den;
-            si -= xi / den;
+          const double ur = xr - zr[j], ui = xi - zi[j];
+          const double dd = ur * ur + ui * ui;
+          if (dd > 0.0) {
+            sr += ur / dd;
+            si -= ui / dd;
           }
         }
-        // w = ratio / (1 - ratio * s)
         const double qr = 1.0 - (rr * sr - ri * si), qi = -(rr * si + ri * sr);
         const double qd = qr * qr + qi * qi;
-        double wr, wi;
-        if (qd == 0.0) {
-          wr = rr;
-          wi = ri;
-        } else {
+        double wr = rr, wi = ri;
+        if (qd != 0.0) {
           wr = (rr * qr + ri * qi) / qd;
           wi = (ri * qr - rr * qi) / qd;
         }
-        zr[k] -= wr;
-        zi[k] -= wi;
-        const double az = fabs(zr[k]) + fabs(zi[k]);
-        if (fabs(wr) + fabs(wi) > 4.0e-16 * az) done = false;
+        zr[k] = xr - wr;
+        zi[k] = xi - wi;
+        if (fabs(wr) + fabs(wi) <= 2.0 * 2.220446049250313e-16 * (fabs(zr[k]) + fabs(zi[k])))
+          conv |= 1u << k;
       }
-      if (done) break;
     }
   }
   for (int k = 0; k < deg; ++k) out[k] = zr[k];
