@@ -174,6 +174,31 @@ int rs_pnp_ransac(rs_ctx *ctx, const double *X_med, const double *y_med, int64_t
                   int64_t *inl_high, int64_t *n_inl_high);
 
 /* ------------------------------------------------------------------------------------------
+ * Batched RANSAC-F over many image pairs (config C4; fun.py:298-328 per pair)
+ * ---------------------------------------------------------------------------------------- */
+typedef struct rs_pair_result {
+  double F[9];            /* F_RANSAC of the pair (NaN if none)                          */
+  int64_t best_index;     /* winning hypothesis, -1 if none (N < 8 or no consensus)      */
+  int64_t best_count;     /* len(S_RANSAC)                                               */
+  double best_std;        /* d_RANSAC = np.std(d)                                        */
+  double best_norm;       /* np.linalg.norm(d) of the winner                             */
+  int64_t n_candidates;   /* hypotheses with count == c*                                 */
+} rs_pair_result;
+
+/* H hypotheses for each of B pairs in one pass.  p1, p2: (2, total) point sets of all pairs
+ * concatenated, pair b = columns off[b] .. off[b+1]-1 (off: B+1 entries, off[0] = 0).
+ * Philox mode: pair b draws from seed_base + id_b with counters 0..H-1 (the stream of
+ * rs_f8_plan_run(seed = seed_base + id_b)), id_b = seed_ids[b] or b when seed_ids is NULL;
+ * tuple mode: host_tuples (B, H, 8) int32.  Pairs with
+ * N < 8 are skipped (best_index -1).  Counts use the reference-order float64 distance.
+ * out (B); inliers (total) int32: S_RANSAC of pair b at inliers[off[b] .. off[b]+count-1]. */
+int rs_pairs_f8_ransac(rs_ctx *ctx, const double *p1, const double *p2, const int64_t *off,
+                       int64_t B, int64_t H, int32_t mode, uint64_t seed_base,
+                       const int64_t *seed_ids, const int32_t *host_tuples, double thresh,
+                       rs_pair_result *out,
+                       int32_t *inliers);
+
+/* ------------------------------------------------------------------------------------------
  * Two-view geometry after RANSAC (fun.py:91-102, 209-280, 336-369; lab3.py:331-475)
  * ---------------------------------------------------------------------------------------- */
 

@@ -105,12 +105,9 @@ def test_dino_ring_pipeline_poses(ctx):
     the reference's chirality convention, pinned by clean_data_eval / twoview.npz pose_t."""
     z = golden("dino_pnp_kat.npz")
     pairs = _dino_pairs()
-    solver = parallel.GpuPairSolver(ctx, 1000)
+    solver = parallel.GpuPairBatchSolver(ctx, 1000)
     refiner = parallel.GpuPairRefiner(ctx, z["K_last"])
-    try:
-        tab = parallel.run_pairs(_Solo(), pairs, 1000, solver, refine=refiner)
-    finally:
-        solver.close()
+    tab = parallel.run_pairs(_Solo(), pairs, 1000, solver, refine=refiner)
     ij = list(itertools.combinations(range(36), 2))
     valid = np.flatnonzero(tab["valid"] == 1)
     assert len(valid) == 203 and np.all(tab["refined"][valid] == 1)

@@ -39,8 +39,12 @@ solver = parallel.GpuPairSolver(ctx, 1000)
 refiner = parallel.GpuPairRefiner(ctx, z["K_last"])
 dt0, _ = t(lambda: parallel.run_pairs(Solo(), pairs, 1000, solver))
 dt1, tab = t(lambda: parallel.run_pairs(Solo(), pairs, 1000, solver, refine=refiner))
-print(f"C4 ransac only: {dt0*1e3:.1f} ms; ransac+gold+pose: {dt1*1e3:.1f} ms "
+print(f"C4 per-pair plans: ransac only: {dt0*1e3:.1f} ms; ransac+gold+pose: {dt1*1e3:.1f} ms "
       f"(203 valid pairs)")
+bsolver = parallel.GpuPairBatchSolver(ctx, 1000)
+dt0, _ = t(lambda: parallel.run_pairs(Solo(), pairs, 1000, bsolver))
+dt1, tab = t(lambda: parallel.run_pairs(Solo(), pairs, 1000, bsolver, refine=refiner))
+print(f"C4 batched: ransac only: {dt0*1e3:.1f} ms; ransac+gold+pose: {dt1*1e3:.1f} ms")
 
 p1, p2, _ = synth.two_view(2000, 0.3, seed=1)
 res = fun.ransac_f(p1, p2, r=10000, rng=np.random.RandomState(0))

@@ -46,6 +46,12 @@ class PnpResult(C.Structure):
                 ("best_count", C.c_int64)]
 
 
+class PairResult(C.Structure):
+    _fields_ = [("F", C.c_double * 9), ("best_index", C.c_int64), ("best_count", C.c_int64),
+                ("best_std", C.c_double), ("best_norm", C.c_double),
+                ("n_candidates", C.c_int64)]
+
+
 class GsInfo(C.Structure):
     _fields_ = [("cost_init", C.c_double), ("cost", C.c_double), ("iterations", C.c_int32),
                 ("accepted", C.c_int32), ("status", C.c_int32), ("n", C.c_int32)]
@@ -83,6 +89,9 @@ _SIGS = {
     "rs_pnp_ransac": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, _dp, C.c_int64, C.c_int32,
                                 C.c_int64, C.c_int32, C.c_uint64, _i32p, C.c_double,
                                 C.POINTER(PnpResult), _i64p, _i64p, _i64p, _i64p]),
+    "rs_pairs_f8_ransac": (C.c_int, [C.c_void_p, _dp, _dp, _i64p, C.c_int64, C.c_int64,
+                                     C.c_int32, C.c_uint64, _i64p, _i32p, C.c_double,
+                                     C.POINTER(PairResult), _i32p]),
     "rs_triangulate_optimal": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, _dp, _i32p,
                                          C.c_int64, _dp]),
     "rs_camera_resectioning": (C.c_int, [C.c_void_p, _dp, C.c_int64, _dp, _dp, _dp]),

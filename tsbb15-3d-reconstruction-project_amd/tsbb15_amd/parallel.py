@@ -215,6 +215,24 @@ class GpuPairSolver:
         self.plans = {}
 
 
+class GpuPairBatchSolver:
+    """All of this rank's pairs in one batched pass (rs_pairs_f8_ransac): same Philox stream
+    per pair as GpuPairSolver (seed_base + pair index), so the results are identical; the
+    solve / count / select stages each run as one launch over every pair."""
+
+    def __init__(self, ctx, H, seed_base=1000, thresh=1.5):
+        self.ctx, self.H, self.seed_base, self.thresh = ctx, int(H), seed_base, thresh
+
+    def many(self, ids, pairs):
+        from . import pairs as pairs_mod
+        if not ids:
+            return []
+        rr = pairs_mod.ransac_pairs(pairs, self.H, self.seed_base, self.thresh, ids=ids,
+                                    ctx=self.ctx)
+        return [(1 if r.best_index >= 0 else 0, r.best_index, r.count, r.std, r.F.ravel(),
+                 r.inliers) for r in rr]
+
+
 class GpuPairRefiner:
     """After RANSAC, for all of this rank's pairs in one launch each: the gold standard
     (fun.py:336-369) on the inliers, then -- given the calibration K -- E = K^T F_gold K and
@@ -260,11 +278,14 @@ def run_pairs(comm, pairs, H, solve, refine=None):
     for f in ("F_gold", "gs_cost", "R", "t"):
         recs[f] = np.nan
     items = []
-    for i in owners[comm.rank]:
+    mine = [i for i in owners[comm.rank] if pairs[i][0].shape[1] >= 8]
+    if hasattr(solve, "many"):
+        results = dict(zip(mine, solve.many(mine, [pairs[i] for i in mine])))
+    else:
+        results = {i: solve(i, *pairs[i]) for i in mine}
+    for i in mine:
         p1, p2 = pairs[i]
-        if p1.shape[1] < 8:
-            continue
-        out = solve(i, p1, p2)
+        out = results[i]
         valid, best, count, std, F = out[:5]
         recs[i]["pair"], recs[i]["valid"], recs[i]["best_index"] = i, valid, best
         recs[i]["count"], recs[i]["std"], recs[i]["F"] = count, std, F
