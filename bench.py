@@ -86,21 +86,35 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def cpu_baseline(p1, p2, budget_s):
-    """Oracle (numpy restatement of fun.py:303-328) on one host core, bounded sample."""
+def _cpu_worker(args):
+    """One host core: the oracle loop (numpy restatement of fun.py:303-328) for budget_s."""
+    p1, p2, seed, budget_s = args
     from oracle import ransac_ref
-    rs = np.random.RandomState(0)
+    rs = np.random.RandomState(seed)
     done, t0 = 0, time.perf_counter()
-    chunk = 250
     while True:
-        ransac_ref.ransac_f(p1, p2, r=chunk, rng=rs)
-        done += chunk
+        ransac_ref.ransac_f(p1, p2, r=250, rng=rs)
+        done += 250
         el = time.perf_counter() - t0
         if el >= budget_s:
-            break
-    return {"value": done / el, "unit": "hypotheses/s", "cores": 1, "kind": "port",
-            "sample": f"{done} hypotheses of the same C2 pair (N={p1.shape[1]}) through "
-                      f"oracle/ransac_ref.ransac_f (numpy, OpenBLAS 1 thread) in {el:.1f} s"}
+            return done, el
+
+
+def cpu_baseline(p1, p2, budget_s, procs):
+    """Oracle CPU baseline on the box's host cores, bounded sample: one process per core
+    (independent seeds, BLAS threads = 1), forked BEFORE the GPU is initialised; plus the
+    single-core figure."""
+    import multiprocessing as mp
+    one = _cpu_worker((p1, p2, 0, budget_s / 2))
+    with mp.get_context("fork").Pool(procs) as pool:
+        res = pool.map(_cpu_worker, [(p1, p2, 1 + k, budget_s) for k in range(procs)])
+    agg = sum(d / e for d, e in res)
+    return {"value": agg, "unit": "hypotheses/s", "cores": procs, "kind": "port",
+            "single_core_value": one[0] / one[1],
+            "sample": f"{sum(d for d, _ in res)} hypotheses of the same C2 pair "
+                      f"(N={p1.shape[1]}) through oracle/ransac_ref.ransac_f (numpy, OpenBLAS "
+                      f"1 thread) in {procs} processes x {budget_s:.0f} s; single core: "
+                      f"{one[0]} hypotheses in {one[1]:.1f} s"}
 
 
 class _CtxComm:
@@ -254,6 +268,8 @@ def main():
     ap.add_argument("--hyps", type=int, default=HYPS)
     ap.add_argument("--n", type=int, default=N_CORR)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-procs", type=int,
+                    default=int(os.environ.get("RSAMD_CPU_PROCS", "16")))  # the box's CPU share
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity-mode", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
@@ -263,6 +279,11 @@ def main():
     if world != args.gpus and not (world == 1 and args.gpus == 1):
         print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
     dist = Dist(world)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # before any HIP call: the worker processes are forked from this one
+        cp1, cp2, _ = synth.two_view(args.n, OUTLIERS, seed=1)
+        cpu = cpu_baseline(cp1, cp2, args.cpu_seconds, args.cpu_procs)
     ctx = _ffi.Context(local_rank)
 
     # one synthetic pair per rank (weak scaling: per-GPU work fixed)
@@ -375,8 +396,8 @@ def main():
         line["parity_mode"] = {"value": H / min(ts), "unit": "hypotheses/s",
                                "note": "np.random legacy stream replayed bit-exactly on one "
                                        "host core, then the GPU pipeline; host-sampler bound"}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(p1, p2, args.cpu_seconds)
+    if cpu is not None:
+        line["cpu_baseline"] = cpu
     if not args.no_extras:
         ex = extras(ctx, rank, world, dist,
                     _CtxComm(ctx, rank, world) if comm else None)
