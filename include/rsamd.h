@@ -251,6 +251,40 @@ int rs_gold_standard(rs_ctx *ctx, const double *F, const double *pl, const doubl
                      double *C1_out, double *X_out, rs_gs_info *info);
 
 /* ------------------------------------------------------------------------------------------
+ * Per-view SfM steps around PnP (tables.py, fun.py:12-21)
+ * ---------------------------------------------------------------------------------------- */
+
+/* The 2D<->3D matching loop of Tables.addNewView (tables.py:116-135): for each query (n, 3)
+ * (C-normalised homogeneous y1), the point index obs_point[k] of the FIRST observation k of
+ * obs (m, 3) -- the last view's observations in observations_index order -- with
+ * ||obs_k - query|| < tol, else -1.  out: (n) int64. */
+int rs_match_observations(rs_ctx *ctx, const double *obs, const int64_t *obs_point, int64_t m,
+                          const double *queries, int64_t n, double tol, int64_t *out);
+
+/* fun.getEFromCameras (fun.py:12-21), batched: C1, C2 (n, 3, 4) = [R | t] -> E (n, 3, 3). */
+int rs_e_from_cameras(rs_ctx *ctx, const double *C1, const double *C2, int64_t n, double *E);
+
+/* Tables.addNewPoints (tables.py:161-175) without the table bookkeeping: C1, C2 (3, 4) the two
+ * views' [R | t]; y1, y2 (n, 3) C-normalised homogeneous putative correspondences.
+ * mask (n) int32 = |y1^T E y2| < gate; X (n, 3) = lab3.triangulate_optimal of the accepted
+ * (NaN where rejected). */
+int rs_add_new_points(rs_ctx *ctx, const double *C1, const double *C2, const double *y1,
+                      const double *y2, int64_t n, double gate, int32_t *mask, double *X);
+
+/* EpsilonBA of Tables.BundleAdjustment2 (tables.py:264-293): cams (nC, 3, 4) as 12 free
+ * parameters each, pts (nP, 3), observations (obs_view, obs_point int32, uv (n, 2)).
+ * r (2n) = interleaved [u - c1.x / c3.x, v - c2.x / c3.x]. */
+int rs_ba_residuals(rs_ctx *ctx, const double *cams, int64_t nC, const double *pts, int64_t nP,
+                    const int32_t *obs_view, const int32_t *obs_point, const double *uv,
+                    int64_t n, double *r);
+
+/* Jacobian blocks of rs_ba_residuals per observation (the nonzeros of Tables.sparsity_mask,
+ * tables.py:339-372): Jc (n, 2, 12) w.r.t. the camera's row-major entries, Jp (n, 2, 3). */
+int rs_ba_jacobian(rs_ctx *ctx, const double *cams, int64_t nC, const double *pts, int64_t nP,
+                   const int32_t *obs_view, const int32_t *obs_point, int64_t n, double *Jc,
+                   double *Jp);
+
+/* ------------------------------------------------------------------------------------------
  * Multi-GPU (RCCL over xGMI).  One process per GPU; the unique id travels out of band.
  * ---------------------------------------------------------------------------------------- */
 #define RS_COMM_ID_BYTES 128

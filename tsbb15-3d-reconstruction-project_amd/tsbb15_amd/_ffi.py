@@ -102,6 +102,15 @@ _SIGS = {
     "rs_fmatrix_from_cameras": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp]),
     "rs_gold_standard": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _i64p, C.c_int64, C.c_int32, _dp,
                                    _dp, _dp, C.POINTER(GsInfo)]),
+    "rs_match_observations": (C.c_int, [C.c_void_p, _dp, _i64p, C.c_int64, _dp, C.c_int64,
+                                        C.c_double, _i64p]),
+    "rs_e_from_cameras": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp]),
+    "rs_add_new_points": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp, C.c_int64, C.c_double, _i32p,
+                                    _dp]),
+    "rs_ba_residuals": (C.c_int, [C.c_void_p, _dp, C.c_int64, _dp, C.c_int64, _i32p, _i32p, _dp,
+                                  C.c_int64, _dp]),
+    "rs_ba_jacobian": (C.c_int, [C.c_void_p, _dp, C.c_int64, _dp, C.c_int64, _i32p, _i32p,
+                                 C.c_int64, _dp, _dp]),
     "rs_comm_unique_id": (C.c_int, [_u8p]),
     "rs_comm_init": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, _u8p]),
     "rs_comm_destroy": (C.c_int, [C.c_void_p]),
