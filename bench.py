@@ -240,6 +240,33 @@ def extras(ctx, rank, world, dist, comm):
                         float(c1["noisy_full_seconds"]))}
     except Exception as e:  # noqa: BLE001
         out["gold_standard_c2"] = {"error": repr(e)}
+    # ---- per-view table steps (tables.py:116-175, 260-380) at the reference's noisy sizes ----
+    try:
+        from tsbb15_amd import tables as gt
+        z = np.load(os.path.join(REPO, "tests", "golden", "tables.npz"))
+        g = lambda k: z["noisy_" + k]
+        nC, nP = int(g("ba_n_views")), int(g("ba_n_points"))
+        x = g("ba_x_final")
+        cams, pts = x[:12 * nC].reshape(nC, 3, 4), x[12 * nC:].reshape(nP, 3)
+        view, point, uv = g("ba_obs_view"), g("ba_obs_point"), g("ba_obs_coords")[:, :2]
+        steps = {
+            "match_observations": lambda: gt.match_observations(
+                g("match_obs_coords"), g("match_obs_point"), g("match_queries")),
+            "add_new_points": lambda: gt.add_new_points(g("new_y1_hom"), g("new_y2_hom"),
+                                                         g("new_C1"), g("new_C2")),
+            "ba_residuals": lambda: gt.ba_residuals(cams, pts, view, point, uv),
+            "ba_jacobian": lambda: gt.ba_jacobian(cams, pts, view, point),
+        }
+        rec = {}
+        for name, f in steps.items():
+            f()
+            rec[name + "_ms"] = _best_of(f, 10)[0] * 1e3
+        rec.update({"observations": int(len(view)), "queries": int(len(g("match_queries"))),
+                    "new_points": int(len(g("new_y1_hom"))),
+                    "note": "one host call each (H2D + launch + D2H), latency-bound sizes"})
+        out["tables_noisy"] = rec
+    except Exception as e:  # noqa: BLE001
+        out["tables_noisy"] = {"error": repr(e)}
     return out
 
 
