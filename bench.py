@@ -270,6 +270,12 @@ def extras(ctx, rank, world, dist, comm):
     return out
 
 
+# counting kernel behind each RSAMD_COUNT choice (f8_plan.hip; "q" is the default)
+COUNT_KERNEL = {"q": "k_f8_count32q", "w": "k_f8_count32x", "x": "k_f8_count32x",
+                "y": "k_f8_count32x", "z": "k_f8_count32x", "fp32": "k_f8_count32",
+                "pk": "k_f8_count32p", "fp64": "k_f8_count"}
+
+
 def load_pmc(n_corr, hyps):
     """HBM bytes per counting launch from the newest committed rocprofv3 PMC summary."""
     import glob
@@ -389,7 +395,8 @@ def main():
                                "threshold 1.5 px",
                    "n_corr": args.n, "hypotheses_per_step": H, "sampler": "philox (throughput)",
                    "parallelism": f"pairs sharded, {world} pair(s) on {world} GPU(s)"},
-        "roofline": {"bound": "valu", "kernel": "k_f8_count32x",
+        "roofline": {"bound": "valu", "kernel": COUNT_KERNEL.get(os.environ.get("RSAMD_COUNT", "q"),
+                                                          "k_f8_count32"),
                      "achieved": achieved, "peak": PEAK_FP32_VALU_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_FP32_VALU_TFLOPS,
                      "frac_of_fp64_peak": achieved / PEAK_FP64_VALU_TFLOPS,

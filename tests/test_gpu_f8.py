@@ -218,9 +218,9 @@ def _near_threshold_points(F, p1, p2, deltas, rng, keep):
     return p2
 
 
-# counting kernels: x / y = packed-pair fp32 with packed / plain decision, fp32 = scalar fp32, pk = two hypotheses
+# counting kernels: q = point-pair packed (default), w / x / y = packed-pair fp32 with packed / plain decision, fp32 = scalar fp32, pk = two hypotheses
 # per lane, fp64 = the float64 reference-order kernel every fp32 variant must match exactly
-COUNT_MODES = ("w", "x", "y", "z", "fp32", "pk", "fp64")
+COUNT_MODES = ("q", "w", "x", "y", "z", "fp32", "pk", "fp64")
 
 
 def test_fp32_guard_band_exact_near_threshold(ctx, monkeypatch):

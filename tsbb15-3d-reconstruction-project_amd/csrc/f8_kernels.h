@@ -88,6 +88,14 @@ hipError_t launch_f8_count32x(const float4 *pts32, const Pt *pts, int n, int H,
                               const Guard &g, int *counts, hipStream_t s, int blk = 8,
                               bool prefetch = true, int *gdone = nullptr,
                               int *status = nullptr, const float4 *G4 = nullptr);
+// Point-pair packed fp32 counting (DEC 3 decisions, bit-identical to launch_f8_count32x<GuardW>);
+// ptsq in the k_pack_points32q layout.
+hipError_t launch_pack_points32q(const Pt *pts, int n, const Frame &fr, float4 *ptsq,
+                                 hipStream_t s);
+hipError_t launch_f8_count32q(const float4 *ptsq, const Pt *pts, int n, int H,
+                              const float *F32soa, const double *Fsoa, int64_t ld, int waves,
+                              const GuardW &g, int *counts, hipStream_t s, int *gdone,
+                              int *status, const float4 *G4);
 hipError_t launch_f8_count(const Pt *pts, int n, int H, const double *Fsoa, int64_t ld,
                            int chunk, double thr2, int *counts, hipStream_t s);
 // Selection tail: c* (k_f8_max, unless the counting kernel fused it), candidates + reference

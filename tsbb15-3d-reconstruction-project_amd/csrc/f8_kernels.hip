@@ -542,6 +542,169 @@ __global__ __launch_bounds__(256) void k_f8_count32x(const float4 *__restrict__ 
 }
 
 // ----------------------------------------------------------------------------------------
+// Point-pair variant ("q").  k_f8_count32x packs the two epipolar lines of ONE point, so the
+// four scalar FMAs of l12 and e cannot pair up.  Here every packed op carries the SAME
+// quantity of TWO consecutive points instead (points 2j and 2j+1 of a block, one aligned
+// SGPR pair per coordinate, k_pack_points32q layout):
+//   a  = fma(F0, X2, fma(F1, Y2, F2))     b  = fma(F3, X2, fma(F4, Y2, F5))
+//   l3 = fma(F6, X2, fma(F7, Y2, F8))     e  = fma(a, X1, fma(b, Y1, l3))
+//   c  = fma(F0, X1, fma(F3, Y1, F6))     d  = fma(F1, X1, fma(F4, Y1, F7))
+//   n1 = fma(a, a, b*b)   n2 = fma(c, c, d*d)   m = min(n1, n2) (two v_min)
+//   P  = fma(e, e, ki)    Q  = fma(e, e, -ko)   R = alpha m   S = beta m
+// Each lane value is the same IEEE expression, in the same order, as k_f8_count32x DEC 3
+// (A.x = a, A.y = c, Bv.x = b, Bv.y = d, N = (n1, n2), l12 = l3), so the DEC 3 guard band
+// and its per-hypothesis constants hold unchanged and the decisions are bit-identical.
+// Per point pair: 12 pk (a, b, l3, e, c, d) + 4 pk (n1, n2) + 2 min + 4 pk (P, Q, R, S) +
+// 4 cmp + 2 add = 28 VALU, 14 per (64 hypotheses x point) against DEC 3's 16.  The splat
+// coefficients are op_sel broadcasts inside one asm block per pair (pair_terms), and the
+// float64 re-test of an ambiguous pair runs right there, so the pair loop holds 54 VGPRs.
+// ----------------------------------------------------------------------------------------
+typedef float f2q __attribute__((ext_vector_type(2)));
+// v_pk_fma_f32 with a broadcast half of a VGPR pair as src0 (and optionally src2) and an
+// SGPR point pair as src1.  OPSEL / OPSELHI pick, per result lane, the half of each source.
+#define RSD_PKFMA_BSV(d, a, b, c, OPSEL, OPSELHI)                                        \
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:" OPSEL " op_sel_hi:" OPSELHI                  \
+      : "=v"(d) : "v"(a), "s"(b), "v"(c))
+#define RSD_PKFMA_VVB(d, a, b, c, OPSEL, OPSELHI)                                        \
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:" OPSEL " op_sel_hi:" OPSELHI                  \
+      : "=v"(d) : "v"(a), "v"(b), "v"(c))
+#define RSD_PKMUL_VB(d, a, b, OPSEL, OPSELHI)                                             \
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel:" OPSEL " op_sel_hi:" OPSELHI : "=v"(d) : "v"(a), "v"(b))
+
+// The k_f8_count32q terms of one point pair (expressions and order as documented above the
+// kernel); P01 = (F0, F1), P23 = (F2, F3), P45 = (F4, F5), P67 = (F6, F7), P8 = (F8, F8),
+// KIO = (ki, -ko), ALB = (alpha, beta).
+__device__ __forceinline__ void pair_terms(f2q P01, f2q P23, f2q P45, f2q P67, f2q P8, f2q KIO,
+                                           f2q ALB, f2q X2, f2q Y2, f2q X1, f2q Y1, f2q &P,
+                                           f2q &Q, f2q &R, f2q &S) {
+#pragma clang fp contract(off)
+  // One asm block from the point pair to (n1, n2, P, Q): the hazard recognizer treats every
+  // inline asm as a possible transcendental and pads its consumers with an s_nop, so the
+  // whole dependent chain is kept inside (plain VALU -> VALU dependencies interlock).
+  // t0..t4 are reused in place: t0 = F1 y2 + F2 -> a -> P, t1 = F4 y2 + F5 -> b -> b^2 -> n1,
+  // t2 = F7 y2 + F8 -> l3 -> b y1 + l3 -> e, t3 = F3 y1 + F6 -> c -> Q, t4 = F4 y1 + F7 -> d ->
+  // d^2 -> n2.
+  f2q t0, t1, t2, t3, t4;
+  asm("v_pk_fma_f32 %[t0], %[P01], %[Y2], %[P23] op_sel:[1,0,0] op_sel_hi:[1,1,0]\n\t"
+      "v_pk_fma_f32 %[t1], %[P45], %[Y2], %[P45] op_sel:[0,0,1] op_sel_hi:[0,1,1]\n\t"
+      "v_pk_fma_f32 %[t2], %[P67], %[Y2], %[P8] op_sel:[1,0,0] op_sel_hi:[1,1,0]\n\t"
+      "v_pk_fma_f32 %[t3], %[P23], %[Y1], %[P67] op_sel:[1,0,0] op_sel_hi:[1,1,0]\n\t"
+      "v_pk_fma_f32 %[t4], %[P45], %[Y1], %[P67] op_sel:[0,0,1] op_sel_hi:[0,1,1]\n\t"
+      "v_pk_fma_f32 %[t0], %[P01], %[X2], %[t0] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"  // a
+      "v_pk_fma_f32 %[t1], %[P23], %[X2], %[t1] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"  // b
+      "v_pk_fma_f32 %[t2], %[P67], %[X2], %[t2] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"  // l3
+      "v_pk_fma_f32 %[t3], %[P01], %[X1], %[t3] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"  // c
+      "v_pk_fma_f32 %[t4], %[P01], %[X1], %[t4] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"  // d
+      "v_pk_fma_f32 %[t2], %[t1], %[Y1], %[t2]\n\t"                                      // b y1 + l3
+      "v_pk_mul_f32 %[t1], %[t1], %[t1]\n\t"                                             // b^2
+      "v_pk_mul_f32 %[t4], %[t4], %[t4]\n\t"                                             // d^2
+      "v_pk_fma_f32 %[t2], %[t0], %[X1], %[t2]\n\t"                                      // e
+      "v_pk_fma_f32 %[t1], %[t0], %[t0], %[t1]\n\t"                                      // n1
+      "v_pk_fma_f32 %[t4], %[t3], %[t3], %[t4]\n\t"                                      // n2
+      "v_pk_fma_f32 %[t0], %[t2], %[t2], %[KIO] op_sel:[0,0,0] op_sel_hi:[1,1,0]\n\t"  // P
+      "v_pk_fma_f32 %[t3], %[t2], %[t2], %[KIO] op_sel:[0,0,1] op_sel_hi:[1,1,1]"        // Q
+      : [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4)
+      : [P01] "v"(P01), [P23] "v"(P23), [P45] "v"(P45), [P67] "v"(P67), [P8] "v"(P8),
+        [KIO] "v"(KIO), [X2] "s"(X2), [Y2] "s"(Y2), [X1] "s"(X1), [Y1] "s"(Y1));
+  P = t0;
+  Q = t3;
+  // m = min(n1, n2): both are >= +0 or NaN, where the unsigned order of the bit patterns is
+  // the float order and NaN loses, exactly as fminf (and no canonicalising v_max)
+  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+  const u2 mu = __builtin_elementwise_min(__builtin_bit_cast(u2, t1), __builtin_bit_cast(u2, t4));
+  const f2q m = __builtin_bit_cast(f2q, mu);
+  RSD_PKMUL_VB(R, m, ALB, "[0,0]", "[1,0]");  // alpha m
+  RSD_PKMUL_VB(S, m, ALB, "[0,1]", "[1,1]");  // beta m
+}
+
+__global__ __launch_bounds__(256) void k_f8_count32q(const float4 *__restrict__ ptsq,
+                                                     const Pt *__restrict__ pts, int n, int H,
+                                                     const float *__restrict__ F32soa,
+                                                     const double *__restrict__ Fsoa,
+                                                     int64_t ld, int64_t per_wave, GuardW g,
+                                                     int *__restrict__ counts,
+                                                     int *__restrict__ gdone,
+                                                     int *__restrict__ status,
+                                                     const float4 *__restrict__ G4) {
+#pragma clang fp contract(off)
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const int lane = threadIdx.x & 63;
+  const int64_t w = wave_uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int64_t npad = (n + 7) / 8 * 8;
+  const int64_t total = static_cast<int64_t>((H + 63) >> 6) * npad;
+  int64_t pos = w * per_wave;
+  const int64_t end = min(total, pos + per_wave);
+  while (pos < end) {
+    const int grp = static_cast<int>(pos / npad);
+    const int p0 = static_cast<int>(pos - grp * npad);
+    const int p1 = static_cast<int>(min(npad, p0 + (end - pos)));
+    pos += p1 - p0;
+    const int h = grp * 64 + lane;
+    const int hl = h < H ? h : H - 1;
+    float f[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) f[k] = F32soa[k * ld + hl];
+    // coefficient pairs; broadcasts of one half are op_sel operands (pkfma_* below), so no
+    // duplicated VGPRs (the compiler's splats cost 12 more and a wave of occupancy)
+    const f2 P01 = {f[0], f[1]}, P23 = {f[2], f[3]}, P45 = {f[4], f[5]}, P67 = {f[6], f[7]};
+    const f2 P8 = {f[8], f[8]};
+    const float4 q = G4[hl];
+    const f2 KIO = {q.x, q.y}, ALB = {q.z, q.w};
+    int cnt = 0;
+    for (int i = p0; i < p1; i += 8) {
+      float4 blk[8];  // (x2[8], y2[8], x1[8], y1[8]) of points i..i+7
+#pragma unroll
+      for (int k = 0; k < 8; ++k) blk[k] = ptsq[i + k];
+      const float *v = reinterpret_cast<const float *>(blk);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f2 X2 = {v[2 * j], v[2 * j + 1]}, Y2 = {v[8 + 2 * j], v[9 + 2 * j]};
+        const f2 X1 = {v[16 + 2 * j], v[17 + 2 * j]}, Y1 = {v[24 + 2 * j], v[25 + 2 * j]};
+        f2 P, Q, R, S;
+        pair_terms(P01, P23, P45, P67, P8, KIO, ALB, X2, Y2, X1, Y1, P, Q, R, S);
+        const unsigned long long i0 = __ballot(P.x < R.x), i1 = __ballot(P.y < R.y);
+        const unsigned long long l0 = __ballot(Q.x <= S.x), l1 = __ballot(Q.y <= S.y);
+        cnt = add_lane_bit(cnt, i0);  // sure inliers
+        cnt = add_lane_bit(cnt, i1);
+        const unsigned long long a0 = i0 ^ l0, a1 = i1 ^ l1;
+        if ((a0 | a1) != 0ull) {  // rare (~1 pair in 40): float64 re-test of the ambiguous lanes
+          // the opaque pointer keeps these loads (and their 18 VGPRs) inside the rare branch
+          const double *fp = Fsoa + hl;
+          asm volatile("" : "+v"(fp));
+          double fdd[9];
+#pragma unroll
+          for (int k = 0; k < 9; ++k) fdd[k] = fp[k * ld];
+          if ((a0 >> lane) & 1ull) cnt += test64(fdd, pts[i + 2 * j], g.thr2_px) ? 1 : 0;
+          if ((a1 >> lane) & 1ull) cnt += test64(fdd, pts[i + 2 * j + 1], g.thr2_px) ? 1 : 0;
+        }
+      }
+    }
+    if (h < H) atomicAdd(&counts[h], cnt);
+    if (gdone) group_done_max(counts, gdone, status, grp, p1 - p0, static_cast<int>(npad), h, H);
+  }
+}
+
+// Point-pair layout of k_f8_count32q: block b of 8 points is 32 floats
+// (x2[8], y2[8], x1[8], y1[8]) in the same unit frame as k_pack_points32; NaN padding.
+__global__ __launch_bounds__(256) void k_pack_points32q(const Pt *__restrict__ pts, int n,
+                                                        Frame fr, float *__restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ((n + 7) & ~7)) return;
+  float *o = out + 32 * (i >> 3) + (i & 7);
+  if (i >= n) {
+    const float qn = __builtin_nanf("");
+    o[0] = o[8] = o[16] = o[24] = qn;
+    return;
+  }
+  const Pt p = pts[i];
+  const double is = 1.0 / fr.s;
+  o[0] = static_cast<float>((p.x2 - fr.cx2) * is);
+  o[8] = static_cast<float>((p.y2 - fr.cy2) * is);
+  o[16] = static_cast<float>((p.x1 - fr.cx1) * is);
+  o[24] = static_cast<float>((p.y1 - fr.cy1) * is);
+}
+
+// ----------------------------------------------------------------------------------------
 // Packed variant: on gfx950 a wave64 v_fma_f32 issues at the float64 rate (4 cycles); only
 // v_pk_fma_f32 doubles fp32 throughput (tools/ubench/valu_rate.hip: 77 vs 154 TFLOP/s).  So
 // each lane carries TWO hypotheses (g*128 + lane and g*128 + 64 + lane) as a float2 and every
@@ -1049,6 +1212,28 @@ hipError_t launch_pack_points32(const Pt *pts, int n, const Frame &fr, float4 *p
                                 hipStream_t s) {
   hipLaunchKernelGGL(k_pack_points32, dim3((n + 7 + 255) / 256), dim3(256), 0, s, pts, n, fr,
                      pts32);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_points32q(const Pt *pts, int n, const Frame &fr, float4 *ptsq,
+                                 hipStream_t s) {
+  hipLaunchKernelGGL(k_pack_points32q, dim3((n + 7 + 255) / 256), dim3(256), 0, s, pts, n, fr,
+                     reinterpret_cast<float *>(ptsq));
+  return hipGetLastError();
+}
+
+hipError_t launch_f8_count32q(const float4 *ptsq, const Pt *pts, int n, int H,
+                              const float *F32soa, const double *Fsoa, int64_t ld, int waves,
+                              const GuardW &g, int *counts, hipStream_t s, int *gdone,
+                              int *status, const float4 *G4) {
+  const int64_t npad = (n + 7) / 8 * 8;
+  const int64_t total = static_cast<int64_t>((H + 63) / 64) * npad;
+  int64_t W = std::max<int64_t>(1, std::min<int64_t>(waves, total / 64));
+  int64_t per = (total + W - 1) / W;
+  per = (per + 7) / 8 * 8;
+  W = (total + per - 1) / per;
+  hipLaunchKernelGGL(k_f8_count32q, dim3(static_cast<unsigned>((W + 3) / 4)), dim3(256), 0, s,
+                     ptsq, pts, n, H, F32soa, Fsoa, ld, per, g, counts, gdone, status, G4);
   return hipGetLastError();
 }
 

@@ -147,6 +147,7 @@ struct rs_f8_plan {
   double *d_p12 = nullptr;     // staging (2,n) p1 then (2,n) p2
   rsd::Pt *d_pts = nullptr;    // AoS float64 points
   float4 *d_pts32 = nullptr;   // unit-frame fp32 points, NaN-padded to a multiple of 8
+  float4 *d_pts32q = nullptr;  // the same, point-pair layout (k_f8_count32q)
   static constexpr int kBufs = 2, kSlots = 4, kEvRing = 64;
   RunBufs buf[kBufs];
   // Each run's tail writes its result header into its own pinned slot (through the host
@@ -168,7 +169,8 @@ struct rs_f8_plan {
   bool pair = true;           // k_f8_count32x (default); RSAMD_COUNT=fp32: k_f8_count32
   bool plain_dec = false;     // RSAMD_COUNT=y: k_f8_count32x with the plain-op decision
   bool folded = false;        // RSAMD_COUNT=z: folded plain decision + SALU bit-plane counts
-  bool per_hyp = true;        // per-hypothesis AM-GM decision constants (default, "w")
+  bool per_hyp = true;        // per-hypothesis AM-GM decision constants ("w", "q")
+  bool pointpair = true;      // "q" (default): DEC 3 decisions, packed over point pairs
   bool fuse_max = true;       // RSAMD_FUSEMAX=0: separate k_f8_max pass instead of the fused c*
   // HIP timing events per run (each is a marker packet between kernels): 0 none, 1 around the
   // counting kernel (default; the bench's roofline timing), 2 also the tail+solve launch
@@ -193,6 +195,7 @@ static void plan_free(rs_f8_plan *p) {
   (void)hipFree(p->d_p12);
   (void)hipFree(p->d_pts);
   (void)hipFree(p->d_pts32);
+  (void)hipFree(p->d_pts32q);
   for (RunBufs &b : p->buf) {
     (void)hipFree(b.d_F);
     (void)hipFree(b.d_F32);
@@ -230,13 +233,14 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
   p->chunk_override = env_int("RSAMD_CHUNK", 0);
   if (const char *cm = std::getenv("RSAMD_COUNT")) {
     p->use_fp32 = std::strcmp(cm, "fp64") != 0;
-    p->packed = std::strcmp(cm, "pk") == 0;  // "w" (default), "x", "y", "z", "fp32", "pk", "fp64"
+    p->packed = std::strcmp(cm, "pk") == 0;  // "q" (default), "w", "x", "y", "z", "fp32", "pk", "fp64"
     p->pair = std::strcmp(cm, "x") == 0 || std::strcmp(cm, "y") == 0 ||
               std::strcmp(cm, "z") == 0;
-    p->pair = p->pair || std::strcmp(cm, "w") == 0;
+    p->pointpair = std::strcmp(cm, "q") == 0;
+    p->pair = p->pair || std::strcmp(cm, "w") == 0 || p->pointpair;
     p->plain_dec = std::strcmp(cm, "y") == 0;
     p->folded = std::strcmp(cm, "z") == 0;
-    p->per_hyp = std::strcmp(cm, "w") == 0;
+    p->per_hyp = std::strcmp(cm, "w") == 0 || p->pointpair;
   }
   p->fuse_max = env_int("RSAMD_FUSEMAX", 1) != 0;
   p->timing = env_int("RSAMD_TIMING", 1);
@@ -258,6 +262,7 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
   ALLOC(p->d_p12, sizeof(double) * 4 * n);
   ALLOC(p->d_pts, sizeof(rsd::Pt) * n);
   ALLOC(p->d_pts32, sizeof(float4) * ((n + 7) & ~7LL));
+  ALLOC(p->d_pts32q, sizeof(float4) * ((n + 7) & ~7LL));
   for (RunBufs &b : p->buf) {
     ALLOC(b.d_F, sizeof(double) * 9 * p->ld);
     ALLOC(b.d_F32, sizeof(float) * 9 * p->ld);
@@ -349,6 +354,8 @@ extern "C" int rs_f8_plan_set_points(rs_f8_plan *p, const double *p1, const doub
     fr.s *= 1.0 + 1e-12;  // |x~| <= 1 after the fp64 division
     p->frame = fr;
     HIP_TRY(rsd::launch_pack_points32(p->d_pts, static_cast<int>(n), fr, p->d_pts32, c->stream));
+    HIP_TRY(rsd::launch_pack_points32q(p->d_pts, static_cast<int>(n), fr, p->d_pts32q,
+                                       c->stream));
   }
   HIP_TRY(hipStreamSynchronize(c->stream));
   return RS_OK;
@@ -428,10 +435,15 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
   else if (fp32 && p->pair && p->per_hyp) {
     rsd::GuardW gw{thresh * thresh};
     if (env_int("RSAMD_NORECHECK", 0)) gw.thr2_px = -1.0;  // timing diagnostic only
-    HIP_TRY(rsd::launch_f8_count32x(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
-                                    p->resident_waves, gw, b.d_counts, ms, p->count_block,
-                                    p->prefetch, fused_max ? b.d_gdone : nullptr, b.d_status,
-                                    b.d_G4));
+    if (p->pointpair)
+      HIP_TRY(rsd::launch_f8_count32q(p->d_pts32q, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
+                                      p->resident_waves, gw, b.d_counts, ms,
+                                      fused_max ? b.d_gdone : nullptr, b.d_status, b.d_G4));
+    else
+      HIP_TRY(rsd::launch_f8_count32x(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
+                                      p->resident_waves, gw, b.d_counts, ms, p->count_block,
+                                      p->prefetch, fused_max ? b.d_gdone : nullptr, b.d_status,
+                                      b.d_G4));
   } else if (fp32 && p->pair && p->folded)
     HIP_TRY(rsd::launch_f8_count32x(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
                                     p->resident_waves, guard_folded(p->frame, thresh),
