@@ -120,6 +120,28 @@ __device__ __forceinline__ void floyd_sample(uint64_t seed, uint64_t h, int n, i
 }
 
 // ----------------------------------------------------------------------------------------
+// Reciprocal square root and reciprocal to float64 accuracy (a few ulp, not correctly
+// rounded) from the hardware estimates v_rsq_f64 / v_rcp_f64 and two Newton steps: ~6
+// dependent FMAs instead of the correctly rounded library sequences (range scaling, class
+// checks, div_scale / div_fixup).  The minimal solves are latency bound, and their parity
+// bar (1e-9 on F) is far above a few ulp.  x must be positive and finite.
+// ----------------------------------------------------------------------------------------
+__device__ __forceinline__ double rsqrt_fast(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  double r = fma(-x * y, y, 1.0);  // 1 - x y^2
+  y = fma(0.5 * y, r, y);
+  r = fma(-x * y, y, 1.0);
+  return fma(0.5 * y, r, y);
+}
+__device__ __forceinline__ double rcp_fast(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-x, y, 1.0);
+  return fma(y, e, y);
+}
+
+// ----------------------------------------------------------------------------------------
 // One-sided Jacobi SVD of a 3x3 matrix (row-major M).  On exit the columns of B = M V are
 // mutually orthogonal (their norms are the singular values) and V holds the right
 // singular vectors as columns.
@@ -129,11 +151,14 @@ __device__ __forceinline__ void jacobi_rot(double (&B)[9], double (&V)[9], int p
   const double a = B[p] * B[p] + B[3 + p] * B[3 + p] + B[6 + p] * B[6 + p];
   const double b = B[q] * B[q] + B[3 + q] * B[3 + q] + B[6 + q] * B[6 + q];
   const double g = B[p] * B[q] + B[3 + p] * B[3 + q] + B[6 + p] * B[6 + q];
-  if (fabs(g) > 1e-15 * sqrt(a * b)) {
+  if (g * g > 1e-30 * (a * b)) {  // |g| > 1e-15 sqrt(a b) without the square root
     rotated = true;
-    const double zeta = (b - a) / (2.0 * g);
-    const double t = copysign(1.0, zeta) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-    const double c = 1.0 / sqrt(1.0 + t * t);
+    const double zeta = (b - a) * (0.5 * rcp_fast(g));
+    // t = sign(zeta) / (|zeta| + sqrt(1 + zeta^2)); 1 / (2 zeta) where zeta^2 would overflow
+    const double az = fabs(zeta), z2 = fma(zeta, zeta, 1.0);
+    const double t = az < 1e150 ? copysign(rcp_fast(az + z2 * rsqrt_fast(z2)), zeta)
+                                : 0.5 * rcp_fast(zeta);
+    const double c = rsqrt_fast(fma(t, t, 1.0));
     const double s = c * t;
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
@@ -192,11 +217,11 @@ __device__ __forceinline__ void lq_null_vector(double (&A)[R][C], double (&q)[C]
     double ss = 0.0;
 #pragma unroll
     for (int j = k; j < C; ++j) ss = fma(A[k][j], A[k][j], ss);
-    const double nrm = sqrt(ss);
+    const double nrm = ss > 0.0 ? ss * rsqrt_fast(ss) : 0.0;
     const double akk = A[k][k];
     const double alpha = akk >= 0.0 ? -nrm : nrm;
     const double denom = nrm * (nrm + fabs(akk));  // = v.v / 2
-    const double tk = denom > 0.0 ? 1.0 / denom : 0.0;
+    const double tk = denom > 0.0 ? rcp_fast(denom) : 0.0;
     A[k][k] = akk - alpha;
     tau[k] = tk;
 #pragma unroll

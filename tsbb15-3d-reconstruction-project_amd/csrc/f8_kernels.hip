@@ -139,12 +139,15 @@ __device__ __forceinline__ void solve_one(const SolveArgs &a, int h) {
       const double u = 0x1p-24, T = a.gT, De = a.gDe, Dn = a.gDn;
       const double f02 = Ft[2] * kap, f12 = Ft[5] * kap, f20 = Ft[6] * kap, f21 = Ft[7] * kap;
       const double mc = fmin(f02 * f02 + f12 * f12, f20 * f20 + f21 * f21);
-      const double c = fmax(sqrt(T * fmax(mc, 1e-12)), 100.0 * De);
-      const double r = De / c;
-      const double alpha = T * (1.0 - u) / ((1.0 + u) * (1.0 + r)) * (1.0 - 4.0 * u);
-      const double beta = T * (1.0 + u) / ((1.0 - u) * (1.0 - r)) * (1.0 + 4.0 * u);
-      const double ki = 1.02 * (De * c + De * De + T * Dn) / (1.0 + r) + 1e-30;
-      const double ko = 1.02 * (T * Dn + De * c) / (1.0 - r) + 1e-30;
+      // (rsqrt_fast / rcp_fast: a few ulp, far inside the 1 -/+ 4u and 1.02 margins)
+      const double tm = T * fmax(mc, 1e-12);
+      const double c = fmax(tm * rsqrt_fast(tm), 100.0 * De);
+      const double r = De * rcp_fast(c);
+      const double ip = rcp_fast(1.0 + r), im = rcp_fast(1.0 - r);
+      const double alpha = T * (1.0 - u) * rcp_fast(1.0 + u) * ip * (1.0 - 4.0 * u);
+      const double beta = T * (1.0 + u) * rcp_fast(1.0 - u) * im * (1.0 + 4.0 * u);
+      const double ki = 1.02 * (De * c + De * De + T * Dn) * ip + 1e-30;
+      const double ko = 1.02 * (T * Dn + De * c) * im + 1e-30;
       a.G4[h] = make_float4(static_cast<float>(ki), -static_cast<float>(ko),
                             static_cast<float>(alpha), static_cast<float>(beta));
     }

@@ -175,22 +175,45 @@ struct MtStream {
   }
 };
 
-// One Fisher-Yates hypothesis x = arange(n); for i = n-1..1: swap(x[i], x[draw(i)]) and the
-// k-prefix of the result.  Position i is final after step i, so x[i] is only written back
-// while i < k (the prefix); x[j] always receives the old x[i].
-template <class Draw>
-inline void fisher_yates_prefix(std::vector<int32_t> &perm, const std::vector<int32_t> &iota,
-                                int64_t n, int32_t k, int32_t *out, Draw draw) {
+// One Fisher-Yates hypothesis x = arange(n); for i = n-1..1: swap(x[i], x[j]) with j drawn
+// by masked rejection, and the k-prefix of the result.  Position i is final after step i, so
+// x[i] is only written back while i < k (the prefix); x[j] always receives the old x[i].
+//
+// Branch-free over the words of one "level" (i in (lo, hi], where the draw's mask / shift is
+// fixed): every word is consumed as  acc = (draw(w) <= i);  j = acc ? draw(w) : i;  a swap
+// that is a no-op for a rejected word;  i -= acc.  The loop-carried chain is one compare and
+// one subtract per word, and the 25-50 % rejections cost no branch mispredictions.
+//   numpy  (random_interval, masked):  draw(w) = w & mask,            level: i in (mask/2, mask]
+//   CPython (randbelow(i+1), top bits): draw(w) = w >> (32 - bl(i+1)), level: i+1 in [2^(b-1), 2^b)
+template <bool NUMPY>
+inline void fisher_yates_prefix(MtStream &mt, std::vector<int32_t> &perm,
+                                const std::vector<int32_t> &iota, int64_t n, int32_t k,
+                                int32_t *out) {
   std::memcpy(perm.data(), iota.data(), sizeof(int32_t) * static_cast<size_t>(n));
   int32_t *x = perm.data();
-  uint32_t mask = smear_mask(static_cast<uint32_t>(n > 1 ? n - 1 : 0));
-  for (int64_t i = n - 1; i >= 1; --i) {
-    const uint32_t iu = static_cast<uint32_t>(i);
-    if (iu <= (mask >> 1)) mask >>= 1;  // mask == smear_mask(i)
-    const int64_t j = draw(iu, mask);
-    const int32_t t = x[i];
-    if (i < k) x[i] = x[j];
-    x[j] = t;
+  uint32_t i = static_cast<uint32_t>(n > 1 ? n - 1 : 0);
+  const uint32_t uk = static_cast<uint32_t>(k);
+  while (i >= 1) {
+    uint32_t lo, mask = 0, sh = 0;
+    if (NUMPY) {
+      mask = smear_mask(i);  // random_interval(i): mask of i, fixed while i > mask / 2
+      lo = mask >> 1;
+    } else {
+      const int b = bit_length(i + 1);  // randbelow(i + 1): getrandbits(b), fixed while
+      sh = static_cast<uint32_t>(32 - b);  // i + 1 >= 2^(b-1)
+      lo = (1u << (b - 1)) - 2u;  // i > lo  <=>  i + 1 >= 2^(b-1)
+      if (b == 1) lo = 0;          // i = 0 never occurs here (loop condition)
+    }
+    while (i > lo) {
+      const uint32_t w = mt.next();
+      const uint32_t v = NUMPY ? (w & mask) : (w >> sh);
+      const uint32_t acc = v <= i ? 1u : 0u;
+      const uint32_t j = acc ? v : i;
+      const int32_t t = x[i];
+      if (i < uk) x[i] = x[j];
+      x[j] = t;
+      i -= acc;
+    }
   }
   std::memcpy(out, x, sizeof(int32_t) * static_cast<size_t>(k));
 }
@@ -212,13 +235,7 @@ extern "C" int rs_np_choice_tuples(uint32_t *mt_key, int32_t *mt_pos, int64_t n,
   std::vector<int32_t> perm(static_cast<size_t>(n > 0 ? n : 1)), iota(perm.size());
   for (int64_t i = 0; i < n; ++i) iota[static_cast<size_t>(i)] = static_cast<int32_t>(i);
   // numpy random_interval(max): draws u32 & smear(max) until <= max
-  auto draw = [&mt](uint32_t max, uint32_t mask) -> int64_t {
-    uint32_t v;
-    while ((v = (mt.next() & mask)) > max) {
-    }
-    return v;
-  };
-  for (int64_t h = 0; h < count; ++h) fisher_yates_prefix(perm, iota, n, k, out + h * k, draw);
+  for (int64_t h = 0; h < count; ++h) fisher_yates_prefix<true>(mt, perm, iota, n, k, out + h * k);
   mt.store(mt_key, mt_pos);
   return RS_OK;
 }
@@ -238,15 +255,9 @@ extern "C" int rs_py_shuffle_tuples(uint32_t *mt_key, int32_t *mt_pos, int64_t n
   mt.load(mt_key, *mt_pos);
   std::vector<int32_t> perm(static_cast<size_t>(n > 0 ? n : 1)), iota(perm.size());
   for (int64_t i = 0; i < n; ++i) iota[static_cast<size_t>(i)] = static_cast<int32_t>(i);
-  auto draw = [&mt](uint32_t i, uint32_t) -> int64_t {  // randbelow(i + 1)
-    const uint32_t lim = i + 1;
-    const int kb = bit_length(lim);
-    uint32_t r;
-    while ((r = (mt.next() >> (32 - kb))) >= lim) {
-    }
-    return r;
-  };
-  for (int64_t h = 0; h < count; ++h) fisher_yates_prefix(perm, iota, n, k, out + h * k, draw);
+  // randbelow(i + 1): getrandbits(bit_length(i + 1)) until < i + 1
+  for (int64_t h = 0; h < count; ++h)
+    fisher_yates_prefix<false>(mt, perm, iota, n, k, out + h * k);
   mt.store(mt_key, mt_pos);
   return RS_OK;
 }
