@@ -148,7 +148,7 @@ struct rs_f8_plan {
   rsd::Pt *d_pts = nullptr;    // AoS float64 points
   float4 *d_pts32 = nullptr;   // unit-frame fp32 points, NaN-padded to a multiple of 8
   float4 *d_pts32q = nullptr;  // the same, point-pair layout (k_f8_count32q)
-  static constexpr int kBufs = 2, kSlots = 4, kEvRing = 64;
+  static constexpr int kBufs = 3, kSlots = 4, kEvRing = 64;
   RunBufs buf[kBufs];
   // Each run's tail writes its result header into its own pinned slot (through the host
   // mapping) and S_RANSAC into its buffer set's HBM result; rs_f8_plan_result waits for the
@@ -160,6 +160,15 @@ struct rs_f8_plan {
   int64_t runs = 0, last_H = 0;
   bool pending = false;              // stream work not yet waited for
   bool tail_pending = false;         // the last run's tail is not enqueued yet
+  // Overlap mode (RSAMD_OVERLAP=1): solves run on their own stream `ss`, ahead of the
+  // counts, so the solve of run k+1 shares the machine with the count of run k.  Run k uses
+  // buffer set k % 3; ev_solved[s] orders count(k) after solve(k), ev_free[s] orders
+  // solve(k+3) after tail(k) (the last reader of set s).  Measured slower on C2 (154 vs
+  // 140 us per run: the cross-stream waits and the shared CUs cost more than the hidden
+  // 23 us solve), so the default is the single-stream [tail | solve] + count pipeline.
+  bool overlap = false;
+  hipStream_t ss = nullptr;
+  hipEvent_t ev_solved[kBufs] = {}, ev_free[kBufs] = {};
   rsd::TailArgs tail{};              // ... its arguments
   // counting kernel selection (environment knobs for A/B sweeps, tools/sweep.py)
   rsd::Frame frame{1.0, 0.0, 0.0, 0.0, 0.0};
@@ -215,6 +224,11 @@ static void plan_free(rs_f8_plan *p) {
   for (auto &r : p->ring)
     for (auto &e : r)
       if (e) (void)hipEventDestroy(e);
+  for (int k = 0; k < rs_f8_plan::kBufs; ++k) {
+    if (p->ev_solved[k]) (void)hipEventDestroy(p->ev_solved[k]);
+    if (p->ev_free[k]) (void)hipEventDestroy(p->ev_free[k]);
+  }
+  if (p->ss) (void)hipStreamDestroy(p->ss);
 }
 
 extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_plan **out) {
@@ -287,6 +301,14 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
   for (auto &r : p->ring)
     for (auto &ev : r)
       if (e == hipSuccess) e = hipEventCreate(&ev);
+  p->overlap = env_int("RSAMD_OVERLAP", 0) != 0;
+  if (p->overlap) {
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->ss, hipStreamNonBlocking);
+    for (int k = 0; k < rs_f8_plan::kBufs; ++k) {
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&p->ev_solved[k], hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&p->ev_free[k], hipEventDisableTiming);
+    }
+  }
   if (e != hipSuccess) {
     plan_free(p);
     delete p;
@@ -304,6 +326,7 @@ static int plan_flush(rs_f8_plan *p) {
     p->tail_pending = false;
   }
   HIP_TRY(hipStreamSynchronize(p->ctx->stream));
+  if (p->ss) HIP_TRY(hipStreamSynchronize(p->ss));
   p->pending = false;
   return RS_OK;
 }
@@ -393,10 +416,14 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
   const bool fp32 = p->use_fp32 && p->fp32_ok;
   const bool fused_max = fp32 && p->pair && !p->packed && p->fuse_max;
   hipStream_t ms = c->stream;
+  const int set = static_cast<int>(p->runs % rs_f8_plan::kBufs);
+  hipStream_t sst = p->overlap ? p->ss : ms;  // the solve's stream
+  if (p->overlap && p->runs >= rs_f8_plan::kBufs)  // set `set` free: run k-3's tail is done
+    HIP_TRY(hipStreamWaitEvent(sst, p->ev_free[set], 0));
 
   if (mode == RS_SAMPLER_TUPLES)
     HIP_TRY(hipMemcpyAsync(b.d_tuples, host_tuples, sizeof(int) * 8 * H, hipMemcpyHostToDevice,
-                           ms));
+                           sst));
   // [tail of the previous run | solve of this run]: buffer set b was last read by run k-2,
   // whose tail is complete (stream order)
   rsd::SolveArgs sa{};
@@ -421,10 +448,14 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
     sa.gDe = gb.De;
     sa.gDn = gb.Dn;
   }
-  if (tl >= 2) HIP_TRY(hipEventRecord(ev[2], ms));
-  HIP_TRY(rsd::launch_f8_tail_solve(p->tail_pending ? &p->tail : nullptr, &sa, ms));
+  if (tl >= 2) HIP_TRY(hipEventRecord(ev[2], sst));
+  HIP_TRY(rsd::launch_f8_tail_solve(p->tail_pending ? &p->tail : nullptr, &sa, sst));
   p->tail_pending = false;
-  if (tl >= 2) HIP_TRY(hipEventRecord(ev[3], ms));
+  if (tl >= 2) HIP_TRY(hipEventRecord(ev[3], sst));
+  if (p->overlap) {
+    HIP_TRY(hipEventRecord(p->ev_solved[set], sst));
+    HIP_TRY(hipStreamWaitEvent(ms, p->ev_solved[set], 0));
+  }
 
   // counts of this run
   if (tl >= 1) HIP_TRY(hipEventRecord(ev[0], ms));
@@ -487,7 +518,14 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
   ta.cnorm = b.d_cnorm;
   ta.res = b.d_res;
   ta.hres = p->h_slot_dev[slot];
-  p->tail_pending = true;
+  if (p->overlap) {
+    // the tail right behind its count on the main stream; the next solves are already
+    // running ahead on `ss`
+    HIP_TRY(rsd::launch_f8_tail_solve(&ta, nullptr, ms));
+    HIP_TRY(hipEventRecord(p->ev_free[set], ms));
+  } else {
+    p->tail_pending = true;
+  }
   ++p->runs;
   p->last_H = H;
   p->pending = true;
