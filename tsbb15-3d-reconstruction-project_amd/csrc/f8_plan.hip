@@ -263,8 +263,10 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
     int cus = 256;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
       cus = 256;
-    p->resident_waves = std::max(1, env_int("RSAMD_WAVES", cus * 4 * 8 * 4));  // 4 slices per
-    p->count_block = env_int("RSAMD_BLOCK", 8) == 4 ? 4 : 8;                  // resident wave
+    // slices of the (group, point) plane: 2 per resident wave slot (8 per SIMD) for the
+    // default "q" kernel (A/B on C2: 16384 ahead of 8192 / 12288 / 24576 / 32768 by 1-3 %)
+    p->resident_waves = std::max(1, env_int("RSAMD_WAVES", cus * 4 * 8 * (p->pointpair ? 2 : 4)));
+    p->count_block = env_int("RSAMD_BLOCK", 8) == 4 ? 4 : 8;
     p->prefetch = env_int("RSAMD_PREFETCH", 0) != 0;
     p->pk_variant = env_int("RSAMD_PKVAR", 0);
     const int minw = p->pk_variant == 1 || p->pk_variant == 3 ? 6 : (p->pk_variant == 2 ? 4 : 8);
