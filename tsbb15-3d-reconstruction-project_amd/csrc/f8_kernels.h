@@ -95,7 +95,7 @@ hipError_t launch_pack_points32q(const Pt *pts, int n, const Frame &fr, float4 *
 hipError_t launch_f8_count32q(const float4 *ptsq, const Pt *pts, int n, int H,
                               const float *F32soa, const double *Fsoa, int64_t ld, int waves,
                               const GuardW &g, int *counts, hipStream_t s, int *gdone,
-                              int *status, const float4 *G4);
+                              int *status, const float4 *G4, bool use_asm = true);
 hipError_t launch_f8_count(const Pt *pts, int n, int H, const double *Fsoa, int64_t ld,
                            int chunk, double thr2, int *counts, hipStream_t s);
 // Selection tail: c* (k_f8_max, unless the counting kernel fused it), candidates + reference

@@ -577,6 +577,30 @@ typedef float f2q __attribute__((ext_vector_type(2)));
 // The k_f8_count32q terms of one point pair (expressions and order as documented above the
 // kernel); P01 = (F0, F1), P23 = (F2, F3), P45 = (F4, F5), P67 = (F6, F7), P8 = (F8, F8),
 // KIO = (ki, -ko), ALB = (alpha, beta).
+// Plain-builtin form of the same terms (the compiler splats the coefficients into VGPR
+// pairs: 66 VGPRs; it can interleave the pairs freely).  Selected by RSAMD_QASM=0.
+__device__ __forceinline__ void pair_terms_builtin(f2q P01, f2q P23, f2q P45, f2q P67, f2q P8, f2q KIO,
+                                           f2q ALB, f2q X2, f2q Y2, f2q X1, f2q Y1, f2q &P,
+                                           f2q &Q, f2q &R, f2q &S) {
+#pragma clang fp contract(off)
+  const f2q F0 = {P01.x, P01.x}, F1 = {P01.y, P01.y}, F2 = {P23.x, P23.x}, F3 = {P23.y, P23.y};
+  const f2q F4 = {P45.x, P45.x}, F5 = {P45.y, P45.y}, F6 = {P67.x, P67.x}, F7 = {P67.y, P67.y};
+  const f2q a = __builtin_elementwise_fma(F0, X2, __builtin_elementwise_fma(F1, Y2, F2));
+  const f2q b = __builtin_elementwise_fma(F3, X2, __builtin_elementwise_fma(F4, Y2, F5));
+  const f2q l3 = __builtin_elementwise_fma(F6, X2, __builtin_elementwise_fma(F7, Y2, P8));
+  const f2q e = __builtin_elementwise_fma(a, X1, __builtin_elementwise_fma(b, Y1, l3));
+  const f2q c = __builtin_elementwise_fma(F0, X1, __builtin_elementwise_fma(F3, Y1, F6));
+  const f2q d = __builtin_elementwise_fma(F1, X1, __builtin_elementwise_fma(F4, Y1, F7));
+  const f2q n1 = __builtin_elementwise_fma(a, a, b * b);
+  const f2q n2 = __builtin_elementwise_fma(c, c, d * d);
+  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+  const f2q m = __builtin_bit_cast(
+      f2q, __builtin_elementwise_min(__builtin_bit_cast(u2, n1), __builtin_bit_cast(u2, n2)));
+  P = __builtin_elementwise_fma(e, e, f2q{KIO.x, KIO.x});
+  Q = __builtin_elementwise_fma(e, e, f2q{KIO.y, KIO.y});
+  R = m * f2q{ALB.x, ALB.x};
+  S = m * f2q{ALB.y, ALB.y};
+}
 __device__ __forceinline__ void pair_terms(f2q P01, f2q P23, f2q P45, f2q P67, f2q P8, f2q KIO,
                                            f2q ALB, f2q X2, f2q Y2, f2q X1, f2q Y1, f2q &P,
                                            f2q &Q, f2q &R, f2q &S) {
@@ -620,6 +644,7 @@ __device__ __forceinline__ void pair_terms(f2q P01, f2q P23, f2q P45, f2q P67, f
   RSD_PKMUL_VB(S, m, ALB, "[0,1]", "[1,1]");  // beta m
 }
 
+template <bool ASM>
 __global__ __launch_bounds__(256) void k_f8_count32q(const float4 *__restrict__ ptsq,
                                                      const Pt *__restrict__ pts, int n, int H,
                                                      const float *__restrict__ F32soa,
@@ -664,7 +689,10 @@ __global__ __launch_bounds__(256) void k_f8_count32q(const float4 *__restrict__ 
         const f2 X2 = {v[2 * j], v[2 * j + 1]}, Y2 = {v[8 + 2 * j], v[9 + 2 * j]};
         const f2 X1 = {v[16 + 2 * j], v[17 + 2 * j]}, Y1 = {v[24 + 2 * j], v[25 + 2 * j]};
         f2 P, Q, R, S;
-        pair_terms(P01, P23, P45, P67, P8, KIO, ALB, X2, Y2, X1, Y1, P, Q, R, S);
+        if constexpr (ASM)
+          pair_terms(P01, P23, P45, P67, P8, KIO, ALB, X2, Y2, X1, Y1, P, Q, R, S);
+        else
+          pair_terms_builtin(P01, P23, P45, P67, P8, KIO, ALB, X2, Y2, X1, Y1, P, Q, R, S);
         const unsigned long long i0 = __ballot(P.x < R.x), i1 = __ballot(P.y < R.y);
         const unsigned long long l0 = __ballot(Q.x <= S.x), l1 = __ballot(Q.y <= S.y);
         cnt = add_lane_bit(cnt, i0);  // sure inliers
@@ -1228,15 +1256,19 @@ hipError_t launch_pack_points32q(const Pt *pts, int n, const Frame &fr, float4 *
 hipError_t launch_f8_count32q(const float4 *ptsq, const Pt *pts, int n, int H,
                               const float *F32soa, const double *Fsoa, int64_t ld, int waves,
                               const GuardW &g, int *counts, hipStream_t s, int *gdone,
-                              int *status, const float4 *G4) {
+                              int *status, const float4 *G4, bool use_asm) {
   const int64_t npad = (n + 7) / 8 * 8;
   const int64_t total = static_cast<int64_t>((H + 63) / 64) * npad;
   int64_t W = std::max<int64_t>(1, std::min<int64_t>(waves, total / 64));
   int64_t per = (total + W - 1) / W;
   per = (per + 7) / 8 * 8;
   W = (total + per - 1) / per;
-  hipLaunchKernelGGL(k_f8_count32q, dim3(static_cast<unsigned>((W + 3) / 4)), dim3(256), 0, s,
-                     ptsq, pts, n, H, F32soa, Fsoa, ld, per, g, counts, gdone, status, G4);
+  if (use_asm)
+    hipLaunchKernelGGL(k_f8_count32q<true>, dim3(static_cast<unsigned>((W + 3) / 4)), dim3(256),
+                       0, s, ptsq, pts, n, H, F32soa, Fsoa, ld, per, g, counts, gdone, status, G4);
+  else
+    hipLaunchKernelGGL(k_f8_count32q<false>, dim3(static_cast<unsigned>((W + 3) / 4)), dim3(256),
+                       0, s, ptsq, pts, n, H, F32soa, Fsoa, ld, per, g, counts, gdone, status, G4);
   return hipGetLastError();
 }
 

@@ -180,6 +180,7 @@ struct rs_f8_plan {
   bool folded = false;        // RSAMD_COUNT=z: folded plain decision + SALU bit-plane counts
   bool per_hyp = true;        // per-hypothesis AM-GM decision constants ("w", "q")
   bool pointpair = true;      // "q" (default): DEC 3 decisions, packed over point pairs
+  bool q_asm = true;          // RSAMD_QASM=0: "q" with compiler-scheduled builtins
   bool fuse_max = true;       // RSAMD_FUSEMAX=0: separate k_f8_max pass instead of the fused c*
   // HIP timing events per run (each is a marker packet between kernels): 0 none, 1 around the
   // counting kernel (default; the bench's roofline timing), 2 also the tail+solve launch
@@ -257,6 +258,7 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
     p->per_hyp = std::strcmp(cm, "w") == 0 || p->pointpair;
   }
   p->fuse_max = env_int("RSAMD_FUSEMAX", 1) != 0;
+  p->q_asm = env_int("RSAMD_QASM", 1) != 0;
   p->timing = env_int("RSAMD_TIMING", 1);
   p->timing_every = std::max(1, env_int("RSAMD_TIMING_EVERY", 1));
   {
@@ -471,7 +473,8 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
     if (p->pointpair)
       HIP_TRY(rsd::launch_f8_count32q(p->d_pts32q, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
                                       p->resident_waves, gw, b.d_counts, ms,
-                                      fused_max ? b.d_gdone : nullptr, b.d_status, b.d_G4));
+                                      fused_max ? b.d_gdone : nullptr, b.d_status, b.d_G4,
+                                      p->q_asm));
     else
       HIP_TRY(rsd::launch_f8_count32x(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
                                       p->resident_waves, gw, b.d_counts, ms, p->count_block,
