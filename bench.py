@@ -133,6 +133,19 @@ class _CtxComm:
         return [recv[i * n:(i + 1) * n].tobytes() for i in range(self.world)]
 
 
+class _GlooComm:
+    """Fallback record exchange over the harness's gloo group, used only if the RCCL
+    communicator cannot be created (reported as config.exchange)."""
+
+    def __init__(self, dist, rank, world):
+        self.dist, self.rank, self.world = dist, rank, world
+
+    def allgather_bytes(self, b):
+        out = [None] * self.world
+        self.dist.dist.all_gather_object(out, b)
+        return out
+
+
 class _Solo:
     rank, world = 0, 1
 
@@ -317,7 +330,9 @@ def main():
         # before any HIP call: the worker processes are forked from this one
         cp1, cp2, _ = synth.two_view(args.n, OUTLIERS, seed=1)
         cpu = cpu_baseline(cp1, cp2, args.cpu_seconds, args.cpu_procs)
-    ctx = _ffi.Context(local_rank)
+    # RSAMD_BENCH_DEVICE pins every rank to one device: a multi-rank rehearsal on a one-GPU
+    # box (RCCL refuses two ranks on one GPU, so that run exercises the gloo exchange)
+    ctx = _ffi.Context(int(os.environ.get("RSAMD_BENCH_DEVICE", local_rank)))
 
     # one synthetic pair per rank (weak scaling: per-GPU work fixed)
     p1, p2, _ = synth.two_view(args.n, OUTLIERS, seed=1 + rank)
@@ -329,12 +344,26 @@ def main():
     plan.set_timing(1, min(TIMING_EVERY, max(1, args.steps)))
 
     comm = world > 1
+    exchange = "none (one GPU)"
     if comm:
         uid = np.zeros(_ffi.COMM_ID_BYTES, np.uint8)
+        st = 0
         if rank == 0:
-            _ffi.check(_ffi.lib().rs_comm_unique_id(_ffi.ptr(uid, ctypes.c_uint8)))
+            st = _ffi.lib().rs_comm_unique_id(_ffi.ptr(uid, ctypes.c_uint8))
         uid = np.frombuffer(dist.bcast_bytes(uid.tobytes()), np.uint8).copy()
-        _ffi.check(_ffi.lib().rs_comm_init(ctx.handle, world, rank, _ffi.ptr(uid, ctypes.c_uint8)))
+        if st == 0:
+            st = _ffi.lib().rs_comm_init(ctx.handle, world, rank, _ffi.ptr(uid, ctypes.c_uint8))
+        ok = dist.max(0.0 if st == 0 else 1.0) == 0.0   # every rank agrees on the transport
+        if ok:
+            exchange = "rccl all-gather"
+            xcomm = _CtxComm(ctx, rank, world)
+        else:
+            if st == 0:
+                _ffi.lib().rs_comm_destroy(ctx.handle)
+            print(f"warning: RCCL communicator init failed on some rank (status {st}: {_ffi.lib().rs_last_error().decode(errors='replace')}); "
+                  "exchanging the per-pair records over gloo", file=sys.stderr)
+            exchange = "gloo all-gather (RCCL init failed)"
+            xcomm = _GlooComm(dist, rank, world)
 
     def step(i):
         # one full RANSAC run; runs are stream-ordered and issued back to back (each run
@@ -351,13 +380,11 @@ def main():
         step(args.warmup + i)
     r, inl = plan.result()          # waits for the last run
     assert r.best_count > 0 and len(inl) == r.best_count
-    if comm:  # RCCL all-gather of the per-pair best models (F, count, index)
+    if comm:  # all-gather of the per-pair best models (F, count, index) over RCCL
         rec = np.zeros(12, np.float64)
         rec[:9] = r.F[:]
         rec[9], rec[10], rec[11] = r.best_count, r.best_index, rank
-        out = np.zeros(12 * world, np.float64)
-        _ffi.check(_ffi.lib().rs_comm_allgather(ctx.handle, rec.ctypes.data_as(ctypes.c_void_p),
-                                                out.ctypes.data_as(ctypes.c_void_p), rec.nbytes))
+        out = np.frombuffer(b"".join(xcomm.allgather_bytes(rec.tobytes())), np.float64)
         assert int(out.reshape(world, 12)[rank, 11]) == rank
     ctx.synchronize()
     el = time.perf_counter() - t0
@@ -394,7 +421,8 @@ def main():
                                "outliers, 100000 hypotheses per RANSAC run, 8-point F, "
                                "threshold 1.5 px",
                    "n_corr": args.n, "hypotheses_per_step": H, "sampler": "philox (throughput)",
-                   "parallelism": f"pairs sharded, {world} pair(s) on {world} GPU(s)"},
+                   "parallelism": f"pairs sharded, {world} pair(s) on {world} GPU(s)",
+                   "exchange": exchange},
         "roofline": {"bound": "valu", "kernel": COUNT_KERNEL.get(os.environ.get("RSAMD_COUNT", "q"),
                                                           "k_f8_count32"),
                      "achieved": achieved, "peak": PEAK_FP32_VALU_TFLOPS, "unit": "TFLOP/s",
@@ -433,13 +461,12 @@ def main():
     if cpu is not None:
         line["cpu_baseline"] = cpu
     if not args.no_extras:
-        ex = extras(ctx, rank, world, dist,
-                    _CtxComm(ctx, rank, world) if comm else None)
+        ex = extras(ctx, rank, world, dist, xcomm if comm else None)
         if rank == 0:
             line["extras"] = ex
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if comm:
+    if comm and isinstance(xcomm, _CtxComm):
         _ffi.lib().rs_comm_destroy(ctx.handle)
     plan.close()
     dist.close()

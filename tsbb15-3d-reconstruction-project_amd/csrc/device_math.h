@@ -273,7 +273,7 @@ __device__ __forceinline__ void scaling8(const double (&x)[8], const double (&y)
 // xl, yl: left points (p1), xr, yr: right points (p2).  F row-major, pl^T F pr = 0.
 __device__ __forceinline__ void fmatrix8(const double (&xl)[8], const double (&yl)[8],
                                          const double (&xr)[8], const double (&yr)[8],
-                                         double (&F)[9]) {
+                                         double (&F)[9], int diag = 0) {
   double s1, ox1, oy1, s2, ox2, oy2;
   scaling8(xl, yl, s1, ox1, oy1);
   scaling8(xr, yr, s2, ox2, oy2);
@@ -297,9 +297,21 @@ __device__ __forceinline__ void fmatrix8(const double (&xl)[8], const double (&y
     A[k][8] = 1.0;
   }
   double fs[9];
-  lq_null_vector<8, 9>(A, fs);  // lab3.py:317-318: V[-1] of svd(A)
+  // diag: timing diagnostics only (RSAMD_SOLVE_DIAG, wrong models): 2 skips the LQ, 1 the
+  // rank-2 step
+  if (diag & 2) {
+#pragma unroll
+    for (int j = 0; j < 9; ++j) fs[j] = A[0][j] + A[7][j];
+  } else {
+    lq_null_vector<8, 9>(A, fs);  // lab3.py:317-318: V[-1] of svd(A)
+  }
   double F2[9];
-  enforce_rank2(fs, F2);
+  if (diag & 1) {
+#pragma unroll
+    for (int j = 0; j < 9; ++j) F2[j] = fs[j];
+  } else {
+    enforce_rank2(fs, F2);
+  }
   // lab3.py:327: F = S^T (F2 T); S = H(s1, ox1, oy1), T = H(s2, ox2, oy2)
   double M[9];
 #pragma unroll

@@ -37,7 +37,7 @@ struct F8DevResult {
 // One run's solve (k_f8_solve / the solve half of k_f8_tail_solve).
 struct SolveArgs {
   const Pt *pts;
-  int n, H, mode, pad_;
+  int n, H, mode, diag;  // diag: RSAMD_SOLVE_DIAG timing knob (0 in production)
   uint64_t seed, hyp_offset;
   const int *tuples;
   double *Fsoa;

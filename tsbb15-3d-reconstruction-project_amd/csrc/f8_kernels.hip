@@ -92,7 +92,10 @@ __device__ __forceinline__ void solve_one(const SolveArgs &a, int h) {
   }
   if (gdone && (h & 63) == 0) gdone[h >> 6] = 0;  // fused c*: per-group finish counters
   int idx[8];
-  if (mode == RSD_SAMPLER_PHILOX) {
+  if (a.diag & 4) {  // timing diagnostic: no sampling
+#pragma unroll
+    for (int k = 0; k < 8; ++k) idx[k] = (h * 8 + k * 977) % n;
+  } else if (mode == RSD_SAMPLER_PHILOX) {
     floyd_sample<8>(seed, hyp_offset + static_cast<uint64_t>(h), n, idx);
   } else {
 #pragma unroll
@@ -108,7 +111,7 @@ __device__ __forceinline__ void solve_one(const SolveArgs &a, int h) {
     yr[k] = p.y2;
   }
   double F[9];
-  fmatrix8(xl, yl, xr, yr, F);
+  fmatrix8(xl, yl, xr, yr, F, a.diag);
 #pragma unroll
   for (int k = 0; k < 9; ++k) Fsoa[k * ld + h] = F[k];
   if (F32soa) {

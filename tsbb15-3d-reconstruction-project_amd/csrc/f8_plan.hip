@@ -191,6 +191,7 @@ struct rs_f8_plan {
   bool prefetch = false;      // ping-pong point prefetch (RSAMD_PREFETCH=1; spills SGPRs at 8)
   int pk_variant = 0, pk_waves = 8192;
   int chunk_override = 0;     // fp64 kernel point chunk (RSAMD_CHUNK)
+  int solve_diag = 0;         // RSAMD_SOLVE_DIAG: timing-only solve variants (wrong models)
 
   const RunBufs &last() const { return buf[(runs - 1) % kBufs]; }
 };
@@ -306,6 +307,7 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
     for (auto &ev : r)
       if (e == hipSuccess) e = hipEventCreate(&ev);
   p->overlap = env_int("RSAMD_OVERLAP", 0) != 0;
+  p->solve_diag = env_int("RSAMD_SOLVE_DIAG", 0);
   if (p->overlap) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->ss, hipStreamNonBlocking);
     for (int k = 0; k < rs_f8_plan::kBufs; ++k) {
@@ -445,6 +447,7 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
   sa.F32soa = fp32 ? b.d_F32 : nullptr;
   sa.frame = fp32 ? p->frame : rsd::Frame{1.0, 0.0, 0.0, 0.0, 0.0};
   sa.gdone = b.d_gdone;
+  sa.diag = p->solve_diag;
   if (fp32 && p->pair && p->per_hyp) {
     const Bounds gb = fp32_bounds(p->frame, thresh);
     sa.G4 = b.d_G4;
