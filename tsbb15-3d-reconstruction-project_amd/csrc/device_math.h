@@ -204,6 +204,73 @@ __device__ __forceinline__ void enforce_rank2(const double (&Fs)[9], double (&F2
                       w2 * B[3 * r + 2] * V[3 * c + 2];
 }
 
+// Nearest rank-2 matrix by the smallest right singular vector: F2 = Fs (I - v v^T), the same
+// matrix as U diag(s0, s1, 0) V^T.  v is the eigenvector of M = Fs^T Fs for its smallest
+// eigenvalue l0: Newton from 0 on det(M - l I) = -l^3 + c2 l^2 - c1 l + c0 (monotone to the
+// smallest root; 4.7 steps on average, <= 12 for 99.99 % of 8-point samples), then the
+// largest column of adj(M - l0 I) = (l1 - l0)(l2 - l0) v v^T.  About 150 flops on a short
+// dependent chain instead of 4-6 Jacobi sweeps.  Returns false (and leaves F2 alone) when
+// Newton has not converged in 40 steps or the gap product is below 1e-12 c2^2 (near-double
+// smallest singular value: the caller falls back to the Jacobi SVD).  Host prototype
+// against numpy's SVD over 40 000 C2 samples: max deviation 2.4e-11 after normalisation,
+// one fallback.
+__device__ __forceinline__ bool enforce_rank2_adj(const double (&Fs)[9], double (&F2)[9]) {
+  double M[9];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = r; c < 3; ++c) {
+      const double v = fma(Fs[r], Fs[c], fma(Fs[3 + r], Fs[3 + c], Fs[6 + r] * Fs[6 + c]));
+      M[3 * r + c] = v;
+      M[3 * c + r] = v;
+    }
+  const double c2 = M[0] + M[4] + M[8];
+  const double m01 = fma(M[4], M[8], -M[5] * M[5]);
+  const double m02 = fma(M[0], M[8], -M[2] * M[2]);
+  const double m12 = fma(M[0], M[4], -M[1] * M[1]);
+  const double c1 = m01 + m02 + m12;
+  const double c0 = M[0] * m01 - M[1] * fma(M[1], M[8], -M[5] * M[2]) +
+                    M[2] * fma(M[1], M[5], -M[4] * M[2]);
+  double lam = 0.0;
+  bool conv = false;
+  for (int it = 0; it < 40; ++it) {
+    const double p = fma(fma(c2 - lam, lam, -c1), lam, c0);        // p(lam)
+    const double ndp = fma(fma(3.0, lam, -2.0 * c2), lam, c1);     // -p'(lam) > 0 below l0
+    const double st = p * rcp_fast(ndp);
+    lam += st;
+    if (fabs(st) <= 1e-15 * c2) {
+      conv = true;
+      break;
+    }
+  }
+  if (!conv) return false;
+  const double a00 = M[0] - lam, a11 = M[4] - lam, a22 = M[8] - lam;
+  const double a01 = M[1], a02 = M[2], a12 = M[5];
+  const double d0 = fma(a11, a22, -a12 * a12), d1 = fma(a00, a22, -a02 * a02),
+               d2 = fma(a00, a11, -a01 * a01);
+  double v0, v1, v2, dj;
+  if (d0 >= d1 && d0 >= d2) {
+    v0 = d0; v1 = fma(a12, a02, -a01 * a22); v2 = fma(a01, a12, -a11 * a02); dj = d0;
+  } else if (d1 >= d2) {
+    v0 = fma(a02, a12, -a01 * a22); v1 = d1; v2 = fma(a01, a02, -a00 * a12); dj = d1;
+  } else {
+    v0 = fma(a01, a12, -a02 * a11); v1 = fma(a02, a01, -a00 * a12); v2 = d2; dj = d2;
+  }
+  if (!(dj > 1e-12 * c2 * c2)) return false;  // also false for NaN
+  const double inv = rsqrt_fast(fma(v0, v0, fma(v1, v1, v2 * v2)));
+  v0 *= inv;
+  v1 *= inv;
+  v2 *= inv;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const double w = fma(Fs[3 * r], v0, fma(Fs[3 * r + 1], v1, Fs[3 * r + 2] * v2));  // Fs v
+    F2[3 * r + 0] = fma(-w, v0, Fs[3 * r + 0]);
+    F2[3 * r + 1] = fma(-w, v1, Fs[3 * r + 1]);
+    F2[3 * r + 2] = fma(-w, v2, Fs[3 * r + 2]);
+  }
+  return true;
+}
+
 // ----------------------------------------------------------------------------------------
 // Null vector of an R x C (R < C) matrix by Householder LQ: A Q = [L 0], null = Q e_{C-1}.
 // The reflector of row k is stored in place of row k (entries k..C-1).  For R = C-1 and
@@ -309,7 +376,7 @@ __device__ __forceinline__ void fmatrix8(const double (&xl)[8], const double (&y
   if (diag & 1) {
 #pragma unroll
     for (int j = 0; j < 9; ++j) F2[j] = fs[j];
-  } else {
+  } else if ((diag & 8) || !enforce_rank2_adj(fs, F2)) {  // 8: the Jacobi path always
     enforce_rank2(fs, F2);
   }
   // lab3.py:327: F = S^T (F2 T); S = H(s1, ox1, oy1), T = H(s2, ox2, oy2)

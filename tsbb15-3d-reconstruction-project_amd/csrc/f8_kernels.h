@@ -30,7 +30,8 @@ struct F8DevResult {
   int64_t guard_mismatch;
   int64_t n_inliers;
   int64_t best_cand;
-  int64_t pad_;
+  int64_t inl_row;  // -1: S_RANSAC in inliers[]; else the select block whose spec row holds it
+
   int64_t inliers[];
 };
 
@@ -61,6 +62,8 @@ struct TailArgs {
   int *status;   // [c*, n_candidates, done counter, spare, per-block candidate counts]
   double thresh;
   int *cand, *ccount;
+  int *cfast;          // fast count of each candidate (guard_mismatch without a gather)
+  int *spec, *spec_j;  // per block: S_RANSAC of its first candidate (n ints), that index
   double *cstd, *cnorm;
   F8DevResult *res;   // HBM result (header + S_RANSAC)
   F8DevResult *hres;  // pinned host header slot (device mapping), may be null
@@ -95,7 +98,8 @@ hipError_t launch_pack_points32q(const Pt *pts, int n, const Frame &fr, float4 *
 hipError_t launch_f8_count32q(const float4 *ptsq, const Pt *pts, int n, int H,
                               const float *F32soa, const double *Fsoa, int64_t ld, int waves,
                               const GuardW &g, int *counts, hipStream_t s, int *gdone,
-                              int *status, const float4 *G4, bool use_asm = true);
+                              int *status, const float4 *G4, bool use_asm = true,
+                              int block_threads = 256, bool xcd_remap = false);
 hipError_t launch_f8_count(const Pt *pts, int n, int H, const double *Fsoa, int64_t ld,
                            int chunk, double thr2, int *counts, hipStream_t s);
 // Selection tail: c* (k_f8_max, unless the counting kernel fused it), candidates + reference
@@ -105,7 +109,8 @@ int select_per_block(int H);
 int select_blocks(int H);
 hipError_t launch_f8_max(const int *counts, int H, int *status, hipStream_t s);
 // Tail of one run and/or solve of the next in one launch (either may be null).
-hipError_t launch_f8_tail_solve(TailArgs *ta, SolveArgs *sa, hipStream_t s);
+hipError_t launch_f8_tail_solve(TailArgs *ta, SolveArgs *sa, hipStream_t s,
+                                int tail_cus = 0);
 hipError_t launch_residuals(const Pt *pts, int n, const double *F, double *out, hipStream_t s);
 
 }  // namespace rsd

@@ -647,8 +647,8 @@ __device__ __forceinline__ void pair_terms(f2q P01, f2q P23, f2q P45, f2q P67, f
   RSD_PKMUL_VB(S, m, ALB, "[0,1]", "[1,1]");  // beta m
 }
 
-template <bool ASM>
-__global__ __launch_bounds__(256) void k_f8_count32q(const float4 *__restrict__ ptsq,
+template <bool ASM, int BT>
+__global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ ptsq,
                                                      const Pt *__restrict__ pts, int n, int H,
                                                      const float *__restrict__ F32soa,
                                                      const double *__restrict__ Fsoa,
@@ -656,11 +656,16 @@ __global__ __launch_bounds__(256) void k_f8_count32q(const float4 *__restrict__ 
                                                      int *__restrict__ counts,
                                                      int *__restrict__ gdone,
                                                      int *__restrict__ status,
-                                                     const float4 *__restrict__ G4) {
+                                                     const float4 *__restrict__ G4,
+                                                     int xcd_rows) {
 #pragma clang fp contract(off)
   typedef float f2 __attribute__((ext_vector_type(2)));
   const int lane = threadIdx.x & 63;
-  const int64_t w = wave_uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+  // xcd_rows > 0: consecutive workgroups go round-robin to the 8 XCDs, so block b takes slice
+  // block (b % 8) * xcd_rows + b / 8 and the slices of one hypothesis group (which re-read
+  // its models) stay on one XCD's L2; the grid is a multiple of 8 blocks then
+  const int b = xcd_rows > 0 ? (blockIdx.x & 7) * xcd_rows + (blockIdx.x >> 3) : blockIdx.x;
+  const int64_t w = wave_uniform(b * (BT / 64) + (threadIdx.x >> 6));
   const int64_t npad = (n + 7) / 8 * 8;
   const int64_t total = static_cast<int64_t>((H + 63) >> 6) * npad;
   int64_t pos = w * per_wave;
@@ -906,12 +911,22 @@ __device__ void replay_inliers(const Pt *__restrict__ pts, int n, const int *cou
                                const double *cstd, const double *cnorm,
                                const double *__restrict__ Fsoa, int64_t ld, int *status,
                                double thresh, F8DevResult *__restrict__ res,
-                               F8DevResult *__restrict__ hres);
+                               F8DevResult *__restrict__ hres, const int *cfast,
+                               const int *spec, const int *spec_j);
 
 // Candidates + their reference-order statistics, one block per slice of hypotheses:
 // every hypothesis of the slice with fast count >= max(c* - slack, 1) is appended in index
 // order to the block's own segment cand[b * per_block + j] (bc[b] entries), then the block
 // re-scores each of them with dist_ref: count, np.std(d) (two-pass), np.linalg.norm(d).
+// Per select block: the candidates of its hypothesis range (count >= c* - slack), each with
+// its exact reference-order count, std and norm (fun.py:316-321).  The distances of a
+// candidate are computed once and kept in registers (n <= kRegPts * kTailThreads; larger n
+// recomputes them in a second pass), the three sums share one LDS round, and the block's
+// first candidate also writes its S_RANSAC = flatnonzero(d < t) to the block's `spec` row,
+// so that the replay only copies the winner's list when the winner is such a candidate.
+constexpr int kRegPts = 8;
+constexpr int kLocalCands = 64;
+
 __device__ void cand_stats_block(const TailArgs &a, int bid, int nblocks) {
   const Pt *__restrict__ pts = a.pts;
   const int n = a.n, H = a.H, slack = a.slack, per_block = a.per_block;
@@ -927,20 +942,25 @@ __device__ void cand_stats_block(const TailArgs &a, int bid, int nblocks) {
   double *__restrict__ cstd = a.cstd;
   double *__restrict__ cnorm = a.cnorm;
   constexpr int NW = kTailThreads / 64;
-  __shared__ double shd[NW];
+  __shared__ double shd[2][NW];
+  __shared__ double sh3[NW];  // s3 has its own row: other waves may still read shd / shi
   __shared__ int last_s;
   __shared__ int shi[NW];
   __shared__ int woff[NW];
+  __shared__ int lcand[kLocalCands];
+  __shared__ int qoff[kRegPts][NW];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int cmax = status[0];
   const int thr = max(cmax - slack, 1);
   const int b0 = bid * per_block, b1 = min(H, b0 + per_block);
   int *seg = cand + static_cast<int64_t>(bid) * per_block;
+  int *segf = a.cfast + static_cast<int64_t>(bid) * per_block;
   int nloc = 0;
   if (cmax > 0) {
     for (int b = b0; b < b1; b += kTailThreads) {
       const int i = b + tid;
-      const bool take = i < b1 && counts[i] >= thr;
+      const int c = i < b1 ? counts[i] : 0;
+      const bool take = i < b1 && c >= thr;
       const unsigned long long bal = __ballot(take);
       if (lane == 0) woff[w] = __popcll(bal);
       __syncthreads();
@@ -949,37 +969,106 @@ __device__ void cand_stats_block(const TailArgs &a, int bid, int nblocks) {
         if (q < w) base += woff[q];
         tot += woff[q];
       }
-      if (take) st_agent(&seg[base + __popcll(bal & ((1ull << lane) - 1ull))], i);
+      if (take) {
+        const int o = base + __popcll(bal & ((1ull << lane) - 1ull));
+        st_agent(&seg[o], i);
+        st_agent(&segf[o], c);
+        if (o < kLocalCands) lcand[o] = i;
+      }
       nloc += tot;
       __syncthreads();
     }
   }
-  if (tid == 0) st_agent(&bc[bid], nloc);
-  wait_vmem();
-  __syncthreads();  // seg[] written by this block is visible to all its threads
+  const bool in_regs = n <= kRegPts * kTailThreads;
+  if (tid == 0) {
+    st_agent(&bc[bid], nloc);
+    st_agent(&a.spec_j[bid], (nloc > 0 && in_regs) ? 0 : -1);
+    if (bid == 0) st_agent(&status_rw[3], per_block);  // the layout, for rs_f8_plan_candidates
+  }
+  int *spec = a.spec + static_cast<int64_t>(bid) * n;
   for (int j = 0; j < nloc; ++j) {
-    const int h = ld_agent(&seg[j]);
+    const int h = j < kLocalCands ? lcand[j] : ld_agent(&seg[j]);
     double f[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) f[k] = Fsoa[k * ld + h];
-    double s1 = 0.0, s2 = 0.0;
+    double s1 = 0.0, s2 = 0.0, s3 = 0.0;
     int cnt = 0;
-    for (int i = tid; i < n; i += kTailThreads) {
-      const double d = dist_ref(f, pts[i]);
-      cnt += d < thresh ? 1 : 0;
-      s1 += d;
-      s2 += d * d;
+    double mean;
+    if (in_regs) {
+      double dv[kRegPts];
+      unsigned long long bl[kRegPts];
+#pragma unroll
+      for (int q = 0; q < kRegPts; ++q) {
+        const int i = tid + q * kTailThreads;
+        double d = 0.0;
+        bool in = false;
+        if (i < n) {
+          d = dist_ref(f, pts[i]);
+          in = d < thresh;
+          s1 += d;
+          s2 += d * d;
+        }
+        dv[q] = d;
+        cnt += in ? 1 : 0;
+        bl[q] = __ballot(in);
+      }
+      s1 = wave_sum(s1);
+      s2 = wave_sum(s2);
+      cnt = wave_sum_i(cnt);
+      if (lane == 0) {
+        shd[0][w] = s1;
+        shd[1][w] = s2;
+        shi[w] = cnt;
+#pragma unroll
+        for (int q = 0; q < kRegPts; ++q) qoff[q][w] = __popcll(bl[q]);
+      }
+      __syncthreads();
+      s1 = 0.0;
+      s2 = 0.0;
+      cnt = 0;
+      for (int q = 0; q < NW; ++q) {  // block_sum_d / block_reduce_sum order
+        s1 += shd[0][q];
+        s2 += shd[1][q];
+        cnt += shi[q];
+      }
+      mean = s1 / static_cast<double>(n);
+      if (j == 0) {  // the block's speculative S_RANSAC, in index order
+#pragma unroll
+        for (int q = 0; q < kRegPts; ++q) {
+          if ((bl[q] >> lane) & 1ull) {
+            int o = __popcll(bl[q] & ((1ull << lane) - 1ull));
+            for (int qq = 0; qq < kRegPts; ++qq)
+              for (int ww = 0; ww < NW; ++ww)
+                if (qq < q || (qq == q && ww < w)) o += qoff[qq][ww];
+            st_agent(&spec[o], tid + q * kTailThreads);
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < kRegPts; ++q) {
+        const int i = tid + q * kTailThreads;
+        if (i < n) {
+          const double v = dv[q] - mean;
+          s3 += v * v;
+        }
+      }
+    } else {
+      for (int i = tid; i < n; i += kTailThreads) {
+        const double d = dist_ref(f, pts[i]);
+        cnt += d < thresh ? 1 : 0;
+        s1 += d;
+        s2 += d * d;
+      }
+      s1 = block_sum_d(s1, shd[0]);
+      s2 = block_sum_d(s2, shd[0]);
+      cnt = block_reduce_sum(cnt, shi);
+      mean = s1 / static_cast<double>(n);
+      for (int i = tid; i < n; i += kTailThreads) {
+        const double v = dist_ref(f, pts[i]) - mean;
+        s3 += v * v;
+      }
     }
-    s1 = block_sum_d(s1, shd);
-    s2 = block_sum_d(s2, shd);
-    cnt = block_reduce_sum(cnt, shi);
-    const double mean = s1 / static_cast<double>(n);
-    double s3 = 0.0;
-    for (int i = tid; i < n; i += kTailThreads) {
-      const double v = dist_ref(f, pts[i]) - mean;
-      s3 += v * v;
-    }
-    s3 = block_sum_d(s3, shd);
+    s3 = block_sum_d(s3, sh3);  // its trailing barrier also retires shd / shi / qoff
     if (tid == 0) {
       const int64_t slot = static_cast<int64_t>(bid) * per_block + j;
       st_agent(&ccount[slot], cnt);
@@ -987,15 +1076,16 @@ __device__ void cand_stats_block(const TailArgs &a, int bid, int nblocks) {
       st_agent(&cnorm[slot], sqrt(s2));
     }
   }
-  // the last block to finish runs the replay: every block's segment, counts and statistics
-  // are agent-scope stores completed (vmcnt) before its done-counter increment
+  // the last block to finish runs the replay: every block's segment, counts, statistics and
+  // speculative list are agent-scope stores completed (vmcnt) before its done-counter
+  // increment
   wait_vmem();
   __syncthreads();
   if (tid == 0) last_s = atomicAdd(&status_rw[2], 1) == static_cast<int>(nblocks) - 1;
   __syncthreads();
   if (!last_s) return;
   replay_inliers(pts, n, counts, nblocks, per_block, bc, cand, ccount, cstd, cnorm, Fsoa, ld,
-                 status_rw, thresh, a.res, a.hres);
+                 status_rw, thresh, a.res, a.hres, a.cfast, a.spec, a.spec_j);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -1021,13 +1111,15 @@ __device__ void replay_inliers(const Pt *__restrict__ pts, int n, const int *cou
                                const double *cstd, const double *cnorm,
                                const double *__restrict__ Fsoa, int64_t ld, int *status,
                                double thresh, F8DevResult *__restrict__ res,
-                               F8DevResult *__restrict__ hres) {
+                               F8DevResult *__restrict__ hres, const int *cfast,
+                               const int *spec, const int *spec_j) {
   int *status_out = status;
   __shared__ int pref[kSelectBlocks + 1];
   __shared__ int woff[kTailThreads / 64];
   __shared__ int base_s;
   __shared__ double fsh[9];
   __shared__ int have_s;
+  __shared__ int spec_row_s;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // exclusive prefix of the per-block candidate counts (nb <= 256): one wave per 64 blocks,
   // then the 4 wave totals
@@ -1058,11 +1150,14 @@ __device__ void replay_inliers(const Pt *__restrict__ pts, int n, const int *cou
   if (w == 0) {
     int best = -1, bcount = 0;
     uint64_t bstd = 0ull;  // S_RANSAC = [], norm([]) = 0
+    // the winner's record travels with the replay (no dependent loads after it)
+    int bh = -1, brow = -1;
+    double bsv = 0.0, bnv = 0.0;
     int mismatch = 0;
     for (int b = 0; b < nc; b += 64) {
       const int c = b + lane;
-      int cc = 0;
-      uint64_t ks = 0, kn = 0;
+      int cc = 0, ch = -1, crow = -1;
+      double sv = 0.0, nv = 0.0;
       if (c < nc) {
         int lo = 0, hi = nb - 1;  // block q with pref[q] <= c < pref[q+1]
         while (lo < hi) {
@@ -1071,73 +1166,79 @@ __device__ void replay_inliers(const Pt *__restrict__ pts, int n, const int *cou
         }
         const int64_t slot = static_cast<int64_t>(lo) * per_block + (c - pref[lo]);
         cc = ld_agent(&ccount[slot]);
-        ks = key_std(ld_agent(&cstd[slot]));
-        kn = key_norm(ld_agent(&cnorm[slot]));
-        mismatch += (cc != counts[ld_agent(&cand[slot])]) ? 1 : 0;
+        sv = ld_agent(&cstd[slot]);
+        nv = ld_agent(&cnorm[slot]);
+        ch = ld_agent(&cand[slot]);
+        // its block's first candidate: its S_RANSAC is already in that block's spec row
+        crow = ld_agent(&spec_j[lo]) == c - pref[lo] ? lo : -1;
+        mismatch += (cc != ld_agent(&cfast[slot])) ? 1 : 0;
       }
+      const uint64_t ks = key_std(sv), kn = key_norm(nv);
       const int lim = min(64, nc - b);
       for (int q = 0; q < lim; ++q) {
         const int qc = __shfl(cc, q);
         const uint64_t qs = __shfl(ks, q);
         const uint64_t qn = __shfl(kn, q);
+        const int qh = __shfl(ch, q), qrow = __shfl(crow, q);
+        const double qsv = __shfl(sv, q), qnv = __shfl(nv, q);
+        bool take = false;
         if (qc > bcount) {
-          best = b + q;
+          take = true;
           bcount = qc;
-          bstd = qs;
         } else if (qc == bcount && bcount > 0 && bstd > qn) {
+          take = true;
+        }
+        if (take) {
           best = b + q;
           bstd = qs;
+          bh = qh;
+          brow = qrow;
+          bsv = qsv;
+          bnv = qnv;
         }
       }
     }
     mismatch = wave_sum_i(mismatch);
     if (lane == 0) {
-      res->n_candidates = nc;
-      res->max_count_fast = status[0];
-      res->guard_mismatch = mismatch;
-      if (hres) {
-        hres->n_candidates = nc;
-        hres->max_count_fast = status[0];
-        hres->guard_mismatch = mismatch;
-      }
-      status_out[1] = nc;
+      const int cfast_max = status[0];
+      double fw[9];
       if (best >= 0) {
-        int lo = 0, hi = nb - 1;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (pref[mid] <= best) lo = mid; else hi = mid - 1;
-        }
-        const int64_t slot = static_cast<int64_t>(lo) * per_block + (best - pref[lo]);
-        const int h = ld_agent(&cand[slot]);
-        res->best_index = h;
-        res->best_count = bcount;
-        res->best_std = ld_agent(&cstd[slot]);
-        res->best_norm = ld_agent(&cnorm[slot]);
-        res->best_cand = best;
-        for (int k = 0; k < 9; ++k) fsh[k] = Fsoa[k * ld + h];
-        have_s = 1;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) fw[k] = Fsoa[k * ld + bh];
       } else {
-        res->best_index = -1;
-        res->best_count = 0;
-        res->best_std = 0.0;
-        res->best_norm = 0.0;
-        res->best_cand = -1;
-        for (int k = 0; k < 9; ++k) fsh[k] = 0.0;
-        have_s = 0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) fw[k] = 0.0;
       }
-      for (int k = 0; k < 9; ++k) res->F[k] = fsh[k];
-      if (hres) {
-        hres->best_index = res->best_index;
-        hres->best_count = res->best_count;
-        hres->best_std = res->best_std;
-        hres->best_norm = res->best_norm;
-        hres->best_cand = res->best_cand;
-        for (int k = 0; k < 9; ++k) hres->F[k] = fsh[k];
+      const bool spec_ok = best >= 0 && brow >= 0;
+      F8DevResult *outs[2] = {res, hres};
+      for (int o = 0; o < 2; ++o) {
+        F8DevResult *r = outs[o];
+        if (!r) continue;
+        r->n_candidates = nc;
+        r->max_count_fast = cfast_max;
+        r->guard_mismatch = mismatch;
+        r->best_index = best >= 0 ? bh : -1;
+        r->best_count = best >= 0 ? bcount : 0;
+        r->best_std = best >= 0 ? bsv : 0.0;
+        r->best_norm = best >= 0 ? bnv : 0.0;
+        r->best_cand = best;
+        r->inl_row = spec_ok ? brow : -1;
+        if (spec_ok) r->n_inliers = bcount;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) r->F[k] = fw[k];
       }
+#pragma unroll
+      for (int k = 0; k < 9; ++k) fsh[k] = fw[k];
+      status_out[1] = nc;
+      have_s = best >= 0 ? 1 : 0;
+      spec_row_s = spec_ok ? brow : -1;
       base_s = 0;
     }
   }
   __syncthreads();
+  // the winner's S_RANSAC is its block's speculative list (the host copies that row:
+  // rs_f8_plan_result, inl_row); otherwise extract it here
+  if (spec_row_s >= 0) return;
   const bool have = have_s != 0;
   double f[9];
 #pragma unroll
@@ -1259,19 +1360,36 @@ hipError_t launch_pack_points32q(const Pt *pts, int n, const Frame &fr, float4 *
 hipError_t launch_f8_count32q(const float4 *ptsq, const Pt *pts, int n, int H,
                               const float *F32soa, const double *Fsoa, int64_t ld, int waves,
                               const GuardW &g, int *counts, hipStream_t s, int *gdone,
-                              int *status, const float4 *G4, bool use_asm) {
+                              int *status, const float4 *G4, bool use_asm, int block_threads,
+                              bool xcd_remap) {
   const int64_t npad = (n + 7) / 8 * 8;
   const int64_t total = static_cast<int64_t>((H + 63) / 64) * npad;
   int64_t W = std::max<int64_t>(1, std::min<int64_t>(waves, total / 64));
   int64_t per = (total + W - 1) / W;
   per = (per + 7) / 8 * 8;
   W = (total + per - 1) / per;
-  if (use_asm)
-    hipLaunchKernelGGL(k_f8_count32q<true>, dim3(static_cast<unsigned>((W + 3) / 4)), dim3(256),
-                       0, s, ptsq, pts, n, H, F32soa, Fsoa, ld, per, g, counts, gdone, status, G4);
-  else
-    hipLaunchKernelGGL(k_f8_count32q<false>, dim3(static_cast<unsigned>((W + 3) / 4)), dim3(256),
-                       0, s, ptsq, pts, n, H, F32soa, Fsoa, ld, per, g, counts, gdone, status, G4);
+  const int bt = block_threads == 1024 ? 1024 : block_threads == 512 ? 512 : 256;
+  const int64_t wpb = bt / 64;
+  int64_t nb = (W + wpb - 1) / wpb;
+  int rows = 0;
+  if (xcd_remap) {  // waves past W find an empty range (pos >= end) and exit
+    rows = static_cast<int>((nb + 7) / 8);
+    nb = 8 * static_cast<int64_t>(rows);
+  }
+  const dim3 grid(static_cast<unsigned>(nb)), block(static_cast<unsigned>(bt));
+#define RSD_Q_LAUNCH(A, B)                                                                     \
+  hipLaunchKernelGGL((k_f8_count32q<A, B>), grid, block, 0, s, ptsq, pts, n, H, F32soa, Fsoa, \
+                     ld, per, g, counts, gdone, status, G4, rows)
+  if (use_asm) {
+    if (bt == 1024) RSD_Q_LAUNCH(true, 1024);
+    else if (bt == 512) RSD_Q_LAUNCH(true, 512);
+    else RSD_Q_LAUNCH(true, 256);
+  } else {
+    if (bt == 1024) RSD_Q_LAUNCH(false, 1024);
+    else if (bt == 512) RSD_Q_LAUNCH(false, 512);
+    else RSD_Q_LAUNCH(false, 256);
+  }
+#undef RSD_Q_LAUNCH
   return hipGetLastError();
 }
 
@@ -1407,18 +1525,23 @@ __global__ __launch_bounds__(kTailThreads) void k_f8_tail_solve(TailArgs ta, int
   }
 }
 
-hipError_t launch_f8_tail_solve(TailArgs *ta, SolveArgs *sa, hipStream_t s) {
+hipError_t launch_f8_tail_solve(TailArgs *ta, SolveArgs *sa, hipStream_t s, int tail_cus) {
   int ntail = 0, nsolve = 0;
   TailArgs t{};
   SolveArgs v{};
-  if (ta) {
-    t = *ta;
-    t.per_block = select_per_block(t.H);
-    ntail = select_blocks(t.H);
-  }
   if (sa) {
     v = *sa;
     nsolve = (v.H + kTailThreads - 1) / kTailThreads;
+  }
+  if (ta) {
+    t = *ta;
+    // a solve workgroup (160 VGPRs) and a tail workgroup cannot share a CU, so the tail takes
+    // the CUs the solve leaves free (>= 32 blocks) and every workgroup starts at once;
+    // tail_blocks = 0 keeps the fixed 256-block split
+    int nb = kSelectBlocks;
+    if (tail_cus > 0) nb = std::min(kSelectBlocks, std::max(32, tail_cus - nsolve));
+    t.per_block = (t.H + nb - 1) / nb;
+    ntail = (t.H + t.per_block - 1) / t.per_block;
   }
   if (ntail + nsolve == 0) return hipSuccess;
   hipLaunchKernelGGL(k_f8_tail_solve, dim3(ntail + nsolve), dim3(kTailThreads), 0, s, t, ntail,

@@ -40,6 +40,9 @@ struct RunBufs {
   int *d_cand = nullptr;       // candidate hypothesis ids, per-block segments
   int *d_status = nullptr;     // [c*, n_candidates, ., ., per-block candidate counts]
   int *d_ccount = nullptr;
+  int *d_cfast = nullptr;      // fast counts of the candidates (guard_mismatch diagnostic)
+  int *d_spec = nullptr;       // per select block: S_RANSAC of its first candidate
+  int *d_spec_j = nullptr;     // per select block: that candidate's local index, or -1
   double *d_cstd = nullptr, *d_cnorm = nullptr;
   rsd::F8DevResult *d_res = nullptr;
   int *d_gdone = nullptr;      // per-group finish counters (fused c* in k_f8_count32x)
@@ -181,6 +184,8 @@ struct rs_f8_plan {
   bool per_hyp = true;        // per-hypothesis AM-GM decision constants ("w", "q")
   bool pointpair = true;      // "q" (default): DEC 3 decisions, packed over point pairs
   bool q_asm = true;          // RSAMD_QASM=0: "q" with compiler-scheduled builtins
+  int q_block = 256;          // RSAMD_QBLOCK: workgroup size of the "q" kernel (256 / 512 / 1024)
+  bool q_xcd = false;         // RSAMD_XCD=1: keep the slices of a hypothesis group on one XCD
   bool fuse_max = true;       // RSAMD_FUSEMAX=0: separate k_f8_max pass instead of the fused c*
   // HIP timing events per run (each is a marker packet between kernels): 0 none, 1 around the
   // counting kernel (default; the bench's roofline timing), 2 also the tail+solve launch
@@ -191,6 +196,7 @@ struct rs_f8_plan {
   bool prefetch = false;      // ping-pong point prefetch (RSAMD_PREFETCH=1; spills SGPRs at 8)
   int pk_variant = 0, pk_waves = 8192;
   int chunk_override = 0;     // fp64 kernel point chunk (RSAMD_CHUNK)
+  int tail_cus = 0;           // CUs for the tail + solve split (RSAMD_TAILCUS; 0: 256 tail blocks)
   int solve_diag = 0;         // RSAMD_SOLVE_DIAG: timing-only solve variants (wrong models)
 
   const RunBufs &last() const { return buf[(runs - 1) % kBufs]; }
@@ -215,6 +221,9 @@ static void plan_free(rs_f8_plan *p) {
     (void)hipFree(b.d_cand);
     (void)hipFree(b.d_status);
     (void)hipFree(b.d_ccount);
+    (void)hipFree(b.d_cfast);
+    (void)hipFree(b.d_spec);
+    (void)hipFree(b.d_spec_j);
     (void)hipFree(b.d_cstd);
     (void)hipFree(b.d_cnorm);
     (void)hipFree(b.d_res);
@@ -268,6 +277,7 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
       cus = 256;
     // slices of the (group, point) plane: 2 per resident wave slot (8 per SIMD) for the
     // default "q" kernel (A/B on C2: 16384 ahead of 8192 / 12288 / 24576 / 32768 by 1-3 %)
+    p->tail_cus = env_int("RSAMD_TAILCUS", cus);
     p->resident_waves = std::max(1, env_int("RSAMD_WAVES", cus * 4 * 8 * (p->pointpair ? 2 : 4)));
     p->count_block = env_int("RSAMD_BLOCK", 8) == 4 ? 4 : 8;
     p->prefetch = env_int("RSAMD_PREFETCH", 0) != 0;
@@ -290,6 +300,9 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
     ALLOC(b.d_cand, sizeof(int) * p->ld);
     ALLOC(b.d_status, sizeof(int) * rsd::kStatusWords);
     ALLOC(b.d_ccount, sizeof(int) * p->ld);
+    ALLOC(b.d_cfast, sizeof(int) * p->ld);
+    ALLOC(b.d_spec, sizeof(int) * rsd::kSelectBlocks * static_cast<size_t>(n));
+    ALLOC(b.d_spec_j, sizeof(int) * rsd::kSelectBlocks);
     ALLOC(b.d_cstd, sizeof(double) * p->ld);
     ALLOC(b.d_cnorm, sizeof(double) * p->ld);
     ALLOC(b.d_res, res_bytes);
@@ -308,6 +321,8 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
       if (e == hipSuccess) e = hipEventCreate(&ev);
   p->overlap = env_int("RSAMD_OVERLAP", 0) != 0;
   p->solve_diag = env_int("RSAMD_SOLVE_DIAG", 0);
+  p->q_block = env_int("RSAMD_QBLOCK", 256);
+  p->q_xcd = env_int("RSAMD_XCD", 0) != 0;
   if (p->overlap) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->ss, hipStreamNonBlocking);
     for (int k = 0; k < rs_f8_plan::kBufs; ++k) {
@@ -456,7 +471,7 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
     sa.gDn = gb.Dn;
   }
   if (tl >= 2) HIP_TRY(hipEventRecord(ev[2], sst));
-  HIP_TRY(rsd::launch_f8_tail_solve(p->tail_pending ? &p->tail : nullptr, &sa, sst));
+  HIP_TRY(rsd::launch_f8_tail_solve(p->tail_pending ? &p->tail : nullptr, &sa, sst, p->tail_cus));
   p->tail_pending = false;
   if (tl >= 2) HIP_TRY(hipEventRecord(ev[3], sst));
   if (p->overlap) {
@@ -477,7 +492,7 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
       HIP_TRY(rsd::launch_f8_count32q(p->d_pts32q, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
                                       p->resident_waves, gw, b.d_counts, ms,
                                       fused_max ? b.d_gdone : nullptr, b.d_status, b.d_G4,
-                                      p->q_asm));
+                                      p->q_asm, p->q_block, p->q_xcd));
     else
       HIP_TRY(rsd::launch_f8_count32x(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
                                       p->resident_waves, gw, b.d_counts, ms, p->count_block,
@@ -522,6 +537,9 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
   ta.thresh = thresh;
   ta.cand = b.d_cand;
   ta.ccount = b.d_ccount;
+  ta.cfast = b.d_cfast;
+  ta.spec = b.d_spec;
+  ta.spec_j = b.d_spec_j;
   ta.cstd = b.d_cstd;
   ta.cnorm = b.d_cnorm;
   ta.res = b.d_res;
@@ -563,9 +581,17 @@ extern "C" int rs_f8_plan_result(rs_f8_plan *p, rs_f8_result *out, int64_t *inli
   out->guard_mismatch = r->guard_mismatch;
   if (n_inliers) *n_inliers = r->n_inliers;
   const int64_t k = std::min<int64_t>(cap, r->n_inliers);
-  if (inliers && k > 0)  // S_RANSAC stays in HBM until asked for
-    HIP_TRY(hipMemcpy(inliers, p->last().d_res->inliers, sizeof(int64_t) * k,
-                      hipMemcpyDeviceToHost));
+  if (inliers && k > 0) {  // S_RANSAC stays in HBM until asked for
+    if (r->inl_row >= 0) {   // the winner's select block kept it (int32 row)
+      std::vector<int32_t> row(static_cast<size_t>(k));
+      HIP_TRY(hipMemcpy(row.data(), p->last().d_spec + r->inl_row * p->n, sizeof(int32_t) * k,
+                        hipMemcpyDeviceToHost));
+      for (int64_t i = 0; i < k; ++i) inliers[i] = row[static_cast<size_t>(i)];
+    } else {
+      HIP_TRY(hipMemcpy(inliers, p->last().d_res->inliers, sizeof(int64_t) * k,
+                        hipMemcpyDeviceToHost));
+    }
+  }
   return RS_OK;
 }
 
@@ -576,7 +602,10 @@ extern "C" int rs_f8_plan_candidates(rs_f8_plan *p, rs_f8_candidate *out, int64_
   if (st) return st;
   const RunBufs &b = p->last();
   const int H = static_cast<int>(p->last_H);
-  const int nb = rsd::select_blocks(H), pb = rsd::select_per_block(H);
+  int pb = 0;  // the select-block layout the tail used (status word 3)
+  HIP_TRY(hipMemcpy(&pb, b.d_status + 3, sizeof(int), hipMemcpyDeviceToHost));
+  if (pb < 1) return fail(RS_EINVAL, "no selection layout recorded for the last run");
+  const int nb = (H + pb - 1) / pb;
   std::vector<int> bc(nb);
   HIP_TRY(hipMemcpy(bc.data(), b.d_status + 4, sizeof(int) * nb, hipMemcpyDeviceToHost));
   std::vector<int> cand, cc;
