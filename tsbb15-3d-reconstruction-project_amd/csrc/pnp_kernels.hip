@@ -33,17 +33,20 @@ constexpr int ridx(int j, int l) { return j * 12 - (j * (j - 1)) / 2 + (l - j); 
 __device__ __forceinline__ void givens_row(double (&R)[78], double (&a)[12]) {
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
+    // rho = |(r, a_j)|, c = r / rho, s = a_j / rho from one reciprocal square root (a few ulp;
+    // the DLT's parity bar is 1e-6 on R, t) instead of a correctly rounded sqrt and divide
     const double r = R[ridx(j, j)];
-    const double rho = sqrt(r * r + a[j] * a[j]);
-    const double inv = rho > 0.0 ? 1.0 / rho : 0.0;
-    const double c = rho > 0.0 ? r * inv : 1.0;
+    const double q = fma(r, r, a[j] * a[j]);
+    const bool live = q > 0.0;
+    const double inv = live ? rsqrt_fast(live ? q : 1.0) : 0.0;
+    const double c = live ? r * inv : 1.0;
     const double s = a[j] * inv;
-    R[ridx(j, j)] = rho;
+    R[ridx(j, j)] = live ? q * inv : 0.0;
 #pragma unroll
     for (int l = j + 1; l < 12; ++l) {
       const double rl = R[ridx(j, l)];
-      R[ridx(j, l)] = c * rl + s * a[l];
-      a[l] = c * a[l] - s * rl;
+      R[ridx(j, l)] = fma(c, rl, s * a[l]);
+      a[l] = fma(c, a[l], -s * rl);
     }
   }
 }
@@ -62,60 +65,137 @@ __device__ __forceinline__ void dlt_rows(const PPt &p, double (&a0)[12], double 
     }
 }
 
-// Smallest right singular vector of the matrix whose R factor is given.
+// Smallest right singular vector of the matrix whose R factor is given: block inverse
+// iteration on R^T R with two vectors and a 2x2 Rayleigh-Ritz step per sweep.  The Ritz
+// vector converges at (s12 / s10)^2 per sweep instead of single-vector inverse iteration's
+// (s12 / s11)^2, which a noisy minimal sample can hold near 1 (C3 samples, host prototype:
+// a wave's slowest lane needs ~17 sweeps instead of ~100; deviation from numpy's SVD
+// <= 2.3e-12).  Stops when the Ritz vector moves <= 1e-15.
+__device__ __forceinline__ void tri_solve_rt_r(const double (&R)[78], const double (&dinv)[12],
+                                               double (&v)[12]) {
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {  // R^T z = v, in place
+    double acc = v[j];
+#pragma unroll
+    for (int i = 0; i < j; ++i) acc = fma(-R[ridx(i, j)], v[i], acc);
+    v[j] = acc * dinv[j];
+  }
+#pragma unroll
+  for (int j = 11; j >= 0; --j) {  // R w = z, in place
+    double acc = v[j];
+#pragma unroll
+    for (int l = j + 1; l < 12; ++l) acc = fma(-R[ridx(j, l)], v[l], acc);
+    v[j] = acc * dinv[j];
+  }
+}
+
+__device__ __forceinline__ double dot12(const double (&a)[12], const double (&b)[12]) {
+  double s = 0.0;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) s = fma(a[j], b[j], s);
+  return s;
+}
+
+// |R u|^2, (R u).(R v), |R v|^2 for upper-triangular R
+__device__ __forceinline__ void r_gram(const double (&R)[78], const double (&u)[12],
+                                       const double (&v)[12], double &uu, double &uv,
+                                       double &vv) {
+  uu = 0.0;
+  uv = 0.0;
+  vv = 0.0;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    double ru = 0.0, rv = 0.0;
+#pragma unroll
+    for (int l = j; l < 12; ++l) {
+      ru = fma(R[ridx(j, l)], u[l], ru);
+      rv = fma(R[ridx(j, l)], v[l], rv);
+    }
+    uu = fma(ru, ru, uu);
+    uv = fma(ru, rv, uv);
+    vv = fma(rv, rv, vv);
+  }
+}
+
+__device__ __forceinline__ void orthonormalize2(double (&u)[12], double (&v)[12]) {
+  const double iu = rsqrt_fast(dot12(u, u));
+#pragma unroll
+  for (int j = 0; j < 12; ++j) u[j] *= iu;
+  const double p = dot12(u, v);
+#pragma unroll
+  for (int j = 0; j < 12; ++j) v[j] = fma(-p, u[j], v[j]);
+  const double iv = rsqrt_fast(dot12(v, v));
+#pragma unroll
+  for (int j = 0; j < 12; ++j) v[j] *= iv;
+}
+
 __device__ __forceinline__ void smallest_right_sv(const double (&R)[78], double (&x)[12]) {
   double dinv[12];
 #pragma unroll
   for (int j = 0; j < 12; ++j) dinv[j] = 1.0 / R[ridx(j, j)];
-  // start: R^-1 e_11
+  // start: span(R^-1 e_11, R^-1 e_10)
+  double u[12], v[12];
 #pragma unroll
   for (int j = 11; j >= 0; --j) {
-    double acc = (j == 11) ? 1.0 : 0.0;
+    double au = (j == 11) ? 1.0 : 0.0, av = (j == 10) ? 1.0 : 0.0;
 #pragma unroll
-    for (int l = j + 1; l < 12; ++l) acc -= R[ridx(j, l)] * x[l];
-    x[j] = acc * dinv[j];
+    for (int l = j + 1; l < 12; ++l) {
+      au = fma(-R[ridx(j, l)], u[l], au);
+      av = fma(-R[ridx(j, l)], v[l], av);
+    }
+    u[j] = au * dinv[j];
+    v[j] = av * dinv[j];
   }
-  // Inverse iteration on R^T R: converges at (s12/s11)^2 per step; a noisy minimal sample can
-  // have s12/s11 ~ 0.5, so iterate to a fixed point (|dx| <= 1e-15) rather than a fixed count.
-  double nn = 0.0;
+  orthonormalize2(u, v);
 #pragma unroll
-  for (int j = 0; j < 12; ++j) nn += x[j] * x[j];
-  double inv = 1.0 / sqrt(nn);
-#pragma unroll
-  for (int j = 0; j < 12; ++j) x[j] *= inv;
-  for (int it = 0; it < 400; ++it) {
-    double z[12], w[12];
-#pragma unroll
-    for (int j = 0; j < 12; ++j) {  // R^T z = x
-      double acc = x[j];
-#pragma unroll
-      for (int i = 0; i < j; ++i) acc -= R[ridx(i, j)] * z[i];
-      z[j] = acc * dinv[j];
+  for (int j = 0; j < 12; ++j) x[j] = u[j];
+  double prev_delta = 1.0;
+  for (int it = 0; it < 200; ++it) {
+    tri_solve_rt_r(R, dinv, u);
+    tri_solve_rt_r(R, dinv, v);
+    orthonormalize2(u, v);
+    // Rayleigh-Ritz: smallest eigenvector y of G = (R [u v])^T (R [u v])
+    double a, b, c;
+    r_gram(R, u, v, a, b, c);
+    const double hd = 0.5 * (a - c);
+    const double lam = 0.5 * (a + c) - sqrt(fma(hd, hd, b * b));
+    // (b, lam - a) and (lam - c, b) both span the eigenvector; take the longer
+    double y0 = b, y1 = lam - a;
+    const double z0 = lam - c, z1 = b;
+    if (fma(z0, z0, z1 * z1) > fma(y0, y0, y1 * y1)) {
+      y0 = z0;
+      y1 = z1;
     }
-#pragma unroll
-    for (int j = 11; j >= 0; --j) {  // R w = z
-      double acc = z[j];
-#pragma unroll
-      for (int l = j + 1; l < 12; ++l) acc -= R[ridx(j, l)] * w[l];
-      w[j] = acc * dinv[j];
+    const double ny = fma(y0, y0, y1 * y1);
+    if (!(ny > 0.0)) {  // G already diagonal: u or v
+      y0 = a <= c ? 1.0 : 0.0;
+      y1 = a <= c ? 0.0 : 1.0;
+    } else {
+      const double iy = rsqrt_fast(ny);
+      y0 *= iy;
+      y1 *= iy;
     }
-    double ww = 0.0, dot = 0.0;
+    double w[12];
 #pragma unroll
-    for (int j = 0; j < 12; ++j) {
-      ww += w[j] * w[j];
-      dot += w[j] * x[j];
-    }
-    const double sgn = dot < 0.0 ? -1.0 : 1.0;
-    const double iw = sgn / sqrt(ww);
+    for (int j = 0; j < 12; ++j) w[j] = fma(y0, u[j], y1 * v[j]);
+    const double sgn = dot12(w, x) < 0.0 ? -1.0 : 1.0;
     double delta = 0.0;
 #pragma unroll
     for (int j = 0; j < 12; ++j) {
-      const double v = w[j] * iw;
-      delta = fmax(delta, fabs(v - x[j]));
-      x[j] = v;
+      const double nv = sgn * w[j];
+      delta = fmax(delta, fabs(nv - x[j]));
+      x[j] = nv;
     }
-    if (!(delta > 1e-15)) break;  // converged (or NaN: give up, the model scores zero)
+    // converged (or NaN: the model scores zero); or at the rounding floor, where the Ritz
+    // vector jitters at ~1e-15 instead of settling (it no longer halves its step)
+    if (it > 0 && !(delta > 1e-15)) break;
+    if (it > 1 && delta < 1e-13 && delta > 0.5 * prev_delta) break;
+    prev_delta = delta;
   }
+  // unit norm to full precision (a combination of an orthonormal pair, up to rounding)
+  const double in = 1.0 / sqrt(dot12(x, x));
+#pragma unroll
+  for (int j = 0; j < 12; ++j) x[j] *= in;
 }
 
 // Constraint enforcement (pnp.py:141-145): C0 = (A | b) -> (R, t).
@@ -193,7 +273,8 @@ __global__ __launch_bounds__(256) void k_pnp_solve(const PPt *__restrict__ pts, 
 }
 
 // One-point DLT over all m correspondences (rs_pnp_dlt): single lane.
-__global__ void k_pnp_dlt_all(const PPt *__restrict__ pts, int m, double *__restrict__ out) {
+__global__ __launch_bounds__(64) void k_pnp_dlt_all(const PPt *__restrict__ pts, int m,
+                                                    double *__restrict__ out) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   double R[78];
   for (int i = 0; i < 78; ++i) R[i] = 0.0;
@@ -252,11 +333,21 @@ __global__ __launch_bounds__(1024) void k_pnp_select(const int *__restrict__ cou
   __shared__ int sm[16], si[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   int bm = 0, bi = 0x7fffffff;
-  for (int i = tid; i < H; i += 1024) {
-    const int c = counts[i];
-    if (c > bm || (c == bm && i < bi)) {
-      bm = c;
-      bi = i;
+  // 8 loads in flight per thread before the (order-free) max / first-index comparisons
+  for (int i0 = tid; i0 < H; i0 += 8 * 1024) {
+    int c[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * 1024;
+      c[u] = i < H ? counts[i] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * 1024;
+      if (c[u] > bm || (c[u] == bm && i < bi)) {
+        bm = c[u];
+        bi = i;
+      }
     }
   }
 #pragma unroll
