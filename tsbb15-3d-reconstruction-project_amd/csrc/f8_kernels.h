@@ -50,6 +50,7 @@ struct SolveArgs {
   int *gdone;    // per-group finish counters zeroed (fused c*)
   float4 *G4;    // per-hypothesis decision constants (k_f8_count32x DEC 3), may be null
   double gT, gDe, gDn;  // their inputs: (t/s)^2 and the fp32 error bounds of e and m
+  int nt;               // non-temporal output stores (RSAMD_NTSTORE)
 };
 
 // One run's selection tail (candidates, reference statistics, replay, S_RANSAC).

@@ -70,6 +70,25 @@ __device__ __forceinline__ int add_block_count8(int cnt, const unsigned long lon
   return cnt;
 }
 
+// The solve's outputs (13 MB per 1e5 hypotheses) are read by the next launch, mostly on
+// another XCD: with nt they stream past this XCD's L2 instead of being written back at the
+// end of the launch (RSAMD_NTSTORE).
+template <class T>
+__device__ __forceinline__ void st_out(T *p, T v, bool nt) {
+  if (nt)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+__device__ __forceinline__ void st_out(float4 *p, float4 v, bool nt) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const f4 w = {v.x, v.y, v.z, v.w};
+  if (nt)
+    __builtin_nontemporal_store(w, reinterpret_cast<f4 *>(p));
+  else
+    *p = v;
+}
+
 // ----------------------------------------------------------------------------------------
 // One hypothesis h of a run: sample, 8-point F (float64), its unit-frame fp32 copy, and the
 // per-run zeroing the counting kernel and the selection tail rely on.
@@ -113,7 +132,7 @@ __device__ __forceinline__ void solve_one(const SolveArgs &a, int h) {
   double F[9];
   fmatrix8(xl, yl, xr, yr, F, a.diag);
 #pragma unroll
-  for (int k = 0; k < 9; ++k) Fsoa[k * ld + h] = F[k];
+  for (int k = 0; k < 9; ++k) st_out(&Fsoa[k * ld + h], F[k], a.nt);
   if (F32soa) {
     // F~ = T1^T F T2 (T_i = [[s,0,cx_i],[0,s,cy_i],[0,0,1]]), scaled to max |F~_ij| = 1
     double G[9];
@@ -135,7 +154,7 @@ __device__ __forceinline__ void solve_one(const SolveArgs &a, int h) {
     for (int k = 0; k < 9; ++k) mx = fmax(mx, fabs(Ft[k]));
     const double kap = 1.0 / mx;  // F = 0 or non-finite -> NaN model, counts 0 on both paths
 #pragma unroll
-    for (int k = 0; k < 9; ++k) F32soa[k * ld + h] = static_cast<float>(Ft[k] * kap);
+    for (int k = 0; k < 9; ++k) st_out(&F32soa[k * ld + h], static_cast<float>(Ft[k] * kap), a.nt);
     if (a.G4) {
       // k_f8_count32x DEC 3 constants, AM-GM split point c = t~ sqrt(m at the frame centre)
       // (any c > 0 is rigorous; this one keeps the band near the exact-|e| band)
@@ -151,8 +170,10 @@ __device__ __forceinline__ void solve_one(const SolveArgs &a, int h) {
       const double beta = T * (1.0 + u) * rcp_fast(1.0 - u) * im * (1.0 + 4.0 * u);
       const double ki = 1.02 * (De * c + De * De + T * Dn) * ip + 1e-30;
       const double ko = 1.02 * (T * Dn + De * c) * im + 1e-30;
-      a.G4[h] = make_float4(static_cast<float>(ki), -static_cast<float>(ko),
-                            static_cast<float>(alpha), static_cast<float>(beta));
+      st_out(&a.G4[h],
+             make_float4(static_cast<float>(ki), -static_cast<float>(ko),
+                         static_cast<float>(alpha), static_cast<float>(beta)),
+             a.nt);
     }
   }
 }

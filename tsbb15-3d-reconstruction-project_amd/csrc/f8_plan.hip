@@ -197,6 +197,7 @@ struct rs_f8_plan {
   int pk_variant = 0, pk_waves = 8192;
   int chunk_override = 0;     // fp64 kernel point chunk (RSAMD_CHUNK)
   int tail_cus = 0;           // CUs for the tail + solve split (RSAMD_TAILCUS; 0: 256 tail blocks)
+  int nt_store = 0;           // RSAMD_NTSTORE: non-temporal solve output stores
   int solve_diag = 0;         // RSAMD_SOLVE_DIAG: timing-only solve variants (wrong models)
 
   const RunBufs &last() const { return buf[(runs - 1) % kBufs]; }
@@ -321,6 +322,7 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
       if (e == hipSuccess) e = hipEventCreate(&ev);
   p->overlap = env_int("RSAMD_OVERLAP", 0) != 0;
   p->solve_diag = env_int("RSAMD_SOLVE_DIAG", 0);
+  p->nt_store = env_int("RSAMD_NTSTORE", 0);
   p->q_block = env_int("RSAMD_QBLOCK", 256);
   p->q_xcd = env_int("RSAMD_XCD", 0) != 0;
   if (p->overlap) {
@@ -463,6 +465,7 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
   sa.frame = fp32 ? p->frame : rsd::Frame{1.0, 0.0, 0.0, 0.0, 0.0};
   sa.gdone = b.d_gdone;
   sa.diag = p->solve_diag;
+  sa.nt = p->nt_store;
   if (fp32 && p->pair && p->per_hyp) {
     const Bounds gb = fp32_bounds(p->frame, thresh);
     sa.G4 = b.d_G4;
