@@ -364,6 +364,9 @@ def main():
                   "exchanging the per-pair records over gloo", file=sys.stderr)
             exchange = "gloo all-gather (RCCL init failed)"
             xcomm = _GlooComm(dist, rank, world)
+        # the first collective on a communicator sets up its channels (lazy, can take far
+        # longer than the timed steps): do it before the timed region
+        xcomm.allgather_bytes(np.zeros(96, np.uint8).tobytes())
 
     def step(i):
         # one full RANSAC run; runs are stream-ordered and issued back to back (each run

@@ -265,3 +265,32 @@ def test_fp32_and_fp64_counting_identical_full_size(ctx, monkeypatch, name):
         plan.close()
     for mode in COUNT_MODES:
         assert np.array_equal(counts[mode], counts["fp64"]), mode
+
+
+@pytest.mark.parametrize("knobs", [
+    {},                              # speculative S_RANSAC rows, tail on the CUs the solve leaves
+    {"RSAMD_NOSPEC": "1"},           # the replay extracts S_RANSAC itself
+    {"RSAMD_TAILCUS": "0"},          # fixed 256-block tail
+    {"RSAMD_SOLVE_DIAG": "8"},       # Jacobi SVD rank-2 step instead of the adjugate form
+])
+def test_selection_and_solve_variants_match_golden(ctx, monkeypatch, knobs):
+    """The selection-tail and rank-2 variants reproduce the reference run (C2 goldens: tuples
+    from np.random.seed(0), per-hypothesis counts, winner, S_RANSAC) back to back: each run's
+    tail rides with the next run's solve, and the last one is flushed alone."""
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    z = golden("synth_c2.npz")
+    H = len(z["counts"])
+    plan = _ffi.F8Plan(ctx, z["p1"].shape[1], H)
+    plan.set_points(z["p1"], z["p2"])
+    tup = z["tuples"].astype(np.int32)
+    for _ in range(3):
+        plan.run(H, mode=_ffi.SAMPLER_TUPLES, tuples=tup)
+    r, inl = plan.result()
+    assert np.array_equal(plan.counts(H), z["counts"])
+    assert r.best_index == int(z["best"])
+    assert np.array_equal(inl, z["S_ransac"].astype(np.int64))
+    assert fclose(np.array(r.F[:]).reshape(3, 3), z["F_ransac"])
+    cands = plan.candidates()
+    assert any(c.index == r.best_index for c in cands)
+    plan.close()

@@ -65,6 +65,7 @@ struct TailArgs {
   int *cand, *ccount;
   int *cfast;          // fast count of each candidate (guard_mismatch without a gather)
   int *spec, *spec_j;  // per block: S_RANSAC of its first candidate (n ints), that index
+  int nospec;          // RSAMD_NOSPEC=1: no speculative lists (the replay extracts S_RANSAC)
   double *cstd, *cnorm;
   F8DevResult *res;   // HBM result (header + S_RANSAC)
   F8DevResult *hres;  // pinned host header slot (device mapping), may be null

@@ -1003,7 +1003,7 @@ __device__ void cand_stats_block(const TailArgs &a, int bid, int nblocks) {
   const bool in_regs = n <= kRegPts * kTailThreads;
   if (tid == 0) {
     st_agent(&bc[bid], nloc);
-    st_agent(&a.spec_j[bid], (nloc > 0 && in_regs) ? 0 : -1);
+    st_agent(&a.spec_j[bid], (nloc > 0 && in_regs && !a.nospec) ? 0 : -1);
     if (bid == 0) st_agent(&status_rw[3], per_block);  // the layout, for rs_f8_plan_candidates
   }
   int *spec = a.spec + static_cast<int64_t>(bid) * n;
@@ -1053,7 +1053,7 @@ __device__ void cand_stats_block(const TailArgs &a, int bid, int nblocks) {
         cnt += shi[q];
       }
       mean = s1 / static_cast<double>(n);
-      if (j == 0) {  // the block's speculative S_RANSAC, in index order
+      if (j == 0 && !a.nospec) {  // the block's speculative S_RANSAC, in index order
 #pragma unroll
         for (int q = 0; q < kRegPts; ++q) {
           if ((bl[q] >> lane) & 1ull) {

@@ -197,6 +197,7 @@ struct rs_f8_plan {
   int pk_variant = 0, pk_waves = 8192;
   int chunk_override = 0;     // fp64 kernel point chunk (RSAMD_CHUNK)
   int tail_cus = 0;           // CUs for the tail + solve split (RSAMD_TAILCUS; 0: 256 tail blocks)
+  int nospec = 0;             // RSAMD_NOSPEC=1: the replay always extracts S_RANSAC itself
   int nt_store = 0;           // RSAMD_NTSTORE: non-temporal solve output stores
   int solve_diag = 0;         // RSAMD_SOLVE_DIAG: timing-only solve variants (wrong models)
 
@@ -323,6 +324,7 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
   p->overlap = env_int("RSAMD_OVERLAP", 0) != 0;
   p->solve_diag = env_int("RSAMD_SOLVE_DIAG", 0);
   p->nt_store = env_int("RSAMD_NTSTORE", 0);
+  p->nospec = env_int("RSAMD_NOSPEC", 0) != 0;
   p->q_block = env_int("RSAMD_QBLOCK", 256);
   p->q_xcd = env_int("RSAMD_XCD", 0) != 0;
   if (p->overlap) {
@@ -543,6 +545,7 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
   ta.cfast = b.d_cfast;
   ta.spec = b.d_spec;
   ta.spec_j = b.d_spec_j;
+  ta.nospec = p->nospec;
   ta.cstd = b.d_cstd;
   ta.cnorm = b.d_cnorm;
   ta.res = b.d_res;
