@@ -118,7 +118,7 @@ __global__ __launch_bounds__(kPairSelT) void k_pairs_select(
   const int n = static_cast<int>(off[b + 1] - o);
   const int *cnt = counts + static_cast<int64_t>(b) * H;
   int *cb = cand + static_cast<int64_t>(b) * H;
-  double *sb = cstd + static_cast<int64_t>(b) * H, *nb = cnorm + static_cast<int64_t>(b) * H;
+  double *nb = cnorm + static_cast<int64_t>(b) * H;  // cstd: kept for the launch layout
   // ---- c* ----
   int m = 0;
   for (int i = tid; i < H; i += kPairSelT) m = max(m, cnt[i]);
@@ -152,64 +152,83 @@ __global__ __launch_bounds__(kPairSelT) void k_pairs_select(
       __syncthreads();
     }
   }
-  // ---- np.std(d) (two-pass) and np.linalg.norm(d), wave per candidate ----
+  // ---- np.linalg.norm(d) of every candidate (wave per candidate, one pass) ----
   for (int j = w; j < nloc; j += kPairSelW) {
     const int64_t g = static_cast<int64_t>(b) * H + cb[j];
     double f[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) f[k] = Fsoa[k * ld + g];
-    double s1 = 0.0, s2 = 0.0;
+    double s2 = 0.0;
     for (int i = lane; i < n; i += 64) {
       const double d = dist_ref(f, pts[o + i]);
-      s1 += d;
       s2 += d * d;
     }
-    s1 = wsum(s1);
     s2 = wsum(s2);
-    const double mean = s1 / static_cast<double>(n);
-    double s3 = 0.0;
-    for (int i = lane; i < n; i += 64) {
-      const double v = dist_ref(f, pts[o + i]) - mean;
-      s3 += v * v;
-    }
-    s3 = wsum(s3);
-    if (lane == 0) {
-      sb[j] = sqrt(s3 / static_cast<double>(n));
-      nb[j] = sqrt(s2);
-    }
+    if (lane == 0) nb[j] = sqrt(s2);
   }
   __syncthreads();
-  // ---- fun.py:320-328 replay over the c* candidates (first one always taken) ----
-  if (tid == 0) {
+  // ---- fun.py:320-328 replay over the c* candidates (wave 0).  The first one is always
+  // taken; later ones replace the best only when best_std > norm(d_j), so the wave searches
+  // 64 norms per load for the next such j (ballot) and computes np.std(d) (two-pass) only for
+  // the candidates that become best.  C4's exact pairs tie at c* = N on ~all 1 000
+  // hypotheses: this replaces ~1 000 serial global loads and 1 000 std passes per pair. ----
+  if (w == 0) {
+    auto std_of = [&](int j) {
+      const int64_t g = static_cast<int64_t>(b) * H + cb[j];
+      double f[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) f[k] = Fsoa[k * ld + g];
+      double s1 = 0.0;
+      for (int i = lane; i < n; i += 64) s1 += dist_ref(f, pts[o + i]);
+      s1 = wsum(s1);
+      const double mean = s1 / static_cast<double>(n);
+      double s3 = 0.0;
+      for (int i = lane; i < n; i += 64) {
+        const double v = dist_ref(f, pts[o + i]) - mean;
+        s3 += v * v;
+      }
+      s3 = wsum(s3);
+      return sqrt(s3 / static_cast<double>(n));
+    };
     int best = -1;
     double bstd = 0.0;
-    for (int j = 0; j < nloc; ++j) {
-      if (best < 0) {
-        best = j;
-        bstd = sb[j];
-      } else if (bstd > nb[j]) {  // false for NaN on either side, as numpy's ">"
-        best = j;
-        bstd = sb[j];
+    if (nloc > 0) {
+      best = 0;
+      bstd = std_of(0);
+      int j0 = 1;
+      while (j0 < nloc) {
+        const int j = j0 + lane;
+        const bool repl = j < nloc && bstd > nb[j];  // false for NaN on either side
+        const unsigned long long bal = __ballot(repl);
+        if (bal == 0ull) {
+          j0 += 64;
+          continue;
+        }
+        best = j0 + __ffsll(static_cast<long long>(bal)) - 1;
+        bstd = std_of(best);
+        j0 = best + 1;
       }
     }
-    s_best = best;
-    PairDevResult r;
-    if (best >= 0) {
-      const int64_t g = static_cast<int64_t>(b) * H + cb[best];
-      for (int k = 0; k < 9; ++k) r.F[k] = Fsoa[k * ld + g];
-      r.best_index = cb[best];
-      r.best_count = cstar;
-      r.best_std = sb[best];
-      r.best_norm = nb[best];
-    } else {
-      for (int k = 0; k < 9; ++k) r.F[k] = __builtin_nan("");
-      r.best_index = -1;
-      r.best_count = 0;
-      r.best_std = __builtin_nan("");
-      r.best_norm = __builtin_nan("");
+    if (lane == 0) {
+      s_best = best;
+      PairDevResult r;
+      if (best >= 0) {
+        const int64_t g = static_cast<int64_t>(b) * H + cb[best];
+        for (int k = 0; k < 9; ++k) r.F[k] = Fsoa[k * ld + g];
+        r.best_index = cb[best];
+        r.best_count = cstar;
+        r.best_std = bstd;
+        r.best_norm = nb[best];
+      } else {
+        for (int k = 0; k < 9; ++k) r.F[k] = __builtin_nan("");
+        r.best_index = -1;
+        r.best_count = 0;
+        r.best_std = __builtin_nan("");
+        r.best_norm = __builtin_nan("");
+      }
+      r.n_candidates = nloc;
+      res[b] = r;
     }
-    r.n_candidates = nloc;
-    res[b] = r;
   }
   __syncthreads();
   if (s_best < 0) return;

@@ -105,14 +105,17 @@ def shard_range(H, world, rank):
 
 
 def lpt_assign(costs, world):
-    """Longest-processing-time greedy: list of item indices per rank (deterministic)."""
-    order = sorted(range(len(costs)), key=lambda i: (-costs[i], i))
-    load = [0.0] * world
+    """Longest-processing-time greedy: list of item indices per rank (deterministic: ties in
+    cost go to the lower index, ties in load to the lower rank)."""
+    import heapq
+    costs = np.asarray(costs, dtype=np.float64)
+    order = np.lexsort((np.arange(len(costs)), -costs))
+    heap = [(0.0, q) for q in range(world)]
     out = [[] for _ in range(world)]
-    for i in order:
-        r = min(range(world), key=lambda q: (load[q], q))
+    for i in order.tolist():
+        load, r = heapq.heappop(heap)
         out[r].append(i)
-        load[r] += costs[i]
+        heapq.heappush(heap, (load + float(costs[i]), r))
     return [sorted(v) for v in out]
 
 
@@ -280,24 +283,30 @@ def run_pairs(comm, pairs, H, solve, refine=None):
     items = []
     mine = [i for i in owners[comm.rank] if pairs[i][0].shape[1] >= 8]
     if hasattr(solve, "many"):
-        results = dict(zip(mine, solve.many(mine, [pairs[i] for i in mine])))
+        outs = solve.many(mine, [pairs[i] for i in mine])
     else:
-        results = {i: solve(i, *pairs[i]) for i in mine}
-    for i in mine:
-        p1, p2 = pairs[i]
-        out = results[i]
-        valid, best, count, std, F = out[:5]
-        recs[i]["pair"], recs[i]["valid"], recs[i]["best_index"] = i, valid, best
-        recs[i]["count"], recs[i]["std"], recs[i]["F"] = count, std, F
-        if refine is not None and valid and len(out) > 5 and len(out[5]) > 0:
+        outs = [solve(i, *pairs[i]) for i in mine]
+    if mine:  # column-wise record fill (one fancy-indexed store per field)
+        idx = np.asarray(mine, dtype=np.int64)
+        recs["valid"][idx] = [o[0] for o in outs]
+        recs["best_index"][idx] = [o[1] for o in outs]
+        recs["count"][idx] = [o[2] for o in outs]
+        recs["std"][idx] = [o[3] for o in outs]
+        recs["F"][idx] = np.stack([np.asarray(o[4], dtype=np.float64).ravel() for o in outs])
+    for i, out in zip(mine, outs):
+        if refine is not None and out[0] and len(out) > 5 and len(out[5]) > 0:
+            p1, p2 = pairs[i]
             S = np.asarray(out[5])
-            items.append((i, np.asarray(F), p1[:, S], p2[:, S], p1[:, 0], p2[:, 0]))
-    if refine is not None:
-        for it, (Fg, cost, found, R, t) in zip(items, refine(items)):
-            r = recs[it[0]]
-            r["refined"], r["F_gold"], r["gs_cost"] = 1, Fg, cost
-            r["pose"], r["R"], r["t"] = found, R, t
-            recs[it[0]] = r
+            items.append((i, np.asarray(out[4]), p1[:, S], p2[:, S], p1[:, 0], p2[:, 0]))
+    if refine is not None and items:
+        ref = refine(items)
+        idx = np.asarray([it[0] for it in items], dtype=np.int64)
+        recs["refined"][idx] = 1
+        recs["F_gold"][idx] = np.stack([np.asarray(r[0], dtype=np.float64).ravel() for r in ref])
+        recs["gs_cost"][idx] = [r[1] for r in ref]
+        recs["pose"][idx] = [r[2] for r in ref]
+        recs["R"][idx] = np.stack([np.asarray(r[3], dtype=np.float64).ravel() for r in ref])
+        recs["t"][idx] = np.stack([np.asarray(r[4], dtype=np.float64).ravel() for r in ref])
     parts = comm.allgather_bytes(recs.tobytes())
     table = np.zeros(len(pairs), dtype=PAIR_DTYPE)
     for r, p in enumerate(parts):
