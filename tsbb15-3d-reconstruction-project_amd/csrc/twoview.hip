@@ -3,7 +3,8 @@
 //   k_triangulate_optimal  lane per point: lab3.triangulate_optimal (lab3.py:382-475)
 //   k_resection            lane per camera: fun.camera_resectioning (fun.py:260-280)
 //   k_essential            lane per pair: E = K^T F K (fun.getEAndK, fun.py:101)
-//   k_relative_pose        lane per pair: fun.relative_camera_pose (fun.py:209-258)
+//   k_relative_pose        quad per pair (lane per candidate pose): fun.relative_camera_pose
+//                          (fun.py:209-258)
 //   k_fmatrix_cameras / k_fmatrix_from_cameras: lab3.py:353-380 / 331-351
 //   k_gold_standard        workgroup per pair: the gold-standard tail of fun.getFFromLabCode
 //                          (fun.py:336-369) -- cameras from F_RANSAC, optimal triangulation of
@@ -128,8 +129,11 @@ __global__ __launch_bounds__(128) void k_relative_pose(const double *__restrict_
                                 const double *__restrict__ y2, int64_t Bn,
                                 double *__restrict__ Rout, double *__restrict__ tout,
                                 int32_t *__restrict__ found) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= Bn) return;
+  const int64_t gt = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t i0 = gt >> 2;
+  const int k = static_cast<int>(gt & 3);
+  const bool live = i0 < Bn;
+  const int64_t i = live ? i0 : Bn - 1;  // padding quads recompute the last pair, store nothing
   double B[9], V[9];
 #pragma unroll
   for (int q = 0; q < 9; ++q) B[q] = Es[9 * i + q];
@@ -166,36 +170,40 @@ __global__ __launch_bounds__(128) void k_relative_pose(const double *__restrict_
       Ra[3 * r + c] = base + x;
       Rb[3 * r + c] = base - x;
     }
+  // the four (R, t) candidates of fun.py:238-254, one per lane of the pair's quad, each with
+  // its optimal triangulation of the first correspondence; the first that passes wins
   const double I34[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
-  int which = 0;
-  double Rw[9], tw[3];
-  for (int k = 0; k < 4 && !which; ++k) {
-    const double *Rk = (k & 1) ? Rb : Ra;
-    const double sg = k < 2 ? 1.0 : -1.0;
-    double C2[12];
+  const double *Rk = (k & 1) ? Rb : Ra;
+  const double sg = k < 2 ? 1.0 : -1.0;
+  double C2[12];
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      C2[4 * r + 0] = Rk[3 * r + 0];
-      C2[4 * r + 1] = Rk[3 * r + 1];
-      C2[4 * r + 2] = Rk[3 * r + 2];
-      C2[4 * r + 3] = sg * v3[r];
-    }
-    double X[3];
-    triangulate_optimal(I34, C2, y1[2 * i], y1[2 * i + 1], y2[2 * i], y2[2 * i + 1], X);
-    const double z2 = Rk[6] * X[0] + Rk[7] * X[1] + Rk[8] * X[2] + sg * v3[2];
-    if (X[2] > 0.0 && z2 > 0.0) {
-      which = k + 1;
-#pragma unroll
-      for (int q2 = 0; q2 < 9; ++q2) Rw[q2] = Rk[q2];
-#pragma unroll
-      for (int r = 0; r < 3; ++r) tw[r] = sg * v3[r];
-    }
+  for (int r = 0; r < 3; ++r) {
+    C2[4 * r + 0] = Rk[3 * r + 0];
+    C2[4 * r + 1] = Rk[3 * r + 1];
+    C2[4 * r + 2] = Rk[3 * r + 2];
+    C2[4 * r + 3] = sg * v3[r];
   }
-  found[i] = which;
+  double X[3];
+  triangulate_optimal(I34, C2, y1[2 * i], y1[2 * i + 1], y2[2 * i], y2[2 * i + 1], X);
+  const double z2 = Rk[6] * X[0] + Rk[7] * X[1] + Rk[8] * X[2] + sg * v3[2];
+  const bool pass = X[2] > 0.0 && z2 > 0.0;
+  // quad lanes 4j..4j+3 hold k = 0..3 of one pair (the grid is a multiple of 4 lanes)
+  const unsigned long long bal = __ballot(pass);
+  const int q0 = (threadIdx.x & 63) & ~3;
+  const unsigned quad = static_cast<unsigned>((bal >> q0) & 0xfull);
+  const int which = quad ? __ffs(quad) : 0;  // first passing candidate, 1-based
+  if (live && which == k + 1) {
 #pragma unroll
-  for (int q2 = 0; q2 < 9; ++q2) Rout[9 * i + q2] = which ? Rw[q2] : __builtin_nan("");
+    for (int q2 = 0; q2 < 9; ++q2) Rout[9 * i + q2] = Rk[q2];
 #pragma unroll
-  for (int r = 0; r < 3; ++r) tout[3 * i + r] = which ? tw[r] : __builtin_nan("");
+    for (int r = 0; r < 3; ++r) tout[3 * i + r] = sg * v3[r];
+  } else if (live && which == 0 && k == 0) {
+#pragma unroll
+    for (int q2 = 0; q2 < 9; ++q2) Rout[9 * i + q2] = __builtin_nan("");
+#pragma unroll
+    for (int r = 0; r < 3; ++r) tout[3 * i + r] = __builtin_nan("");
+  }
+  if (live && k == 0) found[i] = which;
 }
 
 __global__ __launch_bounds__(128) void k_fmatrix_cameras(const double *__restrict__ F, int64_t B,
@@ -340,7 +348,6 @@ __global__ __launch_bounds__(kGsT) void k_gold_standard(
     double *__restrict__ C1out, GsInfo *__restrict__ info) {
   __shared__ double red[kGsW * 94];
   __shared__ double sU[78], sgc[12], sres[94], sC[12], sdc[12];
-  __shared__ double S[12][13];  // damped Schur complement, Cholesky in place (thread 0)
   __shared__ double s_lam, s_nu, s_cost, s_cost0;
   __shared__ int s_state, s_it, s_acc, s_status;
   const int tid = threadIdx.x;
@@ -438,44 +445,54 @@ __global__ __launch_bounds__(kGsT) void k_gold_standard(
       block_reduce<90>(acc, red, sres);
     }
     if (tid == 0) {
-      // S = U + lam diag(U) - sum W Vi W^T;  rhs = -gc + sum W Vi gx;  Cholesky
-      double y[12];
+      // S = U + lam diag(U) - sum W Vi W^T;  rhs = -gc + sum W Vi gx;  Cholesky.  Fully
+      // unrolled over a register copy of S (lower triangle, 78 doubles): the loop-carried
+      // dependences are then FMA latencies, not LDS round trips.
+      double L[78], y[12];
+#pragma unroll
       for (int p = 0; p < 12; ++p)
-        for (int q = p; q < 12; ++q) {
-          double v = sU[up12(p, q)] - sres[up12(p, q)];
+#pragma unroll
+        for (int q = 0; q <= p; ++q) {
+          double v = sU[up12(q, p)] - sres[up12(q, p)];
           if (p == q) v += lam * sU[up12(p, p)];
-          S[p][q] = v;
-          S[q][p] = v;
+          L[p * (p + 1) / 2 + q] = v;
         }
+#pragma unroll
       for (int p = 0; p < 12; ++p) y[p] = -sgc[p] + sres[78 + p];
       bool ok = true;
-      for (int k = 0; k < 12 && ok; ++k) {
-        double d = S[k][k];
-        for (int m = 0; m < k; ++m) d -= S[k][m] * S[k][m];
-        if (!(d > 0.0)) {
-          ok = false;
-          break;
-        }
-        d = sqrt(d);
-        S[k][k] = d;
+      double dinv[12];
+#pragma unroll
+      for (int k = 0; k < 12; ++k) {
+        double d = L[k * (k + 1) / 2 + k];
+#pragma unroll
+        for (int m = 0; m < k; ++m) d -= L[k * (k + 1) / 2 + m] * L[k * (k + 1) / 2 + m];
+        ok = ok && d > 0.0;
+        d = sqrt(d > 0.0 ? d : 1.0);
+        dinv[k] = 1.0 / d;
+        L[k * (k + 1) / 2 + k] = d;
+#pragma unroll
         for (int i = k + 1; i < 12; ++i) {
-          double v = S[i][k];
-          for (int m = 0; m < k; ++m) v -= S[i][m] * S[k][m];
-          S[i][k] = v / d;
+          double v = L[i * (i + 1) / 2 + k];
+#pragma unroll
+          for (int m = 0; m < k; ++m) v -= L[i * (i + 1) / 2 + m] * L[k * (k + 1) / 2 + m];
+          L[i * (i + 1) / 2 + k] = v * dinv[k];
         }
       }
-      if (ok) {
-        for (int i = 0; i < 12; ++i) {
-          double v = y[i];
-          for (int m = 0; m < i; ++m) v -= S[i][m] * y[m];
-          y[i] = v / S[i][i];
-        }
-        for (int i = 11; i >= 0; --i) {
-          double v = y[i];
-          for (int m = i + 1; m < 12; ++m) v -= S[m][i] * y[m];
-          y[i] = v / S[i][i];
-        }
+#pragma unroll
+      for (int i = 0; i < 12; ++i) {
+        double v = y[i];
+#pragma unroll
+        for (int m = 0; m < i; ++m) v -= L[i * (i + 1) / 2 + m] * y[m];
+        y[i] = v * dinv[i];
       }
+#pragma unroll
+      for (int i = 11; i >= 0; --i) {
+        double v = y[i];
+#pragma unroll
+        for (int m = i + 1; m < 12; ++m) v -= L[m * (m + 1) / 2 + i] * y[m];
+        y[i] = v * dinv[i];
+      }
+#pragma unroll
       for (int p = 0; p < 12; ++p) sdc[p] = ok ? y[p] : 0.0;
       s_state = ok ? 0 : 1;
     }
@@ -541,6 +558,10 @@ __global__ __launch_bounds__(kGsT) void k_gold_standard(
           if (s_state == 3) s_status = 1;
         } else {
           s_state = 1;
+          // rejected with a predicted decrease at the rounding level of the cost: more damping
+          // only shrinks the step, so this is the minimum (parameters unchanged).  Stops the
+          // ~15 rejections the lam > 1e32 exit would otherwise spend (status 2 either way).
+          if (pred >= 0.0 && pred <= 1e-15 * cost) s_status = 2;
         }
       }
       __syncthreads();
@@ -713,7 +734,7 @@ extern "C" int rs_relative_camera_pose(rs_ctx *c, const double *E, const double 
   HIP_TRY(hipMemcpyAsync(b[0], E, sizeof(double) * 9 * B, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemcpyAsync(b[1], y1, sizeof(double) * 2 * B, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemcpyAsync(b[2], y2, sizeof(double) * 2 * B, hipMemcpyHostToDevice, c->stream));
-  hipLaunchKernelGGL(rsd::k_relative_pose, dim3(grid(B)), dim3(128), 0, c->stream,
+  hipLaunchKernelGGL(rsd::k_relative_pose, dim3(grid(4 * B)), dim3(128), 0, c->stream,
                      reinterpret_cast<double *>(b[0]), reinterpret_cast<double *>(b[1]),
                      reinterpret_cast<double *>(b[2]), B, reinterpret_cast<double *>(b[3]),
                      reinterpret_cast<double *>(b[4]), reinterpret_cast<int32_t *>(b[5]));
