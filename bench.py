@@ -38,7 +38,7 @@ OUTLIERS = 0.30
 HYPS = 100_000
 PEAK_FP64_VALU_TFLOPS = 78.6   # 256 CU x 4 SIMD x 16 fp64 FMA lanes x 2 x 2.4 GHz
 PEAK_FP32_VALU_TFLOPS = 157.3  # MI355X_MICROARCH.md: 64 FLOP/clk/SIMD (v_pk_fma_f32)
-TIMING_EVERY = 4               # HIP events around the counting kernel on every 4th timed run
+TIMING_EVERY = 8               # HIP events around the counting kernel on every 8th timed run
 PEAK_HBM_GBS = 8000.0
 FLOP_PER_CORR = 42             # score work per (hypothesis, correspondence)
 FLOP_SOLVE = 15000             # minimal solve per hypothesis
@@ -309,8 +309,8 @@ def load_pmc(n_corr, hyps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--hyps", type=int, default=HYPS)
     ap.add_argument("--n", type=int, default=N_CORR)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
