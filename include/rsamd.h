@@ -59,6 +59,14 @@ int rs_py_seed(const uint32_t *words, int32_t n_words, uint32_t *mt_key, int32_t
 int rs_py_shuffle_tuples(uint32_t *mt_key, int32_t *mt_pos, int64_t n, int32_t k, int64_t count,
                          int32_t *out);
 
+/* MT19937 jump-ahead: the (key, pos) state after `steps` more 32-bit outputs, computed as
+ * x^J mod phi applied to the state (phi: the generator's characteristic polynomial), without
+ * generating the words.  Same representation as np.random.get_state() / random.getstate():
+ * key is the raw block holding the next word.  Replaces nothing in the reference; it is the
+ * building block for starting many generators along one np.random / random stream. */
+int rs_mt_jump(const uint32_t *mt_key, int32_t mt_pos, int64_t steps, uint32_t *key_out,
+               int32_t *pos_out);
+
 /* ------------------------------------------------------------------------------------------
  * Context
  * ---------------------------------------------------------------------------------------- */

@@ -107,3 +107,23 @@ def test_py_shuffle_matches_reference_gen_rnd_indices():
     assert tup.tolist() == misc["gen_rnd_indices_seed12345_37_6"]
     with pytest.raises(ValueError, match="Cannot generate more indices"):
         _ffi.py_shuffle_tuples(key, pos, 5, 6, 1)
+
+
+@pytest.mark.parametrize("seed,pre", [(0, 0), (7, 300), (12345, 624)])
+def test_mt_jump_matches_sequential_draws(seed, pre):
+    """rs_mt_jump (x^J mod the characteristic polynomial) lands on the exact state CPython's
+    generator reaches after J getrandbits(32) draws, from fresh and mid-block states."""
+    r = random.Random(seed)
+    for _ in range(pre):
+        r.getrandbits(32)
+    st = r.getstate()[1]
+    key0, pos0 = np.array(st[:624], np.uint32), st[624]
+    done = 0
+    for steps in (0, 1, 623 - pos0 % 624 + 1, 624, 625, 1000, 20_000, 123_457):
+        while done < steps:
+            r.getrandbits(32)
+            done += 1
+        key, pos = _ffi.mt_jump(key0, pos0, steps)
+        ref = r.getstate()[1]
+        assert pos == ref[624], steps
+        assert np.array_equal(key, np.array(ref[:624], np.uint32)), steps

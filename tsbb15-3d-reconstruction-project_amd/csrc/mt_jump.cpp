@@ -1,0 +1,220 @@
+// MT19937 jump-ahead (host): the state after J more words without generating them.
+//
+// The generator is linear over GF(2): the 19937-bit state advances by one word through a
+// fixed matrix T with a primitive characteristic polynomial phi (degree 19937).  Then
+// T^J = p(T) with p(x) = x^J mod phi, and p(T) s = XOR of T^i s over the set bits i of p.
+// With the word sequence y_k of state s (y_0..y_623 = the window, y_{k+624} = y_{k+397} ^
+// twist(y_k, y_{k+1})), T^i s is the window y_i..y_{i+623}, so word w of the jumped window
+// is the XOR of y_{i+w} over the set bits i of p (only the top bit of word 0 is state; the
+// caller asks for the window one word early when it needs that word whole).
+//
+//   phi: Berlekamp-Massey on 2 x 19937 output bits of any seeded generator (once per
+//        process, ~20 ms), verified against the next 4096 bits;
+//   p:   left-to-right binary powering (square, times x) modulo phi;
+//   numpy's state (key[624], pos) is the raw block holding the next word plus the offset.
+//
+// Used by the parity sampler to start many generators along one numpy / CPython stream.
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "common.h"
+
+namespace {
+
+constexpr int kN = 624;
+constexpr int kM = 397;
+constexpr int kDeg = 19937;
+constexpr int kWords = (kDeg + 64) / 64 + 1;  // polynomial words (degree <= kDeg)
+
+inline uint32_t twist(uint32_t a, uint32_t b, uint32_t m) {
+  const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+  return m ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+}
+inline uint32_t temper(uint32_t y) {
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+
+// GF(2)[x] polynomial, bit i = coefficient of x^i
+using Poly = std::vector<uint64_t>;
+
+inline int getbit(const Poly &p, int64_t i) { return static_cast<int>((p[i >> 6] >> (i & 63)) & 1u); }
+inline void flipbit(Poly &p, int64_t i) { p[i >> 6] ^= 1ull << (i & 63); }
+
+// p ^= q << s (words of q beyond p's size must be zero: degrees are bounded by the caller)
+void xor_shifted(Poly &p, const Poly &q, int64_t s) {
+  const int64_t ws = s >> 6;
+  const int bs = static_cast<int>(s & 63);
+  const int64_t np = static_cast<int64_t>(p.size());
+  for (int64_t i = 0; i < static_cast<int64_t>(q.size()); ++i) {
+    const uint64_t v = q[i];
+    if (!v) continue;
+    if (i + ws < np) p[i + ws] ^= v << bs;
+    if (bs && i + ws + 1 < np) p[i + ws + 1] ^= v >> (64 - bs);
+  }
+}
+
+const Poly &charpoly() {
+  static Poly phi;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    // bit 0 of successive outputs of a seeded generator (any seed: phi is primitive)
+    const int64_t nb = 2 * kDeg + 4096;
+    std::vector<uint8_t> s(static_cast<size_t>(nb));
+    uint32_t mt[kN];
+    mt[0] = 5489u;
+    for (int i = 1; i < kN; ++i)
+      mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + static_cast<uint32_t>(i);
+    int pos = kN;
+    for (int64_t t = 0; t < nb; ++t) {
+      if (pos >= kN) {
+        for (int i = 0; i < kN; ++i) mt[i] = twist(mt[i], mt[(i + 1) % kN], mt[(i + kM) % kN]);
+        pos = 0;
+      }
+      s[static_cast<size_t>(t)] = static_cast<uint8_t>(temper(mt[pos++]) & 1u);
+    }
+    // Berlekamp-Massey over GF(2): C(x) = 1 + c1 x + ... + cL x^L, s_n = sum c_i s_{n-i}
+    const int64_t nbm = 2 * kDeg;
+    Poly C(2 * kWords, 0), B(2 * kWords, 0), T;
+    C[0] = B[0] = 1;
+    int64_t L = 0, m = 1;
+    // reversed sequence bits, packed: bit j of rs = s_{nbm - 1 - j}
+    Poly rs((nbm + 64) / 64 + 2, 0);
+    for (int64_t j = 0; j < nbm; ++j)
+      if (s[static_cast<size_t>(nbm - 1 - j)]) rs[j >> 6] |= 1ull << (j & 63);
+    auto window = [&](int64_t bit) -> uint64_t {  // 64 bits of rs from `bit`
+      const int64_t w = bit >> 6;
+      const int b = static_cast<int>(bit & 63);
+      uint64_t lo = rs[w] >> b;
+      if (b) lo |= rs[w + 1] << (64 - b);
+      return lo;
+    };
+    for (int64_t n = 0; n < nbm; ++n) {
+      // d = sum_{i=0..L} c_i s_{n-i}; s_{n-i} = rs bit (nbm - 1 - n + i)
+      uint64_t acc = 0;
+      const int64_t base = nbm - 1 - n;
+      for (int64_t w = 0; w <= (L >> 6); ++w) {
+        uint64_t cw = C[w];
+        if (w == (L >> 6)) {
+          const int keep = static_cast<int>(L & 63) + 1;
+          if (keep < 64) cw &= (1ull << keep) - 1;
+        }
+        if (cw) acc ^= cw & window(base + 64 * w);
+      }
+      const int d = __builtin_parityll(acc);
+      if (!d) {
+        ++m;
+      } else if (2 * L <= n) {
+        T = C;
+        xor_shifted(C, B, m);
+        L = n + 1 - L;
+        B = T;
+        m = 1;
+      } else {
+        xor_shifted(C, B, m);
+        ++m;
+      }
+    }
+    // C is the reciprocal of phi: phi(x) = x^L C(1/x)
+    phi.assign(kWords, 0);
+    for (int64_t i = 0; i <= L; ++i)
+      if (getbit(C, i)) flipbit(phi, L - i);
+    (void)T;
+  });
+  return phi;
+}
+
+// r = r^2 mod phi (deg r < kDeg)
+void square_mod(Poly &r, const Poly &phi) {
+  Poly sq(2 * kWords + 2, 0);
+  for (int64_t i = 0; i < kWords; ++i) {
+    const uint64_t v = r[i];
+    if (!v) continue;
+    for (int b = 0; b < 64; ++b)
+      if ((v >> b) & 1u) flipbit(sq, 2 * (64 * i + b));
+  }
+  for (int64_t i = 2 * (kDeg - 1); i >= kDeg; --i)
+    if (getbit(sq, i)) xor_shifted(sq, phi, i - kDeg);
+  for (int64_t i = 0; i < kWords; ++i) r[i] = sq[i];
+}
+
+// r = r * x mod phi
+void times_x_mod(Poly &r, const Poly &phi) {
+  uint64_t carry = 0;
+  for (int64_t i = 0; i < kWords; ++i) {
+    const uint64_t v = r[i];
+    r[i] = (v << 1) | carry;
+    carry = v >> 63;
+  }
+  if (getbit(r, kDeg))
+    for (int64_t i = 0; i < kWords; ++i) r[i] ^= phi[i];
+}
+
+}  // namespace
+
+namespace rs {
+
+// x^J mod phi as little-endian 64-bit words (kDeg bits); J >= 0.
+void mt_jump_poly(uint64_t J, std::vector<uint64_t> &out) {
+  const Poly &phi = charpoly();
+  Poly r(kWords, 0);
+  r[0] = 1;
+  for (int b = 63; b >= 0; --b) {
+    square_mod(r, phi);
+    if ((J >> b) & 1u) times_x_mod(r, phi);
+  }
+  out = r;
+}
+
+// Window (y_0..y_623) advanced by the polynomial p: out[w] = XOR_{i: p_i} y_{i+w}.
+void mt_apply_poly(const uint32_t *win, const std::vector<uint64_t> &p, uint32_t *out) {
+  std::vector<uint32_t> y(static_cast<size_t>(kDeg + kN + 1));
+  std::memcpy(y.data(), win, sizeof(uint32_t) * kN);
+  for (size_t k = 0; k + kN < y.size(); ++k) y[k + kN] = twist(y[k], y[k + 1], y[k + kM]);
+  uint32_t acc[kN] = {};
+  for (int64_t i = 0; i < kDeg; ++i) {
+    if (!getbit(p, i)) continue;
+    const uint32_t *src = y.data() + i;
+    for (int w = 0; w < kN; ++w) acc[w] ^= src[w];
+  }
+  std::memcpy(out, acc, sizeof(acc));
+}
+
+}  // namespace rs
+
+// numpy / CPython state after `steps` more outputs: (key, pos) of the block holding the next
+// word.  The jumped window starts one word early so that key[0] comes out whole.
+extern "C" int rs_mt_jump(const uint32_t *key, int32_t pos, int64_t steps, uint32_t *key_out,
+                          int32_t *pos_out) {
+  if (!key || !key_out || !pos_out) return rs::fail(RS_EINVAL, "rs_mt_jump: null pointer");
+  if (pos < 0 || pos > kN || steps < 0) return rs::fail(RS_EINVAL, "rs_mt_jump: bad state");
+  if (steps == 0) {
+    std::memmove(key_out, key, sizeof(uint32_t) * kN);
+    *pos_out = pos;
+    return RS_OK;
+  }
+  // absolute index of the last word drawn: W - 1 with W = pos + steps; its block b
+  const int64_t W = static_cast<int64_t>(pos) + steps;
+  const int64_t b = (W - 1) / kN;
+  if (b == 0) {
+    std::memmove(key_out, key, sizeof(uint32_t) * kN);
+    *pos_out = static_cast<int32_t>(W);
+    return RS_OK;
+  }
+  // window at index 624 b - 1: its words 1..623 plus one generated word are block b
+  std::vector<uint64_t> p;
+  rs::mt_jump_poly(static_cast<uint64_t>(kN * b - 1), p);
+  uint32_t win[kN];
+  rs::mt_apply_poly(key, p, win);
+  uint32_t blk[kN];
+  std::memcpy(blk, win + 1, sizeof(uint32_t) * (kN - 1));
+  blk[kN - 1] = twist(win[0], win[1], win[kM]);  // y_{624}: window words 0, 1, 397
+  std::memcpy(key_out, blk, sizeof(blk));
+  *pos_out = static_cast<int32_t>(W - kN * b);
+  return RS_OK;
+}

@@ -64,6 +64,7 @@ _SIGS = {
     "rs_np_choice_tuples": (C.c_int, [_u32p, _i32p, C.c_int64, C.c_int32, C.c_int64, _i32p]),
     "rs_py_seed": (C.c_int, [_u32p, C.c_int32, _u32p, _i32p]),
     "rs_py_shuffle_tuples": (C.c_int, [_u32p, _i32p, C.c_int64, C.c_int32, C.c_int64, _i32p]),
+    "rs_mt_jump": (C.c_int, [_u32p, C.c_int32, C.c_int64, _u32p, _i32p]),
     "rs_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "rs_ctx_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
     "rs_ctx_destroy": (C.c_int, [C.c_void_p]),
@@ -236,6 +237,18 @@ def py_shuffle_tuples(key, pos, n, k, count):
     check(lib().rs_py_shuffle_tuples(ptr(key, C.c_uint32), C.byref(p), int(n), int(k),
                                      int(count), ptr(out, C.c_int32)))
     return out, key, p.value
+
+
+def mt_jump(key, pos, steps):
+    """MT19937 (key, pos) after ``steps`` more 32-bit outputs (jump-ahead, no generation)."""
+    key = np.ascontiguousarray(key, dtype=np.uint32)
+    if key.shape != (MT_N,):
+        raise ValueError("MT19937 key must have 624 words")
+    out = np.empty(MT_N, dtype=np.uint32)
+    p = C.c_int32(0)
+    check(lib().rs_mt_jump(ptr(key, C.c_uint32), int(pos), int(steps), ptr(out, C.c_uint32),
+                           C.byref(p)))
+    return out, p.value
 
 
 def np_seed(seed):
