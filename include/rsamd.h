@@ -68,7 +68,7 @@ int rs_mt_jump(const uint32_t *mt_key, int32_t mt_pos, int64_t steps, uint32_t *
                int32_t *pos_out);
 
 /* ------------------------------------------------------------------------------------------
- * Context
+ * Context: one per host thread; owns the device buffers, stream and RCCL communicator
  * ---------------------------------------------------------------------------------------- */
 typedef struct rs_ctx rs_ctx;
 

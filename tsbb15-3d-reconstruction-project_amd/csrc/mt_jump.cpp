@@ -171,6 +171,9 @@ void mt_jump_poly(uint64_t J, std::vector<uint64_t> &out) {
   out = r;
 }
 
+// p = p^2 mod phi (x^J -> x^(2J))
+void mt_poly_square(std::vector<uint64_t> &p) { square_mod(p, charpoly()); }
+
 // Window (y_0..y_623) advanced by the polynomial p: out[w] = XOR_{i: p_i} y_{i+w}.
 void mt_apply_poly(const uint32_t *win, const std::vector<uint64_t> &p, uint32_t *out) {
   std::vector<uint32_t> y(static_cast<size_t>(kDeg + kN + 1));
