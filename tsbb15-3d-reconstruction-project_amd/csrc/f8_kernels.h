@@ -95,6 +95,7 @@ hipError_t launch_f8_count32x(const float4 *pts32, const Pt *pts, int n, int H,
                               int *status = nullptr, const float4 *G4 = nullptr);
 // Point-pair packed fp32 counting (DEC 3 decisions, bit-identical to launch_f8_count32x<GuardW>);
 // ptsq in the k_pack_points32q layout.
+hipError_t set_count_timeline(uint64_t *buf);  // RSAMD_TSTAMP diagnostics (null: off)
 hipError_t launch_pack_points32q(const Pt *pts, int n, const Frame &fr, float4 *ptsq,
                                  hipStream_t s);
 hipError_t launch_f8_count32q(const float4 *ptsq, const Pt *pts, int n, int H,

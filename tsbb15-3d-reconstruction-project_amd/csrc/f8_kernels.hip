@@ -668,6 +668,10 @@ __device__ __forceinline__ void pair_terms(f2q P01, f2q P23, f2q P45, f2q P67, f
   RSD_PKMUL_VB(S, m, ALB, "[0,1]", "[1,1]");  // beta m
 }
 
+// Wave timeline of the "q" counting kernel (start / end of each wave, 100 MHz real-time
+// counter): set by the plan only under RSAMD_TSTAMP, for the launch-overhead analysis.
+__device__ uint64_t *g_count_ts = nullptr;
+
 template <bool ASM, int BT>
 __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ ptsq,
                                                      const Pt *__restrict__ pts, int n, int H,
@@ -691,6 +695,8 @@ __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ p
   const int64_t total = static_cast<int64_t>((H + 63) >> 6) * npad;
   int64_t pos = w * per_wave;
   const int64_t end = min(total, pos + per_wave);
+  uint64_t *ts = g_count_ts;  // diagnostic wave timeline (RSAMD_TSTAMP), null in production
+  const uint64_t t_start = ts ? __builtin_amdgcn_s_memrealtime() : 0ull;
   while (pos < end) {
     const int grp = static_cast<int>(pos / npad);
     const int p0 = static_cast<int>(pos - grp * npad);
@@ -741,6 +747,10 @@ __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ p
     }
     if (h < H) atomicAdd(&counts[h], cnt);
     if (gdone) group_done_max(counts, gdone, status, grp, p1 - p0, static_cast<int>(npad), h, H);
+  }
+  if (ts && lane == 0) {
+    ts[2 * w] = t_start;
+    ts[2 * w + 1] = __builtin_amdgcn_s_memrealtime();
   }
 }
 
@@ -1369,6 +1379,10 @@ hipError_t launch_pack_points32(const Pt *pts, int n, const Frame &fr, float4 *p
   hipLaunchKernelGGL(k_pack_points32, dim3((n + 7 + 255) / 256), dim3(256), 0, s, pts, n, fr,
                      pts32);
   return hipGetLastError();
+}
+
+hipError_t set_count_timeline(uint64_t *buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_count_ts), &buf, sizeof(buf));
 }
 
 hipError_t launch_pack_points32q(const Pt *pts, int n, const Frame &fr, float4 *ptsq,

@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -198,6 +199,8 @@ struct rs_f8_plan {
   int chunk_override = 0;     // fp64 kernel point chunk (RSAMD_CHUNK)
   int tail_cus = 0;           // CUs for the tail + solve split (RSAMD_TAILCUS; 0: 256 tail blocks)
   int nospec = 0;             // RSAMD_NOSPEC=1: the replay always extracts S_RANSAC itself
+  uint64_t *d_ts = nullptr;   // RSAMD_TSTAMP=<file>: wave timeline of the counting kernel
+  const char *ts_path = nullptr;
   int nt_store = 0;           // RSAMD_NTSTORE: non-temporal solve output stores
   int solve_diag = 0;         // RSAMD_SOLVE_DIAG: timing-only solve variants (wrong models)
 
@@ -215,6 +218,10 @@ static void plan_free(rs_f8_plan *p) {
   (void)hipFree(p->d_pts);
   (void)hipFree(p->d_pts32);
   (void)hipFree(p->d_pts32q);
+  if (p->d_ts) {
+    (void)rsd::set_count_timeline(nullptr);
+    (void)hipFree(p->d_ts);
+  }
   for (RunBufs &b : p->buf) {
     (void)hipFree(b.d_F);
     (void)hipFree(b.d_F32);
@@ -325,6 +332,14 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
   p->solve_diag = env_int("RSAMD_SOLVE_DIAG", 0);
   p->nt_store = env_int("RSAMD_NTSTORE", 0);
   p->nospec = env_int("RSAMD_NOSPEC", 0) != 0;
+  p->ts_path = std::getenv("RSAMD_TSTAMP");
+  if (p->ts_path) {
+    const size_t tsb = sizeof(uint64_t) * 2 * (static_cast<size_t>(p->resident_waves) + 1024);
+    if (hipMalloc(&p->d_ts, tsb) == hipSuccess) {
+      (void)hipMemset(p->d_ts, 0, tsb);
+      (void)rsd::set_count_timeline(p->d_ts);
+    }
+  }
   p->q_block = env_int("RSAMD_QBLOCK", 256);
   p->q_xcd = env_int("RSAMD_XCD", 0) != 0;
   if (p->overlap) {
@@ -585,6 +600,16 @@ extern "C" int rs_f8_plan_result(rs_f8_plan *p, rs_f8_result *out, int64_t *inli
   out->max_count_fast = r->max_count_fast;
   out->n_candidates = r->n_candidates;
   out->guard_mismatch = r->guard_mismatch;
+  if (p->d_ts && p->ts_path) {  // diagnostics: append this run's wave timeline
+    std::vector<uint64_t> t(2 * (static_cast<size_t>(p->resident_waves) + 1024));
+    if (hipMemcpy(t.data(), p->d_ts, sizeof(uint64_t) * t.size(), hipMemcpyDeviceToHost) ==
+        hipSuccess) {
+      if (FILE *f = std::fopen(p->ts_path, "ab")) {
+        std::fwrite(t.data(), sizeof(uint64_t), t.size(), f);
+        std::fclose(f);
+      }
+    }
+  }
   if (n_inliers) *n_inliers = r->n_inliers;
   const int64_t k = std::min<int64_t>(cap, r->n_inliers);
   if (inliers && k > 0) {  // S_RANSAC stays in HBM until asked for
