@@ -3,7 +3,7 @@
 # Usage (through gpurun): bash tools/gpu_round.sh <tag> [steps]
 set -o pipefail
 TAG=${1:-r01}
-STEPS=${2:-20}
+STEPS=${2:-100}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
@@ -12,9 +12,9 @@ cd $R
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 echo "pytest_gpu exit $?" | tee -a $OUT/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo smoke failed; exit 1; }
-timeout -k 10 400 python bench.py --steps $STEPS --warmup 5 > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; exit 1; }
+timeout -k 10 400 python bench.py --steps $STEPS --warmup 200 > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; exit 1; }
 cat $OUT/bench.json
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 bench.py --steps $STEPS --warmup 5 --no-cpu-baseline --no-parity-mode --no-extras > $OUT/prof_bench.log 2>&1 || { echo rocprof failed; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 bench.py --steps $STEPS --warmup 200 --no-cpu-baseline --no-parity-mode --no-extras > $OUT/prof_bench.log 2>&1 || { echo rocprof failed; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o pmc -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-parity-mode --no-extras > $OUT/pmc_fetch.log 2>&1 || { echo pmc fetch failed; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o pmc -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-parity-mode --no-extras > $OUT/pmc_write.log 2>&1 || { echo pmc write failed; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $OUT/pmc_sq -o pmc -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-parity-mode --no-extras > $OUT/pmc_sq.log 2>&1 || echo "pmc sq failed"
