@@ -77,6 +77,14 @@ int rs_ctx_create(int device, rs_ctx **out);
 int rs_ctx_destroy(rs_ctx *ctx);
 int rs_ctx_synchronize(rs_ctx *ctx);
 
+/* The same stream as rs_np_choice_tuples (k <= 8, n - 1 <= 10240), computed on the GPU of
+ * `ctx`: MT19937 jump-ahead windows, the word stream in HBM, a chunked parse from every entry
+ * state (hypothesis boundaries), then one lane per hypothesis for its k indices.  Same output
+ * and (key, pos) advance, bit for bit; out is host memory (count, k) int32.
+ * Replaces the serial host replay behind fun.py:305-306 in parity mode. */
+int rs_np_choice_tuples_gpu(rs_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int64_t n, int32_t k,
+                            int64_t count, int32_t *out);
+
 /* ------------------------------------------------------------------------------------------
  * lab3 primitives on the GPU
  * ---------------------------------------------------------------------------------------- */

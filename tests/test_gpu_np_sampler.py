@@ -1,0 +1,94 @@
+"""GPU parity stream (rs_np_choice_tuples_gpu) against the host replay of numpy's legacy
+MT19937 choice (rs_np_choice_tuples, itself pinned to numpy and to the reference goldens in
+tests/test_samplers.py).  The bar is bit-exact: every tuple and the advanced (key, pos)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import PKG_DIR, REPO, golden
+from tsbb15_amd import _ffi
+
+pytestmark = pytest.mark.gpu
+
+
+def _state(seed, skip=0):
+    rs = np.random.RandomState(seed)
+    if skip:
+        rs.random_sample(skip)
+    st = rs.get_state()
+    return np.asarray(st[1], np.uint32), int(st[2])
+
+
+def _same(n, k, count, seed, skip=0):
+    key, pos = _state(seed, skip)
+    ref, rkey, rpos = _ffi.np_choice_tuples(key, pos, n, k, count)
+    got, gkey, gpos = _ffi.np_choice_tuples_gpu(key, pos, n, k, count)
+    bad = np.flatnonzero((got != ref).any(axis=1))
+    assert bad.size == 0, f"first mismatching hypothesis {bad[:5]}"
+    assert gpos == rpos and np.array_equal(gkey, rkey)
+
+
+@pytest.mark.parametrize("n,count", [(8, 20000), (9, 5000), (37, 3000), (65, 2000), (66, 2000),
+                                     (257, 1000), (2000, 3000), (4097, 300), (10000, 200)])
+def test_gpu_stream_matches_host_replay(ctx, n, count):
+    _same(n, 8, count, seed=n)
+
+
+def test_gpu_stream_midstream_state_and_other_k(ctx):
+    _same(300, 5, 400, seed=3, skip=1001)
+    _same(2000, 8, 50, seed=4, skip=623)
+    _same(50, 1, 1000, seed=5, skip=624)
+
+
+def test_gpu_stream_c2_size(ctx):
+    """Config C2's 1e5 hypotheses at N = 2000 (~2.8e8 words, one segment)."""
+    _same(2000, 8, 100000, seed=11)
+
+
+def test_gpu_stream_reference_goldens(ctx):
+    z = golden("synth_c2.npz")
+    tup, key, pos = _ffi.np_choice_tuples_gpu(z["mt_key_in"], z["mt_pos_in"], 2000, 8,
+                                              len(z["tuples"]))
+    assert np.array_equal(tup, z["tuples"].astype(np.int32))
+    assert np.array_equal(key, z["mt_key_out"]) and pos == int(z["mt_pos_out"])
+    c1 = golden("dino_c1.npz")
+    for tag in ("clean", "noisy"):
+        n = c1[f"{tag}_p1"].shape[1]
+        tup, key, pos = _ffi.np_choice_tuples_gpu(c1[f"{tag}_mt_key_in"],
+                                                  c1[f"{tag}_mt_pos_in"], n, 8, 1000)
+        assert np.array_equal(tup, c1[f"{tag}_tuples"])
+        assert np.array_equal(key, c1[f"{tag}_mt_key_out"])
+        assert pos == int(c1[f"{tag}_mt_pos_out"])
+
+
+def test_gpu_stream_errors(ctx):
+    key, pos = _state(0)
+    with pytest.raises(ValueError, match="larger sample"):
+        _ffi.np_choice_tuples_gpu(key, pos, 7, 8, 1)
+    with pytest.raises(ValueError, match="too large"):
+        _ffi.np_choice_tuples_gpu(key, pos, 20000, 8, 1)
+
+
+_SEG_CHILD = """
+import numpy as np
+from tsbb15_amd import _ffi
+for n, count in ((2000, 2000), (37, 40000)):
+    st = np.random.RandomState(21).get_state()
+    key, pos = np.asarray(st[1], np.uint32), int(st[2])
+    ref = _ffi.np_choice_tuples(key, pos, n, 8, count)
+    got = _ffi.np_choice_tuples_gpu(key, pos, n, 8, count)
+    assert np.array_equal(got[0], ref[0]) and got[2] == ref[2] and np.array_equal(got[1], ref[1])
+print("ok")
+"""
+
+
+def test_gpu_stream_many_segments():
+    """Segments of 2^20 words (the segment size is read once per process, so in a child)."""
+    env = dict(os.environ, RSAMD_NP_SEGWORDS=str(1 << 20),
+               PYTHONPATH=os.pathsep.join([PKG_DIR, REPO, os.environ.get("PYTHONPATH", "")]))
+    r = subprocess.run([sys.executable, "-c", _SEG_CHILD], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]

@@ -5,12 +5,15 @@
 
 #include "rsamd.h"
 
+struct rs_np_work;  // np_sampler.hip: parity-stream workspace
+
 struct rs_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   void *scratch = nullptr;     // grow-only device scratch for single-shot ops
   size_t scratch_bytes = 0;
   rs_f8_plan *np_plan = nullptr;  // cached plan of rs_f8_ransac_np
+  rs_np_work *np_work = nullptr;  // GPU parity-stream buffers (grow-only)
   void *comm = nullptr;        // ncclComm_t
   void *comm_buf = nullptr;    // device staging for collectives
   size_t comm_buf_bytes = 0;
@@ -19,5 +22,8 @@ struct rs_ctx {
 namespace rs {
 int hip_fail(hipError_t e, const char *what);
 int ensure_scratch(rs_ctx *c, size_t bytes);
+void np_work_free(rs_ctx *c);
+int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t k,
+                     int64_t count, int32_t *d_out);
 int fmatrix_stls_lsq(rs_ctx *c, const double *pl, const double *pr, int64_t n, double *F_out);
 }  // namespace rs

@@ -1,0 +1,710 @@
+// numpy-exact parity stream on the GPU: the tuples of rs_np_choice_tuples (fun.py:305-306,
+// np.random.choice(N, 8, replace=False) = permutation(N)[:8]) without the serial host replay.
+//
+// One hypothesis is a Fisher-Yates sweep i = N-1 .. 1 whose step i draws u32 words until
+// (w & mask(i)) <= i (numpy's random_interval).  Where hypotheses start in the word stream is
+// a serial property of the stream; the rest is parallel.  Pipeline per segment of hypotheses:
+//
+//   1. k_mt_jump    MT19937 windows 2^k J words apart by x^(2^k J) mod phi (a doubling tree;
+//                   the polynomials come from mt_jump.cpp, once per process);
+//   2. k_mt_stream  one wave per window: the tempered word stream, materialised in HBM;
+//   3. k_np_entry   per chunk of kW draws, the parse from EVERY entry state at once: parser
+//                   states are i in 1..N-1, trajectories that meet merge, and they stay in
+//                   cyclic order, so a sorted list with member ranges (lo) describes the map
+//                   entry -> exit state.  Every wrap (hypothesis end) of every trajectory is
+//                   logged with the member range it belongs to;
+//   4. host         compose the per-chunk maps (C lookups) -> the true entry state per chunk;
+//   5. k_np_filter  keep the logged wraps whose member range holds the true entry: these are
+//                   exactly the hypothesis starts; k_np_starts gathers them in order;
+//   6. k_np_tuples  one lane per hypothesis: re-parse its own words, keep the swap partners
+//                   j_i, trace positions 0..k-1 back through the swaps -> the k indices.
+//
+// The final (key, pos) state is the stream block holding the next word, untempered on the
+// host.  Exactness does not depend on any tuning constant; tests compare against the host
+// replay (tests/test_gpu_np_sampler.py).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "common.h"
+#include "ctx.h"
+
+namespace rs {
+int hip_fail(hipError_t e, const char *what);
+void mt_jump_poly(uint64_t J, std::vector<uint64_t> &out);
+void mt_poly_square(std::vector<uint64_t> &p);
+}  // namespace rs
+
+#define HIP_TRY(expr)                                     \
+  do {                                                    \
+    hipError_t e_ = (expr);                               \
+    if (e_ != hipSuccess) return rs::hip_fail(e_, #expr); \
+  } while (0)
+
+namespace {
+
+constexpr int kN = 624;
+constexpr int kM = 397;
+constexpr uint32_t kUpper = 0x80000000u;
+constexpr uint32_t kLower = 0x7fffffffu;
+constexpr uint32_t kMatA = 0x9908b0dfu;
+constexpr int kDeg = 19937;
+constexpr int kPrefix = kDeg + kN - 1;       // words of a window's sequence a jump reads
+constexpr int kJB = 1024;                    // stream blocks per generator
+constexpr int64_t kJ = int64_t(kN) * kJB;    // words per generator
+constexpr int kLevels = 11;                  // jump tree depth: up to 2048 generators
+constexpr int64_t kSegWords = int64_t(1) << 29;  // stream words per segment (2 GiB)
+constexpr int kW = 262144;                   // draws per parse chunk
+constexpr int kEntryThreads = 512;
+constexpr int kR = 20;                       // slots per thread: N - 1 <= 10240
+constexpr int kMaxN1 = kEntryThreads * kR;
+constexpr int kK = 64;                       // draws between compactions (<= N - 1 when dense)
+constexpr uint32_t kSentinel = 0x80000000u;  // an empty slot: never reaches 0 within kW steps
+
+__device__ __forceinline__ uint32_t twist(uint32_t a, uint32_t b) {
+  const uint32_t y = (a & kUpper) | (b & kLower);
+  return (y >> 1) ^ ((0u - (y & 1u)) & kMatA);
+}
+__device__ __forceinline__ uint32_t temper(uint32_t y) {
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+// numpy random_interval(i): the draw is w & mask(i), mask = smallest 2^b - 1 >= i (i >= 1)
+__device__ __forceinline__ uint32_t masked(uint32_t w, uint32_t i) {
+  return w & (0xffffffffu >> __builtin_clz(i));
+}
+
+// ---- 1. jump tree level: window[g + half] = x^(half J) applied to window[g] ----------------
+// y_t = y_{t-227} ^ twist(y_{t-624}, y_{t-623}); word w of the jumped window is the XOR of
+// y_{i+w} over the set bits i of the polynomial.  Only the top bit of word 0 is MT state, so
+// word 0 of a jumped window may carry wrong low bits: it is never emitted (k_mt_stream) and
+// the recurrence reads only its top bit.
+__global__ __launch_bounds__(256) void k_mt_jump(uint32_t *__restrict__ win, int half, int G,
+                                                 const int32_t *__restrict__ bits, int nbits) {
+  __shared__ uint32_t y[kPrefix];
+  const int g = blockIdx.x, dst = g + half;
+  if (dst >= G) return;
+  const int tid = threadIdx.x;
+  for (int t = tid; t < kN; t += 256) y[t] = win[static_cast<size_t>(g) * kN + t];
+  __syncthreads();
+  for (int t0 = kN; t0 < kPrefix; t0 += 227) {
+    const int t = t0 + tid;
+    if (tid < 227 && t < kPrefix) y[t] = y[t - 227] ^ twist(y[t - kN], y[t - kN + 1]);
+    __syncthreads();
+  }
+  const int w0 = tid, w1 = tid + 256, w2 = tid + 512 < kN ? tid + 512 : kN - 1;
+  uint32_t a0 = 0, a1 = 0, a2 = 0;
+  for (int b = 0; b < nbits; ++b) {
+    const int i = bits[b];
+    a0 ^= y[i + w0];
+    a1 ^= y[i + w1];
+    a2 ^= y[i + w2];
+  }
+  uint32_t *out = win + static_cast<size_t>(dst) * kN;
+  out[w0] = a0;
+  out[w1] = a1;
+  if (tid + 512 < kN) out[w2] = a2;
+}
+
+// ---- 2. stream: generator g owns blocks (g kJB, (g+1) kJB] plus words 1..623 of its window --
+__global__ __launch_bounds__(64) void k_mt_stream(const uint32_t *__restrict__ win,
+                                                  uint32_t *__restrict__ stream, int64_t Lb) {
+  __shared__ uint32_t ob[kN], nb[kN];
+  const int g = blockIdx.x, l = threadIdx.x;
+  const int64_t b0 = static_cast<int64_t>(g) * kJB;
+  for (int t = l; t < kN; t += 64) {
+    const uint32_t v = win[static_cast<size_t>(g) * kN + t];
+    ob[t] = v;
+    if (t > 0 || g == 0) stream[b0 * kN + t] = temper(v);
+  }
+  __syncthreads();
+  const int64_t bend = std::min<int64_t>(b0 + kJB, Lb - 1);
+  for (int64_t b = b0 + 1; b <= bend; ++b) {
+    for (int t = l; t < 227; t += 64) nb[t] = ob[t + kM] ^ twist(ob[t], ob[t + 1]);
+    __syncthreads();
+    for (int t = 227 + l; t < 454; t += 64) nb[t] = nb[t - 227] ^ twist(ob[t], ob[t + 1]);
+    __syncthreads();
+    for (int t = 454 + l; t < kN; t += 64)
+      nb[t] = nb[t - 227] ^ twist(ob[t], t + 1 < kN ? ob[t + 1] : nb[0]);
+    __syncthreads();
+    uint32_t *o = stream + b * kN;
+    for (int t = l; t < kN; t += 64) {
+      const uint32_t v = nb[t];
+      o[t] = temper(v);
+      ob[t] = v;
+    }
+    __syncthreads();
+  }
+}
+
+// ---- 3. all-entry parse of one chunk ---------------------------------------------------------
+struct EntryArgs {
+  const uint32_t *draws;  // draw 0 of the segment
+  int64_t D;              // draws in the segment
+  int n1;                 // N - 1: parser states 1..n1, entry list index a <-> state n1 - a
+  uint32_t *fin;          // [C][n1] final list: lo | state << 16
+  int *fin_m;             // [C]
+  uint2 *ev;              // [C][ecap] wraps: (draw after the wrap, lo | hi << 16)
+  int *ev_n;              // [C]
+  int ecap;
+  int *err;
+};
+
+__device__ __forceinline__ int block_excl_scan(int v, int *sh, int *total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sh[wid] = x;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kEntryThreads / 64; ++w) {
+    const int s = sh[w];
+    base += w < wid ? s : 0;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + x - v;
+}
+
+__device__ __forceinline__ uint32_t lane_rank(uint64_t bits) {
+  return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(bits >> 32),
+                                   __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bits), 0u));
+}
+
+__global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a) {
+  extern __shared__ uint16_t dyn[];
+  __shared__ uint32_t wbuf[kK];
+  __shared__ int sh_red[kEntryThreads / 64];
+  __shared__ int sh_head, sh_evn;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int n1 = a.n1, n1p = (n1 + 1) & ~1;
+  uint16_t *st = dyn, *lo = dyn + n1p, *st2 = dyn + 2 * n1p, *lo2 = dyn + 3 * n1p;
+  const int c = blockIdx.x;
+  const int64_t t0 = static_cast<int64_t>(c) * kW;
+  const int T = static_cast<int>(std::min<int64_t>(kW, a.D - t0));
+  const uint32_t *wp = a.draws + t0;
+  uint2 *ev = a.ev + static_cast<size_t>(c) * a.ecap;
+  const uint32_t N1 = static_cast<uint32_t>(n1);
+  for (int q = tid; q < n1; q += kEntryThreads) {
+    st[q] = static_cast<uint16_t>(n1 - q);
+    lo[q] = static_cast<uint16_t>(q);
+  }
+  if (tid == 0) sh_evn = 0;
+  __syncthreads();
+  int m = n1, t = 0;
+  if (m > 64) {
+    // dense phase: the whole workgroup, slots q = tid + r * kEntryThreads
+    uint32_t s[kR];
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const int q = tid + r * kEntryThreads;
+      s[r] = q < m ? st[q] : kSentinel;
+    }
+    while (m > 64 && t < T) {
+      const int kk = min(kK, T - t);
+      if (tid < kk) wbuf[tid] = wp[t + tid];
+      __syncthreads();
+      const int nr = (m + kEntryThreads - 1) / kEntryThreads;
+      for (int k = 0; k < kk; ++k) {
+        const uint32_t w = wbuf[k];
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+          if (r >= nr) break;
+          uint32_t sv = s[r];
+          sv -= masked(w, sv) <= sv ? 1u : 0u;
+          if (sv == 0) {  // hypothesis end: log the wrap with this trajectory's member range
+            sv = N1;
+            const int q = tid + r * kEntryThreads;
+            const int e = atomicAdd(&sh_evn, 1);
+            if (e < a.ecap)
+              ev[e] = make_uint2(static_cast<uint32_t>(t + k + 1),
+                                 lo[q] | (static_cast<uint32_t>(lo[q + 1 == m ? 0 : q + 1]) << 16));
+          }
+          s[r] = sv;
+        }
+      }
+      t += kk;
+      // compaction: list order starts at the head (first slot of the maximum run); equal
+      // neighbours merge, the first keeps its lo
+      __syncthreads();
+      int lmax = 0;
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        if (r >= nr) break;
+        const int q = tid + r * kEntryThreads;
+        if (q < m) {
+          st[q] = static_cast<uint16_t>(s[r]);
+          lmax = max(lmax, static_cast<int>(s[r]));
+        }
+      }
+#pragma unroll
+      for (int o = 32; o; o >>= 1) lmax = max(lmax, __shfl_xor(lmax, o));
+      if (lane == 0) sh_red[wid] = lmax;
+      if (tid == 0) sh_head = 0;
+      __syncthreads();
+      int mx = 0;
+#pragma unroll
+      for (int w = 0; w < kEntryThreads / 64; ++w) mx = max(mx, sh_red[w]);
+      for (int q = tid; q < m; q += kEntryThreads) {
+        const int pq = q == 0 ? m - 1 : q - 1;
+        if (st[q] == mx && st[pq] != mx) sh_head = q;
+      }
+      __syncthreads();
+      const int h = sh_head;
+      const int per = (m + kEntryThreads - 1) / kEntryThreads;
+      const int k0 = min(m, tid * per), k1 = min(m, k0 + per);
+      int cnt = 0;
+      for (int k = k0; k < k1; ++k) {
+        const int p = h + k < m ? h + k : h + k - m;
+        const int pp = p == 0 ? m - 1 : p - 1;
+        cnt += (k == 0 || st[p] != st[pp]) ? 1 : 0;
+      }
+      int total;
+      int o = block_excl_scan(cnt, sh_red, &total);
+      for (int k = k0; k < k1; ++k) {
+        const int p = h + k < m ? h + k : h + k - m;
+        const int pp = p == 0 ? m - 1 : p - 1;
+        if (k == 0 || st[p] != st[pp]) {
+          st2[o] = st[p];
+          lo2[o] = lo[p];
+          ++o;
+        }
+      }
+      __syncthreads();
+      uint16_t *x = st;
+      st = st2;
+      st2 = x;
+      x = lo;
+      lo = lo2;
+      lo2 = x;
+      m = total;
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        const int q = tid + r * kEntryThreads;
+        s[r] = q < m ? st[q] : kSentinel;
+      }
+    }
+    if (m > 64) {  // chunk done while still dense
+      for (int q = tid; q < m; q += kEntryThreads)
+        a.fin[static_cast<size_t>(c) * n1 + q] = lo[q] | (static_cast<uint32_t>(st[q]) << 16);
+      if (tid == 0) {
+        a.fin_m[c] = m;
+        a.ev_n[c] = min(sh_evn, a.ecap);
+        if (sh_evn > a.ecap) atomicOr(a.err, 1);
+      }
+      return;
+    }
+  }
+  // sparse phase: one wave, lane l = slot l
+  if (tid >= 64) return;
+  const int l = lane;
+  uint32_t sv = l < m ? st[l] : kSentinel;
+  uint32_t lov = l < m ? lo[l] : 0u;
+  int ecnt = sh_evn;
+  while (t < T) {
+    const int kk = min(64, T - t);
+    const uint32_t wv = l < kk ? wp[t + l] : 0u;
+    for (int k = 0; k < kk; ++k) {
+      const uint32_t w = __builtin_amdgcn_readlane(wv, k);
+      sv -= masked(w, sv) <= sv ? 1u : 0u;
+      const uint64_t wr = __ballot(sv == 0);
+      if (wr) {
+        const uint32_t succ = __shfl(lov, l + 1 == m ? 0 : l + 1);
+        if (sv == 0) {
+          sv = N1;
+          const int e = ecnt + static_cast<int>(lane_rank(wr));
+          if (e < a.ecap) ev[e] = make_uint2(static_cast<uint32_t>(t + k + 1), lov | (succ << 16));
+        }
+        ecnt += __popcll(wr);
+      }
+    }
+    t += kk;
+    // wave compaction
+    const bool valid = l < m;
+    uint32_t mx = valid ? sv : 0u;
+#pragma unroll
+    for (int o = 32; o; o >>= 1) mx = max(mx, static_cast<uint32_t>(__shfl_xor(static_cast<int>(mx), o)));
+    const uint32_t psv = __shfl(sv, l == 0 ? m - 1 : l - 1);
+    const uint64_t hb = __ballot(valid && sv == mx && psv != mx);
+    const int h = hb ? __ffsll(static_cast<long long>(hb)) - 1 : 0;
+    const bool keep = valid && (l == h || sv != psv);
+    const uint64_t kb = __ballot(keep);
+    const uint64_t lmask = (1ull << l) - 1ull;
+    const uint64_t hmask = h == 0 ? 0ull : ((1ull << h) - 1ull);
+    const uint64_t mmask = m >= 64 ? ~0ull : ((1ull << m) - 1ull);
+    const uint64_t before = l >= h ? (lmask & ~hmask) : ((mmask & ~hmask) | lmask);
+    const int m2 = __popcll(kb);
+    const int dest = keep ? __popcll(kb & before) : m2 + __popcll(~kb & lmask);
+    sv = static_cast<uint32_t>(__builtin_amdgcn_ds_permute(dest * 4, static_cast<int>(sv)));
+    lov = static_cast<uint32_t>(__builtin_amdgcn_ds_permute(dest * 4, static_cast<int>(lov)));
+    m = m2;
+    if (l >= m) sv = kSentinel;
+  }
+  if (l < m) a.fin[static_cast<size_t>(c) * n1 + l] = lov | (sv << 16);
+  if (l == 0) {
+    a.fin_m[c] = m;
+    a.ev_n[c] = min(ecnt, a.ecap);
+    if (ecnt > a.ecap) atomicOr(a.err, 1);
+  }
+}
+
+// ---- 5. keep the wraps of the true trajectory (in place, order preserved) -----------------
+__global__ __launch_bounds__(64) void k_np_filter(uint2 *__restrict__ ev, const int *ev_n,
+                                                  const int *ent, int *vcnt, int ecap) {
+  const int c = blockIdx.x, l = threadIdx.x;
+  const uint32_t a = static_cast<uint32_t>(ent[c]);
+  const int n = ev_n[c];
+  uint2 *e = ev + static_cast<size_t>(c) * ecap;
+  int cnt = 0;
+  for (int b = 0; b < n; b += 64) {
+    const int i = b + l;
+    bool ok = false;
+    uint32_t tv = 0;
+    if (i < n) {
+      const uint2 x = e[i];
+      tv = x.x;
+      const uint32_t lo = x.y & 0xffffu, hi = x.y >> 16;
+      ok = lo < hi ? (a >= lo && a < hi) : (a >= lo || a < hi);
+    }
+    const uint64_t bl = __ballot(ok);
+    if (ok) e[cnt + static_cast<int>(lane_rank(bl))].x = tv;
+    cnt += __popcll(bl);
+  }
+  if (l == 0) vcnt[c] = cnt;
+}
+
+__global__ __launch_bounds__(256) void k_np_starts(const uint2 *__restrict__ ev,
+                                                   const int *vcnt, const int *off,
+                                                   int64_t *__restrict__ starts, int64_t H,
+                                                   int ecap) {
+  const int c = blockIdx.x;
+  const int n = vcnt[c];
+  const int64_t base = 1 + off[c];
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const int64_t idx = base + i;
+    if (idx <= H)
+      starts[idx] = static_cast<int64_t>(c) * kW + ev[static_cast<size_t>(c) * ecap + i].x;
+  }
+  if (c == 0 && threadIdx.x == 0) starts[0] = 0;
+}
+
+// ---- 6. one lane per hypothesis: swap partners, then positions 0..k-1 traced back -----------
+__global__ __launch_bounds__(256) void k_np_tuples(const uint32_t *__restrict__ draws,
+                                                   const int64_t *__restrict__ starts,
+                                                   int64_t H, int n1, int kk,
+                                                   uint16_t *__restrict__ jb,
+                                                   int32_t *__restrict__ out, int *err) {
+  const int64_t h = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (h >= H) return;
+  const int64_t a = starts[h], b = starts[h + 1];
+  uint16_t *J = jb + h * n1;
+  uint32_t i = static_cast<uint32_t>(n1);
+  int64_t d = a;
+  for (; d < b && i > 0; ++d) {
+    const uint32_t v = masked(draws[d], i);
+    if (v <= i) {
+      J[i - 1] = static_cast<uint16_t>(v);
+      --i;
+    }
+  }
+  if (i != 0 || d != b) {
+    atomicOr(err, 2);
+    return;
+  }
+  // x_final[p] = x_init[tau_{N-1}(... tau_1(p))], tau_i = (i j_i), x_init = arange
+  uint32_t p[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) p[k] = static_cast<uint32_t>(k);
+  for (uint32_t s = 1; s <= static_cast<uint32_t>(n1); ++s) {
+    const uint32_t j = J[s - 1];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) p[k] = p[k] == s ? j : (p[k] == j ? s : p[k]);
+  }
+  for (int k = 0; k < kk; ++k) out[h * kk + k] = static_cast<int32_t>(p[k]);
+}
+
+// ---- host ------------------------------------------------------------------------------------
+struct JumpPolys {
+  std::vector<std::vector<int32_t>> bits;  // level k: set bits of x^(2^k kJ) mod phi
+};
+
+const JumpPolys &jump_polys() {
+  static JumpPolys jp;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    std::vector<uint64_t> p;
+    rs::mt_jump_poly(static_cast<uint64_t>(kJ), p);
+    for (int k = 0; k < kLevels; ++k) {
+      if (k) rs::mt_poly_square(p);
+      std::vector<int32_t> b;
+      for (int i = 0; i < kDeg; ++i)
+        if ((p[static_cast<size_t>(i) >> 6] >> (i & 63)) & 1u) b.push_back(i);
+      jp.bits.push_back(std::move(b));
+    }
+  });
+  return jp;
+}
+
+uint32_t untemper(uint32_t z) {
+  uint32_t y = z ^ (z >> 18);
+  y ^= (y << 15) & 0xefc60000u;
+  uint32_t x = y;
+  for (int r = 0; r < 5; ++r) x = y ^ ((x << 7) & 0x9d2c5680u);
+  uint32_t u = x;
+  for (int r = 0; r < 3; ++r) u = x ^ (u >> 11);
+  return u;
+}
+
+// expected draws per hypothesis: sum over i of (mask(i) + 1) / (i + 1)
+// stream words per segment: kSegWords, or RSAMD_NP_SEGWORDS (tests of the multi-segment path)
+int64_t seg_words() {
+  static const int64_t v = [] {
+    const char *e = std::getenv("RSAMD_NP_SEGWORDS");
+    const int64_t x = e ? std::atoll(e) : 0;
+    return x > 0 ? std::max<int64_t>(int64_t(1) << 16, std::min(x, kSegWords)) : kSegWords;
+  }();
+  return v;
+}
+
+double expected_draws(int64_t n1) {
+  double e = 0.0;
+  for (int64_t i = 1; i <= n1; ++i) {
+    uint64_t m = static_cast<uint64_t>(i);
+    m |= m >> 1;
+    m |= m >> 2;
+    m |= m >> 4;
+    m |= m >> 8;
+    m |= m >> 16;
+    e += static_cast<double>(m + 1) / static_cast<double>(i + 1);
+  }
+  return e;
+}
+
+}  // namespace
+
+struct rs_np_work {
+  int32_t *d_bits = nullptr;
+  std::vector<int> bit_off, bit_n;
+  uint32_t *d_win = nullptr, *d_stream = nullptr, *d_fin = nullptr;
+  int *d_fin_m = nullptr, *d_ev_n = nullptr, *d_ent = nullptr, *d_vcnt = nullptr,
+      *d_off = nullptr, *d_err = nullptr;
+  uint2 *d_ev = nullptr;
+  int64_t *d_starts = nullptr;
+  uint16_t *d_J = nullptr;
+  int64_t cap_fin = 0, cap_ev = 0, cap_starts = 0, cap_J = 0;
+  int64_t entry_lds = 0;
+};
+
+namespace rs {
+
+void np_work_free(rs_ctx *c) {
+  rs_np_work *w = c->np_work;
+  if (!w) return;
+  void *ptrs[] = {w->d_bits, w->d_win, w->d_stream, w->d_fin, w->d_fin_m, w->d_ev_n,
+                  w->d_ent,  w->d_vcnt, w->d_off,   w->d_err, w->d_ev,    w->d_starts, w->d_J};
+  for (void *p : ptrs)
+    if (p) (void)hipFree(p);
+  delete w;
+  c->np_work = nullptr;
+}
+
+template <class T>
+static int grow(T *&p, int64_t &cap, int64_t need) {
+  if (need <= cap) return RS_OK;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  if (hipMalloc(reinterpret_cast<void **>(&p), sizeof(T) * static_cast<size_t>(need)) != hipSuccess)
+    return fail(RS_ENOMEM, "np sampler: device allocation failed");
+  cap = need;
+  return RS_OK;
+}
+
+// The numpy stream's next `count` choice(n, k) tuples into device memory (count * k int32),
+// on the context stream; advances (key, pos).  Synchronous.
+int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t k,
+                     int64_t count, int32_t *d_out) {
+  if (k < 1 || k > 8) return fail(RS_EINVAL, "np sampler: k must be in 1..8");
+  if (k > n) return fail(RS_EINVAL, "Cannot take a larger sample than population when 'replace=False'");
+  if (n - 1 > kMaxN1) return fail(RS_EINVAL, "np sampler: population too large for the GPU parse");
+  if (*pos < 0 || *pos > kN) return fail(RS_EINVAL, "bad MT19937 position");
+  if (count == 0) return RS_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  if (!c->np_work) c->np_work = new rs_np_work();
+  rs_np_work &w = *c->np_work;
+  int st;
+  const int n1 = static_cast<int>(n - 1);
+  const int64_t Gmax = (kSegWords / kN + kJB - 1) / kJB + 1;
+  const int64_t Cmax = kSegWords / kW + 1;
+  if (!w.d_bits) {
+    const JumpPolys &jp = jump_polys();
+    std::vector<int32_t> all;
+    for (const auto &b : jp.bits) {
+      w.bit_off.push_back(static_cast<int>(all.size()));
+      w.bit_n.push_back(static_cast<int>(b.size()));
+      all.insert(all.end(), b.begin(), b.end());
+    }
+    int64_t cap = 0;
+    if ((st = grow(w.d_bits, cap, static_cast<int64_t>(all.size())))) return st;
+    HIP_TRY(hipMemcpy(w.d_bits, all.data(), sizeof(int32_t) * all.size(), hipMemcpyHostToDevice));
+    int64_t c1 = 0, c2 = 0, c3 = 0, c4 = 0, c5 = 0, c6 = 0, c7 = 0, c8 = 0;
+    if ((st = grow(w.d_win, c1, Gmax * kN)) || (st = grow(w.d_stream, c2, kSegWords)) ||
+        (st = grow(w.d_fin_m, c3, Cmax)) || (st = grow(w.d_ev_n, c4, Cmax)) ||
+        (st = grow(w.d_ent, c5, Cmax)) || (st = grow(w.d_vcnt, c6, Cmax)) ||
+        (st = grow(w.d_off, c7, Cmax)) || (st = grow(w.d_err, c8, 1)))
+      return st;
+  }
+  if ((st = grow(w.d_fin, w.cap_fin, Cmax * n1))) return st;
+  const double E = expected_draws(n1);
+  const int64_t dmax = seg_words() - 3 * kN;
+  const int64_t hcap = std::max<int64_t>(1, static_cast<int64_t>((dmax - 16 * n) / (E * 1.03)));
+  int ecap = static_cast<int>(std::min<int64_t>(kW + 2 * n1, static_cast<int64_t>(70.0 * kW / E) + 4 * n1 + 4096));
+  const int64_t lds = 8 * static_cast<int64_t>((n1 + 1) & ~1);
+  if (lds > w.entry_lds) {
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_np_entry),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+    w.entry_lds = lds;
+  }
+  std::vector<int> fin_m, ev_n, ent, vcnt, off;
+  std::vector<uint32_t> fin;
+  int64_t done = 0;
+  while (done < count) {
+    const int64_t hs = std::min<int64_t>(count - done, hcap);
+    const int64_t D = std::min<int64_t>(dmax, static_cast<int64_t>(std::ceil(hs * E * 1.03)) + 16 * n + 4096);
+    const int C = static_cast<int>((D + kW - 1) / kW);
+    const int64_t Lb = (*pos + D + kN - 1) / kN;
+    const int G = static_cast<int>((Lb + kJB - 1) / kJB);
+    if ((st = grow(w.d_ev, w.cap_ev, static_cast<int64_t>(C) * ecap)) ||
+        (st = grow(w.d_starts, w.cap_starts, hs + 1)) ||
+        (st = grow(w.d_J, w.cap_J, hs * n1)))
+      return st;
+    // 1-2: the word stream from (key, pos): block 0 is the key itself
+    HIP_TRY(hipMemcpyAsync(w.d_win, key, sizeof(uint32_t) * kN, hipMemcpyHostToDevice, s));
+    for (int half = 1, lv = 0; half < G; half *= 2, ++lv) {
+      if (lv >= kLevels) return fail(RS_EINVAL, "np sampler: segment too long");
+      k_mt_jump<<<half, 256, 0, s>>>(w.d_win, half, G, w.d_bits + w.bit_off[lv], w.bit_n[lv]);
+      HIP_TRY(hipGetLastError());
+    }
+    k_mt_stream<<<G, 64, 0, s>>>(w.d_win, w.d_stream, Lb);
+    HIP_TRY(hipGetLastError());
+    // 3: all-entry parse per chunk
+    HIP_TRY(hipMemsetAsync(w.d_err, 0, sizeof(int), s));
+    EntryArgs ea{w.d_stream + *pos, D, n1, w.d_fin, w.d_fin_m, w.d_ev, w.d_ev_n, ecap, w.d_err};
+    k_np_entry<<<C, kEntryThreads, static_cast<size_t>(lds), s>>>(ea);
+    HIP_TRY(hipGetLastError());
+    fin_m.resize(C);
+    ev_n.resize(C);
+    fin.resize(static_cast<size_t>(C) * 64);
+    int err = 0;
+    HIP_TRY(hipMemcpyAsync(fin_m.data(), w.d_fin_m, sizeof(int) * C, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpy2DAsync(fin.data(), 64 * sizeof(uint32_t), w.d_fin, sizeof(uint32_t) * n1,
+                             sizeof(uint32_t) * std::min(64, n1), C, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&err, w.d_err, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (err & 1) {  // wrap log overflow: a larger log and the same segment again
+      if (ecap >= kW + 2 * n1) return fail(RS_EDEVICE, "np sampler: wrap log overflow");
+      ecap = static_cast<int>(std::min<int64_t>(kW + 2 * n1, 2 * static_cast<int64_t>(ecap)));
+      continue;
+    }
+    // 4: compose the chunk maps; entry list index a <-> state n1 - a; chunk 0 starts a hypothesis
+    ent.resize(C);
+    std::vector<uint32_t> big;
+    int a = 0;
+    for (int ci = 0; ci < C; ++ci) {
+      ent[ci] = a;
+      const int m = fin_m[ci];
+      const uint32_t *f = fin.data() + static_cast<size_t>(ci) * 64;
+      if (m > 64) {
+        big.resize(static_cast<size_t>(m));
+        HIP_TRY(hipMemcpy(big.data(), w.d_fin + static_cast<size_t>(ci) * n1, sizeof(uint32_t) * m,
+                          hipMemcpyDeviceToHost));
+        f = big.data();
+      }
+      int best = -1, bst = 0, top = -1, tst = 0;
+      for (int i = 0; i < m; ++i) {
+        const int lo = static_cast<int>(f[i] & 0xffffu), sv = static_cast<int>(f[i] >> 16);
+        if (lo <= a && lo > best) best = lo, bst = sv;
+        if (lo > top) top = lo, tst = sv;
+      }
+      a = n1 - (best >= 0 ? bst : tst);
+    }
+    HIP_TRY(hipMemcpyAsync(w.d_ent, ent.data(), sizeof(int) * C, hipMemcpyHostToDevice, s));
+    // 5: the true wraps = hypothesis starts
+    k_np_filter<<<C, 64, 0, s>>>(w.d_ev, w.d_ev_n, w.d_ent, w.d_vcnt, ecap);
+    HIP_TRY(hipGetLastError());
+    vcnt.resize(C);
+    HIP_TRY(hipMemcpyAsync(vcnt.data(), w.d_vcnt, sizeof(int) * C, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    off.resize(C);
+    int64_t tot = 0;
+    for (int ci = 0; ci < C; ++ci) {
+      off[ci] = static_cast<int>(tot);
+      tot += vcnt[ci];
+    }
+    const int64_t got = std::min<int64_t>(hs, tot);
+    if (got < 1) return fail(RS_EDEVICE, "np sampler: segment holds no complete hypothesis");
+    HIP_TRY(hipMemcpyAsync(w.d_off, off.data(), sizeof(int) * C, hipMemcpyHostToDevice, s));
+    k_np_starts<<<C, 256, 0, s>>>(w.d_ev, w.d_vcnt, w.d_off, w.d_starts, got, ecap);
+    HIP_TRY(hipGetLastError());
+    // 6: tuples
+    k_np_tuples<<<static_cast<unsigned>((got + 255) / 256), 256, 0, s>>>(
+        w.d_stream + *pos, w.d_starts, got, n1, k, w.d_J, d_out + done * k, w.d_err);
+    HIP_TRY(hipGetLastError());
+    int64_t used = 0;
+    HIP_TRY(hipMemcpyAsync(&used, w.d_starts + got, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&err, w.d_err, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (err) return fail(RS_EDEVICE, "np sampler: hypothesis parse mismatch");
+    // state after `used` draws: the block holding the next word (rs_mt_jump's convention)
+    const int64_t W = *pos + used;
+    if (W > kN) {
+      const int64_t b = (W - 1) / kN;
+      uint32_t blk[kN];
+      HIP_TRY(hipMemcpy(blk, w.d_stream + b * kN, sizeof(blk), hipMemcpyDeviceToHost));
+      for (int i = 0; i < kN; ++i) key[i] = untemper(blk[i]);
+      *pos = static_cast<int32_t>(W - b * kN);
+    } else {
+      *pos = static_cast<int32_t>(W);
+    }
+    done += got;
+  }
+  return RS_OK;
+}
+
+}  // namespace rs
+
+extern "C" int rs_np_choice_tuples_gpu(rs_ctx *c, uint32_t *mt_key, int32_t *mt_pos, int64_t n,
+                                       int32_t k, int64_t count, int32_t *out) {
+  if (!c || !mt_key || !mt_pos || (count > 0 && !out))
+    return rs::fail(RS_EINVAL, "rs_np_choice_tuples_gpu: null pointer");
+  if (count < 0 || k < 0) return rs::fail(RS_EINVAL, "negative dimensions are not allowed");
+  if (count == 0) return RS_OK;
+  int st;
+  if ((st = rs::ensure_scratch(c, sizeof(int32_t) * static_cast<size_t>(count) * k))) return st;
+  uint32_t key[kN];
+  int32_t pos = *mt_pos;
+  std::memcpy(key, mt_key, sizeof(key));
+  if ((st = rs::np_choice_device(c, key, &pos, n, k, count, static_cast<int32_t *>(c->scratch))))
+    return st;
+  HIP_TRY(hipMemcpy(out, c->scratch, sizeof(int32_t) * static_cast<size_t>(count) * k,
+                    hipMemcpyDeviceToHost));
+  std::memcpy(mt_key, key, sizeof(key));
+  *mt_pos = pos;
+  return RS_OK;
+}
