@@ -449,18 +449,30 @@ def main():
                                 "frac": pmc / (c_ms * 1e-3) / 1e9 / PEAK_HBM_GBS}
 
     if rank == 0 and world == 1 and not args.no_parity_mode:
-        # numpy-exact sampling (host MT19937 replay) + the same GPU pipeline
-        key, pos = _ffi.np_seed(0)
-        ts = []
+        # numpy-exact sampling + the same GPU pipeline: the np.random stream parsed on the
+        # GPU (rs_f8_plan_run_np), and the serial host replay for comparison
+        key0, pos0 = _ffi.np_seed(0)
+        tg = []
+        for _ in range(6):
+            t = time.perf_counter()
+            plan.run_np(H, key0, pos0)
+            plan.result()
+            tg.append(time.perf_counter() - t)
+        th = []
         for _ in range(2):
             t = time.perf_counter()
-            tup, key, pos = _ffi.np_choice_tuples(key, pos, args.n, 8, H)
+            tup, _, _ = _ffi.np_choice_tuples(key0, pos0, args.n, 8, H)
             plan.run(H, mode=_ffi.SAMPLER_TUPLES, tuples=tup)
             plan.result()
-            ts.append(time.perf_counter() - t)
-        line["parity_mode"] = {"value": H / min(ts), "unit": "hypotheses/s",
-                               "note": "np.random legacy stream replayed bit-exactly on one "
-                                       "host core, then the GPU pipeline; host-sampler bound"}
+            th.append(time.perf_counter() - t)
+        line["parity_mode"] = {"value": H / min(tg[1:]), "unit": "hypotheses/s",
+                               "ms": 1e3 * min(tg[1:]),
+                               "host_replay_value": H / min(th),
+                               "note": "np.random legacy stream (seed 0) reproduced bit-exactly "
+                                       "on the GPU (MT19937 jump-ahead windows, all-entry-state "
+                                       "chunk parse, per-hypothesis swap trace), then the same "
+                                       "GPU pipeline; host_replay_value = the serial replay on "
+                                       "one host core feeding the same pipeline"}
     if cpu is not None:
         line["cpu_baseline"] = cpu
     if not args.no_extras:

@@ -139,6 +139,12 @@ int rs_f8_plan_set_points(rs_f8_plan *plan, const double *p1, const double *p2);
  * counter (seed, hyp_offset + i); tuple mode reads host_tuples (H, 8) int32. */
 int rs_f8_plan_run(rs_f8_plan *plan, int64_t H, int32_t mode, uint64_t seed, uint64_t hyp_offset,
                    const int32_t *host_tuples, double thresh);
+/* Parity-mode run: the next H tuples of the numpy legacy stream (key, pos) -- the
+ * rs_np_choice_tuples stream, fun.py:305-306 -- sampled on the GPU (np_sampler.hip) straight
+ * into the run's tuple buffer, then the same pipeline as rs_f8_plan_run.  Advances
+ * (key, pos) in place.  Populations beyond the GPU parse (n - 1 > 10240) use the host replay. */
+int rs_f8_plan_run_np(rs_f8_plan *plan, int64_t H, uint32_t *mt_key, int32_t *mt_pos,
+                      double thresh);
 /* Wait for the last run and copy its result; inliers (S_RANSAC, ascending) up to cap. */
 int rs_f8_plan_result(rs_f8_plan *plan, rs_f8_result *out, int64_t *inliers, int64_t cap,
                       int64_t *n_inliers);

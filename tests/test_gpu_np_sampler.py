@@ -75,7 +75,7 @@ def test_gpu_stream_errors(ctx):
 _SEG_CHILD = """
 import numpy as np
 from tsbb15_amd import _ffi
-for n, count in ((2000, 2000), (37, 40000)):
+for n, count in ((2000, 2000), (37, 40000), (257, 3000), (10000, 100)):
     st = np.random.RandomState(21).get_state()
     key, pos = np.asarray(st[1], np.uint32), int(st[2])
     ref = _ffi.np_choice_tuples(key, pos, n, 8, count)
@@ -85,10 +85,37 @@ print("ok")
 """
 
 
-def test_gpu_stream_many_segments():
-    """Segments of 2^20 words (the segment size is read once per process, so in a child)."""
-    env = dict(os.environ, RSAMD_NP_SEGWORDS=str(1 << 20),
+@pytest.mark.parametrize("knobs", [{"RSAMD_NP_SEGWORDS": str(1 << 20)},
+                                   {"RSAMD_NP_KW": "8192"},
+                                   {"RSAMD_NP_KW": "262144", "RSAMD_NP_LANE_TUPLES": "1"}])
+def test_gpu_stream_many_segments(knobs):
+    """Segments of 2^20 words, the shortest / longest parse chunks and the lane-per-hypothesis
+    tuple kernel (these knobs are read once per process, so in a child)."""
+    env = dict(os.environ, **knobs,
                PYTHONPATH=os.pathsep.join([PKG_DIR, REPO, os.environ.get("PYTHONPATH", "")]))
     r = subprocess.run([sys.executable, "-c", _SEG_CHILD], env=env, capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("n,H,seed", [(2000, 100000, 0), (257, 10000, 3), (10240, 2000, 7)])
+def test_plan_run_np_equals_host_tuple_run(ctx, n, H, seed):
+    """rs_f8_plan_run_np (tuples parsed on the GPU into the run's buffer) = the same plan fed the
+    host replay's tuples: winner, S_RANSAC, F bits and the advanced stream state."""
+    from tsbb15_amd import synth
+    p1, p2, _ = synth.two_view(n, 0.3, seed=seed + 1)
+    key, pos = _state(seed)
+    plan = _ffi.F8Plan(ctx, n, H)
+    try:
+        plan.set_points(p1, p2)
+        gkey, gpos = plan.run_np(H, key, pos)
+        g = plan.result()
+        tup, rkey, rpos = _ffi.np_choice_tuples(key, pos, n, 8, H)
+        plan.run(H, mode=_ffi.SAMPLER_TUPLES, tuples=tup)
+        h = plan.result()
+    finally:
+        plan.close()
+    assert gpos == rpos and np.array_equal(gkey, rkey)
+    assert g[0].best_index == h[0].best_index and g[0].best_count == h[0].best_count
+    assert np.array_equal(g[1], h[1])
+    assert np.array_equal(np.array(g[0].F[:]), np.array(h[0].F[:]))

@@ -20,7 +20,7 @@ def best(fn, reps):
     return min(t), r
 
 
-for n, count, reps in ((2000, 100000, 5), (10000, 20000, 3), (37, 100000, 3)):
+for n, count, reps in ((2000, 100000, 5), (10000, 20000, 3), (257, 10000, 5), (37, 100000, 3)):
     st = np.random.RandomState(1).get_state()
     key, pos = np.asarray(st[1], np.uint32), int(st[2])
     tg, g = best(lambda: _ffi.np_choice_tuples_gpu(key, pos, n, 8, count), reps)

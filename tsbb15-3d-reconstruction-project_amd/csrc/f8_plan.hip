@@ -433,15 +433,18 @@ static int choose_chunk(const rs_f8_plan *p, int64_t H) {
   return static_cast<int>((p->n + nchunks - 1) / nchunks);
 }
 
-extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t seed,
-                              uint64_t hyp_offset, const int32_t *host_tuples, double thresh) {
+// One run.  dev_tuples: tuple mode with the tuples already written (in range, by the GPU
+// parity stream) into the buffer set this run uses, so there is no host copy or check.
+static int plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t seed, uint64_t hyp_offset,
+                    const int32_t *host_tuples, double thresh, bool dev_tuples) {
   if (!p) return fail(RS_EINVAL, "null plan");
   if (H < 1 || H > p->max_hyp) return fail(RS_EINVAL, "hypothesis count out of plan range");
   if (mode != RS_SAMPLER_PHILOX && mode != RS_SAMPLER_TUPLES)
     return fail(RS_EINVAL, "unknown sampler mode");
-  if (mode == RS_SAMPLER_TUPLES && !host_tuples) return fail(RS_EINVAL, "tuples required");
+  if (mode == RS_SAMPLER_TUPLES && !host_tuples && !dev_tuples)
+    return fail(RS_EINVAL, "tuples required");
   if (!(thresh == thresh)) return fail(RS_EINVAL, "threshold is NaN");
-  if (mode == RS_SAMPLER_TUPLES)
+  if (mode == RS_SAMPLER_TUPLES && !dev_tuples)
     for (int64_t i = 0; i < 8 * H; ++i)
       if (host_tuples[i] < 0 || host_tuples[i] >= p->n)
         return fail(RS_EINVAL, "tuple index out of range");
@@ -461,7 +464,7 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
   if (p->overlap && p->runs >= rs_f8_plan::kBufs)  // set `set` free: run k-3's tail is done
     HIP_TRY(hipStreamWaitEvent(sst, p->ev_free[set], 0));
 
-  if (mode == RS_SAMPLER_TUPLES)
+  if (mode == RS_SAMPLER_TUPLES && !dev_tuples)
     HIP_TRY(hipMemcpyAsync(b.d_tuples, host_tuples, sizeof(int) * 8 * H, hipMemcpyHostToDevice,
                            sst));
   // [tail of the previous run | solve of this run]: buffer set b was last read by run k-2,
@@ -577,6 +580,30 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
   p->last_H = H;
   p->pending = true;
   return RS_OK;
+}
+
+extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t seed,
+                              uint64_t hyp_offset, const int32_t *host_tuples, double thresh) {
+  return plan_run(p, H, mode, seed, hyp_offset, host_tuples, thresh, false);
+}
+
+// Parity mode with the numpy stream sampled on the GPU (np_sampler.hip) straight into the
+// tuple buffer of the run about to be issued; advances (key, pos).  The sampler is synchronous
+// on the context stream, and that buffer set was last read by run k-2's solve, which precedes
+// it in stream order.  The two-stream overlap variant reads tuples on its own stream: it and
+// populations beyond the GPU parse's range go through the host replay.
+extern "C" int rs_f8_plan_run_np(rs_f8_plan *p, int64_t H, uint32_t *key, int32_t *pos,
+                                 double thresh) {
+  if (!p || !key || !pos) return fail(RS_EINVAL, "null pointer");
+  int st;
+  if (!p->overlap && rs::np_gpu_supported(p->n, 8) && std::getenv("RSAMD_NP_HOST") == nullptr) {
+    RunBufs &b = p->buf[p->runs % rs_f8_plan::kBufs];
+    if ((st = rs::np_choice_device(p->ctx, key, pos, p->n, 8, H, b.d_tuples))) return st;
+    return plan_run(p, H, RS_SAMPLER_TUPLES, 0, 0, nullptr, thresh, true);
+  }
+  std::vector<int32_t> tuples(static_cast<size_t>(8 * H));
+  if ((st = rs_np_choice_tuples(key, pos, p->n, 8, H, tuples.data()))) return st;
+  return plan_run(p, H, RS_SAMPLER_TUPLES, 0, 0, tuples.data(), thresh, false);
 }
 
 // Complete the last run (its pending tail) and wait.  Accessors below then read its buffer
@@ -761,13 +788,10 @@ extern "C" int rs_f8_ransac_np(rs_ctx *c, const double *p1, const double *p2, in
   int st;
   if (!c->np_plan && (st = rs_f8_plan_create(c, n, H, &c->np_plan))) return st;
   if ((st = rs_f8_plan_set_points(c->np_plan, p1, p2))) return st;
-  std::vector<int32_t> tuples(static_cast<size_t>(8 * H));
   uint32_t key[RS_MT_N];
   int32_t pos = *mt_pos;
   std::memcpy(key, mt_key, sizeof(key));
-  if ((st = rs_np_choice_tuples(key, &pos, n, 8, H, tuples.data()))) return st;
-  if ((st = rs_f8_plan_run(c->np_plan, H, RS_SAMPLER_TUPLES, 0, 0, tuples.data(), thresh)))
-    return st;
+  if ((st = rs_f8_plan_run_np(c->np_plan, H, key, &pos, thresh))) return st;
   if ((st = rs_f8_plan_result(c->np_plan, out, inliers, cap, n_inliers))) return st;
   std::memcpy(mt_key, key, sizeof(key));
   *mt_pos = pos;

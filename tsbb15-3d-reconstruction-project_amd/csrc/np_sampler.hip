@@ -60,7 +60,8 @@ constexpr int kJB = 1024;                    // stream blocks per generator
 constexpr int64_t kJ = int64_t(kN) * kJB;    // words per generator
 constexpr int kLevels = 11;                  // jump tree depth: up to 2048 generators
 constexpr int64_t kSegWords = int64_t(1) << 29;  // stream words per segment (2 GiB)
-constexpr int kW = 262144;                   // draws per parse chunk
+constexpr int kW = 262144;                   // longest parse chunk (draws)
+constexpr int kWmin = 8192;                  // shortest parse chunk
 constexpr int kEntryThreads = 512;
 constexpr int kR = 20;                       // slots per thread: N - 1 <= 10240
 constexpr int kMaxN1 = kEntryThreads * kR;
@@ -88,31 +89,52 @@ __device__ __forceinline__ uint32_t masked(uint32_t w, uint32_t i) {
 // y_{i+w} over the set bits i of the polynomial.  Only the top bit of word 0 is MT state, so
 // word 0 of a jumped window may carry wrong low bits: it is never emitted (k_mt_stream) and
 // the recurrence reads only its top bit.
-__global__ __launch_bounds__(256) void k_mt_jump(uint32_t *__restrict__ win, int half, int G,
-                                                 const int32_t *__restrict__ bits, int nbits) {
+// 1024 threads: four groups of 256 XOR a quarter of the set bits each (four waves per SIMD
+// hide the LDS latency of the bit loop), then one LDS reduction.
+constexpr int kJumpGroups = 4;
+__global__ __launch_bounds__(256 * kJumpGroups) void k_mt_jump(uint32_t *__restrict__ win, int half,
+                                                               int G, const int32_t *__restrict__ bits,
+                                                               int nbits) {
   __shared__ uint32_t y[kPrefix];
+  __shared__ uint32_t part[kJumpGroups - 1][kN];
   const int g = blockIdx.x, dst = g + half;
   if (dst >= G) return;
-  const int tid = threadIdx.x;
-  for (int t = tid; t < kN; t += 256) y[t] = win[static_cast<size_t>(g) * kN + t];
+  const int tid = threadIdx.x, grp = tid >> 8, lt = tid & 255;
+  for (int t = tid; t < kN; t += 256 * kJumpGroups) y[t] = win[static_cast<size_t>(g) * kN + t];
   __syncthreads();
   for (int t0 = kN; t0 < kPrefix; t0 += 227) {
     const int t = t0 + tid;
     if (tid < 227 && t < kPrefix) y[t] = y[t - 227] ^ twist(y[t - kN], y[t - kN + 1]);
     __syncthreads();
   }
-  const int w0 = tid, w1 = tid + 256, w2 = tid + 512 < kN ? tid + 512 : kN - 1;
+  const int w0 = lt, w1 = lt + 256, w2 = lt + 512 < kN ? lt + 512 : kN - 1;
+  const int per = (nbits + kJumpGroups - 1) / kJumpGroups;
+  const int b0 = grp * per, b1 = min(nbits, b0 + per);
   uint32_t a0 = 0, a1 = 0, a2 = 0;
-  for (int b = 0; b < nbits; ++b) {
+  for (int b = b0; b < b1; ++b) {
     const int i = bits[b];
     a0 ^= y[i + w0];
     a1 ^= y[i + w1];
     a2 ^= y[i + w2];
   }
-  uint32_t *out = win + static_cast<size_t>(dst) * kN;
-  out[w0] = a0;
-  out[w1] = a1;
-  if (tid + 512 < kN) out[w2] = a2;
+  if (grp > 0) {
+    part[grp - 1][w0] = a0;
+    part[grp - 1][w1] = a1;
+    if (lt + 512 < kN) part[grp - 1][w2] = a2;
+  }
+  __syncthreads();
+  if (grp == 0) {
+#pragma unroll
+    for (int q = 0; q < kJumpGroups - 1; ++q) {
+      a0 ^= part[q][w0];
+      a1 ^= part[q][w1];
+      a2 ^= part[q][w2];
+    }
+    uint32_t *out = win + static_cast<size_t>(dst) * kN;
+    out[w0] = a0;
+    out[w1] = a1;
+    if (lt + 512 < kN) out[w2] = a2;
+  }
 }
 
 // ---- 2. stream: generator g owns blocks (g kJB, (g+1) kJB] plus words 1..623 of its window --
@@ -150,11 +172,13 @@ __global__ __launch_bounds__(64) void k_mt_stream(const uint32_t *__restrict__ w
 struct EntryArgs {
   const uint32_t *draws;  // draw 0 of the segment
   int64_t D;              // draws in the segment
+  int W;                  // draws per chunk
   int n1;                 // N - 1: parser states 1..n1, entry list index a <-> state n1 - a
   uint32_t *fin;          // [C][n1] final list: lo | state << 16
   int *fin_m;             // [C]
   uint2 *ev;              // [C][ecap] wraps: (draw after the wrap, lo | hi << 16)
   int *ev_n;              // [C]
+  int *tpos;              // [C] draws parsed by the dense kernel (the sparse kernel resumes there)
   int ecap;
   int *err;
 };
@@ -195,8 +219,8 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a) {
   const int n1 = a.n1, n1p = (n1 + 1) & ~1;
   uint16_t *st = dyn, *lo = dyn + n1p, *st2 = dyn + 2 * n1p, *lo2 = dyn + 3 * n1p;
   const int c = blockIdx.x;
-  const int64_t t0 = static_cast<int64_t>(c) * kW;
-  const int T = static_cast<int>(std::min<int64_t>(kW, a.D - t0));
+  const int64_t t0 = static_cast<int64_t>(c) * a.W;
+  const int T = static_cast<int>(std::min<int64_t>(a.W, a.D - t0));
   const uint32_t *wp = a.draws + t0;
   uint2 *ev = a.ev + static_cast<size_t>(c) * a.ecap;
   const uint32_t N1 = static_cast<uint32_t>(n1);
@@ -217,9 +241,41 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a) {
     }
     while (m > 64 && t < T) {
       const int kk = min(kK, T - t);
+      const int nr = (m + kEntryThreads - 1) / kEntryThreads;
+      if (nr == 1 && kk == 64) {
+        // one slot per thread (the common case after the first ~n1 draws): the 64 words in a
+        // register of every wave, branch-free steps, a slot's wrap (at most one in 64 draws,
+        // as n1 > 64) logged after the batch with one LDS atomic per wave
+        // (waves holding only empty slots skip the batch: sentinels stay sentinels)
+        uint32_t sv = s[0], wk = 0xffffffffu;
+        if ((tid & ~63) < m) {
+          const uint32_t wv = wp[t + lane];
+#pragma unroll
+          for (int k = 0; k < 64; ++k) {
+            const uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wv), k));
+            sv -= masked(w, sv) <= sv ? 1u : 0u;
+            const bool z = sv == 0;
+            sv = z ? N1 : sv;
+            wk = z ? static_cast<uint32_t>(k) : wk;
+          }
+        }
+        s[0] = sv;
+        const uint64_t wr = __ballot(wk != 0xffffffffu);
+        if (wr) {
+          int base = 0;
+          if (lane == 0) base = atomicAdd(&sh_evn, __popcll(wr));
+          base = __shfl(base, 0);
+          if (wk != 0xffffffffu) {
+            const int e = base + static_cast<int>(lane_rank(wr));
+            if (e < a.ecap)
+              ev[e] = make_uint2(static_cast<uint32_t>(t) + wk + 1u,
+                                 lo[tid] | (static_cast<uint32_t>(lo[tid + 1 == m ? 0 : tid + 1]) << 16));
+          }
+        }
+        t += kk;
+      } else {
       if (tid < kk) wbuf[tid] = wp[t + tid];
       __syncthreads();
-      const int nr = (m + kEntryThreads - 1) / kEntryThreads;
       for (int k = 0; k < kk; ++k) {
         const uint32_t w = wbuf[k];
 #pragma unroll
@@ -239,6 +295,7 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a) {
         }
       }
       t += kk;
+      }
       // compaction: list order starts at the head (first slot of the maximum run); equal
       // neighbours merge, the first keeps its lo
       __syncthreads();
@@ -310,27 +367,77 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a) {
       return;
     }
   }
-  // sparse phase: one wave, lane l = slot l
-  if (tid >= 64) return;
-  const int l = lane;
-  uint32_t sv = l < m ? st[l] : kSentinel;
-  uint32_t lov = l < m ? lo[l] : 0u;
-  int ecnt = sh_evn;
+  // hand over to k_np_sparse: the (<= 64) live slots, the wrap count and the position
+  __syncthreads();
+  for (int q = tid; q < m; q += kEntryThreads)
+    a.fin[static_cast<size_t>(c) * n1 + q] = lo[q] | (static_cast<uint32_t>(st[q]) << 16);
+  if (tid == 0) {
+    a.fin_m[c] = m;
+    a.ev_n[c] = sh_evn;
+    a.tpos[c] = t;
+  }
+}
+
+// ---- 3b. sparse phase of a chunk: one wave, lane l = slot l ---------------------------------
+// A separate 64-thread launch so that the long serial tail of every chunk runs at full
+// occupancy (inside the 512-thread dense workgroup it held a CU slot with one wave).
+__device__ __forceinline__ void sparse_step(uint32_t w, uint32_t &sv) {
+  sv -= masked(w, sv) <= sv ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(64) void k_np_sparse(EntryArgs a) {
+  const int c = blockIdx.x, l = threadIdx.x;
+  int m = a.fin_m[c];
+  if (m > 64) return;  // the chunk ended while dense: final already
+  const int n1 = a.n1;
+  const int64_t t0 = static_cast<int64_t>(c) * a.W;
+  const int T = static_cast<int>(std::min<int64_t>(a.W, a.D - t0));
+  const uint32_t *wp = a.draws + t0;
+  uint2 *ev = a.ev + static_cast<size_t>(c) * a.ecap;
+  const uint32_t N1 = static_cast<uint32_t>(n1);
+  int t = a.tpos[c];
+  const uint32_t f0 = l < m ? a.fin[static_cast<size_t>(c) * n1 + l] : 0u;
+  uint32_t sv = l < m ? (f0 >> 16) : kSentinel;
+  uint32_t lov = f0 & 0xffffu;
+  int ecnt = a.ev_n[c];
   while (t < T) {
     const int kk = min(64, T - t);
     const uint32_t wv = l < kk ? wp[t + l] : 0u;
-    for (int k = 0; k < kk; ++k) {
-      const uint32_t w = __builtin_amdgcn_readlane(wv, k);
-      sv -= masked(w, sv) <= sv ? 1u : 0u;
-      const uint64_t wr = __ballot(sv == 0);
+    if (kk == 64 && n1 >= 64) {
+      // a lane wraps at most once in 64 draws (a hypothesis takes >= n1 >= 64): branch-free
+      // steps, the wrap draw kept per lane and logged after the batch
+      uint32_t wk = 0xffffffffu;
+#pragma unroll
+      for (int k = 0; k < 64; ++k) {
+        const uint32_t w = __builtin_amdgcn_readlane(wv, k);
+        sparse_step(w, sv);
+        const bool z = sv == 0;
+        sv = z ? N1 : sv;
+        wk = z ? static_cast<uint32_t>(k) : wk;
+      }
+      const uint64_t wr = __ballot(wk != 0xffffffffu);
       if (wr) {
         const uint32_t succ = __shfl(lov, l + 1 == m ? 0 : l + 1);
-        if (sv == 0) {
-          sv = N1;
+        if (wk != 0xffffffffu) {
           const int e = ecnt + static_cast<int>(lane_rank(wr));
-          if (e < a.ecap) ev[e] = make_uint2(static_cast<uint32_t>(t + k + 1), lov | (succ << 16));
+          if (e < a.ecap) ev[e] = make_uint2(static_cast<uint32_t>(t) + wk + 1u, lov | (succ << 16));
         }
         ecnt += __popcll(wr);
+      }
+    } else {
+      for (int k = 0; k < kk; ++k) {
+        const uint32_t w = __builtin_amdgcn_readlane(wv, k);
+        sparse_step(w, sv);
+        const uint64_t wr = __ballot(sv == 0);
+        if (wr) {
+          const uint32_t succ = __shfl(lov, l + 1 == m ? 0 : l + 1);
+          if (sv == 0) {
+            sv = N1;
+            const int e = ecnt + static_cast<int>(lane_rank(wr));
+            if (e < a.ecap) ev[e] = make_uint2(static_cast<uint32_t>(t + k + 1), lov | (succ << 16));
+          }
+          ecnt += __popcll(wr);
+        }
       }
     }
     t += kk;
@@ -391,14 +498,14 @@ __global__ __launch_bounds__(64) void k_np_filter(uint2 *__restrict__ ev, const 
 __global__ __launch_bounds__(256) void k_np_starts(const uint2 *__restrict__ ev,
                                                    const int *vcnt, const int *off,
                                                    int64_t *__restrict__ starts, int64_t H,
-                                                   int ecap) {
+                                                   int ecap, int W) {
   const int c = blockIdx.x;
   const int n = vcnt[c];
   const int64_t base = 1 + off[c];
   for (int i = threadIdx.x; i < n; i += 256) {
     const int64_t idx = base + i;
     if (idx <= H)
-      starts[idx] = static_cast<int64_t>(c) * kW + ev[static_cast<size_t>(c) * ecap + i].x;
+      starts[idx] = static_cast<int64_t>(c) * W + ev[static_cast<size_t>(c) * ecap + i].x;
   }
   if (c == 0 && threadIdx.x == 0) starts[0] = 0;
 }
@@ -436,6 +543,84 @@ __global__ __launch_bounds__(256) void k_np_tuples(const uint32_t *__restrict__ 
     for (int k = 0; k < 8; ++k) p[k] = p[k] == s ? j : (p[k] == j ? s : p[k]);
   }
   for (int k = 0; k < kk; ++k) out[h * kk + k] = static_cast<int32_t>(p[k]);
+}
+
+// ---- 6'. one wave per hypothesis (default): a window of W <= 64 words per step -------------
+// Within a window every state keeps the mask of the first (W <= i - mask/2), so lane l's draw
+// u_l = w_l & mask is accepted for sure if u_l <= i - l (its state is at least i - l), rejected
+// for sure if u_l > i, and only the rare lanes in between are resolved in order.  Accepted
+// lanes have consecutive states, so the swap partners J[state - 1] land in LDS together.  The
+// trace keeps the k positions in wave-uniform registers: for state s >= 8 a position p < s can
+// only move to s (when J[s - 1] == p), found by a ballot over 64 states at a time.
+constexpr int kTupWaves = 4;
+__global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
+    const uint32_t *__restrict__ draws, const int64_t *__restrict__ starts, int64_t H, int n1,
+    int n1p, int kk, int32_t *__restrict__ out, int *err) {
+  extern __shared__ uint16_t jl[];
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t h = static_cast<int64_t>(blockIdx.x) * kTupWaves + wv;
+  if (h >= H) return;  // wave-uniform; the kernel has no workgroup barrier
+  uint16_t *J = jl + static_cast<size_t>(wv) * n1p;
+  const int64_t a = starts[h], b = starts[h + 1];
+  const uint64_t below = (1ull << l) - 1ull;
+  uint32_t i = static_cast<uint32_t>(n1);
+  int64_t d = a;
+  while (i > 0) {
+    const uint32_t msk = 0xffffffffu >> __builtin_clz(i);
+    const uint32_t L = i - (msk >> 1);
+    const int W = L < 64u ? static_cast<int>(L) : 64;
+    const bool in = l < W;
+    const uint32_t u = in ? (draws[d + l] & msk) : 0xffffffffu;
+    const uint32_t lo_s = i - static_cast<uint32_t>(l);
+    uint64_t acc = __ballot(in && u <= lo_s);
+    uint64_t amb = __ballot(in && u > lo_s && u <= i);
+    while (amb) {
+      const int f = __ffsll(static_cast<long long>(amb)) - 1;
+      const uint32_t uf = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(u), f));
+      const uint32_t sf = i - static_cast<uint32_t>(__popcll(acc & ((1ull << f) - 1ull)));
+      if (uf <= sf) acc |= 1ull << f;
+      amb &= amb - 1ull;
+    }
+    if ((acc >> l) & 1ull)
+      J[i - static_cast<uint32_t>(__popcll(acc & below)) - 1u] = static_cast<uint16_t>(u);
+    i -= static_cast<uint32_t>(__popcll(acc));
+    d += W;
+  }
+  if (d != b) {
+    if (l == 0) atomicOr(err, 2);
+    return;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  uint32_t p[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) p[k] = static_cast<uint32_t>(k);
+  const int s1 = n1 < 7 ? n1 : 7;
+  for (int s = 1; s <= s1; ++s) {  // states below 8: the full transposition rule
+    const uint32_t j = J[s - 1], us = static_cast<uint32_t>(s);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) p[k] = p[k] == us ? j : (p[k] == j ? us : p[k]);
+  }
+  for (int s0 = 8; s0 <= n1; s0 += 64) {
+    const int s = s0 + l;
+    const uint32_t jv = s <= n1 ? static_cast<uint32_t>(J[s - 1]) : 0xffffffffu;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      uint64_t bb = __ballot(jv == p[k]);
+      while (bb) {
+        const int f = __ffsll(static_cast<long long>(bb)) - 1;
+        p[k] = static_cast<uint32_t>(s0 + f);
+        bb = __ballot(jv == p[k]) & ~((2ull << f) - 1ull);
+      }
+    }
+  }
+  if (l < kk) {
+    uint32_t v = p[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) v = l == k ? p[k] : v;
+    out[h * kk + l] = static_cast<int32_t>(v);
+  }
 }
 
 // ---- host ------------------------------------------------------------------------------------
@@ -502,12 +687,12 @@ struct rs_np_work {
   std::vector<int> bit_off, bit_n;
   uint32_t *d_win = nullptr, *d_stream = nullptr, *d_fin = nullptr;
   int *d_fin_m = nullptr, *d_ev_n = nullptr, *d_ent = nullptr, *d_vcnt = nullptr,
-      *d_off = nullptr, *d_err = nullptr;
+      *d_off = nullptr, *d_err = nullptr, *d_tpos = nullptr;
   uint2 *d_ev = nullptr;
   int64_t *d_starts = nullptr;
   uint16_t *d_J = nullptr;
   int64_t cap_fin = 0, cap_ev = 0, cap_starts = 0, cap_J = 0;
-  int64_t entry_lds = 0;
+  int64_t entry_lds = 0, tup_lds = 0;
 };
 
 namespace rs {
@@ -516,7 +701,8 @@ void np_work_free(rs_ctx *c) {
   rs_np_work *w = c->np_work;
   if (!w) return;
   void *ptrs[] = {w->d_bits, w->d_win, w->d_stream, w->d_fin, w->d_fin_m, w->d_ev_n,
-                  w->d_ent,  w->d_vcnt, w->d_off,   w->d_err, w->d_ev,    w->d_starts, w->d_J};
+                  w->d_ent,  w->d_vcnt, w->d_off,   w->d_err, w->d_ev,    w->d_starts, w->d_J,
+                  w->d_tpos};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   delete w;
@@ -535,6 +721,8 @@ static int grow(T *&p, int64_t &cap, int64_t need) {
   return RS_OK;
 }
 
+bool np_gpu_supported(int64_t n, int32_t k) { return k >= 1 && k <= 8 && k <= n && n - 1 <= kMaxN1; }
+
 // The numpy stream's next `count` choice(n, k) tuples into device memory (count * k int32),
 // on the context stream; advances (key, pos).  Synchronous.
 int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t k,
@@ -551,7 +739,22 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
   int st;
   const int n1 = static_cast<int>(n - 1);
   const int64_t Gmax = (kSegWords / kN + kJB - 1) / kJB + 1;
-  const int64_t Cmax = kSegWords / kW + 1;
+  // chunk length: about 1024 chunks per segment (a short serial parse per chunk, enough
+  // chunks to fill the GPU), between 8192 and 262144 draws; RSAMD_NP_KW fixes it
+  static const int kWenv = [] {
+    const char *e = std::getenv("RSAMD_NP_KW");
+    const int v = e ? std::atoi(e) : 0;
+    return v >= kWmin && v <= kW ? v : 0;
+  }();
+  const int64_t Cmax = kSegWords / kWmin + 1;
+  // RSAMD_NP_LANE_TUPLES=1: the lane-per-hypothesis tuple kernel with swap partners in HBM (A/B)
+  static const bool lane_tuples = std::getenv("RSAMD_NP_LANE_TUPLES") != nullptr;
+  const int64_t tup_lds = static_cast<int64_t>(sizeof(uint16_t)) * ((n1 + 1) & ~1) * kTupWaves;
+  if (!lane_tuples && tup_lds > w.tup_lds) {
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_np_tuples_wave),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(tup_lds)));
+    w.tup_lds = tup_lds;
+  }
   if (!w.d_bits) {
     const JumpPolys &jp = jump_polys();
     std::vector<int32_t> all;
@@ -563,18 +766,18 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
     int64_t cap = 0;
     if ((st = grow(w.d_bits, cap, static_cast<int64_t>(all.size())))) return st;
     HIP_TRY(hipMemcpy(w.d_bits, all.data(), sizeof(int32_t) * all.size(), hipMemcpyHostToDevice));
-    int64_t c1 = 0, c2 = 0, c3 = 0, c4 = 0, c5 = 0, c6 = 0, c7 = 0, c8 = 0;
+    int64_t c1 = 0, c2 = 0, c3 = 0, c4 = 0, c5 = 0, c6 = 0, c7 = 0, c8 = 0, c9 = 0;
     if ((st = grow(w.d_win, c1, Gmax * kN)) || (st = grow(w.d_stream, c2, kSegWords)) ||
         (st = grow(w.d_fin_m, c3, Cmax)) || (st = grow(w.d_ev_n, c4, Cmax)) ||
         (st = grow(w.d_ent, c5, Cmax)) || (st = grow(w.d_vcnt, c6, Cmax)) ||
-        (st = grow(w.d_off, c7, Cmax)) || (st = grow(w.d_err, c8, 1)))
+        (st = grow(w.d_off, c7, Cmax)) || (st = grow(w.d_err, c8, 1)) ||
+        (st = grow(w.d_tpos, c9, Cmax)))
       return st;
   }
-  if ((st = grow(w.d_fin, w.cap_fin, Cmax * n1))) return st;
   const double E = expected_draws(n1);
   const int64_t dmax = seg_words() - 3 * kN;
   const int64_t hcap = std::max<int64_t>(1, static_cast<int64_t>((dmax - 16 * n) / (E * 1.03)));
-  int ecap = static_cast<int>(std::min<int64_t>(kW + 2 * n1, static_cast<int64_t>(70.0 * kW / E) + 4 * n1 + 4096));
+  int ecap_shift = 0;  // wrap-log doublings after an overflow
   const int64_t lds = 8 * static_cast<int64_t>((n1 + 1) & ~1);
   if (lds > w.entry_lds) {
     HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_np_entry),
@@ -587,26 +790,37 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
   while (done < count) {
     const int64_t hs = std::min<int64_t>(count - done, hcap);
     const int64_t D = std::min<int64_t>(dmax, static_cast<int64_t>(std::ceil(hs * E * 1.03)) + 16 * n + 4096);
-    const int C = static_cast<int>((D + kW - 1) / kW);
+    int kWr = kWenv;
+    if (!kWr) {
+      kWr = kWmin;
+      while (kWr < kW && static_cast<int64_t>(kWr) * 1024 < D) kWr *= 2;
+    }
+    const int ecap = static_cast<int>(std::min<int64_t>(
+        kWr + 2 * n1, (static_cast<int64_t>(70.0 * kWr / E) + 4 * n1 + 4096) << ecap_shift));
+    const int C = static_cast<int>((D + kWr - 1) / kWr);
+    if ((st = grow(w.d_fin, w.cap_fin, static_cast<int64_t>(C) * n1))) return st;
     const int64_t Lb = (*pos + D + kN - 1) / kN;
     const int G = static_cast<int>((Lb + kJB - 1) / kJB);
     if ((st = grow(w.d_ev, w.cap_ev, static_cast<int64_t>(C) * ecap)) ||
         (st = grow(w.d_starts, w.cap_starts, hs + 1)) ||
-        (st = grow(w.d_J, w.cap_J, hs * n1)))
+        (lane_tuples && (st = grow(w.d_J, w.cap_J, hs * n1))))
       return st;
     // 1-2: the word stream from (key, pos): block 0 is the key itself
     HIP_TRY(hipMemcpyAsync(w.d_win, key, sizeof(uint32_t) * kN, hipMemcpyHostToDevice, s));
     for (int half = 1, lv = 0; half < G; half *= 2, ++lv) {
       if (lv >= kLevels) return fail(RS_EINVAL, "np sampler: segment too long");
-      k_mt_jump<<<half, 256, 0, s>>>(w.d_win, half, G, w.d_bits + w.bit_off[lv], w.bit_n[lv]);
+      k_mt_jump<<<half, 256 * kJumpGroups, 0, s>>>(w.d_win, half, G, w.d_bits + w.bit_off[lv], w.bit_n[lv]);
       HIP_TRY(hipGetLastError());
     }
     k_mt_stream<<<G, 64, 0, s>>>(w.d_win, w.d_stream, Lb);
     HIP_TRY(hipGetLastError());
     // 3: all-entry parse per chunk
     HIP_TRY(hipMemsetAsync(w.d_err, 0, sizeof(int), s));
-    EntryArgs ea{w.d_stream + *pos, D, n1, w.d_fin, w.d_fin_m, w.d_ev, w.d_ev_n, ecap, w.d_err};
+    EntryArgs ea{w.d_stream + *pos, D, kWr, n1, w.d_fin, w.d_fin_m, w.d_ev, w.d_ev_n, w.d_tpos,
+                 ecap, w.d_err};
     k_np_entry<<<C, kEntryThreads, static_cast<size_t>(lds), s>>>(ea);
+    HIP_TRY(hipGetLastError());
+    k_np_sparse<<<C, 64, 0, s>>>(ea);
     HIP_TRY(hipGetLastError());
     fin_m.resize(C);
     ev_n.resize(C);
@@ -618,24 +832,28 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
     HIP_TRY(hipMemcpyAsync(&err, w.d_err, sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (err & 1) {  // wrap log overflow: a larger log and the same segment again
-      if (ecap >= kW + 2 * n1) return fail(RS_EDEVICE, "np sampler: wrap log overflow");
-      ecap = static_cast<int>(std::min<int64_t>(kW + 2 * n1, 2 * static_cast<int64_t>(ecap)));
+      if (ecap >= kWr + 2 * n1) return fail(RS_EDEVICE, "np sampler: wrap log overflow");
+      ++ecap_shift;
       continue;
     }
     // 4: compose the chunk maps; entry list index a <-> state n1 - a; chunk 0 starts a hypothesis
     ent.resize(C);
+    // chunks that ended dense (m > 64): their full lists in one copy of the row range
+    int cb0 = C, cb1 = -1;
+    for (int ci = 0; ci < C; ++ci)
+      if (fin_m[ci] > 64) cb0 = std::min(cb0, ci), cb1 = ci;
     std::vector<uint32_t> big;
+    if (cb1 >= cb0) {
+      big.resize(static_cast<size_t>(cb1 - cb0 + 1) * n1);
+      HIP_TRY(hipMemcpy(big.data(), w.d_fin + static_cast<size_t>(cb0) * n1,
+                        sizeof(uint32_t) * big.size(), hipMemcpyDeviceToHost));
+    }
     int a = 0;
     for (int ci = 0; ci < C; ++ci) {
       ent[ci] = a;
       const int m = fin_m[ci];
-      const uint32_t *f = fin.data() + static_cast<size_t>(ci) * 64;
-      if (m > 64) {
-        big.resize(static_cast<size_t>(m));
-        HIP_TRY(hipMemcpy(big.data(), w.d_fin + static_cast<size_t>(ci) * n1, sizeof(uint32_t) * m,
-                          hipMemcpyDeviceToHost));
-        f = big.data();
-      }
+      const uint32_t *f = m > 64 ? big.data() + static_cast<size_t>(ci - cb0) * n1
+                                 : fin.data() + static_cast<size_t>(ci) * 64;
       int best = -1, bst = 0, top = -1, tst = 0;
       for (int i = 0; i < m; ++i) {
         const int lo = static_cast<int>(f[i] & 0xffffu), sv = static_cast<int>(f[i] >> 16);
@@ -660,11 +878,18 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
     const int64_t got = std::min<int64_t>(hs, tot);
     if (got < 1) return fail(RS_EDEVICE, "np sampler: segment holds no complete hypothesis");
     HIP_TRY(hipMemcpyAsync(w.d_off, off.data(), sizeof(int) * C, hipMemcpyHostToDevice, s));
-    k_np_starts<<<C, 256, 0, s>>>(w.d_ev, w.d_vcnt, w.d_off, w.d_starts, got, ecap);
+    k_np_starts<<<C, 256, 0, s>>>(w.d_ev, w.d_vcnt, w.d_off, w.d_starts, got, ecap, kWr);
     HIP_TRY(hipGetLastError());
     // 6: tuples
-    k_np_tuples<<<static_cast<unsigned>((got + 255) / 256), 256, 0, s>>>(
-        w.d_stream + *pos, w.d_starts, got, n1, k, w.d_J, d_out + done * k, w.d_err);
+    if (lane_tuples) {
+      k_np_tuples<<<static_cast<unsigned>((got + 255) / 256), 256, 0, s>>>(
+          w.d_stream + *pos, w.d_starts, got, n1, k, w.d_J, d_out + done * k, w.d_err);
+    } else {
+      const int n1p = (n1 + 1) & ~1;
+      k_np_tuples_wave<<<static_cast<unsigned>((got + kTupWaves - 1) / kTupWaves), 64 * kTupWaves,
+                         sizeof(uint16_t) * n1p * kTupWaves, s>>>(
+          w.d_stream + *pos, w.d_starts, got, n1, n1p, k, d_out + done * k, w.d_err);
+    }
     HIP_TRY(hipGetLastError());
     int64_t used = 0;
     HIP_TRY(hipMemcpyAsync(&used, w.d_starts + got, sizeof(int64_t), hipMemcpyDeviceToHost, s));

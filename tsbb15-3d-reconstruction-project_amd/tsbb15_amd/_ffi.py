@@ -79,6 +79,7 @@ _SIGS = {
     "rs_f8_plan_set_points": (C.c_int, [C.c_void_p, _dp, _dp]),
     "rs_f8_plan_run": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.c_uint64, C.c_uint64,
                                  _i32p, C.c_double]),
+    "rs_f8_plan_run_np": (C.c_int, [C.c_void_p, C.c_int64, _u32p, _i32p, C.c_double]),
     "rs_f8_plan_result": (C.c_int, [C.c_void_p, C.POINTER(F8Result), _i64p, C.c_int64, _i64p]),
     "rs_f8_plan_candidates": (C.c_int, [C.c_void_p, C.POINTER(F8Candidate), C.c_int64, _i64p]),
     "rs_f8_plan_counts": (C.c_int, [C.c_void_p, _i32p, C.c_int64]),
@@ -328,6 +329,15 @@ class F8Plan:
             tp = ptr(tuples, C.c_int32)
         check(lib().rs_f8_plan_run(self._h, int(H), int(mode), int(seed) & (2**64 - 1),
                                    int(hyp_offset), tp, float(thresh)))
+
+    def run_np(self, H, key, pos, thresh=1.5):
+        """Parity-mode run on the numpy legacy stream (key, pos), sampled on the GPU; returns
+        the advanced (key, pos)."""
+        key = np.array(key, dtype=np.uint32, copy=True)
+        p = C.c_int32(int(pos))
+        check(lib().rs_f8_plan_run_np(self._h, int(H), ptr(key, C.c_uint32), C.byref(p),
+                                      float(thresh)))
+        return key, p.value
 
     def result(self):
         r = F8Result()
