@@ -66,6 +66,7 @@ constexpr int kEntryThreads = 512;
 constexpr int kR = 20;                       // slots per thread: N - 1 <= 10240
 constexpr int kMaxN1 = kEntryThreads * kR;
 constexpr int kK = 64;                       // draws between compactions (<= N - 1 when dense)
+constexpr int kFast = 4;                     // one-slot-per-thread batches between compactions
 constexpr uint32_t kSentinel = 0x80000000u;  // an empty slot: never reaches 0 within kW steps
 
 __device__ __forceinline__ uint32_t twist(uint32_t a, uint32_t b) {
@@ -210,7 +211,8 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t bits) {
                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bits), 0u));
 }
 
-__global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a) {
+__global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a,
+                                                             const uint32_t *__restrict__ draws) {
   extern __shared__ uint16_t dyn[];
   __shared__ uint32_t wbuf[kK];
   __shared__ int sh_red[kEntryThreads / 64];
@@ -221,7 +223,7 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a) {
   const int c = blockIdx.x;
   const int64_t t0 = static_cast<int64_t>(c) * a.W;
   const int T = static_cast<int>(std::min<int64_t>(a.W, a.D - t0));
-  const uint32_t *wp = a.draws + t0;
+  const uint32_t *__restrict__ wp = draws + t0;
   uint2 *ev = a.ev + static_cast<size_t>(c) * a.ecap;
   const uint32_t N1 = static_cast<uint32_t>(n1);
   for (int q = tid; q < n1; q += kEntryThreads) {
@@ -246,33 +248,40 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a) {
         // one slot per thread (the common case after the first ~n1 draws): the 64 words in a
         // register of every wave, branch-free steps, a slot's wrap (at most one in 64 draws,
         // as n1 > 64) logged after the batch with one LDS atomic per wave
-        // (waves holding only empty slots skip the batch: sentinels stay sentinels)
-        uint32_t sv = s[0], wk = 0xffffffffu;
-        if ((tid & ~63) < m) {
-          const uint32_t wv = wp[t + lane];
+        // up to kFast batches between compactions (a slot's list neighbours, used by the wrap
+        // log, change only at a compaction)
+        for (int fb = 0; fb < kFast && T - t >= 64; ++fb) {
+          // (waves holding only empty slots skip the batch: sentinels stay sentinels)
+          uint32_t sv = s[0], wk = 0xffffffffu;
+          if ((tid & ~63) < m) {
+            uint32_t wsg[64];  // wave-uniform words: scalar loads into SGPRs
+            const uint32_t *__restrict__ wq = wp + t;
 #pragma unroll
-          for (int k = 0; k < 64; ++k) {
-            const uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wv), k));
-            sv -= masked(w, sv) <= sv ? 1u : 0u;
-            const bool z = sv == 0;
-            sv = z ? N1 : sv;
-            wk = z ? static_cast<uint32_t>(k) : wk;
+            for (int k = 0; k < 64; ++k) wsg[k] = wq[k];
+#pragma unroll
+            for (int k = 0; k < 64; ++k) {
+              const uint32_t w = wsg[k];
+              sv -= masked(w, sv) <= sv ? 1u : 0u;
+              const bool z = sv == 0;
+              sv = z ? N1 : sv;
+              wk = z ? static_cast<uint32_t>(k) : wk;
+            }
           }
-        }
-        s[0] = sv;
-        const uint64_t wr = __ballot(wk != 0xffffffffu);
-        if (wr) {
-          int base = 0;
-          if (lane == 0) base = atomicAdd(&sh_evn, __popcll(wr));
-          base = __shfl(base, 0);
-          if (wk != 0xffffffffu) {
-            const int e = base + static_cast<int>(lane_rank(wr));
-            if (e < a.ecap)
-              ev[e] = make_uint2(static_cast<uint32_t>(t) + wk + 1u,
-                                 lo[tid] | (static_cast<uint32_t>(lo[tid + 1 == m ? 0 : tid + 1]) << 16));
+          s[0] = sv;
+          const uint64_t wr = __ballot(wk != 0xffffffffu);
+          if (wr) {
+            int base = 0;
+            if (lane == 0) base = atomicAdd(&sh_evn, __popcll(wr));
+            base = __shfl(base, 0);
+            if (wk != 0xffffffffu) {
+              const int e = base + static_cast<int>(lane_rank(wr));
+              if (e < a.ecap)
+                ev[e] = make_uint2(static_cast<uint32_t>(t) + wk + 1u,
+                                   lo[tid] | (static_cast<uint32_t>(lo[tid + 1 == m ? 0 : tid + 1]) << 16));
+            }
           }
+          t += 64;
         }
-        t += kk;
       } else {
       if (tid < kk) wbuf[tid] = wp[t + tid];
       __syncthreads();
@@ -385,14 +394,14 @@ __device__ __forceinline__ void sparse_step(uint32_t w, uint32_t &sv) {
   sv -= masked(w, sv) <= sv ? 1u : 0u;
 }
 
-__global__ __launch_bounds__(64) void k_np_sparse(EntryArgs a) {
+__global__ __launch_bounds__(64) void k_np_sparse(EntryArgs a, const uint32_t *__restrict__ draws) {
   const int c = blockIdx.x, l = threadIdx.x;
   int m = a.fin_m[c];
   if (m > 64) return;  // the chunk ended while dense: final already
   const int n1 = a.n1;
   const int64_t t0 = static_cast<int64_t>(c) * a.W;
   const int T = static_cast<int>(std::min<int64_t>(a.W, a.D - t0));
-  const uint32_t *wp = a.draws + t0;
+  const uint32_t *__restrict__ wp = draws + t0;
   uint2 *ev = a.ev + static_cast<size_t>(c) * a.ecap;
   const uint32_t N1 = static_cast<uint32_t>(n1);
   int t = a.tpos[c];
@@ -402,14 +411,18 @@ __global__ __launch_bounds__(64) void k_np_sparse(EntryArgs a) {
   int ecnt = a.ev_n[c];
   while (t < T) {
     const int kk = min(64, T - t);
-    const uint32_t wv = l < kk ? wp[t + l] : 0u;
     if (kk == 64 && n1 >= 64) {
       // a lane wraps at most once in 64 draws (a hypothesis takes >= n1 >= 64): branch-free
-      // steps, the wrap draw kept per lane and logged after the batch
+      // steps, the wrap draw kept per lane and logged after the batch; the 64 words are
+      // wave-uniform, so they arrive by scalar loads straight into SGPRs
       uint32_t wk = 0xffffffffu;
+      uint32_t wsg[64];
+      const uint32_t *__restrict__ wq = wp + t;
+#pragma unroll
+      for (int k = 0; k < 64; ++k) wsg[k] = wq[k];
 #pragma unroll
       for (int k = 0; k < 64; ++k) {
-        const uint32_t w = __builtin_amdgcn_readlane(wv, k);
+        const uint32_t w = wsg[k];
         sparse_step(w, sv);
         const bool z = sv == 0;
         sv = z ? N1 : sv;
@@ -425,6 +438,7 @@ __global__ __launch_bounds__(64) void k_np_sparse(EntryArgs a) {
         ecnt += __popcll(wr);
       }
     } else {
+      const uint32_t wv = l < kk ? wp[t + l] : 0u;
       for (int k = 0; k < kk; ++k) {
         const uint32_t w = __builtin_amdgcn_readlane(wv, k);
         sparse_step(w, sv);
@@ -818,9 +832,9 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
     HIP_TRY(hipMemsetAsync(w.d_err, 0, sizeof(int), s));
     EntryArgs ea{w.d_stream + *pos, D, kWr, n1, w.d_fin, w.d_fin_m, w.d_ev, w.d_ev_n, w.d_tpos,
                  ecap, w.d_err};
-    k_np_entry<<<C, kEntryThreads, static_cast<size_t>(lds), s>>>(ea);
+    k_np_entry<<<C, kEntryThreads, static_cast<size_t>(lds), s>>>(ea, ea.draws);
     HIP_TRY(hipGetLastError());
-    k_np_sparse<<<C, 64, 0, s>>>(ea);
+    k_np_sparse<<<C, 64, 0, s>>>(ea, ea.draws);
     HIP_TRY(hipGetLastError());
     fin_m.resize(C);
     ev_n.resize(C);
