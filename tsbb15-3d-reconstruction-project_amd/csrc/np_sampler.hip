@@ -56,7 +56,7 @@ constexpr uint32_t kLower = 0x7fffffffu;
 constexpr uint32_t kMatA = 0x9908b0dfu;
 constexpr int kDeg = 19937;
 constexpr int kPrefix = kDeg + kN - 1;       // words of a window's sequence a jump reads
-constexpr int kJB = 1024;                    // stream blocks per generator
+constexpr int kJB = 512;                     // stream blocks per generator
 constexpr int64_t kJ = int64_t(kN) * kJB;    // words per generator
 constexpr int kLevels = 11;                  // jump tree depth: up to 2048 generators
 constexpr int64_t kSegWords = int64_t(1) << 29;  // stream words per segment (2 GiB)
