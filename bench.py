@@ -226,6 +226,20 @@ def extras(ctx, rank, world, dist, comm):
         out["c5_stress"] = {"metric": "RANSAC hypotheses/s (8-pt F, 10k corr, 60% outliers)",
                             "value": H5 / el, "ms": el * 1e3, "best_count": int(r.best_count),
                             "guard_mismatch": int(r.guard_mismatch)}
+        if rank == 0:
+            # the same pair in parity mode: np.random.seed(0), 1e6 numpy-exact choice tuples
+            # sampled on the GPU, then the same pipeline (one timed run after a 1e5 warm-up)
+            key0, pos0 = _ffi.np_seed(0)
+            plan.run_np(100_000, key0, pos0)
+            plan.result()
+            t = time.perf_counter()
+            plan.run_np(H5, key0, pos0)
+            rp, _ = plan.result()
+            el = time.perf_counter() - t
+            out["c5_parity"] = {"metric": "RANSAC hypotheses/s, parity mode (numpy-exact stream)",
+                                "value": H5 / el, "ms": el * 1e3,
+                                "best_index": int(rp.best_index),
+                                "best_count": int(rp.best_count)}
         plan.close()
     except Exception as e:  # noqa: BLE001
         out["c5_stress"] = {"error": repr(e)}
@@ -247,7 +261,7 @@ def extras(ctx, rank, world, dist, comm):
         el, _ = _best_of(getf, 3)
         out["getFFromLabCode_dino_noisy"] = {
             "ms": el * 1e3, "n_corr": int(c1["noisy_p1"].shape[1]), "iterations": 10_000,
-            "note": "drop-in end to end: numpy-exact sampling on the host, GPU RANSAC, GPU gold "
+            "note": "drop-in end to end: numpy-exact sampling on the GPU, GPU RANSAC, GPU gold "
                     "standard; the reference took {:.1f} s for the same call in the build "
                     "container (tests/golden/dino_c1.npz noisy_full_seconds)".format(
                         float(c1["noisy_full_seconds"]))}

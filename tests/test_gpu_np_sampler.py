@@ -98,12 +98,14 @@ def test_gpu_stream_many_segments(knobs):
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
 
 
-@pytest.mark.parametrize("n,H,seed", [(2000, 100000, 0), (257, 10000, 3), (10240, 2000, 7)])
-def test_plan_run_np_equals_host_tuple_run(ctx, n, H, seed):
+@pytest.mark.parametrize("n,H,seed,out", [(2000, 100000, 0, 0.3), (257, 10000, 3, 0.3),
+                                          (10240, 2000, 7, 0.3), (10000, 100000, 5, 0.6)])
+def test_plan_run_np_equals_host_tuple_run(ctx, n, H, seed, out):
     """rs_f8_plan_run_np (tuples parsed on the GPU into the run's buffer) = the same plan fed the
-    host replay's tuples: winner, S_RANSAC, F bits and the advanced stream state."""
+    host replay's tuples: winner, S_RANSAC, F bits and the advanced stream state.  C2 at full
+    size, and C5's pair (N = 10 000, 60 % outliers) with 1e5 of its 1e6 hypotheses."""
     from tsbb15_amd import synth
-    p1, p2, _ = synth.two_view(n, 0.3, seed=seed + 1)
+    p1, p2, _ = synth.two_view(n, out, seed=seed + 1)
     key, pos = _state(seed)
     plan = _ffi.F8Plan(ctx, n, H)
     try:
