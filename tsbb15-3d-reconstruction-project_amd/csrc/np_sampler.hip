@@ -67,6 +67,7 @@ constexpr int kR = 20;                       // slots per thread: N - 1 <= 10240
 constexpr int kMaxN1 = kEntryThreads * kR;
 constexpr int kK = 64;                       // draws between compactions (<= N - 1 when dense)
 constexpr int kFast = 4;                     // one-slot-per-thread batches between compactions
+constexpr int kRFast = 4;                    // slots per thread of the branch-free multi-slot path
 constexpr uint32_t kSentinel = 0x80000000u;  // an empty slot: never reaches 0 within kW steps
 
 __device__ __forceinline__ uint32_t twist(uint32_t a, uint32_t b) {
@@ -282,6 +283,45 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a,
           }
           t += 64;
         }
+      } else if (kk == 64 && nr <= kRFast) {
+        // several slots per thread: the word from LDS, branch-free steps, each slot's wrap (at
+        // most one in 64 draws, as n1 > 64) logged after the batch
+        if (tid < kk) wbuf[tid] = wp[t + tid];
+        __syncthreads();
+        uint32_t wk[kRFast];
+#pragma unroll
+        for (int r = 0; r < kRFast; ++r) wk[r] = 0xffffffffu;
+#pragma unroll 1
+        for (int k = 0; k < 64; ++k) {
+          const uint32_t w = wbuf[k];
+#pragma unroll
+          for (int r = 0; r < kRFast; ++r) {
+            if (r >= nr) break;
+            uint32_t sv = s[r];
+            sv -= masked(w, sv) <= sv ? 1u : 0u;
+            const bool z = sv == 0;
+            s[r] = z ? N1 : sv;
+            wk[r] = z ? static_cast<uint32_t>(k) : wk[r];
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < kRFast; ++r) {
+          if (r >= nr) break;
+          const uint64_t wr = __ballot(wk[r] != 0xffffffffu);
+          if (wr) {
+            int base = 0;
+            if (lane == 0) base = atomicAdd(&sh_evn, __popcll(wr));
+            base = __shfl(base, 0);
+            if (wk[r] != 0xffffffffu) {
+              const int q = tid + r * kEntryThreads;
+              const int e = base + static_cast<int>(lane_rank(wr));
+              if (e < a.ecap)
+                ev[e] = make_uint2(static_cast<uint32_t>(t) + wk[r] + 1u,
+                                   lo[q] | (static_cast<uint32_t>(lo[q + 1 == m ? 0 : q + 1]) << 16));
+            }
+          }
+        }
+        t += 64;
       } else {
       if (tid < kk) wbuf[tid] = wp[t + tid];
       __syncthreads();
