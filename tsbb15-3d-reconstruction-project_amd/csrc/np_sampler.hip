@@ -67,7 +67,7 @@ constexpr int kR = 20;                       // slots per thread: N - 1 <= 10240
 constexpr int kMaxN1 = kEntryThreads * kR;
 constexpr int kK = 64;                       // draws between compactions (<= N - 1 when dense)
 constexpr int kFast = 4;                     // one-slot-per-thread batches between compactions
-constexpr int kRFast = 4;                    // slots per thread of the branch-free multi-slot path
+constexpr int kRFast = 8;                    // slots per thread of the branch-free multi-slot path
 constexpr uint32_t kSentinel = 0x80000000u;  // an empty slot: never reaches 0 within kW steps
 
 __device__ __forceinline__ uint32_t twist(uint32_t a, uint32_t b) {
@@ -893,20 +893,21 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
     // 4: compose the chunk maps; entry list index a <-> state n1 - a; chunk 0 starts a hypothesis
     ent.resize(C);
     // chunks that ended dense (m > 64): their full lists in one copy of the row range
-    int cb0 = C, cb1 = -1;
+    int cb0 = C, cb1 = -1, mb = 0;
     for (int ci = 0; ci < C; ++ci)
-      if (fin_m[ci] > 64) cb0 = std::min(cb0, ci), cb1 = ci;
+      if (fin_m[ci] > 64) cb0 = std::min(cb0, ci), cb1 = ci, mb = std::max(mb, fin_m[ci]);
     std::vector<uint32_t> big;
-    if (cb1 >= cb0) {
-      big.resize(static_cast<size_t>(cb1 - cb0 + 1) * n1);
-      HIP_TRY(hipMemcpy(big.data(), w.d_fin + static_cast<size_t>(cb0) * n1,
-                        sizeof(uint32_t) * big.size(), hipMemcpyDeviceToHost));
+    if (cb1 >= cb0) {  // the first mb entries of each row in the range (rows are n1 long)
+      big.resize(static_cast<size_t>(cb1 - cb0 + 1) * mb);
+      HIP_TRY(hipMemcpy2D(big.data(), sizeof(uint32_t) * mb, w.d_fin + static_cast<size_t>(cb0) * n1,
+                          sizeof(uint32_t) * n1, sizeof(uint32_t) * mb, cb1 - cb0 + 1,
+                          hipMemcpyDeviceToHost));
     }
     int a = 0;
     for (int ci = 0; ci < C; ++ci) {
       ent[ci] = a;
       const int m = fin_m[ci];
-      const uint32_t *f = m > 64 ? big.data() + static_cast<size_t>(ci - cb0) * n1
+      const uint32_t *f = m > 64 ? big.data() + static_cast<size_t>(ci - cb0) * mb
                                  : fin.data() + static_cast<size_t>(ci) * 64;
       int best = -1, bst = 0, top = -1, tst = 0;
       for (int i = 0; i < m; ++i) {
