@@ -60,7 +60,8 @@ constexpr int kJB = 512;                     // stream blocks per generator
 constexpr int64_t kJ = int64_t(kN) * kJB;    // words per generator
 constexpr int kLevels = 11;                  // jump tree depth: up to 2048 generators
 constexpr int64_t kSegWords = int64_t(1) << 29;  // stream words per segment (2 GiB)
-constexpr int kW = 262144;                   // longest parse chunk (draws)
+constexpr int kW = 262144;                   // longest automatic parse chunk (draws)
+constexpr int kWmax = 1 << 20;               // longest chunk (RSAMD_NP_KW)
 constexpr int kWmin = 8192;                  // shortest parse chunk
 constexpr int kEntryThreads = 512;
 constexpr int kR = 20;                       // slots per thread: N - 1 <= 10240
@@ -798,7 +799,7 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
   static const int kWenv = [] {
     const char *e = std::getenv("RSAMD_NP_KW");
     const int v = e ? std::atoi(e) : 0;
-    return v >= kWmin && v <= kW ? v : 0;
+    return v >= kWmin && v <= kWmax ? v : 0;
   }();
   const int64_t Cmax = kSegWords / kWmin + 1;
   // RSAMD_NP_LANE_TUPLES=1: the lane-per-hypothesis tuple kernel with swap partners in HBM (A/B)
