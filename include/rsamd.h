@@ -85,6 +85,13 @@ int rs_ctx_synchronize(rs_ctx *ctx);
 int rs_np_choice_tuples_gpu(rs_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int64_t n, int32_t k,
                             int64_t count, int32_t *out);
 
+/* The same stream as rs_py_shuffle_tuples (ransac.gen_rnd_indices, ransac.py:12-19: CPython
+ * random.shuffle with getrandbits rejection), k <= 8, n - 1 <= 10240, computed on the GPU by
+ * the same pipeline with CPython's draw rule (w >> (32 - bit_length(i + 1)) <= i).  Same
+ * output and (key, pos) advance, bit for bit; out is host memory (count, k) int32. */
+int rs_py_shuffle_tuples_gpu(rs_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int64_t n,
+                             int32_t k, int64_t count, int32_t *out);
+
 /* ------------------------------------------------------------------------------------------
  * lab3 primitives on the GPU
  * ---------------------------------------------------------------------------------------- */

@@ -121,3 +121,64 @@ def test_plan_run_np_equals_host_tuple_run(ctx, n, H, seed, out):
     assert g[0].best_index == h[0].best_index and g[0].best_count == h[0].best_count
     assert np.array_equal(g[1], h[1])
     assert np.array_equal(np.array(g[0].F[:]), np.array(h[0].F[:]))
+
+
+# ---- the CPython stream (ransac.gen_rnd_indices: random.shuffle, getrandbits rejection) ----
+def _py_state(seed, skip=0):
+    import random
+    r = random.Random(seed)
+    for _ in range(skip):
+        r.getrandbits(32)
+    st = r.getstate()[1]
+    return np.asarray(st[:624], np.uint32), int(st[624])
+
+
+@pytest.mark.parametrize("n,k,count,skip", [(2, 1, 5000, 0), (6, 6, 20000, 0), (9, 6, 5000, 7),
+                                            (37, 6, 20000, 0), (65, 3, 3000, 623),
+                                            (500, 6, 50000, 0), (2000, 8, 3000, 1),
+                                            (4097, 6, 300, 0), (10241, 6, 100, 0)])
+def test_gpu_py_stream_matches_host_replay(ctx, n, k, count, skip):
+    key, pos = _py_state(n + skip, skip)
+    ref, rkey, rpos = _ffi.py_shuffle_tuples(key, pos, n, k, count)
+    got, gkey, gpos = _ffi.py_shuffle_tuples_gpu(key, pos, n, k, count)
+    bad = np.flatnonzero((got != ref).any(axis=1))
+    assert bad.size == 0, f"first mismatching hypothesis {bad[:5]}"
+    assert gpos == rpos and np.array_equal(gkey, rkey)
+
+
+def test_gpu_py_stream_reference_goldens_and_errors(ctx):
+    import json
+    with open(os.path.join(REPO, "tests", "golden", "ransac_misc.json")) as f:
+        misc = json.load(f)
+    key, pos = _ffi.py_seed(0)
+    tup, _, _ = _ffi.py_shuffle_tuples_gpu(key, pos, 500, 6, 50)
+    assert tup.tolist() == misc["gen_rnd_indices_seed0_500_6"]
+    key, pos = _ffi.py_seed(12345)
+    tup, _, _ = _ffi.py_shuffle_tuples_gpu(key, pos, 37, 6, 50)
+    assert tup.tolist() == misc["gen_rnd_indices_seed12345_37_6"]
+    with pytest.raises(ValueError, match="Cannot generate more indices"):
+        _ffi.py_shuffle_tuples_gpu(key, pos, 5, 6, 1)
+    tup, k2, p2 = _ffi.py_shuffle_tuples_gpu(key, pos, 1, 1, 10)  # draws nothing
+    assert not tup.any() and p2 == pos and np.array_equal(k2, key)
+
+
+def test_gen_rnd_tuples_gpu_route_equals_cpython(ctx):
+    """ransac.gen_rnd_tuples at C3's size (500 points, 6-point DLT, 5e4 trials) takes the GPU
+    stream; the tuples and the advanced global random state equal CPython's own shuffles
+    replayed on the host."""
+    import random
+    from tsbb15_amd import ransac
+    random.seed(3)
+    st0 = random.getstate()
+    tup = ransac.gen_rnd_tuples(500, 6, 50000)
+    st1 = random.getstate()
+    random.setstate(st0)
+    key, pos = np.asarray(st0[1][:624], np.uint32), int(st0[1][624])
+    ref, rkey, rpos = _ffi.py_shuffle_tuples(key, pos, 500, 6, 50000)
+    assert np.array_equal(tup, ref)
+    assert st1[1][624] == rpos and np.array_equal(np.asarray(st1[1][:624], np.uint32), rkey)
+    x = list(range(500))  # the next CPython shuffle continues from the advanced state
+    random.setstate(st1)
+    random.shuffle(x)
+    random.setstate(st1)
+    assert ransac.gen_rnd_indices(500, 6) == x[:6]

@@ -25,6 +25,6 @@ int ensure_scratch(rs_ctx *c, size_t bytes);
 void np_work_free(rs_ctx *c);
 bool np_gpu_supported(int64_t n, int32_t k);  // within the GPU parse's population range
 int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t k,
-                     int64_t count, int32_t *d_out);
+                     int64_t count, int32_t *d_out, bool py = false);
 int fmatrix_stls_lsq(rs_ctx *c, const double *pl, const double *pr, int64_t n, double *F_out);
 }  // namespace rs

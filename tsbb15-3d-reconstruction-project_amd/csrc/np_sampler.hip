@@ -86,6 +86,15 @@ __device__ __forceinline__ uint32_t temper(uint32_t y) {
 __device__ __forceinline__ uint32_t masked(uint32_t w, uint32_t i) {
   return w & (0xffffffffu >> __builtin_clz(i));
 }
+// The draw of state i under either stream's rule; the step accepts iff draw <= i.
+//   numpy (PY = false): random_interval(i) = w & mask(i)                       (fun.py:305)
+//   CPython (PY = true): randbelow(i + 1) = getrandbits(bit_length(i + 1)) = w >> clz(i + 1)
+//                        (random.shuffle behind ransac.gen_rnd_indices, ransac.py:12-19)
+template <bool PY>
+__device__ __forceinline__ uint32_t draw_of(uint32_t w, uint32_t i) {
+  if constexpr (PY) return w >> __builtin_clz(i + 1u);
+  else return masked(w, i);
+}
 
 // ---- 1. jump tree level: window[g + half] = x^(half J) applied to window[g] ----------------
 // y_t = y_{t-227} ^ twist(y_{t-624}, y_{t-623}); word w of the jumped window is the XOR of
@@ -213,6 +222,7 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t bits) {
                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bits), 0u));
 }
 
+template <bool PY>
 __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a,
                                                              const uint32_t *__restrict__ draws) {
   extern __shared__ uint16_t dyn[];
@@ -263,7 +273,7 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a,
 #pragma unroll
             for (int k = 0; k < 64; ++k) {
               const uint32_t w = wsg[k];
-              sv -= masked(w, sv) <= sv ? 1u : 0u;
+              sv -= draw_of<PY>(w, sv) <= sv ? 1u : 0u;
               const bool z = sv == 0;
               sv = z ? N1 : sv;
               wk = z ? static_cast<uint32_t>(k) : wk;
@@ -299,7 +309,7 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a,
           for (int r = 0; r < kRFast; ++r) {
             if (r >= nr) break;
             uint32_t sv = s[r];
-            sv -= masked(w, sv) <= sv ? 1u : 0u;
+            sv -= draw_of<PY>(w, sv) <= sv ? 1u : 0u;
             const bool z = sv == 0;
             s[r] = z ? N1 : sv;
             wk[r] = z ? static_cast<uint32_t>(k) : wk[r];
@@ -332,7 +342,7 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a,
         for (int r = 0; r < kR; ++r) {
           if (r >= nr) break;
           uint32_t sv = s[r];
-          sv -= masked(w, sv) <= sv ? 1u : 0u;
+          sv -= draw_of<PY>(w, sv) <= sv ? 1u : 0u;
           if (sv == 0) {  // hypothesis end: log the wrap with this trajectory's member range
             sv = N1;
             const int q = tid + r * kEntryThreads;
@@ -431,10 +441,12 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a,
 // ---- 3b. sparse phase of a chunk: one wave, lane l = slot l ---------------------------------
 // A separate 64-thread launch so that the long serial tail of every chunk runs at full
 // occupancy (inside the 512-thread dense workgroup it held a CU slot with one wave).
+template <bool PY>
 __device__ __forceinline__ void sparse_step(uint32_t w, uint32_t &sv) {
-  sv -= masked(w, sv) <= sv ? 1u : 0u;
+  sv -= draw_of<PY>(w, sv) <= sv ? 1u : 0u;
 }
 
+template <bool PY>
 __global__ __launch_bounds__(64) void k_np_sparse(EntryArgs a, const uint32_t *__restrict__ draws) {
   const int c = blockIdx.x, l = threadIdx.x;
   int m = a.fin_m[c];
@@ -464,7 +476,7 @@ __global__ __launch_bounds__(64) void k_np_sparse(EntryArgs a, const uint32_t *_
 #pragma unroll
       for (int k = 0; k < 64; ++k) {
         const uint32_t w = wsg[k];
-        sparse_step(w, sv);
+        sparse_step<PY>(w, sv);
         const bool z = sv == 0;
         sv = z ? N1 : sv;
         wk = z ? static_cast<uint32_t>(k) : wk;
@@ -482,7 +494,7 @@ __global__ __launch_bounds__(64) void k_np_sparse(EntryArgs a, const uint32_t *_
       const uint32_t wv = l < kk ? wp[t + l] : 0u;
       for (int k = 0; k < kk; ++k) {
         const uint32_t w = __builtin_amdgcn_readlane(wv, k);
-        sparse_step(w, sv);
+        sparse_step<PY>(w, sv);
         const uint64_t wr = __ballot(sv == 0);
         if (wr) {
           const uint32_t succ = __shfl(lov, l + 1 == m ? 0 : l + 1);
@@ -608,6 +620,7 @@ __global__ __launch_bounds__(256) void k_np_tuples(const uint32_t *__restrict__ 
 // trace keeps the k positions in wave-uniform registers: for state s >= 8 a position p < s can
 // only move to s (when J[s - 1] == p), found by a ballot over 64 states at a time.
 constexpr int kTupWaves = 4;
+template <bool PY>
 __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
     const uint32_t *__restrict__ draws, const int64_t *__restrict__ starts, int64_t H, int n1,
     int n1p, int kk, int32_t *__restrict__ out, int *err) {
@@ -621,11 +634,18 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
   uint32_t i = static_cast<uint32_t>(n1);
   int64_t d = a;
   while (i > 0) {
-    const uint32_t msk = 0xffffffffu >> __builtin_clz(i);
-    const uint32_t L = i - (msk >> 1);
+    // states i .. i - L + 1 share the draw rule's mask / shift
+    uint32_t L, msk = 0, sh = 0;
+    if constexpr (PY) {
+      sh = static_cast<uint32_t>(__builtin_clz(i + 1u));
+      L = i + 2u - (1u << (31u - sh));
+    } else {
+      msk = 0xffffffffu >> __builtin_clz(i);
+      L = i - (msk >> 1);
+    }
     const int W = L < 64u ? static_cast<int>(L) : 64;
     const bool in = l < W;
-    const uint32_t u = in ? (draws[d + l] & msk) : 0xffffffffu;
+    const uint32_t u = in ? (PY ? (draws[d + l] >> sh) : (draws[d + l] & msk)) : 0xffffffffu;
     const uint32_t lo_s = i - static_cast<uint32_t>(l);
     uint64_t acc = __ballot(in && u <= lo_s);
     uint64_t amb = __ballot(in && u > lo_s && u <= i);
@@ -721,10 +741,10 @@ int64_t seg_words() {
   return v;
 }
 
-double expected_draws(int64_t n1) {
+double expected_draws(int64_t n1, bool py) {
   double e = 0.0;
   for (int64_t i = 1; i <= n1; ++i) {
-    uint64_t m = static_cast<uint64_t>(i);
+    uint64_t m = static_cast<uint64_t>(py ? i + 1 : i);  // CPython: 2^bit_length(i + 1) - 1
     m |= m >> 1;
     m |= m >> 2;
     m |= m >> 4;
@@ -781,14 +801,23 @@ bool np_gpu_supported(int64_t n, int32_t k) { return k >= 1 && k <= 8 && k <= n 
 // The numpy stream's next `count` choice(n, k) tuples into device memory (count * k int32),
 // on the context stream; advances (key, pos).  Synchronous.
 int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t k,
-                     int64_t count, int32_t *d_out) {
+                     int64_t count, int32_t *d_out, bool py) {
   if (k < 1 || k > 8) return fail(RS_EINVAL, "np sampler: k must be in 1..8");
-  if (k > n) return fail(RS_EINVAL, "Cannot take a larger sample than population when 'replace=False'");
+  if (k > n)
+    return fail(RS_EINVAL, py ? "Cannot generate more indices than the amount of values in the set "
+                                "from which they are extracted. n should therefore be smaller or "
+                                "equal to set_length"
+                              : "Cannot take a larger sample than population when 'replace=False'");
   if (n - 1 > kMaxN1) return fail(RS_EINVAL, "np sampler: population too large for the GPU parse");
   if (*pos < 0 || *pos > kN) return fail(RS_EINVAL, "bad MT19937 position");
   if (count == 0) return RS_OK;
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = c->stream;
+  if (n <= 1) {  // a one-element shuffle draws nothing: every tuple is (0)
+    HIP_TRY(hipMemsetAsync(d_out, 0, sizeof(int32_t) * static_cast<size_t>(count) * k, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return RS_OK;
+  }
   if (!c->np_work) c->np_work = new rs_np_work();
   rs_np_work &w = *c->np_work;
   int st;
@@ -806,7 +835,9 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
   static const bool lane_tuples = std::getenv("RSAMD_NP_LANE_TUPLES") != nullptr;
   const int64_t tup_lds = static_cast<int64_t>(sizeof(uint16_t)) * ((n1 + 1) & ~1) * kTupWaves;
   if (!lane_tuples && tup_lds > w.tup_lds) {
-    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_np_tuples_wave),
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_np_tuples_wave<false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(tup_lds)));
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_np_tuples_wave<true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(tup_lds)));
     w.tup_lds = tup_lds;
   }
@@ -829,13 +860,15 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
         (st = grow(w.d_tpos, c9, Cmax)))
       return st;
   }
-  const double E = expected_draws(n1);
+  const double E = expected_draws(n1, py);
   const int64_t dmax = seg_words() - 3 * kN;
   const int64_t hcap = std::max<int64_t>(1, static_cast<int64_t>((dmax - 16 * n) / (E * 1.03)));
   int ecap_shift = 0;  // wrap-log doublings after an overflow
   const int64_t lds = 8 * static_cast<int64_t>((n1 + 1) & ~1);
   if (lds > w.entry_lds) {
-    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_np_entry),
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_np_entry<false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_np_entry<true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
     w.entry_lds = lds;
   }
@@ -858,7 +891,7 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
     const int G = static_cast<int>((Lb + kJB - 1) / kJB);
     if ((st = grow(w.d_ev, w.cap_ev, static_cast<int64_t>(C) * ecap)) ||
         (st = grow(w.d_starts, w.cap_starts, hs + 1)) ||
-        (lane_tuples && (st = grow(w.d_J, w.cap_J, hs * n1))))
+        (lane_tuples && !py && (st = grow(w.d_J, w.cap_J, hs * n1))))
       return st;
     // 1-2: the word stream from (key, pos): block 0 is the key itself
     HIP_TRY(hipMemcpyAsync(w.d_win, key, sizeof(uint32_t) * kN, hipMemcpyHostToDevice, s));
@@ -873,9 +906,15 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
     HIP_TRY(hipMemsetAsync(w.d_err, 0, sizeof(int), s));
     EntryArgs ea{w.d_stream + *pos, D, kWr, n1, w.d_fin, w.d_fin_m, w.d_ev, w.d_ev_n, w.d_tpos,
                  ecap, w.d_err};
-    k_np_entry<<<C, kEntryThreads, static_cast<size_t>(lds), s>>>(ea, ea.draws);
-    HIP_TRY(hipGetLastError());
-    k_np_sparse<<<C, 64, 0, s>>>(ea, ea.draws);
+    if (py) {
+      k_np_entry<true><<<C, kEntryThreads, static_cast<size_t>(lds), s>>>(ea, ea.draws);
+      HIP_TRY(hipGetLastError());
+      k_np_sparse<true><<<C, 64, 0, s>>>(ea, ea.draws);
+    } else {
+      k_np_entry<false><<<C, kEntryThreads, static_cast<size_t>(lds), s>>>(ea, ea.draws);
+      HIP_TRY(hipGetLastError());
+      k_np_sparse<false><<<C, 64, 0, s>>>(ea, ea.draws);
+    }
     HIP_TRY(hipGetLastError());
     fin_m.resize(C);
     ev_n.resize(C);
@@ -937,12 +976,12 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
     k_np_starts<<<C, 256, 0, s>>>(w.d_ev, w.d_vcnt, w.d_off, w.d_starts, got, ecap, kWr);
     HIP_TRY(hipGetLastError());
     // 6: tuples
-    if (lane_tuples) {
+    if (lane_tuples && !py) {
       k_np_tuples<<<static_cast<unsigned>((got + 255) / 256), 256, 0, s>>>(
           w.d_stream + *pos, w.d_starts, got, n1, k, w.d_J, d_out + done * k, w.d_err);
     } else {
       const int n1p = (n1 + 1) & ~1;
-      k_np_tuples_wave<<<static_cast<unsigned>((got + kTupWaves - 1) / kTupWaves), 64 * kTupWaves,
+      (py ? k_np_tuples_wave<true> : k_np_tuples_wave<false>)<<<static_cast<unsigned>((got + kTupWaves - 1) / kTupWaves), 64 * kTupWaves,
                          sizeof(uint16_t) * n1p * kTupWaves, s>>>(
           w.d_stream + *pos, w.d_starts, got, n1, n1p, k, d_out + done * k, w.d_err);
     }
@@ -970,10 +1009,12 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
 
 }  // namespace rs
 
-extern "C" int rs_np_choice_tuples_gpu(rs_ctx *c, uint32_t *mt_key, int32_t *mt_pos, int64_t n,
-                                       int32_t k, int64_t count, int32_t *out) {
+namespace {
+// Tuples of either stream into host memory through the context's scratch buffer.
+int choice_tuples_gpu(rs_ctx *c, uint32_t *mt_key, int32_t *mt_pos, int64_t n, int32_t k,
+                      int64_t count, int32_t *out, bool py) {
   if (!c || !mt_key || !mt_pos || (count > 0 && !out))
-    return rs::fail(RS_EINVAL, "rs_np_choice_tuples_gpu: null pointer");
+    return rs::fail(RS_EINVAL, "tuples_gpu: null pointer");
   if (count < 0 || k < 0) return rs::fail(RS_EINVAL, "negative dimensions are not allowed");
   if (count == 0) return RS_OK;
   int st;
@@ -981,11 +1022,23 @@ extern "C" int rs_np_choice_tuples_gpu(rs_ctx *c, uint32_t *mt_key, int32_t *mt_
   uint32_t key[kN];
   int32_t pos = *mt_pos;
   std::memcpy(key, mt_key, sizeof(key));
-  if ((st = rs::np_choice_device(c, key, &pos, n, k, count, static_cast<int32_t *>(c->scratch))))
+  if ((st = rs::np_choice_device(c, key, &pos, n, k, count, static_cast<int32_t *>(c->scratch),
+                                 py)))
     return st;
   HIP_TRY(hipMemcpy(out, c->scratch, sizeof(int32_t) * static_cast<size_t>(count) * k,
                     hipMemcpyDeviceToHost));
   std::memcpy(mt_key, key, sizeof(key));
   *mt_pos = pos;
   return RS_OK;
+}
+}  // namespace
+
+extern "C" int rs_np_choice_tuples_gpu(rs_ctx *c, uint32_t *mt_key, int32_t *mt_pos, int64_t n,
+                                       int32_t k, int64_t count, int32_t *out) {
+  return choice_tuples_gpu(c, mt_key, mt_pos, n, k, count, out, false);
+}
+
+extern "C" int rs_py_shuffle_tuples_gpu(rs_ctx *c, uint32_t *mt_key, int32_t *mt_pos, int64_t n,
+                                        int32_t k, int64_t count, int32_t *out) {
+  return choice_tuples_gpu(c, mt_key, mt_pos, n, k, count, out, true);
 }

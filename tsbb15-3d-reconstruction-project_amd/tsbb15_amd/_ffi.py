@@ -66,6 +66,8 @@ _SIGS = {
                                           C.c_int64, _i32p]),
     "rs_py_seed": (C.c_int, [_u32p, C.c_int32, _u32p, _i32p]),
     "rs_py_shuffle_tuples": (C.c_int, [_u32p, _i32p, C.c_int64, C.c_int32, C.c_int64, _i32p]),
+    "rs_py_shuffle_tuples_gpu": (C.c_int, [C.c_void_p, _u32p, _i32p, C.c_int64, C.c_int32,
+                                           C.c_int64, _i32p]),
     "rs_mt_jump": (C.c_int, [_u32p, C.c_int32, C.c_int64, _u32p, _i32p]),
     "rs_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "rs_ctx_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
@@ -253,6 +255,20 @@ def py_shuffle_tuples(key, pos, n, k, count):
     out = np.empty((int(count), int(k)), dtype=np.int32)
     check(lib().rs_py_shuffle_tuples(ptr(key, C.c_uint32), C.byref(p), int(n), int(k),
                                      int(count), ptr(out, C.c_int32)))
+    return out, key, p.value
+
+
+def py_shuffle_tuples_gpu(key, pos, n, k, count, ctx=None):
+    """py_shuffle_tuples computed on the GPU (rs_py_shuffle_tuples_gpu): the same tuples and
+    (key', pos'), bit for bit."""
+    ctx = ctx or default_context()
+    key = np.array(key, dtype=np.uint32, copy=True)
+    if key.shape != (MT_N,):
+        raise ValueError("MT19937 key must have 624 words")
+    p = C.c_int32(int(pos))
+    out = np.empty((int(count), int(k)), dtype=np.int32)
+    check(lib().rs_py_shuffle_tuples_gpu(ctx.handle, ptr(key, C.c_uint32), C.byref(p), int(n),
+                                         int(k), int(count), ptr(out, C.c_int32)))
     return out, key, p.value
 
 

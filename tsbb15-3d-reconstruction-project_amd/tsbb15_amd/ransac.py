@@ -52,10 +52,20 @@ def gen_rnd_indices(set_length, n, rng=None):
     return [int(i) for i in tup[0]]
 
 
+# Streams of at least this many expected draws are parsed on the GPU (np_sampler.hip, CPython
+# rule); shorter ones, where its fixed latency (~2 ms) dominates, are replayed on the host.
+_GPU_MIN_DRAWS = 1 << 22
+
+
 def gen_rnd_tuples(set_length, n, count, rng=None):
     """``count`` consecutive gen_rnd_indices draws as an int32 (count, n) array."""
     st, key, pos = _py_rng_state(rng)
-    tup, key, pos = _ffi.py_shuffle_tuples(key, pos, int(set_length), int(n), int(count))
+    if (0 < n <= 8 and 2 <= set_length <= 10241 and n <= set_length
+            and 1.4 * set_length * count >= _GPU_MIN_DRAWS):
+        tup, key, pos = _ffi.py_shuffle_tuples_gpu(key, pos, int(set_length), int(n),
+                                                   int(count))
+    else:
+        tup, key, pos = _ffi.py_shuffle_tuples(key, pos, int(set_length), int(n), int(count))
     _py_rng_set(rng, st, key, pos)
     return tup
 
