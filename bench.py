@@ -209,6 +209,16 @@ def extras(ctx, rank, world, dist, comm):
         out["c3_pnp"] = {"metric": "PnP-DLT RANSAC hypotheses/s", "value": 50_000 / el,
                          "ms": el * 1e3, "points": 500, "hypotheses": 50_000,
                          "consensus": int(r[5])}
+        import random
+        runp = lambda: ransac.ransac_pnp(X, y, X, y, 50_000, thr, 6, sampler="exact",
+                                         rng=random.Random(0))
+        runp()
+        el, r = _best_of(runp, 5)
+        out["c3_pnp_parity"] = {"metric": "PnP-DLT RANSAC hypotheses/s, parity mode "
+                                          "(random.seed(0) stream of gen_rnd_indices, parsed "
+                                          "on the GPU)",
+                                "value": 50_000 / el, "ms": el * 1e3,
+                                "best_index": int(r[4]), "consensus": int(r[5])}
     except Exception as e:  # noqa: BLE001
         out["c3_pnp"] = {"error": repr(e)}
     # ---- C5: N = 10 000, 60 % outliers, 1e6 hypotheses (throughput mode) ----------------
