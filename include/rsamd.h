@@ -50,6 +50,15 @@ int rs_np_seed(uint32_t seed, uint32_t *mt_key, int32_t *mt_pos);
 int rs_np_choice_tuples(uint32_t *mt_key, int32_t *mt_pos, int64_t n, int32_t k, int64_t count,
                         int32_t *out);
 
+/* B independent numpy streams at once on host threads (config C4: one stream per image pair,
+ * np.random.seed(1000 + pair), then `count` x choice(n_b, k, replace=False)): mt_keys (B, 624),
+ * mt_pos (B) advanced in place (with seeds non-null they are first set to np.random.seed(
+ * seeds[b])), out (B, count, k).  Streams with n_b < k are skipped (zero output, state
+ * unchanged).  threads <= 0: one per hardware thread, at most 16 (threads > 0: at most 64). */
+int rs_np_choice_tuples_multi(int64_t B, const uint32_t *seeds, uint32_t *mt_keys,
+                              int32_t *mt_pos, const int64_t *ns, int32_t k, int64_t count,
+                              int32_t *out, int32_t threads);
+
 /* CPython random.seed(int) with the int given as 32-bit little-endian words
  * (init_by_array) -> key[624], pos = 624. */
 int rs_py_seed(const uint32_t *words, int32_t n_words, uint32_t *mt_key, int32_t *mt_pos);

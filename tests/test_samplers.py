@@ -127,3 +127,25 @@ def test_mt_jump_matches_sequential_draws(seed, pre):
         ref = r.getstate()[1]
         assert pos == ref[624], steps
         assert np.array_equal(key, np.array(ref[:624], np.uint32)), steps
+
+
+def test_np_choice_tuples_multi_equals_single_streams():
+    """Threaded replay of many independent numpy streams (config C4's per-pair seeds) = one
+    rs_np_choice_tuples call per stream, state included; streams with n < k stay zero."""
+    ns = [8, 37, 3, 176, 9, 445, 100, 8]
+    keys = np.empty((len(ns), 624), np.uint32)
+    poss = np.empty(len(ns), np.int32)
+    for b in range(len(ns)):
+        keys[b], poss[b] = _ffi.np_seed(1000 + b)
+    out, k2, p2 = _ffi.np_choice_tuples_multi(keys, poss, ns, 8, 300, threads=3)
+    for b, n in enumerate(ns):
+        if n < 8:
+            assert not out[b].any() and p2[b] == poss[b] and np.array_equal(k2[b], keys[b])
+            continue
+        ref, rk, rp = _ffi.np_choice_tuples(keys[b], poss[b], n, 8, 300)
+        assert np.array_equal(out[b], ref) and rp == p2[b] and np.array_equal(rk, k2[b])
+    o2, k3, p3 = _ffi.np_choice_tuples_multi(None, None, ns, 8, 300, seeds=1000 + np.arange(8))
+    assert np.array_equal(o2, out) and np.array_equal(k3, k2) and np.array_equal(p3, p2)
+    rs = np.random.RandomState(1003)  # and numpy itself, for one stream
+    ref = np.array([rs.choice(np.arange(176), 8, replace=False) for _ in range(300)])
+    assert np.array_equal(out[3], ref)

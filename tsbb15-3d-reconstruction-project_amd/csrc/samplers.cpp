@@ -10,8 +10,11 @@
 //
 // The state (key[624], pos) is the one np.random.get_state() / random.getstate() expose,
 // so the Python shims hand it in and write the advanced state back (drop-in fidelity).
+#include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "common.h"
@@ -237,6 +240,52 @@ extern "C" int rs_np_choice_tuples(uint32_t *mt_key, int32_t *mt_pos, int64_t n,
   // numpy random_interval(max): draws u32 & smear(max) until <= max
   for (int64_t h = 0; h < count; ++h) fisher_yates_prefix<true>(mt, perm, iota, n, k, out + h * k);
   mt.store(mt_key, mt_pos);
+  return RS_OK;
+}
+
+// Many independent numpy streams (one per image pair, config C4: np.random.seed(1000 + pair)
+// then H x choice(N_b, k, replace=False)) replayed on host threads.  Streams with n < k are
+// skipped: their outputs are zero and their state is unchanged (the pair batch flags them).
+extern "C" int rs_np_choice_tuples_multi(int64_t B, const uint32_t *seeds, uint32_t *mt_keys,
+                                         int32_t *mt_pos, const int64_t *ns, int32_t k,
+                                         int64_t count, int32_t *out, int32_t threads) {
+  if (B < 0 || k < 0 || count < 0) return rs::fail(RS_EINVAL, "negative dimensions are not allowed");
+  if (B == 0) return RS_OK;
+  if (!mt_keys || !mt_pos || !ns || (count > 0 && !out))
+    return rs::fail(RS_EINVAL, "rs_np_choice_tuples_multi: null pointer");
+  for (int64_t b = 0; b < B; ++b) {
+    if (ns[b] > 0x7fffffffLL) return rs::fail(RS_EINVAL, "population too large");
+    if (seeds) rs_np_seed(seeds[b], mt_keys + b * kN, mt_pos + b);  // np.random.seed(s_b)
+    if (mt_pos[b] < 0 || mt_pos[b] > kN) return rs::fail(RS_EINVAL, "bad MT19937 position");
+  }
+  const int64_t per = count * k;
+  std::atomic<int64_t> next{0};
+  auto work = [&] {
+    std::vector<int32_t> perm, iota;
+    for (int64_t b; (b = next.fetch_add(1)) < B;) {
+      int32_t *o = out + b * per;
+      const int64_t n = ns[b];
+      if (n < k) {
+        std::fill(o, o + per, 0);
+        continue;
+      }
+      MtStream mt;
+      mt.load(mt_keys + b * kN, mt_pos[b]);
+      perm.resize(static_cast<size_t>(n > 0 ? n : 1));
+      iota.resize(perm.size());
+      for (int64_t i = 0; i < n; ++i) iota[static_cast<size_t>(i)] = static_cast<int32_t>(i);
+      for (int64_t h = 0; h < count; ++h) fisher_yates_prefix<true>(mt, perm, iota, n, k, o + h * k);
+      mt.store(mt_keys + b * kN, mt_pos + b);
+    }
+  };
+  // default: the hardware threads, at most 16 (a one-GPU share of a shared host)
+  int nt = threads > 0 ? threads
+                       : std::min(16, static_cast<int>(std::thread::hardware_concurrency()));
+  nt = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>({static_cast<int64_t>(nt), B, 64})));
+  std::vector<std::thread> pool;
+  for (int i = 1; i < nt; ++i) pool.emplace_back(work);
+  work();
+  for (auto &t : pool) t.join();
   return RS_OK;
 }
 

@@ -66,6 +66,8 @@ _SIGS = {
                                           C.c_int64, _i32p]),
     "rs_py_seed": (C.c_int, [_u32p, C.c_int32, _u32p, _i32p]),
     "rs_py_shuffle_tuples": (C.c_int, [_u32p, _i32p, C.c_int64, C.c_int32, C.c_int64, _i32p]),
+    "rs_np_choice_tuples_multi": (C.c_int, [C.c_int64, _u32p, _u32p, _i32p, _i64p, C.c_int32,
+                                            C.c_int64, _i32p, C.c_int32]),
     "rs_py_shuffle_tuples_gpu": (C.c_int, [C.c_void_p, _u32p, _i32p, C.c_int64, C.c_int32,
                                            C.c_int64, _i32p]),
     "rs_mt_jump": (C.c_int, [_u32p, C.c_int32, C.c_int64, _u32p, _i32p]),
@@ -244,6 +246,29 @@ def np_choice_tuples_gpu(key, pos, n, k, count, ctx=None):
     check(lib().rs_np_choice_tuples_gpu(ctx.handle, ptr(key, C.c_uint32), C.byref(p), int(n),
                                         int(k), int(count), ptr(out, C.c_int32)))
     return out, key, p.value
+
+
+def np_choice_tuples_multi(keys, poss, ns, k, count, threads=0, seeds=None):
+    """np_choice_tuples for B independent streams on host threads; returns
+    (tuples (B, count, k), keys', poss').  With ``seeds`` the streams start from
+    np.random.seed(seeds[b]) and keys / poss may be None.  Streams with n < k give zeros."""
+    ns = np.ascontiguousarray(ns, dtype=np.int64).reshape(-1)
+    B = ns.shape[0]
+    sp = None
+    if seeds is not None:
+        seeds = np.ascontiguousarray(np.asarray(seeds, dtype=np.int64) & 0xFFFFFFFF,
+                                     dtype=np.uint32).reshape(B)
+        sp = ptr(seeds, C.c_uint32)
+        keys = np.empty((B, MT_N), dtype=np.uint32)
+        poss = np.empty(B, dtype=np.int32)
+    else:
+        keys = np.array(keys, dtype=np.uint32, copy=True).reshape(B, MT_N)
+        poss = np.array(poss, dtype=np.int32, copy=True).reshape(B)
+    out = np.empty((B, int(count), int(k)), dtype=np.int32)
+    check(lib().rs_np_choice_tuples_multi(B, sp, ptr(keys, C.c_uint32), ptr(poss, C.c_int32),
+                                          ptr(ns, C.c_int64), int(k), int(count),
+                                          ptr(out, C.c_int32), int(threads)))
+    return out, keys, poss
 
 
 def py_shuffle_tuples(key, pos, n, k, count):

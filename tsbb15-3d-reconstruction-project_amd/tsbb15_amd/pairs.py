@@ -27,12 +27,12 @@ class PairRansac:
 
 def np_tuples_pairs(ns, H, seeds):
     """Host tuples (B, H, 8) replaying np.random.seed(seed_b); choice(arange(N_b), 8, False)
-    H times per pair -- the reference's own stream per pair (pairs with N < 8 stay 0)."""
-    out = np.zeros((len(ns), int(H), 8), dtype=np.int32)
-    for b, (n, s) in enumerate(zip(ns, seeds)):
-        if n >= 8:
-            key, pos = _ffi.np_seed(int(s))
-            out[b], _, _ = _ffi.np_choice_tuples(key, pos, int(n), 8, int(H))
+    H times per pair -- the reference's own stream per pair (pairs with N < 8 stay 0).  The
+    independent streams are replayed on host threads (rs_np_choice_tuples_multi)."""
+    B = len(ns)
+    if B == 0:
+        return np.zeros((0, int(H), 8), dtype=np.int32)
+    out, _, _ = _ffi.np_choice_tuples_multi(None, None, ns, 8, int(H), seeds=seeds)
     return out
 
 
