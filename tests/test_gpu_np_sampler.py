@@ -182,3 +182,50 @@ def test_gen_rnd_tuples_gpu_route_equals_cpython(ctx):
     random.shuffle(x)
     random.setstate(st1)
     assert ransac.gen_rnd_indices(500, 6) == x[:6]
+
+
+_HOST_CHILD = """
+import gc
+import numpy as np
+from tsbb15_amd import _ffi, synth
+from oracle import ransac_ref
+ctx = _ffi.default_context()
+p1, p2, _ = synth.two_view(500, 0.3, seed=4)
+plan = _ffi.F8Plan(ctx, 500, 3000)
+plan.set_points(p1, p2)
+key, pos = _ffi.np_seed(9)
+# back-to-back host-replay runs: no result() in between, the host tuples freed at once
+for r in range(4):
+    key, pos = plan.run_np(3000, key, pos)
+    gc.collect()
+out = plan.result()
+rs = np.random.RandomState(9)
+for r in range(4):
+    F, S, _, best, _ = ransac_ref.ransac_f(p1, p2, r=3000, rng=rs)
+assert out[0].best_index == best, (out[0].best_index, best)
+assert np.array_equal(out[1], S)
+assert pos == rs.get_state()[2] and np.array_equal(key, np.asarray(rs.get_state()[1], np.uint32))
+# F8Plan.run with temporaries: each tuple array is dropped right after the call
+for r in range(3):
+    plan.run(3000, mode=_ffi.SAMPLER_TUPLES,
+             tuples=np.random.RandomState(r).randint(0, 500, size=(3000, 8)).astype(np.int32))
+gc.collect()
+res = plan.result()
+tup = np.random.RandomState(2).randint(0, 500, size=(3000, 8)).astype(np.int32)
+plan.run(3000, mode=_ffi.SAMPLER_TUPLES, tuples=tup)
+ref = plan.result()
+assert res[0].best_index == ref[0].best_index and np.array_equal(res[1], ref[1])
+print("ok")
+"""
+
+
+@pytest.mark.parametrize("knobs", [{"RSAMD_NP_HOST": "1"}, {"RSAMD_OVERLAP": "1"}])
+def test_host_tuple_runs_back_to_back(knobs):
+    """The host-replay parity path (RSAMD_NP_HOST, the overlap variant) issues runs whose
+    tuples live in host memory the library no longer references after the call: back-to-back
+    runs with the arrays dropped at once still equal the oracle."""
+    env = dict(os.environ, **knobs,
+               PYTHONPATH=os.pathsep.join([PKG_DIR, REPO, os.environ.get("PYTHONPATH", "")]))
+    r = subprocess.run([sys.executable, "-c", _HOST_CHILD], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]

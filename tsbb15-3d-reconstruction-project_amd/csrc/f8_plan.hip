@@ -48,6 +48,13 @@ struct RunBufs {
   rsd::F8DevResult *d_res = nullptr;
   int *d_gdone = nullptr;      // per-group finish counters (fused c* in k_f8_count32x)
   float4 *d_G4 = nullptr;      // per-hypothesis decision constants (k_f8_count32x DEC 3)
+  // host tuples (parity mode fed from the host) are staged in a pinned buffer owned by the
+  // set, so the caller's array may go away as soon as rs_f8_plan_run returns; ev_copy marks
+  // the end of the H2D copy that last read it (waited for before the buffer is refilled)
+  int *h_tuples = nullptr;
+  int64_t cap_h_tuples = 0;
+  hipEvent_t ev_copy = nullptr;
+  bool copy_pending = false;
 };
 
 // Absolute error bounds of the fp32 test in the unit frame (|x~| <= R); derivation in
@@ -238,6 +245,8 @@ static void plan_free(rs_f8_plan *p) {
     (void)hipFree(b.d_res);
     (void)hipFree(b.d_gdone);
     (void)hipFree(b.d_G4);
+    if (b.h_tuples) (void)hipHostFree(b.h_tuples);
+    if (b.ev_copy) (void)hipEventDestroy(b.ev_copy);
   }
   for (auto &h : p->h_slot)
     if (h) (void)hipHostFree(h);
@@ -464,9 +473,27 @@ static int plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t seed, uint6
   if (p->overlap && p->runs >= rs_f8_plan::kBufs)  // set `set` free: run k-3's tail is done
     HIP_TRY(hipStreamWaitEvent(sst, p->ev_free[set], 0));
 
-  if (mode == RS_SAMPLER_TUPLES && !dev_tuples)
-    HIP_TRY(hipMemcpyAsync(b.d_tuples, host_tuples, sizeof(int) * 8 * H, hipMemcpyHostToDevice,
+  if (mode == RS_SAMPLER_TUPLES && !dev_tuples) {
+    // stage through the set's pinned buffer: the copy no longer reads caller memory after
+    // this call returns (the caller may free or reuse its tuples at once)
+    if (b.copy_pending) {
+      HIP_TRY(hipEventSynchronize(b.ev_copy));
+      b.copy_pending = false;
+    }
+    if (b.cap_h_tuples < 8 * H) {
+      if (b.h_tuples) HIP_TRY(hipHostFree(b.h_tuples));
+      b.h_tuples = nullptr;
+      b.cap_h_tuples = 0;
+      HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&b.h_tuples), sizeof(int) * 8 * p->ld));
+      b.cap_h_tuples = 8 * p->ld;
+    }
+    if (!b.ev_copy) HIP_TRY(hipEventCreateWithFlags(&b.ev_copy, hipEventDisableTiming));
+    std::memcpy(b.h_tuples, host_tuples, sizeof(int) * 8 * H);
+    HIP_TRY(hipMemcpyAsync(b.d_tuples, b.h_tuples, sizeof(int) * 8 * H, hipMemcpyHostToDevice,
                            sst));
+    HIP_TRY(hipEventRecord(b.ev_copy, sst));
+    b.copy_pending = true;
+  }
   // [tail of the previous run | solve of this run]: buffer set b was last read by run k-2,
   // whose tail is complete (stream order)
   rsd::SolveArgs sa{};

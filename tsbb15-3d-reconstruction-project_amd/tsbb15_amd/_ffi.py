@@ -366,7 +366,6 @@ class F8Plan:
             tuples = np.ascontiguousarray(tuples, dtype=np.int32)
             if tuples.shape != (int(H), 8):
                 raise ValueError("tuples must be (H, 8)")
-            self._tuples = tuples  # keep alive until the copy is issued
             tp = ptr(tuples, C.c_int32)
         check(lib().rs_f8_plan_run(self._h, int(H), int(mode), int(seed) & (2**64 - 1),
                                    int(hyp_offset), tp, float(thresh)))
