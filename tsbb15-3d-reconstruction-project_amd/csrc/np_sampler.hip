@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -56,13 +57,14 @@ constexpr uint32_t kLower = 0x7fffffffu;
 constexpr uint32_t kMatA = 0x9908b0dfu;
 constexpr int kDeg = 19937;
 constexpr int kPrefix = kDeg + kN - 1;       // words of a window's sequence a jump reads
-constexpr int kJB = 512;                     // stream blocks per generator
+constexpr int kJB = 1024;                    // stream blocks per generator
 constexpr int64_t kJ = int64_t(kN) * kJB;    // words per generator
 constexpr int kLevels = 11;                  // jump tree depth: up to 2048 generators
 constexpr int64_t kSegWords = int64_t(1) << 29;  // stream words per segment (2 GiB)
-constexpr int kW = 262144;                   // longest automatic parse chunk (draws)
+constexpr int kW = 1 << 20;                  // longest automatic parse chunk (draws)
 constexpr int kWmax = 1 << 20;               // longest chunk (RSAMD_NP_KW)
 constexpr int kWmin = 8192;                  // shortest parse chunk
+constexpr int kChunksTarget = 512;           // automatic chunk length: about this many chunks
 constexpr int kEntryThreads = 512;
 constexpr int kR = 20;                       // slots per thread: N - 1 <= 10240
 constexpr int kMaxN1 = kEntryThreads * kR;
@@ -101,29 +103,48 @@ __device__ __forceinline__ uint32_t draw_of(uint32_t w, uint32_t i) {
 // y_{i+w} over the set bits i of the polynomial.  Only the top bit of word 0 is MT state, so
 // word 0 of a jumped window may carry wrong low bits: it is never emitted (k_mt_stream) and
 // the recurrence reads only its top bit.
-// 1024 threads: four groups of 256 XOR a quarter of the set bits each (four waves per SIMD
-// hide the LDS latency of the bit loop), then one LDS reduction.
+// Each jump is split into S parts over the (sorted) set bits, so that every level of the tree
+// runs on all CUs: part q regenerates in LDS only the prefix y_0 .. y_{hi-1} its bits read, XORs
+// its share (four groups of 256 threads a quarter of the bits each, three output words per
+// thread), and XOR-adds the partial window into the destination (zeroed beforehand) with
+// vector atomics; a single part stores it.
 constexpr int kJumpGroups = 4;
 __global__ __launch_bounds__(256 * kJumpGroups) void k_mt_jump(uint32_t *__restrict__ win, int half,
                                                                int G, const int32_t *__restrict__ bits,
-                                                               int nbits) {
-  __shared__ uint32_t y[kPrefix];
+                                                               int nbits, int S) {
+  extern __shared__ uint32_t y[];  // up to kPrefix words
   __shared__ uint32_t part[kJumpGroups - 1][kN];
-  const int g = blockIdx.x, dst = g + half;
+  const int g = blockIdx.x / S, q = blockIdx.x % S, dst = g + half;
   if (dst >= G) return;
+  const int p0 = static_cast<int>(static_cast<int64_t>(nbits) * q / S);
+  const int p1 = static_cast<int>(static_cast<int64_t>(nbits) * (q + 1) / S);
+  if (p0 >= p1) return;
+  const int hi = bits[p1 - 1] + kN;  // words y_0 .. y_{hi-1} are read
   const int tid = threadIdx.x, grp = tid >> 8, lt = tid & 255;
   for (int t = tid; t < kN; t += 256 * kJumpGroups) y[t] = win[static_cast<size_t>(g) * kN + t];
   __syncthreads();
-  for (int t0 = kN; t0 < kPrefix; t0 += 227) {
+  for (int t0 = kN; t0 < hi; t0 += 227) {
     const int t = t0 + tid;
-    if (tid < 227 && t < kPrefix) y[t] = y[t - 227] ^ twist(y[t - kN], y[t - kN + 1]);
+    if (tid < 227 && t < hi) y[t] = y[t - 227] ^ twist(y[t - kN], y[t - kN + 1]);
     __syncthreads();
   }
   const int w0 = lt, w1 = lt + 256, w2 = lt + 512 < kN ? lt + 512 : kN - 1;
-  const int per = (nbits + kJumpGroups - 1) / kJumpGroups;
-  const int b0 = grp * per, b1 = min(nbits, b0 + per);
+  const int per = (p1 - p0 + kJumpGroups - 1) / kJumpGroups;
+  const int b0 = p0 + grp * per, b1 = min(p1, b0 + per);
   uint32_t a0 = 0, a1 = 0, a2 = 0;
-  for (int b = b0; b < b1; ++b) {
+  int b = b0;
+  for (; b + 16 <= b1; b += 16) {  // 16 bit indices per scalar load batch
+    int ix[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) ix[k] = bits[b + k];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      a0 ^= y[ix[k] + w0];
+      a1 ^= y[ix[k] + w1];
+      a2 ^= y[ix[k] + w2];
+    }
+  }
+  for (; b < b1; ++b) {
     const int i = bits[b];
     a0 ^= y[i + w0];
     a1 ^= y[i + w1];
@@ -137,25 +158,34 @@ __global__ __launch_bounds__(256 * kJumpGroups) void k_mt_jump(uint32_t *__restr
   __syncthreads();
   if (grp == 0) {
 #pragma unroll
-    for (int q = 0; q < kJumpGroups - 1; ++q) {
-      a0 ^= part[q][w0];
-      a1 ^= part[q][w1];
-      a2 ^= part[q][w2];
+    for (int k = 0; k < kJumpGroups - 1; ++k) {
+      a0 ^= part[k][w0];
+      a1 ^= part[k][w1];
+      a2 ^= part[k][w2];
     }
     uint32_t *out = win + static_cast<size_t>(dst) * kN;
-    out[w0] = a0;
-    out[w1] = a1;
-    if (lt + 512 < kN) out[w2] = a2;
+    if (S == 1) {
+      out[w0] = a0;
+      out[w1] = a1;
+      if (lt + 512 < kN) out[w2] = a2;
+    } else {
+      atomicXor(out + w0, a0);
+      atomicXor(out + w1, a1);
+      if (lt + 512 < kN) atomicXor(out + w2, a2);
+    }
   }
 }
 
 // ---- 2. stream: generator g owns blocks (g kJB, (g+1) kJB] plus words 1..623 of its window --
-__global__ __launch_bounds__(64) void k_mt_stream(const uint32_t *__restrict__ win,
-                                                  uint32_t *__restrict__ stream, int64_t Lb) {
-  __shared__ uint32_t ob[kN], nb[kN];
+// 256 threads: a block is the three dependent runs of the recurrence (227, 227, 170 words),
+// one word per thread each, then tempered and stored; the two LDS blocks alternate.
+__global__ __launch_bounds__(256) void k_mt_stream(const uint32_t *__restrict__ win,
+                                                   uint32_t *__restrict__ stream, int64_t Lb) {
+  __shared__ uint32_t bb[2][kN];
   const int g = blockIdx.x, l = threadIdx.x;
   const int64_t b0 = static_cast<int64_t>(g) * kJB;
-  for (int t = l; t < kN; t += 64) {
+  uint32_t *ob = bb[0], *nb = bb[1];
+  for (int t = l; t < kN; t += 256) {
     const uint32_t v = win[static_cast<size_t>(g) * kN + t];
     ob[t] = v;
     if (t > 0 || g == 0) stream[b0 * kN + t] = temper(v);
@@ -163,20 +193,17 @@ __global__ __launch_bounds__(64) void k_mt_stream(const uint32_t *__restrict__ w
   __syncthreads();
   const int64_t bend = std::min<int64_t>(b0 + kJB, Lb - 1);
   for (int64_t b = b0 + 1; b <= bend; ++b) {
-    for (int t = l; t < 227; t += 64) nb[t] = ob[t + kM] ^ twist(ob[t], ob[t + 1]);
+    if (l < 227) nb[l] = ob[l + kM] ^ twist(ob[l], ob[l + 1]);
     __syncthreads();
-    for (int t = 227 + l; t < 454; t += 64) nb[t] = nb[t - 227] ^ twist(ob[t], ob[t + 1]);
+    if (l < 227) nb[227 + l] = nb[l] ^ twist(ob[227 + l], ob[228 + l]);
     __syncthreads();
-    for (int t = 454 + l; t < kN; t += 64)
-      nb[t] = nb[t - 227] ^ twist(ob[t], t + 1 < kN ? ob[t + 1] : nb[0]);
+    if (l < 170) nb[454 + l] = nb[227 + l] ^ twist(ob[454 + l], l + 1 < 170 ? ob[455 + l] : nb[0]);
     __syncthreads();
     uint32_t *o = stream + b * kN;
-    for (int t = l; t < kN; t += 64) {
-      const uint32_t v = nb[t];
-      o[t] = temper(v);
-      ob[t] = v;
-    }
-    __syncthreads();
+    for (int t = l; t < kN; t += 256) o[t] = temper(nb[t]);
+    uint32_t *x = ob;
+    ob = nb;
+    nb = x;
   }
 }
 
@@ -193,6 +220,7 @@ struct EntryArgs {
   int *tpos;              // [C] draws parsed by the dense kernel (the sparse kernel resumes there)
   int ecap;
   int *err;
+  long long *stats;       // RSAMD_DIAG builds only: per-chunk tracking statistics (else null)
 };
 
 __device__ __forceinline__ int block_excl_scan(int v, int *sh, int *total) {
@@ -215,6 +243,12 @@ __device__ __forceinline__ int block_excl_scan(int v, int *sh, int *total) {
   __syncthreads();
   *total = tot;
   return base + x - v;
+}
+
+// a value the compiler cannot prove wave-uniform (threadIdx-derived, LDS-loaded) that is
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t uni(uint32_t v) {
+  return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v)));
 }
 
 __device__ __forceinline__ uint32_t lane_rank(uint64_t bits) {
@@ -438,103 +472,355 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a,
   }
 }
 
-// ---- 3b. sparse phase of a chunk: one wave, lane l = slot l ---------------------------------
-// A separate 64-thread launch so that the long serial tail of every chunk runs at full
-// occupancy (inside the 512-thread dense workgroup it held a CU slot with one wave).
-template <bool PY>
-__device__ __forceinline__ void sparse_step(uint32_t w, uint32_t &sv) {
-  sv -= draw_of<PY>(w, sv) <= sv ? 1u : 0u;
+// ---- 3b. tracking phase of a chunk: the <= 64 trajectories left after the dense parse --------
+// One workgroup per chunk, 8 waves; trajectory q (position q of the chunk's sorted list) runs on
+// wave q % 8.  A trajectory advances by windows of 64 draws with the lanes as draws: lane l's
+// state is s_l = i - (accepts among lanes < l) (wrapping from 1 to n1 at a hypothesis end), its
+// step accepts iff draw_of(w_l, s_l) <= s_l.  The accept mask is the fixed point of
+//     acc <- ballot(draw_of(w_l, i - rank_l(acc)) <= i - rank_l(acc)),
+// iterated from "all accept": lane 0's state is always right, and once lanes < l are right lane
+// l is, so the iteration reaches the sequential answer in at most 65 rounds (2.9 on average at
+// N = 2000), and a fixed point IS that answer (induction over the lanes).  Windows cross bucket
+// boundaries and hypothesis ends freely.
+// Every kCheck draws the trajectories meet at a checkpoint: states that are equal there are the
+// same trajectory from then on, so all but the first of each run of equal states (cyclic order
+// is preserved by the parse) are dropped, and the survivor's member range extends to the next
+// survivor's start.  Wraps are logged with the member range as in k_np_entry.
+constexpr int kTrackWaves = 8;
+constexpr int kCheck = 4096;
+
+template <bool PY, bool SMALL>
+__device__ __forceinline__ uint32_t wrap_state(int si, int n1) {
+  if (si > 0) return static_cast<uint32_t>(si);
+  if constexpr (SMALL) return static_cast<uint32_t>(n1 - ((-si) % n1));
+  else return static_cast<uint32_t>(si + n1);
 }
 
-template <bool PY>
-__global__ __launch_bounds__(64) void k_np_sparse(EntryArgs a, const uint32_t *__restrict__ draws) {
-  const int c = blockIdx.x, l = threadIdx.x;
+// ---- one window of one trajectory -----------------------------------------------------------
+// State i before the window, lane l holds draw l of the window (lanes >= Wn, outside wm, are
+// never accepted).  Returns the accept mask; advances i; wraps (hypothesis ends) in *wr.
+//
+// Fast path: every state the window can reach keeps i's draw rule (i - 63 >= the bucket's lowest
+// state), so no hypothesis ends inside and lane l's draw u_l is fixed.  With rank_l = accepts
+// among lanes < l, lane l accepts iff rank_l <= v_l := i - u_l, and 0 <= rank_l <= l: v_l >= l
+// accepts surely, v_l < 0 rejects surely, and the few lanes between (about l / 2^bits each) are
+// resolved in order on the scalar unit; more than kAmbSeq of them go to the fixed point below.
+// General path (bucket crossings, hypothesis ends): the fixed point of
+//     acc <- ballot(draw_of(w_l, s_l) <= s_l),  s_l = i - rank_l(acc) (wrapped into 1..n1),
+// from "all accept": lanes < l right => lane l right, so it reaches the sequential answer, and
+// any fixed point is that answer.
+constexpr int kAmbSeq = 4;
+
+template <bool PY, bool SMALL>
+__device__ __forceinline__ uint64_t window_step(uint32_t w, uint64_t wm, uint32_t &i, int n1,
+                                                uint64_t &wr, uint32_t &sl_out) {
+  const int lane = threadIdx.x & 63;
+  uint32_t lowest, u;
+  if constexpr (PY) {
+    const uint32_t sh = static_cast<uint32_t>(__builtin_clz(i + 1u));
+    lowest = (1u << (31u - sh)) - 1u;  // i + 1 in [2^(31-sh), 2^(32-sh) - 1]
+    u = w >> sh;
+  } else {
+    const uint32_t M = 0xffffffffu >> __builtin_clz(i);
+    lowest = (M >> 1) + 1u;
+    u = w & M;
+  }
+  if (i >= lowest + 63u) {
+    const int v = static_cast<int>(i) - static_cast<int>(u);
+    uint64_t acc = __ballot(v >= lane) & wm;
+    uint64_t amb = __ballot(v >= 0) & wm & ~acc;
+    if (amb) {
+      if (__popcll(amb) <= kAmbSeq) {
+        do {
+          const int f = __ffsll(static_cast<long long>(amb)) - 1;
+          const int rk = __popcll(acc & ((1ull << f) - 1ull));
+          if (rk <= __builtin_amdgcn_readlane(v, f)) acc |= 1ull << f;
+          amb &= amb - 1ull;
+        } while (amb);
+      } else {
+        acc |= amb;
+        uint64_t prev;
+        do {
+          prev = acc;
+          acc = __ballot(static_cast<int>(lane_rank(prev)) <= v) & wm;
+        } while (acc != prev);
+      }
+    }
+    i -= static_cast<uint32_t>(__popcll(acc));
+    wr = 0;
+    sl_out = 0;
+    return acc;
+  }
+  uint64_t acc = wm, prev;
+  uint32_t sl;
+  do {
+    prev = acc;
+    sl = wrap_state<PY, SMALL>(static_cast<int>(i) - static_cast<int>(lane_rank(prev)), n1);
+    acc = __ballot(draw_of<PY>(w, sl) <= sl) & wm;
+  } while (acc != prev);
+  wr = __ballot(sl == 1u) & acc;
+  sl_out = sl;
+  i = wrap_state<PY, SMALL>(static_cast<int>(i) - static_cast<int>(__popcll(acc)), n1);
+  return acc;
+}
+
+// One checkpoint interval [t, cp) of a single trajectory (the common case once a chunk's
+// trajectories have merged down to at most one per wave): the tight loop.
+// While every state a window can reach lies in i's bucket or the one below (and no hypothesis
+// ends), lane l's draw is u_hi (i's rule) or u_lo (the lower rule) by whether its state
+// i - rank_l is at least `lowest`: with v = i - u, lane l accepts iff
+//     rank_l <= (rank_l <= i - lowest ? v_hi : v_lo),
+// and the accept masks are the fixed point of that test over rank_l(acc) (four quarters of 64
+// draws at once, lane l holding draws 64 k + l; any fixed point is the sequential answer).
+// Other windows (states below 2 x 64, hypothesis ends) go through window_step.
+template <bool PY, bool SMALL>
+__device__ __forceinline__ uint32_t track_one(const EntryArgs &a, const uint32_t *sw, int *s_evn,
+                                              uint2 *ev, uint32_t i, uint32_t range, int t,
+                                              int cp) {
+  const int lane = threadIdx.x & 63;
+  const int n1 = a.n1;
+  int d = t;
+  while (d < cp) {
+    uint32_t lowest, lowest2, sh = 0, M = 0;
+    if constexpr (PY) {
+      sh = static_cast<uint32_t>(__builtin_clz(i + 1u));
+      lowest = (1u << (31u - sh)) - 1u;
+      lowest2 = sh < 30u ? (1u << (30u - sh)) - 1u : 0x7fffffffu;
+    } else {
+      M = 0xffffffffu >> __builtin_clz(i);
+      lowest = (M >> 1) + 1u;
+      lowest2 = M > 1u ? (M >> 2) + 1u : 0x7fffffffu;
+    }
+    const uint32_t *wq = sw + ((d - t) & (kCheck - 1));
+    const int c = static_cast<int>(i) - static_cast<int>(lowest);
+    if (d + 256 <= cp && i >= lowest2 + 255u && lowest2 >= 1u) {
+      int vh[4], vl[4];
+      uint64_t acc[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t w = wq[64 * k + lane];
+        vh[k] = static_cast<int>(i) - static_cast<int>(PY ? (w >> sh) : (w & M));
+        vl[k] = static_cast<int>(i) - static_cast<int>(PY ? (w >> (sh + 1u)) : (w & (M >> 1)));
+        acc[k] = __ballot(vh[k] >= 0);
+      }
+      bool again;
+      do {
+        int base = 0;
+        uint64_t nacc[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int rk = base + static_cast<int>(lane_rank(acc[k]));
+          nacc[k] = __ballot(rk <= (rk <= c ? vh[k] : vl[k]));
+          base += static_cast<int>(__popcll(acc[k]));
+        }
+        again = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          again |= nacc[k] != acc[k];
+          acc[k] = nacc[k];
+        }
+      } while (again);
+      int tot = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) tot += static_cast<int>(__popcll(acc[k]));
+      i -= static_cast<uint32_t>(tot);
+      d += 256;
+      continue;
+    }
+    const int Wn = min(64, cp - d);
+    const uint64_t wm = Wn == 64 ? ~0ull : ((1ull << Wn) - 1ull);
+    const uint32_t w = wq[lane];  // lanes >= Wn read draws of the wrapped buffer, never accepted
+    if (i >= lowest2 + 63u && lowest2 >= 1u) {
+      const int vh = static_cast<int>(i) - static_cast<int>(PY ? (w >> sh) : (w & M));
+      const int vl = static_cast<int>(i) - static_cast<int>(PY ? (w >> (sh + 1u)) : (w & (M >> 1)));
+      uint64_t acc = __ballot(vh >= 0) & wm, prev;
+      do {
+        prev = acc;
+        const int rk = static_cast<int>(lane_rank(prev));
+        acc = __ballot(rk <= (rk <= c ? vh : vl)) & wm;
+      } while (acc != prev);
+      i -= static_cast<uint32_t>(__popcll(acc));
+      d += Wn;
+      continue;
+    }
+    uint64_t wr;
+    uint32_t sl;
+    (void)window_step<PY, SMALL>(w, wm, i, n1, wr, sl);
+    if (wr) {  // hypothesis ends: the next hypothesis starts at the following draw
+      int eb = 0;
+      if (lane == 0) eb = atomicAdd(s_evn, __popcll(wr));
+      eb = __shfl(eb, 0);
+      if (((wr >> lane) & 1ull)) {
+        const int e = eb + static_cast<int>(lane_rank(wr));
+        if (e < a.ecap) ev[e] = make_uint2(static_cast<uint32_t>(d + lane + 1), range);
+      }
+    }
+    d += Wn;
+  }
+  return i;
+}
+
+// One checkpoint interval [t, cp) of R trajectories q = wv + r kTrackWaves (r < nq), a window
+// of 64 draws per step.
+template <int R, bool PY, bool SMALL>
+__device__ __forceinline__ void track_interval(const EntryArgs &a, const uint32_t *sw,
+                                               uint32_t *s_st, const uint32_t *s_lo, int *s_evn,
+                                               uint2 *ev, int m, int wv, int nq, int t, int cp,
+                                               long long *dg) {
+  const int lane = threadIdx.x & 63;
+  const int n1 = a.n1;
+  uint32_t i[R], range[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int q = wv + (r < nq ? r : nq - 1) * kTrackWaves;
+    i[r] = uni(s_st[q]);
+    range[r] = uni(s_lo[q] | (s_lo[q + 1 == m ? 0 : q + 1] << 16));
+  }
+  int d = t;
+  uint32_t wn = sw[lane];  // draws beyond cp are never accepted (lanes >= Wn)
+  while (d < cp) {
+    const int Wn = min(64, cp - d);
+    const uint64_t wm = Wn == 64 ? ~0ull : ((1ull << Wn) - 1ull);
+    const uint32_t w = wn;
+    if (d + 64 < cp) wn = sw[(d + 64 - t + lane) & (kCheck - 1)];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (r < nq) {
+        uint64_t wr;
+        uint32_t sl;
+        (void)window_step<PY, SMALL>(w, wm, i[r], n1, wr, sl);
+        if (wr) {  // hypothesis ends: the next hypothesis starts at the following draw
+          int eb = 0;
+          if (lane == 0) eb = atomicAdd(s_evn, __popcll(wr));
+          eb = __shfl(eb, 0);
+          if (((wr >> lane) & 1ull)) {
+            const int e = eb + static_cast<int>(lane_rank(wr));
+            if (e < a.ecap) ev[e] = make_uint2(static_cast<uint32_t>(d + lane + 1), range[r]);
+          }
+        }
+      }
+    }
+#ifdef RSAMD_DIAG
+    dg[0] += 1;
+#endif
+    d += Wn;
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    if (r < nq && lane == 0) s_st[wv + r * kTrackWaves] = i[r];
+}
+
+template <bool PY, bool SMALL>
+__global__ __launch_bounds__(64 * kTrackWaves) void k_np_track(EntryArgs a,
+                                                                const uint32_t *__restrict__ draws) {
+  // the draws of the current checkpoint interval in LDS (all trajectories of the chunk read
+  // them; a window's read is issued one window ahead), the next interval in flight in VGPRs
+  __shared__ uint32_t s_w[2][kCheck];
+  __shared__ uint32_t s_st[64], s_lo[64];
+  __shared__ int s_m, s_evn;
+  constexpr int kPer = kCheck / (64 * kTrackWaves);  // draws per thread per interval
+  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = uni(tid >> 6);
   int m = a.fin_m[c];
   if (m > 64) return;  // the chunk ended while dense: final already
   const int n1 = a.n1;
   const int64_t t0 = static_cast<int64_t>(c) * a.W;
   const int T = static_cast<int>(std::min<int64_t>(a.W, a.D - t0));
+  int t = a.tpos[c];
+  if (t >= T) return;
   const uint32_t *__restrict__ wp = draws + t0;
   uint2 *ev = a.ev + static_cast<size_t>(c) * a.ecap;
-  const uint32_t N1 = static_cast<uint32_t>(n1);
-  int t = a.tpos[c];
-  const uint32_t f0 = l < m ? a.fin[static_cast<size_t>(c) * n1 + l] : 0u;
-  uint32_t sv = l < m ? (f0 >> 16) : kSentinel;
-  uint32_t lov = f0 & 0xffffu;
-  int ecnt = a.ev_n[c];
+  // RSAMD_DIAG: windows (multi-slot path), cycles with one / several trajectories, wave-intervals
+  // with one / several, intervals
+  long long dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#ifdef RSAMD_DIAG
+  const long long k0 = __builtin_amdgcn_s_memtime();
+#endif
+  if (tid < m) {
+    const uint32_t f = a.fin[static_cast<size_t>(c) * n1 + tid];
+    s_st[tid] = f >> 16;
+    s_lo[tid] = f & 0xffffu;
+  }
+  if (tid == 0) s_evn = a.ev_n[c];
+  uint32_t nx[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int x = t + k * 64 * kTrackWaves + tid;
+    nx[k] = x < T ? wp[x] : 0u;
+  }
+  int buf = 0;
   while (t < T) {
-    const int kk = min(64, T - t);
-    if (kk == 64 && n1 >= 64) {
-      // a lane wraps at most once in 64 draws (a hypothesis takes >= n1 >= 64): branch-free
-      // steps, the wrap draw kept per lane and logged after the batch; the 64 words are
-      // wave-uniform, so they arrive by scalar loads straight into SGPRs
-      uint32_t wk = 0xffffffffu;
-      uint32_t wsg[64];
-      const uint32_t *__restrict__ wq = wp + t;
+    const int cp = min(T, t + kCheck);
+    uint32_t *sw = s_w[buf];
 #pragma unroll
-      for (int k = 0; k < 64; ++k) wsg[k] = wq[k];
+    for (int k = 0; k < kPer; ++k) sw[k * 64 * kTrackWaves + tid] = nx[k];
+    __syncthreads();
 #pragma unroll
-      for (int k = 0; k < 64; ++k) {
-        const uint32_t w = wsg[k];
-        sparse_step<PY>(w, sv);
-        const bool z = sv == 0;
-        sv = z ? N1 : sv;
-        wk = z ? static_cast<uint32_t>(k) : wk;
-      }
-      const uint64_t wr = __ballot(wk != 0xffffffffu);
-      if (wr) {
-        const uint32_t succ = __shfl(lov, l + 1 == m ? 0 : l + 1);
-        if (wk != 0xffffffffu) {
-          const int e = ecnt + static_cast<int>(lane_rank(wr));
-          if (e < a.ecap) ev[e] = make_uint2(static_cast<uint32_t>(t) + wk + 1u, lov | (succ << 16));
-        }
-        ecnt += __popcll(wr);
-      }
-    } else {
-      const uint32_t wv = l < kk ? wp[t + l] : 0u;
-      for (int k = 0; k < kk; ++k) {
-        const uint32_t w = __builtin_amdgcn_readlane(wv, k);
-        sparse_step<PY>(w, sv);
-        const uint64_t wr = __ballot(sv == 0);
-        if (wr) {
-          const uint32_t succ = __shfl(lov, l + 1 == m ? 0 : l + 1);
-          if (sv == 0) {
-            sv = N1;
-            const int e = ecnt + static_cast<int>(lane_rank(wr));
-            if (e < a.ecap) ev[e] = make_uint2(static_cast<uint32_t>(t + k + 1), lov | (succ << 16));
-          }
-          ecnt += __popcll(wr);
-        }
-      }
+    for (int k = 0; k < kPer; ++k) {  // the next interval's draws
+      const int x = cp + k * 64 * kTrackWaves + tid;
+      nx[k] = x < T ? wp[x] : 0u;
     }
-    t += kk;
-    // wave compaction
-    const bool valid = l < m;
-    uint32_t mx = valid ? sv : 0u;
-#pragma unroll
-    for (int o = 32; o; o >>= 1) mx = max(mx, static_cast<uint32_t>(__shfl_xor(static_cast<int>(mx), o)));
-    const uint32_t psv = __shfl(sv, l == 0 ? m - 1 : l - 1);
-    const uint64_t hb = __ballot(valid && sv == mx && psv != mx);
-    const int h = hb ? __ffsll(static_cast<long long>(hb)) - 1 : 0;
-    const bool keep = valid && (l == h || sv != psv);
-    const uint64_t kb = __ballot(keep);
-    const uint64_t lmask = (1ull << l) - 1ull;
-    const uint64_t hmask = h == 0 ? 0ull : ((1ull << h) - 1ull);
-    const uint64_t mmask = m >= 64 ? ~0ull : ((1ull << m) - 1ull);
-    const uint64_t before = l >= h ? (lmask & ~hmask) : ((mmask & ~hmask) | lmask);
-    const int m2 = __popcll(kb);
-    const int dest = keep ? __popcll(kb & before) : m2 + __popcll(~kb & lmask);
-    sv = static_cast<uint32_t>(__builtin_amdgcn_ds_permute(dest * 4, static_cast<int>(sv)));
-    lov = static_cast<uint32_t>(__builtin_amdgcn_ds_permute(dest * 4, static_cast<int>(lov)));
-    m = m2;
-    if (l >= m) sv = kSentinel;
+    // this wave's trajectories q = wv, wv + 8, ... advance together (independent fixed-point
+    // chains interleaved: the latency of one round is shared by up to kTrackSlots of them)
+    const int nq = m > wv ? (m - wv + kTrackWaves - 1) / kTrackWaves : 0;
+#ifdef RSAMD_DIAG
+    const long long c0 = __builtin_amdgcn_s_memtime();
+#endif
+    if (nq == 1) {
+      const uint32_t i1 = track_one<PY, SMALL>(
+          a, sw, &s_evn, ev, uni(s_st[wv]), uni(s_lo[wv] | (s_lo[wv + 1 == m ? 0 : wv + 1] << 16)),
+          t, cp);
+      if (lane == 0) s_st[wv] = i1;
+    }
+    else if (nq == 2) track_interval<2, PY, SMALL>(a, sw, s_st, s_lo, &s_evn, ev, m, wv, 2, t, cp, dg);
+    else if (nq > 2 && nq <= 4) track_interval<4, PY, SMALL>(a, sw, s_st, s_lo, &s_evn, ev, m, wv, nq, t, cp, dg);
+    else if (nq > 4) track_interval<8, PY, SMALL>(a, sw, s_st, s_lo, &s_evn, ev, m, wv, nq, t, cp, dg);
+#ifdef RSAMD_DIAG
+    {
+      const long long dc = __builtin_amdgcn_s_memtime() - c0;  // busy cycles of this wave
+      if (nq == 1) dg[1] += dc, dg[3] += 1;
+      else if (nq > 1) dg[2] += dc, dg[4] += 1;
+      dg[5] += 1;
+    }
+#endif
+    __syncthreads();
+    if (wv == 0) {  // merge equal states (runs are contiguous in cyclic order)
+      const bool v = lane < m;
+      const uint32_t sq = v ? s_st[lane] : 0u;
+      const uint32_t sp = v ? s_st[lane == 0 ? m - 1 : lane - 1] : 0u;
+      const uint32_t lq = v ? s_lo[lane] : 0u;
+      const uint64_t vm = m >= 64 ? ~0ull : ((1ull << m) - 1ull);
+      const uint64_t eq = __ballot(v && m > 1 && sq == sp);
+      bool keep = v && !((eq >> lane) & 1ull);
+      if (eq == vm) keep = lane == 0;  // one trajectory left
+      const uint64_t kb = __ballot(keep);
+      __builtin_amdgcn_wave_barrier();
+      if (keep) {
+        const int dst = static_cast<int>(lane_rank(kb));
+        s_st[dst] = sq;
+        s_lo[dst] = lq;
+      }
+      if (lane == 0) s_m = static_cast<int>(__popcll(kb));
+    }
+    __syncthreads();
+    m = uni(s_m);
+    t = cp;
+    buf ^= 1;
   }
-  if (l < m) a.fin[static_cast<size_t>(c) * n1 + l] = lov | (sv << 16);
-  if (l == 0) {
+  if (tid < m) a.fin[static_cast<size_t>(c) * n1 + tid] = s_lo[tid] | (s_st[tid] << 16);
+  if (tid == 0) {
     a.fin_m[c] = m;
-    a.ev_n[c] = min(ecnt, a.ecap);
-    if (ecnt > a.ecap) atomicOr(a.err, 1);
+    a.ev_n[c] = min(s_evn, a.ecap);
+    if (s_evn > a.ecap) atomicOr(a.err, 1);
   }
+#ifdef RSAMD_DIAG
+  if (a.stats && lane == 0) {
+    long long *o = a.stats + static_cast<size_t>(c) * 64 + wv * 6;
+    for (int k = 0; k < 6; ++k) o[k] = dg[k];
+    if (wv == 0) a.stats[static_cast<size_t>(c) * 64 + 60] = __builtin_amdgcn_s_memtime() - k0;
+  }
+#else
+  (void)dg;
+#endif
 }
 
 // ---- 5. keep the wraps of the true trajectory (in place, order preserved) -----------------
@@ -562,12 +848,85 @@ __global__ __launch_bounds__(64) void k_np_filter(uint2 *__restrict__ ev, const 
   if (l == 0) vcnt[c] = cnt;
 }
 
+// ---- 4. compose the chunk maps on the GPU (one wave, serial over chunks) -----------------
+// Chunk c's final list maps entry list index a (state n1 - a) to the state of the first entry
+// with the largest start lo <= a (cyclically: the largest lo overall if none); chunk 0 starts
+// a hypothesis (a = 0).  Keys lo << 16 | state: their maximum is the wanted entry.  The rows
+// of chunk c + 1 are loaded while chunk c's reduction runs.
+__global__ __launch_bounds__(64) void k_np_compose(const uint32_t *__restrict__ fin,
+                                                   const int *__restrict__ fin_m, int n1, int C,
+                                                   int *__restrict__ ent) {
+  const int l = threadIdx.x;
+  int a = 0;
+  int m = fin_m[0];
+  uint32_t f = l < m ? fin[l] : 0u;
+  for (int c = 0; c < C; ++c) {
+    const int mn = c + 1 < C ? fin_m[c + 1] : 0;
+    const uint32_t fn = l < mn ? fin[static_cast<size_t>(c + 1) * n1 + l] : 0u;
+    uint32_t kb = 0, kt = 0;  // best key with lo <= a, top key (0: none; keys of valid rows are
+    bool hb = false, ht = false;  //  nonzero only if lo or state is, so flags are kept apart)
+    for (int k = l; k < m; k += 64) {
+      const uint32_t x = k < 64 ? f : fin[static_cast<size_t>(c) * n1 + k];
+      const uint32_t lo = x & 0xffffu, key = (lo << 16) | (x >> 16);
+      if (static_cast<int>(lo) <= a && (!hb || key > kb)) kb = key, hb = true;
+      if (!ht || key > kt) kt = key, ht = true;
+    }
+    const uint64_t anyb = __ballot(hb);
+#pragma unroll
+    for (int o = 32; o; o >>= 1) {
+      const uint32_t ob = static_cast<uint32_t>(__shfl_xor(static_cast<int>(kb), o));
+      const uint32_t ot = static_cast<uint32_t>(__shfl_xor(static_cast<int>(kt), o));
+      const int obh = __shfl_xor(hb ? 1 : 0, o), oth = __shfl_xor(ht ? 1 : 0, o);
+      if (obh && (!hb || ob > kb)) kb = ob, hb = true;
+      if (oth && (!ht || ot > kt)) kt = ot, ht = true;
+    }
+    if (l == 0) ent[c] = a;
+    const uint32_t key = anyb ? kb : kt;
+    a = n1 - static_cast<int>(key & 0xffffu);
+    m = mn;
+    f = fn;
+  }
+}
+
+// exclusive prefix sum of the per-chunk start counts; cnt[0] = min(H, total) hypotheses this
+// segment delivers (the tuple kernel and the host read it)
+__global__ __launch_bounds__(1024) void k_np_scan(const int *__restrict__ vcnt, int C,
+                                                  int *__restrict__ off, int64_t H,
+                                                  int64_t *__restrict__ got) {
+  __shared__ int sh[16];
+  __shared__ int carry;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (int b = 0; b < C; b += 1024) {
+    const int i = b + tid;
+    const int v = i < C ? vcnt[i] : 0;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) sh[wid] = x;
+    __syncthreads();
+    int base = carry;
+    for (int w = 0; w < wid; ++w) base += sh[w];
+    if (i < C) off[i] = base + x - v;
+    __syncthreads();
+    if (tid == 1023) carry = base + x;
+    __syncthreads();
+  }
+  if (tid == 0) *got = std::min<int64_t>(H, static_cast<int64_t>(carry));
+}
+
 __global__ __launch_bounds__(256) void k_np_starts(const uint2 *__restrict__ ev,
                                                    const int *vcnt, const int *off,
-                                                   int64_t *__restrict__ starts, int64_t H,
-                                                   int ecap, int W) {
+                                                   int64_t *__restrict__ starts,
+                                                   const int64_t *__restrict__ got, int ecap,
+                                                   int W) {
   const int c = blockIdx.x;
   const int n = vcnt[c];
+  const int64_t H = *got;
   const int64_t base = 1 + off[c];
   for (int i = threadIdx.x; i < n; i += 256) {
     const int64_t idx = base + i;
@@ -580,11 +939,11 @@ __global__ __launch_bounds__(256) void k_np_starts(const uint2 *__restrict__ ev,
 // ---- 6. one lane per hypothesis: swap partners, then positions 0..k-1 traced back -----------
 __global__ __launch_bounds__(256) void k_np_tuples(const uint32_t *__restrict__ draws,
                                                    const int64_t *__restrict__ starts,
-                                                   int64_t H, int n1, int kk,
+                                                   const int64_t *__restrict__ got, int n1, int kk,
                                                    uint16_t *__restrict__ jb,
                                                    int32_t *__restrict__ out, int *err) {
   const int64_t h = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (h >= H) return;
+  if (h >= *got) return;
   const int64_t a = starts[h], b = starts[h + 1];
   uint16_t *J = jb + h * n1;
   uint32_t i = static_cast<uint32_t>(n1);
@@ -622,12 +981,12 @@ __global__ __launch_bounds__(256) void k_np_tuples(const uint32_t *__restrict__ 
 constexpr int kTupWaves = 4;
 template <bool PY>
 __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
-    const uint32_t *__restrict__ draws, const int64_t *__restrict__ starts, int64_t H, int n1,
-    int n1p, int kk, int32_t *__restrict__ out, int *err) {
+    const uint32_t *__restrict__ draws, const int64_t *__restrict__ starts,
+    const int64_t *__restrict__ got, int n1, int n1p, int kk, int32_t *__restrict__ out, int *err) {
   extern __shared__ uint16_t jl[];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t h = static_cast<int64_t>(blockIdx.x) * kTupWaves + wv;
-  if (h >= H) return;  // wave-uniform; the kernel has no workgroup barrier
+  if (h >= *got) return;  // wave-uniform; the kernel has no workgroup barrier
   uint16_t *J = jl + static_cast<size_t>(wv) * n1p;
   const int64_t a = starts[h], b = starts[h + 1];
   const uint64_t below = (1ull << l) - 1ull;
@@ -698,6 +1057,32 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
   }
 }
 
+// ---- 7. what the host needs after a segment, in one copy ----------------------------------
+struct NpResult {
+  int64_t got;      // hypotheses delivered
+  int64_t used;     // draws they consumed (starts[got])
+  int32_t err, pad_;
+  uint32_t blk[kN];  // tempered stream block holding the next draw (when pos + used > 624)
+};
+
+__global__ __launch_bounds__(64) void k_np_result(const uint32_t *__restrict__ stream,
+                                                  const int64_t *__restrict__ starts, int pos,
+                                                  const int *__restrict__ err,
+                                                  NpResult *__restrict__ r) {
+  const int l = threadIdx.x;
+  const int64_t got = r->got;
+  const int64_t used = got > 0 ? starts[got] : 0;
+  const int64_t W = pos + used;
+  if (W > kN) {
+    const int64_t b = (W - 1) / kN;
+    for (int t = l; t < kN; t += 64) r->blk[t] = stream[b * kN + t];
+  }
+  if (l == 0) {
+    r->used = used;
+    r->err = *err;
+  }
+}
+
 // ---- host ------------------------------------------------------------------------------------
 struct JumpPolys {
   std::vector<std::vector<int32_t>> bits;  // level k: set bits of x^(2^k kJ) mod phi
@@ -765,6 +1150,7 @@ struct rs_np_work {
       *d_off = nullptr, *d_err = nullptr, *d_tpos = nullptr;
   uint2 *d_ev = nullptr;
   int64_t *d_starts = nullptr;
+  NpResult *d_res = nullptr;
   uint16_t *d_J = nullptr;
   int64_t cap_fin = 0, cap_ev = 0, cap_starts = 0, cap_J = 0;
   int64_t entry_lds = 0, tup_lds = 0;
@@ -777,7 +1163,7 @@ void np_work_free(rs_ctx *c) {
   if (!w) return;
   void *ptrs[] = {w->d_bits, w->d_win, w->d_stream, w->d_fin, w->d_fin_m, w->d_ev_n,
                   w->d_ent,  w->d_vcnt, w->d_off,   w->d_err, w->d_ev,    w->d_starts, w->d_J,
-                  w->d_tpos};
+                  w->d_tpos, w->d_res};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   delete w;
@@ -842,6 +1228,9 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
     w.tup_lds = tup_lds;
   }
   if (!w.d_bits) {
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_mt_jump),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                static_cast<int>(sizeof(uint32_t) * kPrefix)));
     const JumpPolys &jp = jump_polys();
     std::vector<int32_t> all;
     for (const auto &b : jp.bits) {
@@ -859,6 +1248,8 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
         (st = grow(w.d_off, c7, Cmax)) || (st = grow(w.d_err, c8, 1)) ||
         (st = grow(w.d_tpos, c9, Cmax)))
       return st;
+    int64_t c10 = 0;
+    if ((st = grow(w.d_res, c10, 1))) return st;
   }
   const double E = expected_draws(n1, py);
   const int64_t dmax = seg_words() - 3 * kN;
@@ -872,8 +1263,6 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
     w.entry_lds = lds;
   }
-  std::vector<int> fin_m, ev_n, ent, vcnt, off;
-  std::vector<uint32_t> fin;
   int64_t done = 0;
   while (done < count) {
     const int64_t hs = std::min<int64_t>(count - done, hcap);
@@ -881,7 +1270,7 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
     int kWr = kWenv;
     if (!kWr) {
       kWr = kWmin;
-      while (kWr < kW && static_cast<int64_t>(kWr) * 1024 < D) kWr *= 2;
+      while (kWr < kW && static_cast<int64_t>(kWr) * kChunksTarget < D) kWr *= 2;
     }
     const int ecap = static_cast<int>(std::min<int64_t>(
         kWr + 2 * n1, (static_cast<int64_t>(70.0 * kWr / E) + 4 * n1 + 4096) << ecap_shift));
@@ -895,109 +1284,91 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
       return st;
     // 1-2: the word stream from (key, pos): block 0 is the key itself
     HIP_TRY(hipMemcpyAsync(w.d_win, key, sizeof(uint32_t) * kN, hipMemcpyHostToDevice, s));
+    if (G > 1)
+      HIP_TRY(hipMemsetAsync(w.d_win + kN, 0, sizeof(uint32_t) * kN * static_cast<size_t>(G - 1), s));
     for (int half = 1, lv = 0; half < G; half *= 2, ++lv) {
       if (lv >= kLevels) return fail(RS_EINVAL, "np sampler: segment too long");
-      k_mt_jump<<<half, 256 * kJumpGroups, 0, s>>>(w.d_win, half, G, w.d_bits + w.bit_off[lv], w.bit_n[lv]);
+      // parts per jump: about 512 workgroups per level (two per CU)
+      const int S = std::max(1, std::min(64, 512 / half));
+      k_mt_jump<<<half * S, 256 * kJumpGroups, sizeof(uint32_t) * kPrefix, s>>>(
+          w.d_win, half, G, w.d_bits + w.bit_off[lv], w.bit_n[lv], S);
       HIP_TRY(hipGetLastError());
     }
-    k_mt_stream<<<G, 64, 0, s>>>(w.d_win, w.d_stream, Lb);
+    k_mt_stream<<<G, 256, 0, s>>>(w.d_win, w.d_stream, Lb);
     HIP_TRY(hipGetLastError());
     // 3: all-entry parse per chunk
     HIP_TRY(hipMemsetAsync(w.d_err, 0, sizeof(int), s));
+    long long *d_stats = nullptr;
+#ifdef RSAMD_DIAG
+    static const char *stats_path = std::getenv("RSAMD_NP_STATS");
+    if (stats_path) HIP_TRY(hipMalloc(&d_stats, sizeof(long long) * 64 * C));
+    if (d_stats) HIP_TRY(hipMemsetAsync(d_stats, 0, sizeof(long long) * 64 * C, s));
+#endif
     EntryArgs ea{w.d_stream + *pos, D, kWr, n1, w.d_fin, w.d_fin_m, w.d_ev, w.d_ev_n, w.d_tpos,
-                 ecap, w.d_err};
+                 ecap, w.d_err, d_stats};
+    const bool small = n1 < 64;  // several hypothesis ends in one tracking window
     if (py) {
       k_np_entry<true><<<C, kEntryThreads, static_cast<size_t>(lds), s>>>(ea, ea.draws);
       HIP_TRY(hipGetLastError());
-      k_np_sparse<true><<<C, 64, 0, s>>>(ea, ea.draws);
+      (small ? k_np_track<true, true> : k_np_track<true, false>)<<<C, 64 * kTrackWaves, 0, s>>>(ea, ea.draws);
     } else {
       k_np_entry<false><<<C, kEntryThreads, static_cast<size_t>(lds), s>>>(ea, ea.draws);
       HIP_TRY(hipGetLastError());
-      k_np_sparse<false><<<C, 64, 0, s>>>(ea, ea.draws);
+      (small ? k_np_track<false, true> : k_np_track<false, false>)<<<C, 64 * kTrackWaves, 0, s>>>(ea, ea.draws);
     }
     HIP_TRY(hipGetLastError());
-    fin_m.resize(C);
-    ev_n.resize(C);
-    fin.resize(static_cast<size_t>(C) * 64);
-    int err = 0;
-    HIP_TRY(hipMemcpyAsync(fin_m.data(), w.d_fin_m, sizeof(int) * C, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpy2DAsync(fin.data(), 64 * sizeof(uint32_t), w.d_fin, sizeof(uint32_t) * n1,
-                             sizeof(uint32_t) * std::min(64, n1), C, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(&err, w.d_err, sizeof(int), hipMemcpyDeviceToHost, s));
+    // 4-5: compose the chunk maps, keep the true wraps (= hypothesis starts), gather them
+    k_np_compose<<<1, 64, 0, s>>>(w.d_fin, w.d_fin_m, n1, C, w.d_ent);
+    HIP_TRY(hipGetLastError());
+    k_np_filter<<<C, 64, 0, s>>>(w.d_ev, w.d_ev_n, w.d_ent, w.d_vcnt, ecap);
+    HIP_TRY(hipGetLastError());
+    k_np_scan<<<1, 1024, 0, s>>>(w.d_vcnt, C, w.d_off, hs, &w.d_res->got);
+    HIP_TRY(hipGetLastError());
+    k_np_starts<<<C, 256, 0, s>>>(w.d_ev, w.d_vcnt, w.d_off, w.d_starts, &w.d_res->got, ecap, kWr);
+    HIP_TRY(hipGetLastError());
+    // 6: tuples (launched for hs hypotheses; waves beyond the delivered count exit)
+    if (lane_tuples && !py) {
+      k_np_tuples<<<static_cast<unsigned>((hs + 255) / 256), 256, 0, s>>>(
+          w.d_stream + *pos, w.d_starts, &w.d_res->got, n1, k, w.d_J, d_out + done * k, w.d_err);
+    } else {
+      const int n1p = (n1 + 1) & ~1;
+      (py ? k_np_tuples_wave<true> : k_np_tuples_wave<false>)<<<static_cast<unsigned>((hs + kTupWaves - 1) / kTupWaves), 64 * kTupWaves,
+                         sizeof(uint16_t) * n1p * kTupWaves, s>>>(
+          w.d_stream + *pos, w.d_starts, &w.d_res->got, n1, n1p, k, d_out + done * k, w.d_err);
+    }
+    HIP_TRY(hipGetLastError());
+    // 7: delivered count, draws used, errors and the stream block holding the next word
+    k_np_result<<<1, 64, 0, s>>>(w.d_stream, w.d_starts, *pos, w.d_err, w.d_res);
+    HIP_TRY(hipGetLastError());
+    NpResult res;
+    HIP_TRY(hipMemcpyAsync(&res, w.d_res, sizeof(res), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    if (err & 1) {  // wrap log overflow: a larger log and the same segment again
+#ifdef RSAMD_DIAG
+    if (d_stats) {
+      std::vector<long long> hst(static_cast<size_t>(64) * C);
+      HIP_TRY(hipMemcpy(hst.data(), d_stats, sizeof(long long) * hst.size(), hipMemcpyDeviceToHost));
+      if (FILE *f = std::fopen(stats_path, "ab")) {
+        const int64_t hdr[4] = {n1, C, kWr, D};
+        std::fwrite(hdr, sizeof(hdr), 1, f);
+        std::fwrite(hst.data(), sizeof(long long), hst.size(), f);
+        std::fclose(f);
+      }
+      (void)hipFree(d_stats);
+    }
+#endif
+    if (res.err & 1) {  // wrap log overflow: a larger log and the same segment again
       if (ecap >= kWr + 2 * n1) return fail(RS_EDEVICE, "np sampler: wrap log overflow");
       ++ecap_shift;
       continue;
     }
-    // 4: compose the chunk maps; entry list index a <-> state n1 - a; chunk 0 starts a hypothesis
-    ent.resize(C);
-    // chunks that ended dense (m > 64): their full lists in one copy of the row range
-    int cb0 = C, cb1 = -1, mb = 0;
-    for (int ci = 0; ci < C; ++ci)
-      if (fin_m[ci] > 64) cb0 = std::min(cb0, ci), cb1 = ci, mb = std::max(mb, fin_m[ci]);
-    std::vector<uint32_t> big;
-    if (cb1 >= cb0) {  // the first mb entries of each row in the range (rows are n1 long)
-      big.resize(static_cast<size_t>(cb1 - cb0 + 1) * mb);
-      HIP_TRY(hipMemcpy2D(big.data(), sizeof(uint32_t) * mb, w.d_fin + static_cast<size_t>(cb0) * n1,
-                          sizeof(uint32_t) * n1, sizeof(uint32_t) * mb, cb1 - cb0 + 1,
-                          hipMemcpyDeviceToHost));
-    }
-    int a = 0;
-    for (int ci = 0; ci < C; ++ci) {
-      ent[ci] = a;
-      const int m = fin_m[ci];
-      const uint32_t *f = m > 64 ? big.data() + static_cast<size_t>(ci - cb0) * mb
-                                 : fin.data() + static_cast<size_t>(ci) * 64;
-      int best = -1, bst = 0, top = -1, tst = 0;
-      for (int i = 0; i < m; ++i) {
-        const int lo = static_cast<int>(f[i] & 0xffffu), sv = static_cast<int>(f[i] >> 16);
-        if (lo <= a && lo > best) best = lo, bst = sv;
-        if (lo > top) top = lo, tst = sv;
-      }
-      a = n1 - (best >= 0 ? bst : tst);
-    }
-    HIP_TRY(hipMemcpyAsync(w.d_ent, ent.data(), sizeof(int) * C, hipMemcpyHostToDevice, s));
-    // 5: the true wraps = hypothesis starts
-    k_np_filter<<<C, 64, 0, s>>>(w.d_ev, w.d_ev_n, w.d_ent, w.d_vcnt, ecap);
-    HIP_TRY(hipGetLastError());
-    vcnt.resize(C);
-    HIP_TRY(hipMemcpyAsync(vcnt.data(), w.d_vcnt, sizeof(int) * C, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    off.resize(C);
-    int64_t tot = 0;
-    for (int ci = 0; ci < C; ++ci) {
-      off[ci] = static_cast<int>(tot);
-      tot += vcnt[ci];
-    }
-    const int64_t got = std::min<int64_t>(hs, tot);
+    if (res.err) return fail(RS_EDEVICE, "np sampler: hypothesis parse mismatch");
+    const int64_t got = res.got;
     if (got < 1) return fail(RS_EDEVICE, "np sampler: segment holds no complete hypothesis");
-    HIP_TRY(hipMemcpyAsync(w.d_off, off.data(), sizeof(int) * C, hipMemcpyHostToDevice, s));
-    k_np_starts<<<C, 256, 0, s>>>(w.d_ev, w.d_vcnt, w.d_off, w.d_starts, got, ecap, kWr);
-    HIP_TRY(hipGetLastError());
-    // 6: tuples
-    if (lane_tuples && !py) {
-      k_np_tuples<<<static_cast<unsigned>((got + 255) / 256), 256, 0, s>>>(
-          w.d_stream + *pos, w.d_starts, got, n1, k, w.d_J, d_out + done * k, w.d_err);
-    } else {
-      const int n1p = (n1 + 1) & ~1;
-      (py ? k_np_tuples_wave<true> : k_np_tuples_wave<false>)<<<static_cast<unsigned>((got + kTupWaves - 1) / kTupWaves), 64 * kTupWaves,
-                         sizeof(uint16_t) * n1p * kTupWaves, s>>>(
-          w.d_stream + *pos, w.d_starts, got, n1, n1p, k, d_out + done * k, w.d_err);
-    }
-    HIP_TRY(hipGetLastError());
-    int64_t used = 0;
-    HIP_TRY(hipMemcpyAsync(&used, w.d_starts + got, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(&err, w.d_err, sizeof(int), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    if (err) return fail(RS_EDEVICE, "np sampler: hypothesis parse mismatch");
     // state after `used` draws: the block holding the next word (rs_mt_jump's convention)
-    const int64_t W = *pos + used;
+    const int64_t W = *pos + res.used;
     if (W > kN) {
       const int64_t b = (W - 1) / kN;
-      uint32_t blk[kN];
-      HIP_TRY(hipMemcpy(blk, w.d_stream + b * kN, sizeof(blk), hipMemcpyDeviceToHost));
-      for (int i = 0; i < kN; ++i) key[i] = untemper(blk[i]);
+      for (int i = 0; i < kN; ++i) key[i] = untemper(res.blk[i]);
       *pos = static_cast<int32_t>(W - b * kN);
     } else {
       *pos = static_cast<int32_t>(W);
