@@ -11,10 +11,10 @@ if len(sys.argv) > 2 and sys.argv[1] == "--read":
     p = 0
     while p < raw.size:
         n1, C, kW, D = raw[p:p + 4]
-        st = raw[p + 4:p + 4 + 64 * C].reshape(C, 64)
-        p += 4 + 64 * C
-        w = st[:, :48].reshape(C, 8, 6)  # per wave: windows, cyc1, cycN, n1, nN, intervals
-        kern = st[:, 60]
+        st = raw[p + 4:p + 4 + 128 * C].reshape(C, 128)
+        p += 4 + 128 * C
+        w = st[:, :96].reshape(C, 16, 6)  # per wave: windows, cyc1, cycN, n1, nN, intervals
+        kern = st[:, 120]
         print(f"n1={n1} C={C} kW={kW} D={D}")
         print(f"  kernel cycles per chunk: mean {kern.mean():.3g} max {kern.max():.3g}")
         c1, cN = w[:, :, 1], w[:, :, 2]

@@ -486,7 +486,7 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a,
 // same trajectory from then on, so all but the first of each run of equal states (cyclic order
 // is preserved by the parse) are dropped, and the survivor's member range extends to the next
 // survivor's start.  Wraps are logged with the member range as in k_np_entry.
-constexpr int kTrackWaves = 8;
+constexpr int kTrackWaves = 16;
 constexpr int kCheck = 4096;
 
 template <bool PY, bool SMALL>
@@ -814,9 +814,9 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_np_track(EntryArgs a,
   }
 #ifdef RSAMD_DIAG
   if (a.stats && lane == 0) {
-    long long *o = a.stats + static_cast<size_t>(c) * 64 + wv * 6;
+    long long *o = a.stats + static_cast<size_t>(c) * 128 + wv * 6;
     for (int k = 0; k < 6; ++k) o[k] = dg[k];
-    if (wv == 0) a.stats[static_cast<size_t>(c) * 64 + 60] = __builtin_amdgcn_s_memtime() - k0;
+    if (wv == 0) a.stats[static_cast<size_t>(c) * 128 + 120] = __builtin_amdgcn_s_memtime() - k0;
   }
 #else
   (void)dg;
@@ -848,43 +848,53 @@ __global__ __launch_bounds__(64) void k_np_filter(uint2 *__restrict__ ev, const 
   if (l == 0) vcnt[c] = cnt;
 }
 
-// ---- 4. compose the chunk maps on the GPU (one wave, serial over chunks) -----------------
-// Chunk c's final list maps entry list index a (state n1 - a) to the state of the first entry
-// with the largest start lo <= a (cyclically: the largest lo overall if none); chunk 0 starts
-// a hypothesis (a = 0).  Keys lo << 16 | state: their maximum is the wanted entry.  The rows
-// of chunk c + 1 are loaded while chunk c's reduction runs.
-__global__ __launch_bounds__(64) void k_np_compose(const uint32_t *__restrict__ fin,
-                                                   const int *__restrict__ fin_m, int n1, int C,
-                                                   int *__restrict__ ent) {
-  const int l = threadIdx.x;
+// ---- 4. compose the chunk maps on the GPU ------------------------------------------------
+// Chunk c's final list maps entry list index a (state n1 - a) to the state of the entry with the
+// largest start lo <= a (cyclically: the largest lo overall if none); chunk 0 starts a
+// hypothesis (a = 0).  Keys lo << 16 | state: their maximum is the wanted entry.  The whole
+// workgroup stages the first 64 entries of kComposeBlock chunks at a time in LDS (coalesced),
+// then wave 0 walks them serially; longer lists (chunks that ended dense) are read from HBM.
+constexpr int kComposeBlock = 256;
+__global__ __launch_bounds__(1024) void k_np_compose(const uint32_t *__restrict__ fin,
+                                                     const int *__restrict__ fin_m, int n1, int C,
+                                                     int *__restrict__ ent) {
+  __shared__ uint32_t rows[kComposeBlock][64];
+  __shared__ int ms[kComposeBlock];
+  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
   int a = 0;
-  int m = fin_m[0];
-  uint32_t f = l < m ? fin[l] : 0u;
-  for (int c = 0; c < C; ++c) {
-    const int mn = c + 1 < C ? fin_m[c + 1] : 0;
-    const uint32_t fn = l < mn ? fin[static_cast<size_t>(c + 1) * n1 + l] : 0u;
-    uint32_t kb = 0, kt = 0;  // best key with lo <= a, top key (0: none; keys of valid rows are
-    bool hb = false, ht = false;  //  nonzero only if lo or state is, so flags are kept apart)
-    for (int k = l; k < m; k += 64) {
-      const uint32_t x = k < 64 ? f : fin[static_cast<size_t>(c) * n1 + k];
-      const uint32_t lo = x & 0xffffu, key = (lo << 16) | (x >> 16);
-      if (static_cast<int>(lo) <= a && (!hb || key > kb)) kb = key, hb = true;
-      if (!ht || key > kt) kt = key, ht = true;
+  for (int c0 = 0; c0 < C; c0 += kComposeBlock) {
+    const int nb = min(kComposeBlock, C - c0);
+    for (int k = tid; k < nb; k += 1024) ms[k] = fin_m[c0 + k];
+    __syncthreads();
+    for (int r = wv; r < nb; r += 16) {
+      const int m = ms[r];
+      rows[r][l] = l < m ? fin[static_cast<size_t>(c0 + r) * n1 + l] : 0u;
     }
-    const uint64_t anyb = __ballot(hb);
+    __syncthreads();
+    if (wv == 0) {
+      for (int r = 0; r < nb; ++r) {
+        const int c = c0 + r, m = ms[r];
+        uint32_t kb = 0, kt = 0;
+        bool hb = false, ht = false;
+        for (int k = l; k < m; k += 64) {
+          const uint32_t x = k < 64 ? rows[r][k] : fin[static_cast<size_t>(c) * n1 + k];
+          const uint32_t lo = x & 0xffffu, key = (lo << 16) | (x >> 16);
+          if (static_cast<int>(lo) <= a && (!hb || key > kb)) kb = key, hb = true;
+          if (!ht || key > kt) kt = key, ht = true;
+        }
+        const uint64_t anyb = __ballot(hb);
+        // keys of valid rows are distinct; invalid lanes hold 0 and lose every max below
+        uint32_t mb = hb ? kb : 0u, mt = ht ? kt : 0u;
 #pragma unroll
-    for (int o = 32; o; o >>= 1) {
-      const uint32_t ob = static_cast<uint32_t>(__shfl_xor(static_cast<int>(kb), o));
-      const uint32_t ot = static_cast<uint32_t>(__shfl_xor(static_cast<int>(kt), o));
-      const int obh = __shfl_xor(hb ? 1 : 0, o), oth = __shfl_xor(ht ? 1 : 0, o);
-      if (obh && (!hb || ob > kb)) kb = ob, hb = true;
-      if (oth && (!ht || ot > kt)) kt = ot, ht = true;
+        for (int o = 32; o; o >>= 1) {
+          mb = max(mb, static_cast<uint32_t>(__shfl_xor(static_cast<int>(mb), o)));
+          mt = max(mt, static_cast<uint32_t>(__shfl_xor(static_cast<int>(mt), o)));
+        }
+        if (l == 0) ent[c] = a;
+        a = n1 - static_cast<int>((anyb ? mb : mt) & 0xffffu);
+      }
     }
-    if (l == 0) ent[c] = a;
-    const uint32_t key = anyb ? kb : kt;
-    a = n1 - static_cast<int>(key & 0xffffu);
-    m = mn;
-    f = fn;
+    __syncthreads();
   }
 }
 
@@ -1301,8 +1311,8 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
     long long *d_stats = nullptr;
 #ifdef RSAMD_DIAG
     static const char *stats_path = std::getenv("RSAMD_NP_STATS");
-    if (stats_path) HIP_TRY(hipMalloc(&d_stats, sizeof(long long) * 64 * C));
-    if (d_stats) HIP_TRY(hipMemsetAsync(d_stats, 0, sizeof(long long) * 64 * C, s));
+    if (stats_path) HIP_TRY(hipMalloc(&d_stats, sizeof(long long) * 128 * C));
+    if (d_stats) HIP_TRY(hipMemsetAsync(d_stats, 0, sizeof(long long) * 128 * C, s));
 #endif
     EntryArgs ea{w.d_stream + *pos, D, kWr, n1, w.d_fin, w.d_fin_m, w.d_ev, w.d_ev_n, w.d_tpos,
                  ecap, w.d_err, d_stats};
@@ -1318,7 +1328,7 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
     }
     HIP_TRY(hipGetLastError());
     // 4-5: compose the chunk maps, keep the true wraps (= hypothesis starts), gather them
-    k_np_compose<<<1, 64, 0, s>>>(w.d_fin, w.d_fin_m, n1, C, w.d_ent);
+    k_np_compose<<<1, 1024, 0, s>>>(w.d_fin, w.d_fin_m, n1, C, w.d_ent);
     HIP_TRY(hipGetLastError());
     k_np_filter<<<C, 64, 0, s>>>(w.d_ev, w.d_ev_n, w.d_ent, w.d_vcnt, ecap);
     HIP_TRY(hipGetLastError());
@@ -1345,7 +1355,7 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
     HIP_TRY(hipStreamSynchronize(s));
 #ifdef RSAMD_DIAG
     if (d_stats) {
-      std::vector<long long> hst(static_cast<size_t>(64) * C);
+      std::vector<long long> hst(static_cast<size_t>(128) * C);
       HIP_TRY(hipMemcpy(hst.data(), d_stats, sizeof(long long) * hst.size(), hipMemcpyDeviceToHost));
       if (FILE *f = std::fopen(stats_path, "ab")) {
         const int64_t hdr[4] = {n1, C, kWr, D};
