@@ -59,7 +59,17 @@ class Dist:
         if world > 1:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("gloo")
+            # gloo prints its connection banner on fd 1: keep stdout for the one JSON line
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                dist.init_process_group("gloo")
+                dist.barrier()
+            finally:
+                sys.stdout.flush()
+                os.dup2(saved, 1)
+                os.close(saved)
             self.dist = dist
 
     def barrier(self):
@@ -118,10 +128,15 @@ def cpu_baseline(p1, p2, budget_s, procs):
 
 
 class _CtxComm:
-    """All-gather over the RCCL communicator already initialised on ``ctx``."""
+    """All-gather / max-all-reduce over the RCCL communicator already initialised on ``ctx``."""
 
     def __init__(self, ctx, rank, world):
         self.ctx, self.rank, self.world = ctx, rank, world
+
+    def allreduce_max_int(self, v):
+        x = ctypes.c_int64(int(v))
+        _ffi.check(_ffi.lib().rs_comm_allreduce_max_i64(self.ctx.handle, ctypes.byref(x)))
+        return int(x.value)
 
     def allgather_bytes(self, b):
         n = len(b)
@@ -145,12 +160,18 @@ class _GlooComm:
         self.dist.dist.all_gather_object(out, b)
         return out
 
+    def allreduce_max_int(self, v):
+        return int(self.dist.max(float(v)))
+
 
 class _Solo:
     rank, world = 0, 1
 
     def allgather_bytes(self, b):
         return [b]
+
+    def allreduce_max_int(self, v):
+        return int(v)
 
 
 def _best_of(f, reps):
@@ -343,6 +364,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity-mode", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--no-fp64-count", action="store_true")
+    ap.add_argument("--fp64-steps", type=int, default=20)
     args = ap.parse_args()
 
     rank, local_rank, world = dist_env()
@@ -358,8 +381,9 @@ def main():
     # box (RCCL refuses two ranks on one GPU, so that run exercises the gloo exchange)
     ctx = _ffi.Context(int(os.environ.get("RSAMD_BENCH_DEVICE", local_rank)))
 
-    # one synthetic pair per rank (weak scaling: per-GPU work fixed)
+    # one synthetic pair per rank (weak scaling: per-GPU work fixed); p0_* is rank 0's pair
     p1, p2, _ = synth.two_view(args.n, OUTLIERS, seed=1 + rank)
+    p0_1, p0_2, _ = synth.two_view(args.n, OUTLIERS, seed=1)
     H = args.hyps
     plan = _ffi.F8Plan(ctx, args.n, H)
     plan.set_points(p1, p2)
@@ -454,13 +478,15 @@ def main():
                                                           "k_f8_count32"),
                      "achieved": achieved, "peak": PEAK_FP32_VALU_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_FP32_VALU_TFLOPS,
-                     "frac_of_fp64_peak": achieved / PEAK_FP64_VALU_TFLOPS,
                      "traffic": pmc,
                      "per_launch": {"hypotheses": H, "flop": H * FLOP_PER_CORR * args.n,
                                     "avg_ms": c_ms, "timed_launches_every": TIMING_EVERY},
-                     "whole_run": {"flop_per_hypothesis": FLOP_PER_CORR * args.n + FLOP_SOLVE,
-                                   "achieved": value * (FLOP_PER_CORR * args.n + FLOP_SOLVE)
-                                   / 1e12},
+                     "whole_run_nominal": {
+                         "flop_per_hypothesis": FLOP_PER_CORR * args.n + FLOP_SOLVE,
+                         "tflops": value * (FLOP_PER_CORR * args.n + FLOP_SOLVE) / 1e12,
+                         "note": "SURVEY.md 8(d)'s nominal 15 000 flop per solve is an SVD "
+                                 "estimate; the LQ solve does far less, so this is not a "
+                                 "roofline figure"},
                      "note": "vector-ALU (issue) bound, SURVEY.md 8(d): 42 flop per "
                              "(hypothesis, correspondence) algorithmic; HBM traffic per launch "
                              "from rocprofv3 PMC in profiles/ (traffic, bytes)"},
@@ -472,31 +498,76 @@ def main():
                                 "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                 "frac": pmc / (c_ms * 1e-3) / 1e9 / PEAK_HBM_GBS}
 
-    if rank == 0 and world == 1 and not args.no_parity_mode:
+    if not args.no_fp64_count:
+        # the plain float64 counting kernel on the same runs: the precision question settled
+        # by measurement (identical counts; bounded by the FP64 vector peak)
+        plan.set_count_precision(True)
+        for i in range(20):
+            step(i)
+        plan.result()
+        dist.barrier()
+        t = time.perf_counter()
+        for i in range(args.fp64_steps):
+            step(i)
+        plan.result()
+        el64 = dist.max(time.perf_counter() - t)
+        k64 = plan.kernel_ms(last_n=args.fp64_steps)["count_ms"]
+        plan.set_count_precision(False)
+        a64 = H * FLOP_PER_CORR * args.n / (k64 * 1e-3) / 1e12
+        line["fp64_count"] = {"value": H * args.fp64_steps * world / el64,
+                              "unit": "hypotheses/s", "kernel": "k_f8_count",
+                              "kernel_ms": k64, "achieved": a64, "peak": PEAK_FP64_VALU_TFLOPS,
+                              "unit_roofline": "TFLOP/s", "frac": a64 / PEAK_FP64_VALU_TFLOPS,
+                              "note": "RANSAC runs with the plain float64 counting kernel "
+                                      "(reference-order residuals); counts are bit-identical "
+                                      "to the fp32 + exact-guard-band default"}
+
+    if not args.no_parity_mode:
         # numpy-exact sampling + the same GPU pipeline: the np.random stream parsed on the
-        # GPU (rs_f8_plan_run_np), and the serial host replay for comparison
+        # GPU (rs_f8_plan_run_np).  Weak: every rank its own pair's run.  Sharded: ONE pair's
+        # H hypotheses split over the ranks (rs_f8_plan_run_np_slice + c* all-reduce and
+        # candidate all-gather), the fun.py:320-328 decision replayed on every rank.
+        from tsbb15_amd import parallel
         key0, pos0 = _ffi.np_seed(0)
         tg = []
         for _ in range(6):
+            dist.barrier()
             t = time.perf_counter()
             plan.run_np(H, key0, pos0)
             plan.result()
-            tg.append(time.perf_counter() - t)
-        th = []
-        for _ in range(2):
-            t = time.perf_counter()
-            tup, _, _ = _ffi.np_choice_tuples(key0, pos0, args.n, 8, H)
-            plan.run(H, mode=_ffi.SAMPLER_TUPLES, tuples=tup)
-            plan.result()
-            th.append(time.perf_counter() - t)
-        line["parity_mode"] = {"value": H / min(tg[1:]), "unit": "hypotheses/s",
-                               "ms": 1e3 * min(tg[1:]),
-                               "host_replay_value": H / min(th),
-                               "note": "np.random legacy stream (seed 0) reproduced bit-exactly "
-                                       "on the GPU (MT19937 jump-ahead windows, all-entry-state "
-                                       "chunk parse, per-hypothesis swap trace), then the same "
-                                       "GPU pipeline; host_replay_value = the serial replay on "
-                                       "one host core feeding the same pipeline"}
+            tg.append(dist.max(time.perf_counter() - t))
+        pm = {"value": world * H / min(tg[1:]), "unit": "hypotheses/s",
+              "ms": 1e3 * min(tg[1:]), "scaling": "weak", "n_gpus": world,
+              "note": "np.random legacy stream (seed 0) reproduced bit-exactly on the GPU "
+                      "(MT19937 jump-ahead windows, all-entry-state chunk parse + windowed "
+                      "tracking, per-hypothesis swap trace), then the same GPU pipeline; one "
+                      "pair per rank"}
+        if world > 1:
+            c = xcomm
+            ev = parallel.GpuSliceEvaluator(ctx, p0_1, p0_2, H, max_slice=H // world + 1)
+            ts = []
+            for _ in range(4):
+                dist.barrier()
+                t = time.perf_counter()
+                best, _, _ = parallel.ransac_f_sharded_np(c, p0_1, p0_2, H, key0, pos0, ev)
+                ts.append(dist.max(time.perf_counter() - t))
+            ev.close()
+            pm["sharded"] = {"value": H / min(ts[1:]), "unit": "hypotheses/s",
+                             "ms": 1e3 * min(ts[1:]), "scaling": "strong", "n_gpus": world,
+                             "best_index": int(best["index"]) if best is not None else -1,
+                             "note": "one pair's H hypotheses over all ranks: each parses the "
+                                     "whole stream, evaluates its slice; c* all-reduce + "
+                                     "candidate all-gather"}
+        if rank == 0 and world == 1:
+            th = []
+            for _ in range(2):
+                t = time.perf_counter()
+                tup, _, _ = _ffi.np_choice_tuples(key0, pos0, args.n, 8, H)
+                plan.run(H, mode=_ffi.SAMPLER_TUPLES, tuples=tup)
+                plan.result()
+                th.append(time.perf_counter() - t)
+            pm["host_replay_value"] = H / min(th)
+        line["parity_mode"] = pm
     if cpu is not None:
         line["cpu_baseline"] = cpu
     if not args.no_extras:

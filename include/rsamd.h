@@ -161,12 +161,22 @@ int rs_f8_plan_run(rs_f8_plan *plan, int64_t H, int32_t mode, uint64_t seed, uin
  * (key, pos) in place.  Populations beyond the GPU parse (n - 1 > 10240) use the host replay. */
 int rs_f8_plan_run_np(rs_f8_plan *plan, int64_t H, uint32_t *mt_key, int32_t *mt_pos,
                       double thresh);
+/* Hypotheses [start, start + count) of that H-hypothesis parity run (one rank's shard of the
+ * fun.py:303-328 loop): the stream of all H hypotheses is parsed on the GPU,
+ * only the slice's tuples are produced and evaluated (candidate indices are local; add start),
+ * and (key, pos) advance past all H, exactly as rs_f8_plan_run_np. */
+int rs_f8_plan_run_np_slice(rs_f8_plan *plan, int64_t H, int64_t start, int64_t count,
+                            uint32_t *mt_key, int32_t *mt_pos, double thresh);
 /* Wait for the last run and copy its result; inliers (S_RANSAC, ascending) up to cap. */
 int rs_f8_plan_result(rs_f8_plan *plan, rs_f8_result *out, int64_t *inliers, int64_t cap,
                       int64_t *n_inliers);
 /* Candidates (count == max re-scored count) of the last run, ascending index, up to cap. */
 int rs_f8_plan_candidates(rs_f8_plan *plan, rs_f8_candidate *out, int64_t cap, int64_t *n_out);
 /* Per-hypothesis fast counts / models of the last run (test & diagnostics). */
+/* Counting precision of later runs: fp64 != 0 selects the plain float64 counting kernel
+ * (reference-order residuals, no fp32 filter); 0 (default) the fp32 kernel with its exact
+ * float64 guard band.  Both give bit-identical counts; fp64 is the slower reference form. */
+int rs_f8_plan_set_count_precision(rs_f8_plan *plan, int32_t fp64);
 int rs_f8_plan_counts(rs_f8_plan *plan, int32_t *counts, int64_t H);
 int rs_f8_plan_models(rs_f8_plan *plan, double *F_out, int64_t H);
 /* Device time (ms, HIP events on the plan's stream) of the counting kernel, the solve kernel

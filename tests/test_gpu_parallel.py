@@ -66,6 +66,55 @@ def test_rccl_world_one_sharded_api(ctx):
     assert np.array_equal(inl, rinl)
 
 
+def test_parity_mode_slices_reproduce_run_np(ctx):
+    """Parity-mode sharding in one process: four slices of a C2-sized numpy-stream run
+    (rs_f8_plan_run_np_slice), merged by the fun.py:320-328 replay, equal the single run_np:
+    winner, count, and the advanced stream state of every slice."""
+    p1, p2, _ = synth.two_view(2000, 0.3, seed=1)
+    H = 100_000
+    key, pos = _ffi.np_seed(0)
+    plan = _ffi.F8Plan(ctx, 2000, H)
+    plan.set_points(p1, p2)
+    rkey, rpos = plan.run_np(H, key, pos)
+    ref, ref_inl = plan.result()
+    ref_counts = plan.counts(H)
+    plan.close()
+    ev = parallel.GpuSliceEvaluator(ctx, p1, p2, H, max_slice=H // 4 + 1)
+    parts = []
+    try:
+        for w in range(4):
+            lo, n = parallel.shard_range(H, 4, w)
+            local, k2, p2_ = ev(lo, n, key, pos)
+            assert p2_ == rpos and np.array_equal(k2, rkey)
+            assert np.array_equal(ev.plan.counts(n), ref_counts[lo:lo + n])
+            parts.append(local)
+        allc = np.concatenate(parts)
+        win = parallel.replay_rule(allc[allc["count"] == allc["count"].max()])
+        assert int(win["index"]) == ref.best_index and int(win["count"]) == ref.best_count
+        assert np.array_equal(ev.inliers(win), ref_inl)
+    finally:
+        ev.close()
+
+
+def test_rccl_world_one_parity_mode(ctx):
+    """ransac_f_sharded_np over the RCCL communicator at world size 1 = run_np, and the C2
+    reference golden (tests/golden/full_c2.npz: winner of the unmodified loop at 1e5)."""
+    z, b = golden("full_c2.npz"), golden("synth_c2.npz")
+    H = int(z["H"])
+    comm = parallel.RcclComm(ctx, 0, 1, _Boot())
+    ev = parallel.GpuSliceEvaluator(ctx, b["p1"], b["p2"], H)
+    try:
+        key, pos = parallel.np_state(np.random.RandomState(0))
+        best, key2, pos2 = parallel.ransac_f_sharded_np(comm, b["p1"], b["p2"], H, key, pos, ev)
+        inl = ev.inliers(best)
+    finally:
+        ev.close()
+        comm.close()
+    assert int(best["index"]) == int(z["best"])
+    assert np.array_equal(inl, z["S_ransac"].astype(np.int64))
+    assert pos2 == int(z["mt_pos_out"]) and np.array_equal(key2, z["mt_key_out"])
+
+
 def _dino_pairs():
     z = golden("dino_pnp_kat.npz")
     P = z["points2d"]

@@ -61,7 +61,28 @@ def _worker(rank, world, port, case, q):
                             world_size=world)
     comm = parallel.TorchComm()
     try:
-        if case["kind"] == "shard":
+        if case["kind"] == "shard_np":
+            # parity mode: the stream's tuples from the host replay of numpy's choice (pinned to
+            # numpy in tests/test_samplers.py), the slice evaluated by the oracle
+            p1, p2, H = case["p1"], case["p2"], case["H"]
+            key, pos = parallel.np_state(np.random.RandomState(case["seed"]))
+
+            def evaluate(start, cnt, key, pos):
+                from tsbb15_amd import _ffi
+                tup, key2, pos2 = _ffi.np_choice_tuples(key, pos, p1.shape[1], 8, H)
+                rec = np.zeros(cnt, dtype=parallel.CAND_DTYPE)
+                for k, h in enumerate(range(start, start + cnt)):
+                    F = ransac_ref.fmatrix_stls(p1[:, tup[h]], p2[:, tup[h]])
+                    d = ransac_ref.inlier_distance(F, p1, p2)
+                    with np.errstate(all="ignore"):
+                        rec[k] = (h, np.count_nonzero(d < 1.5), np.std(d), np.linalg.norm(d),
+                                  F.ravel())
+                return rec, key2, pos2
+            best, key2, pos2 = parallel.ransac_f_sharded_np(comm, p1, p2, H, key, pos, evaluate)
+            F = best["F"].reshape(3, 3)
+            S = np.flatnonzero(ransac_ref.inlier_distance(F, p1, p2) < 1.5)
+            q.put((rank, (int(best["index"]), S, F, key2, pos2), None))
+        elif case["kind"] == "shard":
             p1, p2, H = case["p1"], case["p2"], case["H"]
             F, S, _, best, tr = _oracle_trace(p1, p2, H)
             lo, n = parallel.shard_range(H, world, rank)
@@ -139,6 +160,23 @@ def test_gloo_hypothesis_sharding_equals_single_process(world):
     out = _spawn(world, {"kind": "shard", "p1": p1, "p2": p2, "H": 240})
     for rank, idx, best in out:
         assert idx == best
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_parity_mode_sharding_equals_single_process(world):
+    """Parity mode sharded over gloo ranks: winner, S_RANSAC, F_RANSAC and the advanced MT
+    state equal the single-process oracle loop on the same np.random stream."""
+    p1, p2, _ = synth.two_view(150, 0.3, seed=23)
+    H, seed = 241, 5
+    out = _spawn(world, {"kind": "shard_np", "p1": p1, "p2": p2, "H": H, "seed": seed})
+    rs = np.random.RandomState(seed)
+    F, S, _, best, _ = ransac_ref.ransac_f(p1, p2, r=H, rng=rs)
+    st = rs.get_state()
+    for rank, (idx, S_r, F_r, key2, pos2), _ in out:
+        assert idx == best
+        assert np.array_equal(S_r, S)
+        np.testing.assert_array_equal(F_r, F)
+        assert pos2 == st[2] and np.array_equal(key2, np.asarray(st[1], np.uint32))
 
 
 def test_gloo_hypothesis_sharding_all_ties():

@@ -24,7 +24,11 @@ int hip_fail(hipError_t e, const char *what);
 int ensure_scratch(rs_ctx *c, size_t bytes);
 void np_work_free(rs_ctx *c);
 bool np_gpu_supported(int64_t n, int32_t k);  // within the GPU parse's population range
+// The numpy (py: CPython) stream's next `count` choice(n, k) tuples; rows [skip, skip + take)
+// (take < 0: to the end) are written to d_out (take * k int32); (key, pos) advance past all
+// `count`.  Synchronous on the context stream.
 int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t k,
-                     int64_t count, int32_t *d_out, bool py = false);
+                     int64_t count, int32_t *d_out, bool py = false, int64_t skip = 0,
+                     int64_t take = -1);
 int fmatrix_stls_lsq(rs_ctx *c, const double *pl, const double *pr, int64_t n, double *F_out);
 }  // namespace rs

@@ -619,18 +619,29 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
 // on the context stream, and that buffer set was last read by run k-2's solve, which precedes
 // it in stream order.  The two-stream overlap variant reads tuples on its own stream: it and
 // populations beyond the GPU parse's range go through the host replay.
-extern "C" int rs_f8_plan_run_np(rs_f8_plan *p, int64_t H, uint32_t *key, int32_t *pos,
-                                 double thresh) {
+extern "C" int rs_f8_plan_run_np_slice(rs_f8_plan *p, int64_t H, int64_t start, int64_t count,
+                                       uint32_t *key, int32_t *pos, double thresh) {
   if (!p || !key || !pos) return fail(RS_EINVAL, "null pointer");
+  if (H < 1 || start < 0 || count < 1 || start + count > H)
+    return fail(RS_EINVAL, "hypothesis slice out of range");
+  if (count > p->max_hyp) return fail(RS_EINVAL, "hypothesis count out of plan range");
   int st;
   if (!p->overlap && rs::np_gpu_supported(p->n, 8) && std::getenv("RSAMD_NP_HOST") == nullptr) {
     RunBufs &b = p->buf[p->runs % rs_f8_plan::kBufs];
-    if ((st = rs::np_choice_device(p->ctx, key, pos, p->n, 8, H, b.d_tuples))) return st;
-    return plan_run(p, H, RS_SAMPLER_TUPLES, 0, 0, nullptr, thresh, true);
+    if ((st = rs::np_choice_device(p->ctx, key, pos, p->n, 8, H, b.d_tuples, false, start, count)))
+      return st;
+    return plan_run(p, count, RS_SAMPLER_TUPLES, 0, static_cast<uint64_t>(start), nullptr, thresh,
+                    true);
   }
   std::vector<int32_t> tuples(static_cast<size_t>(8 * H));
   if ((st = rs_np_choice_tuples(key, pos, p->n, 8, H, tuples.data()))) return st;
-  return plan_run(p, H, RS_SAMPLER_TUPLES, 0, 0, tuples.data(), thresh, false);
+  return plan_run(p, count, RS_SAMPLER_TUPLES, 0, static_cast<uint64_t>(start),
+                  tuples.data() + 8 * start, thresh, false);
+}
+
+extern "C" int rs_f8_plan_run_np(rs_f8_plan *p, int64_t H, uint32_t *key, int32_t *pos,
+                                 double thresh) {
+  return rs_f8_plan_run_np_slice(p, H, 0, H, key, pos, thresh);
 }
 
 // Complete the last run (its pending tail) and wait.  Accessors below then read its buffer
@@ -781,6 +792,14 @@ extern "C" int rs_f8_plan_kernel_avg(rs_f8_plan *p, int64_t last_n, double *scor
   if (solve_ms) *solve_ms = p->timing >= 2 ? sa / nt : -1.0;
   if (score_ms) *score_ms = sb / nt;
   if (total_ms) *total_ms = p->timing >= 2 ? sc / nt : -1.0;
+  return RS_OK;
+}
+
+extern "C" int rs_f8_plan_set_count_precision(rs_f8_plan *p, int32_t fp64) {
+  if (!p) return fail(RS_EINVAL, "null plan");
+  int st = plan_flush(p);  // runs in flight use the current kernel's buffers
+  if (st) return st;
+  p->use_fp32 = fp64 == 0;
   return RS_OK;
 }
 

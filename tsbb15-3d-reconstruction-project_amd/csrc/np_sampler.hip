@@ -946,42 +946,7 @@ __global__ __launch_bounds__(256) void k_np_starts(const uint2 *__restrict__ ev,
   if (c == 0 && threadIdx.x == 0) starts[0] = 0;
 }
 
-// ---- 6. one lane per hypothesis: swap partners, then positions 0..k-1 traced back -----------
-__global__ __launch_bounds__(256) void k_np_tuples(const uint32_t *__restrict__ draws,
-                                                   const int64_t *__restrict__ starts,
-                                                   const int64_t *__restrict__ got, int n1, int kk,
-                                                   uint16_t *__restrict__ jb,
-                                                   int32_t *__restrict__ out, int *err) {
-  const int64_t h = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (h >= *got) return;
-  const int64_t a = starts[h], b = starts[h + 1];
-  uint16_t *J = jb + h * n1;
-  uint32_t i = static_cast<uint32_t>(n1);
-  int64_t d = a;
-  for (; d < b && i > 0; ++d) {
-    const uint32_t v = masked(draws[d], i);
-    if (v <= i) {
-      J[i - 1] = static_cast<uint16_t>(v);
-      --i;
-    }
-  }
-  if (i != 0 || d != b) {
-    atomicOr(err, 2);
-    return;
-  }
-  // x_final[p] = x_init[tau_{N-1}(... tau_1(p))], tau_i = (i j_i), x_init = arange
-  uint32_t p[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) p[k] = static_cast<uint32_t>(k);
-  for (uint32_t s = 1; s <= static_cast<uint32_t>(n1); ++s) {
-    const uint32_t j = J[s - 1];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) p[k] = p[k] == s ? j : (p[k] == j ? s : p[k]);
-  }
-  for (int k = 0; k < kk; ++k) out[h * kk + k] = static_cast<int32_t>(p[k]);
-}
-
-// ---- 6'. one wave per hypothesis (default): a window of W <= 64 words per step -------------
+// ---- 6. one wave per hypothesis: a window of W <= 64 words per step ------------------------
 // Within a window every state keeps the mask of the first (W <= i - mask/2), so lane l's draw
 // u_l = w_l & mask is accepted for sure if u_l <= i - l (its state is at least i - l), rejected
 // for sure if u_l > i, and only the rare lanes in between are resolved in order.  Accepted
@@ -992,11 +957,13 @@ constexpr int kTupWaves = 4;
 template <bool PY>
 __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
     const uint32_t *__restrict__ draws, const int64_t *__restrict__ starts,
-    const int64_t *__restrict__ got, int n1, int n1p, int kk, int32_t *__restrict__ out, int *err) {
+    const int64_t *__restrict__ got, int64_t lo, int64_t hi, int n1, int n1p, int kk,
+    int32_t *__restrict__ out, int *err) {
   extern __shared__ uint16_t jl[];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t h = static_cast<int64_t>(blockIdx.x) * kTupWaves + wv;
-  if (h >= *got) return;  // wave-uniform; the kernel has no workgroup barrier
+  // hypotheses [lo, hi) of the segment (those the caller asked for), out row h - lo
+  const int64_t h = lo + static_cast<int64_t>(blockIdx.x) * kTupWaves + wv;
+  if (h >= hi || h >= *got) return;  // wave-uniform; the kernel has no workgroup barrier
   uint16_t *J = jl + static_cast<size_t>(wv) * n1p;
   const int64_t a = starts[h], b = starts[h + 1];
   const uint64_t below = (1ull << l) - 1ull;
@@ -1063,7 +1030,7 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
     uint32_t v = p[0];
 #pragma unroll
     for (int k = 1; k < 8; ++k) v = l == k ? p[k] : v;
-    out[h * kk + l] = static_cast<int32_t>(v);
+    out[(h - lo) * kk + l] = static_cast<int32_t>(v);
   }
 }
 
@@ -1161,8 +1128,7 @@ struct rs_np_work {
   uint2 *d_ev = nullptr;
   int64_t *d_starts = nullptr;
   NpResult *d_res = nullptr;
-  uint16_t *d_J = nullptr;
-  int64_t cap_fin = 0, cap_ev = 0, cap_starts = 0, cap_J = 0;
+  int64_t cap_fin = 0, cap_ev = 0, cap_starts = 0;
   int64_t entry_lds = 0, tup_lds = 0;
 };
 
@@ -1172,7 +1138,7 @@ void np_work_free(rs_ctx *c) {
   rs_np_work *w = c->np_work;
   if (!w) return;
   void *ptrs[] = {w->d_bits, w->d_win, w->d_stream, w->d_fin, w->d_fin_m, w->d_ev_n,
-                  w->d_ent,  w->d_vcnt, w->d_off,   w->d_err, w->d_ev,    w->d_starts, w->d_J,
+                  w->d_ent,  w->d_vcnt, w->d_off,   w->d_err, w->d_ev,    w->d_starts,
                   w->d_tpos, w->d_res};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
@@ -1197,7 +1163,9 @@ bool np_gpu_supported(int64_t n, int32_t k) { return k >= 1 && k <= 8 && k <= n 
 // The numpy stream's next `count` choice(n, k) tuples into device memory (count * k int32),
 // on the context stream; advances (key, pos).  Synchronous.
 int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t k,
-                     int64_t count, int32_t *d_out, bool py) {
+                     int64_t count, int32_t *d_out, bool py, int64_t skip, int64_t take) {
+  if (take < 0) take = count - skip;
+  if (skip < 0 || skip + take > count) return fail(RS_EINVAL, "np sampler: slice out of range");
   if (k < 1 || k > 8) return fail(RS_EINVAL, "np sampler: k must be in 1..8");
   if (k > n)
     return fail(RS_EINVAL, py ? "Cannot generate more indices than the amount of values in the set "
@@ -1227,10 +1195,8 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
     return v >= kWmin && v <= kWmax ? v : 0;
   }();
   const int64_t Cmax = kSegWords / kWmin + 1;
-  // RSAMD_NP_LANE_TUPLES=1: the lane-per-hypothesis tuple kernel with swap partners in HBM (A/B)
-  static const bool lane_tuples = std::getenv("RSAMD_NP_LANE_TUPLES") != nullptr;
   const int64_t tup_lds = static_cast<int64_t>(sizeof(uint16_t)) * ((n1 + 1) & ~1) * kTupWaves;
-  if (!lane_tuples && tup_lds > w.tup_lds) {
+  if (tup_lds > w.tup_lds) {
     HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_np_tuples_wave<false>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(tup_lds)));
     HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_np_tuples_wave<true>),
@@ -1289,8 +1255,7 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
     const int64_t Lb = (*pos + D + kN - 1) / kN;
     const int G = static_cast<int>((Lb + kJB - 1) / kJB);
     if ((st = grow(w.d_ev, w.cap_ev, static_cast<int64_t>(C) * ecap)) ||
-        (st = grow(w.d_starts, w.cap_starts, hs + 1)) ||
-        (lane_tuples && !py && (st = grow(w.d_J, w.cap_J, hs * n1))))
+        (st = grow(w.d_starts, w.cap_starts, hs + 1)))
       return st;
     // 1-2: the word stream from (key, pos): block 0 is the key itself
     HIP_TRY(hipMemcpyAsync(w.d_win, key, sizeof(uint32_t) * kN, hipMemcpyHostToDevice, s));
@@ -1336,17 +1301,17 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
     HIP_TRY(hipGetLastError());
     k_np_starts<<<C, 256, 0, s>>>(w.d_ev, w.d_vcnt, w.d_off, w.d_starts, &w.d_res->got, ecap, kWr);
     HIP_TRY(hipGetLastError());
-    // 6: tuples (launched for hs hypotheses; waves beyond the delivered count exit)
-    if (lane_tuples && !py) {
-      k_np_tuples<<<static_cast<unsigned>((hs + 255) / 256), 256, 0, s>>>(
-          w.d_stream + *pos, w.d_starts, &w.d_res->got, n1, k, w.d_J, d_out + done * k, w.d_err);
-    } else {
+    // 6: tuples of the requested slice [skip, skip + take) within this segment's hypotheses
+    // [done, done + hs) (waves beyond the delivered count exit)
+    const int64_t lo = std::max<int64_t>(skip - done, 0), hi = std::min<int64_t>(skip + take - done, hs);
+    if (hi > lo) {
       const int n1p = (n1 + 1) & ~1;
-      (py ? k_np_tuples_wave<true> : k_np_tuples_wave<false>)<<<static_cast<unsigned>((hs + kTupWaves - 1) / kTupWaves), 64 * kTupWaves,
+      (py ? k_np_tuples_wave<true> : k_np_tuples_wave<false>)<<<static_cast<unsigned>((hi - lo + kTupWaves - 1) / kTupWaves), 64 * kTupWaves,
                          sizeof(uint16_t) * n1p * kTupWaves, s>>>(
-          w.d_stream + *pos, w.d_starts, &w.d_res->got, n1, n1p, k, d_out + done * k, w.d_err);
+          w.d_stream + *pos, w.d_starts, &w.d_res->got, lo, hi, n1, n1p, k,
+          d_out + (done + lo - skip) * k, w.d_err);
+      HIP_TRY(hipGetLastError());
     }
-    HIP_TRY(hipGetLastError());
     // 7: delivered count, draws used, errors and the stream block holding the next word
     k_np_result<<<1, 64, 0, s>>>(w.d_stream, w.d_starts, *pos, w.d_err, w.d_res);
     HIP_TRY(hipGetLastError());

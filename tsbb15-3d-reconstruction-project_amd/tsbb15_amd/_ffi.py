@@ -84,6 +84,8 @@ _SIGS = {
     "rs_f8_plan_run": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.c_uint64, C.c_uint64,
                                  _i32p, C.c_double]),
     "rs_f8_plan_run_np": (C.c_int, [C.c_void_p, C.c_int64, _u32p, _i32p, C.c_double]),
+    "rs_f8_plan_run_np_slice": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_int64, _u32p,
+                                          _i32p, C.c_double]),
     "rs_f8_plan_result": (C.c_int, [C.c_void_p, C.POINTER(F8Result), _i64p, C.c_int64, _i64p]),
     "rs_f8_plan_candidates": (C.c_int, [C.c_void_p, C.POINTER(F8Candidate), C.c_int64, _i64p]),
     "rs_f8_plan_counts": (C.c_int, [C.c_void_p, _i32p, C.c_int64]),
@@ -91,6 +93,7 @@ _SIGS = {
     "rs_f8_plan_kernel_ms": (C.c_int, [C.c_void_p, _dp, _dp, _dp]),
     "rs_f8_plan_kernel_avg": (C.c_int, [C.c_void_p, C.c_int64, _dp, _dp, _dp]),
     "rs_f8_plan_set_timing": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
+    "rs_f8_plan_set_count_precision": (C.c_int, [C.c_void_p, C.c_int32]),
     "rs_f8_ransac_np": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, C.c_int64, _u32p, _i32p,
                                   C.c_double, C.POINTER(F8Result), _i64p, C.c_int64, _i64p]),
     "rs_pnp_dlt": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, _dp]),
@@ -379,6 +382,16 @@ class F8Plan:
                                       float(thresh)))
         return key, p.value
 
+    def run_np_slice(self, H, start, count, key, pos, thresh=1.5):
+        """Hypotheses [start, start + count) of an H-hypothesis parity run (one rank's shard):
+        the numpy stream of all H is parsed on the GPU, the slice is evaluated; returns the
+        (key, pos) after all H.  Candidate indices of the run are slice-local."""
+        key = np.array(key, dtype=np.uint32, copy=True)
+        p = C.c_int32(int(pos))
+        check(lib().rs_f8_plan_run_np_slice(self._h, int(H), int(start), int(count),
+                                            ptr(key, C.c_uint32), C.byref(p), float(thresh)))
+        return key, p.value
+
     def result(self):
         r = F8Result()
         inl = np.empty(self.n, dtype=np.int64)
@@ -403,6 +416,10 @@ class F8Plan:
         out = np.empty((int(H), 9), dtype=np.float64)
         check(lib().rs_f8_plan_models(self._h, ptr(out, C.c_double), int(H)))
         return out.reshape(-1, 3, 3)
+
+    def set_count_precision(self, fp64):
+        """fp64=True: the plain float64 counting kernel for later runs (same counts, slower)."""
+        check(lib().rs_f8_plan_set_count_precision(self._h, 1 if fp64 else 0))
 
     def set_timing(self, level=1, every=1):
         """HIP timing events per run: level 0 none, 1 counting kernel, 2 also solve / run;

@@ -12,6 +12,10 @@ Two shardings:
     union is exactly the single-GPU run); then one max-all-reduce of c* and one all-gather of
     the candidates with count == c*, which every rank replays in global index order with the
     fun.py:320-328 rule (first c* hypothesis, then std/norm tie replacements).
+  * the same in parity mode (the reference's own stream, fun.py:305-306): every rank parses
+    the numpy stream of all H hypotheses on its GPU (where each hypothesis starts is a serial
+    property of the stream), produces and evaluates only its slice's tuples, and advances the
+    MT state past all H -- so the winner, S_RANSAC and the state equal the single-process run.
 
 Communicators: :class:`RcclComm` (librsamd, device buffers, xGMI) on GPUs and
 :class:`TorchComm` (torch.distributed, e.g. gloo on the CPU) for tests; both expose
@@ -192,6 +196,58 @@ def ransac_f_sharded(comm, ctx, p1, p2, H, seed=0, thresh=1.5, plan=None):
     r = np.abs(lab3.fmatrix_residuals(F, p1, p2))
     d = np.where(np.isnan(r).any(axis=0), np.nan, r.max(axis=0))
     return best, np.flatnonzero(d < thresh)
+
+
+def np_state(rng=None):
+    """(key, pos) of the numpy legacy MT19937 stream (the global np.random when rng is None)."""
+    st = (np.random if rng is None else rng).get_state()
+    if st[0] != "MT19937":
+        raise ValueError("only the legacy MT19937 RandomState stream is supported")
+    return np.asarray(st[1], np.uint32), int(st[2])
+
+
+def ransac_f_sharded_np(comm, p1, p2, H, key, pos, evaluate, thresh=1.5):
+    """Parity-mode hypothesis sharding of the fun.py:303-328 loop.
+
+    ``evaluate(start, count, key, pos)`` evaluates hypotheses [start, start + count) of the H
+    drawn from the numpy stream (key, pos) and returns (candidate records with GLOBAL indices,
+    key', pos') where (key', pos') is the state after all H (:class:`GpuSliceEvaluator` on a
+    GPU).  Returns (winner record or None, key', pos'), identical on every rank."""
+    start, cnt = shard_range(H, comm.world, comm.rank)
+    local, key2, pos2 = evaluate(start, cnt, key, pos)
+    best = merge_shard_candidates(comm, local)
+    return best, key2, pos2
+
+
+class GpuSliceEvaluator:
+    """This rank's slice of a parity-mode run on its GPU (rs_f8_plan_run_np_slice): the stream
+    of all H hypotheses is parsed on the GPU, only the slice is solved, counted and selected."""
+
+    def __init__(self, ctx, p1, p2, H, thresh=1.5, max_slice=None):
+        self.p1, self.p2 = _ffi.f64c(p1), _ffi.f64c(p2)
+        self.H, self.thresh = int(H), float(thresh)
+        self.plan = _ffi.F8Plan(ctx, self.p1.shape[1], max(1, int(max_slice or self.H)))
+        self.plan.set_points(self.p1, self.p2)
+
+    def __call__(self, start, count, key, pos):
+        if count < 1:  # more ranks than hypotheses: only the state advance
+            _, key2, pos2 = _ffi.np_choice_tuples(key, pos, self.p1.shape[1], 8, self.H)
+            return np.zeros(0, CAND_DTYPE), key2, pos2
+        key2, pos2 = self.plan.run_np_slice(self.H, start, count, key, pos, self.thresh)
+        self.plan.result()
+        return candidates_from_plan(self.plan, start), key2, pos2
+
+    def inliers(self, best):
+        if best is None:
+            return np.zeros(0, np.int64)
+        from . import lab3
+        F = best["F"].reshape(3, 3)
+        r = np.abs(lab3.fmatrix_residuals(F, self.p1, self.p2))
+        d = np.where(np.isnan(r).any(axis=0), np.nan, r.max(axis=0))
+        return np.flatnonzero(d < self.thresh)
+
+    def close(self):
+        self.plan.close()
 
 
 class GpuPairSolver:
