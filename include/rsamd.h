@@ -289,6 +289,15 @@ typedef struct rs_gs_info {
   int32_t n;              /* inliers of the pair                                           */
 } rs_gs_info;
 
+/* The residual of lab3.fmatrix_residuals_gs (lab3.py:228-266) at the parameter vector x
+ * (12 camera entries row-major, then n points xyz; f: 4n, order left x, left y, right x,
+ * right y) and, when J is non-null, the forward-difference Jacobian scipy's
+ * least_squares(jac='2-point') forms (fun.py:358): J (4n, 12 + 3n) row-major, column j =
+ * (f(x with x_j -> xp[j]) - f(x)) / dx[j]; xp and dx are the caller's (scipy's step rule).
+ * The host-side TRF iteration of the reference-faithful gold standard calls this. */
+int rs_gs_residuals_fd(rs_ctx *ctx, const double *x, const double *xp, const double *dx,
+                       const double *pl, const double *pr, int64_t n, double *f, double *J);
+
 /* The gold-standard tail of fun.getFFromLabCode (fun.py:336-369), batched over pairs:
  * F (B, 3, 3) = F_RANSAC per pair; pl, pr (2, total) the inlier points of all pairs
  * concatenated, pair b = columns off[b] .. off[b+1]-1 (off has B+1 entries, off[0] = 0).

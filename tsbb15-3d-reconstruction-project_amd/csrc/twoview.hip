@@ -341,6 +341,69 @@ struct GsInfo {  // == rs_gs_info
   int32_t n;
 };
 
+// ---- reference-faithful gold standard (fun.py:358 as scipy runs it) ------------------------
+// Residuals of lab3.fmatrix_residuals_gs (lab3.py:228-266) for one point k of the parameter
+// vector (C1 row-major, X_k): left = pl - project(X_k, C1), right = pr - project(X_k, [I|0]).
+__device__ __forceinline__ void gs_res4(const double *C, double X0, double X1, double X2,
+                                        double plx, double ply, double prx, double pry,
+                                        double r[4]) {
+#pragma clang fp contract(off)
+  const double y0 = ((C[0] * X0 + C[1] * X1) + C[2] * X2) + C[3];
+  const double y1 = ((C[4] * X0 + C[5] * X1) + C[6] * X2) + C[7];
+  const double y2 = ((C[8] * X0 + C[9] * X1) + C[10] * X2) + C[11];
+  r[0] = plx - y0 / y2;
+  r[1] = ply - y1 / y2;
+  r[2] = prx - X0 / X2;
+  r[3] = pry - X1 / X2;
+}
+
+// Thread per point k: the residual f(x) (rows k, n+k, 2n+k, 3n+k) and the 2-point forward
+// differences scipy's approx_derivative forms for least_squares(jac='2-point'): column j is
+// (f(x with x_j -> xp_j) - f(x)) / dx_j, xp and dx computed by the caller exactly as scipy
+// does.  Entries a parameter cannot reach are left as the caller zeroed them (their forward
+// differences are exactly 0: the same inputs give the same values).
+__global__ __launch_bounds__(128) void k_gs_fd(const double *__restrict__ x,
+                                               const double *__restrict__ xp,
+                                               const double *__restrict__ dx,
+                                               const double *__restrict__ pl,
+                                               const double *__restrict__ pr, int64_t n,
+                                               double *__restrict__ f, double *__restrict__ J) {
+#pragma clang fp contract(off)
+  const int64_t k = static_cast<int64_t>(blockIdx.x) * 128 + threadIdx.x;
+  if (k >= n) return;
+  const int64_t nc = 12 + 3 * n;
+  double C[12];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) C[j] = x[j];
+  const double X0 = x[12 + 3 * k], X1 = x[13 + 3 * k], X2 = x[14 + 3 * k];
+  const double plx = pl[k], ply = pl[n + k], prx = pr[k], pry = pr[n + k];
+  double r0[4];
+  gs_res4(C, X0, X1, X2, plx, ply, prx, pry, r0);
+  const int64_t row[4] = {k, n + k, 2 * n + k, 3 * n + k};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) f[row[q]] = r0[q];
+  if (!J) return;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {  // camera parameters: the two left residuals of every point
+    const double keep = C[j];
+    C[j] = xp[j];
+    double r[4];
+    gs_res4(C, X0, X1, X2, plx, ply, prx, pry, r);
+    C[j] = keep;
+    J[row[0] * nc + j] = (r[0] - r0[0]) / dx[j];
+    J[row[1] * nc + j] = (r[1] - r0[1]) / dx[j];
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {  // this point's coordinates: its four residuals
+    const int64_t col = 12 + 3 * k + c;
+    double r[4];
+    gs_res4(C, c == 0 ? xp[col] : X0, c == 1 ? xp[col] : X1, c == 2 ? xp[col] : X2, plx, ply,
+            prx, pry, r);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) J[row[q] * nc + col] = (r[q] - r0[q]) / dx[col];
+  }
+}
+
 __global__ __launch_bounds__(kGsT) void k_gold_standard(
     const double *__restrict__ Fin, const double *__restrict__ pl, const double *__restrict__ pr,
     int64_t total, const int64_t *__restrict__ off, int max_iter, double *__restrict__ Xb,
@@ -823,6 +886,39 @@ extern "C" int rs_gold_standard(rs_ctx *c, const double *F, const double *pl, co
   if (X_out && total > 0)
     HIP_TRY(hipMemcpyAsync(X_out, b[4], sizeof(double) * 3 * total, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipMemcpyAsync(info, b[9], sizeof(rs_gs_info) * B, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return RS_OK;
+}
+
+extern "C" int rs_gs_residuals_fd(rs_ctx *c, const double *x, const double *xp, const double *dx,
+                                  const double *pl, const double *pr, int64_t n, double *f,
+                                  double *J) {
+  if (!c || !x || !pl || !pr || !f || (J && (!xp || !dx))) return fail(RS_EINVAL, "null pointer");
+  if (n < 1 || n > (1LL << 20)) return fail(RS_EINVAL, "Wrong size of parameter vector");
+  HIP_TRY(hipSetDevice(c->device));
+  const int64_t np = 12 + 3 * n, nr = 4 * n;
+  const size_t jb = J ? sizeof(double) * static_cast<size_t>(nr) * np : 0;
+  std::vector<char *> b;
+  int st = carve(c, {sizeof(double) * np, J ? sizeof(double) * np : 0, J ? sizeof(double) * np : 0,
+                     sizeof(double) * 2 * n, sizeof(double) * 2 * n, sizeof(double) * nr, jb},
+                 b);
+  if (st) return st;
+  HIP_TRY(hipMemcpyAsync(b[0], x, sizeof(double) * np, hipMemcpyHostToDevice, c->stream));
+  if (J) {
+    HIP_TRY(hipMemcpyAsync(b[1], xp, sizeof(double) * np, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(b[2], dx, sizeof(double) * np, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(b[6], 0, jb, c->stream));
+  }
+  HIP_TRY(hipMemcpyAsync(b[3], pl, sizeof(double) * 2 * n, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(b[4], pr, sizeof(double) * 2 * n, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(rsd::k_gs_fd, dim3(static_cast<unsigned>((n + 127) / 128)), dim3(128), 0,
+                     c->stream, reinterpret_cast<double *>(b[0]), reinterpret_cast<double *>(b[1]),
+                     reinterpret_cast<double *>(b[2]), reinterpret_cast<double *>(b[3]),
+                     reinterpret_cast<double *>(b[4]), n, reinterpret_cast<double *>(b[5]),
+                     J ? reinterpret_cast<double *>(b[6]) : nullptr);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(f, b[5], sizeof(double) * nr, hipMemcpyDeviceToHost, c->stream));
+  if (J) HIP_TRY(hipMemcpyAsync(J, b[6], jb, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return RS_OK;
 }

@@ -113,6 +113,7 @@ _SIGS = {
     "rs_fmatrix_from_cameras": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp]),
     "rs_gold_standard": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _i64p, C.c_int64, C.c_int32, _dp,
                                    _dp, _dp, C.POINTER(GsInfo)]),
+    "rs_gs_residuals_fd": (C.c_int, [C.c_void_p, _dp, _dp, _dp, _dp, _dp, C.c_int64, _dp, _dp]),
     "rs_match_observations": (C.c_int, [C.c_void_p, _dp, _i64p, C.c_int64, _dp, C.c_int64,
                                         C.c_double, _i64p]),
     "rs_e_from_cameras": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp]),

@@ -7,9 +7,12 @@
     ``np.random.choice(arange(N), 8, replace=False)`` would consume, fun.py:305-306), every
     hypothesis is solved, counted and selected by the HIP kernels of librsamd, and the
     advanced MT state is written back into ``np.random`` exactly as the reference leaves it;
-  * the gold-standard refinement (fun.py:336-369) follows on the GPU
-    (:func:`tsbb15_amd.twoview.gold_standard`: optimal triangulation of the inliers and a
-    converged Levenberg-Marquardt on the reference's objective, one workgroup per pair).
+  * the gold-standard refinement (fun.py:336-369) follows.  ``GOLD_STANDARD = 'trf'`` (the
+    default) runs it as the reference does: scipy's TRF (fun.py:358's options) over a
+    residual and forward-difference Jacobian computed on the GPU
+    (:func:`tsbb15_amd.twoview.gold_standard_trf`); ``'lm'`` runs a converged
+    Levenberg-Marquardt on the same objective entirely on the GPU
+    (:func:`tsbb15_amd.twoview.gold_standard`, one workgroup per pair, lower final cost).
 
 The E / pose functions of fun.py (camera_resectioning, getEAndK, MakeHomogenous,
 relative_camera_pose) are re-exported from :mod:`tsbb15_amd.twoview` (HIP kernels).
@@ -27,6 +30,7 @@ from .twoview import (MakeHomogenous, camera_resectioning, getEAndK,  # noqa: F4
                       relative_camera_pose)
 
 REFERENCE_ITERATIONS = 10000   # fun.py:302
+GOLD_STANDARD = 'trf'          # 'trf': the reference's scipy TRF path; 'lm': converged GPU LM
 INLIER_THRESHOLD = 1.5         # fun.py:317 (strict "<")
 
 
@@ -90,4 +94,8 @@ def getFFromLabCode(p1, p2):
         raise ValueError('RANSAC found no hypothesis with a non-empty consensus set')
     p1 = np.asarray(p1, dtype=np.float64)
     p2 = np.asarray(p2, dtype=np.float64)
-    return twoview.gold_standard(res.F, p1[:, res.inliers], p2[:, res.inliers])
+    if GOLD_STANDARD == 'lm':
+        return twoview.gold_standard(res.F, p1[:, res.inliers], p2[:, res.inliers])
+    if GOLD_STANDARD != 'trf':
+        raise ValueError("GOLD_STANDARD must be 'trf' or 'lm'")
+    return twoview.gold_standard_trf(res.F, p1[:, res.inliers], p2[:, res.inliers])

@@ -12,11 +12,17 @@ they replace:
   * ``relative_camera_pose(E, y1, y2)``        fun.py:209-258    (rs_relative_camera_pose)
   * ``gold_standard(F, pl, pr)``               fun.py:336-369    (rs_gold_standard)
   * ``gold_standard_batch(Fs, pls, prs)``      the same, one workgroup per pair
+  * ``gold_standard_trf(F, pl, pr)``           fun.py:336-369 as the reference runs it:
+    scipy's TRF (least_squares(xtol=2.22e-14, tr_solver='lsmr'), fun.py:358) on the host with
+    the residual and its forward-difference Jacobian on the GPU (rs_gs_residuals_fd)
 
 ``MakeHomogenous`` (fun.py:48-55) and ``project`` are input / output formatting helpers.
-The gold standard minimises the reference's objective (lab3.fmatrix_residuals_gs) to
+``gold_standard`` minimises the reference's objective (lab3.fmatrix_residuals_gs) to
 convergence; the reference's scipy TRF stops on ftol = 1e-8 at a path-dependent point with a
-higher objective (see oracle/twoview_ref.py and DESIGN.md).
+higher objective (see oracle/twoview_ref.py and DESIGN.md).  ``gold_standard_trf`` follows that
+TRF path itself; where it stops depends on the last bits of every residual (the reference's
+own result moves by ~1e-5 between one and eight BLAS threads), so it lands near, not on, the
+reference's F_gold.
 """
 from __future__ import annotations
 
@@ -216,3 +222,81 @@ def gold_standard_batch(Fs, pls, prs, max_iter=MAX_ITER, ctx=None):
 def gold_standard(F, pl, pr, max_iter=MAX_ITER, ctx=None):
     """F_gold of fun.py:336-369 from F_RANSAC and the inlier points pl, pr (2, n)."""
     return gold_standard_batch(np.asarray(F).reshape(1, 3, 3), [pl], [pr], max_iter, ctx)[0].F
+
+
+_EPS_2POINT = float(np.finfo(np.float64).eps) ** 0.5  # scipy _eps_for_method(f64, f64, '2-point')
+
+
+def gs_residuals(x, pl, pr, ctx=None):
+    """lab3.fmatrix_residuals_gs(params, pl, pr) on the GPU: (4n,) left x, left y, right x,
+    right y."""
+    x = _ffi.f64c(x)
+    pl, pr = _ffi.f64c(pl), _ffi.f64c(pr)
+    n = pl.shape[1]
+    if pl.shape != pr.shape or x.shape != (12 + 3 * n,):
+        raise ValueError('Wrong size of parameter vector')
+    f = np.empty(4 * n)
+    _ffi.check(_ffi.lib().rs_gs_residuals_fd(_ctx(ctx), _ffi.ptr(x, _d), None, None,
+                                             _ffi.ptr(pl, _d), _ffi.ptr(pr, _d), n,
+                                             _ffi.ptr(f, _d), None))
+    return f
+
+
+def gs_jacobian_2point(x, pl, pr, ctx=None):
+    """The Jacobian scipy's approx_derivative(method='2-point') forms for
+    lab3.fmatrix_residuals_gs at x (steps and dx exactly as scipy computes them), on the GPU."""
+    x = _ffi.f64c(x)
+    pl, pr = _ffi.f64c(pl), _ffi.f64c(pr)
+    n = pl.shape[1]
+    if pl.shape != pr.shape or x.shape != (12 + 3 * n,):
+        raise ValueError('Wrong size of parameter vector')
+    sign = (x >= 0).astype(float) * 2 - 1
+    h = _EPS_2POINT * sign * np.maximum(1.0, np.abs(x))
+    xp = x + h
+    dx = xp - x
+    f = np.empty(4 * n)
+    J = np.empty((4 * n, 12 + 3 * n))
+    _ffi.check(_ffi.lib().rs_gs_residuals_fd(_ctx(ctx), _ffi.ptr(x, _d), _ffi.ptr(xp, _d),
+                                             _ffi.ptr(dx, _d), _ffi.ptr(pl, _d),
+                                             _ffi.ptr(pr, _d), n, _ffi.ptr(f, _d),
+                                             _ffi.ptr(J, _d)))
+    return J
+
+
+@dataclass
+class GoldStandardTRF:
+    F: np.ndarray
+    C1: np.ndarray
+    X: np.ndarray
+    cost_init: float
+    cost: float
+    nfev: int
+    status: int   # scipy least_squares status (1 gtol, 2 ftol, 3 xtol, 4 ftol and xtol, 0 max_nfev)
+
+
+def gold_standard_trf_full(F, pl, pr, ctx=None):
+    """fun.py:343-369 as the reference runs it.  Cameras from F_RANSAC and the optimal
+    triangulation of the inliers on the GPU, then scipy.optimize.least_squares with the
+    reference's options (fun.py:358: method 'trf', xtol=2.22e-14, tr_solver='lsmr', default
+    ftol / gtol / x_scale / max_nfev) over a residual and a forward-difference Jacobian
+    computed on the GPU, then F from the refined cameras on the GPU."""
+    from scipy.optimize import least_squares
+    pl = _ffi.f64c(pl)
+    pr = _ffi.f64c(pr)
+    if pl.shape != pr.shape or pl.ndim != 2 or pl.shape[0] != 2:
+        raise ValueError('pl and pr must both be (2, n)')
+    C1, C2 = fmatrix_cameras(F, ctx)
+    X = triangulate_optimal_batch(C1, C2, pl, pr, ctx=ctx)      # fun.py:352
+    params = np.hstack((C1.ravel(), X.ravel()))                  # fun.py:355
+    f0 = gs_residuals(params, pl, pr, ctx)
+    res = least_squares(gs_residuals, params, jac=gs_jacobian_2point, xtol=2.22e-14,
+                        tr_solver='lsmr', args=(pl, pr), kwargs={"ctx": ctx})
+    C1g = res.x[:12].reshape(3, 4)
+    Fg = fmatrix_from_cameras(C1g, I34, ctx)                     # fun.py:362-368
+    return GoldStandardTRF(Fg, C1g, res.x[12:].reshape(-1, 3), 0.5 * float(f0 @ f0),
+                           float(res.cost), int(res.nfev), int(res.status))
+
+
+def gold_standard_trf(F, pl, pr, ctx=None):
+    """F_gold of fun.py:336-369 along the reference's own TRF path (see gold_standard_trf_full)."""
+    return gold_standard_trf_full(F, pl, pr, ctx).F
