@@ -221,6 +221,21 @@ int rs_pnp_ransac(rs_ctx *ctx, const double *X_med, const double *y_med, int64_t
                   double thresh, rs_pnp_result *out, int64_t *inl_med, int64_t *n_inl_med,
                   int64_t *inl_high, int64_t *n_inl_high);
 
+/* cv.solvePnPRansac drop-in (tables.py:141-145 call site): world points X (m,3), PIXEL
+ * image points uv (m,2), camera matrix K (3,3 row-major, upper triangular), zero distortion.
+ * Up to max_iters hypotheses (Philox 6-point samples from `seed`, DLT minimal solver on the
+ * sample's centred, RMS-scaled world points -- Hartley conditioning) are
+ * solved and counted on the GPU with OpenCV's pixel test |K pi(R x + t) - uv|^2 <=
+ * reproj_err^2; OpenCV's sequential loop (a model wins with goodCount > max(best,
+ * model_points - 1), then RANSACUpdateNumIters(confidence, outlier ratio, model_points,
+ * niters) shrinks the budget) is replayed over that hypothesis order.  out->best_index = -1
+ * when nothing wins; *iters_used = hypotheses the loop consumed; inliers (<= m) in point
+ * order.  m >= 6 (the DLT), unlike OpenCV's EPnP kernel (m >= 4). */
+int rs_pnp_ransac_cv(rs_ctx *ctx, const double *X, const double *uv, int64_t m, const double *K,
+                     int64_t max_iters, uint64_t seed, double reproj_err, double confidence,
+                     int32_t model_points, rs_pnp_result *out, int64_t *inliers,
+                     int64_t *n_inliers, int64_t *iters_used);
+
 /* ------------------------------------------------------------------------------------------
  * Batched RANSAC-F over many image pairs (config C4; fun.py:298-328 per pair)
  * ---------------------------------------------------------------------------------------- */

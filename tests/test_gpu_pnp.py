@@ -118,3 +118,82 @@ def test_solvepnpransac_surface_badino2(ctx):
     R, _ = cv.Rodrigues(rvec)
     np.testing.assert_allclose(R, z["R"][v], atol=1e-8)
     np.testing.assert_allclose(tvec[:, 0], z["t"][v], atol=1e-8)
+
+
+def _aniso_scene(seed=4):
+    """Anisotropic, skewed camera (fx 800, fy 1200, skew 0.5): 100 exact correspondences, 10
+    moved 7 px along u, 10 moved 9 px along v, 20 gross outliers (>= 60 px)."""
+    rs = np.random.RandomState(seed)
+    K = np.array([[800.0, 0.5, 640.0], [0.0, 1200.0, 480.0], [0.0, 0.0, 1.0]])
+    R, _ = cv.Rodrigues(np.array([0.1, -0.2, 0.05]))
+    t = np.array([0.2, -0.1, 6.0])
+    X = rs.uniform(-2, 2, (140, 3))
+    uv = cv.project_points(X, cv.Rodrigues(R)[0], t, K)
+    uv[100:110, 0] += 7.0
+    uv[110:120, 1] += 9.0
+    uv[120:] += rs.choice([-1, 1], (20, 2)) * rs.uniform(60, 200, (20, 2))
+    return X, uv, K, R, t
+
+
+def test_solvepnpransac_pixel_threshold_through_K(ctx):
+    """The consensus test is |K pi(R x + t) - uv| <= reprojectionError in PIXELS: with
+    fx != fy a 7 px offset along u is an inlier and a 9 px offset along v is not (the old
+    normalised test with f = sqrt(fx fy) decided both the other way)."""
+    X, uv, K, Rt, tt = _aniso_scene()
+    ok, rvec, tvec, inl = cv.solvePnPRansac(X, uv, K, np.zeros((4, 1)), iterationsCount=500,
+                                            confidence=0.999999)
+    assert ok
+    inl = inl[:, 0]
+    # exactly the pixel test under the RANSAC pose (before refinement)
+    rr = cv.last_ransac
+    e = np.linalg.norm(cv.project_points(X, cv.Rodrigues(rr["R"])[0], rr["t"], K) - uv, axis=1)
+    np.testing.assert_array_equal(inl, np.flatnonzero(e <= 8.0))
+    np.testing.assert_array_equal(inl, np.arange(110))
+    # LM refinement on the consensus set: no worse than the RANSAC pose, near the truth
+    R, _ = cv.Rodrigues(rvec)
+    e2 = np.linalg.norm(cv.project_points(X[inl], rvec, tvec[:, 0], K) - uv[inl], axis=1)
+    assert (e2 ** 2).sum() <= (e[inl] ** 2).sum() * (1 + 1e-12)
+    np.testing.assert_allclose(R, Rt, atol=5e-3)
+
+
+def test_solvepnpransac_adaptive_iterations_and_determinism(ctx):
+    X, uv, K, _, _ = _aniso_scene()
+    # noise-free, no outliers: the first model has outlier ratio 0 -> RANSACUpdateNumIters = 0
+    ok, *_ = cv.solvePnPRansac(X[:100], uv[:100], K, None, iterationsCount=1000)
+    assert ok and cv.last_ransac["iterations"] == 1
+    # confidence 1: the budget never shrinks below iterationsCount while outliers remain
+    ok, *_ = cv.solvePnPRansac(X, uv, K, None, iterationsCount=300, confidence=1.0)
+    assert ok and cv.last_ransac["iterations"] == 300
+    used, best = [], []
+    for conf in (0.5, 0.99, 0.9999):
+        ok, _, _, inl = cv.solvePnPRansac(X, uv, K, None, iterationsCount=1000, confidence=conf)
+        used.append(cv.last_ransac["iterations"])
+        best.append((cv.last_ransac["best_index"], len(inl)))
+    assert used == sorted(used) and used[-1] < 1000, used
+    # OpenCV's budget at the winner's outlier ratio (m = 6): log(1 - p) / log(1 - (1 - ep)^6);
+    # the loop stops at that budget, or right after the winner when it came later
+    ep = 1 - best[1][1] / 140
+    bound = int(np.ceil(np.log(0.01) / np.log(1 - (1 - ep) ** 6))) + 1
+    assert used[1] <= max(bound, best[1][0] + 1), (used, best, bound)
+    # equal inputs, equal outputs, whatever ran in between
+    a = cv.solvePnPRansac(X, uv, K, None)
+    cv.solvePnPRansac(X[::-1].copy(), uv[::-1].copy(), K, None, iterationsCount=37)
+    b = cv.solvePnPRansac(X, uv, K, None)
+    for u, v in zip(a[1:], b[1:]):
+        np.testing.assert_array_equal(u, v)
+
+
+def test_solvepnpransac_rejects_bad_input(ctx):
+    X, uv, K, _, _ = _aniso_scene()
+    assert cv.solvePnPRansac(X[:5], uv[:5], K, None) == (False, None, None, None)
+    with pytest.raises(ValueError):
+        cv.solvePnPRansac(X, uv, K, np.array([0.1, 0, 0, 0]))
+    Kb = K.copy()
+    Kb[1, 0] = 1.0
+    with pytest.raises(ValueError, match="upper triangular"):
+        cv.solvePnPRansac(X, uv, Kb, None)
+    # nothing agrees: False, like OpenCV
+    rs = np.random.RandomState(0)
+    ok, r, t, inl = cv.solvePnPRansac(X[:12], rs.uniform(0, 2000, (12, 2)), K, None,
+                                      reprojectionError=1e-6)
+    assert not ok and inl is None

@@ -149,3 +149,36 @@ def test_np_choice_tuples_multi_equals_single_streams():
     rs = np.random.RandomState(1003)  # and numpy itself, for one stream
     ref = np.array([rs.choice(np.arange(176), 8, replace=False) for _ in range(300)])
     assert np.array_equal(out[3], ref)
+
+
+@pytest.mark.parametrize("bad", [-1, 2 ** 32, 2 ** 40, 1.5])
+def test_np_seeds_outside_numpy_range_raise(bad):
+    """np.random.seed raises ValueError outside [0, 2**32); so do the seeded samplers
+    (instead of silently wrapping into another stream)."""
+    with pytest.raises((ValueError, TypeError)):
+        np.random.RandomState(bad)
+    with pytest.raises(ValueError):
+        _ffi.np_seed(bad)
+    with pytest.raises(ValueError):
+        _ffi.np_choice_tuples_multi(None, None, [50, 60], 8, 3, seeds=[0, bad])
+    t, _, _ = _ffi.np_choice_tuples_multi(None, None, [50], 8, 3, seeds=[2 ** 32 - 1])
+    rs = np.random.RandomState(2 ** 32 - 1)
+    np.testing.assert_array_equal(t[0], [rs.choice(np.arange(50), 8, replace=False)
+                                         for _ in range(3)])
+
+
+def test_gen_rnd_tuples_host_route_without_device():
+    """With no device (this container) or with the GPU route switched off, gen_rnd_tuples
+    draws a long stream on the native host replay: CPython's own tuples and final state."""
+    from tsbb15_amd import ransac
+    assert 1.4 * 600 * 5000 >= ransac._GPU_MIN_DRAWS  # long enough for the GPU route
+    for gpu in (None, False):
+        rng, ref = random.Random(5), random.Random(5)
+        tup = ransac.gen_rnd_tuples(600, 6, 5000, rng, gpu=gpu)
+        want = []
+        for _ in range(5000):  # ransac.py:12-19 (random.shuffle of the index list)
+            x = list(range(600))
+            ref.shuffle(x)
+            want.append(x[:6])
+        np.testing.assert_array_equal(tup, np.array(want))
+        assert rng.getstate() == ref.getstate()

@@ -10,10 +10,19 @@
 //                 e = |pi(y) - pi(R x + t)|^2 <= thresh, evaluated division-free.
 //   k_pnp_select  one workgroup: first hypothesis with the largest count (strict ">").
 //   k_pnp_inliers consensus sets of the winner on `med` and `high` (reference order).
+//
+// The cv.solvePnPRansac drop-in (rs_pnp_ransac_cv) reuses solve / count with the test in
+// PIXELS: the residual pi(y) - pi(R x + t) in C-normalised units is mapped through the upper
+// 2x2 block of K, [[fx, s], [0, fy]] (K is affine on the image plane, so this IS the pixel
+// reprojection error K pi(R x + t) - uv), and compared with reprojectionError^2.  The
+// reference-mode metric is the identity (a, b, c) = (1, 0, 1), which leaves its arithmetic
+// bit-unchanged.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
+#include <limits>
 #include <vector>
 
 #include "common.h"
@@ -26,6 +35,11 @@ namespace rsd {
 // A 3D<->2D correspondence: world point (X, Y, Z) and pi(y) = (y0/y2, y1/y2).
 struct PPt {
   double X, Y, Z, u, v, y0, y1, y2;
+};
+
+// Pixel metric: residual (du, dv) -> (a du + b dv, c dv).
+struct PxMetric {
+  double a, b, c;
 };
 
 constexpr int ridx(int j, int l) { return j * 12 - (j * (j - 1)) / 2 + (l - j); }
@@ -229,21 +243,58 @@ __device__ __forceinline__ void enforce_pose(const double (&c0)[12], double (&Rm
   t[2] = lam * c0[11];
 }
 
-template <class IndexAt>
+// cond = false: the reference DLT on the raw world points (pnp.py:132-160).
+// cond = true (the cv.solvePnPRansac drop-in): the sample's world points are first centred on
+// their centroid c and scaled to unit RMS distance s (Hartley conditioning), the DLT solves for
+// the pose of X' = (X - c) / s, and t = s t' - R c maps it back.  Exact data give the same pose
+// either way; on compact, distant point sets (near-affine views, BAdino2's noisy reconstruction:
+// depth 5.7-6.1, spread ~0.3) the raw 12x12 system is too ill-conditioned to survive pixel noise.
+template <bool Cond, class IndexAt>
 __device__ __forceinline__ void pnp_solve_points(const PPt *pts, int k, IndexAt index_at,
                                                  double (&Rm)[9], double (&t)[3]) {
   double R[78];
 #pragma unroll
   for (int i = 0; i < 78; ++i) R[i] = 0.0;
+  double cx = 0.0, cy = 0.0, cz = 0.0, sc = 1.0;
+  if (Cond) {
+    for (int q = 0; q < k; ++q) {
+      const PPt &p = pts[index_at(q)];
+      cx += p.X;
+      cy += p.Y;
+      cz += p.Z;
+    }
+    cx /= k;
+    cy /= k;
+    cz /= k;
+    double ss = 0.0;
+    for (int q = 0; q < k; ++q) {
+      const PPt &p = pts[index_at(q)];
+      ss += (p.X - cx) * (p.X - cx) + (p.Y - cy) * (p.Y - cy) + (p.Z - cz) * (p.Z - cz);
+    }
+    sc = sqrt(ss / k);
+    if (!(sc > 0.0)) sc = 1.0;
+  }
+  const double isc = 1.0 / sc;
   for (int q = 0; q < k; ++q) {
+    PPt p = pts[index_at(q)];
+    if (Cond) {
+      p.X = (p.X - cx) * isc;
+      p.Y = (p.Y - cy) * isc;
+      p.Z = (p.Z - cz) * isc;
+    }
     double a0[12], a1[12];
-    dlt_rows(pts[index_at(q)], a0, a1);
+    dlt_rows(p, a0, a1);
     givens_row(R, a0);
     givens_row(R, a1);
   }
   double c0[12];
   smallest_right_sv(R, c0);
   enforce_pose(c0, Rm, t);
+  if (Cond) {
+    t[0] = sc * t[0] - (Rm[0] * cx + Rm[1] * cy + Rm[2] * cz);
+    t[1] = sc * t[1] - (Rm[3] * cx + Rm[4] * cy + Rm[5] * cz);
+    t[2] = sc * t[2] - (Rm[6] * cx + Rm[7] * cy + Rm[8] * cz);
+  }
 }
 
 constexpr int kMaxK = 16;
@@ -251,7 +302,8 @@ constexpr int kMaxK = 16;
 __global__ __launch_bounds__(256) void k_pnp_solve(const PPt *__restrict__ pts, int m, int H,
                                                    int k, int mode, uint64_t seed,
                                                    const int *__restrict__ tuples,
-                                                   double *__restrict__ Psoa, int64_t ld) {
+                                                   double *__restrict__ Psoa, int64_t ld,
+                                                   int cond) {
   const int h = blockIdx.x * blockDim.x + threadIdx.x;
   if (h >= H) return;
   double Rm[9], t[3];
@@ -259,12 +311,16 @@ __global__ __launch_bounds__(256) void k_pnp_solve(const PPt *__restrict__ pts, 
     int s6[6];
     floyd_sample<6>(seed, static_cast<uint64_t>(h), m, s6);
     // select from the 6 registers without dynamic indexing
-    pnp_solve_points(pts, 6, [&](int q) {
+    auto at = [&](int q) {
       return q == 0 ? s6[0] : q == 1 ? s6[1] : q == 2 ? s6[2] : q == 3 ? s6[3] : q == 4 ? s6[4] : s6[5];
-    }, Rm, t);
+    };
+    if (cond)
+      pnp_solve_points<true>(pts, 6, at, Rm, t);
+    else
+      pnp_solve_points<false>(pts, 6, at, Rm, t);
   } else {
     const int *tup = tuples + static_cast<int64_t>(h) * k;
-    pnp_solve_points(pts, k, [&](int q) { return tup[q]; }, Rm, t);
+    pnp_solve_points<false>(pts, k, [&](int q) { return tup[q]; }, Rm, t);
   }
 #pragma unroll
   for (int q = 0; q < 9; ++q) Psoa[q * ld + h] = Rm[q];
@@ -294,7 +350,7 @@ __global__ __launch_bounds__(64) void k_pnp_dlt_all(const PPt *__restrict__ pts,
 __global__ __launch_bounds__(256) void k_pnp_count(const PPt *__restrict__ pts, int m, int H,
                                                    const double *__restrict__ Psoa, int64_t ld,
                                                    int chunk, int nchunks, double thresh,
-                                                   int *__restrict__ counts) {
+                                                   PxMetric mt, int *__restrict__ counts) {
   const int lane = threadIdx.x & 63;
   const int u = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   const int ngroups = (H + 63) >> 6;
@@ -312,9 +368,11 @@ __global__ __launch_bounds__(256) void k_pnp_count(const PPt *__restrict__ pts, 
     const double q0 = fma(P[0], p.X, fma(P[1], p.Y, fma(P[2], p.Z, P[9])));
     const double q1 = fma(P[3], p.X, fma(P[4], p.Y, fma(P[5], p.Z, P[10])));
     const double q2 = fma(P[6], p.X, fma(P[7], p.Y, fma(P[8], p.Z, P[11])));
-    // |pi(y) - pi(q)|^2 <= thr  <=>  (u q2 - q0)^2 + (v q2 - q1)^2 <= thr q2^2, q2 != 0
-    const double du = fma(p.u, q2, -q0), dv = fma(p.v, q2, -q1);
-    const double lhs = fma(du, du, dv * dv);
+    // |M (pi(y) - pi(q))|^2 <= thr  <=>  |M (u q2 - q0, v q2 - q1)|^2 <= thr q2^2, q2 != 0
+    // (identity M: a du + 0 dv == du and 1 dv == dv exactly, the reference-mode test)
+    const double du0 = fma(p.u, q2, -q0), dv = fma(p.v, q2, -q1);
+    const double du = fma(mt.a, du0, mt.b * dv), dvm = mt.c * dv;
+    const double lhs = fma(du, du, dvm * dvm);
     cnt += (q2 != 0.0 && lhs <= thresh * (q2 * q2)) ? 1 : 0;
   }
   if (h < H) atomicAdd(&counts[h], cnt);
@@ -397,15 +455,26 @@ __device__ __forceinline__ bool pnp_inlier_ref(const double (&Rm)[9], const doub
   return thresh >= e;
 }
 
-__device__ void ordered_compact(const PPt *pts, int m, const double (&Rm)[9],
-                                const double (&t)[3], double thresh, bool have, int64_t *out,
-                                int64_t *n_out, int *woff, int *base_s) {
+// cv.solvePnPRansac's inlier test (OpenCV: projectPoints, dx^2 + dy^2 <= err^2) in pixels.
+__device__ __forceinline__ bool pnp_inlier_px(const double (&Rm)[9], const double (&t)[3],
+                                              const PPt &p, double thresh, const PxMetric &mt) {
+  const double q0 = fma(Rm[0], p.X, fma(Rm[1], p.Y, fma(Rm[2], p.Z, t[0])));
+  const double q1 = fma(Rm[3], p.X, fma(Rm[4], p.Y, fma(Rm[5], p.Z, t[1])));
+  const double q2 = fma(Rm[6], p.X, fma(Rm[7], p.Y, fma(Rm[8], p.Z, t[2])));
+  const double du0 = fma(p.u, q2, -q0), dv = fma(p.v, q2, -q1);
+  const double du = fma(mt.a, du0, mt.b * dv), dvm = mt.c * dv;
+  return q2 != 0.0 && fma(du, du, dvm * dvm) <= thresh * (q2 * q2);
+}
+
+template <class Pred>
+__device__ void ordered_compact(int m, Pred pred, bool have, int64_t *out, int64_t *n_out,
+                                int *woff, int *base_s) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (tid == 0) *base_s = 0;
   __syncthreads();
   for (int b = 0; b < m; b += 1024) {
     const int i = b + tid;
-    const bool take = have && i < m && pnp_inlier_ref(Rm, t, pts[i], thresh);
+    const bool take = have && i < m && pred(i);
     const unsigned long long bal = __ballot(take);
     const int before = __popcll(bal & ((1ull << lane) - 1ull));
     if (lane == 0) woff[w] = __popcll(bal);
@@ -438,9 +507,38 @@ __global__ __launch_bounds__(1024) void k_pnp_inliers(const PPt *__restrict__ me
   for (int q = 0; q < 9; ++q) Rm[q] = res->R[q];
 #pragma unroll
   for (int q = 0; q < 3; ++q) t[q] = res->t[q];
-  ordered_compact(med, m_med, Rm, t, thresh, have, res->inliers, &res->n_med, woff, &base_s);
-  ordered_compact(high, m_high, Rm, t, thresh, have, res->inliers + m_med, &res->n_high, woff,
-                  &base_s);
+  ordered_compact(
+      m_med, [&](int i) { return pnp_inlier_ref(Rm, t, med[i], thresh); }, have, res->inliers,
+      &res->n_med, woff, &base_s);
+  ordered_compact(
+      m_high, [&](int i) { return pnp_inlier_ref(Rm, t, high[i], thresh); }, have,
+      res->inliers + m_med, &res->n_high, woff, &base_s);
+}
+
+// rs_pnp_ransac_cv: the pose of hypothesis `best` (chosen on the host by the adaptive
+// replay), then its pixel-space consensus set in point order.
+__global__ __launch_bounds__(1024) void k_pnp_inliers_px(const PPt *__restrict__ pts, int m,
+                                                         const double *__restrict__ Psoa,
+                                                         int64_t ld, int64_t best, int64_t count,
+                                                         double thresh, PxMetric mt,
+                                                         PnpDevResult *res) {
+  __shared__ int woff[16];
+  __shared__ int base_s;
+  double Rm[9], t[3];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) Rm[q] = Psoa[q * ld + best];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) t[q] = Psoa[(9 + q) * ld + best];
+  if (threadIdx.x == 0) {
+    for (int q = 0; q < 9; ++q) res->R[q] = Rm[q];
+    for (int q = 0; q < 3; ++q) res->t[q] = t[q];
+    res->best_index = best;
+    res->best_count = count;
+    res->n_high = 0;
+  }
+  ordered_compact(
+      m, [&](int i) { return pnp_inlier_px(Rm, t, pts[i], thresh, mt); }, true, res->inliers,
+      &res->n_med, woff, &base_s);
 }
 
 __global__ __launch_bounds__(256) void k_pack_ppts(const double *__restrict__ X,
@@ -563,7 +661,8 @@ extern "C" int rs_pnp_ransac(rs_ctx *c, const double *X_med, const double *y_med
                      static_cast<int>(m_high), ph);
   HIP_TRY(hipMemsetAsync(dcnt, 0, sizeof(int) * H, s));
   hipLaunchKernelGGL(rsd::k_pnp_solve, dim3((H + 255) / 256), dim3(256), 0, s, ph,
-                     static_cast<int>(m_high), static_cast<int>(H), k, mode, seed, dtup, dP, ld);
+                     static_cast<int>(m_high), static_cast<int>(H), k, mode, seed, dtup, dP, ld,
+                     0);
   HIP_TRY(hipGetLastError());
   const int64_t groups = (H + 63) / 64;
   int64_t nch = std::max<int64_t>(1, std::min<int64_t>((8192 + groups - 1) / groups, (m_med + 63) / 64));
@@ -572,7 +671,7 @@ extern "C" int rs_pnp_ransac(rs_ctx *c, const double *X_med, const double *y_med
   const int64_t units = groups * nch;
   hipLaunchKernelGGL(rsd::k_pnp_count, dim3((units + 3) / 4), dim3(256), 0, s, pm,
                      static_cast<int>(m_med), static_cast<int>(H), dP, ld, chunk,
-                     static_cast<int>(nch), thresh, dcnt);
+                     static_cast<int>(nch), thresh, rsd::PxMetric{1.0, 0.0, 1.0}, dcnt);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(rsd::k_pnp_select, dim3(1), dim3(1024), 0, s, dcnt, static_cast<int>(H), dP,
                      ld, dres);
@@ -592,5 +691,127 @@ extern "C" int rs_pnp_ransac(rs_ctx *c, const double *X_med, const double *y_med
   if (n_inl_high) *n_inl_high = r->n_high;
   if (inl_med) std::memcpy(inl_med, r->inliers, sizeof(int64_t) * r->n_med);
   if (inl_high) std::memcpy(inl_high, r->inliers + m_med, sizeof(int64_t) * r->n_high);
+  return RS_OK;
+}
+
+// OpenCV's RANSACUpdateNumIters (the adaptive stopping rule of cv::solvePnPRansac's RANSAC
+// loop): iterations needed to draw one all-inlier sample of `model_points` with probability
+// `p` at outlier ratio `ep`, never more than `max_iters`.
+static int64_t ransac_update_num_iters(double p, double ep, int model_points, int64_t max_iters) {
+  p = std::min(std::max(p, 0.0), 1.0);
+  ep = std::min(std::max(ep, 0.0), 1.0);
+  double num = std::max(1.0 - p, std::numeric_limits<double>::min());
+  double denom = 1.0 - std::pow(1.0 - ep, model_points);
+  if (denom < std::numeric_limits<double>::min()) return 0;
+  num = std::log(num);
+  denom = std::log(denom);
+  return (denom >= 0.0 || -num >= static_cast<double>(max_iters) * (-denom))
+             ? max_iters
+             : static_cast<int64_t>(std::lrint(num / denom));
+}
+
+extern "C" int rs_pnp_ransac_cv(rs_ctx *c, const double *X, const double *uv, int64_t m,
+                                const double *K, int64_t max_iters, uint64_t seed,
+                                double reproj_err, double confidence, int32_t model_points,
+                                rs_pnp_result *out, int64_t *inliers, int64_t *n_inliers,
+                                int64_t *iters_used) {
+  if (!c || !X || !uv || !K || !out) return fail(RS_EINVAL, "null pointer");
+  if (m < 6) return fail(RS_EINVAL, "the DLT minimal solver needs m >= 6 correspondences");
+  if (m > (1 << 26) || max_iters < 1 || max_iters > (1LL << 28))
+    return fail(RS_EINVAL, "bad dimensions");
+  if (model_points < 1 || model_points > 64) return fail(RS_EINVAL, "bad model_points");
+  if (!(reproj_err >= 0.0) || !std::isfinite(reproj_err))
+    return fail(RS_EINVAL, "reprojectionError must be finite and >= 0");
+  if (K[3] != 0.0 || K[6] != 0.0 || K[7] != 0.0 || !(K[8] != 0.0))
+    return fail(RS_EINVAL, "cameraMatrix must be upper triangular with K[2,2] != 0");
+  const double k8 = K[8];
+  const double fx = K[0] / k8, sk = K[1] / k8, cx = K[2] / k8, fy = K[4] / k8, cy = K[5] / k8;
+  if (!(fx != 0.0) || !(fy != 0.0) || !std::isfinite(fx * fy * sk * cx * cy))
+    return fail(RS_EINVAL, "cameraMatrix must have finite, nonzero fx and fy");
+  HIP_TRY(hipSetDevice(c->device));
+  // C-normalised homogeneous image points y = K^-1 (u, v, 1) for the DLT
+  std::vector<double> yn(3 * m);
+  for (int64_t i = 0; i < m; ++i) {
+    const double y1 = (uv[2 * i + 1] - cy) / fy;
+    yn[3 * i] = (uv[2 * i] - cx - sk * y1) / fx;
+    yn[3 * i + 1] = y1;
+    yn[3 * i + 2] = 1.0;
+  }
+  const int64_t H = max_iters, ld = (H + 63) / 64 * 64;
+  const size_t b_in = align256(sizeof(double) * 3 * m), b_p = align256(sizeof(rsd::PPt) * m);
+  const size_t b_P = align256(sizeof(double) * 12 * ld), b_cnt = align256(sizeof(int) * ld);
+  const size_t b_res = align256(sizeof(rsd::PnpDevResult) + sizeof(int64_t) * m);
+  int st = rs::ensure_scratch(c, 2 * b_in + b_p + b_P + b_cnt + b_res);
+  if (st) return st;
+  char *p = static_cast<char *>(c->scratch);
+  auto take = [&p](size_t b) {
+    char *q = p;
+    p += b;
+    return q;
+  };
+  double *dX = reinterpret_cast<double *>(take(b_in));
+  double *dy = reinterpret_cast<double *>(take(b_in));
+  auto *pts = reinterpret_cast<rsd::PPt *>(take(b_p));
+  double *dP = reinterpret_cast<double *>(take(b_P));
+  int *dcnt = reinterpret_cast<int *>(take(b_cnt));
+  auto *dres = reinterpret_cast<rsd::PnpDevResult *>(take(b_res));
+  hipStream_t s = c->stream;
+  const rsd::PxMetric mt{fx, sk, fy};
+  const double thresh = reproj_err * reproj_err;
+  HIP_TRY(hipMemcpyAsync(dX, X, sizeof(double) * 3 * m, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(dy, yn.data(), sizeof(double) * 3 * m, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(rsd::k_pack_ppts, dim3((m + 255) / 256), dim3(256), 0, s, dX, dy,
+                     static_cast<int>(m), pts);
+  HIP_TRY(hipMemsetAsync(dcnt, 0, sizeof(int) * H, s));
+  hipLaunchKernelGGL(rsd::k_pnp_solve, dim3((H + 255) / 256), dim3(256), 0, s, pts,
+                     static_cast<int>(m), static_cast<int>(H), 6, RS_SAMPLER_PHILOX, seed,
+                     static_cast<const int *>(nullptr), dP, ld, 1);
+  HIP_TRY(hipGetLastError());
+  const int64_t groups = (H + 63) / 64;
+  int64_t nch = std::max<int64_t>(1, std::min<int64_t>((8192 + groups - 1) / groups, (m + 63) / 64));
+  const int chunk = static_cast<int>((m + nch - 1) / nch);
+  nch = (m + chunk - 1) / chunk;
+  const int64_t units = groups * nch;
+  hipLaunchKernelGGL(rsd::k_pnp_count, dim3((units + 3) / 4), dim3(256), 0, s, pts,
+                     static_cast<int>(m), static_cast<int>(H), dP, ld, chunk,
+                     static_cast<int>(nch), thresh, mt, dcnt);
+  HIP_TRY(hipGetLastError());
+  std::vector<int> cnt(H);
+  HIP_TRY(hipMemcpyAsync(cnt.data(), dcnt, sizeof(int) * H, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  // OpenCV's sequential loop over the same hypothesis order: a model replaces the best only
+  // with goodCount > max(maxGoodCount, modelPoints - 1), and then shrinks the iteration budget
+  int64_t niters = H, best = -1, it = 0;
+  int good = 0;
+  for (; it < niters; ++it) {
+    const int g = cnt[it];
+    if (g > std::max(good, model_points - 1)) {
+      best = it;
+      good = g;
+      niters = ransac_update_num_iters(confidence, static_cast<double>(m - g) / m, model_points,
+                                       niters);
+    }
+  }
+  if (iters_used) *iters_used = it;
+  if (best < 0) {
+    std::memset(out, 0, sizeof(*out));
+    out->best_index = -1;
+    if (n_inliers) *n_inliers = 0;
+    return RS_OK;
+  }
+  hipLaunchKernelGGL(rsd::k_pnp_inliers_px, dim3(1), dim3(1024), 0, s, pts, static_cast<int>(m),
+                     dP, ld, best, static_cast<int64_t>(good), thresh, mt, dres);
+  HIP_TRY(hipGetLastError());
+  std::vector<char> host(sizeof(rsd::PnpDevResult) + sizeof(int64_t) * m);
+  HIP_TRY(hipMemcpyAsync(host.data(), dres, host.size(), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  const auto *r = reinterpret_cast<const rsd::PnpDevResult *>(host.data());
+  if (r->n_med != good) return fail(RS_EDEVICE, "pixel consensus recount mismatch");
+  std::memcpy(out->R, r->R, sizeof(out->R));
+  std::memcpy(out->t, r->t, sizeof(out->t));
+  out->best_index = best;
+  out->best_count = good;
+  if (n_inliers) *n_inliers = r->n_med;
+  if (inliers) std::memcpy(inliers, r->inliers, sizeof(int64_t) * r->n_med);
   return RS_OK;
 }

@@ -260,7 +260,10 @@ extern "C" int rs_np_choice_tuples_multi(int64_t B, const uint32_t *seeds, uint3
   }
   const int64_t per = count * k;
   std::atomic<int64_t> next{0};
-  auto work = [&] {
+  std::atomic<bool> oom{false};
+  // no exception may leave a worker (std::terminate would take the host process down): an
+  // allocation failure stops the whole batch and the call returns RS_ENOMEM
+  auto work_streams = [&] {
     std::vector<int32_t> perm, iota;
     for (int64_t b; (b = next.fetch_add(1)) < B;) {
       int32_t *o = out + b * per;
@@ -278,15 +281,30 @@ extern "C" int rs_np_choice_tuples_multi(int64_t B, const uint32_t *seeds, uint3
       mt.store(mt_keys + b * kN, mt_pos + b);
     }
   };
+  auto work = [&]() noexcept {
+    try {
+      work_streams();
+    } catch (...) {
+      oom = true;
+      next = B;
+    }
+  };
   // default: the hardware threads, at most 16 (a one-GPU share of a shared host)
   int nt = threads > 0 ? threads
                        : std::min(16, static_cast<int>(std::thread::hardware_concurrency()));
   nt = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>({static_cast<int64_t>(nt), B, 64})));
   std::vector<std::thread> pool;
-  for (int i = 1; i < nt; ++i) pool.emplace_back(work);
+  try {
+    pool.reserve(static_cast<size_t>(nt));
+    for (int i = 1; i < nt; ++i) pool.emplace_back(work);
+  } catch (...) {
+    // fewer threads than asked (thread creation or the pool's allocation failed): the
+    // streams are handed out dynamically, so the ones that exist -- at least this one --
+    // still draw every stream
+  }
   work();
   for (auto &t : pool) t.join();
-  return RS_OK;
+  return oom ? rs::fail(RS_ENOMEM, "rs_np_choice_tuples_multi: out of host memory") : RS_OK;
 }
 
 extern "C" int rs_py_shuffle_tuples(uint32_t *mt_key, int32_t *mt_pos, int64_t n, int32_t k,

@@ -100,6 +100,9 @@ _SIGS = {
     "rs_pnp_ransac": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, _dp, C.c_int64, C.c_int32,
                                 C.c_int64, C.c_int32, C.c_uint64, _i32p, C.c_double,
                                 C.POINTER(PnpResult), _i64p, _i64p, _i64p, _i64p]),
+    "rs_pnp_ransac_cv": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, C.c_int64, C.c_uint64,
+                                   C.c_double, C.c_double, C.c_int32, C.POINTER(PnpResult),
+                                   _i64p, _i64p, _i64p]),
     "rs_pairs_f8_ransac": (C.c_int, [C.c_void_p, _dp, _dp, _i64p, C.c_int64, C.c_int64,
                                      C.c_int32, C.c_uint64, _i64p, _i32p, C.c_double,
                                      C.POINTER(PairResult), _i32p]),
@@ -260,8 +263,10 @@ def np_choice_tuples_multi(keys, poss, ns, k, count, threads=0, seeds=None):
     B = ns.shape[0]
     sp = None
     if seeds is not None:
-        seeds = np.ascontiguousarray(np.asarray(seeds, dtype=np.int64) & 0xFFFFFFFF,
-                                     dtype=np.uint32).reshape(B)
+        seeds = np.asarray(seeds).reshape(-1)
+        for sd in seeds:
+            _check_np_seed(sd)
+        seeds = np.ascontiguousarray(seeds.astype(np.int64), dtype=np.uint32).reshape(B)
         sp = ptr(seeds, C.c_uint32)
         keys = np.empty((B, MT_N), dtype=np.uint32)
         poss = np.empty(B, dtype=np.int32)
@@ -313,10 +318,18 @@ def mt_jump(key, pos, steps):
     return out, p.value
 
 
+def _check_np_seed(seed):
+    """np.random.seed's accepted range for an integer seed (it raises ValueError outside)."""
+    s = int(seed)
+    if s != seed or not 0 <= s < 2 ** 32:
+        raise ValueError("Seed must be between 0 and 2**32 - 1")
+    return s
+
+
 def np_seed(seed):
     key = np.empty(MT_N, dtype=np.uint32)
     p = C.c_int32(0)
-    check(lib().rs_np_seed(int(seed) & 0xFFFFFFFF, ptr(key, C.c_uint32), C.byref(p)))
+    check(lib().rs_np_seed(_check_np_seed(seed), ptr(key, C.c_uint32), C.byref(p)))
     return key, p.value
 
 

@@ -4,21 +4,45 @@
 ``(retval, rvec (3,1), tvec (3,1), inliers (k,1) int32)`` like ``cv.solvePnPRansac`` and
 ``Rodrigues(src)`` returns ``(dst, jacobian)``, so ``Tables.addNewView`` drops them in.
 
-Behind it: pixels are C-normalised with K (zero distortion only, as tables.py:140 passes),
-then the GPU PnP-RANSAC (DLT minimal solver, pnp.py:132-160) runs ``iterationsCount``
-hypotheses with the reprojection test |pi(y) - pi(Rx + t)| <= reprojectionError / f in
-normalised units (f = sqrt(fx fy)), and the pose is re-estimated by the DLT on the consensus
-set.  OpenCV's own EPnP + Levenberg-Marquardt refinement is not reproduced: parity with
-OpenCV is unpinned (it is absent and unversioned).
+What runs (rs_pnp_ransac_cv, pnp_kernels.hip), following OpenCV's solvePnPRansac structure:
+
+  * up to ``iterationsCount`` 6-point hypotheses (DLT minimal solver on C-normalised points,
+    pnp.py:132-160, with the sample's world points centred and RMS-scaled first -- without
+    that conditioning the 12x12 DLT system does not survive pixel noise on compact, distant
+    point sets such as BAdino2's reconstruction) are solved and scored on the GPU with
+    OpenCV's test in PIXELS,
+    ``|K pi(R x + t) - uv|^2 <= reprojectionError^2``;
+  * OpenCV's sequential loop is replayed over that hypothesis order: a model replaces the best
+    only if its inlier count exceeds ``max(best, modelPoints - 1)``, and each new best shrinks
+    the budget with RANSACUpdateNumIters(confidence, outlier ratio, modelPoints, budget), so
+    ``confidence`` stops the search early exactly as OpenCV's does (here modelPoints = 6, the
+    DLT sample size; OpenCV's EPnP kernel samples 5);
+  * the sampling stream is a fixed-seed Philox stream per call, the analogue of OpenCV seeding
+    its RANSAC RNG with the same constant on every call: equal inputs give equal outputs;
+  * the winning pose is refined on its consensus set by Levenberg-Marquardt on the pixel
+    reprojection error (OpenCV's SOLVEPNP_ITERATIVE refinement, started from the RANSAC pose),
+    and ``inliers`` is the RANSAC consensus set, in point order.
+
+Limits: zero lens distortion only (tables.py:140 passes zeros); m >= 6 correspondences (the
+DLT) where OpenCV's EPnP kernel accepts m >= 4 -- fewer return ``(False, None, None, None)``
+and tables.add_new_view raises a ValueError naming the count.  OpenCV itself is absent and
+unversioned here, so parity with its exact samples is unpinned; the tests
+check the documented semantics (pixel threshold, adaptive budget, determinism).
 """
 from __future__ import annotations
 
 import numpy as np
 
-from . import pnp as _pnp
-from . import ransac as _ransac
+from . import _ffi
 
-_seed_counter = [0]
+# OpenCV constructs its RANSAC RNG as RNG((uint64)-1) on every call
+CV_RANSAC_SEED = 0xFFFFFFFFFFFFFFFF
+MODEL_POINTS = 6
+LM_MAX_ITERS = 20  # OpenCV's solvePnP ITERATIVE: CvLevMarq criteria (20 iterations, FLT_EPSILON)
+
+# the last call's RANSAC outcome before refinement: hypotheses the loop consumed, the winning
+# hypothesis and its pose (diagnostics / tests)
+last_ransac = {}
 
 
 def Rodrigues(src, dst=None, jacobian=None):
@@ -46,26 +70,60 @@ def Rodrigues(src, dst=None, jacobian=None):
     return (th * w).reshape(3, 1), None
 
 
+def project_points(X, rvec, tvec, K):
+    """Pixel projections K pi(R x + t) (cv.projectPoints with zero distortion)."""
+    R, _ = Rodrigues(rvec)
+    q = np.asarray(X, dtype=np.float64).reshape(-1, 3) @ R.T + np.asarray(tvec).reshape(1, 3)
+    p = q[:, :2] / q[:, 2:3]
+    K = np.asarray(K, dtype=np.float64) / float(K[2][2])
+    return np.stack((K[0, 0] * p[:, 0] + K[0, 1] * p[:, 1] + K[0, 2],
+                     K[1, 1] * p[:, 1] + K[1, 2]), axis=1)
+
+
+def _refine_lm(X, uv, K, rvec, tvec):
+    from scipy.optimize import least_squares
+
+    def res(x):
+        return (project_points(X, x[:3], x[3:], K) - uv).ravel()
+
+    x0 = np.concatenate((np.ravel(rvec), np.ravel(tvec)))
+    r0 = res(x0)
+    if not np.all(np.isfinite(r0)) or len(r0) < 6:
+        return rvec, tvec
+    sol = least_squares(res, x0, method="lm", max_nfev=LM_MAX_ITERS * 7,
+                        xtol=np.finfo(np.float32).eps, ftol=np.finfo(np.float32).eps)
+    if not np.all(np.isfinite(sol.x)) or sol.cost > 0.5 * float(r0 @ r0):
+        return rvec, tvec  # CvLevMarq only accepts steps that lower the error
+    return sol.x[:3].reshape(3, 1), sol.x[3:].reshape(3, 1)
+
+
 def solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec=None, tvec=None,
                    useExtrinsicGuess=False, iterationsCount=100, reprojectionError=8.0,
-                   confidence=0.99, inliers=None, flags=0):
-    X = np.asarray(objectPoints, dtype=np.float64).reshape(-1, 3)
-    uv = np.asarray(imagePoints, dtype=np.float64).reshape(-1, 2)
+                   confidence=0.99, inliers=None, flags=0, ctx=None):
+    X = np.ascontiguousarray(np.asarray(objectPoints, dtype=np.float64).reshape(-1, 3))
+    uv = np.ascontiguousarray(np.asarray(imagePoints, dtype=np.float64).reshape(-1, 2))
     if len(X) != len(uv):
         raise ValueError("objectPoints and imagePoints must have the same count")
     if distCoeffs is not None and np.any(np.asarray(distCoeffs) != 0):
         raise ValueError("only zero lens distortion is supported")
-    K = np.asarray(cameraMatrix, dtype=np.float64)
-    if len(X) < 6:
+    K = np.ascontiguousarray(np.asarray(cameraMatrix, dtype=np.float64).reshape(3, 3))
+    last_ransac.clear()
+    if len(X) < MODEL_POINTS:
         return False, None, None, None
-    y = (np.linalg.inv(K) @ np.vstack([uv.T, np.ones((1, len(uv)))])).T
-    f = np.sqrt(K[0, 0] * K[1, 1])
-    thr = (float(reprojectionError) / f) ** 2
-    _seed_counter[0] += 1
-    R, t, inl, _, best, _ = _ransac.ransac_pnp(X, y, X, y, int(iterationsCount), thr, 6,
-                                               sampler="philox", seed=_seed_counter[0])
-    if best < 0 or len(inl) < 6:
+    ctx = ctx or _ffi.default_context()
+    res = _ffi.PnpResult()
+    inl = np.empty(len(X), np.int64)
+    n_inl, used = _ffi.C.c_int64(0), _ffi.C.c_int64(0)
+    _ffi.check(_ffi.lib().rs_pnp_ransac_cv(
+        ctx.handle, _ffi.ptr(X, _ffi.C.c_double), _ffi.ptr(uv, _ffi.C.c_double), len(X),
+        _ffi.ptr(K, _ffi.C.c_double), int(iterationsCount), CV_RANSAC_SEED,
+        float(reprojectionError), float(confidence), MODEL_POINTS, _ffi.C.byref(res),
+        _ffi.ptr(inl, _ffi.C.c_int64), _ffi.C.byref(n_inl), _ffi.C.byref(used)))
+    last_ransac.update(iterations=int(used.value), best_index=int(res.best_index))
+    if res.best_index < 0:
         return False, None, None, None
-    R, t = _pnp.pnp_minimize(X[inl], y[inl], len(inl))
-    rv, _ = Rodrigues(R)
-    return True, rv.reshape(3, 1), t.reshape(3, 1), inl.astype(np.int32).reshape(-1, 1)
+    inl = inl[:n_inl.value]
+    last_ransac.update(R=np.array(res.R[:]).reshape(3, 3), t=np.array(res.t[:]))
+    rv, _ = Rodrigues(last_ransac["R"])
+    rv, tv = _refine_lm(X[inl], uv[inl], K, rv, np.array(res.t[:]))
+    return True, rv.reshape(3, 1), tv.reshape(3, 1), inl.astype(np.int32).reshape(-1, 1)

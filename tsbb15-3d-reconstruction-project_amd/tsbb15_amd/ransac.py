@@ -57,14 +57,30 @@ def gen_rnd_indices(set_length, n, rng=None):
 _GPU_MIN_DRAWS = 1 << 22
 
 
-def gen_rnd_tuples(set_length, n, count, rng=None):
-    """``count`` consecutive gen_rnd_indices draws as an int32 (count, n) array."""
+# gen_rnd_tuples may route large streams to the GPU parser; False keeps every stream on the
+# native host replay (e.g. in a process that forks CPU workers and must not open a device).
+GPU_SHUFFLE = True
+
+
+def gen_rnd_tuples(set_length, n, count, rng=None, ctx=None, gpu=None):
+    """``count`` consecutive gen_rnd_indices draws as an int32 (count, n) array.
+
+    Both routes give the same tuples and advance ``rng`` identically.  The GPU route is taken
+    for long streams when ``gpu`` (default GPU_SHUFFLE) allows it; if no device or context can
+    be had there, the draw falls back to the native host replay (rs_py_shuffle_tuples)."""
     st, key, pos = _py_rng_state(rng)
-    if (0 < n <= 8 and 2 <= set_length <= 10241 and n <= set_length
+    use_gpu = GPU_SHUFFLE if gpu is None else bool(gpu)
+    tup = None
+    if (use_gpu and 0 < n <= 8 and 2 <= set_length <= 10241 and n <= set_length
             and 1.4 * set_length * count >= _GPU_MIN_DRAWS):
-        tup, key, pos = _ffi.py_shuffle_tuples_gpu(key, pos, int(set_length), int(n),
-                                                   int(count))
-    else:
+        try:
+            c = ctx or _ffi.default_context()
+        except (RuntimeError, OSError):
+            c = None  # no visible device / runtime: host replay below
+        if c is not None:
+            tup, key, pos = _ffi.py_shuffle_tuples_gpu(key, pos, int(set_length), int(n),
+                                                       int(count), ctx=c)
+    if tup is None:
         tup, key, pos = _ffi.py_shuffle_tuples(key, pos, int(set_length), int(n), int(count))
     _py_rng_set(rng, st, key, pos)
     return tup
