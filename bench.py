@@ -328,10 +328,9 @@ def extras(ctx, rank, world, dist, comm):
     return out
 
 
-# counting kernel behind each RSAMD_COUNT choice (f8_plan.hip; "q" is the default)
-COUNT_KERNEL = {"q": "k_f8_count32q", "w": "k_f8_count32x", "x": "k_f8_count32x",
-                "y": "k_f8_count32x", "z": "k_f8_count32x", "fp32": "k_f8_count32",
-                "pk": "k_f8_count32p", "fp64": "k_f8_count"}
+# the counting kernel the plan runs: fp32 with the float64 guard re-test, or (RSAMD_COUNT=fp64,
+# tools only) the plain float64 kernel
+COUNT_KERNEL = {"fp32": "k_f8_count32q", "fp64": "k_f8_count"}
 
 
 def load_pmc(n_corr, hyps):
@@ -474,8 +473,8 @@ def main():
                    "n_corr": args.n, "hypotheses_per_step": H, "sampler": "philox (throughput)",
                    "parallelism": f"pairs sharded, {world} pair(s) on {world} GPU(s)",
                    "exchange": exchange},
-        "roofline": {"bound": "valu", "kernel": COUNT_KERNEL.get(os.environ.get("RSAMD_COUNT", "q"),
-                                                          "k_f8_count32"),
+        "roofline": {"bound": "valu", "kernel": COUNT_KERNEL["fp64" if os.environ.get("RSAMD_COUNT") == "fp64"
+                                                         else "fp32"],
                      "achieved": achieved, "peak": PEAK_FP32_VALU_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_FP32_VALU_TFLOPS,
                      "traffic": pmc,

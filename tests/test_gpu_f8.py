@@ -220,7 +220,7 @@ def _near_threshold_points(F, p1, p2, deltas, rng, keep):
 
 # counting kernels: q = point-pair packed (default), w / x / y = packed-pair fp32 with packed / plain decision, fp32 = scalar fp32, pk = two hypotheses
 # per lane, fp64 = the float64 reference-order kernel every fp32 variant must match exactly
-COUNT_MODES = ("q", "w", "x", "y", "z", "fp32", "pk", "fp64")
+COUNT_MODES = ("fp32", "fp64")  # k_f8_count32q (guard band + re-test), k_f8_count
 
 
 def test_fp32_guard_band_exact_near_threshold(ctx, monkeypatch):
@@ -234,8 +234,8 @@ def test_fp32_guard_band_exact_near_threshold(ctx, monkeypatch):
                                  set(tup.ravel().tolist()))
     res = {}
     for mode in COUNT_MODES:
-        monkeypatch.setenv("RSAMD_COUNT", mode)
         plan = _ffi.F8Plan(ctx, 512, 4)
+        plan.set_count_precision(mode == "fp64")
         plan.set_points(p1, p2n)
         plan.run(4, mode=_ffi.SAMPLER_TUPLES, tuples=tup)
         plan.result()
@@ -256,8 +256,8 @@ def test_fp32_and_fp64_counting_identical_full_size(ctx, monkeypatch, name):
     H = 20_000
     counts = {}
     for mode in COUNT_MODES:
-        monkeypatch.setenv("RSAMD_COUNT", mode)
         plan = _ffi.F8Plan(ctx, n, H)
+        plan.set_count_precision(mode == "fp64")
         plan.set_points(z["p1"], z["p2"])
         plan.run(H, mode=_ffi.SAMPLER_PHILOX, seed=99)
         plan.result()
@@ -270,11 +270,11 @@ def test_fp32_and_fp64_counting_identical_full_size(ctx, monkeypatch, name):
 @pytest.mark.parametrize("knobs", [
     {},                              # speculative S_RANSAC rows, tail on the CUs the solve leaves
     {"RSAMD_NOSPEC": "1"},           # the replay extracts S_RANSAC itself
-    {"RSAMD_TAILCUS": "0"},          # fixed 256-block tail
-    {"RSAMD_SOLVE_DIAG": "8"},       # Jacobi SVD rank-2 step instead of the adjugate form
+    {"RSAMD_QSLICES": "9"},          # many short count slices (more group boundaries)
+    {"RSAMD_WAVES": "37"},           # few waves: long slices over many groups
 ])
-def test_selection_and_solve_variants_match_golden(ctx, monkeypatch, knobs):
-    """The selection-tail and rank-2 variants reproduce the reference run (C2 goldens: tuples
+def test_selection_and_count_shapes_match_golden(ctx, monkeypatch, knobs):
+    """The selection-tail variants and counting launch shapes reproduce the reference run (C2 goldens: tuples
     from np.random.seed(0), per-hypothesis counts, winner, S_RANSAC) back to back: each run's
     tail rides with the next run's solve, and the last one is flushed alone."""
     for k, v in knobs.items():

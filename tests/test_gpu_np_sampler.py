@@ -87,10 +87,10 @@ print("ok")
 
 @pytest.mark.parametrize("knobs", [{"RSAMD_NP_SEGWORDS": str(1 << 20)},
                                    {"RSAMD_NP_KW": "8192"},
-                                   {"RSAMD_NP_KW": "262144", "RSAMD_NP_LANE_TUPLES": "1"}])
+                                   {"RSAMD_NP_KW": "262144"}])
 def test_gpu_stream_many_segments(knobs):
-    """Segments of 2^20 words, the shortest / longest parse chunks and the lane-per-hypothesis
-    tuple kernel (these knobs are read once per process, so in a child)."""
+    """Segments of 2^20 words and the shortest / longest parse chunks (these knobs are read
+    once per process, so in a child)."""
     env = dict(os.environ, **knobs,
                PYTHONPATH=os.pathsep.join([PKG_DIR, REPO, os.environ.get("PYTHONPATH", "")]))
     r = subprocess.run([sys.executable, "-c", _SEG_CHILD], env=env, capture_output=True,
@@ -219,9 +219,9 @@ print("ok")
 """
 
 
-@pytest.mark.parametrize("knobs", [{"RSAMD_NP_HOST": "1"}, {"RSAMD_OVERLAP": "1"}])
+@pytest.mark.parametrize("knobs", [{"RSAMD_NP_HOST": "1"}])
 def test_host_tuple_runs_back_to_back(knobs):
-    """The host-replay parity path (RSAMD_NP_HOST, the overlap variant) issues runs whose
+    """The host-replay parity path (RSAMD_NP_HOST) issues runs whose
     tuples live in host memory the library no longer references after the call: back-to-back
     runs with the arrays dropped at once still equal the oracle."""
     env = dict(os.environ, **knobs,

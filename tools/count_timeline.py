@@ -1,5 +1,6 @@
 """Wave timeline of the counting kernel (RSAMD_TSTAMP): when waves start and end within a
-C2 launch, to split the launch into ramp, steady state and drain.
+C2 launch, to split the launch into ramp, steady state and drain, and what makes waves of
+equal work take different times (re-test branches taken, XCD, SIMD occupancy at start).
 
   RSAMD_TSTAMP=/tmp/ts.bin python tools/count_timeline.py
 """
@@ -26,19 +27,47 @@ def main():
     for r in range(runs):
         plan.run(H, mode=_ffi.SAMPLER_PHILOX, seed=r)
         plan.result()
-    raw = np.fromfile(path, dtype=np.uint64).reshape(runs, -1, 2)
+    raw = np.fromfile(path, dtype=np.uint64).reshape(runs, -1, 4)
     for r in (runs - 2, runs - 1):
-        t = raw[r]
-        t = t[t[:, 0] > 0].astype(np.float64) * 10.0 / 1000.0  # 100 MHz ticks -> us
+        rec = raw[r]
+        rec = rec[rec[:, 0] > 0]
+        t = rec[:, :2].astype(np.float64) * 10.0 / 1000.0  # 100 MHz ticks -> us
         t0 = t[:, 0].min()
         st, en = t[:, 0] - t0, t[:, 1] - t0
         dur = en - st
+        nre = rec[:, 2].astype(np.int64)
+        hw = rec[:, 3].astype(np.int64)
+        xcc = hw & 7
+        hwid = hw >> 8
+        simd = (hwid >> 4) & 3
+        cu = (hwid >> 8) & 15
+        se = (hwid >> 13) & 7
         q = lambda a, p: float(np.percentile(a, p))
         print({"waves": len(t), "launch_us": round(en.max(), 1),
                "start_p0_p50_p90_max": [round(q(st, x), 1) for x in (0, 50, 90, 100)],
                "end_min_p10_p50_max": [round(q(en, x), 1) for x in (0, 10, 50, 100)],
-               "dur_p10_p50_p90": [round(q(dur, x), 1) for x in (10, 50, 90)]})
-        # resident waves over time
+               "dur_p10_p50_p90": [round(q(dur, x), 1) for x in (10, 50, 90)],
+               "retest_p10_p50_p90_max": [int(q(nre, x)) for x in (10, 50, 90, 100)]})
+        first = st < 2.0  # the first round (all resident at once)
+        if first.sum() > 10:
+            d, k = dur[first], nre[first]
+            c = np.corrcoef(d, k)[0, 1] if k.std() > 0 else 0.0
+            print("first round: corr(duration, retests) = %.2f" % c)
+            for x in range(8):
+                m = first & (xcc == x)
+                if m.any():
+                    print("  xcc %d: waves %d dur p50 %.1f us, retests p50 %d"
+                          % (x, m.sum(), np.median(dur[m]), int(np.median(nre[m]))))
+            lo, hi = k <= np.percentile(k, 25), k >= np.percentile(k, 75)
+            print("  dur p50 at low / high retest quartile: %.1f / %.1f us"
+                  % (np.median(d[lo]), np.median(d[hi])))
+            # waves sharing a SIMD at the start
+            key = (xcc * 8 + se) * 16 * 4 + cu * 4 + simd
+            _, inv, cnt = np.unique(key[first], return_inverse=True, return_counts=True)
+            per = cnt[inv]
+            for v in np.unique(per):
+                print("  %d waves on the SIMD: %d waves, dur p50 %.1f us"
+                      % (v, (per == v).sum(), np.median(d[per == v])))
         grid = np.arange(0, en.max() + 1, 2.0)
         live = [int(((st <= g) & (en > g)).sum()) for g in grid]
         print("live waves every 2 us:", live[:8], "...", live[-12:])

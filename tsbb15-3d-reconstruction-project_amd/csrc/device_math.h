@@ -18,49 +18,12 @@ struct Frame {
   double s, cx1, cy1, cx2, cy2;
 };
 
-// Rigorous error bounds of the fp32 test (see f8_kernels.hip, k_f8_count32).
-struct Guard32 {
-  float thr2;  // (t / s)^2 rounded to fp32
-  float K0, K1, Ku;
-  double thr2_px;  // t^2 for the fp64 re-test in pixel units
-};
-
-// Bound constants of the packed fp32 test (k_f8_count32p): B = Ka e^2 + Kb rhs + K0.
-struct GuardPk {
-  float thr2, Ka, Kb, K0;
-  double thr2_px;
-};
-
-// Decision constants of the packed-pair test (k_f8_count32x, derivation above it):
-//   sure inlier   (|e| + K1i) |e| + K0i  <  alpha m
-//   sure outlier  (|e| - K1o) |e| - K0o  >  beta  m
-// each side evaluated as one half of a v_pk_* pair.
-struct GuardX {
-  float K1i, K1o_neg;  // ( K1i, -K1o)
-  float K0i, K0o_neg;  // ( K0i, -K0o)
-  float alpha, beta;
-  double thr2_px;
-};
-
-// Decision constants of the plain-op decision (k_f8_count32x, DEC = 1):
-//   G = fl(e^2 - fl(alpha m)),  h = fl(K1 |e| + K0)
-//   sure inlier  G < -h;   sure outlier  G > fl(delta m + h)
-struct GuardY {
-  float K1, K0, alpha, delta;
-  double thr2_px;
-};
-
-// Per-hypothesis decision (k_f8_count32x, DEC = 3): constants live with each model (G4,
+// Per-hypothesis decision (k_f8_count32q): constants live with each model (G4,
 // written by the solve); only the float64 re-test threshold is global.
 struct GuardW {
   double thr2_px;
 };
 
-// Folded plain decision (k_f8_count32x, DEC = 2): sure inlier G < -h, ambiguous |G| <= h.
-struct GuardF {
-  float K1, K0, alpha, pad_;
-  double thr2_px;
-};
 
 // ----------------------------------------------------------------------------------------
 // Philox4x32-10 counter-based generator (throughput-mode sampler).
@@ -340,7 +303,7 @@ __device__ __forceinline__ void scaling8(const double (&x)[8], const double (&y)
 // xl, yl: left points (p1), xr, yr: right points (p2).  F row-major, pl^T F pr = 0.
 __device__ __forceinline__ void fmatrix8(const double (&xl)[8], const double (&yl)[8],
                                          const double (&xr)[8], const double (&yr)[8],
-                                         double (&F)[9], int diag = 0) {
+                                         double (&F)[9]) {
   double s1, ox1, oy1, s2, ox2, oy2;
   scaling8(xl, yl, s1, ox1, oy1);
   scaling8(xr, yr, s2, ox2, oy2);
@@ -364,21 +327,9 @@ __device__ __forceinline__ void fmatrix8(const double (&xl)[8], const double (&y
     A[k][8] = 1.0;
   }
   double fs[9];
-  // diag: timing diagnostics only (RSAMD_SOLVE_DIAG, wrong models): 2 skips the LQ, 1 the
-  // rank-2 step
-  if (diag & 2) {
-#pragma unroll
-    for (int j = 0; j < 9; ++j) fs[j] = A[0][j] + A[7][j];
-  } else {
-    lq_null_vector<8, 9>(A, fs);  // lab3.py:317-318: V[-1] of svd(A)
-  }
+  lq_null_vector<8, 9>(A, fs);  // lab3.py:317-318: V[-1] of svd(A)
   double F2[9];
-  if (diag & 1) {
-#pragma unroll
-    for (int j = 0; j < 9; ++j) F2[j] = fs[j];
-  } else if ((diag & 8) || !enforce_rank2_adj(fs, F2)) {  // 8: the Jacobi path always
-    enforce_rank2(fs, F2);
-  }
+  if (!enforce_rank2_adj(fs, F2)) enforce_rank2(fs, F2);
   // lab3.py:327: F = S^T (F2 T); S = H(s1, ox1, oy1), T = H(s2, ox2, oy2)
   double M[9];
 #pragma unroll

@@ -38,7 +38,7 @@ struct F8DevResult {
 // One run's solve (k_f8_solve / the solve half of k_f8_tail_solve).
 struct SolveArgs {
   const Pt *pts;
-  int n, H, mode, diag;  // diag: RSAMD_SOLVE_DIAG timing knob (0 in production)
+  int n, H, mode;
   uint64_t seed, hyp_offset;
   const int *tuples;
   double *Fsoa;
@@ -48,9 +48,8 @@ struct SolveArgs {
   float *F32soa; // unit-frame fp32 models (null: fp64 counting)
   Frame frame;
   int *gdone;    // per-group finish counters zeroed (fused c*)
-  float4 *G4;    // per-hypothesis decision constants (k_f8_count32x DEC 3), may be null
+  float4 *G4;    // per-hypothesis decision constants (k_f8_count32q), may be null
   double gT, gDe, gDn;  // their inputs: (t/s)^2 and the fp32 error bounds of e and m
-  int nt;               // non-temporal output stores (RSAMD_NTSTORE)
 };
 
 // One run's selection tail (candidates, reference statistics, replay, S_RANSAC).
@@ -77,32 +76,24 @@ hipError_t launch_f8_solve(const Pt *pts, int n, int H, int mode, uint64_t seed,
                            uint64_t hyp_offset, const int *tuples, double *Fsoa, int64_t ld,
                            int *counts, int *status, hipStream_t s, float *F32soa = nullptr,
                            const Frame *frame = nullptr, int *gdone = nullptr);
-hipError_t launch_pack_points32(const Pt *pts, int n, const Frame &fr, float4 *pts32,
-                                hipStream_t s);
-hipError_t launch_f8_count32p(const float4 *pts32, const Pt *pts, int n, int H,
-                              const float *F32soa, const double *Fsoa, int64_t ld, int waves,
-                              const GuardPk &g, int *counts, hipStream_t s, int variant = 0);
-hipError_t launch_f8_count32(const float4 *pts32, const Pt *pts, int n, int H,
-                             const float *F32soa, const double *Fsoa, int64_t ld, int waves,
-                             const Guard32 &g, int *counts, hipStream_t s, int blk = 8,
-                             bool prefetch = false);
-// Packed-pair fp32 counting; Guard = GuardX (packed decision) or GuardY (plain decision).
-template <class Guard>
-hipError_t launch_f8_count32x(const float4 *pts32, const Pt *pts, int n, int H,
-                              const float *F32soa, const double *Fsoa, int64_t ld, int waves,
-                              const Guard &g, int *counts, hipStream_t s, int blk = 8,
-                              bool prefetch = true, int *gdone = nullptr,
-                              int *status = nullptr, const float4 *G4 = nullptr);
-// Point-pair packed fp32 counting (DEC 3 decisions, bit-identical to launch_f8_count32x<GuardW>);
-// ptsq in the k_pack_points32q layout.
+// Point-pair packed fp32 counting (guard band + float64 re-test: counts bit-identical to
+// launch_f8_count); ptsq in the k_pack_points32q layout.
 hipError_t set_count_timeline(uint64_t *buf);  // RSAMD_TSTAMP diagnostics (null: off)
 hipError_t launch_pack_points32q(const Pt *pts, int n, const Frame &fr, float4 *ptsq,
                                  hipStream_t s);
+struct Count32qShape {
+  int64_t per_wave;  // points of the (group, point) plane per wave (a multiple of 8)
+  int64_t blocks;    // workgroups launched
+  int block_threads; // 64, 128 or 256
+  int prio;          // progress-levelled issue priority (s_setprio) on / off
+};
+int count32q_resident_waves(int device);
+Count32qShape count32q_shape(int n, int H, int waves, int slices_per_wave = 0,
+                            int block_threads = 256, int prio = 0);
 hipError_t launch_f8_count32q(const float4 *ptsq, const Pt *pts, int n, int H,
-                              const float *F32soa, const double *Fsoa, int64_t ld, int waves,
-                              const GuardW &g, int *counts, hipStream_t s, int *gdone,
-                              int *status, const float4 *G4, bool use_asm = true,
-                              int block_threads = 256, bool xcd_remap = false);
+                              const float *F32soa, const double *Fsoa, int64_t ld,
+                              const Count32qShape &sh, const GuardW &g, int *counts,
+                              hipStream_t s, int *gdone, int *status, const float4 *G4);
 hipError_t launch_f8_count(const Pt *pts, int n, int H, const double *Fsoa, int64_t ld,
                            int chunk, double thr2, int *counts, hipStream_t s);
 // Selection tail: c* (k_f8_max, unless the counting kernel fused it), candidates + reference

@@ -14,7 +14,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <type_traits>
 
 #include "device_math.h"
 #include "f8_kernels.h"
@@ -46,49 +45,6 @@ __device__ __forceinline__ T ld_agent(const T *p) {
 }
 __device__ __forceinline__ void wait_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// Per-lane sum of 8 wave masks (0..8) added to cnt: the masks are summed as bit planes by
-// scalar full adders (SALU, wave-uniform), then 5 VALU add the planes' lane bits.
-__device__ __forceinline__ int add_block_count8(int cnt, const unsigned long long (&b)[8]) {
-  const unsigned long long s01 = b[0] ^ b[1], c01 = b[0] & b[1];
-  const unsigned long long s23 = b[2] ^ b[3], c23 = b[2] & b[3];
-  const unsigned long long s45 = b[4] ^ b[5], c45 = b[4] & b[5];
-  const unsigned long long s67 = b[6] ^ b[7], c67 = b[6] & b[7];
-  const unsigned long long q0 = s01 ^ s23, kq = s01 & s23, tq = c01 ^ c23;
-  const unsigned long long q1 = tq ^ kq, q2 = (c01 & c23) | (kq & tq);
-  const unsigned long long r0 = s45 ^ s67, kr = s45 & s67, tr = c45 ^ c67;
-  const unsigned long long r1 = tr ^ kr, r2 = (c45 & c67) | (kr & tr);
-  const unsigned long long o0 = q0 ^ r0, k0 = q0 & r0, t1 = q1 ^ r1;
-  const unsigned long long o1 = t1 ^ k0, k1 = (q1 & r1) | (k0 & t1), t2 = q2 ^ r2;
-  const unsigned long long o2 = t2 ^ k1, o3 = (q2 & r2) | (k1 & t2);
-  int a, c, d, r;
-  unsigned long long co;
-  asm("v_cndmask_b32_e64 %0, 0, 2, %1" : "=v"(a) : "s"(o1));
-  asm("v_cndmask_b32_e64 %0, 0, 4, %1" : "=v"(c) : "s"(o2));
-  asm("v_cndmask_b32_e64 %0, 0, 8, %1" : "=v"(d) : "s"(o3));
-  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(cnt), "v"(a), "v"(c));
-  asm("v_addc_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(cnt), "=s"(co) : "v"(r), "v"(d), "s"(o0));
-  return cnt;
-}
-
-// The solve's outputs (13 MB per 1e5 hypotheses) are read by the next launch, mostly on
-// another XCD: with nt they stream past this XCD's L2 instead of being written back at the
-// end of the launch (RSAMD_NTSTORE).
-template <class T>
-__device__ __forceinline__ void st_out(T *p, T v, bool nt) {
-  if (nt)
-    __builtin_nontemporal_store(v, p);
-  else
-    *p = v;
-}
-__device__ __forceinline__ void st_out(float4 *p, float4 v, bool nt) {
-  typedef float f4 __attribute__((ext_vector_type(4)));
-  const f4 w = {v.x, v.y, v.z, v.w};
-  if (nt)
-    __builtin_nontemporal_store(w, reinterpret_cast<f4 *>(p));
-  else
-    *p = v;
-}
-
 // ----------------------------------------------------------------------------------------
 // One hypothesis h of a run: sample, 8-point F (float64), its unit-frame fp32 copy, and the
 // per-run zeroing the counting kernel and the selection tail rely on.
@@ -111,10 +67,7 @@ __device__ __forceinline__ void solve_one(const SolveArgs &a, int h) {
   }
   if (gdone && (h & 63) == 0) gdone[h >> 6] = 0;  // fused c*: per-group finish counters
   int idx[8];
-  if (a.diag & 4) {  // timing diagnostic: no sampling
-#pragma unroll
-    for (int k = 0; k < 8; ++k) idx[k] = (h * 8 + k * 977) % n;
-  } else if (mode == RSD_SAMPLER_PHILOX) {
+  if (mode == RSD_SAMPLER_PHILOX) {
     floyd_sample<8>(seed, hyp_offset + static_cast<uint64_t>(h), n, idx);
   } else {
 #pragma unroll
@@ -130,9 +83,9 @@ __device__ __forceinline__ void solve_one(const SolveArgs &a, int h) {
     yr[k] = p.y2;
   }
   double F[9];
-  fmatrix8(xl, yl, xr, yr, F, a.diag);
+  fmatrix8(xl, yl, xr, yr, F);
 #pragma unroll
-  for (int k = 0; k < 9; ++k) st_out(&Fsoa[k * ld + h], F[k], a.nt);
+  for (int k = 0; k < 9; ++k) Fsoa[k * ld + h] = F[k];
   if (F32soa) {
     // F~ = T1^T F T2 (T_i = [[s,0,cx_i],[0,s,cy_i],[0,0,1]]), scaled to max |F~_ij| = 1
     double G[9];
@@ -154,9 +107,9 @@ __device__ __forceinline__ void solve_one(const SolveArgs &a, int h) {
     for (int k = 0; k < 9; ++k) mx = fmax(mx, fabs(Ft[k]));
     const double kap = 1.0 / mx;  // F = 0 or non-finite -> NaN model, counts 0 on both paths
 #pragma unroll
-    for (int k = 0; k < 9; ++k) st_out(&F32soa[k * ld + h], static_cast<float>(Ft[k] * kap), a.nt);
+    for (int k = 0; k < 9; ++k) F32soa[k * ld + h] = static_cast<float>(Ft[k] * kap);
     if (a.G4) {
-      // k_f8_count32x DEC 3 constants, AM-GM split point c = t~ sqrt(m at the frame centre)
+      // k_f8_count32q decision constants, AM-GM split point c = t~ sqrt(m at the frame centre)
       // (any c > 0 is rigorous; this one keeps the band near the exact-|e| band)
       const double u = 0x1p-24, T = a.gT, De = a.gDe, Dn = a.gDn;
       const double f02 = Ft[2] * kap, f12 = Ft[5] * kap, f20 = Ft[6] * kap, f21 = Ft[7] * kap;
@@ -170,10 +123,8 @@ __device__ __forceinline__ void solve_one(const SolveArgs &a, int h) {
       const double beta = T * (1.0 + u) * rcp_fast(1.0 - u) * im * (1.0 + 4.0 * u);
       const double ki = 1.02 * (De * c + De * De + T * Dn) * ip + 1e-30;
       const double ko = 1.02 * (T * Dn + De * c) * im + 1e-30;
-      st_out(&a.G4[h],
-             make_float4(static_cast<float>(ki), -static_cast<float>(ko),
-                         static_cast<float>(alpha), static_cast<float>(beta)),
-             a.nt);
+      a.G4[h] = make_float4(static_cast<float>(ki), -static_cast<float>(ko),
+                            static_cast<float>(alpha), static_cast<float>(beta));
     }
   }
 }
@@ -226,36 +177,50 @@ __global__ __launch_bounds__(256) void k_f8_count(const Pt *__restrict__ pts, in
 }
 
 // ----------------------------------------------------------------------------------------
-// fp32 counting with a rigorous fp64 guard band.
+// fp32 counting with a rigorous fp64 guard band (k_f8_count32q, the product kernel).
 //
 // In the frame x~ = (x - c_i)/s (|x~| <= R = 1) with F~ = T1^T F T2 / max|.| the test
-// e^2 < t^2 min(n1, n2) becomes e~^2 < (t/s)^2 min(n~1, n~2) exactly (e scales with the
-// model scale, n with its square, both line lengths with s^2).  Each fp32 operation and the
-// fp64->fp32 rounding of F~ and of the points is bounded absolutely (Dl for a line
-// component, De for e, Dn for a squared length; constants from the host, api.hip
-// guard_constants), giving a per-point bound
-//     B = 2 De |e| + De^2 + u (e^2 + 2 rhs) + (t/s)^2 Dn     (x 1.02 slack)
-// on |fl(e^2 - rhs) - (e^2 - rhs)_exact|.  Outside |d| <= B the fp32 sign is the exact one;
-// inside, the lane re-runs the fp64 test of k_f8_count (pixel units) -- bit-identical counts.
-// 26 fp32 VALU ops per (hypothesis, point) instead of 21 fp64 ones.
+// e^2 < t^2 min(n1, n2) becomes e~^2 < T min(n~1, n~2), T = (t/s)^2, exactly (e scales with
+// the model scale, n with its square, both line lengths with s^2).  Each fp32 operation and
+// the fp64 -> fp32 rounding of F~ and of the points is bounded absolutely (f8_plan.hip
+// fp32_bounds: De for e, Dn for a squared length), |e_c - e| <= De, |m_c - m| <= Dn,
+// m = min(n1, n2), u = 2^-24.
+//
+// Decision (per-hypothesis constants, written by the solve into G4): with the AM-GM split
+// 2De|e_c| <= De (e_c^2/c + c) at a per-hypothesis c (c = t~ sqrt(m at the frame centre),
+// r = De/c) both sides are one packed fma of e and one packed multiply of m:
+//   sure inlier  fl(e^2 + ki) < fl(alpha m):  e_c^2 + ki < alpha m_c (1+u)/(1-u), and with
+//     alpha <= T (1-u)/((1+u)(1+r)), ki >= (De c + De^2 + T Dn)/(1+r):
+//     e^2 <= e_c^2 (1+r) + De c + De^2 < T m_c - T Dn <= T m;
+//   sure outlier fl(e^2 - ko) > fl(beta m) (>= 0):  e_c^2 > ko + beta m_c (1-u)/(1+u), and
+//     with beta >= T (1+u)/((1-u)(1-r)), ko >= (T Dn + De c)/(1-r):
+//     e^2 >= e_c^2 (1-r) - De c > T m_c + T Dn >= T m.
+// (ki, -ko, alpha, beta) are one float4 per hypothesis (G4); ambiguous = XOR of the two
+// ballots (fl(e^2 - ko) <= fl(e^2 + ki) and alpha <= beta).  An ambiguous (hypothesis, point)
+// is re-tested in float64 in pixel units (test64, the k_f8_count expression), so the counts
+// are bit-identical to k_f8_count's.  NaN (padding points, NaN models) fails every compare,
+// as the float64 test fails.
+//
+// Point-pair packing.  Every v_pk_fma_f32 carries the SAME quantity of TWO consecutive points
+// (2j and 2j+1 of a block of 8, one aligned SGPR pair per coordinate, k_pack_points32q):
+//   a  = fma(F0, X2, fma(F1, Y2, F2))     b  = fma(F3, X2, fma(F4, Y2, F5))
+//   l3 = fma(F6, X2, fma(F7, Y2, F8))     e  = fma(a, X1, fma(b, Y1, l3))
+//   c  = fma(F0, X1, fma(F3, Y1, F6))     d  = fma(F1, X1, fma(F4, Y1, F7))
+//   n1 = fma(a, a, b*b)   n2 = fma(c, c, d*d)   m = min(n1, n2) (two v_min)
+//   P  = fma(e, e, ki)    Q  = fma(e, e, -ko)   R = alpha m   S = beta m
+// Per point pair: 12 pk (a, b, l3, e, c, d) + 4 pk (n1, n2) + 2 min + 4 pk (P, Q, R, S) +
+// 4 cmp + 2 add = 28 VALU, 14 per (64 hypotheses x point).  The splat coefficients are op_sel
+// broadcasts inside one asm block per pair (pair_terms); the float64 re-test of an ambiguous
+// pair runs right there.
+//
+// Work distribution.  The (group of 64 hypotheses) x (point) plane, flattened group-major, is
+// cut into W equal contiguous slices (a multiple of 8 points), one per wave; a slice that
+// crosses a group boundary runs as two segments, each with its own model load and one
+// coalesced count atomic.  W is a multiple of the resident wave count (6 per SIMD), so every
+// wave slot runs the same number of slices.  Measured and not kept: claiming chunks from
+// per-XCD atomic head words (0.13-0.19 ms per C2 launch instead of ~0.1: a returning
+// device-scope atomic per chunk queues behind thousands of pullers).
 // ----------------------------------------------------------------------------------------
-// One point of the fp32 test: returns d = e^2 - t~^2 m and its error bound B.
-__device__ __forceinline__ void test32(const float (&f)[9], const float4 &p, const Guard32 &g,
-                                       float &d, float &B) {
-  const float x2 = p.x, x1 = p.y, y2 = p.z, y1 = p.w;  // k_pack_points32 layout
-  const float l10 = fmaf(f[0], x2, fmaf(f[1], y2, f[2]));
-  const float l11 = fmaf(f[3], x2, fmaf(f[4], y2, f[5]));
-  const float l12 = fmaf(f[6], x2, fmaf(f[7], y2, f[8]));
-  const float l20 = fmaf(f[0], x1, fmaf(f[3], y1, f[6]));
-  const float l21 = fmaf(f[1], x1, fmaf(f[4], y1, f[7]));
-  const float e = fmaf(l10, x1, fmaf(l11, y1, l12));
-  const float n1 = fmaf(l10, l10, l11 * l11);
-  const float n2 = fmaf(l20, l20, l21 * l21);
-  const float ee = e * e;
-  const float rhs = g.thr2 * fminf(n1, n2);
-  d = ee - rhs;
-  B = fmaf(fabsf(e), g.K1, fmaf(fmaf(rhs, 2.0f, ee), g.Ku, g.K0));
-}
 
 // The float64 test of k_f8_count (pixel units) for one (hypothesis, point).
 __device__ __forceinline__ bool test64(const double (&fd)[9], const Pt &q, double thr2) {
@@ -270,86 +235,9 @@ __device__ __forceinline__ bool test64(const double (&fd)[9], const Pt &q, doubl
   return ed * ed < thr2 * fmin(m1, m2);
 }
 
-// Work partition: the (group of 64 hypotheses) x (point) plane, flattened group-major, is cut
-// into W equal contiguous slices, one per wave, W = the number of waves the chip holds at
-// once (all resident, no tail round).  A slice covers the end of one group and the start of
-// the next (two segments, each with its own model load and one coalesced atomic).
-//
-// Points are processed in blocks of 4 (one s_load_dwordx16; the point arrays are padded with
-// NaN points, which are neither inliers nor ambiguous).  The main path counts only sure
-// inliers, d < -B; each point's ambiguity ballot |d| <= B stays in SGPRs and, once per block,
-// the flagged (lane, point) pairs are re-tested in float64.
-template <int BLK, bool PREFETCH>
-__global__ __launch_bounds__(256) void k_f8_count32(const float4 *__restrict__ pts32,
-                                                    const Pt *__restrict__ pts, int n, int H,
-                                                    const float *__restrict__ F32soa,
-                                                    const double *__restrict__ Fsoa, int64_t ld,
-                                                    int64_t per_wave, Guard32 g,
-                                                    int *__restrict__ counts) {
-  const int lane = threadIdx.x & 63;
-  const int64_t w = wave_uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
-  const int64_t npad = (n + BLK - 1) / BLK * BLK;
-  const int64_t total = static_cast<int64_t>((H + 63) >> 6) * npad;
-  int64_t pos = w * per_wave;
-  const int64_t end = min(total, pos + per_wave);
-  while (pos < end) {
-    const int grp = static_cast<int>(pos / npad);
-    const int p0 = static_cast<int>(pos - grp * npad);
-    const int p1 = static_cast<int>(min(npad, p0 + (end - pos)));
-    pos += p1 - p0;
-    const int h = grp * 64 + lane;
-    const int hl = h < H ? h : H - 1;
-    float f[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) f[k] = F32soa[k * ld + hl];
-    int cnt = 0;
-    float4 cur[BLK];
-    if (PREFETCH) {
-#pragma unroll
-      for (int k = 0; k < BLK; ++k) cur[k] = pts32[p0 + k];
-    }
-    for (int i = p0; i < p1; i += BLK) {
-      // optional software pipelining of the scalar loads (prefetch the next block)
-      float4 nxt[BLK];
-      if (PREFETCH) {
-        const int j = (i + BLK < p1) ? i + BLK : i;
-#pragma unroll
-        for (int k = 0; k < BLK; ++k) nxt[k] = pts32[j + k];
-      } else {
-#pragma unroll
-        for (int k = 0; k < BLK; ++k) cur[k] = pts32[i + k];
-      }
-      unsigned long long amb[BLK];
-#pragma unroll
-      for (int k = 0; k < BLK; ++k) {
-        float d, B;
-        test32(f, cur[k], g, d, B);
-        cnt += (d < -B) ? 1 : 0;  // sure inlier
-        amb[k] = __ballot(fabsf(d) <= B);
-      }
-      unsigned long long any = 0ull;
-#pragma unroll
-      for (int k = 0; k < BLK; ++k) any |= amb[k];
-      if (any != 0ull) {
-        double fd[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) fd[k] = Fsoa[k * ld + hl];
-#pragma unroll
-        for (int k = 0; k < BLK; ++k)
-          if ((amb[k] >> lane) & 1ull) cnt += test64(fd, pts[i + k], g.thr2_px) ? 1 : 0;
-      }
-      if (PREFETCH) {
-#pragma unroll
-        for (int k = 0; k < BLK; ++k) cur[k] = nxt[k];
-      }
-    }
-    if (h < H) atomicAdd(&counts[h], cnt);
-  }
-}
-
-// Last-finisher reduction of one hypothesis group (64 lanes): the wave whose segment brings
+// Last-finisher reduction of one hypothesis group (64 lanes): the wave whose chunk brings
 // gdone[grp] to npad reads the group's final counts and folds their max into status[0].  Every
-// segment's count atomics complete (vmcnt) before its gdone atomic, and the reader's atomic
+// chunk's count atomics complete (vmcnt) before its gdone atomic, and the reader's atomic
 // loads issue after its gdone atomic returned, so they see all of them.
 __device__ __forceinline__ void group_done_max(int *counts, int *gdone, int *status, int grp,
                                                int len, int npad, int h, int H) {
@@ -364,267 +252,15 @@ __device__ __forceinline__ void group_done_max(int *counts, int *gdone, int *sta
   if ((threadIdx.x & 63) == 0 && v > 0) atomicMax(&status[0], v);
 }
 
-// ----------------------------------------------------------------------------------------
-// Packed-pair variant (default).  On gfx950 a wave64 v_fma_f32 issues at the float64 rate
-// and only v_pk_fma_f32 doubles fp32 throughput, so the two epipolar lines of ONE hypothesis
-// travel as pairs:  A = (l10, l20),  Bv = (l11, l21),  N = A*A + Bv*Bv = (n1, n2),
-//   A  = pk_fma((f0, f0), (x2, x1), pk_fma((f1, f3), (y2, y1), (f2, f6)))
-//   Bv = pk_fma((f3, f1), (x2, x1), pk_fma((f4, f4), (y2, y1), (f5, f7)))
-// with the point pairs (x2, x1), (y2, y1) straight from SGPRs (k_pack_points32 layout).  Every
-// value is the same IEEE expression as in test32, so De and Dn hold unchanged.
-//
-// The decision folds the guard band into the two compared sides.  With T = (t/s)^2,
-// |e_c - e| <= De, |m_c - m| <= Dn (m = min(n1, n2)) and u = 2^-24:
-//   sure inlier   P = fl(fl(|e_c| + K1i)|e_c| + K0i) < fl(alpha m_c)
-//     P >= (1-u)^2 (e_c^2 + K1i|e_c| + K0i) and fl(alpha m_c) <= alpha m_c (1+u); with
-//     K1i >= 2De, K0i >= De^2 + T Dn, alpha <= T (1-u)^2/(1+u) this gives
-//     e^2 <= e_c^2 + 2De|e_c| + De^2 < T m_c - T Dn <= T m    (exact inlier);
-//   sure outlier  Q = fl(fl(|e_c| - K1o)|e_c| - K0o) > fl(beta m_c)  (>= 0, so |e_c| > K1o)
-//     Q <= (1+u)^2 (e_c^2 - K1o|e_c|) - (1+u) K0o; with K1o >= 2De, K0o >= (1+u) T Dn,
-//     beta >= T (1+u)^2/(1-u) this gives e^2 >= e_c^2 - 2De|e_c| > T m_c + T Dn >= T m.
-// Neither side -> the lane re-tests in float64 (test64).  NaN (padding points, NaN models)
-// fails both compares and the ambiguity compare (Q <= beta m), as the float64 test fails.
-// Per (hypothesis, point): 6 pk + 1 pk-mul + 2 pk (P, Q) + 4 fma (l12, e) + min + abs
-// + 2 cmp + 1 add = 18 VALU instead of test32's 26.
-// ----------------------------------------------------------------------------------------
-//
-// Variant DEC = 1 keeps the packed lines and decides with plain ops (GuardY):
-//   R = fl(alpha m), G = fl(e^2 - R) (one fma), h = fl(K1|e| + K0), h2 = fl(delta m + h)
-//   sure inlier  G < -h:  e_c^2 - R <= G/(1+u) < -c1 (K1|e_c| + K0), c1 = (1-u)/(1+u), so
-//     with c1 K1 >= 2De, c1 K0 >= De^2 + T Dn, alpha (1+u) <= T: e^2 < T m_c - T Dn <= T m;
-//   sure outlier G > h2 (>= 0):  e_c^2 > R + c1 (delta m_c + (1-u)(K1|e_c| + K0)); with
-//     alpha (1-u) + c1 delta >= T and c1 (1-u) K1 >= 2De, c1 (1-u) K0 >= T Dn this gives
-//     e^2 >= e_c^2 - 2De|e_c| > T m_c + T Dn >= T m.
-//   Ambiguous = (G <= h2) XOR (G < -h)  (h2 >= 0 > -h, NaN fails both).
-// 6 pk + 4 fma + min + 4 (R, G, h, h2) + 2 cmp + 1 add = 18 VALU, 6 of them packed.
-//
-// Variant DEC = 2 folds delta m into K0: |F~_ij| <= 1 and |x~| <= 1 bound every line
-// component by 3 and m_c by M = 18 (1 + 1e-5), so (T - alpha (1-u)) m_c <= D0 =
-// (T - alpha (1-u)) M and one h serves both sides (K0 >= (De^2 + T Dn + D0)/c1):
-//   sure inlier  G < -h,   ambiguous |G| <= h  (disjoint; NaN fails both),
-// and the per-point inlier add becomes a SALU bit-plane sum per block (add_block_count8):
-// 6 pk + 4 fma + min + 3 (R, G, h) + 2 cmp + 5/8 = 16.6 VALU.
-//
-// c* is fused in (gdone != nullptr): every segment adds its length to its group's counter
-// gdone[grp] after its count atomics; the segment that completes the group (total npad)
-// reads the 64 final counts and issues one atomicMax(status[0]) -- no k_f8_max pass.
-//
-// Variant DEC = 3 (default) bounds 2De|e_c| <= De (e_c^2/c + c) (AM-GM, any c > 0) with a
-// per-hypothesis c (k_f8_solve: c = t~ sqrt(m at the frame centre), r = De/c), so both sides
-// are one packed fma of the broadcast e and one packed multiply of the broadcast m:
-//   sure inlier  fl(e^2 + ki) < fl(alpha m):  e_c^2 + ki < alpha m_c (1+u)/(1-u), and with
-//     alpha <= T (1-u)/((1+u)(1+r)), ki >= (De c + De^2 + T Dn)/(1+r):
-//     e^2 <= e_c^2 (1+r) + De c + De^2 < T m_c - T Dn <= T m;
-//   sure outlier fl(e^2 - ko) > fl(beta m) (>= 0):  e_c^2 > ko + beta m_c (1-u)/(1+u), and
-//     with beta >= T (1+u)/((1-u)(1-r)), ko >= (T Dn + De c)/(1-r):
-//     e^2 >= e_c^2 (1-r) - De c > T m_c + T Dn >= T m.
-// (ki, -ko, alpha, beta) are one float4 per hypothesis (G4); ambiguous = XOR of the ballots
-// (fl(e^2 - ko) <= fl(e^2 + ki) and alpha <= beta).  6 pk + 4 fma + min + 2 pk + 2 cmp + 1 add
-// = 16 VALU.
-template <int BLK, bool PREFETCH, int DEC, class Guard>
-__global__ __launch_bounds__(256) void k_f8_count32x(const float4 *__restrict__ pts32,
-                                                     const Pt *__restrict__ pts, int n, int H,
-                                                     const float *__restrict__ F32soa,
-                                                     const double *__restrict__ Fsoa,
-                                                     int64_t ld, int64_t per_wave, Guard g,
-                                                     int *__restrict__ counts,
-                                                     int *__restrict__ gdone,
-                                                     int *__restrict__ status,
-                                                     const float4 *__restrict__ G4) {
-#pragma clang fp contract(off)
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  const int lane = threadIdx.x & 63;
-  const int64_t w = wave_uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
-  const int64_t npad = (n + BLK - 1) / BLK * BLK;
-  const int64_t total = static_cast<int64_t>((H + 63) >> 6) * npad;
-  int64_t pos = w * per_wave;
-  const int64_t end = min(total, pos + per_wave);
-  f2 k1 = {0.f, 0.f}, k0 = {0.f, 0.f}, ab = {0.f, 0.f};
-  if constexpr (DEC == 0) {
-    k1 = f2{g.K1i, g.K1o_neg};
-    k0 = f2{g.K0i, g.K0o_neg};
-    ab = f2{g.alpha, g.beta};
-  }
-  while (pos < end) {
-    const int grp = static_cast<int>(pos / npad);
-    const int p0 = static_cast<int>(pos - grp * npad);
-    const int p1 = static_cast<int>(min(npad, p0 + (end - pos)));
-    pos += p1 - p0;
-    const int h = grp * 64 + lane;
-    const int hl = h < H ? h : H - 1;
-    float f[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) f[k] = F32soa[k * ld + hl];
-    const f2 fa = {f[0], f[0]}, fb = {f[1], f[3]}, fc = {f[2], f[6]};
-    const f2 fd = {f[3], f[1]}, fe = {f[4], f[4]}, ff = {f[5], f[7]};
-    f2 kw = {0.f, 0.f}, abw = {0.f, 0.f};
-    if constexpr (DEC == 3) {
-      const float4 q = G4[hl];
-      kw = f2{q.x, q.y};
-      abw = f2{q.z, q.w};
-    }
-    // one block of BLK points starting at i: fast fp32 decisions, then the float64 re-test of
-    // the ambiguous (lane, point) pairs
-    auto block = [&](const float4 (&cur)[BLK], int i, int cnt) -> int {
-      unsigned long long amb[BLK], inl[BLK];
-#pragma unroll
-      for (int k = 0; k < BLK; ++k) {
-        const f2 X = {cur[k].x, cur[k].y}, Y = {cur[k].z, cur[k].w};  // (x2, x1), (y2, y1)
-        const f2 A = __builtin_elementwise_fma(fa, X, __builtin_elementwise_fma(fb, Y, fc));
-        const f2 Bv = __builtin_elementwise_fma(fd, X, __builtin_elementwise_fma(fe, Y, ff));
-        const f2 N = __builtin_elementwise_fma(A, A, Bv * Bv);
-        const float l12 = fmaf(f[6], cur[k].x, fmaf(f[7], cur[k].z, f[8]));
-        const float e = fmaf(A.x, cur[k].y, fmaf(Bv.x, cur[k].w, l12));
-        const float m = fminf(N.x, N.y);
-        unsigned long long bi, bl;
-        if constexpr (DEC == 0) {
-          const float ae = fabsf(e);
-          const f2 AE = {ae, ae};
-          const f2 PQ = __builtin_elementwise_fma(AE + k1, AE, k0);
-          const f2 RS = f2{m, m} * ab;
-          // P >= Q and alpha m <= beta m survive rounding (monotone), so a sure inlier
-          // always has Q <= beta m: the ambiguous lanes are the XOR of the two ballots.
-          bi = __ballot(PQ.x < RS.x);
-          bl = __ballot(PQ.y <= RS.y);
-        } else if constexpr (DEC == 1) {
-          const float R = g.alpha * m;
-          const float G = fmaf(e, e, -R);
-          const float h = fmaf(fabsf(e), g.K1, g.K0);
-          const float h2 = fmaf(g.delta, m, h);
-          bi = __ballot(G < -h);
-          bl = __ballot(G <= h2);
-        } else if constexpr (DEC == 2) {
-          const float R = g.alpha * m;
-          const float G = fmaf(e, e, -R);
-          const float h = fmaf(fabsf(e), g.K1, g.K0);
-          bi = __ballot(G < -h);
-          bl = __ballot(fabsf(G) <= h);
-        } else {
-          const f2 PQ = __builtin_elementwise_fma(f2{e, e}, f2{e, e}, kw);
-          const f2 RS = f2{m, m} * abw;
-          bi = __ballot(PQ.x < RS.x);
-          bl = __ballot(PQ.y <= RS.y);
-        }
-        if constexpr (DEC == 2) {
-          amb[k] = bl;
-          inl[k] = bi;
-        } else {
-          amb[k] = bi ^ bl;
-          cnt = add_lane_bit(cnt, bi);  // sure inlier
-        }
-      }
-      if constexpr (DEC == 2) {
-        if constexpr (BLK == 8) {
-          cnt = add_block_count8(cnt, inl);
-        } else {
-#pragma unroll
-          for (int k = 0; k < BLK; ++k) cnt = add_lane_bit(cnt, inl[k]);
-        }
-      }
-      unsigned long long any = 0ull;
-#pragma unroll
-      for (int k = 0; k < BLK; ++k) any |= amb[k];
-      if (g.thr2_px < 0.0) any = 0ull;  // diagnostic only (RSAMD_NORECHECK): counts wrong
-      if (any != 0ull) {
-        double fdd[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) fdd[k] = Fsoa[k * ld + hl];
-#pragma unroll
-        for (int k = 0; k < BLK; ++k)
-          if ((amb[k] >> lane) & 1ull) cnt += test64(fdd, pts[i + k], g.thr2_px) ? 1 : 0;
-      }
-      return cnt;
-    };
-    int cnt = 0;
-    float4 ba[BLK], bb[BLK];
-#pragma unroll
-    for (int k = 0; k < BLK; ++k) ba[k] = pts32[p0 + k];
-    if (PREFETCH) {
-      // ping-pong: the next block's scalar loads land in the other buffer while this one is
-      // tested (no register rotation; the last prefetch re-reads the current block)
-      for (int i = p0;;) {
-        const int ja = (i + BLK < p1) ? i + BLK : i;
-#pragma unroll
-        for (int k = 0; k < BLK; ++k) bb[k] = pts32[ja + k];
-        cnt = block(ba, i, cnt);
-        i += BLK;
-        if (i >= p1) break;
-        const int jb = (i + BLK < p1) ? i + BLK : i;
-#pragma unroll
-        for (int k = 0; k < BLK; ++k) ba[k] = pts32[jb + k];
-        cnt = block(bb, i, cnt);
-        i += BLK;
-        if (i >= p1) break;
-      }
-    } else {
-      for (int i = p0; i < p1; i += BLK) {
-#pragma unroll
-        for (int k = 0; k < BLK; ++k) ba[k] = pts32[i + k];
-        cnt = block(ba, i, cnt);
-      }
-    }
-    if (h < H) atomicAdd(&counts[h], cnt);
-    if (gdone) group_done_max(counts, gdone, status, grp, p1 - p0, static_cast<int>(npad), h, H);
-  }
-}
-
-// ----------------------------------------------------------------------------------------
-// Point-pair variant ("q").  k_f8_count32x packs the two epipolar lines of ONE point, so the
-// four scalar FMAs of l12 and e cannot pair up.  Here every packed op carries the SAME
-// quantity of TWO consecutive points instead (points 2j and 2j+1 of a block, one aligned
-// SGPR pair per coordinate, k_pack_points32q layout):
-//   a  = fma(F0, X2, fma(F1, Y2, F2))     b  = fma(F3, X2, fma(F4, Y2, F5))
-//   l3 = fma(F6, X2, fma(F7, Y2, F8))     e  = fma(a, X1, fma(b, Y1, l3))
-//   c  = fma(F0, X1, fma(F3, Y1, F6))     d  = fma(F1, X1, fma(F4, Y1, F7))
-//   n1 = fma(a, a, b*b)   n2 = fma(c, c, d*d)   m = min(n1, n2) (two v_min)
-//   P  = fma(e, e, ki)    Q  = fma(e, e, -ko)   R = alpha m   S = beta m
-// Each lane value is the same IEEE expression, in the same order, as k_f8_count32x DEC 3
-// (A.x = a, A.y = c, Bv.x = b, Bv.y = d, N = (n1, n2), l12 = l3), so the DEC 3 guard band
-// and its per-hypothesis constants hold unchanged and the decisions are bit-identical.
-// Per point pair: 12 pk (a, b, l3, e, c, d) + 4 pk (n1, n2) + 2 min + 4 pk (P, Q, R, S) +
-// 4 cmp + 2 add = 28 VALU, 14 per (64 hypotheses x point) against DEC 3's 16.  The splat
-// coefficients are op_sel broadcasts inside one asm block per pair (pair_terms), and the
-// float64 re-test of an ambiguous pair runs right there, so the pair loop holds 54 VGPRs.
-// ----------------------------------------------------------------------------------------
 typedef float f2q __attribute__((ext_vector_type(2)));
-// v_pk_fma_f32 with a broadcast half of a VGPR pair as src0 (and optionally src2) and an
-// SGPR point pair as src1.  OPSEL / OPSELHI pick, per result lane, the half of each source.
-#define RSD_PKFMA_BSV(d, a, b, c, OPSEL, OPSELHI)                                        \
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:" OPSEL " op_sel_hi:" OPSELHI                  \
-      : "=v"(d) : "v"(a), "s"(b), "v"(c))
-#define RSD_PKFMA_VVB(d, a, b, c, OPSEL, OPSELHI)                                        \
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:" OPSEL " op_sel_hi:" OPSELHI                  \
-      : "=v"(d) : "v"(a), "v"(b), "v"(c))
+// v_pk_mul_f32 with a broadcast half of a VGPR pair (OPSEL / OPSELHI pick, per result lane,
+// the half of each source).
 #define RSD_PKMUL_VB(d, a, b, OPSEL, OPSELHI)                                             \
   asm("v_pk_mul_f32 %0, %1, %2 op_sel:" OPSEL " op_sel_hi:" OPSELHI : "=v"(d) : "v"(a), "v"(b))
 
-// The k_f8_count32q terms of one point pair (expressions and order as documented above the
-// kernel); P01 = (F0, F1), P23 = (F2, F3), P45 = (F4, F5), P67 = (F6, F7), P8 = (F8, F8),
-// KIO = (ki, -ko), ALB = (alpha, beta).
-// Plain-builtin form of the same terms (the compiler splats the coefficients into VGPR
-// pairs: 66 VGPRs; it can interleave the pairs freely).  Selected by RSAMD_QASM=0.
-__device__ __forceinline__ void pair_terms_builtin(f2q P01, f2q P23, f2q P45, f2q P67, f2q P8, f2q KIO,
-                                           f2q ALB, f2q X2, f2q Y2, f2q X1, f2q Y1, f2q &P,
-                                           f2q &Q, f2q &R, f2q &S) {
-#pragma clang fp contract(off)
-  const f2q F0 = {P01.x, P01.x}, F1 = {P01.y, P01.y}, F2 = {P23.x, P23.x}, F3 = {P23.y, P23.y};
-  const f2q F4 = {P45.x, P45.x}, F5 = {P45.y, P45.y}, F6 = {P67.x, P67.x}, F7 = {P67.y, P67.y};
-  const f2q a = __builtin_elementwise_fma(F0, X2, __builtin_elementwise_fma(F1, Y2, F2));
-  const f2q b = __builtin_elementwise_fma(F3, X2, __builtin_elementwise_fma(F4, Y2, F5));
-  const f2q l3 = __builtin_elementwise_fma(F6, X2, __builtin_elementwise_fma(F7, Y2, P8));
-  const f2q e = __builtin_elementwise_fma(a, X1, __builtin_elementwise_fma(b, Y1, l3));
-  const f2q c = __builtin_elementwise_fma(F0, X1, __builtin_elementwise_fma(F3, Y1, F6));
-  const f2q d = __builtin_elementwise_fma(F1, X1, __builtin_elementwise_fma(F4, Y1, F7));
-  const f2q n1 = __builtin_elementwise_fma(a, a, b * b);
-  const f2q n2 = __builtin_elementwise_fma(c, c, d * d);
-  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
-  const f2q m = __builtin_bit_cast(
-      f2q, __builtin_elementwise_min(__builtin_bit_cast(u2, n1), __builtin_bit_cast(u2, n2)));
-  P = __builtin_elementwise_fma(e, e, f2q{KIO.x, KIO.x});
-  Q = __builtin_elementwise_fma(e, e, f2q{KIO.y, KIO.y});
-  R = m * f2q{ALB.x, ALB.x};
-  S = m * f2q{ALB.y, ALB.y};
-}
+// The terms of one point pair (expressions and order as documented above); P01 = (F0, F1),
+// P23 = (F2, F3), P45 = (F4, F5), P67 = (F6, F7), P8 = (F8, F8), KIO = (ki, -ko),
+// ALB = (alpha, beta).
 __device__ __forceinline__ void pair_terms(f2q P01, f2q P23, f2q P45, f2q P67, f2q P8, f2q KIO,
                                            f2q ALB, f2q X2, f2q Y2, f2q X1, f2q Y1, f2q &P,
                                            f2q &Q, f2q &R, f2q &S) {
@@ -668,53 +304,65 @@ __device__ __forceinline__ void pair_terms(f2q P01, f2q P23, f2q P45, f2q P67, f
   RSD_PKMUL_VB(S, m, ALB, "[0,1]", "[1,1]");  // beta m
 }
 
-// Wave timeline of the "q" counting kernel (start / end of each wave, 100 MHz real-time
-// counter): set by the plan only under RSAMD_TSTAMP, for the launch-overhead analysis.
+// Wave timeline of the counting kernel (start / end of each wave, 100 MHz real-time counter):
+// set by the plan only under RSAMD_TSTAMP, for the launch-shape analysis.
 __device__ uint64_t *g_count_ts = nullptr;
 
-template <bool ASM, int BT>
+template <int BT>
 __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ ptsq,
                                                      const Pt *__restrict__ pts, int n, int H,
                                                      const float *__restrict__ F32soa,
                                                      const double *__restrict__ Fsoa,
-                                                     int64_t ld, int64_t per_wave, GuardW g,
+                                                     int64_t ld, int64_t per_wave, int prio,
+                                                     GuardW g,
                                                      int *__restrict__ counts,
                                                      int *__restrict__ gdone,
                                                      int *__restrict__ status,
-                                                     const float4 *__restrict__ G4,
-                                                     int xcd_rows) {
+                                                     const float4 *__restrict__ G4) {
 #pragma clang fp contract(off)
   typedef float f2 __attribute__((ext_vector_type(2)));
   const int lane = threadIdx.x & 63;
-  // xcd_rows > 0: consecutive workgroups go round-robin to the 8 XCDs, so block b takes slice
-  // block (b % 8) * xcd_rows + b / 8 and the slices of one hypothesis group (which re-read
-  // its models) stay on one XCD's L2; the grid is a multiple of 8 blocks then
-  const int b = xcd_rows > 0 ? (blockIdx.x & 7) * xcd_rows + (blockIdx.x >> 3) : blockIdx.x;
-  const int64_t w = wave_uniform(b * (BT / 64) + (threadIdx.x >> 6));
-  const int64_t npad = (n + 7) / 8 * 8;
+  const int64_t w = wave_uniform(blockIdx.x * (BT / 64) + (threadIdx.x >> 6));
+  const int npad = (n + 7) / 8 * 8;
   const int64_t total = static_cast<int64_t>((H + 63) >> 6) * npad;
   int64_t pos = w * per_wave;
   const int64_t end = min(total, pos + per_wave);
   uint64_t *ts = g_count_ts;  // diagnostic wave timeline (RSAMD_TSTAMP), null in production
   const uint64_t t_start = ts ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  int n_retest = 0;  // re-test branches taken (timeline diagnostics)
+  // progress-levelled issue priority: the arbiter serves the highest priority, then the
+  // oldest wave, so waves of equal work otherwise finish up to 2.5x apart; a wave that is
+  // ahead steps its priority down at 1/4, 1/2 and 3/4 of its slice
+  const int64_t wbeg = pos;
+  int64_t next_step = prio ? wbeg + (end - wbeg) / 4 : INT64_MAX;
+  int level = 3;
+  if (prio) __builtin_amdgcn_s_setprio(3);
   while (pos < end) {
     const int grp = static_cast<int>(pos / npad);
-    const int p0 = static_cast<int>(pos - grp * npad);
-    const int p1 = static_cast<int>(min(npad, p0 + (end - pos)));
+    const int p0 = static_cast<int>(pos - static_cast<int64_t>(grp) * npad);
+    const int p1 = static_cast<int>(min(static_cast<int64_t>(npad), p0 + (end - pos)));
     pos += p1 - p0;
     const int h = grp * 64 + lane;
     const int hl = h < H ? h : H - 1;
     float f[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) f[k] = F32soa[k * ld + hl];
-    // coefficient pairs; broadcasts of one half are op_sel operands (pkfma_* below), so no
-    // duplicated VGPRs (the compiler's splats cost 12 more and a wave of occupancy)
+    // coefficient pairs; broadcasts of one half are op_sel operands (pair_terms), so no
+    // duplicated VGPRs
     const f2 P01 = {f[0], f[1]}, P23 = {f[2], f[3]}, P45 = {f[4], f[5]}, P67 = {f[6], f[7]};
     const f2 P8 = {f[8], f[8]};
     const float4 q = G4[hl];
     const f2 KIO = {q.x, q.y}, ALB = {q.z, q.w};
     int cnt = 0;
+    const int64_t seg0 = pos - (p1 - p0) - p0;  // plane position of point 0 of this group
     for (int i = p0; i < p1; i += 8) {
+      if (seg0 + i >= next_step) {
+        --level;
+        if (level == 2) __builtin_amdgcn_s_setprio(2);
+        else if (level == 1) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+        next_step = level > 0 ? wbeg + (end - wbeg) * (4 - level) / 4 : INT64_MAX;
+      }
       float4 blk[8];  // (x2[8], y2[8], x1[8], y1[8]) of points i..i+7
 #pragma unroll
       for (int k = 0; k < 8; ++k) blk[k] = ptsq[i + k];
@@ -724,16 +372,14 @@ __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ p
         const f2 X2 = {v[2 * j], v[2 * j + 1]}, Y2 = {v[8 + 2 * j], v[9 + 2 * j]};
         const f2 X1 = {v[16 + 2 * j], v[17 + 2 * j]}, Y1 = {v[24 + 2 * j], v[25 + 2 * j]};
         f2 P, Q, R, S;
-        if constexpr (ASM)
-          pair_terms(P01, P23, P45, P67, P8, KIO, ALB, X2, Y2, X1, Y1, P, Q, R, S);
-        else
-          pair_terms_builtin(P01, P23, P45, P67, P8, KIO, ALB, X2, Y2, X1, Y1, P, Q, R, S);
+        pair_terms(P01, P23, P45, P67, P8, KIO, ALB, X2, Y2, X1, Y1, P, Q, R, S);
         const unsigned long long i0 = __ballot(P.x < R.x), i1 = __ballot(P.y < R.y);
         const unsigned long long l0 = __ballot(Q.x <= S.x), l1 = __ballot(Q.y <= S.y);
         cnt = add_lane_bit(cnt, i0);  // sure inliers
         cnt = add_lane_bit(cnt, i1);
         const unsigned long long a0 = i0 ^ l0, a1 = i1 ^ l1;
-        if ((a0 | a1) != 0ull) {  // rare (~1 pair in 40): float64 re-test of the ambiguous lanes
+        if ((a0 | a1) != 0ull) {  // rare: float64 re-test of the ambiguous lanes
+          ++n_retest;
           // the opaque pointer keeps these loads (and their 18 VGPRs) inside the rare branch
           const double *fp = Fsoa + hl;
           asm volatile("" : "+v"(fp));
@@ -746,16 +392,20 @@ __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ p
       }
     }
     if (h < H) atomicAdd(&counts[h], cnt);
-    if (gdone) group_done_max(counts, gdone, status, grp, p1 - p0, static_cast<int>(npad), h, H);
+    if (gdone) group_done_max(counts, gdone, status, grp, p1 - p0, npad, h, H);
   }
   if (ts && lane == 0) {
-    ts[2 * w] = t_start;
-    ts[2 * w + 1] = __builtin_amdgcn_s_memrealtime();
+    ts[4 * w] = t_start;
+    ts[4 * w + 1] = __builtin_amdgcn_s_memrealtime();
+    ts[4 * w + 2] = static_cast<uint64_t>(n_retest);
+    // where it ran: HW_ID (wave, SIMD, CU, SE fields) and XCC_ID
+    ts[4 * w + 3] = (static_cast<uint64_t>(__builtin_amdgcn_s_getreg((31 << 11) | 4)) << 8) |
+                    static_cast<uint64_t>(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7);
   }
 }
 
 // Point-pair layout of k_f8_count32q: block b of 8 points is 32 floats
-// (x2[8], y2[8], x1[8], y1[8]) in the same unit frame as k_pack_points32; NaN padding.
+// (x2[8], y2[8], x1[8], y1[8]) in the unit frame; NaN padding.
 __global__ __launch_bounds__(256) void k_pack_points32q(const Pt *__restrict__ pts, int n,
                                                         Frame fr, float *__restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -772,108 +422,6 @@ __global__ __launch_bounds__(256) void k_pack_points32q(const Pt *__restrict__ p
   o[8] = static_cast<float>((p.y2 - fr.cy2) * is);
   o[16] = static_cast<float>((p.x1 - fr.cx1) * is);
   o[24] = static_cast<float>((p.y1 - fr.cy1) * is);
-}
-
-// ----------------------------------------------------------------------------------------
-// Packed variant: on gfx950 a wave64 v_fma_f32 issues at the float64 rate (4 cycles); only
-// v_pk_fma_f32 doubles fp32 throughput (tools/ubench/valu_rate.hip: 77 vs 154 TFLOP/s).  So
-// each lane carries TWO hypotheses (g*128 + lane and g*128 + 64 + lane) as a float2 and every
-// FMA is packed; the wave-uniform point coordinate is an SGPR broadcast to both halves
-// (op_sel_hi).  The |e| term of the bound uses 2|e| <= e^2/c + c (c = t~, any c > 0 is
-// rigorous) because packed FMAs take no abs modifier:
-//     B = Ka e^2 + Kb rhs + K0,  Ka = 1.02 (De/c (1+2u) + u), Kb = 1.02 (2u),
-//                                K0 = 1.02 (De c + De^2 + t~^2 Dn).
-// 29 VALU per lane and point for two hypotheses (14.5 per hypothesis-point).
-// ----------------------------------------------------------------------------------------
-typedef float f2v __attribute__((ext_vector_type(2)));
-
-template <int BLK, int MINW>
-__global__ __launch_bounds__(256, MINW) void k_f8_count32p(const float4 *__restrict__ pts32,
-                                                     const Pt *__restrict__ pts, int n, int H,
-                                                     const float *__restrict__ F32soa,
-                                                     const double *__restrict__ Fsoa,
-                                                     int64_t ld, int64_t per_wave,
-                                                     GuardPk g, int *__restrict__ counts) {
-  const int lane = threadIdx.x & 63;
-  const int64_t w = wave_uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
-  const int64_t npad = (n + BLK - 1) / BLK * BLK;
-  const int64_t total = static_cast<int64_t>((H + 127) >> 7) * npad;
-  int64_t pos = w * per_wave;
-  const int64_t end = min(total, pos + per_wave);
-  const f2v thr2 = g.thr2, ka = g.Ka, kb = g.Kb, k0 = g.K0;
-  while (pos < end) {
-    const int grp = static_cast<int>(pos / npad);
-    const int p0 = static_cast<int>(pos - grp * npad);
-    const int p1 = static_cast<int>(min(npad, p0 + (end - pos)));
-    pos += p1 - p0;
-    const int hlo = grp * 128 + lane, hhi = hlo + 64;
-    const int llo = hlo < H ? hlo : H - 1, lhi = hhi < H ? hhi : H - 1;
-    f2v f[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) f[k] = f2v{F32soa[k * ld + llo], F32soa[k * ld + lhi]};
-    int clo = 0, chi = 0;
-    for (int i = p0; i < p1; i += BLK) {
-      unsigned long long alo[BLK], ahi[BLK];
-#pragma unroll
-      for (int k = 0; k < BLK; ++k) {
-        const float4 p = pts32[i + k];
-        const f2v x2 = p.x, x1 = p.y, y2 = p.z, y1 = p.w;
-        const f2v l10 = __builtin_elementwise_fma(f[0], x2, __builtin_elementwise_fma(f[1], y2, f[2]));
-        const f2v l11 = __builtin_elementwise_fma(f[3], x2, __builtin_elementwise_fma(f[4], y2, f[5]));
-        const f2v l12 = __builtin_elementwise_fma(f[6], x2, __builtin_elementwise_fma(f[7], y2, f[8]));
-        const f2v l20 = __builtin_elementwise_fma(f[0], x1, __builtin_elementwise_fma(f[3], y1, f[6]));
-        const f2v l21 = __builtin_elementwise_fma(f[1], x1, __builtin_elementwise_fma(f[4], y1, f[7]));
-        const f2v e = __builtin_elementwise_fma(l10, x1, __builtin_elementwise_fma(l11, y1, l12));
-        const f2v n1 = __builtin_elementwise_fma(l10, l10, l11 * l11);
-        const f2v n2 = __builtin_elementwise_fma(l20, l20, l21 * l21);
-        const f2v m = f2v{fminf(n1.x, n2.x), fminf(n1.y, n2.y)};
-        const f2v ee = e * e;
-        const f2v rhs = thr2 * m;
-        const f2v d = ee - rhs;
-        const f2v B = __builtin_elementwise_fma(ee, ka, __builtin_elementwise_fma(rhs, kb, k0));
-        clo += (d.x < -B.x) ? 1 : 0;  // sure inliers
-        chi += (d.y < -B.y) ? 1 : 0;
-        alo[k] = __ballot(fabsf(d.x) <= B.x);
-        ahi[k] = __ballot(fabsf(d.y) <= B.y);
-      }
-      unsigned long long any = 0ull;
-#pragma unroll
-      for (int k = 0; k < BLK; ++k) any |= alo[k] | ahi[k];
-      if (any != 0ull) {
-        double fd[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) fd[k] = Fsoa[k * ld + llo];
-#pragma unroll
-        for (int k = 0; k < BLK; ++k)
-          if ((alo[k] >> lane) & 1ull) clo += test64(fd, pts[i + k], g.thr2_px) ? 1 : 0;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) fd[k] = Fsoa[k * ld + lhi];
-#pragma unroll
-        for (int k = 0; k < BLK; ++k)
-          if ((ahi[k] >> lane) & 1ull) chi += test64(fd, pts[i + k], g.thr2_px) ? 1 : 0;
-      }
-    }
-    if (hlo < H) atomicAdd(&counts[hlo], clo);
-    if (hhi < H) atomicAdd(&counts[hhi], chi);
-  }
-}
-
-__global__ __launch_bounds__(256) void k_pack_points32(const Pt *__restrict__ pts, int n,
-                                                       Frame fr, float4 *__restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= ((n + 7) & ~7)) return;
-  if (i >= n) {  // padding: NaN points are never inliers and never ambiguous
-    const float qn = __builtin_nanf("");
-    out[i] = make_float4(qn, qn, qn, qn);
-    return;
-  }
-  const Pt p = pts[i];
-  const double is = 1.0 / fr.s;
-  // layout (x2, x1, y2, y1): the SGPR pairs (x2, x1) and (y2, y1) feed v_pk_fma_f32
-  out[i] = make_float4(static_cast<float>((p.x2 - fr.cx2) * is),
-                       static_cast<float>((p.x1 - fr.cx1) * is),
-                       static_cast<float>((p.y2 - fr.cy2) * is),
-                       static_cast<float>((p.y1 - fr.cy1) * is));
 }
 
 // ----------------------------------------------------------------------------------------
@@ -1374,13 +922,6 @@ hipError_t launch_f8_count(const Pt *pts, int n, int H, const double *Fsoa, int6
   return hipGetLastError();
 }
 
-hipError_t launch_pack_points32(const Pt *pts, int n, const Frame &fr, float4 *pts32,
-                                hipStream_t s) {
-  hipLaunchKernelGGL(k_pack_points32, dim3((n + 7 + 255) / 256), dim3(256), 0, s, pts, n, fr,
-                     pts32);
-  return hipGetLastError();
-}
-
 hipError_t set_count_timeline(uint64_t *buf) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_count_ts), &buf, sizeof(buf));
 }
@@ -1392,149 +933,53 @@ hipError_t launch_pack_points32q(const Pt *pts, int n, const Frame &fr, float4 *
   return hipGetLastError();
 }
 
-hipError_t launch_f8_count32q(const float4 *ptsq, const Pt *pts, int n, int H,
-                              const float *F32soa, const double *Fsoa, int64_t ld, int waves,
-                              const GuardW &g, int *counts, hipStream_t s, int *gdone,
-                              int *status, const float4 *G4, bool use_asm, int block_threads,
-                              bool xcd_remap) {
+// Resident waves of k_f8_count32q: its ~106 SGPRs admit 6 waves per SIMD
+// (floor(800 / (ceil(sgpr / 16) * 16 + 16)), MI355X_MICROARCH.md; the occupancy API reports 7,
+// one block per CU too many for SGPR-heavy kernels; the wave timeline shows 6144 resident).
+int count32q_resident_waves(int device) {
+  int cus = 256;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+    cus = 256;
+  return cus * 4 * 6;
+}
+
+Count32qShape count32q_shape(int n, int H, int waves, int slices_per_wave, int block_threads,
+                            int prio) {
+  Count32qShape sh{};
   const int64_t npad = (n + 7) / 8 * 8;
   const int64_t total = static_cast<int64_t>((H + 63) / 64) * npad;
-  int64_t W = std::max<int64_t>(1, std::min<int64_t>(waves, total / 64));
+  // slices_per_wave x the resident waves (2 by default: A/B on C2 in r01 and r02, 2x ahead
+  // of 1x, 2.67x and 5.3x by 1-6 %), at least 64 points each, a multiple of 8 points
+  const int64_t k = slices_per_wave > 0 ? slices_per_wave : 2;
+  int64_t W = std::max<int64_t>(1, std::min<int64_t>(k * waves, total / 64));
   int64_t per = (total + W - 1) / W;
   per = (per + 7) / 8 * 8;
   W = (total + per - 1) / per;
-  const int bt = block_threads == 1024 ? 1024 : block_threads == 512 ? 512 : 256;
-  const int64_t wpb = bt / 64;
-  int64_t nb = (W + wpb - 1) / wpb;
-  int rows = 0;
-  if (xcd_remap) {  // waves past W find an empty range (pos >= end) and exit
-    rows = static_cast<int>((nb + 7) / 8);
-    nb = 8 * static_cast<int64_t>(rows);
-  }
-  const dim3 grid(static_cast<unsigned>(nb)), block(static_cast<unsigned>(bt));
-#define RSD_Q_LAUNCH(A, B)                                                                     \
-  hipLaunchKernelGGL((k_f8_count32q<A, B>), grid, block, 0, s, ptsq, pts, n, H, F32soa, Fsoa, \
-                     ld, per, g, counts, gdone, status, G4, rows)
-  if (use_asm) {
-    if (bt == 1024) RSD_Q_LAUNCH(true, 1024);
-    else if (bt == 512) RSD_Q_LAUNCH(true, 512);
-    else RSD_Q_LAUNCH(true, 256);
-  } else {
-    if (bt == 1024) RSD_Q_LAUNCH(false, 1024);
-    else if (bt == 512) RSD_Q_LAUNCH(false, 512);
-    else RSD_Q_LAUNCH(false, 256);
-  }
+  sh.per_wave = per;
+  sh.prio = prio;
+  sh.block_threads = block_threads == 64 || block_threads == 128 ? block_threads : 256;
+  const int64_t wpb = sh.block_threads / 64;
+  sh.blocks = (W + wpb - 1) / wpb;
+  return sh;
+}
+
+hipError_t launch_f8_count32q(const float4 *ptsq, const Pt *pts, int n, int H,
+                              const float *F32soa, const double *Fsoa, int64_t ld,
+                              const Count32qShape &sh, const GuardW &g, int *counts,
+                              hipStream_t s, int *gdone, int *status, const float4 *G4) {
+#define RSD_Q_LAUNCH(BT)                                                                       \
+  hipLaunchKernelGGL((k_f8_count32q<BT>), dim3(static_cast<unsigned>(sh.blocks)), dim3(BT), 0, s, \
+                     ptsq, pts, n, H, F32soa, Fsoa, ld, sh.per_wave, sh.prio, g, counts, gdone,   \
+                     status, G4)
+  if (sh.block_threads == 64)
+    RSD_Q_LAUNCH(64);
+  else if (sh.block_threads == 128)
+    RSD_Q_LAUNCH(128);
+  else
+    RSD_Q_LAUNCH(256);
 #undef RSD_Q_LAUNCH
   return hipGetLastError();
 }
-
-hipError_t launch_f8_count32p(const float4 *pts32, const Pt *pts, int n, int H,
-                              const float *F32soa, const double *Fsoa, int64_t ld, int waves,
-                              const GuardPk &g, int *counts, hipStream_t s, int variant) {
-  const int blk = variant == 3 ? 4 : 2;
-  const int64_t npad = (n + blk - 1) / blk * blk;
-  const int64_t total = static_cast<int64_t>((H + 127) / 128) * npad;
-  int64_t W = std::max<int64_t>(1, std::min<int64_t>(waves, total / 32));
-  int64_t per = (total + W - 1) / W;
-  per = (per + blk - 1) / blk * blk;
-  W = (total + per - 1) / per;
-  const dim3 grid(static_cast<unsigned>((W + 3) / 4));
-  switch (variant) {
-    case 1:
-      hipLaunchKernelGGL((k_f8_count32p<2, 6>), grid, dim3(256), 0, s, pts32, pts, n, H, F32soa,
-                         Fsoa, ld, per, g, counts);
-      break;
-    case 2:
-      hipLaunchKernelGGL((k_f8_count32p<2, 4>), grid, dim3(256), 0, s, pts32, pts, n, H, F32soa,
-                         Fsoa, ld, per, g, counts);
-      break;
-    case 3:
-      hipLaunchKernelGGL((k_f8_count32p<4, 6>), grid, dim3(256), 0, s, pts32, pts, n, H, F32soa,
-                         Fsoa, ld, per, g, counts);
-      break;
-    default:
-      hipLaunchKernelGGL((k_f8_count32p<2, 8>), grid, dim3(256), 0, s, pts32, pts, n, H, F32soa,
-                         Fsoa, ld, per, g, counts);
-  }
-  return hipGetLastError();
-}
-
-hipError_t launch_f8_count32(const float4 *pts32, const Pt *pts, int n, int H,
-                             const float *F32soa, const double *Fsoa, int64_t ld, int waves,
-                             const Guard32 &g, int *counts, hipStream_t s, int blk,
-                             bool prefetch) {
-  blk = blk == 8 ? 8 : 4;
-  const int64_t npad = (n + blk - 1) / blk * blk;
-  const int64_t total = static_cast<int64_t>((H + 63) / 64) * npad;
-  // at least 64 points per slice; slices are multiples of the point block
-  int64_t W = std::max<int64_t>(1, std::min<int64_t>(waves, total / 64));
-  int64_t per = (total + W - 1) / W;
-  per = (per + blk - 1) / blk * blk;
-  W = (total + per - 1) / per;
-  const dim3 grid(static_cast<unsigned>((W + 3) / 4));
-  if (blk == 8 && prefetch)
-    hipLaunchKernelGGL((k_f8_count32<8, true>), grid, dim3(256), 0, s, pts32, pts, n, H, F32soa,
-                       Fsoa, ld, per, g, counts);
-  else if (blk == 8)
-    hipLaunchKernelGGL((k_f8_count32<8, false>), grid, dim3(256), 0, s, pts32, pts, n, H,
-                       F32soa, Fsoa, ld, per, g, counts);
-  else if (prefetch)
-    hipLaunchKernelGGL((k_f8_count32<4, true>), grid, dim3(256), 0, s, pts32, pts, n, H, F32soa,
-                       Fsoa, ld, per, g, counts);
-  else
-    hipLaunchKernelGGL((k_f8_count32<4, false>), grid, dim3(256), 0, s, pts32, pts, n, H,
-                       F32soa, Fsoa, ld, per, g, counts);
-  return hipGetLastError();
-}
-
-template <class Guard>
-hipError_t launch_f8_count32x(const float4 *pts32, const Pt *pts, int n, int H,
-                              const float *F32soa, const double *Fsoa, int64_t ld, int waves,
-                              const Guard &g, int *counts, hipStream_t s, int blk,
-                              bool prefetch, int *gdone, int *status, const float4 *G4) {
-  constexpr int D = std::is_same<Guard, GuardX>::value   ? 0
-                    : std::is_same<Guard, GuardY>::value ? 1
-                    : std::is_same<Guard, GuardF>::value ? 2
-                                                         : 3;
-  blk = blk == 8 ? 8 : 4;
-  const int64_t npad = (n + blk - 1) / blk * blk;
-  const int64_t total = static_cast<int64_t>((H + 63) / 64) * npad;
-  int64_t W = std::max<int64_t>(1, std::min<int64_t>(waves, total / 64));
-  int64_t per = (total + W - 1) / W;
-  per = (per + blk - 1) / blk * blk;
-  W = (total + per - 1) / per;
-  const dim3 grid(static_cast<unsigned>((W + 3) / 4));
-  if (blk == 8 && prefetch)
-    hipLaunchKernelGGL((k_f8_count32x<8, true, D, Guard>), grid, dim3(256), 0, s, pts32, pts, n, H,
-                       F32soa, Fsoa, ld, per, g, counts, gdone, status, G4);
-  else if (blk == 8)
-    hipLaunchKernelGGL((k_f8_count32x<8, false, D, Guard>), grid, dim3(256), 0, s, pts32, pts, n, H,
-                       F32soa, Fsoa, ld, per, g, counts, gdone, status, G4);
-  else if (prefetch)
-    hipLaunchKernelGGL((k_f8_count32x<4, true, D, Guard>), grid, dim3(256), 0, s, pts32, pts, n, H,
-                       F32soa, Fsoa, ld, per, g, counts, gdone, status, G4);
-  else
-    hipLaunchKernelGGL((k_f8_count32x<4, false, D, Guard>), grid, dim3(256), 0, s, pts32, pts, n, H,
-                       F32soa, Fsoa, ld, per, g, counts, gdone, status, G4);
-  return hipGetLastError();
-}
-
-template hipError_t launch_f8_count32x<GuardX>(const float4 *, const Pt *, int, int,
-                                               const float *, const double *, int64_t, int,
-                                               const GuardX &, int *, hipStream_t, int, bool,
-                                               int *, int *, const float4 *);
-template hipError_t launch_f8_count32x<GuardY>(const float4 *, const Pt *, int, int,
-                                               const float *, const double *, int64_t, int,
-                                               const GuardY &, int *, hipStream_t, int, bool,
-                                               int *, int *, const float4 *);
-template hipError_t launch_f8_count32x<GuardW>(const float4 *, const Pt *, int, int,
-                                               const float *, const double *, int64_t, int,
-                                               const GuardW &, int *, hipStream_t, int, bool,
-                                               int *, int *, const float4 *);
-template hipError_t launch_f8_count32x<GuardF>(const float4 *, const Pt *, int, int,
-                                               const float *, const double *, int64_t, int,
-                                               const GuardF &, int *, hipStream_t, int, bool,
-                                               int *, int *, const float4 *);
 
 int select_per_block(int H) { return (H + kSelectBlocks - 1) / kSelectBlocks; }
 int select_blocks(int H) {

@@ -47,7 +47,7 @@ struct RunBufs {
   double *d_cstd = nullptr, *d_cnorm = nullptr;
   rsd::F8DevResult *d_res = nullptr;
   int *d_gdone = nullptr;      // per-group finish counters (fused c* in k_f8_count32x)
-  float4 *d_G4 = nullptr;      // per-hypothesis decision constants (k_f8_count32x DEC 3)
+  float4 *d_G4 = nullptr;      // per-hypothesis decision constants (k_f8_count32q)
   // host tuples (parity mode fed from the host) are staged in a pinned buffer owned by the
   // set, so the caller's array may go away as soon as rs_f8_plan_run returns; ev_copy marks
   // the end of the H2D copy that last read it (waited for before the buffer is refilled)
@@ -72,79 +72,6 @@ Bounds fp32_bounds(const rsd::Frame &fr, double thresh) {
   return {u, De, Dn, (thresh / fr.s) * (thresh / fr.s)};
 }
 
-rsd::Guard32 guard_constants(const rsd::Frame &fr, double thresh) {
-  const Bounds b = fp32_bounds(fr, thresh);
-  rsd::Guard32 g;
-  g.thr2 = static_cast<float>(b.thr2);
-  g.K1 = static_cast<float>(1.02 * 2.0 * b.De);
-  g.Ku = static_cast<float>(1.02 * b.u);
-  g.K0 = static_cast<float>(1.02 * (b.De * b.De + b.thr2 * (1.0 + 1e-6) * b.Dn));
-  g.thr2_px = thresh * thresh;
-  return g;
-}
-
-rsd::GuardPk guard_packed(const rsd::Frame &fr, double thresh) {
-  const Bounds b = fp32_bounds(fr, thresh);
-  const double c = std::sqrt(b.thr2);  // AM-GM split point for 2 De |e| <= De (e^2 / c + c)
-  rsd::GuardPk g;
-  g.thr2 = static_cast<float>(b.thr2);
-  g.Ka = static_cast<float>(1.02 * (b.De / c * (1.0 + 2.0 * b.u) + b.u));
-  g.Kb = static_cast<float>(1.02 * 2.0 * b.u);
-  g.K0 = static_cast<float>(1.02 * (b.De * c + b.De * b.De + b.thr2 * (1.0 + 1e-6) * b.Dn));
-  g.thr2_px = thresh * thresh;
-  return g;
-}
-
-// k_f8_count32x decision constants (derivation above the kernel in f8_kernels.hip).  The
-// 1.02 and 1 -/+ 4u factors absorb the fp64 -> fp32 rounding of the constants themselves.
-rsd::GuardX guard_pair(const rsd::Frame &fr, double thresh) {
-  const Bounds b = fp32_bounds(fr, thresh);
-  const double T = b.thr2, u = b.u, tiny = 1e-30;  // tiny: denormal flushing headroom
-  rsd::GuardX g;
-  g.K1i = static_cast<float>(1.02 * 2.0 * b.De);
-  g.K1o_neg = -g.K1i;
-  g.K0i = static_cast<float>(1.02 * (b.De * b.De + T * b.Dn) + tiny);
-  g.K0o_neg = -static_cast<float>(1.02 * (1.0 + u) * T * b.Dn + tiny);
-  g.alpha = static_cast<float>(T * (1.0 - u) * (1.0 - u) / (1.0 + u) * (1.0 - 4.0 * u));
-  g.beta = static_cast<float>(T * (1.0 + u) * (1.0 + u) / (1.0 - u) * (1.0 + 4.0 * u));
-  g.thr2_px = thresh * thresh;
-  return g;
-}
-
-int env_int(const char *name, int dflt);
-
-// Plain-op decision constants (derivation above k_f8_count32x, DEC = 1).
-rsd::GuardY guard_plain(const rsd::Frame &fr, double thresh) {
-  const Bounds b = fp32_bounds(fr, thresh);
-  const double T = b.thr2, u = b.u, tiny = 1e-30;
-  const double c1 = (1.0 - u) / (1.0 + u);
-  rsd::GuardY g;
-  g.K1 = static_cast<float>(1.02 * 2.0 * b.De / (c1 * (1.0 - u)));
-  g.K0 = static_cast<float>(1.02 * (b.De * b.De + T * b.Dn) / (c1 * (1.0 - u)) + tiny);
-  g.alpha = static_cast<float>(T * (1.0 - 4.0 * u) / (1.0 + u));
-  const double alpha = g.alpha;  // the fp32 value the kernel multiplies with
-  g.delta = static_cast<float>(1.02 * (T - alpha * (1.0 - u)) / c1 + tiny);
-  g.thr2_px = thresh * thresh;
-  if (env_int("RSAMD_NORECHECK", 0)) g.thr2_px = -1.0;  // timing diagnostic: no fp64 re-test
-  return g;
-}
-
-// Folded plain-op decision constants (derivation above k_f8_count32x, DEC = 2).
-rsd::GuardF guard_folded(const rsd::Frame &fr, double thresh) {
-  const Bounds b = fp32_bounds(fr, thresh);
-  const double T = b.thr2, u = b.u, tiny = 1e-30;
-  const double c1 = (1.0 - u) / (1.0 + u), M = 18.0 * (1.0 + 1e-5);
-  rsd::GuardF g;
-  g.alpha = static_cast<float>(T * (1.0 - 4.0 * u) / (1.0 + u));
-  const double alpha = g.alpha;
-  const double D0 = (T - alpha * (1.0 - u)) * M;
-  g.K1 = static_cast<float>(1.02 * 2.0 * b.De / (c1 * (1.0 - u)));
-  g.K0 = static_cast<float>(1.02 * (b.De * b.De + T * b.Dn + D0) / (c1 * (1.0 - u)) + tiny);
-  g.pad_ = 0.f;
-  g.thr2_px = thresh * thresh;
-  return g;
-}
-
 int env_int(const char *name, int dflt) {
   const char *v = std::getenv(name);
   return v ? std::atoi(v) : dflt;
@@ -157,7 +84,6 @@ struct rs_f8_plan {
   int64_t n = 0, max_hyp = 0, ld = 0;
   double *d_p12 = nullptr;     // staging (2,n) p1 then (2,n) p2
   rsd::Pt *d_pts = nullptr;    // AoS float64 points
-  float4 *d_pts32 = nullptr;   // unit-frame fp32 points, NaN-padded to a multiple of 8
   float4 *d_pts32q = nullptr;  // the same, point-pair layout (k_f8_count32q)
   static constexpr int kBufs = 3, kSlots = 4, kEvRing = 64;
   RunBufs buf[kBufs];
@@ -171,45 +97,24 @@ struct rs_f8_plan {
   int64_t runs = 0, last_H = 0;
   bool pending = false;              // stream work not yet waited for
   bool tail_pending = false;         // the last run's tail is not enqueued yet
-  // Overlap mode (RSAMD_OVERLAP=1): solves run on their own stream `ss`, ahead of the
-  // counts, so the solve of run k+1 shares the machine with the count of run k.  Run k uses
-  // buffer set k % 3; ev_solved[s] orders count(k) after solve(k), ev_free[s] orders
-  // solve(k+3) after tail(k) (the last reader of set s).  Measured slower on C2 (154 vs
-  // 140 us per run: the cross-stream waits and the shared CUs cost more than the hidden
-  // 23 us solve), so the default is the single-stream [tail | solve] + count pipeline.
-  bool overlap = false;
-  hipStream_t ss = nullptr;
-  hipEvent_t ev_solved[kBufs] = {}, ev_free[kBufs] = {};
   rsd::TailArgs tail{};              // ... its arguments
-  // counting kernel selection (environment knobs for A/B sweeps, tools/sweep.py)
+  // counting kernel: fp32 point-pair kernel with the float64 guard re-test (default), or the
+  // plain float64 kernel (rs_f8_plan_set_count_precision; both give identical counts)
   rsd::Frame frame{1.0, 0.0, 0.0, 0.0, 0.0};
   bool fp32_ok = false;       // finite points and a non-degenerate frame
-  bool use_fp32 = true;       // RSAMD_COUNT=fp64 selects the float64 kernel
-  bool packed = false;        // RSAMD_COUNT=pk: two hypotheses per lane (v_pk_fma_f32)
-  bool pair = true;           // k_f8_count32x (default); RSAMD_COUNT=fp32: k_f8_count32
-  bool plain_dec = false;     // RSAMD_COUNT=y: k_f8_count32x with the plain-op decision
-  bool folded = false;        // RSAMD_COUNT=z: folded plain decision + SALU bit-plane counts
-  bool per_hyp = true;        // per-hypothesis AM-GM decision constants ("w", "q")
-  bool pointpair = true;      // "q" (default): DEC 3 decisions, packed over point pairs
-  bool q_asm = true;          // RSAMD_QASM=0: "q" with compiler-scheduled builtins
-  int q_block = 256;          // RSAMD_QBLOCK: workgroup size of the "q" kernel (256 / 512 / 1024)
-  bool q_xcd = false;         // RSAMD_XCD=1: keep the slices of a hypothesis group on one XCD
-  bool fuse_max = true;       // RSAMD_FUSEMAX=0: separate k_f8_max pass instead of the fused c*
+  bool use_fp32 = true;
   // HIP timing events per run (each is a marker packet between kernels): 0 none, 1 around the
   // counting kernel (default; the bench's roofline timing), 2 also the tail+solve launch
   int timing = 1;
   int timing_every = 1;       // RSAMD_TIMING_EVERY / rs_f8_plan_set_timing: time every k-th run
-  int resident_waves = 8192;  // slices of the fp32 kernel (RSAMD_WAVES)
-  int count_block = 8;        // points per scalar-load block (RSAMD_BLOCK = 4 | 8)
-  bool prefetch = false;      // ping-pong point prefetch (RSAMD_PREFETCH=1; spills SGPRs at 8)
-  int pk_variant = 0, pk_waves = 8192;
-  int chunk_override = 0;     // fp64 kernel point chunk (RSAMD_CHUNK)
-  int tail_cus = 0;           // CUs for the tail + solve split (RSAMD_TAILCUS; 0: 256 tail blocks)
-  int nospec = 0;             // RSAMD_NOSPEC=1: the replay always extracts S_RANSAC itself
+  int q_waves = 6144;         // resident waves of the fp32 kernel (RSAMD_WAVES)
+  int q_bt = 256;             // workgroup size of the fp32 kernel (RSAMD_QBT: 64 / 128 / 256)
+  int q_prio = 0;             // progress-levelled priority (RSAMD_QPRIO)
+  int q_slices = 0;           // slices per resident wave (RSAMD_QSLICES; 0: count32q_shape)
+  int tail_cus = 256;         // CUs shared by the tail + solve launch
+  int nospec = 0;             // RSAMD_NOSPEC=1 (test hook): the replay extracts S_RANSAC itself
   uint64_t *d_ts = nullptr;   // RSAMD_TSTAMP=<file>: wave timeline of the counting kernel
   const char *ts_path = nullptr;
-  int nt_store = 0;           // RSAMD_NTSTORE: non-temporal solve output stores
-  int solve_diag = 0;         // RSAMD_SOLVE_DIAG: timing-only solve variants (wrong models)
 
   const RunBufs &last() const { return buf[(runs - 1) % kBufs]; }
 };
@@ -223,7 +128,6 @@ struct rs_f8_plan {
 static void plan_free(rs_f8_plan *p) {
   (void)hipFree(p->d_p12);
   (void)hipFree(p->d_pts);
-  (void)hipFree(p->d_pts32);
   (void)hipFree(p->d_pts32q);
   if (p->d_ts) {
     (void)rsd::set_count_timeline(nullptr);
@@ -253,11 +157,6 @@ static void plan_free(rs_f8_plan *p) {
   for (auto &r : p->ring)
     for (auto &e : r)
       if (e) (void)hipEventDestroy(e);
-  for (int k = 0; k < rs_f8_plan::kBufs; ++k) {
-    if (p->ev_solved[k]) (void)hipEventDestroy(p->ev_solved[k]);
-    if (p->ev_free[k]) (void)hipEventDestroy(p->ev_free[k]);
-  }
-  if (p->ss) (void)hipStreamDestroy(p->ss);
 }
 
 extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_plan **out) {
@@ -273,42 +172,25 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
   p->max_hyp = max_hyp;
   p->ld = (max_hyp + 63) / 64 * 64;
   const size_t res_bytes = sizeof(rsd::F8DevResult) + sizeof(int64_t) * static_cast<size_t>(n);
-  p->chunk_override = env_int("RSAMD_CHUNK", 0);
-  if (const char *cm = std::getenv("RSAMD_COUNT")) {
+  if (const char *cm = std::getenv("RSAMD_COUNT"))  // tools: RSAMD_COUNT=fp64
     p->use_fp32 = std::strcmp(cm, "fp64") != 0;
-    p->packed = std::strcmp(cm, "pk") == 0;  // "q" (default), "w", "x", "y", "z", "fp32", "pk", "fp64"
-    p->pair = std::strcmp(cm, "x") == 0 || std::strcmp(cm, "y") == 0 ||
-              std::strcmp(cm, "z") == 0;
-    p->pointpair = std::strcmp(cm, "q") == 0;
-    p->pair = p->pair || std::strcmp(cm, "w") == 0 || p->pointpair;
-    p->plain_dec = std::strcmp(cm, "y") == 0;
-    p->folded = std::strcmp(cm, "z") == 0;
-    p->per_hyp = std::strcmp(cm, "w") == 0 || p->pointpair;
-  }
-  p->fuse_max = env_int("RSAMD_FUSEMAX", 1) != 0;
-  p->q_asm = env_int("RSAMD_QASM", 1) != 0;
   p->timing = env_int("RSAMD_TIMING", 1);
   p->timing_every = std::max(1, env_int("RSAMD_TIMING_EVERY", 1));
   {
     int cus = 256;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
       cus = 256;
-    // slices of the (group, point) plane: 2 per resident wave slot (8 per SIMD) for the
-    // default "q" kernel (A/B on C2: 16384 ahead of 8192 / 12288 / 24576 / 32768 by 1-3 %)
-    p->tail_cus = env_int("RSAMD_TAILCUS", cus);
-    p->resident_waves = std::max(1, env_int("RSAMD_WAVES", cus * 4 * 8 * (p->pointpair ? 2 : 4)));
-    p->count_block = env_int("RSAMD_BLOCK", 8) == 4 ? 4 : 8;
-    p->prefetch = env_int("RSAMD_PREFETCH", 0) != 0;
-    p->pk_variant = env_int("RSAMD_PKVAR", 0);
-    const int minw = p->pk_variant == 1 || p->pk_variant == 3 ? 6 : (p->pk_variant == 2 ? 4 : 8);
-    p->pk_waves = std::max(1, env_int("RSAMD_WAVES", cus * 4 * minw));
+    p->tail_cus = cus;
+    p->q_waves = std::max(1, env_int("RSAMD_WAVES", rsd::count32q_resident_waves(c->device)));
+    p->q_slices = env_int("RSAMD_QSLICES", 0);
+    p->q_bt = env_int("RSAMD_QBT", 256);
+    p->q_prio = env_int("RSAMD_QPRIO", 0);
   }
   hipError_t e = hipSuccess;
 #define ALLOC(ptr, bytes) \
   if (e == hipSuccess) e = hipMalloc(&(ptr), (bytes));
   ALLOC(p->d_p12, sizeof(double) * 4 * n);
   ALLOC(p->d_pts, sizeof(rsd::Pt) * n);
-  ALLOC(p->d_pts32, sizeof(float4) * ((n + 7) & ~7LL));
   ALLOC(p->d_pts32q, sizeof(float4) * ((n + 7) & ~7LL));
   for (RunBufs &b : p->buf) {
     ALLOC(b.d_F, sizeof(double) * 9 * p->ld);
@@ -337,25 +219,13 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
   for (auto &r : p->ring)
     for (auto &ev : r)
       if (e == hipSuccess) e = hipEventCreate(&ev);
-  p->overlap = env_int("RSAMD_OVERLAP", 0) != 0;
-  p->solve_diag = env_int("RSAMD_SOLVE_DIAG", 0);
-  p->nt_store = env_int("RSAMD_NTSTORE", 0);
   p->nospec = env_int("RSAMD_NOSPEC", 0) != 0;
   p->ts_path = std::getenv("RSAMD_TSTAMP");
   if (p->ts_path) {
-    const size_t tsb = sizeof(uint64_t) * 2 * (static_cast<size_t>(p->resident_waves) + 1024);
+    const size_t tsb = sizeof(uint64_t) * 4 * (static_cast<size_t>(p->q_waves) * 64 + 1024);
     if (hipMalloc(&p->d_ts, tsb) == hipSuccess) {
       (void)hipMemset(p->d_ts, 0, tsb);
       (void)rsd::set_count_timeline(p->d_ts);
-    }
-  }
-  p->q_block = env_int("RSAMD_QBLOCK", 256);
-  p->q_xcd = env_int("RSAMD_XCD", 0) != 0;
-  if (p->overlap) {
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->ss, hipStreamNonBlocking);
-    for (int k = 0; k < rs_f8_plan::kBufs; ++k) {
-      if (e == hipSuccess) e = hipEventCreateWithFlags(&p->ev_solved[k], hipEventDisableTiming);
-      if (e == hipSuccess) e = hipEventCreateWithFlags(&p->ev_free[k], hipEventDisableTiming);
     }
   }
   if (e != hipSuccess) {
@@ -375,7 +245,6 @@ static int plan_flush(rs_f8_plan *p) {
     p->tail_pending = false;
   }
   HIP_TRY(hipStreamSynchronize(p->ctx->stream));
-  if (p->ss) HIP_TRY(hipStreamSynchronize(p->ss));
   p->pending = false;
   return RS_OK;
 }
@@ -425,7 +294,6 @@ extern "C" int rs_f8_plan_set_points(rs_f8_plan *p, const double *p1, const doub
   if (p->fp32_ok) {
     fr.s *= 1.0 + 1e-12;  // |x~| <= 1 after the fp64 division
     p->frame = fr;
-    HIP_TRY(rsd::launch_pack_points32(p->d_pts, static_cast<int>(n), fr, p->d_pts32, c->stream));
     HIP_TRY(rsd::launch_pack_points32q(p->d_pts, static_cast<int>(n), fr, p->d_pts32q,
                                        c->stream));
   }
@@ -434,7 +302,6 @@ extern "C" int rs_f8_plan_set_points(rs_f8_plan *p, const double *p1, const doub
 }
 
 static int choose_chunk(const rs_f8_plan *p, int64_t H) {
-  if (p->chunk_override > 0) return p->chunk_override;
   const int64_t groups = (H + 63) / 64;
   // aim for >= 8 units of work per SIMD (1024 SIMDs) without chunks below 64 points
   int64_t nchunks = (8192 + groups - 1) / groups;
@@ -466,12 +333,7 @@ static int plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t seed, uint6
   p->timed[p->runs % rs_f8_plan::kEvRing] = tl >= 1;
   const int slot = static_cast<int>(p->runs % rs_f8_plan::kSlots);
   const bool fp32 = p->use_fp32 && p->fp32_ok;
-  const bool fused_max = fp32 && p->pair && !p->packed && p->fuse_max;
   hipStream_t ms = c->stream;
-  const int set = static_cast<int>(p->runs % rs_f8_plan::kBufs);
-  hipStream_t sst = p->overlap ? p->ss : ms;  // the solve's stream
-  if (p->overlap && p->runs >= rs_f8_plan::kBufs)  // set `set` free: run k-3's tail is done
-    HIP_TRY(hipStreamWaitEvent(sst, p->ev_free[set], 0));
 
   if (mode == RS_SAMPLER_TUPLES && !dev_tuples) {
     // stage through the set's pinned buffer: the copy no longer reads caller memory after
@@ -490,8 +352,8 @@ static int plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t seed, uint6
     if (!b.ev_copy) HIP_TRY(hipEventCreateWithFlags(&b.ev_copy, hipEventDisableTiming));
     std::memcpy(b.h_tuples, host_tuples, sizeof(int) * 8 * H);
     HIP_TRY(hipMemcpyAsync(b.d_tuples, b.h_tuples, sizeof(int) * 8 * H, hipMemcpyHostToDevice,
-                           sst));
-    HIP_TRY(hipEventRecord(b.ev_copy, sst));
+                           ms));
+    HIP_TRY(hipEventRecord(b.ev_copy, ms));
     b.copy_pending = true;
   }
   // [tail of the previous run | solve of this run]: buffer set b was last read by run k-2,
@@ -511,66 +373,32 @@ static int plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t seed, uint6
   sa.F32soa = fp32 ? b.d_F32 : nullptr;
   sa.frame = fp32 ? p->frame : rsd::Frame{1.0, 0.0, 0.0, 0.0, 0.0};
   sa.gdone = b.d_gdone;
-  sa.diag = p->solve_diag;
-  sa.nt = p->nt_store;
-  if (fp32 && p->pair && p->per_hyp) {
+  if (fp32) {
     const Bounds gb = fp32_bounds(p->frame, thresh);
     sa.G4 = b.d_G4;
     sa.gT = gb.thr2;
     sa.gDe = gb.De;
     sa.gDn = gb.Dn;
   }
-  if (tl >= 2) HIP_TRY(hipEventRecord(ev[2], sst));
-  HIP_TRY(rsd::launch_f8_tail_solve(p->tail_pending ? &p->tail : nullptr, &sa, sst, p->tail_cus));
+  if (tl >= 2) HIP_TRY(hipEventRecord(ev[2], ms));
+  HIP_TRY(rsd::launch_f8_tail_solve(p->tail_pending ? &p->tail : nullptr, &sa, ms, p->tail_cus));
   p->tail_pending = false;
-  if (tl >= 2) HIP_TRY(hipEventRecord(ev[3], sst));
-  if (p->overlap) {
-    HIP_TRY(hipEventRecord(p->ev_solved[set], sst));
-    HIP_TRY(hipStreamWaitEvent(ms, p->ev_solved[set], 0));
-  }
+  if (tl >= 2) HIP_TRY(hipEventRecord(ev[3], ms));
 
   // counts of this run
   if (tl >= 1) HIP_TRY(hipEventRecord(ev[0], ms));
-  if (fp32 && p->packed)
-    HIP_TRY(rsd::launch_f8_count32p(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
-                                    p->pk_waves, guard_packed(p->frame, thresh), b.d_counts, ms,
-                                    p->pk_variant));
-  else if (fp32 && p->pair && p->per_hyp) {
-    rsd::GuardW gw{thresh * thresh};
-    if (env_int("RSAMD_NORECHECK", 0)) gw.thr2_px = -1.0;  // timing diagnostic only
-    if (p->pointpair)
-      HIP_TRY(rsd::launch_f8_count32q(p->d_pts32q, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
-                                      p->resident_waves, gw, b.d_counts, ms,
-                                      fused_max ? b.d_gdone : nullptr, b.d_status, b.d_G4,
-                                      p->q_asm, p->q_block, p->q_xcd));
-    else
-      HIP_TRY(rsd::launch_f8_count32x(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
-                                      p->resident_waves, gw, b.d_counts, ms, p->count_block,
-                                      p->prefetch, fused_max ? b.d_gdone : nullptr, b.d_status,
-                                      b.d_G4));
-  } else if (fp32 && p->pair && p->folded)
-    HIP_TRY(rsd::launch_f8_count32x(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
-                                    p->resident_waves, guard_folded(p->frame, thresh),
-                                    b.d_counts, ms, p->count_block, p->prefetch,
-                                    fused_max ? b.d_gdone : nullptr, b.d_status));
-  else if (fp32 && p->pair && p->plain_dec)
-    HIP_TRY(rsd::launch_f8_count32x(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
-                                    p->resident_waves, guard_plain(p->frame, thresh),
-                                    b.d_counts, ms, p->count_block, p->prefetch,
-                                    fused_max ? b.d_gdone : nullptr, b.d_status));
-  else if (fp32 && p->pair)
-    HIP_TRY(rsd::launch_f8_count32x(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
-                                    p->resident_waves, guard_pair(p->frame, thresh),
-                                    b.d_counts, ms, p->count_block, p->prefetch,
-                                    fused_max ? b.d_gdone : nullptr, b.d_status));
-  else if (fp32)
-    HIP_TRY(rsd::launch_f8_count32(p->d_pts32, p->d_pts, n, h, b.d_F32, b.d_F, p->ld,
-                                   p->resident_waves, guard_constants(p->frame, thresh),
-                                   b.d_counts, ms, p->count_block, p->prefetch));
-  else
+  if (fp32) {
+    // fused c*: the chunk that completes a hypothesis group folds its max into status[0]
+    const rsd::Count32qShape sh = rsd::count32q_shape(n, h, p->q_waves, p->q_slices, p->q_bt,
+                                                      p->q_prio);
+    HIP_TRY(rsd::launch_f8_count32q(p->d_pts32q, p->d_pts, n, h, b.d_F32, b.d_F, p->ld, sh,
+                                    rsd::GuardW{thresh * thresh}, b.d_counts, ms, b.d_gdone,
+                                    b.d_status, b.d_G4));
+  } else {
     HIP_TRY(rsd::launch_f8_count(p->d_pts, n, h, b.d_F, p->ld, choose_chunk(p, H),
                                  thresh * thresh, b.d_counts, ms));
-  if (!fused_max) HIP_TRY(rsd::launch_f8_max(b.d_counts, h, b.d_status, ms));
+    HIP_TRY(rsd::launch_f8_max(b.d_counts, h, b.d_status, ms));
+  }
   if (tl >= 1) HIP_TRY(hipEventRecord(ev[1], ms));
 
   // this run's tail rides along with the next run's solve (or plan_flush)
@@ -595,14 +423,7 @@ static int plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t seed, uint6
   ta.cnorm = b.d_cnorm;
   ta.res = b.d_res;
   ta.hres = p->h_slot_dev[slot];
-  if (p->overlap) {
-    // the tail right behind its count on the main stream; the next solves are already
-    // running ahead on `ss`
-    HIP_TRY(rsd::launch_f8_tail_solve(&ta, nullptr, ms));
-    HIP_TRY(hipEventRecord(p->ev_free[set], ms));
-  } else {
-    p->tail_pending = true;
-  }
+  p->tail_pending = true;
   ++p->runs;
   p->last_H = H;
   p->pending = true;
@@ -617,8 +438,8 @@ extern "C" int rs_f8_plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t s
 // Parity mode with the numpy stream sampled on the GPU (np_sampler.hip) straight into the
 // tuple buffer of the run about to be issued; advances (key, pos).  The sampler is synchronous
 // on the context stream, and that buffer set was last read by run k-2's solve, which precedes
-// it in stream order.  The two-stream overlap variant reads tuples on its own stream: it and
-// populations beyond the GPU parse's range go through the host replay.
+// it in stream order.  Populations beyond the GPU parse's range (and RSAMD_NP_HOST, a test
+// hook) go through the host replay.
 extern "C" int rs_f8_plan_run_np_slice(rs_f8_plan *p, int64_t H, int64_t start, int64_t count,
                                        uint32_t *key, int32_t *pos, double thresh) {
   if (!p || !key || !pos) return fail(RS_EINVAL, "null pointer");
@@ -626,7 +447,7 @@ extern "C" int rs_f8_plan_run_np_slice(rs_f8_plan *p, int64_t H, int64_t start, 
     return fail(RS_EINVAL, "hypothesis slice out of range");
   if (count > p->max_hyp) return fail(RS_EINVAL, "hypothesis count out of plan range");
   int st;
-  if (!p->overlap && rs::np_gpu_supported(p->n, 8) && std::getenv("RSAMD_NP_HOST") == nullptr) {
+  if (rs::np_gpu_supported(p->n, 8) && std::getenv("RSAMD_NP_HOST") == nullptr) {
     RunBufs &b = p->buf[p->runs % rs_f8_plan::kBufs];
     if ((st = rs::np_choice_device(p->ctx, key, pos, p->n, 8, H, b.d_tuples, false, start, count)))
       return st;
@@ -666,7 +487,7 @@ extern "C" int rs_f8_plan_result(rs_f8_plan *p, rs_f8_result *out, int64_t *inli
   out->n_candidates = r->n_candidates;
   out->guard_mismatch = r->guard_mismatch;
   if (p->d_ts && p->ts_path) {  // diagnostics: append this run's wave timeline
-    std::vector<uint64_t> t(2 * (static_cast<size_t>(p->resident_waves) + 1024));
+    std::vector<uint64_t> t(4 * (static_cast<size_t>(p->q_waves) * 64 + 1024));
     if (hipMemcpy(t.data(), p->d_ts, sizeof(uint64_t) * t.size(), hipMemcpyDeviceToHost) ==
         hipSuccess) {
       if (FILE *f = std::fopen(p->ts_path, "ab")) {
