@@ -237,6 +237,33 @@ int rs_pnp_ransac_cv(rs_ctx *ctx, const double *X, const double *uv, int64_t m, 
                      int64_t *n_inliers, int64_t *iters_used);
 
 /* ------------------------------------------------------------------------------------------
+ * Five-point essential matrix (Nister) and E-RANSAC.  No reference counterpart (SURVEY.md 8(a)
+ * row a-15, north_star "5-point E"); the reference's convention: y1^T E y2 = 0, E = R^T [t]_x
+ * (fun.py:12-21), F = K1^-T E K2^-1 in pixels.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct rs_e5_result {
+  double E[9];            /* winning essential matrix (unit Frobenius norm), row-major      */
+  double F[9];            /* its pixel-space F = K1^-T E K2^-1                               */
+  int64_t best_sample;    /* minimal sample of the winner, -1 if none                       */
+  int64_t best_solution;  /* which of that sample's real solutions (0..9)                   */
+  int64_t best_count;     /* consensus size                                                 */
+} rs_e5_result;
+
+/* All real solutions of S minimal samples: y1, y2 (5 S, 3) homogeneous C-normalised points,
+ * sample s = rows 5s .. 5s+4.  E_out (S, 10, 9): unit-norm solutions, NaN past nsol[s]. */
+int rs_e5_solve(rs_ctx *ctx, const double *y1, const double *y2, int64_t S, double *E_out,
+                int32_t *nsol);
+
+/* E-RANSAC over S Philox 5-point samples of n pixel correspondences p1, p2 ((2, n) each, the
+ * layout of fun.py:298) with cameras K1, K2: every real solution is a hypothesis, scored with
+ * the reference's F-RANSAC test (lab3.fmatrix_residuals, max(|r1|, |r2|) < thresh, fun.py:
+ * 315-317); among the hypotheses with the largest count the smallest ||d|| (d_i =
+ * max(|r1_i|, |r2_i|) over all points, fun.py:317) wins, the first on equal norms. */
+int rs_e5_ransac(rs_ctx *ctx, const double *p1, const double *p2, int64_t n, const double *K1,
+                 const double *K2, int64_t S, uint64_t seed, double thresh, rs_e5_result *out,
+                 int64_t *inliers, int64_t *n_inliers);
+
+/* ------------------------------------------------------------------------------------------
  * Batched RANSAC-F over many image pairs (config C4; fun.py:298-328 per pair)
  * ---------------------------------------------------------------------------------------- */
 typedef struct rs_pair_result {

@@ -1,0 +1,742 @@
+// Five-point essential matrix (Nister 2004) and E-RANSAC for gfx950 (SURVEY.md 8(a) row a-15;
+// no reference counterpart: parity unpinned, known answers from the reference's BAdino2 scene,
+// oracle/essential_ref.py).
+//
+// Convention of the reference (fun.py:12-21, lab3.fmatrix_residuals): y1^T E y2 = 0 for
+// C-normalised points y1 (left) and y2 (right), E = R^T [t]_x for x2 = R x1 + t; pixel
+// points x = K y, so F = K1^-T E K2^-1 satisfies x1^T F x2 = 0.
+//
+//   k_e5_solve   lane per minimal sample of 5 correspondences:
+//                  1. Q (5 x 9), row i = vec(y1_i y2_i^T); Householder LQ of its rows, null
+//                     basis {X, Y, Z, W} = H_0 .. H_4 e_{5..8}: E = x X + y Y + z Z + W;
+//                  2. the ten cubics det E = 0 and 2 E E^T E - tr(E E^T) E = 0 over the 20
+//                     monomials (Nister's order, kT3), Gauss-Jordan with partial pivoting on the
+//                     first ten columns -> [I | B];
+//                  3. k = row(x^2 z) - z row(x^2), l = row(y^2 z) - z row(y^2),
+//                     m = row(x y z) - z row(x y): linear in (x, y, 1), polynomial in z;
+//                     det [k; l; m](z) has degree 10;
+//                  4. its roots by Aberth-Ehrlich (twoview_math.h aberth_roots<10>), real ones
+//                     polished by Newton; (x, y, 1) = the null vector of [k; l; m](z) (the
+//                     row cross product with the largest third component);
+//                writes up to 10 unit-norm E per sample, their F = K1^-T E K2^-1 (NaN slots
+//                past the sample's count, so they count 0).
+//   counting     k_f8_count (f8_kernels.hip) over the S x 10 slots: the reference's residual
+//                test d = max(|r1|, |r2|) < thresh of lab3.fmatrix_residuals in pixels.
+//   k_e5_select  c* = the largest count; among the slots with c* the smallest residual norm
+//                ||d||, d_i = max(|r1_i|, |r2_i|) over all points (the quantity the
+//                reference's F loop compares on ties, fun.py:317-325), first slot on equal norms.
+//   k_e5_inliers one workgroup: the winner's consensus set in point order.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+#include "ctx.h"
+#include "device_math.h"
+#include "f8_kernels.h"
+#include "twoview_math.h"
+
+namespace rsd {
+
+// monomial products: degree-1 [x, y, z, 1] x degree-1 -> degree-2
+// [xx, xy, xz, x, yy, yz, y, zz, z, 1]; degree-2 x degree-1 -> Nister's 20 cubic monomials
+// [x3, y3, x2y, xy2, x2z, x2, y2z, y2, xyz, xy | xz2, xz, x, yz2, yz, y, z3, z2, z, 1]
+__constant__ constexpr int kT2[4][4] = {{0, 1, 2, 3}, {1, 4, 5, 6}, {2, 5, 7, 8}, {3, 6, 8, 9}};
+__constant__ constexpr int kT3[10][4] = {{0, 2, 4, 5},    {2, 3, 8, 9},    {4, 8, 10, 11},
+                                         {5, 9, 11, 12},  {3, 1, 6, 7},    {8, 6, 13, 14},
+                                         {9, 7, 14, 15},  {10, 13, 16, 17}, {11, 14, 17, 18},
+                                         {12, 15, 18, 19}};
+
+constexpr int kE5Sol = 10;  // solution slots per sample
+
+struct P1 {
+  double c[4];
+};
+struct P2 {
+  double c[10];
+};
+
+__device__ __forceinline__ P2 mul11(const P1 &a, const P1 &b) {
+  P2 r;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) r.c[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r.c[kT2[i][j]] = fma(a.c[i], b.c[j], r.c[kT2[i][j]]);
+  return r;
+}
+
+// acc += s * (a b), a of degree 2, b of degree 1
+__device__ __forceinline__ void fma21(double (&acc)[20], double s, const P2 &a, const P1 &b) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[kT3[i][j]] = fma(s * a.c[i], b.c[j], acc[kT3[i][j]]);
+}
+
+// Null basis of the 5 x 9 epipolar constraint matrix by Householder LQ (rows reduced left to
+// right); basis[j] = H_0 H_1 .. H_4 e_{5+j}, orthonormal.
+__device__ __forceinline__ void e5_null_basis(double (&A)[5][9], double (&basis)[4][9]) {
+  double tau[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    double ss = 0.0;
+#pragma unroll
+    for (int j = k; j < 9; ++j) ss = fma(A[k][j], A[k][j], ss);
+    const double nrm = sqrt(ss);
+    const double akk = A[k][k];
+    const double alpha = akk >= 0.0 ? -nrm : nrm;
+    const double denom = nrm * (nrm + fabs(akk));
+    const double tk = denom > 0.0 ? 1.0 / denom : 0.0;
+    A[k][k] = akk - alpha;
+    tau[k] = tk;
+#pragma unroll
+    for (int i = k + 1; i < 5; ++i) {
+      double w = 0.0;
+#pragma unroll
+      for (int j = k; j < 9; ++j) w = fma(A[i][j], A[k][j], w);
+      w *= tk;
+#pragma unroll
+      for (int j = k; j < 9; ++j) A[i][j] = fma(-w, A[k][j], A[i][j]);
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    double q[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) q[j] = (j == 5 + b) ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 4; k >= 0; --k) {
+      double w = 0.0;
+#pragma unroll
+      for (int j = k; j < 9; ++j) w = fma(A[k][j], q[j], w);
+      w *= tau[k];
+#pragma unroll
+      for (int j = k; j < 9; ++j) q[j] = fma(-w, A[k][j], q[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 9; ++j) basis[b][j] = q[j];
+  }
+}
+
+// The ten cubic constraints (rows 0-8: 2 E E^T E - tr(E E^T) E, row 9: det E).
+__device__ __forceinline__ void e5_constraints(const double (&basis)[4][9], double (&M)[10][20]) {
+  P1 E[9];
+#pragma unroll
+  for (int e = 0; e < 9; ++e) {
+    E[e].c[0] = basis[0][e];
+    E[e].c[1] = basis[1][e];
+    E[e].c[2] = basis[2][e];
+    E[e].c[3] = basis[3][e];
+  }
+  P2 EEt[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = i; j < 3; ++j) {
+      P2 s = mul11(E[3 * i], E[3 * j]);
+      const P2 s1 = mul11(E[3 * i + 1], E[3 * j + 1]);
+      const P2 s2 = mul11(E[3 * i + 2], E[3 * j + 2]);
+#pragma unroll
+      for (int q = 0; q < 10; ++q) s.c[q] = (s.c[q] + s1.c[q]) + s2.c[q];
+      EEt[i][j] = s;
+      EEt[j][i] = s;
+    }
+  P2 tr;
+#pragma unroll
+  for (int q = 0; q < 10; ++q) tr.c[q] = (EEt[0][0].c[q] + EEt[1][1].c[q]) + EEt[2][2].c[q];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      double acc[20];
+#pragma unroll
+      for (int q = 0; q < 20; ++q) acc[q] = 0.0;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) fma21(acc, 2.0, EEt[i][k], E[3 * k + j]);
+      fma21(acc, -1.0, tr, E[3 * i + j]);
+#pragma unroll
+      for (int q = 0; q < 20; ++q) M[3 * i + j][q] = acc[q];
+    }
+  double det[20];
+#pragma unroll
+  for (int q = 0; q < 20; ++q) det[q] = 0.0;
+  const P2 c0 = mul11(E[4], E[8]), c0b = mul11(E[5], E[7]);  // E11 E22 - E12 E21
+  const P2 c1 = mul11(E[3], E[8]), c1b = mul11(E[5], E[6]);  // E10 E22 - E12 E20
+  const P2 c2 = mul11(E[3], E[7]), c2b = mul11(E[4], E[6]);  // E10 E21 - E11 E20
+  fma21(det, 1.0, c0, E[0]);
+  fma21(det, -1.0, c0b, E[0]);
+  fma21(det, -1.0, c1, E[1]);
+  fma21(det, 1.0, c1b, E[1]);
+  fma21(det, 1.0, c2, E[2]);
+  fma21(det, -1.0, c2b, E[2]);
+#pragma unroll
+  for (int q = 0; q < 20; ++q) M[9][q] = det[q];
+}
+
+// Gauss-Jordan on the first ten columns with partial pivoting (row swaps as selects, so every
+// index stays static); returns false for a singular leading block.
+__device__ __forceinline__ bool e5_reduce(double (&M)[10][20]) {
+#pragma unroll
+  for (int c = 0; c < 10; ++c) {
+    int piv = c;
+    double best = fabs(M[c][c]);
+#pragma unroll
+    for (int r = c + 1; r < 10; ++r) {
+      const double v = fabs(M[r][c]);
+      if (v > best) {
+        best = v;
+        piv = r;
+      }
+    }
+    if (!(best > 0.0)) return false;
+#pragma unroll
+    for (int r = c + 1; r < 10; ++r) {
+      const bool sw = r == piv;
+#pragma unroll
+      for (int j = c; j < 20; ++j) {
+        const double a = M[c][j], b = M[r][j];
+        M[c][j] = sw ? b : a;
+        M[r][j] = sw ? a : b;
+      }
+    }
+    const double inv = 1.0 / M[c][c];
+#pragma unroll
+    for (int j = c + 1; j < 20; ++j) M[c][j] *= inv;
+    M[c][c] = 1.0;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+      if (r == c) continue;
+      const double f = M[r][c];
+#pragma unroll
+      for (int j = c + 1; j < 20; ++j) M[r][j] = fma(-f, M[c][j], M[r][j]);
+      M[r][c] = 0.0;
+    }
+  }
+  return true;
+}
+
+template <int A, int B>
+__device__ __forceinline__ void polymul(const double (&a)[A], const double (&b)[B],
+                                        double (&r)[A + B - 1]) {
+#pragma unroll
+  for (int i = 0; i < A + B - 1; ++i) r[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < A; ++i)
+#pragma unroll
+    for (int j = 0; j < B; ++j) r[i + j] = fma(a[i], b[j], r[i + j]);
+}
+
+// row(a) - z row(b) of the reduced system (B rows a, b; columns 10..19): coefficients of x,
+// y and 1, ascending in z
+__device__ __forceinline__ void e5_row(const double (&M)[10][20], int a, int b, double (&px)[4],
+                                       double (&py)[4], double (&p1)[5]) {
+  const double *A = &M[a][10], *Bb = &M[b][10];
+  px[0] = A[2];
+  px[1] = A[1] - Bb[2];
+  px[2] = A[0] - Bb[1];
+  px[3] = -Bb[0];
+  py[0] = A[5];
+  py[1] = A[4] - Bb[5];
+  py[2] = A[3] - Bb[4];
+  py[3] = -Bb[3];
+  p1[0] = A[9];
+  p1[1] = A[8] - Bb[9];
+  p1[2] = A[7] - Bb[8];
+  p1[3] = A[6] - Bb[7];
+  p1[4] = -Bb[6];
+}
+
+template <int N>
+__device__ __forceinline__ double horner_asc(const double (&p)[N], double z) {
+  double v = p[N - 1];
+#pragma unroll
+  for (int i = N - 2; i >= 0; --i) v = fma(v, z, p[i]);
+  return v;
+}
+
+// All real solutions of one sample; returns their number (<= 10), E row-major, unit norm.
+__device__ int e5_solve_one(const double (&y1)[5][2], const double (&y2)[5][2],
+                            double (&Es)[kE5Sol][9]) {
+  double Q[5][9];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const double a0 = y1[i][0], a1 = y1[i][1], b0 = y2[i][0], b1 = y2[i][1];
+    Q[i][0] = a0 * b0;
+    Q[i][1] = a0 * b1;
+    Q[i][2] = a0;
+    Q[i][3] = a1 * b0;
+    Q[i][4] = a1 * b1;
+    Q[i][5] = a1;
+    Q[i][6] = b0;
+    Q[i][7] = b1;
+    Q[i][8] = 1.0;
+  }
+  double basis[4][9];
+  e5_null_basis(Q, basis);
+  double M[10][20];
+  e5_constraints(basis, M);
+  if (!e5_reduce(M)) return 0;
+  double kx[4], ky[4], k1[5], lx[4], ly[4], l1[5], mx[4], my[4], m1[5];
+  e5_row(M, 4, 5, kx, ky, k1);
+  e5_row(M, 6, 7, lx, ly, l1);
+  e5_row(M, 8, 9, mx, my, m1);
+  // det [k; l; m] = kx (ly m1 - l1 my) - ky (lx m1 - l1 mx) + k1 (lx my - ly mx)
+  double t7a[8], t7b[8], t7[8], d[11], u[11];
+  polymul(ly, m1, t7a);
+  polymul(l1, my, t7b);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) t7[i] = t7a[i] - t7b[i];
+  polymul(kx, t7, d);
+  polymul(lx, m1, t7a);
+  polymul(l1, mx, t7b);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) t7[i] = t7a[i] - t7b[i];
+  polymul(ky, t7, u);
+#pragma unroll
+  for (int i = 0; i < 11; ++i) d[i] -= u[i];
+  double t6a[7], t6b[7], t6[7];
+  polymul(lx, my, t6a);
+  polymul(ly, mx, t6b);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) t6[i] = t6a[i] - t6b[i];
+  polymul(k1, t6, u);
+#pragma unroll
+  for (int i = 0; i < 11; ++i) d[i] += u[i];
+  double g[11];  // descending for aberth_roots
+#pragma unroll
+  for (int i = 0; i < 11; ++i) g[i] = d[10 - i];
+  double dp[10];  // derivative, ascending
+#pragma unroll
+  for (int i = 0; i < 10; ++i) dp[i] = (i + 1) * d[i + 1];
+  double zr[10], zi[10];
+  int trailing = 0;
+  const int deg = aberth_roots<10>(g, zr, zi, trailing);
+  int ns = 0;
+  for (int r = 0; r < deg + trailing && ns < kE5Sol; ++r) {
+    double z = r < deg ? zr[r] : 0.0;
+    if (r < deg && !(fabs(zi[r]) <= 1e-6 * fmax(1.0, fabs(z)))) continue;
+    // Newton polish on the real axis (the complex iteration may stop at its rounding floor)
+    for (int it = 0; it < 3; ++it) {
+      const double f = horner_asc(d, z), fp = horner_asc(dp, z);
+      if (!(fp != 0.0)) break;
+      const double step = f / fp;
+      if (!(fabs(step) <= 1e-3 * fmax(1.0, fabs(z)))) break;
+      z -= step;
+    }
+    const double A0[3] = {horner_asc(kx, z), horner_asc(ky, z), horner_asc(k1, z)};
+    const double A1[3] = {horner_asc(lx, z), horner_asc(ly, z), horner_asc(l1, z)};
+    const double A2[3] = {horner_asc(mx, z), horner_asc(my, z), horner_asc(m1, z)};
+    double v[3][3];
+    const double *rows[3][2] = {{A0, A1}, {A0, A2}, {A1, A2}};
+    int bi = 0;
+    double bz = -1.0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const double *a = rows[c][0], *b = rows[c][1];
+      v[c][0] = a[1] * b[2] - a[2] * b[1];
+      v[c][1] = a[2] * b[0] - a[0] * b[2];
+      v[c][2] = a[0] * b[1] - a[1] * b[0];
+      if (fabs(v[c][2]) > bz) {
+        bz = fabs(v[c][2]);
+        bi = c;
+      }
+    }
+    if (!(bz > 0.0)) continue;
+    const double x = v[bi][0] / v[bi][2], y = v[bi][1] / v[bi][2];
+    double E[9], nn = 0.0;
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+      E[e] = fma(x, basis[0][e], fma(y, basis[1][e], fma(z, basis[2][e], basis[3][e])));
+      nn = fma(E[e], E[e], nn);
+    }
+    if (!(nn > 0.0) || !isfinite(nn)) continue;
+    const double in = 1.0 / sqrt(nn);
+#pragma unroll
+    for (int e = 0; e < 9; ++e) Es[ns][e] = E[e] * in;
+    ++ns;
+  }
+  return ns;
+}
+
+struct E5Args {
+  const Pt *pts;            // pixel points (ransac) or C-normalised points (direct solve)
+  int n, S, mode;           // mode: 0 Philox samples of the n points, 1 consecutive fives
+  uint64_t seed;
+  double Kin1[9], Kin2[9];  // pixel -> normalised (K^-1), identity for the direct solve
+  double M1[9], M2[9];      // F = M1 E M2 (K1^-T, K2^-1)
+  double *Esoa;             // 9 x ld models (ld >= 10 S), NaN past the sample's count
+  double *Fsoa;             // 9 x ld (may be null)
+  int *nsol;                // per sample (may be null)
+  int64_t ld;
+};
+
+__device__ __forceinline__ void norm_pt(const double (&K)[9], double u, double v, double &x,
+                                        double &y) {
+  const double w = fma(K[6], u, fma(K[7], v, K[8]));
+  x = fma(K[0], u, fma(K[1], v, K[2])) / w;
+  y = fma(K[3], u, fma(K[4], v, K[5])) / w;
+}
+
+__global__ __launch_bounds__(64) void k_e5_solve(E5Args a) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= a.S) return;
+  int idx[5];
+  if (a.mode == 0) {
+    floyd_sample<5>(a.seed, static_cast<uint64_t>(s), a.n, idx);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) idx[i] = 5 * s + i;
+  }
+  double y1[5][2], y2[5][2];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const Pt p = a.pts[idx[i]];
+    norm_pt(a.Kin1, p.x1, p.y1, y1[i][0], y1[i][1]);
+    norm_pt(a.Kin2, p.x2, p.y2, y2[i][0], y2[i][1]);
+  }
+  double Es[kE5Sol][9];
+  const int ns = e5_solve_one(y1, y2, Es);
+  if (a.nsol) a.nsol[s] = ns;
+  const double qn = __builtin_nan("");
+  for (int j = 0; j < kE5Sol; ++j) {
+    const int64_t slot = static_cast<int64_t>(s) * kE5Sol + j;
+    double E[9];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) E[e] = j < ns ? Es[j][e] : qn;
+#pragma unroll
+    for (int e = 0; e < 9; ++e) a.Esoa[e * a.ld + slot] = E[e];
+    if (a.Fsoa) {
+      double T[9];  // E M2
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          T[3 * r + c] = fma(E[3 * r], a.M2[c], fma(E[3 * r + 1], a.M2[3 + c], E[3 * r + 2] * a.M2[6 + c]));
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          a.Fsoa[(3 * r + c) * a.ld + slot] =
+              fma(a.M1[3 * r], T[c], fma(a.M1[3 * r + 1], T[3 + c], a.M1[3 * r + 2] * T[6 + c]));
+    }
+  }
+}
+
+struct E5DevResult {
+  double E[9], F[9];
+  int64_t best_slot, best_count, n_inliers;
+  int64_t inliers[];
+};
+
+// c* = max count (one workgroup; strict ">" against 0: no consensus, no winner).
+__global__ __launch_bounds__(1024) void k_e5_max(const int *__restrict__ counts, int64_t H,
+                                                 int *cmax) {
+  __shared__ int sm[16];
+  const int tid = threadIdx.x;
+  int bm = 0;
+  for (int64_t i = tid; i < H; i += 1024) bm = max(bm, counts[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) bm = max(bm, __shfl_xor(bm, o));
+  if ((tid & 63) == 0) sm[tid >> 6] = bm;
+  __syncthreads();
+  if (tid == 0) {
+    for (int q = 1; q < 16; ++q) bm = max(bm, sm[q]);
+    *cmax = bm;
+  }
+}
+
+// ||d||^2 of every slot with count c* (lane per slot, +inf elsewhere), reference-order d_i:
+// max(|x1^T F x2| / |l1|, |x1^T F x2| / |l2|) (lab3.fmatrix_residuals, fun.py:315).
+__global__ __launch_bounds__(256) void k_e5_norms(const Pt *__restrict__ pts, int n, int64_t H,
+                                                  const int *__restrict__ counts,
+                                                  const int *__restrict__ cmax,
+                                                  const double *__restrict__ Fsoa, int64_t ld,
+                                                  double *__restrict__ norms) {
+  const int64_t h = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (h >= H) return;
+  const int c = *cmax;
+  if (c <= 0 || counts[h] != c) {
+    norms[h] = __builtin_inf();
+    return;
+  }
+  double f[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) f[q] = Fsoa[q * ld + h];
+  double ss = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const Pt p = pts[i];
+    const double l10 = fma(f[0], p.x2, fma(f[1], p.y2, f[2]));
+    const double l11 = fma(f[3], p.x2, fma(f[4], p.y2, f[5]));
+    const double l12 = fma(f[6], p.x2, fma(f[7], p.y2, f[8]));
+    const double l20 = fma(f[0], p.x1, fma(f[3], p.y1, f[6]));
+    const double l21 = fma(f[1], p.x1, fma(f[4], p.y1, f[7]));
+    const double e = fabs(fma(l10, p.x1, fma(l11, p.y1, l12)));
+    const double d = fmax(e / sqrt(fma(l10, l10, l11 * l11)), e / sqrt(fma(l20, l20, l21 * l21)));
+    ss = fma(d, d, ss);
+  }
+  norms[h] = ss == ss ? ss : __builtin_inf();
+}
+
+// The slot with count c* and the smallest norm (first on ties).
+__global__ __launch_bounds__(1024) void k_e5_select(const double *__restrict__ norms, int64_t H,
+                                                    const int *__restrict__ cmax,
+                                                    const double *__restrict__ Esoa,
+                                                    const double *__restrict__ Fsoa, int64_t ld,
+                                                    E5DevResult *res) {
+  __shared__ double sv[16];
+  __shared__ int64_t si[16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  double bv = __builtin_inf();
+  int64_t bi = INT64_MAX;
+  for (int64_t i = tid; i < H; i += 1024) {
+    const double v = norms[i];
+    if (v < bv) {
+      bv = v;
+      bi = i;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ov = __shfl_xor(bv, o);
+    const int64_t oi = __shfl_xor(bi, o);
+    if (ov < bv || (ov == bv && oi < bi)) {
+      bv = ov;
+      bi = oi;
+    }
+  }
+  if (lane == 0) {
+    sv[w] = bv;
+    si[w] = bi;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int q = 1; q < 16; ++q)
+      if (sv[q] < bv || (sv[q] == bv && si[q] < bi)) {
+        bv = sv[q];
+        bi = si[q];
+      }
+    const int c = *cmax;
+    const bool ok = c > 0 && bi != INT64_MAX;
+    res->best_slot = ok ? bi : -1;
+    res->best_count = ok ? c : 0;
+    for (int q = 0; q < 9; ++q) {
+      res->E[q] = ok ? Esoa[q * ld + bi] : 0.0;
+      res->F[q] = ok ? Fsoa[q * ld + bi] : 0.0;
+    }
+  }
+}
+
+// The winner's consensus set, in point order (the k_f8_count test in pixels).
+__global__ __launch_bounds__(1024) void k_e5_inliers(const Pt *__restrict__ pts, int n,
+                                                     double thr2, E5DevResult *res) {
+  __shared__ int woff[16];
+  __shared__ int base_s;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const bool have = res->best_slot >= 0;
+  double f[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) f[q] = res->F[q];
+  if (tid == 0) base_s = 0;
+  __syncthreads();
+  for (int b = 0; b < n; b += 1024) {
+    const int i = b + tid;
+    bool take = false;
+    if (have && i < n) {
+      const Pt p = pts[i];
+      const double l10 = fma(f[0], p.x2, fma(f[1], p.y2, f[2]));
+      const double l11 = fma(f[3], p.x2, fma(f[4], p.y2, f[5]));
+      const double l12 = fma(f[6], p.x2, fma(f[7], p.y2, f[8]));
+      const double l20 = fma(f[0], p.x1, fma(f[3], p.y1, f[6]));
+      const double l21 = fma(f[1], p.x1, fma(f[4], p.y1, f[7]));
+      const double e = fma(l10, p.x1, fma(l11, p.y1, l12));
+      const double n1 = fma(l10, l10, l11 * l11);
+      const double n2 = fma(l20, l20, l21 * l21);
+      take = e * e < thr2 * fmin(n1, n2);
+    }
+    const unsigned long long bal = __ballot(take);
+    const int before = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) woff[w] = __popcll(bal);
+    __syncthreads();
+    if (tid == 0) {
+      int acc = base_s;
+      for (int q = 0; q < 16; ++q) {
+        const int t = woff[q];
+        woff[q] = acc;
+        acc += t;
+      }
+      base_s = acc;
+    }
+    __syncthreads();
+    if (take) res->inliers[woff[w] + before] = i;
+    __syncthreads();
+  }
+  if (tid == 0) res->n_inliers = base_s;
+}
+
+}  // namespace rsd
+
+// ------------------------------------------------------------------------------------------
+using rs::fail;
+using rs::hip_fail;
+
+#define HIP_TRY(expr)                                 \
+  do {                                                \
+    hipError_t e_ = (expr);                           \
+    if (e_ != hipSuccess) return hip_fail(e_, #expr); \
+  } while (0)
+
+static size_t e5_align(size_t b) { return (b + 255) / 256 * 256; }
+
+static bool inv3(const double *K, double *Ki) {
+  const double det = K[0] * (K[4] * K[8] - K[5] * K[7]) - K[1] * (K[3] * K[8] - K[5] * K[6]) +
+                     K[2] * (K[3] * K[7] - K[4] * K[6]);
+  if (!(det != 0.0) || !std::isfinite(det)) return false;
+  const double id = 1.0 / det;
+  Ki[0] = (K[4] * K[8] - K[5] * K[7]) * id;
+  Ki[1] = (K[2] * K[7] - K[1] * K[8]) * id;
+  Ki[2] = (K[1] * K[5] - K[2] * K[4]) * id;
+  Ki[3] = (K[5] * K[6] - K[3] * K[8]) * id;
+  Ki[4] = (K[0] * K[8] - K[2] * K[6]) * id;
+  Ki[5] = (K[2] * K[3] - K[0] * K[5]) * id;
+  Ki[6] = (K[3] * K[7] - K[4] * K[6]) * id;
+  Ki[7] = (K[1] * K[6] - K[0] * K[7]) * id;
+  Ki[8] = (K[0] * K[4] - K[1] * K[3]) * id;
+  return true;
+}
+
+extern "C" int rs_e5_solve(rs_ctx *c, const double *y1, const double *y2, int64_t S,
+                           double *E_out, int32_t *nsol) {
+  if (!c || !y1 || !y2 || !E_out || !nsol) return fail(RS_EINVAL, "null pointer");
+  if (S < 1 || S > (1 << 24)) return fail(RS_EINVAL, "sample count out of range");
+  HIP_TRY(hipSetDevice(c->device));
+  const int64_t m = 5 * S, ld = rsd::kE5Sol * S;
+  std::vector<rsd::Pt> hp(static_cast<size_t>(m));
+  for (int64_t i = 0; i < m; ++i) {
+    if (!(y1[3 * i + 2] != 0.0) || !(y2[3 * i + 2] != 0.0))
+      return fail(RS_EINVAL, "homogeneous points need a nonzero third coordinate");
+    hp[i] = rsd::Pt{y1[3 * i] / y1[3 * i + 2], y1[3 * i + 1] / y1[3 * i + 2],
+                    y2[3 * i] / y2[3 * i + 2], y2[3 * i + 1] / y2[3 * i + 2]};
+  }
+  const size_t bp = e5_align(sizeof(rsd::Pt) * m), bE = e5_align(sizeof(double) * 9 * ld),
+               bn = e5_align(sizeof(int) * S);
+  int st = rs::ensure_scratch(c, bp + bE + bn);
+  if (st) return st;
+  char *base = static_cast<char *>(c->scratch);
+  auto *dp = reinterpret_cast<rsd::Pt *>(base);
+  auto *dE = reinterpret_cast<double *>(base + bp);
+  auto *dn = reinterpret_cast<int *>(base + bp + bE);
+  hipStream_t s = c->stream;
+  HIP_TRY(hipMemcpyAsync(dp, hp.data(), sizeof(rsd::Pt) * m, hipMemcpyHostToDevice, s));
+  rsd::E5Args a{};
+  a.pts = dp;
+  a.n = static_cast<int>(m);
+  a.S = static_cast<int>(S);
+  a.mode = 1;
+  const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+  std::memcpy(a.Kin1, I, sizeof(I));
+  std::memcpy(a.Kin2, I, sizeof(I));
+  std::memcpy(a.M1, I, sizeof(I));
+  std::memcpy(a.M2, I, sizeof(I));
+  a.Esoa = dE;
+  a.nsol = dn;
+  a.ld = ld;
+  hipLaunchKernelGGL(rsd::k_e5_solve, dim3((S + 63) / 64), dim3(64), 0, s, a);
+  HIP_TRY(hipGetLastError());
+  std::vector<double> soa(static_cast<size_t>(9 * ld));
+  HIP_TRY(hipMemcpyAsync(soa.data(), dE, sizeof(double) * 9 * ld, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(nsol, dn, sizeof(int) * S, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  for (int64_t q = 0; q < ld; ++q)
+    for (int e = 0; e < 9; ++e) E_out[q * 9 + e] = soa[e * ld + q];
+  return RS_OK;
+}
+
+extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64_t n,
+                            const double *K1, const double *K2, int64_t S, uint64_t seed,
+                            double thresh, rs_e5_result *out, int64_t *inliers,
+                            int64_t *n_inliers) {
+  if (!c || !p1 || !p2 || !K1 || !K2 || !out) return fail(RS_EINVAL, "null pointer");
+  if (n < 5) return fail(RS_EINVAL, "the five-point solver needs n >= 5 correspondences");
+  if (n > (1 << 26) || S < 1 || S > (1 << 24)) return fail(RS_EINVAL, "bad dimensions");
+  if (!(thresh == thresh)) return fail(RS_EINVAL, "threshold is NaN");
+  rsd::E5Args a{};
+  if (!inv3(K1, a.Kin1) || !inv3(K2, a.Kin2)) return fail(RS_EINVAL, "singular camera matrix");
+  for (int r = 0; r < 3; ++r)
+    for (int q = 0; q < 3; ++q) {
+      a.M1[3 * r + q] = a.Kin1[3 * q + r];  // K1^-T
+      a.M2[3 * r + q] = a.Kin2[3 * r + q];  // K2^-1
+    }
+  HIP_TRY(hipSetDevice(c->device));
+  const int64_t H = rsd::kE5Sol * S, ld = (H + 63) / 64 * 64;
+  const size_t bin = e5_align(sizeof(double) * 2 * n), bp = e5_align(sizeof(rsd::Pt) * n);
+  const size_t bE = e5_align(sizeof(double) * 9 * ld), bc = e5_align(sizeof(int) * ld);
+  const size_t br = e5_align(sizeof(rsd::E5DevResult) + sizeof(int64_t) * n);
+  const size_t bnorm = e5_align(sizeof(double) * ld);
+  int st = rs::ensure_scratch(c, 2 * bin + bp + 2 * bE + bc + br + bnorm + 256);
+  if (st) return st;
+  char *ptr = static_cast<char *>(c->scratch);
+  auto take = [&ptr](size_t b) {
+    char *q = ptr;
+    ptr += b;
+    return q;
+  };
+  double *d1 = reinterpret_cast<double *>(take(bin));
+  double *d2 = reinterpret_cast<double *>(take(bin));
+  auto *dp = reinterpret_cast<rsd::Pt *>(take(bp));
+  double *dE = reinterpret_cast<double *>(take(bE));
+  double *dF = reinterpret_cast<double *>(take(bE));
+  int *dc = reinterpret_cast<int *>(take(bc));
+  auto *dr = reinterpret_cast<rsd::E5DevResult *>(take(br));
+  double *dnorm = reinterpret_cast<double *>(take(bnorm));
+  int *dcmax = reinterpret_cast<int *>(take(256));
+  hipStream_t s = c->stream;
+  HIP_TRY(hipMemcpyAsync(d1, p1, sizeof(double) * 2 * n, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d2, p2, sizeof(double) * 2 * n, hipMemcpyHostToDevice, s));
+  HIP_TRY(rsd::launch_pack_points(d1, d2, static_cast<int>(n), dp, s));
+  a.pts = dp;
+  a.n = static_cast<int>(n);
+  a.S = static_cast<int>(S);
+  a.mode = 0;
+  a.seed = seed;
+  a.Esoa = dE;
+  a.Fsoa = dF;
+  a.ld = ld;
+  hipLaunchKernelGGL(rsd::k_e5_solve, dim3((S + 63) / 64), dim3(64), 0, s, a);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemsetAsync(dc, 0, sizeof(int) * H, s));
+  // chunking of k_f8_count: >= 8 units of work per SIMD, chunks of >= 64 points
+  const int64_t groups = (H + 63) / 64;
+  int64_t nch = std::max<int64_t>(1, std::min<int64_t>((8192 + groups - 1) / groups, (n + 63) / 64));
+  const int chunk = static_cast<int>((n + nch - 1) / nch);
+  HIP_TRY(rsd::launch_f8_count(dp, static_cast<int>(n), static_cast<int>(H), dF, ld, chunk,
+                               thresh * thresh, dc, s));
+  hipLaunchKernelGGL(rsd::k_e5_max, dim3(1), dim3(1024), 0, s, dc, H, dcmax);
+  hipLaunchKernelGGL(rsd::k_e5_norms, dim3((H + 255) / 256), dim3(256), 0, s, dp,
+                     static_cast<int>(n), H, dc, dcmax, dF, ld, dnorm);
+  hipLaunchKernelGGL(rsd::k_e5_select, dim3(1), dim3(1024), 0, s, dnorm, H, dcmax, dE, dF, ld,
+                     dr);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(rsd::k_e5_inliers, dim3(1), dim3(1024), 0, s, dp, static_cast<int>(n),
+                     thresh * thresh, dr);
+  HIP_TRY(hipGetLastError());
+  std::vector<char> host(sizeof(rsd::E5DevResult) + sizeof(int64_t) * n);
+  HIP_TRY(hipMemcpyAsync(host.data(), dr, host.size(), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  const auto *r = reinterpret_cast<const rsd::E5DevResult *>(host.data());
+  std::memcpy(out->E, r->E, sizeof(out->E));
+  std::memcpy(out->F, r->F, sizeof(out->F));
+  out->best_sample = r->best_slot >= 0 ? r->best_slot / rsd::kE5Sol : -1;
+  out->best_solution = r->best_slot >= 0 ? r->best_slot % rsd::kE5Sol : -1;
+  out->best_count = r->best_count;
+  if (r->best_slot >= 0 && r->n_inliers != r->best_count)
+    return fail(RS_EDEVICE, "consensus recount mismatch");
+  if (n_inliers) *n_inliers = r->best_slot >= 0 ? r->n_inliers : 0;
+  if (inliers && r->best_slot >= 0)
+    std::memcpy(inliers, r->inliers, sizeof(int64_t) * r->n_inliers);
+  return RS_OK;
+}

@@ -233,24 +233,29 @@ __device__ __forceinline__ void triangulate_linear(const double *C1, const doubl
 // A root is frozen once |p(z)| is within the rounding error of its Horner evaluation
 // (8 eps sum |a_j| |z|^j) or its correction is below 2 eps |z|; 4-11 sweeps on the goldens.
 // ----------------------------------------------------------------------------------------
-__device__ __forceinline__ int roots_real_parts(const double (&g)[7], double (&out)[6]) {
+// Generic degree-N form: g descending (g[0] the z^N coefficient).  Leading zeros lower the
+// degree, trailing zeros are roots at 0 (not iterated): returns the iterated degree `deg`,
+// with the roots in zr / zi[0 .. deg), and the number of zero roots in `trailing`.
+template <int N>
+__device__ __forceinline__ int aberth_roots(const double (&g)[N + 1], double (&zr)[N],
+                                            double (&zi)[N], int &trailing) {
+  trailing = 0;
   int lo = 0;
-  while (lo < 7 && g[lo] == 0.0) ++lo;
-  if (lo == 7) return 0;
-  int hi = 6;
+  while (lo < N + 1 && g[lo] == 0.0) ++lo;
+  if (lo == N + 1) return 0;
+  int hi = N;
   while (g[hi] == 0.0) --hi;
-  const int trailing = 6 - hi;
+  trailing = N - hi;
   const int deg = hi - lo;
-  double a[7];  // monic, descending: z^deg + a[1] z^(deg-1) + ... + a[deg]
+  double a[N + 1];  // monic, descending: z^deg + a[1] z^(deg-1) + ... + a[deg]
   for (int k = 0; k <= deg; ++k) a[k] = g[lo + k] / g[lo];
-  double zr[6], zi[6];
   if (deg > 0) {
-    double lg[7];  // log |b_k|, b_k = a[deg - k] (ascending)
+    double lg[N + 1];  // log |b_k|, b_k = a[deg - k] (ascending)
     for (int k = 0; k <= deg; ++k) {
       const double v = fabs(a[deg - k]);
       lg[k] = v > 0.0 ? log(v) : -1.0e300;
     }
-    int hull[7], nh = 0;
+    int hull[N + 1], nh = 0;
     hull[nh++] = 0;
     for (int k = 1; k <= deg; ++k) {
       if (lg[k] == -1.0e300) continue;
@@ -327,6 +332,13 @@ __device__ __forceinline__ int roots_real_parts(const double (&g)[7], double (&o
       }
     }
   }
+  return deg;
+}
+
+__device__ __forceinline__ int roots_real_parts(const double (&g)[7], double (&out)[6]) {
+  double zr[6], zi[6];
+  int trailing = 0;
+  const int deg = aberth_roots<6>(g, zr, zi, trailing);
   for (int k = 0; k < deg; ++k) out[k] = zr[k];
   for (int k = 0; k < trailing; ++k) out[deg + k] = 0.0;
   return deg + trailing;

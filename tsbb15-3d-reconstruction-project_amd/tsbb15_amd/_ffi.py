@@ -52,6 +52,11 @@ class PairResult(C.Structure):
                 ("n_candidates", C.c_int64)]
 
 
+class E5Result(C.Structure):
+    _fields_ = [("E", C.c_double * 9), ("F", C.c_double * 9), ("best_sample", C.c_int64),
+                ("best_solution", C.c_int64), ("best_count", C.c_int64)]
+
+
 class GsInfo(C.Structure):
     _fields_ = [("cost_init", C.c_double), ("cost", C.c_double), ("iterations", C.c_int32),
                 ("accepted", C.c_int32), ("status", C.c_int32), ("n", C.c_int32)]
@@ -103,6 +108,9 @@ _SIGS = {
     "rs_pnp_ransac_cv": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, C.c_int64, C.c_uint64,
                                    C.c_double, C.c_double, C.c_int32, C.POINTER(PnpResult),
                                    _i64p, _i64p, _i64p]),
+    "rs_e5_solve": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, _i32p]),
+    "rs_e5_ransac": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, _dp, C.c_int64, C.c_uint64,
+                               C.c_double, C.POINTER(E5Result), _i64p, _i64p]),
     "rs_pairs_f8_ransac": (C.c_int, [C.c_void_p, _dp, _dp, _i64p, C.c_int64, C.c_int64,
                                      C.c_int32, C.c_uint64, _i64p, _i32p, C.c_double,
                                      C.POINTER(PairResult), _i32p]),
