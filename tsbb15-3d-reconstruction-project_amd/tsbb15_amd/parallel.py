@@ -328,7 +328,9 @@ def run_pairs(comm, pairs, H, solve, refine=None):
     items = [(i, F, pl_inliers, pr_inliers, first p1 point, first p2 point)], returns per item
     (F_gold[9], gs_cost, pose found, R[9], t[3]) for all of the rank's valid pairs at once.
     Returns the PAIR_DTYPE table of every pair, identical on every rank, after one
-    all-gather of fixed-size records."""
+    all-gather in which each rank sends only the records of the pairs it owns (padded to the
+    largest owner list, as an all-gather needs equal sizes; every rank derives the same
+    owner lists from the costs)."""
     costs = [p1.shape[1] * H if p1.shape[1] >= 8 else 0 for p1, _ in pairs]
     owners = lpt_assign(costs, comm.world)
     recs = np.zeros(len(pairs), dtype=PAIR_DTYPE)
@@ -363,11 +365,15 @@ def run_pairs(comm, pairs, H, solve, refine=None):
         recs["pose"][idx] = [r[2] for r in ref]
         recs["R"][idx] = np.stack([np.asarray(r[3], dtype=np.float64).ravel() for r in ref])
         recs["t"][idx] = np.stack([np.asarray(r[4], dtype=np.float64).ravel() for r in ref])
-    parts = comm.allgather_bytes(recs.tobytes())
+    width = max(len(o) for o in owners)
+    send = np.zeros(width, dtype=PAIR_DTYPE)
+    own = np.asarray(owners[comm.rank], dtype=np.int64)
+    send[:len(own)] = recs[own]
+    parts = comm.allgather_bytes(send.tobytes())
     table = np.zeros(len(pairs), dtype=PAIR_DTYPE)
     for r, p in enumerate(parts):
         a = np.frombuffer(p, dtype=PAIR_DTYPE)
-        table[owners[r]] = a[owners[r]]
+        table[np.asarray(owners[r], dtype=np.int64)] = a[:len(owners[r])]
     table["pair"] = np.arange(len(pairs))
     table["best_index"][table["valid"] == 0] = -1
     return table
