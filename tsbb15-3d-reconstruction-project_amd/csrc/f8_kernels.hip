@@ -217,9 +217,12 @@ __global__ __launch_bounds__(256) void k_f8_count(const Pt *__restrict__ pts, in
 // cut into W equal contiguous slices (a multiple of 8 points), one per wave; a slice that
 // crosses a group boundary runs as two segments, each with its own model load and one
 // coalesced count atomic.  W is a multiple of the resident wave count (6 per SIMD), so every
-// wave slot runs the same number of slices.  Measured and not kept: claiming chunks from
-// per-XCD atomic head words (0.13-0.19 ms per C2 launch instead of ~0.1: a returning
-// device-scope atomic per chunk queues behind thousands of pullers).
+// wave slot runs the same number of slices.  Waves of equal work still finish up to 2.5x
+// apart (wave timeline, tools/count_timeline.py: not re-tests, not XCD, not SIMD occupancy),
+// which is the launch's drain.  Measured and not kept: claiming chunks from per-XCD atomic
+// head words (0.13-0.19 ms per C2 launch instead of ~0.1: a returning device-scope atomic per
+// chunk queues behind thousands of pullers), 64 / 128-thread workgroups (same), and
+// progress-levelled s_setprio (same durations).
 // ----------------------------------------------------------------------------------------
 
 // The float64 test of k_f8_count (pixel units) for one (hypothesis, point).
@@ -313,8 +316,7 @@ __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ p
                                                      const Pt *__restrict__ pts, int n, int H,
                                                      const float *__restrict__ F32soa,
                                                      const double *__restrict__ Fsoa,
-                                                     int64_t ld, int64_t per_wave, int prio,
-                                                     GuardW g,
+                                                     int64_t ld, int64_t per_wave, GuardW g,
                                                      int *__restrict__ counts,
                                                      int *__restrict__ gdone,
                                                      int *__restrict__ status,
@@ -330,13 +332,6 @@ __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ p
   uint64_t *ts = g_count_ts;  // diagnostic wave timeline (RSAMD_TSTAMP), null in production
   const uint64_t t_start = ts ? __builtin_amdgcn_s_memrealtime() : 0ull;
   int n_retest = 0;  // re-test branches taken (timeline diagnostics)
-  // progress-levelled issue priority: the arbiter serves the highest priority, then the
-  // oldest wave, so waves of equal work otherwise finish up to 2.5x apart; a wave that is
-  // ahead steps its priority down at 1/4, 1/2 and 3/4 of its slice
-  const int64_t wbeg = pos;
-  int64_t next_step = prio ? wbeg + (end - wbeg) / 4 : INT64_MAX;
-  int level = 3;
-  if (prio) __builtin_amdgcn_s_setprio(3);
   while (pos < end) {
     const int grp = static_cast<int>(pos / npad);
     const int p0 = static_cast<int>(pos - static_cast<int64_t>(grp) * npad);
@@ -354,15 +349,7 @@ __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ p
     const float4 q = G4[hl];
     const f2 KIO = {q.x, q.y}, ALB = {q.z, q.w};
     int cnt = 0;
-    const int64_t seg0 = pos - (p1 - p0) - p0;  // plane position of point 0 of this group
     for (int i = p0; i < p1; i += 8) {
-      if (seg0 + i >= next_step) {
-        --level;
-        if (level == 2) __builtin_amdgcn_s_setprio(2);
-        else if (level == 1) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-        next_step = level > 0 ? wbeg + (end - wbeg) * (4 - level) / 4 : INT64_MAX;
-      }
       float4 blk[8];  // (x2[8], y2[8], x1[8], y1[8]) of points i..i+7
 #pragma unroll
       for (int k = 0; k < 8; ++k) blk[k] = ptsq[i + k];
@@ -943,8 +930,7 @@ int count32q_resident_waves(int device) {
   return cus * 4 * 6;
 }
 
-Count32qShape count32q_shape(int n, int H, int waves, int slices_per_wave, int block_threads,
-                            int prio) {
+Count32qShape count32q_shape(int n, int H, int waves, int slices_per_wave) {
   Count32qShape sh{};
   const int64_t npad = (n + 7) / 8 * 8;
   const int64_t total = static_cast<int64_t>((H + 63) / 64) * npad;
@@ -956,10 +942,7 @@ Count32qShape count32q_shape(int n, int H, int waves, int slices_per_wave, int b
   per = (per + 7) / 8 * 8;
   W = (total + per - 1) / per;
   sh.per_wave = per;
-  sh.prio = prio;
-  sh.block_threads = block_threads == 64 || block_threads == 128 ? block_threads : 256;
-  const int64_t wpb = sh.block_threads / 64;
-  sh.blocks = (W + wpb - 1) / wpb;
+  sh.blocks = (W + 3) / 4;
   return sh;
 }
 
@@ -967,17 +950,9 @@ hipError_t launch_f8_count32q(const float4 *ptsq, const Pt *pts, int n, int H,
                               const float *F32soa, const double *Fsoa, int64_t ld,
                               const Count32qShape &sh, const GuardW &g, int *counts,
                               hipStream_t s, int *gdone, int *status, const float4 *G4) {
-#define RSD_Q_LAUNCH(BT)                                                                       \
-  hipLaunchKernelGGL((k_f8_count32q<BT>), dim3(static_cast<unsigned>(sh.blocks)), dim3(BT), 0, s, \
-                     ptsq, pts, n, H, F32soa, Fsoa, ld, sh.per_wave, sh.prio, g, counts, gdone,   \
-                     status, G4)
-  if (sh.block_threads == 64)
-    RSD_Q_LAUNCH(64);
-  else if (sh.block_threads == 128)
-    RSD_Q_LAUNCH(128);
-  else
-    RSD_Q_LAUNCH(256);
-#undef RSD_Q_LAUNCH
+  hipLaunchKernelGGL((k_f8_count32q<256>), dim3(static_cast<unsigned>(sh.blocks)), dim3(256), 0,
+                     s, ptsq, pts, n, H, F32soa, Fsoa, ld, sh.per_wave, g, counts, gdone, status,
+                     G4);
   return hipGetLastError();
 }
 
