@@ -489,7 +489,7 @@ def main():
                      "note": "vector-ALU (issue) bound, SURVEY.md 8(d): 42 flop per "
                              "(hypothesis, correspondence) algorithmic; HBM traffic per launch "
                              "from rocprofv3 PMC in profiles/ (traffic, bytes)"},
-        "kernels_ms": {"k_f8_count": c_ms, "k_f8_solve": km["solve_ms"],
+        "kernels_ms": {"k_f8_count32q": c_ms, "k_f8_solve": km["solve_ms"],
                        "run_device_total": km["total_ms"]},
     }
     if pmc:

@@ -14,8 +14,11 @@ echo "pytest_gpu exit $?" | tee -a $OUT/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo smoke failed; exit 1; }
 timeout -k 10 400 python bench.py --steps $STEPS --warmup 200 > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; exit 1; }
 cat $OUT/bench.json
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 bench.py --steps $STEPS --warmup 200 --no-cpu-baseline --no-parity-mode --no-extras > $OUT/prof_bench.log 2>&1 || { echo rocprof failed; exit 1; }
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o pmc -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-parity-mode --no-extras > $OUT/pmc_fetch.log 2>&1 || { echo pmc fetch failed; exit 1; }
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o pmc -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-parity-mode --no-extras > $OUT/pmc_write.log 2>&1 || { echo pmc write failed; exit 1; }
-timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $OUT/pmc_sq -o pmc -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-parity-mode --no-extras > $OUT/pmc_sq.log 2>&1 || echo "pmc sq failed"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 bench.py --steps $STEPS --warmup 200 --no-cpu-baseline --no-extras > $OUT/prof_bench.log 2>&1 || { echo rocprof failed; exit 1; }
+# PMC passes on a warmed, clock-ramped run (200 warm-up launches, 50 counted), one pass per
+# counter block (MI355X_MICROARCH.md: FETCH_SIZE alone, WRITE_SIZE alone)
+B="python3 bench.py --steps 50 --warmup 200 --no-cpu-baseline --no-parity-mode --no-extras --no-fp64-count"
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o pmc -- $B > $OUT/pmc_fetch.log 2>&1 || { echo pmc fetch failed; exit 1; }
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_write -o pmc -- $B > $OUT/pmc_write.log 2>&1 || { echo pmc write failed; exit 1; }
+timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU_FMA_F64 --output-format csv -d $OUT/pmc_sq -o pmc -- $B > $OUT/pmc_sq.log 2>&1 || echo "pmc sq failed"
 find $OUT -name "*.csv" | head -50

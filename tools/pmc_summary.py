@@ -15,13 +15,17 @@ import shutil
 import sys
 from collections import defaultdict
 
-KERNEL = "k_f8_count32"
+KERNEL = "k_f8_count32q"
+# v_fma_f64 per executed float64 re-test (test64, one per ambiguous point of a pair; the
+# kernel's only float64 FMAs, counted in its ISA)
+FMA64_PER_RETEST = 10
 
 
 def per_launch(path, kernel):
     vals = defaultdict(list)
     for r in csv.DictReader(open(path)):
-        if kernel in r["Kernel_Name"]:
+        if r["Kernel_Name"].split("(")[0].split("<")[0].endswith(kernel) or \
+                r["Kernel_Name"].startswith(kernel + "<"):
             vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
 
@@ -55,10 +59,16 @@ def main():
         "hbm_bytes_per_launch": fetch + write,
         "hbm_bytes_per_launch_fetch_x2_upper": 2 * fetch + write,
         "kernel_stats_avg_ns": next((v["avg_ns"] for k, v in stats.items() if KERNEL in k), None),
-        "bench_hip_event_avg_ms": bench["kernels_ms"]["k_f8_count"],
+        "bench_hip_event_avg_ms": bench["kernels_ms"].get("k_f8_count32q",
+                                                          bench["kernels_ms"].get("k_f8_count")),
         "valu_insts_per_wave_point": (counters.get("SQ_INSTS_VALU", 0.0) /
                                       (bench["config"]["hypotheses_per_step"] *
                                        bench["config"]["n_corr"] / 64.0)),
+        "retests_per_launch_est": counters.get("SQ_INSTS_VALU_FMA_F64", 0.0) / FMA64_PER_RETEST,
+        "ambiguous_pair_rate_est": (counters.get("SQ_INSTS_VALU_FMA_F64", 0.0) / FMA64_PER_RETEST /
+                                    (bench["config"]["hypotheses_per_step"] / 64.0 *
+                                     bench["config"]["n_corr"] / 2.0)),
+        "pmc_run": "50 counted launches after 200 warm-up launches (clock ramped)",
         "source": f"rocprofv3 --pmc passes of bench.py (tools/gpu_round.sh), {src}",
     }
     with open(os.path.join(prof, f"{tag}_pmc_k_f8_count.json"), "w") as f:
