@@ -720,6 +720,7 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_np_track(EntryArgs a,
   __shared__ int s_m, s_evn;
   constexpr int kPer = kCheck / (64 * kTrackWaves);  // draws per thread per interval
   const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = uni(tid >> 6);
+  const int wq = wv;  // (rotating the busy wave across SIMDs by chunk: measured, no change)
   int m = a.fin_m[c];
   if (m > 64) return;  // the chunk ended while dense: final already
   const int n1 = a.n1;
@@ -761,19 +762,19 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_np_track(EntryArgs a,
     }
     // this wave's trajectories q = wv, wv + 8, ... advance together (independent fixed-point
     // chains interleaved: the latency of one round is shared by up to kTrackSlots of them)
-    const int nq = m > wv ? (m - wv + kTrackWaves - 1) / kTrackWaves : 0;
+    const int nq = m > wq ? (m - wq + kTrackWaves - 1) / kTrackWaves : 0;
 #ifdef RSAMD_DIAG
     const long long c0 = __builtin_amdgcn_s_memtime();
 #endif
     if (nq == 1) {
       const uint32_t i1 = track_one<PY, SMALL>(
-          a, sw, &s_evn, ev, uni(s_st[wv]), uni(s_lo[wv] | (s_lo[wv + 1 == m ? 0 : wv + 1] << 16)),
+          a, sw, &s_evn, ev, uni(s_st[wq]), uni(s_lo[wq] | (s_lo[wq + 1 == m ? 0 : wq + 1] << 16)),
           t, cp);
-      if (lane == 0) s_st[wv] = i1;
+      if (lane == 0) s_st[wq] = i1;
     }
-    else if (nq == 2) track_interval<2, PY, SMALL>(a, sw, s_st, s_lo, &s_evn, ev, m, wv, 2, t, cp, dg);
-    else if (nq > 2 && nq <= 4) track_interval<4, PY, SMALL>(a, sw, s_st, s_lo, &s_evn, ev, m, wv, nq, t, cp, dg);
-    else if (nq > 4) track_interval<8, PY, SMALL>(a, sw, s_st, s_lo, &s_evn, ev, m, wv, nq, t, cp, dg);
+    else if (nq == 2) track_interval<2, PY, SMALL>(a, sw, s_st, s_lo, &s_evn, ev, m, wq, 2, t, cp, dg);
+    else if (nq > 2 && nq <= 4) track_interval<4, PY, SMALL>(a, sw, s_st, s_lo, &s_evn, ev, m, wq, nq, t, cp, dg);
+    else if (nq > 4) track_interval<8, PY, SMALL>(a, sw, s_st, s_lo, &s_evn, ev, m, wq, nq, t, cp, dg);
 #ifdef RSAMD_DIAG
     {
       const long long dc = __builtin_amdgcn_s_memtime() - c0;  // busy cycles of this wave
