@@ -292,12 +292,38 @@ def extras(ctx, rank, world, dist, comm):
         el, _ = _best_of(getf, 3)
         out["getFFromLabCode_dino_noisy"] = {
             "ms": el * 1e3, "n_corr": int(c1["noisy_p1"].shape[1]), "iterations": 10_000,
-            "note": "drop-in end to end: numpy-exact sampling on the GPU, GPU RANSAC, GPU gold "
-                    "standard; the reference took {:.1f} s for the same call in the build "
-                    "container (tests/golden/dino_c1.npz noisy_full_seconds)".format(
+            "gold_standard": fun.GOLD_STANDARD,
+            "note": "drop-in end to end: numpy-exact sampling on the GPU, GPU RANSAC, the "
+                    "reference's scipy TRF gold standard over GPU residuals / Jacobian; the "
+                    "reference took {:.1f} s for the same call in the build container "
+                    "(tests/golden/dino_c1.npz noisy_full_seconds)".format(
                         float(c1["noisy_full_seconds"]))}
+        saved = fun.GOLD_STANDARD
+        try:
+            fun.GOLD_STANDARD = "lm"
+            getf()
+            el, _ = _best_of(getf, 3)
+        finally:
+            fun.GOLD_STANDARD = saved
+        out["getFFromLabCode_dino_noisy_lm"] = {
+            "ms": el * 1e3, "gold_standard": "lm",
+            "note": "the same call with the converged GPU Levenberg-Marquardt gold standard"}
     except Exception as e:  # noqa: BLE001
         out["gold_standard_c2"] = {"error": repr(e)}
+    # ---- five-point E-RANSAC on the C2 pair (a-15; no reference counterpart) ------------
+    try:
+        from tsbb15_amd import essential
+        p1, p2, _ = synth.two_view(N_CORR, OUTLIERS, seed=1)
+        S = 20_000
+        essential.ransac_e(p1, p2, synth.K_SYNTH, samples=S, seed=1)
+        el, r = _best_of(lambda: essential.ransac_e(p1, p2, synth.K_SYNTH, samples=S, seed=1), 3)
+        out["e5_ransac_c2"] = {"metric": "five-point E-RANSAC minimal samples/s", "value": S / el,
+                               "ms": el * 1e3, "samples": S, "hypotheses": 10 * S,
+                               "consensus": r.count,
+                               "note": "k_e5_solve (all real roots of each sample) + k_f8_count "
+                                       "over 10 slots per sample + selection, N = 2000"}
+    except Exception as e:  # noqa: BLE001
+        out["e5_ransac_c2"] = {"error": repr(e)}
     # ---- per-view table steps (tables.py:116-175, 260-380) at the reference's noisy sizes ----
     try:
         from tsbb15_amd import tables as gt

@@ -111,3 +111,39 @@ def test_two_view_pairs_pipeline(ctx):
         assert np.abs(g.t + tt / np.linalg.norm(tt)).max() < 1e-6
         n_ok += 1
     assert n_ok == 203
+
+
+def test_tuple_mode_matches_oracle_dino_ring(ctx):
+    """The Dino ring (C4's pair set) against the oracle restatement, not against the per-pair
+    plans: every 14th of the ring's pairs with >= 8 correspondences (and one with 7), with
+    0.5 px noise and 20 % of the correspondences replaced by random points (seeded),
+    numpy-exact streams np.random.seed(2000 + pair)."""
+    ring = _dino_pairs()
+    valid = [k for k, (a, _) in enumerate(ring) if a.shape[1] >= 8]
+    small = [k for k, (a, _) in enumerate(ring) if a.shape[1] == 7][:1]
+    rs = np.random.RandomState(17)
+    pairs, seeds = [], []
+    for k in valid[::14] + small:
+        p1, p2 = (a.astype(np.float64).copy() for a in ring[k])
+        n = p1.shape[1]
+        p1 += rs.normal(0, 0.5, p1.shape)
+        p2 += rs.normal(0, 0.5, p2.shape)
+        out = rs.rand(n) < 0.2
+        p2[:, out] = rs.uniform(0, 700, (2, int(out.sum())))
+        pairs.append((p1, p2))
+        seeds.append(2000 + k)
+    H = 400
+    tup = P.np_tuples_pairs([p.shape[1] for p, _ in pairs], H, seeds)
+    rr = P.ransac_pairs(pairs, H, tuples=tup, ctx=ctx)
+    checked = 0
+    for k, (p1, p2) in enumerate(pairs):
+        if p1.shape[1] < 8:
+            assert rr[k].best_index == -1
+            continue
+        F, S, d, best, _ = ransac_ref.ransac_f(p1, p2, r=H, rng=np.random.RandomState(seeds[k]))
+        assert rr[k].best_index == best, k
+        assert np.array_equal(rr[k].inliers, S), k
+        np.testing.assert_allclose(ransac_ref.normalize_F(rr[k].F), ransac_ref.normalize_F(F),
+                                   atol=1e-9)
+        checked += 1
+    assert checked >= 10
