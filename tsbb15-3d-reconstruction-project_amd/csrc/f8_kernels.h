@@ -83,11 +83,10 @@ hipError_t launch_pack_points32q(const Pt *pts, int n, const Frame &fr, float4 *
                                  hipStream_t s);
 struct Count32qShape {
   int64_t per_wave;  // points of the (group, point) plane per wave (a multiple of 8)
-  int tile;          // > 0: tile-major cells (point tile x group), this many points each
   int64_t blocks;    // 256-thread workgroups launched
 };
 int count32q_resident_waves(int device);
-Count32qShape count32q_shape(int n, int H, int waves, int slices_per_wave = 0, int tiled = 1);
+Count32qShape count32q_shape(int n, int H, int waves, int slices_per_wave = 0);
 hipError_t launch_f8_count32q(const float4 *ptsq, const Pt *pts, int n, int H,
                               const float *F32soa, const double *Fsoa, int64_t ld,
                               const Count32qShape &sh, const GuardW &g, int *counts,

@@ -221,8 +221,10 @@ __global__ __launch_bounds__(256) void k_f8_count(const Pt *__restrict__ pts, in
 // apart (wave timeline, tools/count_timeline.py: not re-tests, not XCD, not SIMD occupancy),
 // which is the launch's drain.  Measured and not kept: claiming chunks from per-XCD atomic
 // head words (0.13-0.19 ms per C2 launch instead of ~0.1: a returning device-scope atomic per
-// chunk queues behind thousands of pullers), 64 / 128-thread workgroups (same), and
-// progress-levelled s_setprio (same durations).
+// chunk queues behind thousands of pullers), 64 / 128-thread workgroups (same),
+// progress-levelled s_setprio (same durations), and tile-major cells (a point tile x one
+// hypothesis group per wave, so a workgroup's waves share scalar-cache lines: 0.108 vs 0.0995
+// ms, slower ramp).  The scalar data cache misses 62 % of the point loads (PMC SQC_DCACHE_*).
 // ----------------------------------------------------------------------------------------
 
 // The float64 test of k_f8_count (pixel units) for one (hypothesis, point).
@@ -316,8 +318,7 @@ __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ p
                                                      const Pt *__restrict__ pts, int n, int H,
                                                      const float *__restrict__ F32soa,
                                                      const double *__restrict__ Fsoa,
-                                                     int64_t ld, int64_t per_wave, int tile,
-                                                     GuardW g,
+                                                     int64_t ld, int64_t per_wave, GuardW g,
                                                      int *__restrict__ counts,
                                                      int *__restrict__ gdone,
                                                      int *__restrict__ status,
@@ -327,18 +328,9 @@ __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ p
   const int lane = threadIdx.x & 63;
   const int64_t w = wave_uniform(blockIdx.x * (BT / 64) + (threadIdx.x >> 6));
   const int npad = (n + 7) / 8 * 8;
-  const int G = (H + 63) >> 6;
-  const int64_t total = static_cast<int64_t>(G) * npad;
-  int64_t pos, end;
-  if (tile > 0) {  // tile-major: wave w = cell (point tile w / G, group w % G)
-    const int tl = static_cast<int>(w / G), grp = static_cast<int>(w - static_cast<int64_t>(tl) * G);
-    const int p0 = tl * tile;
-    pos = static_cast<int64_t>(grp) * npad + p0;
-    end = p0 < npad ? pos + min(tile, npad - p0) : pos;
-  } else {  // group-major: a contiguous range of the flattened (group, point) plane
-    pos = w * per_wave;
-    end = min(total, pos + per_wave);
-  }
+  const int64_t total = static_cast<int64_t>((H + 63) >> 6) * npad;
+  int64_t pos = w * per_wave;
+  const int64_t end = min(total, pos + per_wave);
   uint64_t *ts = g_count_ts;  // diagnostic wave timeline (RSAMD_TSTAMP), null in production
   const uint64_t t_start = ts ? __builtin_amdgcn_s_memrealtime() : 0ull;
   int n_retest = 0;  // re-test branches taken (timeline diagnostics)
@@ -940,29 +932,17 @@ int count32q_resident_waves(int device) {
   return cus * 4 * 6;
 }
 
-Count32qShape count32q_shape(int n, int H, int waves, int slices_per_wave, int tiled) {
+Count32qShape count32q_shape(int n, int H, int waves, int slices_per_wave) {
   Count32qShape sh{};
   const int64_t npad = (n + 7) / 8 * 8;
-  const int64_t G = (H + 63) / 64;
-  const int64_t total = G * npad;
-  // slices_per_wave x the resident waves (2 by default), at least 64 points each, a multiple
-  // of 8 points
+  const int64_t total = static_cast<int64_t>((H + 63) / 64) * npad;
+  // slices_per_wave x the resident waves (2 by default: A/B on C2 in r01 and r02, 2x ahead
+  // of 1x, 2.67x and 5.3x by 1-6 %), at least 64 points each, a multiple of 8 points
   const int64_t k = slices_per_wave > 0 ? slices_per_wave : 2;
-  if (tiled) {
-    // tile-major cells: T tiles of P points, G x T ~ k x the resident waves
-    int64_t T = std::max<int64_t>(1, std::min<int64_t>((k * waves + G / 2) / G, npad / 64));
-    const int64_t P = ((npad + T - 1) / T + 7) / 8 * 8;
-    T = (npad + P - 1) / P;
-    sh.tile = static_cast<int>(P);
-    sh.per_wave = P;
-    sh.blocks = (G * T + 3) / 4;
-    return sh;
-  }
   int64_t W = std::max<int64_t>(1, std::min<int64_t>(k * waves, total / 64));
   int64_t per = (total + W - 1) / W;
   per = (per + 7) / 8 * 8;
   W = (total + per - 1) / per;
-  sh.tile = 0;
   sh.per_wave = per;
   sh.blocks = (W + 3) / 4;
   return sh;
@@ -973,8 +953,8 @@ hipError_t launch_f8_count32q(const float4 *ptsq, const Pt *pts, int n, int H,
                               const Count32qShape &sh, const GuardW &g, int *counts,
                               hipStream_t s, int *gdone, int *status, const float4 *G4) {
   hipLaunchKernelGGL((k_f8_count32q<256>), dim3(static_cast<unsigned>(sh.blocks)), dim3(256), 0,
-                     s, ptsq, pts, n, H, F32soa, Fsoa, ld, sh.per_wave, sh.tile, g, counts, gdone,
-                     status, G4);
+                     s, ptsq, pts, n, H, F32soa, Fsoa, ld, sh.per_wave, g, counts, gdone, status,
+                     G4);
   return hipGetLastError();
 }
 
