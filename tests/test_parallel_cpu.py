@@ -221,3 +221,23 @@ def test_gloo_pair_pipeline_refined_equals_single_process():
         assert row["refined"] == 1 and row["pose"] == found
         np.testing.assert_array_equal(row["F_gold"], Fg)
         np.testing.assert_array_equal(row["R"], R)
+
+
+def _fileboot_worker(d, rank, q):
+    from tsbb15_amd import parallel
+    got = parallel.FileBoot(d, rank, timeout=30).broadcast_bytes(b"id-%d" % 7 if rank == 0 else b"")
+    q.put((rank, got))
+
+
+def test_fileboot_broadcasts_the_id(tmp_path):
+    """The torch-free RCCL bootstrap: rank 0's bytes reach every rank through the directory."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_fileboot_worker, args=(str(tmp_path), r, q)) for r in (2, 1, 0)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=60) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert out == {0: b"id-7", 1: b"id-7", 2: b"id-7"}

@@ -19,7 +19,8 @@ Two shardings:
 
 Communicators: :class:`RcclComm` (librsamd, device buffers, xGMI) on GPUs and
 :class:`TorchComm` (torch.distributed, e.g. gloo on the CPU) for tests; both expose
-``allgather_bytes`` and ``allreduce_max_int``.
+``allgather_bytes`` and ``allreduce_max_int``.  RcclComm needs only a one-off broadcast of
+its unique id: a TorchComm, or :class:`FileBoot` (a shared directory) without torch.
 """
 from __future__ import annotations
 
@@ -65,6 +66,35 @@ class TorchComm:
         obj = [b]
         self.dist.broadcast_object_list(obj, src=src, group=self.group)
         return obj[0]
+
+
+class FileBoot:
+    """Bootstrap without torch.distributed: rank 0 publishes a byte string (the RCCL unique
+    id) as a file in a directory every rank can see (written to a temporary name, then
+    renamed, so readers never see a partial file); the others poll for it.  Pass it as
+    ``RcclComm(ctx, rank, world, boot=FileBoot(path, rank))``."""
+
+    def __init__(self, directory, rank, timeout=60.0, name="rsamd_comm_id"):
+        import os
+        self.path = os.path.join(directory, name)
+        self.rank, self.timeout = int(rank), float(timeout)
+
+    def broadcast_bytes(self, b, src=0):
+        import os
+        import time
+        if self.rank == src:
+            tmp = f"{self.path}.{os.getpid()}.tmp"
+            with open(tmp, "wb") as f:
+                f.write(bytes(b))
+            os.replace(tmp, self.path)
+            return bytes(b)
+        t0 = time.monotonic()
+        while not os.path.exists(self.path):
+            if time.monotonic() - t0 > self.timeout:
+                raise TimeoutError(f"no communicator id at {self.path} after {self.timeout} s")
+            time.sleep(0.01)
+        with open(self.path, "rb") as f:
+            return f.read()
 
 
 class RcclComm:
