@@ -83,7 +83,6 @@ hipError_t launch_pack_points32q(const Pt *pts, int n, const Frame &fr, float4 *
                                  hipStream_t s);
 struct Count32qShape {
   int64_t per_wave;  // points of the (group, point) plane per wave (a multiple of 8)
-  bool lds_points;   // stage the points through an LDS tile per wave (VGPR operands)
   int64_t blocks;    // 256-thread workgroups launched
 };
 int count32q_resident_waves(int device);

@@ -224,7 +224,9 @@ __global__ __launch_bounds__(256) void k_f8_count(const Pt *__restrict__ pts, in
 // chunk queues behind thousands of pullers), 64 / 128-thread workgroups (same),
 // progress-levelled s_setprio (same durations), and tile-major cells (a point tile x one
 // hypothesis group per wave, so a workgroup's waves share scalar-cache lines: 0.108 vs 0.0995
-// ms, slower ramp).  The scalar data cache misses 62 % of the point loads (PMC SQC_DCACHE_*).
+// ms, slower ramp).  The scalar data cache misses 62 % of the point loads (PMC SQC_DCACHE_*),
+// yet staging each wave's points through an LDS tile (broadcast ds_read_b128 into VGPR
+// operands, 80 SGPRs / 62 VGPRs, 8 waves per SIMD) was slower too (0.104-0.106 ms).
 // ----------------------------------------------------------------------------------------
 
 // The float64 test of k_f8_count (pixel units) for one (hypothesis, point).
@@ -266,8 +268,6 @@ typedef float f2q __attribute__((ext_vector_type(2)));
 // The terms of one point pair (expressions and order as documented above); P01 = (F0, F1),
 // P23 = (F2, F3), P45 = (F4, F5), P67 = (F6, F7), P8 = (F8, F8), KIO = (ki, -ko),
 // ALB = (alpha, beta).
-// VPTS: the point pairs come from VGPRs (LDS-staged) instead of SGPRs.
-template <bool VPTS>
 __device__ __forceinline__ void pair_terms(f2q P01, f2q P23, f2q P45, f2q P67, f2q P8, f2q KIO,
                                            f2q ALB, f2q X2, f2q Y2, f2q X1, f2q Y1, f2q &P,
                                            f2q &Q, f2q &R, f2q &S) {
@@ -279,29 +279,6 @@ __device__ __forceinline__ void pair_terms(f2q P01, f2q P23, f2q P45, f2q P67, f
   // t2 = F7 y2 + F8 -> l3 -> b y1 + l3 -> e, t3 = F3 y1 + F6 -> c -> Q, t4 = F4 y1 + F7 -> d ->
   // d^2 -> n2.
   f2q t0, t1, t2, t3, t4;
-  if constexpr (VPTS) {
-  asm("v_pk_fma_f32 %[t0], %[P01], %[Y2], %[P23] op_sel:[1,0,0] op_sel_hi:[1,1,0]\n\t"
-      "v_pk_fma_f32 %[t1], %[P45], %[Y2], %[P45] op_sel:[0,0,1] op_sel_hi:[0,1,1]\n\t"
-      "v_pk_fma_f32 %[t2], %[P67], %[Y2], %[P8] op_sel:[1,0,0] op_sel_hi:[1,1,0]\n\t"
-      "v_pk_fma_f32 %[t3], %[P23], %[Y1], %[P67] op_sel:[1,0,0] op_sel_hi:[1,1,0]\n\t"
-      "v_pk_fma_f32 %[t4], %[P45], %[Y1], %[P67] op_sel:[0,0,1] op_sel_hi:[0,1,1]\n\t"
-      "v_pk_fma_f32 %[t0], %[P01], %[X2], %[t0] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"  // a
-      "v_pk_fma_f32 %[t1], %[P23], %[X2], %[t1] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"  // b
-      "v_pk_fma_f32 %[t2], %[P67], %[X2], %[t2] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"  // l3
-      "v_pk_fma_f32 %[t3], %[P01], %[X1], %[t3] op_sel:[0,0,0] op_sel_hi:[0,1,1]\n\t"  // c
-      "v_pk_fma_f32 %[t4], %[P01], %[X1], %[t4] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"  // d
-      "v_pk_fma_f32 %[t2], %[t1], %[Y1], %[t2]\n\t"                                      // b y1 + l3
-      "v_pk_mul_f32 %[t1], %[t1], %[t1]\n\t"                                             // b^2
-      "v_pk_mul_f32 %[t4], %[t4], %[t4]\n\t"                                             // d^2
-      "v_pk_fma_f32 %[t2], %[t0], %[X1], %[t2]\n\t"                                      // e
-      "v_pk_fma_f32 %[t1], %[t0], %[t0], %[t1]\n\t"                                      // n1
-      "v_pk_fma_f32 %[t4], %[t3], %[t3], %[t4]\n\t"                                      // n2
-      "v_pk_fma_f32 %[t0], %[t2], %[t2], %[KIO] op_sel:[0,0,0] op_sel_hi:[1,1,0]\n\t"  // P
-      "v_pk_fma_f32 %[t3], %[t2], %[t2], %[KIO] op_sel:[0,0,1] op_sel_hi:[1,1,1]"        // Q
-      : [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4)
-      : [P01] "v"(P01), [P23] "v"(P23), [P45] "v"(P45), [P67] "v"(P67), [P8] "v"(P8),
-        [KIO] "v"(KIO), [X2] "v"(X2), [Y2] "v"(Y2), [X1] "v"(X1), [Y1] "v"(Y1));
-  } else {
   asm("v_pk_fma_f32 %[t0], %[P01], %[Y2], %[P23] op_sel:[1,0,0] op_sel_hi:[1,1,0]\n\t"
       "v_pk_fma_f32 %[t1], %[P45], %[Y2], %[P45] op_sel:[0,0,1] op_sel_hi:[0,1,1]\n\t"
       "v_pk_fma_f32 %[t2], %[P67], %[Y2], %[P8] op_sel:[1,0,0] op_sel_hi:[1,1,0]\n\t"
@@ -323,7 +300,6 @@ __device__ __forceinline__ void pair_terms(f2q P01, f2q P23, f2q P45, f2q P67, f
       : [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4)
       : [P01] "v"(P01), [P23] "v"(P23), [P45] "v"(P45), [P67] "v"(P67), [P8] "v"(P8),
         [KIO] "v"(KIO), [X2] "s"(X2), [Y2] "s"(Y2), [X1] "s"(X1), [Y1] "s"(Y1));
-  }
   P = t0;
   Q = t3;
   // m = min(n1, n2): both are >= +0 or NaN, where the unsigned order of the bit patterns is
@@ -339,9 +315,7 @@ __device__ __forceinline__ void pair_terms(f2q P01, f2q P23, f2q P45, f2q P67, f
 // set by the plan only under RSAMD_TSTAMP, for the launch-shape analysis.
 __device__ uint64_t *g_count_ts = nullptr;
 
-constexpr int kQTile = 256;  // points per LDS tile of a wave (LDSP variant): 4 KB
-
-template <int BT, bool LDSP>
+template <int BT>
 __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ ptsq,
                                                      const Pt *__restrict__ pts, int n, int H,
                                                      const float *__restrict__ F32soa,
@@ -362,11 +336,6 @@ __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ p
   uint64_t *ts = g_count_ts;  // diagnostic wave timeline (RSAMD_TSTAMP), null in production
   const uint64_t t_start = ts ? __builtin_amdgcn_s_memrealtime() : 0ull;
   int n_retest = 0;  // re-test branches taken (timeline diagnostics)
-  // LDSP: the wave's points go through its own LDS tile (coalesced vector loads, then
-  // broadcast ds_read_b128 into VGPR pairs) instead of scalar loads (the scalar data cache
-  // misses 62 % of those: PMC SQC_DCACHE_*)
-  __shared__ float4 s_tile[LDSP ? BT / 64 : 1][LDSP ? kQTile : 1];
-  float4 *tile = s_tile[LDSP ? (threadIdx.x >> 6) : 0];
   while (pos < end) {
     const int grp = static_cast<int>(pos / npad);
     const int p0 = static_cast<int>(pos - static_cast<int64_t>(grp) * npad);
@@ -384,19 +353,17 @@ __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ p
     const float4 q = G4[hl];
     const f2 KIO = {q.x, q.y}, ALB = {q.z, q.w};
     int cnt = 0;
-    if constexpr (!LDSP) {
-      constexpr bool VP = false;
-      for (int i = p0; i < p1; i += 8) {
-        float4 blk[8];  // (x2[8], y2[8], x1[8], y1[8]) of points i..i+7
+    for (int i = p0; i < p1; i += 8) {
+      float4 blk[8];  // (x2[8], y2[8], x1[8], y1[8]) of points i..i+7
 #pragma unroll
-        for (int k = 0; k < 8; ++k) blk[k] = ptsq[i + k];
-        const float *v = reinterpret_cast<const float *>(blk);
+      for (int k = 0; k < 8; ++k) blk[k] = ptsq[i + k];
+      const float *v = reinterpret_cast<const float *>(blk);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const f2 X2 = {v[2 * j], v[2 * j + 1]}, Y2 = {v[8 + 2 * j], v[9 + 2 * j]};
-          const f2 X1 = {v[16 + 2 * j], v[17 + 2 * j]}, Y1 = {v[24 + 2 * j], v[25 + 2 * j]};
+      for (int j = 0; j < 4; ++j) {
+        const f2 X2 = {v[2 * j], v[2 * j + 1]}, Y2 = {v[8 + 2 * j], v[9 + 2 * j]};
+        const f2 X1 = {v[16 + 2 * j], v[17 + 2 * j]}, Y1 = {v[24 + 2 * j], v[25 + 2 * j]};
         f2 P, Q, R, S;
-        pair_terms<VP>(P01, P23, P45, P67, P8, KIO, ALB, X2, Y2, X1, Y1, P, Q, R, S);
+        pair_terms(P01, P23, P45, P67, P8, KIO, ALB, X2, Y2, X1, Y1, P, Q, R, S);
         const unsigned long long i0 = __ballot(P.x < R.x), i1 = __ballot(P.y < R.y);
         const unsigned long long l0 = __ballot(Q.x <= S.x), l1 = __ballot(Q.y <= S.y);
         cnt = add_lane_bit(cnt, i0);  // sure inliers
@@ -412,53 +379,6 @@ __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ p
           for (int k = 0; k < 9; ++k) fdd[k] = fp[k * ld];
           if ((a0 >> lane) & 1ull) cnt += test64(fdd, pts[i + 2 * j], g.thr2_px) ? 1 : 0;
           if ((a1 >> lane) & 1ull) cnt += test64(fdd, pts[i + 2 * j + 1], g.thr2_px) ? 1 : 0;
-        }
-        }
-      }
-    } else {
-      constexpr bool VP = true;
-      for (int tb = p0; tb < p1; tb += kQTile) {
-        const int te = min(p1, tb + kQTile);
-        // tile [tb, te): float4 k of the point-pair layout is point tb + k's share
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int k = 0; k < kQTile / 64; ++k) {
-          const int x = k * 64 + lane;
-          if (tb + x < te) tile[x] = ptsq[tb + x];
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        for (int i = tb; i < te; i += 4) {
-          // half block: x2, y2, x1, y1 of points i..i+3 (two pairs), one broadcast read each
-          const int b = (i - tb) & ~7, o = ((i - tb) & 4) >> 2;
-          const float4 x2 = tile[b + o], y2 = tile[b + 2 + o];
-          const float4 x1 = tile[b + 4 + o], y1 = tile[b + 6 + o];
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const f2 X2 = j ? f2{x2.z, x2.w} : f2{x2.x, x2.y};
-            const f2 Y2 = j ? f2{y2.z, y2.w} : f2{y2.x, y2.y};
-            const f2 X1 = j ? f2{x1.z, x1.w} : f2{x1.x, x1.y};
-            const f2 Y1 = j ? f2{y1.z, y1.w} : f2{y1.x, y1.y};
-        f2 P, Q, R, S;
-            pair_terms<VP>(P01, P23, P45, P67, P8, KIO, ALB, X2, Y2, X1, Y1, P, Q, R, S);
-            const unsigned long long i0 = __ballot(P.x < R.x), i1 = __ballot(P.y < R.y);
-            const unsigned long long l0 = __ballot(Q.x <= S.x), l1 = __ballot(Q.y <= S.y);
-            cnt = add_lane_bit(cnt, i0);  // sure inliers
-            cnt = add_lane_bit(cnt, i1);
-            const unsigned long long a0 = i0 ^ l0, a1 = i1 ^ l1;
-            if ((a0 | a1) != 0ull) {  // rare: float64 re-test of the ambiguous lanes
-              ++n_retest;
-              // the opaque pointer keeps these loads (and their 18 VGPRs) inside the rare branch
-              const double *fp = Fsoa + hl;
-              asm volatile("" : "+v"(fp));
-              double fdd[9];
-#pragma unroll
-              for (int k = 0; k < 9; ++k) fdd[k] = fp[k * ld];
-              if ((a0 >> lane) & 1ull) cnt += test64(fdd, pts[i + 2 * j], g.thr2_px) ? 1 : 0;
-              if ((a1 >> lane) & 1ull) cnt += test64(fdd, pts[i + 2 * j + 1], g.thr2_px) ? 1 : 0;
-            }
-          }
         }
       }
     }
@@ -1034,14 +954,9 @@ hipError_t launch_f8_count32q(const float4 *ptsq, const Pt *pts, int n, int H,
                               const float *F32soa, const double *Fsoa, int64_t ld,
                               const Count32qShape &sh, const GuardW &g, int *counts,
                               hipStream_t s, int *gdone, int *status, const float4 *G4) {
-  if (sh.lds_points)
-    hipLaunchKernelGGL((k_f8_count32q<256, true>), dim3(static_cast<unsigned>(sh.blocks)),
-                       dim3(256), 0, s, ptsq, pts, n, H, F32soa, Fsoa, ld, sh.per_wave, g, counts,
-                       gdone, status, G4);
-  else
-    hipLaunchKernelGGL((k_f8_count32q<256, false>), dim3(static_cast<unsigned>(sh.blocks)),
-                       dim3(256), 0, s, ptsq, pts, n, H, F32soa, Fsoa, ld, sh.per_wave, g, counts,
-                       gdone, status, G4);
+  hipLaunchKernelGGL((k_f8_count32q<256>), dim3(static_cast<unsigned>(sh.blocks)), dim3(256), 0,
+                     s, ptsq, pts, n, H, F32soa, Fsoa, ld, sh.per_wave, g, counts, gdone, status,
+                     G4);
   return hipGetLastError();
 }
 

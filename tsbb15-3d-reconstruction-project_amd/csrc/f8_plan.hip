@@ -108,7 +108,6 @@ struct rs_f8_plan {
   int timing = 1;
   int timing_every = 1;       // RSAMD_TIMING_EVERY / rs_f8_plan_set_timing: time every k-th run
   int q_waves = 6144;         // resident waves of the fp32 kernel (RSAMD_WAVES)
-  bool q_lds = false;         // LDS-staged points (RSAMD_QLDS=1)
   int q_slices = 0;           // slices per resident wave (RSAMD_QSLICES; 0: count32q_shape)
   int tail_cus = 256;         // CUs shared by the tail + solve launch
   int nospec = 0;             // RSAMD_NOSPEC=1 (test hook): the replay extracts S_RANSAC itself
@@ -182,7 +181,6 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
     p->tail_cus = cus;
     p->q_waves = std::max(1, env_int("RSAMD_WAVES", rsd::count32q_resident_waves(c->device)));
     p->q_slices = env_int("RSAMD_QSLICES", 0);
-    p->q_lds = env_int("RSAMD_QLDS", 0) != 0;
   }
   hipError_t e = hipSuccess;
 #define ALLOC(ptr, bytes) \
@@ -387,8 +385,7 @@ static int plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t seed, uint6
   if (tl >= 1) HIP_TRY(hipEventRecord(ev[0], ms));
   if (fp32) {
     // fused c*: the chunk that completes a hypothesis group folds its max into status[0]
-    rsd::Count32qShape sh = rsd::count32q_shape(n, h, p->q_waves, p->q_slices);
-    sh.lds_points = p->q_lds;
+    const rsd::Count32qShape sh = rsd::count32q_shape(n, h, p->q_waves, p->q_slices);
     HIP_TRY(rsd::launch_f8_count32q(p->d_pts32q, p->d_pts, n, h, b.d_F32, b.d_F, p->ld, sh,
                                     rsd::GuardW{thresh * thresh}, b.d_counts, ms, b.d_gdone,
                                     b.d_status, b.d_G4));
