@@ -226,7 +226,10 @@ __global__ __launch_bounds__(256) void k_f8_count(const Pt *__restrict__ pts, in
 // hypothesis group per wave, so a workgroup's waves share scalar-cache lines: 0.108 vs 0.0995
 // ms, slower ramp).  The scalar data cache misses 62 % of the point loads (PMC SQC_DCACHE_*),
 // yet staging each wave's points through an LDS tile (broadcast ds_read_b128 into VGPR
-// operands, 80 SGPRs / 62 VGPRs, 8 waves per SIMD) was slower too (0.104-0.106 ms).
+// operands, 80 SGPRs / 62 VGPRs, 8 waves per SIMD) was slower too (0.104-0.106 ms).  Folding
+// the guard band into per-hypothesis G constants (one compare chain per side, counts kept as
+// bit planes) cut VALU by 6 % and left the time unchanged at C2 (0.1118 vs 0.1108 ms) and C5
+// (4.35 vs 4.36 ms, tools/probe_c5_count.py): the issue slots are not what binds.
 // ----------------------------------------------------------------------------------------
 
 // The float64 test of k_f8_count (pixel units) for one (hypothesis, point).
