@@ -61,10 +61,9 @@ constexpr int kJB = 1024;                    // stream blocks per generator
 constexpr int64_t kJ = int64_t(kN) * kJB;    // words per generator
 constexpr int kLevels = 11;                  // jump tree depth: up to 2048 generators
 constexpr int64_t kSegWords = int64_t(1) << 29;  // stream words per segment (2 GiB)
-constexpr int kW = 1 << 20;                  // longest automatic parse chunk (draws)
-constexpr int kWmax = 1 << 20;               // longest chunk (RSAMD_NP_KW)
+constexpr int kW = 1 << 21;                  // longest automatic parse chunk (draws)
+constexpr int kWmax = 1 << 21;               // longest chunk (RSAMD_NP_KW)
 constexpr int kWmin = 8192;                  // shortest parse chunk
-constexpr int kChunksTarget = 512;           // automatic chunk length: about this many chunks
 constexpr int kEntryThreads = 512;
 constexpr int kR = 20;                       // slots per thread: N - 1 <= 10240
 constexpr int kMaxN1 = kEntryThreads * kR;
@@ -1131,6 +1130,7 @@ struct rs_np_work {
   NpResult *d_res = nullptr;
   int64_t cap_fin = 0, cap_ev = 0, cap_starts = 0;
   int64_t entry_lds = 0, tup_lds = 0;
+  int cus = 256;  // compute units of the context's device
 };
 
 namespace rs {
@@ -1188,8 +1188,7 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
   int st;
   const int n1 = static_cast<int>(n - 1);
   const int64_t Gmax = (kSegWords / kN + kJB - 1) / kJB + 1;
-  // chunk length: about 1024 chunks per segment (a short serial parse per chunk, enough
-  // chunks to fill the GPU), between 8192 and 262144 draws; RSAMD_NP_KW fixes it
+  // RSAMD_NP_KW fixes the chunk length (kWmin .. kWmax draws); else automatic (below)
   static const int kWenv = [] {
     const char *e = std::getenv("RSAMD_NP_KW");
     const int v = e ? std::atoi(e) : 0;
@@ -1227,6 +1226,9 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
       return st;
     int64_t c10 = 0;
     if ((st = grow(w.d_res, c10, 1))) return st;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && cus > 0)
+      w.cus = cus;
   }
   const double E = expected_draws(n1, py);
   const int64_t dmax = seg_words() - 3 * kN;
@@ -1244,10 +1246,15 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
   while (done < count) {
     const int64_t hs = std::min<int64_t>(count - done, hcap);
     const int64_t D = std::min<int64_t>(dmax, static_cast<int64_t>(std::ceil(hs * E * 1.03)) + 16 * n + 4096);
+    // automatic chunk length: every chunk in one resident round of k_np_track (16-wave
+    // workgroups, two per CU) with equal lengths: C = 2 x CUs chunks for N - 1 < 4096; for
+    // larger N the dense entry phase (cost ~ N per chunk) favours one chunk per CU.  Measured
+    // (C2, 1e5 tuples): 274 chunks of 2^20 9.9 ms, 508 of 565 248 8.3 ms, 765 of 376 832 9.9 ms.
     int kWr = kWenv;
     if (!kWr) {
-      kWr = kWmin;
-      while (kWr < kW && static_cast<int64_t>(kWr) * kChunksTarget < D) kWr *= 2;
+      const int64_t C0 = static_cast<int64_t>(w.cus) * (n1 < 4096 ? 2 : 1);
+      const int64_t L = ((D + C0 - 1) / C0 + 4095) / 4096 * 4096;
+      kWr = static_cast<int>(std::max<int64_t>(kWmin, std::min<int64_t>(kW, L)));
     }
     const int ecap = static_cast<int>(std::min<int64_t>(
         kWr + 2 * n1, (static_cast<int64_t>(70.0 * kWr / E) + 4 * n1 + 4096) << ecap_shift));
