@@ -22,6 +22,13 @@ if len(sys.argv) > 2 and sys.argv[1] == "--read":
         print(f"  one-trajectory wave-intervals {i1.sum()/C:.0f} per chunk, {c1.sum()/max(i1.sum(),1):.3g} cycles each")
         print(f"  multi-trajectory wave-intervals {iN.sum()/C:.0f} per chunk, {cN.sum()/max(iN.sum(),1):.3g} cycles each")
         print(f"  busiest wave per chunk: one {c1.max(1).mean():.3g} multi {cN.max(1).mean():.3g} cycles; intervals {w[:,0,5].mean():.0f}")
+        k0 = st[:, 121]
+        if k0.any():
+            rel = k0 - k0.min()
+            end = rel + kern
+            print(f"  chunk start offsets: median {np.median(rel):.3g} max {rel.max():.3g}; last end {end.max():.3g}; "
+                  f"chunks starting after {np.percentile(kern, 50):.3g}: {(rel > np.percentile(kern, 50)).sum()}")
+            print(f"  distinct hw ids {len(np.unique(st[:, 122]))}")
     sys.exit(0)
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tsbb15-3d-reconstruction-project_amd"))

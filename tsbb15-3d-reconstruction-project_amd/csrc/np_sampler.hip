@@ -499,52 +499,42 @@ __device__ __forceinline__ uint32_t wrap_state(int si, int n1) {
 // State i before the window, lane l holds draw l of the window (lanes >= Wn, outside wm, are
 // never accepted).  Returns the accept mask; advances i; wraps (hypothesis ends) in *wr.
 //
-// Fast path: every state the window can reach keeps i's draw rule (i - 63 >= the bucket's lowest
-// state), so no hypothesis ends inside and lane l's draw u_l is fixed.  With rank_l = accepts
-// among lanes < l, lane l accepts iff rank_l <= v_l := i - u_l, and 0 <= rank_l <= l: v_l >= l
-// accepts surely, v_l < 0 rejects surely, and the few lanes between (about l / 2^bits each) are
-// resolved in order on the scalar unit; more than kAmbSeq of them go to the fixed point below.
-// General path (bucket crossings, hypothesis ends): the fixed point of
+// Fast path: every state the window can reach lies in i's bucket or the one below (i - 63 >=
+// the lower bucket's lowest state), so no hypothesis ends inside and lane l's draw is u_hi (i's
+// rule) or u_lo (the lower rule) by whether its state i - rank_l is at least `lowest`: with
+// v = i - u and rank_l = accepts among lanes < l, lane l accepts iff
+//     rank_l <= (rank_l <= i - lowest ? v_hi : v_lo),
+// and the accept mask is the fixed point of that test over rank_l(acc), from "accept unless
+// v_hi < 0" (lanes < l right => lane l right, so it reaches the sequential answer, and any
+// fixed point is that answer).
+// General path (states below 2 x 64, hypothesis ends): the fixed point of
 //     acc <- ballot(draw_of(w_l, s_l) <= s_l),  s_l = i - rank_l(acc) (wrapped into 1..n1),
-// from "all accept": lanes < l right => lane l right, so it reaches the sequential answer, and
-// any fixed point is that answer.
-constexpr int kAmbSeq = 4;
-
+// from "all accept".
+// (Measured, tools/ubench/amb_bench2.hip, one wave alone: 5.1 cycles per draw; the one-bucket
+// sure / ambiguous split with the ambiguous lanes resolved one by one on the scalar unit: 6.3.)
 template <bool PY, bool SMALL>
 __device__ __forceinline__ uint64_t window_step(uint32_t w, uint64_t wm, uint32_t &i, int n1,
                                                 uint64_t &wr, uint32_t &sl_out) {
-  const int lane = threadIdx.x & 63;
-  uint32_t lowest, u;
+  uint32_t lowest, lowest2, sh = 0, M = 0;
   if constexpr (PY) {
-    const uint32_t sh = static_cast<uint32_t>(__builtin_clz(i + 1u));
+    sh = static_cast<uint32_t>(__builtin_clz(i + 1u));
     lowest = (1u << (31u - sh)) - 1u;  // i + 1 in [2^(31-sh), 2^(32-sh) - 1]
-    u = w >> sh;
+    lowest2 = sh < 30u ? (1u << (30u - sh)) - 1u : 0x7fffffffu;
   } else {
-    const uint32_t M = 0xffffffffu >> __builtin_clz(i);
+    M = 0xffffffffu >> __builtin_clz(i);
     lowest = (M >> 1) + 1u;
-    u = w & M;
+    lowest2 = M > 1u ? (M >> 2) + 1u : 0x7fffffffu;
   }
-  if (i >= lowest + 63u) {
-    const int v = static_cast<int>(i) - static_cast<int>(u);
-    uint64_t acc = __ballot(v >= lane) & wm;
-    uint64_t amb = __ballot(v >= 0) & wm & ~acc;
-    if (amb) {
-      if (__popcll(amb) <= kAmbSeq) {
-        do {
-          const int f = __ffsll(static_cast<long long>(amb)) - 1;
-          const int rk = __popcll(acc & ((1ull << f) - 1ull));
-          if (rk <= __builtin_amdgcn_readlane(v, f)) acc |= 1ull << f;
-          amb &= amb - 1ull;
-        } while (amb);
-      } else {
-        acc |= amb;
-        uint64_t prev;
-        do {
-          prev = acc;
-          acc = __ballot(static_cast<int>(lane_rank(prev)) <= v) & wm;
-        } while (acc != prev);
-      }
-    }
+  if (i >= lowest2 + 63u && lowest2 >= 1u) {
+    const int c = static_cast<int>(i) - static_cast<int>(lowest);
+    const int vh = static_cast<int>(i) - static_cast<int>(PY ? (w >> sh) : (w & M));
+    const int vl = static_cast<int>(i) - static_cast<int>(PY ? (w >> (sh + 1u)) : (w & (M >> 1)));
+    uint64_t acc = __ballot(vh >= 0) & wm, prev;
+    do {
+      prev = acc;
+      const int rk = static_cast<int>(lane_rank(prev));
+      acc = __ballot(rk <= (rk <= c ? vh : vl)) & wm;
+    } while (acc != prev);
     i -= static_cast<uint32_t>(__popcll(acc));
     wr = 0;
     sl_out = 0;
@@ -564,97 +554,50 @@ __device__ __forceinline__ uint64_t window_step(uint32_t w, uint64_t wm, uint32_
 }
 
 // One checkpoint interval [t, cp) of a single trajectory (the common case once a chunk's
-// trajectories have merged down to at most one per wave): the tight loop.
-// While every state a window can reach lies in i's bucket or the one below (and no hypothesis
-// ends), lane l's draw is u_hi (i's rule) or u_lo (the lower rule) by whether its state
-// i - rank_l is at least `lowest`: with v = i - u, lane l accepts iff
-//     rank_l <= (rank_l <= i - lowest ? v_hi : v_lo),
-// and the accept masks are the fixed point of that test over rank_l(acc) (four quarters of 64
-// draws at once, lane l holding draws 64 k + l; any fixed point is the sequential answer).
-// Other windows (states below 2 x 64, hypothesis ends) go through window_step.
+// trajectories have merged down to at most one per wave): the tight loop.  Windows of 64 draws
+// at fixed offsets, so their words are read from LDS four windows ahead into registers (the
+// read never waits on the state).  While every state a window can reach lies in i's bucket or
+// the one below, window_step's two-bucket fixed point decides it.  (Measured,
+// tools/ubench/amb_bench2.hip: 5.1 cycles per draw for one wave alone, against 7.9 for the
+// earlier 256-draw windows read from LDS at the top of each step.)
+template <bool PY, bool SMALL>
+__device__ __forceinline__ void track_window(const EntryArgs &a, uint32_t w, int *s_evn, uint2 *ev,
+                                             uint32_t &i, uint32_t range, int d, int cp) {
+  const int lane = threadIdx.x & 63;
+  const int Wn = min(64, cp - d);
+  const uint64_t wm = Wn == 64 ? ~0ull : ((1ull << Wn) - 1ull);
+  uint64_t wr;
+  uint32_t sl;
+  (void)window_step<PY, SMALL>(w, wm, i, a.n1, wr, sl);
+  if (wr) {  // hypothesis ends: the next hypothesis starts at the following draw
+    int eb = 0;
+    if (lane == 0) eb = atomicAdd(s_evn, __popcll(wr));
+    eb = __shfl(eb, 0);
+    if (((wr >> lane) & 1ull)) {
+      const int e = eb + static_cast<int>(lane_rank(wr));
+      if (e < a.ecap) ev[e] = make_uint2(static_cast<uint32_t>(d + lane + 1), range);
+    }
+  }
+}
+
 template <bool PY, bool SMALL>
 __device__ __forceinline__ uint32_t track_one(const EntryArgs &a, const uint32_t *sw, int *s_evn,
                                               uint2 *ev, uint32_t i, uint32_t range, int t,
                                               int cp) {
   const int lane = threadIdx.x & 63;
-  const int n1 = a.n1;
-  int d = t;
-  while (d < cp) {
-    uint32_t lowest, lowest2, sh = 0, M = 0;
-    if constexpr (PY) {
-      sh = static_cast<uint32_t>(__builtin_clz(i + 1u));
-      lowest = (1u << (31u - sh)) - 1u;
-      lowest2 = sh < 30u ? (1u << (30u - sh)) - 1u : 0x7fffffffu;
-    } else {
-      M = 0xffffffffu >> __builtin_clz(i);
-      lowest = (M >> 1) + 1u;
-      lowest2 = M > 1u ? (M >> 2) + 1u : 0x7fffffffu;
-    }
-    const uint32_t *wq = sw + ((d - t) & (kCheck - 1));
-    const int c = static_cast<int>(i) - static_cast<int>(lowest);
-    if (d + 256 <= cp && i >= lowest2 + 255u && lowest2 >= 1u) {
-      int vh[4], vl[4];
-      uint64_t acc[4];
+  constexpr int kAhead = 4;
+  // lanes beyond cp read words of the wrapped buffer: never accepted (wm)
+  uint32_t q[kAhead];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t w = wq[64 * k + lane];
-        vh[k] = static_cast<int>(i) - static_cast<int>(PY ? (w >> sh) : (w & M));
-        vl[k] = static_cast<int>(i) - static_cast<int>(PY ? (w >> (sh + 1u)) : (w & (M >> 1)));
-        acc[k] = __ballot(vh[k] >= 0);
-      }
-      bool again;
-      do {
-        int base = 0;
-        uint64_t nacc[4];
+  for (int k = 0; k < kAhead; ++k) q[k] = sw[(64 * k + lane) & (kCheck - 1)];
+  for (int d = t; d < cp; d += 64 * kAhead) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int rk = base + static_cast<int>(lane_rank(acc[k]));
-          nacc[k] = __ballot(rk <= (rk <= c ? vh[k] : vl[k]));
-          base += static_cast<int>(__popcll(acc[k]));
-        }
-        again = false;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          again |= nacc[k] != acc[k];
-          acc[k] = nacc[k];
-        }
-      } while (again);
-      int tot = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) tot += static_cast<int>(__popcll(acc[k]));
-      i -= static_cast<uint32_t>(tot);
-      d += 256;
-      continue;
+    for (int k = 0; k < kAhead; ++k) {
+      const uint32_t w = q[k];
+      q[k] = sw[(d - t + 64 * (kAhead + k) + lane) & (kCheck - 1)];
+      const int dk = d + 64 * k;
+      if (dk < cp) track_window<PY, SMALL>(a, w, s_evn, ev, i, range, dk, cp);
     }
-    const int Wn = min(64, cp - d);
-    const uint64_t wm = Wn == 64 ? ~0ull : ((1ull << Wn) - 1ull);
-    const uint32_t w = wq[lane];  // lanes >= Wn read draws of the wrapped buffer, never accepted
-    if (i >= lowest2 + 63u && lowest2 >= 1u) {
-      const int vh = static_cast<int>(i) - static_cast<int>(PY ? (w >> sh) : (w & M));
-      const int vl = static_cast<int>(i) - static_cast<int>(PY ? (w >> (sh + 1u)) : (w & (M >> 1)));
-      uint64_t acc = __ballot(vh >= 0) & wm, prev;
-      do {
-        prev = acc;
-        const int rk = static_cast<int>(lane_rank(prev));
-        acc = __ballot(rk <= (rk <= c ? vh : vl)) & wm;
-      } while (acc != prev);
-      i -= static_cast<uint32_t>(__popcll(acc));
-      d += Wn;
-      continue;
-    }
-    uint64_t wr;
-    uint32_t sl;
-    (void)window_step<PY, SMALL>(w, wm, i, n1, wr, sl);
-    if (wr) {  // hypothesis ends: the next hypothesis starts at the following draw
-      int eb = 0;
-      if (lane == 0) eb = atomicAdd(s_evn, __popcll(wr));
-      eb = __shfl(eb, 0);
-      if (((wr >> lane) & 1ull)) {
-        const int e = eb + static_cast<int>(lane_rank(wr));
-        if (e < a.ecap) ev[e] = make_uint2(static_cast<uint32_t>(d + lane + 1), range);
-      }
-    }
-    d += Wn;
   }
   return i;
 }
@@ -816,7 +759,11 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_np_track(EntryArgs a,
   if (a.stats && lane == 0) {
     long long *o = a.stats + static_cast<size_t>(c) * 128 + wv * 6;
     for (int k = 0; k < 6; ++k) o[k] = dg[k];
-    if (wv == 0) a.stats[static_cast<size_t>(c) * 128 + 120] = __builtin_amdgcn_s_memtime() - k0;
+    if (wv == 0) {
+      a.stats[static_cast<size_t>(c) * 128 + 120] = __builtin_amdgcn_s_memtime() - k0;
+      a.stats[static_cast<size_t>(c) * 128 + 121] = k0;  // absolute start (schedule)
+      a.stats[static_cast<size_t>(c) * 128 + 122] = static_cast<long long>(__smid());
+    }
   }
 #else
   (void)dg;
