@@ -22,13 +22,12 @@ if len(sys.argv) > 2 and sys.argv[1] == "--read":
         print(f"  one-trajectory wave-intervals {i1.sum()/C:.0f} per chunk, {c1.sum()/max(i1.sum(),1):.3g} cycles each")
         print(f"  multi-trajectory wave-intervals {iN.sum()/C:.0f} per chunk, {cN.sum()/max(iN.sum(),1):.3g} cycles each")
         print(f"  busiest wave per chunk: one {c1.max(1).mean():.3g} multi {cN.max(1).mean():.3g} cycles; intervals {w[:,0,5].mean():.0f}")
-        k0 = st[:, 121]
-        if k0.any():
-            rel = k0 - k0.min()
-            end = rel + kern
-            print(f"  chunk start offsets: median {np.median(rel):.3g} max {rel.max():.3g}; last end {end.max():.3g}; "
-                  f"chunks starting after {np.percentile(kern, 50):.3g}: {(rel > np.percentile(kern, 50)).sum()}")
-            print(f"  distinct hw ids {len(np.unique(st[:, 122]))}")
+        r0, r1 = st[:, 121], st[:, 122]
+        if r0.any():
+            rel0, rel1 = (r0 - r0.min()) / 100.0, (r1 - r0.min()) / 100.0  # us
+            dur = rel1 - rel0
+            print(f"  real time (us): start median {np.median(rel0):.1f} max {rel0.max():.1f}; duration mean {dur.mean():.0f} "
+                  f"max {dur.max():.0f}; last end {rel1.max():.0f}; clock {kern.mean() / dur.mean() / 1e3:.2f} GHz (memtime / real)")
     sys.exit(0)
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tsbb15-3d-reconstruction-project_amd"))

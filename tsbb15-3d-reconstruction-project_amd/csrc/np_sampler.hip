@@ -485,8 +485,14 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a,
 // same trajectory from then on, so all but the first of each run of equal states (cyclic order
 // is preserved by the parse) are dropped, and the survivor's member range extends to the next
 // survivor's start.  Wraps are logged with the member range as in k_np_entry.
-constexpr int kTrackWaves = 16;
-constexpr int kCheck = 4096;
+#ifndef RSAMD_TRACK_WAVES
+#define RSAMD_TRACK_WAVES 16
+#endif
+constexpr int kTrackWaves = RSAMD_TRACK_WAVES;  // waves per chunk workgroup, >= 8 (A/B builds may override)
+#ifndef RSAMD_KCHECK
+#define RSAMD_KCHECK 4096
+#endif
+constexpr int kCheck = RSAMD_KCHECK;  // draws per checkpoint interval (A/B builds may override)
 
 template <bool PY, bool SMALL>
 __device__ __forceinline__ uint32_t wrap_state(int si, int n1) {
@@ -677,6 +683,7 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_np_track(EntryArgs a,
   long long dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #ifdef RSAMD_DIAG
   const long long k0 = __builtin_amdgcn_s_memtime();
+  const long long r0 = __builtin_amdgcn_s_memrealtime();
 #endif
   if (tid < m) {
     const uint32_t f = a.fin[static_cast<size_t>(c) * n1 + tid];
@@ -761,8 +768,8 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_np_track(EntryArgs a,
     for (int k = 0; k < 6; ++k) o[k] = dg[k];
     if (wv == 0) {
       a.stats[static_cast<size_t>(c) * 128 + 120] = __builtin_amdgcn_s_memtime() - k0;
-      a.stats[static_cast<size_t>(c) * 128 + 121] = k0;  // absolute start (schedule)
-      a.stats[static_cast<size_t>(c) * 128 + 122] = static_cast<long long>(__smid());
+      a.stats[static_cast<size_t>(c) * 128 + 121] = r0;  // start / end, 100 MHz real-time clock
+      a.stats[static_cast<size_t>(c) * 128 + 122] = __builtin_amdgcn_s_memrealtime();
     }
   }
 #else
