@@ -84,7 +84,6 @@ hipError_t launch_pack_points32q(const Pt *pts, int n, const Frame &fr, float4 *
 struct Count32qShape {
   int64_t per_wave;  // points of the (group, point) plane per wave (a multiple of 8)
   int64_t blocks;    // 256-thread workgroups launched
-  float sched = 0.f;  // > 0: slice w of the 4 x blocks covers total x (1 - (1 - x)^sched), x = w / waves
 };
 int count32q_resident_waves(int device);
 Count32qShape count32q_shape(int n, int H, int waves, int slices_per_wave = 0);

@@ -229,7 +229,10 @@ __global__ __launch_bounds__(256) void k_f8_count(const Pt *__restrict__ pts, in
 // operands, 80 SGPRs / 62 VGPRs, 8 waves per SIMD) was slower too (0.104-0.106 ms).  Folding
 // the guard band into per-hypothesis G constants (one compare chain per side, counts kept as
 // bit planes) cut VALU by 6 % and left the time unchanged at C2 (0.1118 vs 0.1108 ms) and C5
-// (4.35 vs 4.36 ms, tools/probe_c5_count.py): the issue slots are not what binds.
+// (4.35 vs 4.36 ms, tools/probe_c5_count.py): the issue slots are not what binds.  Slices
+// shrinking with the wave index (slice w covering total x (1 - (1 - w/W)^p), so the last waves
+// to start carry the least work) were slower too: 0.103-0.108 ms at p = 1.3-2.0 against
+// 0.098-0.101 for equal slices, interleaved runs on one box (round 2).
 // ----------------------------------------------------------------------------------------
 
 // The float64 test of k_f8_count (pixel units) for one (hypothesis, point).
@@ -323,8 +326,7 @@ __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ p
                                                      const Pt *__restrict__ pts, int n, int H,
                                                      const float *__restrict__ F32soa,
                                                      const double *__restrict__ Fsoa,
-                                                     int64_t ld, int64_t per_wave, float sched,
-                                                     GuardW g,
+                                                     int64_t ld, int64_t per_wave, GuardW g,
                                                      int *__restrict__ counts,
                                                      int *__restrict__ gdone,
                                                      int *__restrict__ status,
@@ -335,19 +337,8 @@ __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ p
   const int64_t w = wave_uniform(blockIdx.x * (BT / 64) + (threadIdx.x >> 6));
   const int npad = (n + 7) / 8 * 8;
   const int64_t total = static_cast<int64_t>((H + 63) >> 6) * npad;
-  int64_t pos, end;
-  if (sched > 0.f) {  // decreasing slices: the last waves to start get the least work
-    const double nw = static_cast<double>(gridDim.x) * (BT / 64);
-    const double g0 = 1.0 - pow(1.0 - static_cast<double>(w) / nw, static_cast<double>(sched));
-    const double g1 = 1.0 - pow(1.0 - static_cast<double>(w + 1) / nw, static_cast<double>(sched));
-    pos = static_cast<int64_t>(static_cast<double>(total) * g0) / 8 * 8;
-    end = w + 1 >= static_cast<int64_t>(nw) ? total
-                                             : static_cast<int64_t>(static_cast<double>(total) * g1) / 8 * 8;
-    end = min(total, end);
-  } else {
-    pos = w * per_wave;
-    end = min(total, pos + per_wave);
-  }
+  int64_t pos = w * per_wave;
+  const int64_t end = min(total, pos + per_wave);
   uint64_t *ts = g_count_ts;  // diagnostic wave timeline (RSAMD_TSTAMP), null in production
   const uint64_t t_start = ts ? __builtin_amdgcn_s_memrealtime() : 0ull;
   int n_retest = 0;  // re-test branches taken (timeline diagnostics)
@@ -962,11 +953,6 @@ Count32qShape count32q_shape(int n, int H, int waves, int slices_per_wave) {
   W = (total + per - 1) / per;
   sh.per_wave = per;
   sh.blocks = (W + 3) / 4;
-  static const float sched = [] {
-    const char *e = std::getenv("RSAMD_QSCHED");
-    return e ? static_cast<float>(std::atof(e)) : 0.f;
-  }();
-  sh.sched = sched;
   return sh;
 }
 
@@ -975,7 +961,7 @@ hipError_t launch_f8_count32q(const float4 *ptsq, const Pt *pts, int n, int H,
                               const Count32qShape &sh, const GuardW &g, int *counts,
                               hipStream_t s, int *gdone, int *status, const float4 *G4) {
   hipLaunchKernelGGL((k_f8_count32q<256>), dim3(static_cast<unsigned>(sh.blocks)), dim3(256), 0,
-                     s, ptsq, pts, n, H, F32soa, Fsoa, ld, sh.per_wave, sh.sched, g, counts, gdone, status,
+                     s, ptsq, pts, n, H, F32soa, Fsoa, ld, sh.per_wave, g, counts, gdone, status,
                      G4);
   return hipGetLastError();
 }
