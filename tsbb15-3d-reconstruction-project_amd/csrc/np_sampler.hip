@@ -68,7 +68,10 @@ constexpr int kEntryThreads = 512;
 constexpr int kR = 20;                       // slots per thread: N - 1 <= 10240
 constexpr int kMaxN1 = kEntryThreads * kR;
 constexpr int kK = 64;                       // draws between compactions (<= N - 1 when dense)
-constexpr int kFast = 4;                     // one-slot-per-thread batches between compactions
+#ifndef RSAMD_KFAST
+#define RSAMD_KFAST 4
+#endif
+constexpr int kFast = RSAMD_KFAST;           // one-slot-per-thread batches between compactions
 constexpr int kRFast = 8;                    // slots per thread of the branch-free multi-slot path
 constexpr uint32_t kSentinel = 0x80000000u;  // an empty slot: never reaches 0 within kW steps
 
@@ -278,6 +281,23 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a,
   if (tid == 0) sh_evn = 0;
   __syncthreads();
   int m = n1, t = 0;
+#ifdef RSAMD_DIAG
+  // per path: cycles [0..2] (several slots / multi-slot fast / one-slot), compaction [3], draws [4..6]
+  long long eg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const long long e0 = __builtin_amdgcn_s_memtime();
+  long long ec = e0;
+#define RSD_ETICK(slot, draws)                                   \
+  do {                                                          \
+    const long long now_ = __builtin_amdgcn_s_memtime();       \
+    eg[slot] += now_ - ec;                                      \
+    if ((slot) < 3) eg[(slot) + 4] += (draws);                  \
+    ec = now_;                                                  \
+  } while (0)
+#else
+#define RSD_ETICK(slot, draws) \
+  do {                         \
+  } while (0)
+#endif
   if (m > 64) {
     // dense phase: the whole workgroup, slots q = tid + r * kEntryThreads
     uint32_t s[kR];
@@ -286,6 +306,10 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a,
       const int q = tid + r * kEntryThreads;
       s[r] = q < m ? st[q] : kSentinel;
     }
+    // the words of the next two 64-draw batches, lane l holding draw l of each, loaded one
+    // batch ahead in every wave: the stream comes from HBM, and a load issued where it is
+    // used cost ~40 cycles per draw (one HBM round trip per batch)
+    uint32_t wa = lane < T ? wp[lane] : 0u, wb = 64 + lane < T ? wp[64 + lane] : 0u;
     while (m > 64 && t < T) {
       const int kk = min(kK, T - t);
       const int nr = (m + kEntryThreads - 1) / kEntryThreads;
@@ -299,13 +323,9 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a,
           // (waves holding only empty slots skip the batch: sentinels stay sentinels)
           uint32_t sv = s[0], wk = 0xffffffffu;
           if ((tid & ~63) < m) {
-            uint32_t wsg[64];  // wave-uniform words: scalar loads into SGPRs
-            const uint32_t *__restrict__ wq = wp + t;
-#pragma unroll
-            for (int k = 0; k < 64; ++k) wsg[k] = wq[k];
 #pragma unroll
             for (int k = 0; k < 64; ++k) {
-              const uint32_t w = wsg[k];
+              const uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wa), k));
               sv -= draw_of<PY>(w, sv) <= sv ? 1u : 0u;
               const bool z = sv == 0;
               sv = z ? N1 : sv;
@@ -326,11 +346,14 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a,
             }
           }
           t += 64;
+          wa = wb;
+          wb = t + 64 + lane < T ? wp[t + 64 + lane] : 0u;
+          RSD_ETICK(2, 64);
         }
       } else if (kk == 64 && nr <= kRFast) {
         // several slots per thread: the word from LDS, branch-free steps, each slot's wrap (at
         // most one in 64 draws, as n1 > 64) logged after the batch
-        if (tid < kk) wbuf[tid] = wp[t + tid];
+        if (tid < 64) wbuf[tid] = wa;
         __syncthreads();
         uint32_t wk[kRFast];
 #pragma unroll
@@ -366,8 +389,11 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a,
           }
         }
         t += 64;
+        wa = wb;
+        wb = t + 64 + lane < T ? wp[t + 64 + lane] : 0u;
+        RSD_ETICK(1, 64);
       } else {
-      if (tid < kk) wbuf[tid] = wp[t + tid];
+      if (tid < kk) wbuf[tid] = wa;
       __syncthreads();
       for (int k = 0; k < kk; ++k) {
         const uint32_t w = wbuf[k];
@@ -388,6 +414,9 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a,
         }
       }
       t += kk;
+      wa = wb;
+      wb = t + 64 + lane < T ? wp[t + 64 + lane] : 0u;
+      RSD_ETICK(0, kk);
       }
       // compaction: list order starts at the head (first slot of the maximum run); equal
       // neighbours merge, the first keeps its lo
@@ -448,7 +477,17 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a,
         const int q = tid + r * kEntryThreads;
         s[r] = q < m ? st[q] : kSentinel;
       }
+      RSD_ETICK(3, 0);
     }
+#ifdef RSAMD_DIAG
+    if (a.stats && tid == 0) {
+      long long *o = a.stats + static_cast<size_t>(c) * 128 + 100;
+      for (int k = 0; k < 7; ++k) o[k] = eg[k];
+      o[7] = __builtin_amdgcn_s_memtime() - e0;
+      o[8] = t;
+      o[9] = m;
+    }
+#endif
     if (m > 64) {  // chunk done while still dense
       for (int q = tid; q < m; q += kEntryThreads)
         a.fin[static_cast<size_t>(c) * n1 + q] = lo[q] | (static_cast<uint32_t>(st[q]) << 16);
