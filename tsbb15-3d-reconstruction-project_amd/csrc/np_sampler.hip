@@ -68,10 +68,12 @@ constexpr int kEntryThreads = 512;
 constexpr int kR = 20;                       // slots per thread: N - 1 <= 10240
 constexpr int kMaxN1 = kEntryThreads * kR;
 constexpr int kK = 64;                       // draws between compactions (<= N - 1 when dense)
-#ifndef RSAMD_KFAST
-#define RSAMD_KFAST 4
-#endif
-constexpr int kFast = RSAMD_KFAST;           // one-slot-per-thread batches between compactions
+// dense-phase batches of 64 draws between compactions (the one-slot and the multi-slot paths):
+// a compaction costs ~8k cycles (block scans, barriers), merges are slow at large N.  Measured
+// (C2 / N = 10 000 ms): one-slot 4 / 16 / 32 batches 7.90 / 7.75 / - and 41.4 / 38.6 / 36.6;
+// multi-slot 1 / 4 / 8 batches 7.78 / 8.17 / 8.22 and 38.0 / 37.1 / 36.9.
+__host__ __device__ constexpr int fast_batches(int n1) { return n1 >= 4096 ? 32 : 16; }
+__host__ __device__ constexpr int fast_batches_multi(int n1) { return n1 >= 4096 ? 4 : 1; }
 constexpr int kRFast = 8;                    // slots per thread of the branch-free multi-slot path
 constexpr uint32_t kSentinel = 0x80000000u;  // an empty slot: never reaches 0 within kW steps
 
@@ -259,7 +261,7 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t bits) {
 }
 
 template <bool PY>
-__global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a,
+__global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
                                                              const uint32_t *__restrict__ draws) {
   extern __shared__ uint16_t dyn[];
   __shared__ uint32_t wbuf[kK];
@@ -281,6 +283,7 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a,
   if (tid == 0) sh_evn = 0;
   __syncthreads();
   int m = n1, t = 0;
+  const int nfast = fast_batches(n1), nfastm = fast_batches_multi(n1);
 #ifdef RSAMD_DIAG
   // per path: cycles [0..2] (several slots / multi-slot fast / one-slot), compaction [3], draws [4..6]
   long long eg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -317,9 +320,9 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a,
         // one slot per thread (the common case after the first ~n1 draws): the 64 words in a
         // register of every wave, branch-free steps, a slot's wrap (at most one in 64 draws,
         // as n1 > 64) logged after the batch with one LDS atomic per wave
-        // up to kFast batches between compactions (a slot's list neighbours, used by the wrap
+        // up to nfast batches between compactions (a slot's list neighbours, used by the wrap
         // log, change only at a compaction)
-        for (int fb = 0; fb < kFast && T - t >= 64; ++fb) {
+        for (int fb = 0; fb < nfast && T - t >= 64; ++fb) {
           // (waves holding only empty slots skip the batch: sentinels stay sentinels)
           uint32_t sv = s[0], wk = 0xffffffffu;
           if ((tid & ~63) < m) {
@@ -351,47 +354,48 @@ __global__ __launch_bounds__(kEntryThreads) void k_np_entry(EntryArgs a,
           RSD_ETICK(2, 64);
         }
       } else if (kk == 64 && nr <= kRFast) {
-        // several slots per thread: the word from LDS, branch-free steps, each slot's wrap (at
-        // most one in 64 draws, as n1 > 64) logged after the batch
-        if (tid < 64) wbuf[tid] = wa;
-        __syncthreads();
-        uint32_t wk[kRFast];
+        // several slots per thread: branch-free steps, each slot's wrap (at most one in 64
+        // draws, as n1 > 64) logged after the batch; up to nfastm batches between compactions
+        // (member ranges change only at a compaction)
+        for (int fb = 0; fb < nfastm && T - t >= 64; ++fb) {
+          uint32_t wk[kRFast];
 #pragma unroll
-        for (int r = 0; r < kRFast; ++r) wk[r] = 0xffffffffu;
+          for (int r = 0; r < kRFast; ++r) wk[r] = 0xffffffffu;
 #pragma unroll 1
-        for (int k = 0; k < 64; ++k) {
-          const uint32_t w = wbuf[k];
+          for (int k = 0; k < 64; ++k) {
+            const uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wa), k));
+#pragma unroll
+            for (int r = 0; r < kRFast; ++r) {
+              if (r >= nr) break;
+              uint32_t sv = s[r];
+              sv -= draw_of<PY>(w, sv) <= sv ? 1u : 0u;
+              const bool z = sv == 0;
+              s[r] = z ? N1 : sv;
+              wk[r] = z ? static_cast<uint32_t>(k) : wk[r];
+            }
+          }
 #pragma unroll
           for (int r = 0; r < kRFast; ++r) {
             if (r >= nr) break;
-            uint32_t sv = s[r];
-            sv -= draw_of<PY>(w, sv) <= sv ? 1u : 0u;
-            const bool z = sv == 0;
-            s[r] = z ? N1 : sv;
-            wk[r] = z ? static_cast<uint32_t>(k) : wk[r];
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < kRFast; ++r) {
-          if (r >= nr) break;
-          const uint64_t wr = __ballot(wk[r] != 0xffffffffu);
-          if (wr) {
-            int base = 0;
-            if (lane == 0) base = atomicAdd(&sh_evn, __popcll(wr));
-            base = __shfl(base, 0);
-            if (wk[r] != 0xffffffffu) {
-              const int q = tid + r * kEntryThreads;
-              const int e = base + static_cast<int>(lane_rank(wr));
-              if (e < a.ecap)
-                ev[e] = make_uint2(static_cast<uint32_t>(t) + wk[r] + 1u,
-                                   lo[q] | (static_cast<uint32_t>(lo[q + 1 == m ? 0 : q + 1]) << 16));
+            const uint64_t wr = __ballot(wk[r] != 0xffffffffu);
+            if (wr) {
+              int base = 0;
+              if (lane == 0) base = atomicAdd(&sh_evn, __popcll(wr));
+              base = __shfl(base, 0);
+              if (wk[r] != 0xffffffffu) {
+                const int q = tid + r * kEntryThreads;
+                const int e = base + static_cast<int>(lane_rank(wr));
+                if (e < a.ecap)
+                  ev[e] = make_uint2(static_cast<uint32_t>(t) + wk[r] + 1u,
+                                     lo[q] | (static_cast<uint32_t>(lo[q + 1 == m ? 0 : q + 1]) << 16));
+              }
             }
           }
+          t += 64;
+          wa = wb;
+          wb = t + 64 + lane < T ? wp[t + 64 + lane] : 0u;
+          RSD_ETICK(1, 64);
         }
-        t += 64;
-        wa = wb;
-        wb = t + 64 + lane < T ? wp[t + 64 + lane] : 0u;
-        RSD_ETICK(1, 64);
       } else {
       if (tid < kk) wbuf[tid] = wa;
       __syncthreads();
