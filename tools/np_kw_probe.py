@@ -12,7 +12,11 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tsbb15-3d-reco
 from tsbb15_amd import _ffi  # noqa: E402
 
 kw = os.environ.get("RSAMD_NP_KW", "auto")
-for n, count, reps in ((2000, 100000, 6), (10000, 20000, 4)):
+cases = ((2000, 100000, 6), (10000, 20000, 4))
+only = os.environ.get("NP_ONLY")  # restrict to one N (kernel traces)
+for n, count, reps in cases:
+    if only and int(only) != n:
+        continue
     st = np.random.RandomState(1).get_state()
     key, pos = np.asarray(st[1], np.uint32), int(st[2])
     g = _ffi.np_choice_tuples_gpu(key, pos, n, 8, count)

@@ -950,23 +950,64 @@ __global__ __launch_bounds__(256) void k_np_starts(const uint2 *__restrict__ ev,
 // lanes have consecutive states, so the swap partners J[state - 1] land in LDS together.  The
 // trace keeps the k positions in wave-uniform registers: for state s >= 8 a position p < s can
 // only move to s (when J[s - 1] == p), found by a ballot over 64 states at a time.
-constexpr int kTupWaves = 4;
+#ifndef RSAMD_TUP_WAVES
+#define RSAMD_TUP_WAVES 4
+#endif
+constexpr int kTupWaves = RSAMD_TUP_WAVES;  // waves (hypotheses) per tuple workgroup
+#ifndef RSAMD_TUP_BLK
+#define RSAMD_TUP_BLK 128
+#endif
+// words per ring block (loaded one block ahead).  Measured (C2, k_np_tuples_wave per launch):
+// direct global loads per window 872 us; blocks of 64 / 128 / 256 / 512 / 1024 words 691 / 684
+// / 744 / 906 / 1099 us (the larger rings cost occupancy)
+constexpr int kTupBlk = RSAMD_TUP_BLK;
+constexpr int kTupRing = 2 * kTupBlk;       // words staged per wave
 template <bool PY>
 __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
     const uint32_t *__restrict__ draws, const int64_t *__restrict__ starts,
     const int64_t *__restrict__ got, int64_t lo, int64_t hi, int n1, int n1p, int kk,
-    int32_t *__restrict__ out, int *err) {
-  extern __shared__ uint16_t jl[];
+    int32_t *__restrict__ out, int *err, int64_t nwords) {
+  // per wave: a ring of kTupRing words of the hypothesis (blocks of kTupBlk words loaded one
+  // block ahead, so the window reads wait on LDS, not on HBM: the stream is far larger than
+  // the caches), then the swap partners J (uint16 x n1p)
+  extern __shared__ uint32_t tup_lds[];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
   // hypotheses [lo, hi) of the segment (those the caller asked for), out row h - lo
   const int64_t h = lo + static_cast<int64_t>(blockIdx.x) * kTupWaves + wv;
   if (h >= hi || h >= *got) return;  // wave-uniform; the kernel has no workgroup barrier
-  uint16_t *J = jl + static_cast<size_t>(wv) * n1p;
+  uint32_t *ring = tup_lds + static_cast<size_t>(wv) * (kTupRing + n1p / 2);
+  uint16_t *J = reinterpret_cast<uint16_t *>(ring + kTupRing);
   const int64_t a = starts[h], b = starts[h + 1];
+  const uint32_t *__restrict__ src = draws + a;
+  // read-ahead never leaves the stream allocation (nwords words from draws[0])
+  const int64_t lim = nwords - 1 - a;
+  auto ld = [&](int64_t x) { return src[x < lim ? x : lim]; };
+  constexpr int kPerLane = kTupBlk / 64;
+  uint32_t nb[kPerLane];
+#pragma unroll
+  for (int k = 0; k < kPerLane; ++k) nb[k] = ld(64 * k + l);
+#pragma unroll
+  for (int k = 0; k < kPerLane; ++k) ring[64 * k + l] = nb[k];
+#pragma unroll
+  for (int k = 0; k < kPerLane; ++k) nb[k] = ld(kTupBlk + 64 * k + l);
+  int filled = kTupBlk;  // words of the hypothesis in the ring (relative to a); one block in flight
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const uint64_t below = (1ull << l) - 1ull;
   uint32_t i = static_cast<uint32_t>(n1);
-  int64_t d = a;
+  int o = 0;  // words parsed
   while (i > 0) {
+    if (o + 64 > filled) {  // the block in flight lands in the ring; the next one is issued
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k) ring[(filled + 64 * k + l) & (kTupRing - 1)] = nb[k];
+#pragma unroll
+      for (int k = 0; k < kPerLane; ++k) nb[k] = ld(filled + kTupBlk + 64 * k + l);
+      filled += kTupBlk;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
     // states i .. i - L + 1 share the draw rule's mask / shift
     uint32_t L, msk = 0, sh = 0;
     if constexpr (PY) {
@@ -978,7 +1019,8 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
     }
     const int W = L < 64u ? static_cast<int>(L) : 64;
     const bool in = l < W;
-    const uint32_t u = in ? (PY ? (draws[d + l] >> sh) : (draws[d + l] & msk)) : 0xffffffffu;
+    const uint32_t wd = ring[(o + l) & (kTupRing - 1)];
+    const uint32_t u = in ? (PY ? (wd >> sh) : (wd & msk)) : 0xffffffffu;
     const uint32_t lo_s = i - static_cast<uint32_t>(l);
     uint64_t acc = __ballot(in && u <= lo_s);
     uint64_t amb = __ballot(in && u > lo_s && u <= i);
@@ -992,8 +1034,9 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
     if ((acc >> l) & 1ull)
       J[i - static_cast<uint32_t>(__popcll(acc & below)) - 1u] = static_cast<uint16_t>(u);
     i -= static_cast<uint32_t>(__popcll(acc));
-    d += W;
+    o += W;
   }
+  const int64_t d = a + o;
   if (d != b) {
     if (l == 0) atomicOr(err, 2);
     return;
@@ -1192,7 +1235,7 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
     return v >= kWmin && v <= kWmax ? v : 0;
   }();
   const int64_t Cmax = kSegWords / kWmin + 1;
-  const int64_t tup_lds = static_cast<int64_t>(sizeof(uint16_t)) * ((n1 + 1) & ~1) * kTupWaves;
+  const int64_t tup_lds = (static_cast<int64_t>(sizeof(uint32_t)) * kTupRing + static_cast<int64_t>(sizeof(uint16_t)) * ((n1 + 1) & ~1)) * kTupWaves;
   if (tup_lds > w.tup_lds) {
     HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_np_tuples_wave<false>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(tup_lds)));
@@ -1312,9 +1355,9 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
     if (hi > lo) {
       const int n1p = (n1 + 1) & ~1;
       (py ? k_np_tuples_wave<true> : k_np_tuples_wave<false>)<<<static_cast<unsigned>((hi - lo + kTupWaves - 1) / kTupWaves), 64 * kTupWaves,
-                         sizeof(uint16_t) * n1p * kTupWaves, s>>>(
+                         static_cast<size_t>(tup_lds), s>>>(
           w.d_stream + *pos, w.d_starts, &w.d_res->got, lo, hi, n1, n1p, k,
-          d_out + (done + lo - skip) * k, w.d_err);
+          d_out + (done + lo - skip) * k, w.d_err, kSegWords - *pos);
       HIP_TRY(hipGetLastError());
     }
     // 7: delivered count, draws used, errors and the stream block holding the next word
