@@ -709,7 +709,8 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_np_track(EntryArgs a,
   __shared__ uint32_t s_w[2][kCheck];
   __shared__ uint32_t s_st[64], s_lo[64];
   __shared__ int s_m, s_evn;
-  constexpr int kPer = kCheck / (64 * kTrackWaves);  // draws per thread per interval
+  constexpr int kStride = 64 * kTrackWaves;
+  constexpr int kPer = (kCheck + kStride - 1) / kStride;  // draws per thread per interval
   const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = uni(tid >> 6);
   const int wq = wv;  // (rotating the busy wave across SIMDs by chunk: measured, no change)
   int m = a.fin_m[c];
@@ -737,20 +738,21 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_np_track(EntryArgs a,
   uint32_t nx[kPer];
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
-    const int x = t + k * 64 * kTrackWaves + tid;
-    nx[k] = x < T ? wp[x] : 0u;
+    const int j = k * kStride + tid, x = t + j;
+    nx[k] = j < kCheck && x < T ? wp[x] : 0u;
   }
   int buf = 0;
   while (t < T) {
     const int cp = min(T, t + kCheck);
     uint32_t *sw = s_w[buf];
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) sw[k * 64 * kTrackWaves + tid] = nx[k];
+    for (int k = 0; k < kPer; ++k)
+      if (k * kStride + tid < kCheck) sw[k * kStride + tid] = nx[k];
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {  // the next interval's draws
-      const int x = cp + k * 64 * kTrackWaves + tid;
-      nx[k] = x < T ? wp[x] : 0u;
+      const int j = k * kStride + tid, x = cp + j;
+      nx[k] = j < kCheck && x < T ? wp[x] : 0u;
     }
     // this wave's trajectories q = wv, wv + 8, ... advance together (independent fixed-point
     // chains interleaved: the latency of one round is shared by up to kTrackSlots of them)
