@@ -610,21 +610,21 @@ __device__ __forceinline__ uint64_t window_step(uint32_t w, uint64_t wm, uint32_
 // tools/ubench/amb_bench2.hip: 5.1 cycles per draw for one wave alone, against 7.9 for the
 // earlier 256-draw windows read from LDS at the top of each step.)
 template <bool PY, bool SMALL>
-__device__ __forceinline__ void track_window(const EntryArgs &a, uint32_t w, int *s_evn, uint2 *ev,
+__device__ __forceinline__ void track_window(int n1, int ecap, uint32_t w, int *s_evn, uint2 *ev,
                                              uint32_t &i, uint32_t range, int d, int cp) {
   const int lane = threadIdx.x & 63;
   const int Wn = min(64, cp - d);
   const uint64_t wm = Wn == 64 ? ~0ull : ((1ull << Wn) - 1ull);
   uint64_t wr;
   uint32_t sl;
-  (void)window_step<PY, SMALL>(w, wm, i, a.n1, wr, sl);
+  (void)window_step<PY, SMALL>(w, wm, i, n1, wr, sl);
   if (wr) {  // hypothesis ends: the next hypothesis starts at the following draw
     int eb = 0;
     if (lane == 0) eb = atomicAdd(s_evn, __popcll(wr));
     eb = __shfl(eb, 0);
     if (((wr >> lane) & 1ull)) {
       const int e = eb + static_cast<int>(lane_rank(wr));
-      if (e < a.ecap) ev[e] = make_uint2(static_cast<uint32_t>(d + lane + 1), range);
+      if (e < ecap) ev[e] = make_uint2(static_cast<uint32_t>(d + lane + 1), range);
     }
   }
 }
@@ -634,6 +634,7 @@ __device__ __forceinline__ uint32_t track_one(const EntryArgs &a, const uint32_t
                                               uint2 *ev, uint32_t i, uint32_t range, int t,
                                               int cp) {
   const int lane = threadIdx.x & 63;
+  const int n1 = uni(a.n1), ecap = uni(a.ecap);  // in SGPRs for the whole loop
   constexpr int kAhead = 4;
   // lanes beyond cp read words of the wrapped buffer: never accepted (wm)
   uint32_t q[kAhead];
@@ -645,7 +646,7 @@ __device__ __forceinline__ uint32_t track_one(const EntryArgs &a, const uint32_t
       const uint32_t w = q[k];
       q[k] = sw[(d - t + 64 * (kAhead + k) + lane) & (kCheck - 1)];
       const int dk = d + 64 * k;
-      if (dk < cp) track_window<PY, SMALL>(a, w, s_evn, ev, i, range, dk, cp);
+      if (dk < cp) track_window<PY, SMALL>(n1, ecap, w, s_evn, ev, i, range, dk, cp);
     }
   }
   return i;
