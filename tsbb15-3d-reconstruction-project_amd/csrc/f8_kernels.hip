@@ -232,7 +232,9 @@ __global__ __launch_bounds__(256) void k_f8_count(const Pt *__restrict__ pts, in
 // (4.35 vs 4.36 ms, tools/probe_c5_count.py): the issue slots are not what binds.  Slices
 // shrinking with the wave index (slice w covering total x (1 - (1 - w/W)^p), so the last waves
 // to start carry the least work) were slower too: 0.103-0.108 ms at p = 1.3-2.0 against
-// 0.098-0.101 for equal slices, interleaved runs on one box (round 2).
+// 0.098-0.101 for equal slices, interleaved runs on one box (round 2).  Points loaded four at a
+// time (16 SGPRs per load group: 90 SGPRs, 7-8 waves per SIMD) were not faster either:
+// 97.0-99.3 us against 96.9-97.1 us, with 6 144 / 7 168 / 8 192 resident-wave launch shapes.
 // ----------------------------------------------------------------------------------------
 
 // The float64 test of k_f8_count (pixel units) for one (hypothesis, point).
