@@ -197,3 +197,41 @@ def test_solvepnpransac_rejects_bad_input(ctx):
     ok, r, t, inl = cv.solvePnPRansac(X[:12], rs.uniform(0, 2000, (12, 2)), K, None,
                                       reprojectionError=1e-6)
     assert not ok and inl is None
+
+
+def test_p3p_solvepnp_iterative(ctx):
+    """pnp.p3p = cv.solvePnP(SOLVEPNP_ITERATIVE) over all points (pnp.py:7-10): known answers
+    on noise-free BAdino2 views, and on a noisy view the LM refinement never raises the pixel
+    reprojection error of its DLT start and lands near the true pose.  OpenCV parity unpinned."""
+    z = golden("dino_pnp_kat.npz")
+    for v in (1, 20):
+        X, uv, _ = _view(z, v)
+        R, t = pnp.p3p(X, uv, z["K"][v])
+        np.testing.assert_allclose(R, z["R"][v], atol=1e-7)
+        np.testing.assert_allclose(t, z["t"][v], rtol=1e-6, atol=1e-7)
+        ok, rv, tv = cv.solvePnP(X, uv, z["K"][v], np.zeros((4, 1)))
+        assert ok and rv.shape == (3, 1) and tv.shape == (3, 1)
+    # noisy pixels: refinement against the DLT start
+    X, uv, _ = _view(z, 5)
+    K = z["K"][5]
+    rs = np.random.RandomState(3)
+    uvn = uv + rs.normal(0.0, 0.7, uv.shape)
+    ok, rv, tv = cv.solvePnP(X, uvn, K, None)
+    assert ok
+    err = np.sum((cv.project_points(X, rv, tv, K) - uvn) ** 2)
+    c = X.mean(axis=0)
+    s = np.sqrt(np.mean(np.sum((X - c) ** 2, axis=1)))
+    y = (np.linalg.inv(K) @ np.vstack([uvn.T, np.ones((1, len(uvn)))])).T
+    Rd, td = pnp.pnp_minimize((X - c) / s, y, len(X))
+    rd, _ = cv.Rodrigues(Rd)
+    err_dlt = np.sum((cv.project_points(X, rd, s * td - Rd @ c, K) - uvn) ** 2)
+    err_true = np.sum((cv.project_points(X, cv.Rodrigues(z["R"][5])[0], z["t"][5], K) - uvn) ** 2)
+    assert err <= err_dlt * (1 + 1e-12)
+    assert err <= err_true * (1 + 1e-9)  # the least-squares pose fits the noisy pixels best
+    R, _ = cv.Rodrigues(rv)
+    assert np.linalg.norm(R - z["R"][5]) < 1e-2
+    # the guess path starts from the given pose; too few points without a guess raises
+    ok, rv2, tv2 = cv.solvePnP(X, uvn, K, None, rv, tv, useExtrinsicGuess=True)
+    assert ok and np.allclose(rv2, rv, atol=1e-6) and np.allclose(tv2, tv, atol=1e-6)
+    with pytest.raises(ValueError):
+        cv.solvePnP(X[:5], uvn[:5], K, None)

@@ -127,3 +127,53 @@ def solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec=Non
     rv, _ = Rodrigues(last_ransac["R"])
     rv, tv = _refine_lm(X[inl], uv[inl], K, rv, np.array(res.t[:]))
     return True, rv.reshape(3, 1), tv.reshape(3, 1), inl.astype(np.int32).reshape(-1, 1)
+
+
+SOLVEPNP_ITERATIVE = 0
+
+
+def solvePnP(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec=None, tvec=None,
+             useExtrinsicGuess=False, flags=SOLVEPNP_ITERATIVE, ctx=None):
+    """``cv.solvePnP`` with OpenCV's SOLVEPNP_ITERATIVE semantics, the call behind the
+    reference's ``pnp.p3p`` (pnp.py:7-10): the pose over ALL correspondences, initialised by the
+    DLT (rs_pnp_dlt on the GPU; world points centred and RMS-scaled first, the conditioning
+    OpenCV's DLT initialisation applies too) -- or by (rvec, tvec) when ``useExtrinsicGuess`` --
+    then refined by Levenberg-Marquardt on the pixel reprojection error.  Returns
+    ``(retval, rvec (3,1), tvec (3,1))``.  Zero distortion only; m >= 6 (the DLT; OpenCV's
+    ITERATIVE also needs >= 6 non-coplanar points for its DLT start).  OpenCV is absent here,
+    so parity with it is unpinned; the tests check the known answers (noise-free BAdino2
+    views) and that the refinement never raises the reprojection error of its start."""
+    if flags != SOLVEPNP_ITERATIVE:
+        raise ValueError("only SOLVEPNP_ITERATIVE is provided")
+    X = np.ascontiguousarray(np.asarray(objectPoints, dtype=np.float64).reshape(-1, 3))
+    uv = np.ascontiguousarray(np.asarray(imagePoints, dtype=np.float64).reshape(-1, 2))
+    if len(X) != len(uv):
+        raise ValueError("objectPoints and imagePoints must have the same count")
+    if distCoeffs is not None and np.any(np.asarray(distCoeffs) != 0):
+        raise ValueError("only zero lens distortion is supported")
+    K = np.asarray(cameraMatrix, dtype=np.float64).reshape(3, 3)
+    if useExtrinsicGuess and rvec is not None and tvec is not None:
+        r0 = np.asarray(rvec, dtype=np.float64).reshape(3, 1)
+        t0 = np.asarray(tvec, dtype=np.float64).reshape(3, 1)
+    else:
+        if len(X) < 6:
+            raise ValueError("SOLVEPNP_ITERATIVE needs at least 6 non-coplanar points for its DLT start")
+        c = X.mean(axis=0)
+        s = float(np.sqrt(np.mean(np.sum((X - c) ** 2, axis=1)))) or 1.0
+        Xc = np.ascontiguousarray((X - c) / s)
+        y = np.linalg.solve(K, np.vstack([uv.T, np.ones((1, len(uv)))])).T
+        y = np.ascontiguousarray(y)
+        R = np.empty(9)
+        t = np.empty(3)
+        _ffi.check(_ffi.lib().rs_pnp_dlt((ctx or _ffi.default_context()).handle,
+                                         _ffi.ptr(Xc, _ffi.C.c_double), _ffi.ptr(y, _ffi.C.c_double),
+                                         len(X), _ffi.ptr(R, _ffi.C.c_double),
+                                         _ffi.ptr(t, _ffi.C.c_double)))
+        R = R.reshape(3, 3)
+        if not np.all(np.isfinite(R)):
+            return False, None, None
+        # the conditioned frame: x = s x' + c, so R x + t = s (R x' + t') gives t = s t' - R c
+        r0, _ = Rodrigues(R)
+        t0 = (s * t - R @ c).reshape(3, 1)
+    rv, tv = _refine_lm(X, uv, K, r0, t0)
+    return True, np.asarray(rv, dtype=np.float64).reshape(3, 1), np.asarray(tv, dtype=np.float64).reshape(3, 1)

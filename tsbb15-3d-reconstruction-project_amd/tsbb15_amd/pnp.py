@@ -4,9 +4,12 @@
     reference): m >= 6 world points (m, 3) or homogeneous (m, 4) and C-normalised homogeneous
     image points (m, 3); rows vec(r_l x_k^T) of [y_k]_x (first two rows, pnp.py:152), null
     vector, tau = sign det A, R = U V^T of tau A, lambda = 3 tau / tr S, t = lambda b.
-  * ``p3p(_3d_pts, img_pts, K)``  pnp.py:7-10 wraps OpenCV's solvePnP; OpenCV is absent, so
-    this normalises the pixel points with K and returns the DLT pose over all points (needs
-    >= 6 points).  Parity with OpenCV is unpinned.
+  * ``p3p(_3d_pts, img_pts, K)``  pnp.py:7-10 wraps OpenCV's solvePnP(SOLVEPNP_ITERATIVE);
+    OpenCV is absent, so this runs ``cv.solvePnP``: the conditioned DLT pose over all points
+    (needs >= 6) refined by Levenberg-Marquardt on the pixel reprojection error, returned as
+    (R (3,3), t (3,)).  (The reference's own unpacking ``R, t = cv2.solvePnP(...)`` of a
+    3-tuple would raise; the drop-in returns the pose the call site wants.)  Parity with
+    OpenCV is unpinned.
 The Lambda-Twist fragments (pnp.py:13-121) are unfinished and never called: not provided.
 """
 from __future__ import annotations
@@ -52,8 +55,12 @@ def pnp_minimize(_3d_pts, img_pts, m):
 
 
 def p3p(_3d_pts, img_pts, K):
+    from . import cv
+
     X = np.asarray(_3d_pts, dtype=np.float64).reshape(-1, 3)
     uv = np.asarray(img_pts, dtype=np.float64).reshape(-1, 2)
-    y = (np.linalg.inv(np.asarray(K, dtype=np.float64)) @
-         np.vstack([uv.T, np.ones((1, len(uv)))])).T
-    return pnp_minimize(X, y, len(X))
+    ok, rv, tv = cv.solvePnP(X, uv, K, None)
+    if not ok:
+        raise ValueError("solvePnP failed (degenerate point set)")
+    R, _ = cv.Rodrigues(rv)
+    return R, tv.reshape(3)
