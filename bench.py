@@ -32,6 +32,23 @@ sys.path.insert(0, REPO)
 
 from tsbb15_amd import _ffi, synth  # noqa: E402
 
+
+class _stdout_to_stderr:
+    """RCCL prints a version banner on the process's stdout (C stdio) at communicator set-up;
+    the bench's stdout carries exactly one JSON line, so file descriptor 1 points at stderr
+    while the library runs (C stdio flushed before it is restored)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        ctypes.CDLL(None).fflush(None)
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
+
 METRIC = "RANSAC hypotheses/sec (8-pt F, 2k corr) at 1/2/4/8 GPUs; % HBM roofline"
 N_CORR = 2000
 OUTLIERS = 0.30
@@ -422,10 +439,12 @@ def main():
         uid = np.zeros(_ffi.COMM_ID_BYTES, np.uint8)
         st = 0
         if rank == 0:
-            st = _ffi.lib().rs_comm_unique_id(_ffi.ptr(uid, ctypes.c_uint8))
+            with _stdout_to_stderr():
+                st = _ffi.lib().rs_comm_unique_id(_ffi.ptr(uid, ctypes.c_uint8))
         uid = np.frombuffer(dist.bcast_bytes(uid.tobytes()), np.uint8).copy()
         if st == 0:
-            st = _ffi.lib().rs_comm_init(ctx.handle, world, rank, _ffi.ptr(uid, ctypes.c_uint8))
+            with _stdout_to_stderr():
+                st = _ffi.lib().rs_comm_init(ctx.handle, world, rank, _ffi.ptr(uid, ctypes.c_uint8))
         ok = dist.max(0.0 if st == 0 else 1.0) == 0.0   # every rank agrees on the transport
         if ok:
             exchange = "rccl all-gather"
