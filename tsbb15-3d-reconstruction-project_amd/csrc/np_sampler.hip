@@ -851,15 +851,19 @@ __global__ __launch_bounds__(64) void k_np_filter(uint2 *__restrict__ ev, const 
 // ---- 4. compose the chunk maps on the GPU ------------------------------------------------
 // Chunk c's final list maps entry list index a (state n1 - a) to the state of the entry with the
 // largest start lo <= a (cyclically: the largest lo overall if none); chunk 0 starts a
-// hypothesis (a = 0).  Keys lo << 16 | state: their maximum is the wanted entry.  The whole
-// workgroup stages the first 64 entries of kComposeBlock chunks at a time in LDS (coalesced),
-// then wave 0 walks them serially; longer lists (chunks that ended dense) are read from HBM.
+// hypothesis (a = 0).  The whole workgroup stages kComposeBlock chunks at a time in LDS
+// (coalesced), then wave 0 walks them serially.  (C2, 512 chunks: 187 us with a key-maximum
+// shuffle reduction per chunk, 101 us with the rotated rows and one ballot per chunk.)
 constexpr int kComposeBlock = 256;
+// Rows of <= 64 entries are first rotated (by all 16 waves, in parallel) so that lo ascends
+// along the lanes; the serial walk of wave 0 is then one ballot per chunk: the wanted entry is
+// the highest lane with lo <= a (none: the last lane, the largest lo).  Longer lists (chunks
+// that ended dense) take the key-maximum scan from HBM.
 __global__ __launch_bounds__(1024) void k_np_compose(const uint32_t *__restrict__ fin,
                                                      const int *__restrict__ fin_m, int n1, int C,
                                                      int *__restrict__ ent) {
   __shared__ uint32_t rows[kComposeBlock][64];
-  __shared__ int ms[kComposeBlock];
+  __shared__ int ms[kComposeBlock], es[kComposeBlock];
   const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
   int a = 0;
   for (int c0 = 0; c0 < C; c0 += kComposeBlock) {
@@ -868,16 +872,40 @@ __global__ __launch_bounds__(1024) void k_np_compose(const uint32_t *__restrict_
     __syncthreads();
     for (int r = wv; r < nb; r += 16) {
       const int m = ms[r];
-      rows[r][l] = l < m ? fin[static_cast<size_t>(c0 + r) * n1 + l] : 0u;
+      if (m > 64) continue;
+      const uint32_t x = l < m ? fin[static_cast<size_t>(c0 + r) * n1 + l] : 0xffffffffu;
+      // the lane holding the smallest lo starts the rotated row
+      uint32_t mn = x & 0xffffu;
+#pragma unroll
+      for (int o = 32; o; o >>= 1) mn = min(mn, static_cast<uint32_t>(__shfl_xor(static_cast<int>(mn), o)));
+      const uint64_t at = __ballot(l < m && (x & 0xffffu) == mn);
+      const int p0 = __ffsll(static_cast<long long>(at)) - 1;
+      if (l < m) rows[r][l - p0 >= 0 ? l - p0 : l - p0 + m] = x;
     }
     __syncthreads();
     if (wv == 0) {
+      // the next row is read while the current one is walked (the walk is the serial chain)
+      uint32_t xn = rows[0][l];
+      int mn = ms[0];
       for (int r = 0; r < nb; ++r) {
-        const int c = c0 + r, m = ms[r];
+        const int c = c0 + r, m = mn;
+        const uint32_t xr = xn;
+        if (r + 1 < nb) {
+          xn = rows[r + 1][l];
+          mn = ms[r + 1];
+        }
+        es[r] = a;  // (every lane writes the same value)
+        if (m <= 64) {
+          const uint32_t x = l < m ? xr : 0xffffffffu;
+          const uint64_t le = __ballot(l < m && static_cast<int>(x & 0xffffu) <= a);
+          const int idx = le ? 63 - __builtin_clzll(le) : m - 1;
+          a = n1 - static_cast<int>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), idx)) >> 16);
+          continue;
+        }
         uint32_t kb = 0, kt = 0;
         bool hb = false, ht = false;
         for (int k = l; k < m; k += 64) {
-          const uint32_t x = k < 64 ? rows[r][k] : fin[static_cast<size_t>(c) * n1 + k];
+          const uint32_t x = fin[static_cast<size_t>(c) * n1 + k];
           const uint32_t lo = x & 0xffffu, key = (lo << 16) | (x >> 16);
           if (static_cast<int>(lo) <= a && (!hb || key > kb)) kb = key, hb = true;
           if (!ht || key > kt) kt = key, ht = true;
@@ -890,11 +918,11 @@ __global__ __launch_bounds__(1024) void k_np_compose(const uint32_t *__restrict_
           mb = max(mb, static_cast<uint32_t>(__shfl_xor(static_cast<int>(mb), o)));
           mt = max(mt, static_cast<uint32_t>(__shfl_xor(static_cast<int>(mt), o)));
         }
-        if (l == 0) ent[c] = a;
         a = n1 - static_cast<int>((anyb ? mb : mt) & 0xffffu);
       }
     }
     __syncthreads();
+    for (int k = tid; k < nb; k += 1024) ent[c0 + k] = es[k];
   }
 }
 
