@@ -182,7 +182,8 @@ __global__ __launch_bounds__(256 * kJumpGroups) void k_mt_jump(uint32_t *__restr
 
 // ---- 2. stream: generator g owns blocks (g kJB, (g+1) kJB] plus words 1..623 of its window --
 // 256 threads: a block is the three dependent runs of the recurrence (227, 227, 170 words),
-// one word per thread each, then tempered and stored; the two LDS blocks alternate.
+// one word per thread each, then tempered and stored; the two LDS blocks alternate.  (One wave
+// per generator with wave-level fences instead of barriers: 1.45 ms against 0.61 at C2.)
 __global__ __launch_bounds__(256) void k_mt_stream(const uint32_t *__restrict__ win,
                                                    uint32_t *__restrict__ stream, int64_t Lb) {
   __shared__ uint32_t bb[2][kN];
