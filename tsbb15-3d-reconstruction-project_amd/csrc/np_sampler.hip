@@ -267,8 +267,8 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
   extern __shared__ uint16_t dyn[];
   __shared__ uint32_t wbuf[kK];
   __shared__ int sh_red[kEntryThreads / 64];
-  __shared__ int sh_head, sh_evn;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  __shared__ int sh_evn;
+  const int tid = threadIdx.x, lane = tid & 63;
   const int n1 = a.n1, n1p = (n1 + 1) & ~1;
   uint16_t *st = dyn, *lo = dyn + n1p, *st2 = dyn + 2 * n1p, *lo2 = dyn + 3 * n1p;
   const int c = blockIdx.x;
@@ -423,51 +423,36 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
       wb = t + 64 + lane < T ? wp[t + 64 + lane] : 0u;
       RSD_ETICK(0, kk);
       }
-      // compaction: list order starts at the head (first slot of the maximum run); equal
-      // neighbours merge, the first keeps its lo
+      // compaction: equal cyclic neighbours merge, the first of a run keeps its lo (the list
+      // stays in cyclic order; where it starts does not matter, so no rotation to a run head:
+      // two barriers and a block reduction fewer per compaction); all equal: one survivor
       __syncthreads();
-      int lmax = 0;
 #pragma unroll
       for (int r = 0; r < kR; ++r) {
         if (r >= nr) break;
         const int q = tid + r * kEntryThreads;
-        if (q < m) {
-          st[q] = static_cast<uint16_t>(s[r]);
-          lmax = max(lmax, static_cast<int>(s[r]));
-        }
-      }
-#pragma unroll
-      for (int o = 32; o; o >>= 1) lmax = max(lmax, __shfl_xor(lmax, o));
-      if (lane == 0) sh_red[wid] = lmax;
-      if (tid == 0) sh_head = 0;
-      __syncthreads();
-      int mx = 0;
-#pragma unroll
-      for (int w = 0; w < kEntryThreads / 64; ++w) mx = max(mx, sh_red[w]);
-      for (int q = tid; q < m; q += kEntryThreads) {
-        const int pq = q == 0 ? m - 1 : q - 1;
-        if (st[q] == mx && st[pq] != mx) sh_head = q;
+        if (q < m) st[q] = static_cast<uint16_t>(s[r]);
       }
       __syncthreads();
-      const int h = sh_head;
       const int per = (m + kEntryThreads - 1) / kEntryThreads;
       const int k0 = min(m, tid * per), k1 = min(m, k0 + per);
       int cnt = 0;
-      for (int k = k0; k < k1; ++k) {
-        const int p = h + k < m ? h + k : h + k - m;
-        const int pp = p == 0 ? m - 1 : p - 1;
-        cnt += (k == 0 || st[p] != st[pp]) ? 1 : 0;
-      }
+      for (int p = k0; p < k1; ++p) cnt += st[p] != st[p == 0 ? m - 1 : p - 1] ? 1 : 0;
       int total;
       int o = block_excl_scan(cnt, sh_red, &total);
-      for (int k = k0; k < k1; ++k) {
-        const int p = h + k < m ? h + k : h + k - m;
-        const int pp = p == 0 ? m - 1 : p - 1;
-        if (k == 0 || st[p] != st[pp]) {
+      for (int p = k0; p < k1; ++p) {
+        if (st[p] != st[p == 0 ? m - 1 : p - 1]) {
           st2[o] = st[p];
           lo2[o] = lo[p];
           ++o;
         }
+      }
+      if (total == 0) {  // every trajectory in one state: one survivor covering every entry
+        if (tid == 0) {
+          st2[0] = st[0];
+          lo2[0] = lo[0];
+        }
+        total = 1;
       }
       __syncthreads();
       uint16_t *x = st;
