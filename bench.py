@@ -67,50 +67,29 @@ def dist_env():
 
 
 class Dist:
-    """Barrier / max-reduce / broadcast for the harness (gloo on the host); the data-path
-    exchange uses RCCL through librsamd."""
+    """Barrier / max-reduce / broadcast for the harness, without torch.distributed: a TCP hub
+    on MASTER_PORT + 1 (tsbb15_amd.parallel.TcpHub; torch.distributed.run's own store holds
+    MASTER_PORT).  Nothing in this process imports torch, so librsamd's librccl.so resolves
+    through its RUNPATH to /opt/rocm/lib (config.exchange_library records which one ran)."""
 
     def __init__(self, world):
+        from tsbb15_amd import parallel
         self.world = world
-        self.pg = None
-        if world > 1:
-            import torch.distributed as dist
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            # gloo prints its connection banner on fd 1: keep stdout for the one JSON line
-            sys.stdout.flush()
-            saved = os.dup(1)
-            os.dup2(2, 1)
-            try:
-                dist.init_process_group("gloo")
-                dist.barrier()
-            finally:
-                sys.stdout.flush()
-                os.dup2(saved, 1)
-                os.close(saved)
-            self.dist = dist
+        self.hub = parallel.TcpHub.from_env() if world > 1 else None
 
     def barrier(self):
-        if self.world > 1:
-            self.dist.barrier()
+        if self.hub:
+            self.hub.barrier()
 
     def max(self, x):
-        if self.world == 1:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
+        return float(x) if self.hub is None else self.hub.max_float(x)
 
     def bcast_bytes(self, b, src=0):
-        if self.world == 1:
-            return b
-        obj = [b]
-        self.dist.broadcast_object_list(obj, src=src)
-        return obj[0]
+        return b if self.hub is None else self.hub.broadcast_bytes(b, src)
 
     def close(self):
-        if self.world > 1:
-            self.dist.destroy_process_group()
+        if self.hub:
+            self.hub.close()
 
 
 def _cpu_worker(args):
@@ -165,20 +144,18 @@ class _CtxComm:
         return [recv[i * n:(i + 1) * n].tobytes() for i in range(self.world)]
 
 
-class _GlooComm:
-    """Fallback record exchange over the harness's gloo group, used only if the RCCL
+class _HubComm:
+    """Fallback record exchange over the harness's TCP hub, used only if the RCCL
     communicator cannot be created (reported as config.exchange)."""
 
     def __init__(self, dist, rank, world):
-        self.dist, self.rank, self.world = dist, rank, world
+        self.hub, self.rank, self.world = dist.hub, rank, world
 
     def allgather_bytes(self, b):
-        out = [None] * self.world
-        self.dist.dist.all_gather_object(out, b)
-        return out
+        return self.hub.allgather_bytes(b)
 
     def allreduce_max_int(self, v):
-        return int(self.dist.max(float(v)))
+        return self.hub.allreduce_max_int(v)
 
 
 class _Solo:
@@ -420,7 +397,7 @@ def main():
         cp1, cp2, _ = synth.two_view(args.n, OUTLIERS, seed=1)
         cpu = cpu_baseline(cp1, cp2, args.cpu_seconds, args.cpu_procs)
     # RSAMD_BENCH_DEVICE pins every rank to one device: a multi-rank rehearsal on a one-GPU
-    # box (RCCL refuses two ranks on one GPU, so that run exercises the gloo exchange)
+    # box (RCCL refuses two ranks on one GPU, so that run exercises the TCP-hub exchange)
     ctx = _ffi.Context(int(os.environ.get("RSAMD_BENCH_DEVICE", local_rank)))
 
     # one synthetic pair per rank (weak scaling: per-GPU work fixed); p0_* is rank 0's pair
@@ -453,12 +430,20 @@ def main():
             if st == 0:
                 _ffi.lib().rs_comm_destroy(ctx.handle)
             print(f"warning: RCCL communicator init failed on some rank (status {st}: {_ffi.lib().rs_last_error().decode(errors='replace')}); "
-                  "exchanging the per-pair records over gloo", file=sys.stderr)
-            exchange = "gloo all-gather (RCCL init failed)"
-            xcomm = _GlooComm(dist, rank, world)
+                  "exchanging the per-pair records over the TCP hub", file=sys.stderr)
+            exchange = "tcp-hub all-gather (RCCL init failed)"
+            xcomm = _HubComm(dist, rank, world)
         # the first collective on a communicator sets up its channels (lazy, can take far
         # longer than the timed steps): do it before the timed region
         xcomm.allgather_bytes(np.zeros(96, np.uint8).tobytes())
+
+    rccl_lib = None
+    if comm:
+        try:
+            v, path = _ffi.rccl_library()
+            rccl_lib = {"version": v, "path": path, "torch_imported": "torch" in sys.modules}
+        except Exception as e:  # noqa: BLE001
+            rccl_lib = {"error": repr(e)}
 
     def step(i):
         # one full RANSAC run; runs are stream-ordered and issued back to back (each run
@@ -517,7 +502,8 @@ def main():
                                "threshold 1.5 px",
                    "n_corr": args.n, "hypotheses_per_step": H, "sampler": "philox (throughput)",
                    "parallelism": f"pairs sharded, {world} pair(s) on {world} GPU(s)",
-                   "exchange": exchange},
+                   "exchange": exchange, "exchange_library": rccl_lib,
+                   "harness": "tcp hub (no torch.distributed)" if world > 1 else "one process"},
         "roofline": {"bound": "valu", "kernel": COUNT_KERNEL["fp64" if os.environ.get("RSAMD_COUNT") == "fp64"
                                                          else "fp32"],
                      "achieved": achieved, "peak": PEAK_FP32_VALU_TFLOPS, "unit": "TFLOP/s",
@@ -587,21 +573,29 @@ def main():
                       "tracking, per-hypothesis swap trace), then the same GPU pipeline; one "
                       "pair per rank"}
         if world > 1:
+            # ONE pair's H hypotheses over all ranks with the stream parse itself split: each
+            # rank parses its share of the chunks, the chunk maps are all-gathered and composed
+            # everywhere, each rank evaluates the hypotheses starting in its share
             c = xcomm
-            ev = parallel.GpuSliceEvaluator(ctx, p0_1, p0_2, H, max_slice=H // world + 1)
+            sp = _ffi.F8Plan(ctx, args.n, H)
+            sp.set_points(p0_1, p0_2)
+            sh = _ffi.NpShard(ctx, args.n, 8, world, rank)
             ts = []
             for _ in range(4):
                 dist.barrier()
                 t = time.perf_counter()
-                best, _, _ = parallel.ransac_f_sharded_np(c, p0_1, p0_2, H, key0, pos0, ev)
+                best, _, _ = parallel.ransac_f_split_np(c, ctx, p0_1, p0_2, H, key0, pos0,
+                                                        plan=sp, shard=sh)
                 ts.append(dist.max(time.perf_counter() - t))
-            ev.close()
+            sh.close()
+            sp.close()
             pm["sharded"] = {"value": H / min(ts[1:]), "unit": "hypotheses/s",
                              "ms": 1e3 * min(ts[1:]), "scaling": "strong", "n_gpus": world,
                              "best_index": int(best["index"]) if best is not None else -1,
-                             "note": "one pair's H hypotheses over all ranks: each parses the "
-                                     "whole stream, evaluates its slice; c* all-reduce + "
-                                     "candidate all-gather"}
+                             "note": "one pair's H hypotheses over all ranks, the numpy stream "
+                                     "parse split by chunk (rs_np_shard_*: per-rank parse, "
+                                     "all-gather + compose of the chunk maps, start-count scan), "
+                                     "then the c* all-reduce + candidate all-gather"}
         if rank == 0 and world == 1:
             th = []
             for _ in range(2):

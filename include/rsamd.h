@@ -101,6 +101,36 @@ int rs_np_choice_tuples_gpu(rs_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int6
 int rs_py_shuffle_tuples_gpu(rs_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int64_t n,
                              int32_t k, int64_t count, int32_t *out);
 
+/* Sharded parity stream ("the host sampler must emit tuples in stream order
+ * and hand each GPU its slice; that serial step is the scaling limiter").  The numpy (py = 0)
+ * or CPython (py = 1) stream of fun.py:305-306 / ransac.py:12-19 is cut into world x Cr
+ * chunks; rank r parses only its own chunks, and the ranks exchange two small records:
+ *   rs_np_shard_parse    rank-local: jump to the rank's first word, generate its words, parse
+ *                        its chunks from every entry state.  layout[6] = {hypotheses this
+ *                        segment covers at most, C, Cr, Wc, draws, map blob bytes};
+ *   rs_np_shard_maps     the rank's chunk maps as a blob                -> all-gather;
+ *   rs_np_shard_compose  all ranks' blobs (rank order, `stride` bytes apart): the true entry
+ *                        state of every chunk, then the rank's hypothesis starts: their number
+ *                        and the first (segment draw index)          -> all-gather;
+ *   rs_np_shard_tuples   the rank's hypotheses [base, hi) (global indices; base = starts of
+ *                        lower ranks) as (hi - base, k) int32 rows, given the next rank's
+ *                        first start; final_idx >= 0 on the rank holding start `got`: the
+ *                        (key, pos) after the segment's `got` hypotheses (key_out untouched
+ *                        when the state stays in the caller's block).
+ * tsbb15_amd.parallel.np_sharded_segments runs the exchange; world 1 reproduces
+ * rs_np_choice_tuples_gpu bit for bit. */
+typedef struct rs_np_shard rs_np_shard;
+int rs_np_shard_create(rs_ctx *ctx, int64_t n, int32_t k, int32_t world, int32_t rank, int32_t py,
+                       rs_np_shard **out);
+int rs_np_shard_destroy(rs_np_shard *shard);
+int rs_np_shard_parse(rs_np_shard *shard, const uint32_t *mt_key, int32_t mt_pos, int64_t count,
+                      int64_t *layout);
+int rs_np_shard_maps(rs_np_shard *shard, uint8_t *out, int64_t cap, int64_t *nbytes);
+int rs_np_shard_compose(rs_np_shard *shard, const uint8_t *blobs, int64_t stride, int64_t *nstarts,
+                        int64_t *first_start);
+int rs_np_shard_tuples(rs_np_shard *shard, int64_t base, int64_t hi, int64_t next_start,
+                       int64_t final_idx, int32_t *out, uint32_t *key_out, int32_t *pos_out);
+
 /* ------------------------------------------------------------------------------------------
  * lab3 primitives on the GPU
  * ---------------------------------------------------------------------------------------- */
@@ -167,6 +197,13 @@ int rs_f8_plan_run_np(rs_f8_plan *plan, int64_t H, uint32_t *mt_key, int32_t *mt
  * and (key, pos) advance past all H, exactly as rs_f8_plan_run_np. */
 int rs_f8_plan_run_np_slice(rs_f8_plan *plan, int64_t H, int64_t start, int64_t count,
                             uint32_t *mt_key, int32_t *mt_pos, double thresh);
+/* Parity mode, sharded: this rank's hypotheses [base, hi) of a sharded parse (rs_np_shard_*
+ * after compose) produced straight into the run's tuple buffer, then the same pipeline as
+ * rs_f8_plan_run (candidate indices are run-local: add base).  hi == base runs nothing and
+ * only reads the final state (final_idx >= 0). */
+int rs_f8_plan_run_np_shard(rs_f8_plan *plan, rs_np_shard *shard, int64_t base, int64_t hi,
+                            int64_t next_start, int64_t final_idx, uint32_t *key_out,
+                            int32_t *pos_out, double thresh);
 /* Wait for the last run and copy its result; inliers (S_RANSAC, ascending) up to cap. */
 int rs_f8_plan_result(rs_f8_plan *plan, rs_f8_result *out, int64_t *inliers, int64_t cap,
                       int64_t *n_inliers);
@@ -392,6 +429,9 @@ int rs_comm_init(rs_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t *id);
 int rs_comm_destroy(rs_ctx *ctx);
 /* All-gather of `bytes` per rank (host buffers; staged through HBM). */
 int rs_comm_allgather(rs_ctx *ctx, const void *send, void *recv, int64_t bytes);
+/* The RCCL this process runs: version (ncclGetVersion) and the path of the shared object
+ * that provides it (up to cap bytes, NUL-terminated). */
+int rs_comm_library(int32_t *version, char *path, int64_t cap);
 /* Max-all-reduce of one int64 (c* across hypothesis shards). */
 int rs_comm_allreduce_max_i64(rs_ctx *ctx, int64_t *value);
 

@@ -1,4 +1,8 @@
 """Host-side helpers (CPU): Rodrigues, ransac.py helpers."""
+import json
+import os
+import random
+
 import numpy as np
 
 from tsbb15_amd import cv, ransac
@@ -23,3 +27,29 @@ def test_ransac_helpers():
     assert ransac.dpp_squared(y1, y2) == 1.0 and ransac.dpp(y1, y2) == 1.0
     R = np.eye(3)
     assert np.array_equal(ransac.calc_y_prim(np.ones(3), R, np.ones(3)), 2 * np.ones(3))
+
+
+def _misc():
+    with open(os.path.join(os.path.dirname(__file__), "golden", "ransac_misc.json")) as f:
+        return json.load(f)
+
+
+def test_calc_p_calc_r_drop_in_equal_reference():
+    """The drop-in ransac.calc_p / calc_r (ransac.py:6-10) against the values the reference
+    itself returned (tests/golden/ransac_misc.json, written by tests/golden/make_golden.py)."""
+    misc = _misc()
+    for w, n, p, val in misc["calc_r"]:
+        assert ransac.calc_r(w, n, p) == val
+    for w, n, r, val in misc["calc_p"]:
+        assert ransac.calc_p(w, n, r) == val
+
+
+def test_gen_rnd_indices_drop_in_equal_reference():
+    """ransac.gen_rnd_indices (ransac.py:12-19) on the global CPython stream: the reference's
+    own output after random.seed(s), call by call."""
+    misc = _misc()
+    for key, (seed, L, n) in (("gen_rnd_indices_seed0_500_6", (0, 500, 6)),
+                              ("gen_rnd_indices_seed12345_37_6", (12345, 37, 6))):
+        random.seed(seed)
+        got = [list(ransac.gen_rnd_indices(L, n)) for _ in range(len(misc[key]))]
+        assert got == [list(x) for x in misc[key]]

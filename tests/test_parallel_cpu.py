@@ -241,3 +241,54 @@ def test_fileboot_broadcasts_the_id(tmp_path):
     for p in procs:
         p.join(timeout=60)
     assert out == {0: b"id-7", 1: b"id-7", 2: b"id-7"}
+
+
+def _hub_worker(port, rank, world, q):
+    from tsbb15_amd import parallel
+    hub = parallel.TcpHub(rank, world, "127.0.0.1", port, timeout=60)
+    try:
+        parts = hub.allgather_bytes(b"r%d" % rank * (rank + 1))
+        m = hub.allreduce_max_int(10 * rank - 7)
+        f = hub.max_float(0.5 * rank)
+        b = hub.broadcast_bytes(b"uid" if rank == 0 else b"", 0)
+        hub.barrier()
+        # the sharded parity exchange over the hub (MockNpShard steps)
+        import sys
+        import os
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from np_shard_mock import MockNpShard
+        from tsbb15_amd import _ffi
+        key, pos = _ffi.np_seed(5)
+        parts2, k2, p2 = parallel.np_sharded_tuples(hub, MockNpShard(30, 8, world, rank, seg_cap=20),
+                                                    key, pos, 45)
+        q.put((rank, (parts, m, f, b, [(g, r.tolist()) for g, r in parts2], k2.tolist(), p2)))
+    finally:
+        hub.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tcp_hub_collectives(world):
+    """The torch-free harness (bench.py): all-gather in rank order, max-reduce, broadcast,
+    barrier, and the split-stream exchange carried over it."""
+    import multiprocessing as mp
+    from tsbb15_amd import _ffi
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hub_worker, args=(port, r, world, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want, wkey, wpos = _ffi.np_choice_tuples(*_ffi.np_seed(5), 30, 8, 45)
+    got = np.full((45, 8), -1)
+    for r in range(world):
+        parts, m, f, b, tp, k2, p2 = out[r]
+        assert parts == [b"r%d" % q_ * (q_ + 1) for q_ in range(world)]
+        assert m == 10 * (world - 1) - 7 and f == 0.5 * (world - 1) and b == b"uid"
+        for g, rows in tp:
+            got[g:g + len(rows)] = rows
+        assert p2 == wpos and k2 == wkey.tolist()
+    assert np.array_equal(got, want)

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <dlfcn.h>
+
 #include <cstring>
 
 #include "common.h"
@@ -103,5 +105,25 @@ extern "C" int rs_comm_allreduce_max_i64(rs_ctx *c, int64_t *value) {
   e = hipMemcpyAsync(value, d, 8, hipMemcpyDeviceToHost, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) return rs::hip_fail(e, "allreduce D2H");
+  return RS_OK;
+}
+
+// Which RCCL this process runs: ncclGetVersion and the path of the shared object that holds it
+// (dladdr).  A process that loaded another librccl.so first (torch's bundled copy, through
+// `import torch.distributed`) binds the soname to that one; bench.py reports both.
+extern "C" int rs_comm_library(int32_t *version, char *path, int64_t cap) {
+  if (!version) return fail(RS_EINVAL, "null pointer");
+  int v = 0;
+  ncclResult_t r = ncclGetVersion(&v);
+  if (r != ncclSuccess) return nccl_fail(r, "ncclGetVersion");
+  *version = v;
+  if (path && cap > 0) {
+    Dl_info info{};
+    const char *p = dladdr(reinterpret_cast<void *>(&ncclGetVersion), &info) && info.dli_fname
+                        ? info.dli_fname
+                        : "";
+    std::strncpy(path, p, static_cast<size_t>(cap - 1));
+    path[cap - 1] = '\0';
+  }
   return RS_OK;
 }

@@ -30,5 +30,8 @@ bool np_gpu_supported(int64_t n, int32_t k);  // within the GPU parse's populati
 int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t k,
                      int64_t count, int32_t *d_out, bool py = false, int64_t skip = 0,
                      int64_t take = -1);
+// Step 4 of a sharded parse (np_sampler.hip, rs_np_shard_*) into device memory.
+int np_shard_tuples_device(rs_np_shard *w, int64_t base, int64_t hi, int64_t next_start,
+                           int64_t final_idx, int32_t *d_out, uint32_t *key_out, int32_t *pos_out);
 int fmatrix_stls_lsq(rs_ctx *c, const double *pl, const double *pr, int64_t n, double *F_out);
 }  // namespace rs

@@ -455,6 +455,24 @@ extern "C" int rs_f8_plan_run_np_slice(rs_f8_plan *p, int64_t H, int64_t start, 
                   tuples.data() + 8 * start, thresh, false);
 }
 
+// This rank's hypotheses [base, hi) of a sharded parse (rs_np_shard_*, step 4) straight into
+// the tuple buffer of the run about to be issued, then that run; a rank holding no
+// hypothesis only reads the final state (final_idx >= 0).  Candidate indices are run-local.
+extern "C" int rs_f8_plan_run_np_shard(rs_f8_plan *p, rs_np_shard *sh, int64_t base, int64_t hi,
+                                       int64_t next_start, int64_t final_idx, uint32_t *key_out,
+                                       int32_t *pos_out, double thresh) {
+  if (!p || !sh) return fail(RS_EINVAL, "null pointer");
+  const int64_t count = hi - base;
+  if (count > p->max_hyp) return fail(RS_EINVAL, "hypothesis count out of plan range");
+  RunBufs &b = p->buf[p->runs % rs_f8_plan::kBufs];
+  int st;
+  if ((st = rs::np_shard_tuples_device(sh, base, hi, next_start, final_idx,
+                                       count > 0 ? b.d_tuples : nullptr, key_out, pos_out)))
+    return st;
+  if (count < 1) return RS_OK;
+  return plan_run(p, count, RS_SAMPLER_TUPLES, 0, static_cast<uint64_t>(base), nullptr, thresh, true);
+}
+
 extern "C" int rs_f8_plan_run_np(rs_f8_plan *p, int64_t H, uint32_t *key, int32_t *pos,
                                  double thresh) {
   return rs_f8_plan_run_np_slice(p, H, 0, H, key, pos, thresh);

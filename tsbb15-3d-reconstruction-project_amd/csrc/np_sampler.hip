@@ -30,6 +30,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <mutex>
 #include <vector>
 
@@ -59,7 +60,7 @@ constexpr int kDeg = 19937;
 constexpr int kPrefix = kDeg + kN - 1;       // words of a window's sequence a jump reads
 constexpr int kJB = 1024;                    // stream blocks per generator
 constexpr int64_t kJ = int64_t(kN) * kJB;    // words per generator
-constexpr int kLevels = 11;                  // jump tree depth: up to 2048 generators
+constexpr int kLevels = 16;                  // jump levels: windows up to 2^16 generators apart
 constexpr int64_t kSegWords = int64_t(1) << 29;  // stream words per segment (2 GiB)
 constexpr int kW = 1 << 21;                  // longest automatic parse chunk (draws)
 constexpr int kWmax = 1 << 21;               // longest chunk (RSAMD_NP_KW)
@@ -887,9 +888,15 @@ constexpr int kComposeBlock = 256;
 // along the lanes; the serial walk of wave 0 is then one ballot per chunk: the wanted entry is
 // the highest lane with lo <= a (none: the last lane, the largest lo).  Longer lists (chunks
 // that ended dense) take the key-maximum scan from HBM.
+// row_off (optional): where chunk c's list starts in fin (the gathered, packed maps of a
+// sharded parse); null: row c at c * n1.
 __global__ __launch_bounds__(1024) void k_np_compose(const uint32_t *__restrict__ fin,
                                                      const int *__restrict__ fin_m, int n1, int C,
-                                                     int *__restrict__ ent) {
+                                                     int *__restrict__ ent,
+                                                     const int64_t *__restrict__ row_off) {
+  auto row = [&](int c) -> const uint32_t * {
+    return fin + (row_off ? row_off[c] : static_cast<int64_t>(c) * n1);
+  };
   __shared__ uint32_t rows[kComposeBlock][64];
   __shared__ int ms[kComposeBlock], es[kComposeBlock];
   const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
@@ -901,7 +908,7 @@ __global__ __launch_bounds__(1024) void k_np_compose(const uint32_t *__restrict_
     for (int r = wv; r < nb; r += 16) {
       const int m = ms[r];
       if (m > 64) continue;
-      const uint32_t x = l < m ? fin[static_cast<size_t>(c0 + r) * n1 + l] : 0xffffffffu;
+      const uint32_t x = l < m ? row(c0 + r)[l] : 0xffffffffu;
       // the lane holding the smallest lo starts the rotated row
       uint32_t mn = x & 0xffffu;
 #pragma unroll
@@ -933,7 +940,7 @@ __global__ __launch_bounds__(1024) void k_np_compose(const uint32_t *__restrict_
         uint32_t kb = 0, kt = 0;
         bool hb = false, ht = false;
         for (int k = l; k < m; k += 64) {
-          const uint32_t x = fin[static_cast<size_t>(c) * n1 + k];
+          const uint32_t x = row(c)[k];
           const uint32_t lo = x & 0xffffu, key = (lo << 16) | (x >> 16);
           if (static_cast<int>(lo) <= a && (!hb || key > kb)) kb = key, hb = true;
           if (!ht || key > kt) kt = key, ht = true;
@@ -1400,7 +1407,7 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
     }
     HIP_TRY(hipGetLastError());
     // 4-5: compose the chunk maps, keep the true wraps (= hypothesis starts), gather them
-    k_np_compose<<<1, 1024, 0, s>>>(w.d_fin, w.d_fin_m, n1, C, w.d_ent);
+    k_np_compose<<<1, 1024, 0, s>>>(w.d_fin, w.d_fin_m, n1, C, w.d_ent, nullptr);
     HIP_TRY(hipGetLastError());
     k_np_filter<<<C, 64, 0, s>>>(w.d_ev, w.d_ev_n, w.d_ent, w.d_vcnt, ecap);
     HIP_TRY(hipGetLastError());
@@ -1494,4 +1501,520 @@ extern "C" int rs_np_choice_tuples_gpu(rs_ctx *c, uint32_t *mt_key, int32_t *mt_
 extern "C" int rs_py_shuffle_tuples_gpu(rs_ctx *c, uint32_t *mt_key, int32_t *mt_pos, int64_t n,
                                         int32_t k, int64_t count, int32_t *out) {
   return choice_tuples_gpu(c, mt_key, mt_pos, n, k, count, out, true);
+}
+
+// ==== sharded parse: the chunks of one stream split across ranks ==========
+//
+// Every rank runs the same deterministic layout: the segment's draws are C = world x Cr chunks
+// of Wc draws, rank r owns chunks [r Cr, (r+1) Cr).  A rank
+//   1. jumps its first MT19937 window to the generator holding its first word (the set bits of
+//      g0 as level jumps, then the doubling tree over its own generators only), writes its
+//      own words plus a margin (the hypothesis that straddles its end) and parses its chunks
+//      from every entry state (k_np_entry / k_np_track, exactly as np_choice_device);
+//   2. ships its chunk maps (the <= 64-entry lists entry -> exit, a blob of a few KB);
+//   3. composes ALL chunks' maps (every rank, identically) into the true entry state of each
+//      chunk and keeps its own chunks' wraps: its hypothesis starts, counted;
+//   4. given the global offset of its first start (an all-gathered count scan) and the next
+//      rank's first start, re-parses its own hypotheses into tuples; the rank holding the
+//      start of hypothesis `got` reads the (key, pos) after the segment off its stream.
+// Steps 2 -> 3 and 3 -> 4 are the all-gathers (Python, tsbb15_amd.parallel); nothing here
+// depends on the transport.  World 1 gives the np_choice_device result, bit for bit.
+namespace {
+
+constexpr int64_t kShardSegWords = int64_t(1) << 31;  // own words per rank and segment (8 GiB)
+constexpr int64_t kMapsMagic = 0x5253485044414d53LL;   // blob header tag
+
+// start draw (relative to the rank's draw 0) of every kept wrap, in order; lead = 1 puts the
+// segment's first hypothesis (draw 0, rank 0 only) in front
+__global__ __launch_bounds__(256) void k_np_starts_local(const uint2 *__restrict__ ev,
+                                                         const int *__restrict__ vcnt,
+                                                         const int *__restrict__ off,
+                                                         int64_t *__restrict__ starts, int ecap,
+                                                         int W, int lead) {
+  const int c = blockIdx.x;
+  const int n = vcnt[c];
+  const int64_t base = lead + off[c];
+  for (int i = threadIdx.x; i < n; i += 256)
+    starts[base + i] = static_cast<int64_t>(c) * W + ev[static_cast<size_t>(c) * ecap + i].x;
+  if (lead && c == 0 && threadIdx.x == 0) starts[0] = 0;
+}
+
+template <class T>
+int sgrow(T *&p, int64_t &cap, int64_t need) {
+  if (need <= cap) return RS_OK;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  if (hipMalloc(reinterpret_cast<void **>(&p), sizeof(T) * static_cast<size_t>(need)) != hipSuccess)
+    return rs::fail(RS_ENOMEM, "np shard: device allocation failed");
+  cap = need;
+  return RS_OK;
+}
+
+}  // namespace
+
+struct rs_np_shard {
+  rs_ctx *ctx = nullptr;
+  int world = 1, rank = 0, n1 = 0, cus = 256;
+  int32_t k = 8;
+  int64_t n = 0;
+  bool py = false;
+  // layout of the current segment (shard_layout)
+  int64_t count = 0, Wc = 0, Cr = 0, C = 0, D = 0;
+  int64_t s_lo = 0, g0 = 0, wbase = 0, Lb = 0, G = 0, nwords = 0;
+  int ecap = 0, ecap_shift = 0;
+  int state = 0;  // 0 idle, 1 parsed, 2 composed
+  int64_t nstarts = 0, first_start = -1;
+  std::vector<uint8_t> maps;  // this rank's chunk-map blob
+  // device
+  int32_t *d_bits = nullptr;
+  std::vector<int> bit_off, bit_n;
+  uint32_t *d_win = nullptr, *d_chain = nullptr, *d_stream = nullptr, *d_fin = nullptr,
+           *d_fin_all = nullptr;
+  int *d_fin_m = nullptr, *d_fin_m_all = nullptr, *d_ev_n = nullptr, *d_ent = nullptr,
+      *d_vcnt = nullptr, *d_off = nullptr, *d_err = nullptr, *d_tpos = nullptr;
+  int64_t *d_row_off = nullptr, *d_starts = nullptr, *d_got = nullptr;
+  uint2 *d_ev = nullptr;
+  int64_t cap_win = 0, cap_chain = 0, cap_stream = 0, cap_fin = 0, cap_fin_all = 0, cap_fm = 0,
+          cap_fm_all = 0, cap_ev = 0, cap_evn = 0, cap_ent = 0, cap_vcnt = 0, cap_off = 0,
+          cap_tpos = 0, cap_row = 0, cap_starts = 0;
+};
+
+namespace {
+
+void shard_free(rs_np_shard *w) {
+  void *ptrs[] = {w->d_bits, w->d_win,   w->d_chain, w->d_stream, w->d_fin,     w->d_fin_all,
+                  w->d_fin_m, w->d_fin_m_all, w->d_ev_n, w->d_ent, w->d_vcnt, w->d_off,
+                  w->d_err,  w->d_tpos,  w->d_row_off, w->d_starts, w->d_got, w->d_ev};
+  for (void *p : ptrs)
+    if (p) (void)hipFree(p);
+}
+
+// kernel attributes for populations up to n1 (dynamic LDS of the entry and tuple kernels)
+int shard_kernel_attrs(int n1) {
+  static std::mutex mu;
+  static int64_t entry_lds = 0, tup_lds = 0;
+  static bool jump = false;
+  std::lock_guard<std::mutex> g(mu);
+  if (!jump) {
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_mt_jump),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                static_cast<int>(sizeof(uint32_t) * kPrefix)));
+    jump = true;
+  }
+  const int64_t lds = 8 * static_cast<int64_t>((n1 + 1) & ~1);
+  if (lds > entry_lds) {
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_np_entry<false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_np_entry<true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+    entry_lds = lds;
+  }
+  const int64_t tl = (static_cast<int64_t>(sizeof(uint32_t)) * kTupRing +
+                      static_cast<int64_t>(sizeof(uint16_t)) * ((n1 + 1) & ~1)) * kTupWaves;
+  if (tl > tup_lds) {
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_np_tuples_wave<false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(tl)));
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_np_tuples_wave<true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(tl)));
+    tup_lds = tl;
+  }
+  return RS_OK;
+}
+
+int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// The segment's layout for `count` more hypotheses from (., pos): identical on every rank with
+// the same (n, count, pos, world, CUs); the compose step checks that it is.
+int shard_layout(rs_np_shard &w, int32_t pos, int64_t count) {
+  const double E = expected_draws(w.n1, w.py);
+  const int64_t margin = 16 * w.n + 4096 + 8 * static_cast<int64_t>(std::ceil(E)) + kN;
+  const int64_t own_cap = kShardSegWords - margin - 2 * kJ;
+  const int64_t hcap = std::max<int64_t>(
+      1, static_cast<int64_t>(static_cast<double>(own_cap * w.world - 16 * w.n - 4096) / (E * 1.03)));
+  const int64_t hs = std::min<int64_t>(count, hcap);
+  const int64_t need = static_cast<int64_t>(std::ceil(hs * E * 1.03)) + 16 * w.n + 4096;
+  const int64_t Dr = cdiv(need, w.world);
+  // chunk length as np_choice_device: 2 x CUs chunks per rank for N - 1 < 4096, else 1 x CUs
+  const int64_t C0 = static_cast<int64_t>(w.cus) * (w.n1 < 4096 ? 2 : 1);
+  const int64_t L = cdiv(cdiv(Dr, C0), 4096) * 4096;
+  w.Wc = std::max<int64_t>(kWmin, std::min<int64_t>(kW, L));
+  w.Cr = cdiv(Dr, w.Wc);
+  w.C = w.Cr * w.world;
+  w.D = w.C * w.Wc;
+  w.count = hs;
+  const int64_t own0 = static_cast<int64_t>(w.rank) * w.Cr * w.Wc;  // own draw 0
+  w.s_lo = pos + own0;
+  const int64_t s_end = w.s_lo + w.Cr * w.Wc + margin;
+  // the first generator: every word the rank reads lies in a block it writes whole (a jumped
+  // window's word 0 carries only its top bit)
+  w.g0 = w.rank == 0 ? 0 : (w.s_lo - kN) / kJ;
+  if (w.g0 >> kLevels) return rs::fail(RS_EINVAL, "np shard: stream offset beyond the jump table");
+  w.wbase = w.g0 * kJ;
+  w.Lb = cdiv(s_end, kN) - w.g0 * kJB;
+  w.G = cdiv(w.Lb, kJB);
+  if (w.G > (int64_t(1) << kLevels)) return rs::fail(RS_EINVAL, "np shard: segment too long");
+  w.nwords = w.Lb * kN - (w.s_lo - w.wbase);
+  w.ecap_shift = 0;
+  return RS_OK;
+}
+
+// windows of local generators 0 .. G-1 (global g0 ..) from the stream whose block 0 is key
+int shard_windows(rs_np_shard &w, const uint32_t *key, hipStream_t s) {
+  int st;
+  if ((st = sgrow(w.d_win, w.cap_win, w.G * kN))) return st;
+  const JumpPolys &jp = jump_polys();
+  (void)jp;
+  if (w.g0 == 0) {
+    HIP_TRY(hipMemcpyAsync(w.d_win, key, sizeof(uint32_t) * kN, hipMemcpyHostToDevice, s));
+  } else {
+    // a chain of level jumps, one per set bit of g0 (jumps commute)
+    const int nb = __builtin_popcountll(static_cast<unsigned long long>(w.g0));
+    if ((st = sgrow(w.d_chain, w.cap_chain, static_cast<int64_t>(nb + 1) * kN))) return st;
+    HIP_TRY(hipMemcpyAsync(w.d_chain, key, sizeof(uint32_t) * kN, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(w.d_chain + kN, 0, sizeof(uint32_t) * kN * static_cast<size_t>(nb), s));
+    int j = 0;
+    for (int lv = 0; lv < kLevels; ++lv) {
+      if (!((w.g0 >> lv) & 1)) continue;
+      k_mt_jump<<<64, 256 * kJumpGroups, sizeof(uint32_t) * kPrefix, s>>>(
+          w.d_chain + static_cast<size_t>(j) * kN, 1, 2, w.d_bits + w.bit_off[lv], w.bit_n[lv], 64);
+      HIP_TRY(hipGetLastError());
+      ++j;
+    }
+    HIP_TRY(hipMemcpyAsync(w.d_win, w.d_chain + static_cast<size_t>(j) * kN, sizeof(uint32_t) * kN,
+                           hipMemcpyDeviceToDevice, s));
+  }
+  if (w.G > 1)
+    HIP_TRY(hipMemsetAsync(w.d_win + kN, 0, sizeof(uint32_t) * kN * static_cast<size_t>(w.G - 1), s));
+  for (int half = 1, lv = 0; half < w.G; half *= 2, ++lv) {
+    const int S = std::max(1, std::min(64, 512 / half));
+    k_mt_jump<<<half * S, 256 * kJumpGroups, sizeof(uint32_t) * kPrefix, s>>>(
+        w.d_win, half, static_cast<int>(w.G), w.d_bits + w.bit_off[lv], w.bit_n[lv], S);
+    HIP_TRY(hipGetLastError());
+  }
+  return RS_OK;
+}
+
+int shard_parse(rs_np_shard &w, const uint32_t *key, int32_t pos, int64_t count) {
+  rs_ctx *c = w.ctx;
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  int st;
+  if ((st = shard_kernel_attrs(w.n1))) return st;
+  if (!w.d_bits) {
+    const JumpPolys &jp = jump_polys();
+    std::vector<int32_t> all;
+    for (const auto &b : jp.bits) {
+      w.bit_off.push_back(static_cast<int>(all.size()));
+      w.bit_n.push_back(static_cast<int>(b.size()));
+      all.insert(all.end(), b.begin(), b.end());
+    }
+    int64_t cap = 0;
+    if ((st = sgrow(w.d_bits, cap, static_cast<int64_t>(all.size())))) return st;
+    HIP_TRY(hipMemcpy(w.d_bits, all.data(), sizeof(int32_t) * all.size(), hipMemcpyHostToDevice));
+    int64_t c1 = 0, c2 = 0;
+    if ((st = sgrow(w.d_err, c1, 1)) || (st = sgrow(w.d_got, c2, 1))) return st;
+  }
+  if ((st = shard_layout(w, pos, count))) return st;
+  // 1: own words (+ margin)
+  if ((st = sgrow(w.d_stream, w.cap_stream, w.Lb * kN))) return st;
+  if ((st = shard_windows(w, key, s))) return st;
+  k_mt_stream<<<static_cast<unsigned>(w.G), 256, 0, s>>>(w.d_win, w.d_stream, w.Lb);
+  HIP_TRY(hipGetLastError());
+  // 1: all-entry parse of own chunks
+  const int Cr = static_cast<int>(w.Cr), Wc = static_cast<int>(w.Wc);
+  if ((st = sgrow(w.d_fin, w.cap_fin, w.Cr * w.n1)) || (st = sgrow(w.d_fin_m, w.cap_fm, w.Cr)) ||
+      (st = sgrow(w.d_ev_n, w.cap_evn, w.Cr)) || (st = sgrow(w.d_tpos, w.cap_tpos, w.Cr)) ||
+      (st = sgrow(w.d_vcnt, w.cap_vcnt, w.Cr)) || (st = sgrow(w.d_off, w.cap_off, w.Cr)))
+    return st;
+  const double E = expected_draws(w.n1, w.py);
+  const uint32_t *own = w.d_stream + (w.s_lo - w.wbase);
+  const int64_t lds = 8 * static_cast<int64_t>((w.n1 + 1) & ~1);
+  for (;;) {
+    w.ecap = static_cast<int>(std::min<int64_t>(
+        w.Wc + 2 * w.n1, (static_cast<int64_t>(70.0 * w.Wc / E) + 4 * w.n1 + 4096) << w.ecap_shift));
+    if ((st = sgrow(w.d_ev, w.cap_ev, w.Cr * w.ecap))) return st;
+    HIP_TRY(hipMemsetAsync(w.d_err, 0, sizeof(int), s));
+    EntryArgs ea{own, w.Cr * w.Wc, Wc, w.n1, w.d_fin, w.d_fin_m, w.d_ev, w.d_ev_n, w.d_tpos,
+                 w.ecap, w.d_err, nullptr};
+    const bool small = w.n1 < 64;
+    if (w.py) {
+      k_np_entry<true><<<Cr, kEntryThreads, static_cast<size_t>(lds), s>>>(ea, ea.draws);
+      HIP_TRY(hipGetLastError());
+      (small ? k_np_track<true, true> : k_np_track<true, false>)<<<Cr, 64 * kTrackWaves, 0, s>>>(ea, ea.draws);
+    } else {
+      k_np_entry<false><<<Cr, kEntryThreads, static_cast<size_t>(lds), s>>>(ea, ea.draws);
+      HIP_TRY(hipGetLastError());
+      (small ? k_np_track<false, true> : k_np_track<false, false>)<<<Cr, 64 * kTrackWaves, 0, s>>>(ea, ea.draws);
+    }
+    HIP_TRY(hipGetLastError());
+    int err = 0;
+    HIP_TRY(hipMemcpyAsync(&err, w.d_err, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (err & 1) {  // wrap log overflow: a larger log, the same chunks again
+      if (w.ecap >= w.Wc + 2 * w.n1) return rs::fail(RS_EDEVICE, "np shard: wrap log overflow");
+      ++w.ecap_shift;
+      continue;
+    }
+    if (err) return rs::fail(RS_EDEVICE, "np shard: parse error");
+    break;
+  }
+  // 2: the chunk-map blob: header, fin_m[Cr], then each chunk's list
+  std::vector<int> fm(static_cast<size_t>(Cr));
+  HIP_TRY(hipMemcpy(fm.data(), w.d_fin_m, sizeof(int) * fm.size(), hipMemcpyDeviceToHost));
+  const int width = std::min(w.n1, 64);
+  std::vector<uint32_t> rows(static_cast<size_t>(Cr) * width);
+  HIP_TRY(hipMemcpy2D(rows.data(), sizeof(uint32_t) * width, w.d_fin, sizeof(uint32_t) * w.n1,
+                      sizeof(uint32_t) * width, static_cast<size_t>(Cr), hipMemcpyDeviceToHost));
+  int64_t nent = 0;
+  for (int q = 0; q < Cr; ++q) {
+    if (fm[q] < 1 || fm[q] > w.n1) return rs::fail(RS_EDEVICE, "np shard: bad chunk map");
+    nent += fm[q];
+  }
+  const int64_t hdr[8] = {kMapsMagic, w.rank, w.Cr, w.Wc, w.D, w.n1, nent, w.C};
+  w.maps.assign(sizeof(hdr) + sizeof(int32_t) * Cr + sizeof(uint32_t) * nent, 0);
+  uint8_t *o = w.maps.data();
+  std::memcpy(o, hdr, sizeof(hdr));
+  std::memcpy(o + sizeof(hdr), fm.data(), sizeof(int32_t) * Cr);
+  uint32_t *e = reinterpret_cast<uint32_t *>(o + sizeof(hdr) + sizeof(int32_t) * Cr);
+  for (int q = 0; q < Cr; ++q) {
+    if (fm[q] <= width) {
+      std::memcpy(e, rows.data() + static_cast<size_t>(q) * width, sizeof(uint32_t) * fm[q]);
+    } else {  // the chunk ended dense: its whole list
+      HIP_TRY(hipMemcpy(e, w.d_fin + static_cast<size_t>(q) * w.n1, sizeof(uint32_t) * fm[q],
+                        hipMemcpyDeviceToHost));
+    }
+    e += fm[q];
+  }
+  w.state = 1;
+  return RS_OK;
+}
+
+int shard_compose(rs_np_shard &w, const uint8_t *blobs, int64_t stride) {
+  if (w.state < 1) return rs::fail(RS_EINVAL, "np shard: compose before parse");
+  rs_ctx *c = w.ctx;
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  int st;
+  std::vector<int> fm_all(static_cast<size_t>(w.C));
+  std::vector<int64_t> row(static_cast<size_t>(w.C));
+  std::vector<uint32_t> ent;
+  for (int r = 0; r < w.world; ++r) {
+    const uint8_t *b = blobs + static_cast<size_t>(r) * stride;
+    int64_t hdr[8];
+    if (stride < static_cast<int64_t>(sizeof(hdr))) return rs::fail(RS_EINVAL, "np shard: short map blob");
+    std::memcpy(hdr, b, sizeof(hdr));
+    if (hdr[0] != kMapsMagic || hdr[1] != r)
+      return rs::fail(RS_EINVAL, "np shard: map blobs must be the ranks' own, in rank order");
+    if (hdr[2] != w.Cr || hdr[3] != w.Wc || hdr[4] != w.D || hdr[5] != w.n1 || hdr[7] != w.C)
+      return rs::fail(RS_EINVAL, "np shard: ranks disagree on the segment layout");
+    const int64_t nent = hdr[6];
+    if (static_cast<int64_t>(sizeof(hdr) + sizeof(int32_t) * w.Cr + sizeof(uint32_t) * nent) > stride)
+      return rs::fail(RS_EINVAL, "np shard: truncated map blob");
+    const int32_t *fm = reinterpret_cast<const int32_t *>(b + sizeof(hdr));
+    const uint32_t *e = reinterpret_cast<const uint32_t *>(b + sizeof(hdr) + sizeof(int32_t) * w.Cr);
+    int64_t o = 0;
+    for (int64_t q = 0; q < w.Cr; ++q) {
+      const int m = fm[q];
+      if (m < 1 || m > w.n1 || o + m > nent) return rs::fail(RS_EINVAL, "np shard: corrupt map blob");
+      const int64_t cg = r * w.Cr + q;
+      fm_all[static_cast<size_t>(cg)] = m;
+      row[static_cast<size_t>(cg)] = static_cast<int64_t>(ent.size());
+      ent.insert(ent.end(), e + o, e + o + m);
+      o += m;
+    }
+  }
+  if ((st = sgrow(w.d_fin_all, w.cap_fin_all, static_cast<int64_t>(ent.size()))) ||
+      (st = sgrow(w.d_fin_m_all, w.cap_fm_all, w.C)) || (st = sgrow(w.d_row_off, w.cap_row, w.C)) ||
+      (st = sgrow(w.d_ent, w.cap_ent, w.C)))
+    return st;
+  HIP_TRY(hipMemcpyAsync(w.d_fin_all, ent.data(), sizeof(uint32_t) * ent.size(), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(w.d_fin_m_all, fm_all.data(), sizeof(int) * fm_all.size(), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(w.d_row_off, row.data(), sizeof(int64_t) * row.size(), hipMemcpyHostToDevice, s));
+  // 3: true entry state of every chunk, then this rank's wraps of the true trajectory
+  k_np_compose<<<1, 1024, 0, s>>>(w.d_fin_all, w.d_fin_m_all, w.n1, static_cast<int>(w.C), w.d_ent,
+                                  w.d_row_off);
+  HIP_TRY(hipGetLastError());
+  const int Cr = static_cast<int>(w.Cr);
+  k_np_filter<<<Cr, 64, 0, s>>>(w.d_ev, w.d_ev_n, w.d_ent + w.rank * w.Cr, w.d_vcnt, w.ecap);
+  HIP_TRY(hipGetLastError());
+  k_np_scan<<<1, 1024, 0, s>>>(w.d_vcnt, Cr, w.d_off, std::numeric_limits<int64_t>::max(), w.d_got);
+  HIP_TRY(hipGetLastError());
+  // every hypothesis spans at least n1 draws: a bound on the own starts
+  const int lead = w.rank == 0 ? 1 : 0;
+  if ((st = sgrow(w.d_starts, w.cap_starts, w.Cr * w.Wc / std::max(1, w.n1) + 4))) return st;
+  k_np_starts_local<<<Cr, 256, 0, s>>>(w.d_ev, w.d_vcnt, w.d_off, w.d_starts, w.ecap,
+                                       static_cast<int>(w.Wc), lead);
+  HIP_TRY(hipGetLastError());
+  int64_t got = 0, first = -1;
+  HIP_TRY(hipMemcpyAsync(&got, w.d_got, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  w.nstarts = got + lead;
+  if (w.nstarts + 1 > w.cap_starts) return rs::fail(RS_EDEVICE, "np shard: start count out of range");
+  if (w.nstarts > 0) {
+    HIP_TRY(hipMemcpy(&first, w.d_starts, sizeof(int64_t), hipMemcpyDeviceToHost));
+    first += static_cast<int64_t>(w.rank) * w.Cr * w.Wc;
+  }
+  w.first_start = first;
+  w.state = 2;
+  return RS_OK;
+}
+
+// 4: tuples of own hypotheses [base, hi) (global indices within the segment) into d_out;
+// next_start: the following rank's first start (segment draw index), needed when hi reaches
+// past the own starts; final_idx >= 0: the (key, pos) after hypothesis final_idx - 1.
+int shard_tuples(rs_np_shard &w, int64_t base, int64_t hi, int64_t next_start, int64_t final_idx,
+                 int32_t *d_out, uint32_t *key_out, int32_t *pos_out) {
+  if (w.state < 2) return rs::fail(RS_EINVAL, "np shard: tuples before compose");
+  const int64_t cnt = hi - base;
+  if (base < 0 || cnt < 0 || cnt > w.nstarts) return rs::fail(RS_EINVAL, "np shard: hypothesis range out of range");
+  if (cnt > 0 && !d_out) return rs::fail(RS_EINVAL, "np shard: null output");
+  rs_ctx *c = w.ctx;
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const int64_t own0 = static_cast<int64_t>(w.rank) * w.Cr * w.Wc;
+  const uint32_t *own = w.d_stream + (w.s_lo - w.wbase);
+  if (cnt > 0) {
+    if (cnt == w.nstarts) {  // the last own hypothesis ends at the next rank's first start
+      if (next_start < 0) return rs::fail(RS_EINVAL, "np shard: the last hypothesis needs the next start");
+      const int64_t nl = next_start - own0;
+      if (nl <= 0 || nl > w.nwords)
+        return rs::fail(RS_EDEVICE, "np shard: a hypothesis crosses beyond the rank's stream margin");
+      HIP_TRY(hipMemcpy(w.d_starts + w.nstarts, &nl, sizeof(int64_t), hipMemcpyHostToDevice));
+    }
+    HIP_TRY(hipMemcpy(w.d_got, &cnt, sizeof(int64_t), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemsetAsync(w.d_err, 0, sizeof(int), s));
+    const int n1p = (w.n1 + 1) & ~1;
+    const int64_t tl = (static_cast<int64_t>(sizeof(uint32_t)) * kTupRing +
+                        static_cast<int64_t>(sizeof(uint16_t)) * n1p) * kTupWaves;
+    (w.py ? k_np_tuples_wave<true> : k_np_tuples_wave<false>)<<<static_cast<unsigned>(cdiv(cnt, kTupWaves)),
+                                                                 64 * kTupWaves, static_cast<size_t>(tl), s>>>(
+        own, w.d_starts, w.d_got, 0, cnt, w.n1, n1p, w.k, d_out, w.d_err, w.nwords);
+    HIP_TRY(hipGetLastError());
+    int err = 0;
+    HIP_TRY(hipMemcpyAsync(&err, w.d_err, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (err) return rs::fail(RS_EDEVICE, "np shard: hypothesis parse mismatch");
+  }
+  if (final_idx >= 0) {
+    const int64_t j = final_idx - base;
+    if (j < 0 || j >= w.nstarts) return rs::fail(RS_EINVAL, "np shard: final start not held by this rank");
+    if (!key_out || !pos_out) return rs::fail(RS_EINVAL, "np shard: null state output");
+    int64_t used = 0;
+    HIP_TRY(hipMemcpy(&used, w.d_starts + j, sizeof(int64_t), hipMemcpyDeviceToHost));
+    const int64_t W = w.s_lo + used;  // global word index of the next draw
+    if (W > kN) {
+      const int64_t b = (W - 1) / kN;
+      const int64_t lb = b - w.g0 * kJB;
+      if (lb < (w.g0 ? 1 : 0) || lb >= w.Lb) return rs::fail(RS_EDEVICE, "np shard: final block outside the rank's stream");
+      uint32_t blk[kN];
+      HIP_TRY(hipMemcpy(blk, w.d_stream + lb * kN, sizeof(blk), hipMemcpyDeviceToHost));
+      for (int i = 0; i < kN; ++i) key_out[i] = untemper(blk[i]);
+      *pos_out = static_cast<int32_t>(W - b * kN);
+    } else {
+      *pos_out = static_cast<int32_t>(W);  // key unchanged (the caller's copy)
+    }
+  }
+  return RS_OK;
+}
+
+}  // namespace
+
+namespace rs {
+int np_shard_tuples_device(rs_np_shard *w, int64_t base, int64_t hi, int64_t next_start,
+                           int64_t final_idx, int32_t *d_out, uint32_t *key_out, int32_t *pos_out) {
+  if (!w) return fail(RS_EINVAL, "null shard");
+  return shard_tuples(*w, base, hi, next_start, final_idx, d_out, key_out, pos_out);
+}
+}  // namespace rs
+
+extern "C" int rs_np_shard_create(rs_ctx *c, int64_t n, int32_t k, int32_t world, int32_t rank,
+                                  int32_t py, rs_np_shard **out) {
+  if (!c || !out) return rs::fail(RS_EINVAL, "null pointer");
+  *out = nullptr;
+  if (world < 1 || rank < 0 || rank >= world) return rs::fail(RS_EINVAL, "np shard: bad rank / world");
+  if (k < 1 || k > 8) return rs::fail(RS_EINVAL, "np sampler: k must be in 1..8");
+  if (k > n)
+    return rs::fail(RS_EINVAL, py ? "Cannot generate more indices than the amount of values in the set "
+                                    "from which they are extracted. n should therefore be smaller or "
+                                    "equal to set_length"
+                                  : "Cannot take a larger sample than population when 'replace=False'");
+  if (n < 2) return rs::fail(RS_EINVAL, "np shard: population must be at least 2");
+  if (n - 1 > kMaxN1) return rs::fail(RS_EINVAL, "np sampler: population too large for the GPU parse");
+  auto *w = new rs_np_shard();
+  w->ctx = c;
+  w->n = n;
+  w->n1 = static_cast<int>(n - 1);
+  w->k = k;
+  w->world = world;
+  w->rank = rank;
+  w->py = py != 0;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && cus > 0)
+    w->cus = cus;
+  *out = w;
+  return RS_OK;
+}
+
+extern "C" int rs_np_shard_destroy(rs_np_shard *w) {
+  if (!w) return RS_OK;
+  (void)hipSetDevice(w->ctx->device);
+  (void)hipStreamSynchronize(w->ctx->stream);
+  shard_free(w);
+  delete w;
+  return RS_OK;
+}
+
+extern "C" int rs_np_shard_parse(rs_np_shard *w, const uint32_t *mt_key, int32_t mt_pos,
+                                 int64_t count, int64_t *layout) {
+  if (!w || !mt_key) return rs::fail(RS_EINVAL, "null pointer");
+  if (mt_pos < 0 || mt_pos > kN) return rs::fail(RS_EINVAL, "bad MT19937 position");
+  if (count < 1) return rs::fail(RS_EINVAL, "np shard: count must be positive");
+  w->state = 0;
+  int st = shard_parse(*w, mt_key, mt_pos, count);
+  if (st) return st;
+  if (layout) {
+    const int64_t v[6] = {w->count, w->C, w->Cr, w->Wc, w->D, static_cast<int64_t>(w->maps.size())};
+    std::memcpy(layout, v, sizeof(v));
+  }
+  return RS_OK;
+}
+
+extern "C" int rs_np_shard_maps(rs_np_shard *w, uint8_t *out, int64_t cap, int64_t *nbytes) {
+  if (!w || !nbytes) return rs::fail(RS_EINVAL, "null pointer");
+  if (w->state < 1) return rs::fail(RS_EINVAL, "np shard: maps before parse");
+  *nbytes = static_cast<int64_t>(w->maps.size());
+  if (out) {
+    if (cap < *nbytes) return rs::fail(RS_EINVAL, "np shard: map buffer too small");
+    std::memcpy(out, w->maps.data(), w->maps.size());
+  }
+  return RS_OK;
+}
+
+extern "C" int rs_np_shard_compose(rs_np_shard *w, const uint8_t *blobs, int64_t stride,
+                                   int64_t *nstarts, int64_t *first_start) {
+  if (!w || !blobs || !nstarts || !first_start) return rs::fail(RS_EINVAL, "null pointer");
+  const int st = shard_compose(*w, blobs, stride);
+  if (st) return st;
+  *nstarts = w->nstarts;
+  *first_start = w->first_start;
+  return RS_OK;
+}
+
+extern "C" int rs_np_shard_tuples(rs_np_shard *w, int64_t base, int64_t hi, int64_t next_start,
+                                  int64_t final_idx, int32_t *out, uint32_t *key_out,
+                                  int32_t *pos_out) {
+  if (!w) return rs::fail(RS_EINVAL, "null shard");
+  const int64_t cnt = hi - base;
+  int32_t *d = nullptr;
+  int st;
+  if (cnt > 0) {
+    if (!out) return rs::fail(RS_EINVAL, "null output");
+    if ((st = rs::ensure_scratch(w->ctx, sizeof(int32_t) * static_cast<size_t>(cnt) * w->k))) return st;
+    d = static_cast<int32_t *>(w->ctx->scratch);
+  }
+  if ((st = shard_tuples(*w, base, hi, next_start, final_idx, d, key_out, pos_out))) return st;
+  if (cnt > 0)
+    HIP_TRY(hipMemcpy(out, d, sizeof(int32_t) * static_cast<size_t>(cnt) * w->k, hipMemcpyDeviceToHost));
+  return RS_OK;
 }

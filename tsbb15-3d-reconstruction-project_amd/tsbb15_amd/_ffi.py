@@ -134,11 +134,22 @@ _SIGS = {
                                   C.c_int64, _dp]),
     "rs_ba_jacobian": (C.c_int, [C.c_void_p, _dp, C.c_int64, _dp, C.c_int64, _i32p, _i32p,
                                  C.c_int64, _dp, _dp]),
+    "rs_np_shard_create": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
+                                     C.c_int32, C.POINTER(C.c_void_p)]),
+    "rs_np_shard_destroy": (C.c_int, [C.c_void_p]),
+    "rs_np_shard_parse": (C.c_int, [C.c_void_p, _u32p, C.c_int32, C.c_int64, _i64p]),
+    "rs_np_shard_maps": (C.c_int, [C.c_void_p, _u8p, C.c_int64, _i64p]),
+    "rs_np_shard_compose": (C.c_int, [C.c_void_p, _u8p, C.c_int64, _i64p, _i64p]),
+    "rs_np_shard_tuples": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
+                                     _i32p, _u32p, _i32p]),
+    "rs_f8_plan_run_np_shard": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64,
+                                          C.c_int64, C.c_int64, _u32p, _i32p, C.c_double]),
     "rs_comm_unique_id": (C.c_int, [_u8p]),
     "rs_comm_init": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, _u8p]),
     "rs_comm_destroy": (C.c_int, [C.c_void_p]),
     "rs_comm_allgather": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]),
     "rs_comm_allreduce_max_i64": (C.c_int, [C.c_void_p, _i64p]),
+    "rs_comm_library": (C.c_int, [_i32p, C.c_char_p, C.c_int64]),
 }
 
 _lib = None
@@ -182,6 +193,14 @@ def ptr(a, ctype):
 
 def f64c(a):
     return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def rccl_library():
+    """(version, path) of the RCCL shared object this process runs (rs_comm_library)."""
+    v = C.c_int32(0)
+    buf = C.create_string_buffer(4096)
+    check(lib().rs_comm_library(C.byref(v), buf, 4096))
+    return v.value, buf.value.decode(errors="replace")
 
 
 def device_count():
@@ -354,6 +373,78 @@ def py_seed(seed):
     return key, p.value
 
 
+class NpShard:
+    """One rank's share of a parity-stream parse (rs_np_shard_*): the numpy (py=False) or
+    CPython (py=True) stream cut into chunks, this rank parsing only its own.  The exchange
+    between the steps is :func:`tsbb15_amd.parallel.np_sharded_segments`."""
+
+    def __init__(self, ctx, n, k, world, rank, py=False):
+        self.ctx, self.n, self.k = ctx, int(n), int(k)
+        self.world, self.rank = int(world), int(rank)
+        h = C.c_void_p()
+        check(lib().rs_np_shard_create(ctx.handle, self.n, self.k, self.world, self.rank,
+                                       1 if py else 0, C.byref(h)))
+        self._h = h
+
+    @property
+    def handle(self):
+        if self._h is None:
+            raise RuntimeError("shard destroyed")
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None:
+            lib().rs_np_shard_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def parse(self, key, pos, count):
+        """Step 1 (rank-local).  Returns the layout dict of this segment."""
+        key = np.ascontiguousarray(key, dtype=np.uint32)
+        if key.shape != (MT_N,):
+            raise ValueError("MT19937 key must have 624 words")
+        lay = np.zeros(6, np.int64)
+        check(lib().rs_np_shard_parse(self.handle, ptr(key, C.c_uint32), int(pos), int(count),
+                                      ptr(lay, C.c_int64)))
+        return dict(zip(("count", "C", "Cr", "Wc", "D", "map_bytes"), lay.tolist()))
+
+    def maps(self):
+        """Step 2: this rank's chunk-map blob (bytes)."""
+        nb = C.c_int64(0)
+        check(lib().rs_np_shard_maps(self.handle, None, 0, C.byref(nb)))
+        out = np.zeros(nb.value, np.uint8)
+        check(lib().rs_np_shard_maps(self.handle, ptr(out, C.c_uint8), nb.value, C.byref(nb)))
+        return out.tobytes()
+
+    def compose(self, blobs):
+        """Step 3: all ranks' blobs in rank order -> (own start count, first start)."""
+        stride = max(len(b) for b in blobs)
+        buf = np.zeros(stride * len(blobs), np.uint8)
+        for r, b in enumerate(blobs):
+            buf[r * stride:r * stride + len(b)] = np.frombuffer(b, np.uint8)
+        ns, first = C.c_int64(0), C.c_int64(0)
+        check(lib().rs_np_shard_compose(self.handle, ptr(buf, C.c_uint8), stride, C.byref(ns),
+                                        C.byref(first)))
+        return ns.value, first.value
+
+    def tuples(self, base, hi, next_start, final_idx, key):
+        """Step 4: own hypotheses [base, hi) as (hi - base, k) int32; with final_idx >= 0 also
+        the (key, pos) after the segment (key: the segment's entry key, the default)."""
+        cnt = int(hi) - int(base)
+        out = np.empty((max(cnt, 0), self.k), np.int32)
+        key2 = np.array(key, dtype=np.uint32, copy=True)
+        p = C.c_int32(-1)
+        check(lib().rs_np_shard_tuples(self.handle, int(base), int(hi), int(next_start),
+                                       int(final_idx), ptr(out, C.c_int32),
+                                       ptr(key2, C.c_uint32), C.byref(p)))
+        return out, (key2, p.value) if final_idx >= 0 else None
+
+
 # ------------------------------------------------------------------------------------------
 # RANSAC-F plan
 # ------------------------------------------------------------------------------------------
@@ -413,6 +504,17 @@ class F8Plan:
         check(lib().rs_f8_plan_run_np_slice(self._h, int(H), int(start), int(count),
                                             ptr(key, C.c_uint32), C.byref(p), float(thresh)))
         return key, p.value
+
+    def run_np_shard(self, shard, base, hi, next_start, final_idx, key, thresh=1.5):
+        """Sharded parity mode: this rank's hypotheses [base, hi) of ``shard`` (after its
+        compose step) evaluated as one run (candidate indices run-local: add base).  Returns
+        the (key, pos) after the segment when final_idx >= 0, else None."""
+        key2 = np.array(key, dtype=np.uint32, copy=True)
+        p = C.c_int32(-1)
+        check(lib().rs_f8_plan_run_np_shard(self._h, shard.handle, int(base), int(hi),
+                                            int(next_start), int(final_idx),
+                                            ptr(key2, C.c_uint32), C.byref(p), float(thresh)))
+        return (key2, p.value) if final_idx >= 0 else None
 
     def result(self):
         r = F8Result()

@@ -12,15 +12,19 @@ Two shardings:
     union is exactly the single-GPU run); then one max-all-reduce of c* and one all-gather of
     the candidates with count == c*, which every rank replays in global index order with the
     fun.py:320-328 rule (first c* hypothesis, then std/norm tie replacements).
-  * the same in parity mode (the reference's own stream, fun.py:305-306): every rank parses
-    the numpy stream of all H hypotheses on its GPU (where each hypothesis starts is a serial
-    property of the stream), produces and evaluates only its slice's tuples, and advances the
-    MT state past all H -- so the winner, S_RANSAC and the state equal the single-process run.
+  * the same in parity mode (the reference's own stream, fun.py:305-306), two ways:
+    ``ransac_f_split_np`` splits the stream parse itself -- each rank parses only its share
+    of the chunks, the small chunk maps are all-gathered and composed on every rank, and each
+    rank evaluates the hypotheses that start in its share (np_sharded_segments);
+    ``ransac_f_sharded_np`` (the earlier form) has every rank parse the whole stream and
+    evaluate a slice.  Either way the winner, S_RANSAC and the MT state equal the
+    single-process run.
 
-Communicators: :class:`RcclComm` (librsamd, device buffers, xGMI) on GPUs and
-:class:`TorchComm` (torch.distributed, e.g. gloo on the CPU) for tests; both expose
-``allgather_bytes`` and ``allreduce_max_int``.  RcclComm needs only a one-off broadcast of
-its unique id: a TorchComm, or :class:`FileBoot` (a shared directory) without torch.
+Communicators: :class:`RcclComm` (librsamd, device buffers, xGMI) on GPUs,
+:class:`TorchComm` (torch.distributed, e.g. gloo on the CPU) and :class:`ThreadComm` (ranks as
+threads) for tests; all expose ``allgather_bytes`` and ``allreduce_max_int``.  RcclComm needs
+only a one-off broadcast of its unique id: :class:`TcpHub` (a socket hub, no torch; bench.py's
+harness), :class:`FileBoot` (a shared directory) or a TorchComm.
 """
 from __future__ import annotations
 
@@ -95,6 +99,121 @@ class FileBoot:
             time.sleep(0.01)
         with open(self.path, "rb") as f:
             return f.read()
+
+
+class TcpHub:
+    """Host-side collectives for a one-node job without torch.distributed: rank 0 is a hub on
+    ``addr:port`` that every other rank connects to; each operation is a gather to the hub
+    and a broadcast back of length-prefixed frames.  It carries the RCCL unique id (as a
+    ``boot``), the harness barrier and max-reduce -- a few bytes per call, never data.
+
+    ``TcpHub.from_env()`` reads RANK / WORLD_SIZE / MASTER_ADDR and listens on
+    MASTER_PORT + 1 (torch.distributed.run's own store holds MASTER_PORT)."""
+
+    def __init__(self, rank, world, addr="127.0.0.1", port=29611, timeout=120.0):
+        import socket
+        import time
+        self.rank, self.world = int(rank), int(world)
+        self.peers = {}
+        self.sock = None
+        if self.world == 1:
+            return
+        if self.rank == 0:
+            srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            srv.bind((addr, int(port)))
+            srv.listen(self.world)
+            srv.settimeout(timeout)
+            try:
+                while len(self.peers) < self.world - 1:
+                    c, _ = srv.accept()
+                    c.settimeout(timeout)
+                    c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                    r = int.from_bytes(self._recvn(c, 4), "little")
+                    if not 0 < r < self.world or r in self.peers:
+                        raise RuntimeError(f"TcpHub: unexpected rank {r}")
+                    self.peers[r] = c
+            finally:
+                srv.close()
+        else:
+            t0 = time.monotonic()
+            while True:
+                try:
+                    c = socket.create_connection((addr, int(port)), timeout=timeout)
+                    break
+                except OSError:
+                    if time.monotonic() - t0 > timeout:
+                        raise
+                    time.sleep(0.05)
+            c.settimeout(timeout)
+            c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            c.sendall(self.rank.to_bytes(4, "little"))
+            self.sock = c
+
+    @classmethod
+    def from_env(cls, timeout=120.0):
+        import os
+        return cls(int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+                   os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                   int(os.environ.get("MASTER_PORT", "29610")) + 1, timeout)
+
+    @staticmethod
+    def _recvn(c, n):
+        buf = bytearray()
+        while len(buf) < n:
+            part = c.recv(n - len(buf))
+            if not part:
+                raise ConnectionError("TcpHub: peer closed the connection")
+            buf += part
+        return bytes(buf)
+
+    @classmethod
+    def _send(cls, c, b):
+        c.sendall(len(b).to_bytes(8, "little") + b)
+
+    @classmethod
+    def _recv(cls, c):
+        return cls._recvn(c, int.from_bytes(cls._recvn(c, 8), "little"))
+
+    def allgather_bytes(self, b):
+        b = bytes(b)
+        if self.world == 1:
+            return [b]
+        if self.rank == 0:
+            parts = [b] + [self._recv(self.peers[r]) for r in range(1, self.world)]
+            frame = b"".join(len(p).to_bytes(8, "little") + p for p in parts)
+            for r in range(1, self.world):
+                self._send(self.peers[r], frame)
+            return parts
+        self._send(self.sock, b)
+        frame, parts, o = self._recv(self.sock), [], 0
+        while o < len(frame):
+            n = int.from_bytes(frame[o:o + 8], "little")
+            parts.append(frame[o + 8:o + 8 + n])
+            o += 8 + n
+        return parts
+
+    def allreduce_max_int(self, v):
+        return max(int.from_bytes(x, "little", signed=True)
+                   for x in self.allgather_bytes(int(v).to_bytes(8, "little", signed=True)))
+
+    def max_float(self, x):
+        return max(float(np.frombuffer(p, np.float64)[0])
+                   for p in self.allgather_bytes(np.float64(x).tobytes()))
+
+    def broadcast_bytes(self, b, src=0):
+        return self.allgather_bytes(b if self.rank == src else b"")[src]
+
+    def barrier(self):
+        self.allgather_bytes(b"")
+
+    def close(self):
+        for c in list(self.peers.values()) + ([self.sock] if self.sock else []):
+            try:
+                c.close()
+            except OSError:
+                pass
+        self.peers, self.sock = {}, None
 
 
 class RcclComm:
@@ -278,6 +397,189 @@ class GpuSliceEvaluator:
 
     def close(self):
         self.plan.close()
+
+
+# ------------------------------------------------------------------------------------------
+# parity mode with the stream parse itself split across ranks (rs_np_shard_*)
+# ------------------------------------------------------------------------------------------
+def shard_schedule(stats, count, rank):
+    """Host logic of the sharded parse, identical on every rank.
+
+    ``stats`` = [(own start count, first start)] of every rank in rank order (rank 0's first
+    start is the segment's draw 0).  Start i (global, in stream order) begins hypothesis i; a
+    hypothesis is complete when the next start exists, so the segment delivers
+    got = min(count, starts - 1).  Returns (got, base, hi, next_start, final_rank): this rank's
+    hypotheses are [base, hi), the first start of the next rank holding any (-1: none) ends
+    its last one, and final_rank holds start ``got`` (the state after the segment)."""
+    ns = [int(s[0]) for s in stats]
+    total = sum(ns)
+    got = min(int(count), total - 1)
+    if got < 1:
+        raise RuntimeError("parity stream: the segment holds no complete hypothesis")
+    bases = np.concatenate([[0], np.cumsum(ns)[:-1]]).astype(np.int64)
+    base = int(bases[rank])
+    hi = max(base, min(base + ns[rank], got))
+    nxt = -1
+    for q in range(rank + 1, len(ns)):
+        if ns[q] > 0:
+            nxt = int(stats[q][1])
+            break
+    final_rank = next(q for q in range(len(ns)) if bases[q] <= got < bases[q] + ns[q])
+    return got, base, hi, nxt, final_rank
+
+
+def np_sharded_segments(comm, shard, key, pos, H, consume):
+    """The exchange of a sharded parity-stream parse (fun.py:305-306 / ransac.py:12-19 over
+    all ranks).  Per segment: every rank parses its own chunks
+    (``shard.parse``), the chunk maps are all-gathered and composed on every rank
+    (``shard.compose``), the (start count, first start) pairs are all-gathered, and
+    ``consume(offset, base, hi, next_start, final_idx, key)`` handles this rank's hypotheses
+    [offset + base, offset + hi) of the H (``shard.tuples`` or ``F8Plan.run_np_shard``) and
+    returns the (key, pos) after the segment on the rank with final_idx >= 0; that state is
+    all-gathered and starts the next segment.  Returns the (key, pos) after all H hypotheses,
+    identical on every rank (and to the single-stream replay)."""
+    key = np.array(key, dtype=np.uint32, copy=True)
+    pos = int(pos)
+    done = 0
+    while done < H:
+        shard.parse(key, pos, H - done)
+        blob = shard.maps()
+        width = comm.allreduce_max_int(len(blob))
+        blobs = comm.allgather_bytes(blob + bytes(width - len(blob)))
+        ns, first = shard.compose(blobs)
+        stats = [np.frombuffer(b, np.int64) for b in
+                 comm.allgather_bytes(np.array([ns, first], np.int64).tobytes())]
+        got, base, hi, nxt, final_rank = shard_schedule(stats, H - done, comm.rank)
+        fin = consume(done, base, hi, nxt, got if final_rank == comm.rank else -1, key)
+        rec = np.zeros(_MT_REC, np.uint32)
+        if final_rank == comm.rank:
+            rec[:624] = fin[0]
+            rec[624] = int(fin[1])
+        rec = np.frombuffer(comm.allgather_bytes(rec.tobytes())[final_rank], np.uint32)
+        key, pos = rec[:624].copy(), int(rec[624])
+        done += got
+    return key, pos
+
+
+_MT_REC = 625
+
+
+def np_sharded_tuples(comm, shard, key, pos, H):
+    """This rank's share of the next H tuples of the stream: (list of (global start index,
+    (count, k) int32 rows)), key', pos')."""
+    parts = []
+
+    def consume(off, base, hi, nxt, fidx, key):
+        rows, fin = shard.tuples(base, hi, nxt, fidx, key)
+        if hi > base:
+            parts.append((off + base, rows))
+        return fin
+
+    key2, pos2 = np_sharded_segments(comm, shard, key, pos, H, consume)
+    return parts, key2, pos2
+
+
+def ransac_f_split_np(comm, ctx, p1, p2, H, key, pos, thresh=1.5, plan=None, shard=None):
+    """Parity-mode fun.py:303-328 loop with the stream parse itself split across the ranks:
+    each rank parses and evaluates only the hypotheses that start in its share of the stream,
+    then the c* all-reduce / candidate all-gather / global-order replay decides.  Returns
+    (winner record or None, key', pos'), identical on every rank and equal to the
+    single-GPU run (winner, S_RANSAC via :func:`inliers_of`, MT state)."""
+    p1, p2 = _ffi.f64c(p1), _ffi.f64c(p2)
+    own_plan, own_shard = plan is None, shard is None
+    if own_plan:
+        plan = _ffi.F8Plan(ctx, p1.shape[1], max(1, int(H)))
+        plan.set_points(p1, p2)
+    if own_shard:
+        shard = _ffi.NpShard(ctx, p1.shape[1], 8, comm.world, comm.rank)
+    cands = []
+
+    def consume(off, base, hi, nxt, fidx, key):
+        fin = plan.run_np_shard(shard, base, hi, nxt, fidx, key, thresh)
+        if hi > base:
+            cands.append(candidates_from_plan(plan, off + base))
+        return fin
+
+    try:
+        key2, pos2 = np_sharded_segments(comm, shard, key, pos, H, consume)
+    finally:
+        if own_shard:
+            shard.close()
+    local = np.concatenate(cands) if cands else np.zeros(0, CAND_DTYPE)
+    best = merge_shard_candidates(comm, local)
+    if own_plan:
+        plan.close()
+    return best, key2, pos2
+
+
+def inliers_of(best, p1, p2, thresh=1.5):
+    """S_RANSAC of a merged winner record (fun.py:316-317, reference-order residuals)."""
+    if best is None:
+        return np.zeros(0, np.int64)
+    from . import lab3
+    r = np.abs(lab3.fmatrix_residuals(best["F"].reshape(3, 3), _ffi.f64c(p1), _ffi.f64c(p2)))
+    d = np.where(np.isnan(r).any(axis=0), np.nan, r.max(axis=0))
+    return np.flatnonzero(d < thresh)
+
+
+class ThreadComm:
+    """Ranks as threads of one process (a multi-rank rehearsal on one GPU, tests): all-gather
+    through a shared board and a barrier.  ``ThreadComm.group(world)`` gives one per rank."""
+
+    class _Board:
+        def __init__(self, world):
+            import threading
+            self.world = world
+            self.slots = [None] * world
+            self.barrier = threading.Barrier(world)
+
+    def __init__(self, board, rank):
+        self.board, self.rank, self.world = board, int(rank), board.world
+
+    @classmethod
+    def group(cls, world):
+        board = cls._Board(int(world))
+        return [cls(board, r) for r in range(int(world))]
+
+    def allgather_bytes(self, b):
+        bd = self.board
+        bd.slots[self.rank] = bytes(b)
+        bd.barrier.wait()
+        out = list(bd.slots)
+        bd.barrier.wait()
+        return out
+
+    def allreduce_max_int(self, v):
+        return max(int.from_bytes(x, "little", signed=True)
+                   for x in self.allgather_bytes(int(v).to_bytes(8, "little", signed=True)))
+
+
+def run_ranks(world, fn):
+    """fn(rank, comm) on ``world`` threads with ThreadComm; returns the per-rank results
+    (the first exception of any rank is re-raised)."""
+    import threading
+    comms = ThreadComm.group(world)
+    out, errs = [None] * world, [None] * world
+
+    def body(r):
+        try:
+            out[r] = fn(r, comms[r])
+        except BaseException as e:  # noqa: BLE001
+            errs[r] = e
+            comms[r].board.barrier.abort()
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for e in errs:
+        if e is not None and not isinstance(e, threading.BrokenBarrierError):
+            raise e
+    for e in errs:
+        if e is not None:
+            raise e
+    return out
 
 
 class GpuPairSolver:
