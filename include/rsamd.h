@@ -371,9 +371,12 @@ typedef struct rs_gs_info {
 /* The residual of lab3.fmatrix_residuals_gs (lab3.py:228-266) at the parameter vector x
  * (12 camera entries row-major, then n points xyz; f: 4n, order left x, left y, right x,
  * right y) and, when J is non-null, the forward-difference Jacobian scipy's
- * least_squares(jac='2-point') forms (fun.py:358): J (4n, 12 + 3n) row-major, column j =
- * (f(x with x_j -> xp[j]) - f(x)) / dx[j]; xp and dx are the caller's (scipy's step rule).
- * The host-side TRF iteration of the reference-faithful gold standard calls this. */
+ * least_squares(jac='2-point') forms (fun.py:358): the (4n, 12 + 3n) Jacobian stored
+ * column-major (J[j * 4n + i] = dF_i / dx_j, scipy's Fortran-ordered J_transposed.T), column
+ * j = (f(x with x_j -> xp[j]) - f(x)) / dx[j]; xp and dx are the caller's (scipy's step rule).
+ * The projection uses numpy's dgemm bits (FMA chain over k), so f equals the reference's
+ * residual bit for bit.  The host-side TRF iteration of the reference-faithful gold standard
+ * calls this. */
 int rs_gs_residuals_fd(rs_ctx *ctx, const double *x, const double *xp, const double *dx,
                        const double *pl, const double *pr, int64_t n, double *f, double *J);
 

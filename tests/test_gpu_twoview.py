@@ -187,54 +187,148 @@ def _gs_case(tag):
 
 
 def test_gs_residuals_and_2point_jacobian_match_reference_form(ctx):
-    """rs_gs_residuals_fd: the residual equals lab3.fmatrix_residuals_gs (oracle restatement)
-    at the reference's starting parameters, and the forward-difference Jacobian equals scipy's
-    approx_derivative('2-point') of that residual."""
+    """rs_gs_residuals_fd: the residual equals lab3.fmatrix_residuals_gs bit for bit -- the
+    reference's own f(x0) (tests/golden/gs_trace.npz, written by the reference in the build
+    container) and the oracle restatement on this host (numpy's dgemm) -- and the forward-
+    difference Jacobian equals scipy's approx_derivative('2-point') of that residual bit for
+    bit, in scipy's column-major layout."""
     from scipy.optimize._numdiff import approx_derivative
+    tr = golden("gs_trace.npz")
+    for tag in ("noisy", "s300"):
+        a, b, _, z = _gs_case(tag)
+        x = np.hstack((z[f"gs_{tag}_C1_init"].ravel(), z[f"gs_{tag}_X_init"].ravel()))
+        assert np.array_equal(x, tr[f"{tag}_x0"])
+        f = twoview.gs_residuals(x, a, b)
+        assert np.array_equal(f, tr[f"{tag}_f0"]), np.abs(f - tr[f"{tag}_f0"]).max()
+        assert np.array_equal(f, tvr.fmatrix_residuals_gs(x, a, b))
+        J = twoview.gs_jacobian_2point(x, a, b)
+        Jr = approx_derivative(tvr.fmatrix_residuals_gs, x, method="2-point", args=(a, b))
+        assert J.shape == Jr.shape == (4 * a.shape[1], 12 + 3 * a.shape[1])
+        assert J.flags["F_CONTIGUOUS"] and Jr.flags["F_CONTIGUOUS"]
+        assert np.array_equal(J, Jr), np.count_nonzero(J != Jr)
+
+
+def _traced_trf(x0, a, b):
+    """twoview.gs_trf from x0, recording every residual evaluation scipy makes outside the
+    Jacobian, as make_golden_gs_trace.py recorded the reference's."""
+    xs, cs = [], []
+    real = twoview.gs_residuals
+
+    def rec(x, pl, pr, ctx=None):
+        f = real(x, pl, pr, ctx)
+        xs.append(np.array(x, copy=True))
+        cs.append(0.5 * float(f @ f))
+        return f
+
+    twoview.gs_residuals = rec
+    try:
+        res = twoview.gs_trf(x0, a, b)
+    finally:
+        twoview.gs_residuals = real
+    return res, xs, cs
+
+
+def _oracle_trf_trace(x0, a, b):
+    """The reference's call (fun.py:358) with the oracle's restatement of
+    lab3.fmatrix_residuals_gs and scipy's own '2-point' Jacobian, on THIS host, recording the
+    evaluations made outside the Jacobian (as make_golden_gs_trace.py did in the build
+    container)."""
+    import sys
+    from scipy.optimize import least_squares
+    lsq_mod = sys.modules["scipy.optimize._lsq.least_squares"]
+    rec = {"x": [], "c": [], "j": False}
+    real_ad = lsq_mod.approx_derivative
+
+    def ad(*args, **kw):
+        rec["j"] = True
+        try:
+            return real_ad(*args, **kw)
+        finally:
+            rec["j"] = False
+
+    def fun(x, pl, pr):
+        f = tvr.fmatrix_residuals_gs(x, pl, pr)
+        if not rec["j"]:
+            rec["x"].append(x.copy())
+            rec["c"].append(0.5 * float(f @ f))
+        return f
+
+    lsq_mod.approx_derivative = ad
+    try:
+        res = least_squares(fun, x0, xtol=2.22e-14, tr_solver='lsmr', args=(a, b))
+    finally:
+        lsq_mod.approx_derivative = real_ad
+    return res, rec["x"], rec["c"]
+
+
+def _first_divergence(xs, cs, ref_x, ref_c, kept_idx=None):
+    first = next((k for k in range(min(len(cs), len(ref_c))) if cs[k] != ref_c[k]), None)
+    if kept_idx is None:
+        kx = next((k for k in range(min(len(xs), len(ref_x)))
+                   if not np.array_equal(xs[k], ref_x[k])), None)
+    else:
+        kx = next((int(k) for k, xk in zip(kept_idx, ref_x)
+                   if k < len(xs) and not np.array_equal(xs[k], xk)), None)
+    return first, kx
+
+
+def test_gold_standard_trf_retraces_reference_path(ctx):
+    """fun.py:358 as the reference runs it (scipy TRF, xtol=2.22e-14, tr_solver='lsmr') with
+    the residual / Jacobian on the GPU, from the reference's own start (gs_trace.npz x0), on
+    the noisy Dino pair: every evaluated x and cost equals those of the reference's own form
+    run on the same host (the oracle residual with scipy's '2-point' Jacobian, 1 067
+    evaluations in the build container), and so does the result, bit for bit.
+
+    The host half is the reference's own code (scipy over OpenBLAS), so across hosts the
+    reference's path itself changes with the BLAS kernels OpenBLAS picks for the CPU; the
+    comparison with the trace recorded in the build container is reported, and is exact
+    there (tools/gs_trace_cpu.py: numpy with the GPU's arithmetic retraces all 1 067 / 20 021
+    evaluations of the noisy / s300 traces)."""
     a, b, _, z = _gs_case("noisy")
-    x = np.hstack((z["gs_noisy_C1_init"].ravel(), z["gs_noisy_X_init"].ravel()))
-    f = twoview.gs_residuals(x, a, b)
-    fr = tvr.fmatrix_residuals_gs(x, a, b)
-    np.testing.assert_allclose(f, fr, rtol=1e-12, atol=1e-12)
-    assert 0.5 * f @ f == pytest.approx(float(z["gs_noisy_cost_init"]), rel=1e-12)
-    J = twoview.gs_jacobian_2point(x, a, b)
-    Jr = approx_derivative(tvr.fmatrix_residuals_gs, x, method="2-point", args=(a, b))
-    assert J.shape == Jr.shape == (4 * a.shape[1], 12 + 3 * a.shape[1])
-    # both are forward differences with the same steps; they differ only through the last
-    # bits of the residuals (~1e-16 / 1.5e-8)
-    assert np.abs(J - Jr).max() <= 1e-6 * max(1.0, np.abs(Jr).max())
-    assert np.array_equal(J == 0, Jr == 0) or np.count_nonzero((J == 0) != (Jr == 0)) < 10
+    tr = golden("gs_trace.npz")
+    x0 = tr["noisy_x0"]
+    res, xs, cs = _traced_trf(x0, a, b)
+    ores, oxs, ocs = _oracle_trf_trace(x0, a, b)
+    first, kx = _first_divergence(xs, cs, oxs, ocs)
+    tfirst, tkx = _first_divergence(xs, cs, tr["noisy_kept_x"], tr["noisy_costs"],
+                                    tr["noisy_kept_idx"])
+    print(f"\n[noisy] GPU residuals + scipy TRF from the reference start: nfev {res.nfev}, "
+          f"cost {res.cost!r}; the reference form on this host: nfev {ores.nfev}, cost "
+          f"{ores.cost!r}; first divergence from it: cost {first}, x {kx}; from the build "
+          f"container's trace (nfev {int(tr['noisy_nfev'])}, cost "
+          f"{float(tr['noisy_cost_final'])!r}): cost {tfirst}, x {tkx}")
+    assert first is None and kx is None and len(cs) == len(ocs), (first, kx, len(cs), len(ocs))
+    assert res.nfev == ores.nfev and res.status == ores.status
+    assert np.array_equal(res.x, ores.x)
 
 
 @pytest.mark.parametrize("tag", ["clean", "noisy", "s300"])
-def test_gold_standard_trf_follows_reference(ctx, tag):
-    """fun.py:358 as the reference runs it (scipy TRF, xtol=2.22e-14, tr_solver='lsmr') with
-    the residual / Jacobian on the GPU.  Clean pair: the reference's F_gold to 1e-9.  Noisy
-    pair: TRF's stopping point depends on the last bits of every residual -- the reference
-    itself lands 1.7e-5 away from its own golden under eight BLAS threads instead of one
-    (measured in the build container) -- so the bar is that distance's order: F within 1e-3
-    (measured below), the same termination kind, and a cost within 5 % of the reference's."""
+def test_gold_standard_trf_end_to_end(ctx, tag):
+    """fun.py:343-369 end to end on the GPU (cameras of F_RANSAC, optimal triangulation,
+    then the TRF above).  Clean pair: the reference's F_gold to 1e-9.  Noisy pairs: the start
+    differs from the reference's in the last bits (GPU SVD / root finder against LAPACK), and
+    the reference's own end point moves by 3e-4 under a 1e-15 relative change of its start
+    (tools/gs_trace_cpu.py): there the bar is the start (cost to 1e-9), the
+    termination kind and the final cost within 5 %."""
     a, b, F0, z = _gs_case(tag)
     g = twoview.gold_standard_trf_full(F0, a, b)
     dF = np.abs(nF(g.F) - nF(z[f"gs_{tag}_F_gold"])).max()
-    # clean pair: the starting cost is pure rounding (~1e-21), so only an absolute bar applies
     assert g.cost_init == pytest.approx(float(z[f"gs_{tag}_cost_init"]), rel=1e-9, abs=1e-16)
     if tag == "clean":
         assert dF <= 1e-9, dF
         return
-    print(f"\n[{tag}] TRF on GPU residuals: nfev {g.nfev} (reference {int(z[f'gs_{tag}_nfev'])}), "
+    print(f"\n[{tag}] end to end: nfev {g.nfev} (reference {int(z[f'gs_{tag}_nfev'])}), "
           f"status {g.status}, cost {g.cost:.6f} (reference {float(z[f'gs_{tag}_cost_final']):.6f}), "
           f"|dF| {dF:.3g}")
-    assert dF <= 1e-3, dF
     assert g.status in (2, 4) and int(z[f"gs_{tag}_status"]) in (2, 4)
-    # measured (DESIGN.md): noisy |dF| 2.3e-4, cost 8.510 vs 8.241 (TRF stops on ftol after
-    # 120 evaluations where the reference ran 1 067 along the same flat valley)
     assert g.cost == pytest.approx(float(z[f"gs_{tag}_cost_final"]), rel=5e-2)
+    assert dF <= 1e-3, dF
 
 
 def test_getFFromLabCode_dropin_noisy_pair_trf(ctx):
-    """The drop-in with the default reference-faithful gold standard on the noisy Dino pair:
-    RANSAC part bit-exact (tested elsewhere), F_gold near the reference's (see above)."""
+    """The drop-in with the default reference-faithful gold standard on the noisy Dino pair
+    (main.py:39's call): RANSAC part bit-exact (tested elsewhere), F_gold within the distance
+    the reference's own end point moves under last-bit changes of its start (see above)."""
     c1 = golden("dino_c1.npz")
     np.random.seed(0)
     Fg = fun.getFFromLabCode(c1["noisy_p1"], c1["noisy_p2"])

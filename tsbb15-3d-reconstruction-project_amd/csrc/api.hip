@@ -97,7 +97,7 @@ extern "C" int rs_ctx_destroy(rs_ctx *c) {
   (void)hipSetDevice(c->device);
   (void)rs_comm_destroy(c);
   if (c->np_plan) rs_f8_plan_destroy(c->np_plan);
-  rs::np_work_free(c);
+  rs::np_shard_free(c);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;

@@ -5,7 +5,6 @@
 
 #include "rsamd.h"
 
-struct rs_np_work;  // np_sampler.hip: parity-stream workspace
 
 struct rs_ctx {
   int device = 0;
@@ -13,7 +12,7 @@ struct rs_ctx {
   void *scratch = nullptr;     // grow-only device scratch for single-shot ops
   size_t scratch_bytes = 0;
   rs_f8_plan *np_plan = nullptr;  // cached plan of rs_f8_ransac_np
-  rs_np_work *np_work = nullptr;  // GPU parity-stream buffers (grow-only)
+  rs_np_shard *np_shard = nullptr;  // world-1 parity-stream session (np_choice_device)
   void *comm = nullptr;        // ncclComm_t
   void *comm_buf = nullptr;    // device staging for collectives
   size_t comm_buf_bytes = 0;
@@ -22,7 +21,7 @@ struct rs_ctx {
 namespace rs {
 int hip_fail(hipError_t e, const char *what);
 int ensure_scratch(rs_ctx *c, size_t bytes);
-void np_work_free(rs_ctx *c);
+void np_shard_free(rs_ctx *c);
 bool np_gpu_supported(int64_t n, int32_t k);  // within the GPU parse's population range
 // The numpy (py: CPython) stream's next `count` choice(n, k) tuples; rows [skip, skip + take)
 // (take < 0: to the end) are written to d_out (take * k int32); (key, pos) advance past all

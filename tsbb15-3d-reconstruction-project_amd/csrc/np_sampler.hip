@@ -61,7 +61,6 @@ constexpr int kPrefix = kDeg + kN - 1;       // words of a window's sequence a j
 constexpr int kJB = 1024;                    // stream blocks per generator
 constexpr int64_t kJ = int64_t(kN) * kJB;    // words per generator
 constexpr int kLevels = 16;                  // jump levels: windows up to 2^16 generators apart
-constexpr int64_t kSegWords = int64_t(1) << 29;  // stream words per segment (2 GiB)
 constexpr int kW = 1 << 21;                  // longest automatic parse chunk (draws)
 constexpr int kWmax = 1 << 21;               // longest chunk (RSAMD_NP_KW)
 constexpr int kWmin = 8192;                  // shortest parse chunk
@@ -992,23 +991,6 @@ __global__ __launch_bounds__(1024) void k_np_scan(const int *__restrict__ vcnt, 
   if (tid == 0) *got = std::min<int64_t>(H, static_cast<int64_t>(carry));
 }
 
-__global__ __launch_bounds__(256) void k_np_starts(const uint2 *__restrict__ ev,
-                                                   const int *vcnt, const int *off,
-                                                   int64_t *__restrict__ starts,
-                                                   const int64_t *__restrict__ got, int ecap,
-                                                   int W) {
-  const int c = blockIdx.x;
-  const int n = vcnt[c];
-  const int64_t H = *got;
-  const int64_t base = 1 + off[c];
-  for (int i = threadIdx.x; i < n; i += 256) {
-    const int64_t idx = base + i;
-    if (idx <= H)
-      starts[idx] = static_cast<int64_t>(c) * W + ev[static_cast<size_t>(c) * ecap + i].x;
-  }
-  if (c == 0 && threadIdx.x == 0) starts[0] = 0;
-}
-
 // ---- 6. one wave per hypothesis: a window of W <= 64 words per step ------------------------
 // Within a window every state keeps the mask of the first (W <= i - mask/2), so lane l's draw
 // u_l = w_l & mask is accepted for sure if u_l <= i - l (its state is at least i - l), rejected
@@ -1199,16 +1181,6 @@ uint32_t untemper(uint32_t z) {
 }
 
 // expected draws per hypothesis: sum over i of (mask(i) + 1) / (i + 1)
-// stream words per segment: kSegWords, or RSAMD_NP_SEGWORDS (tests of the multi-segment path)
-int64_t seg_words() {
-  static const int64_t v = [] {
-    const char *e = std::getenv("RSAMD_NP_SEGWORDS");
-    const int64_t x = e ? std::atoll(e) : 0;
-    return x > 0 ? std::max<int64_t>(int64_t(1) << 16, std::min(x, kSegWords)) : kSegWords;
-  }();
-  return v;
-}
-
 double expected_draws(int64_t n1, bool py) {
   double e = 0.0;
   for (int64_t i = 1; i <= n1; ++i) {
@@ -1224,284 +1196,6 @@ double expected_draws(int64_t n1, bool py) {
 }
 
 }  // namespace
-
-struct rs_np_work {
-  int32_t *d_bits = nullptr;
-  std::vector<int> bit_off, bit_n;
-  uint32_t *d_win = nullptr, *d_stream = nullptr, *d_fin = nullptr;
-  int *d_fin_m = nullptr, *d_ev_n = nullptr, *d_ent = nullptr, *d_vcnt = nullptr,
-      *d_off = nullptr, *d_err = nullptr, *d_tpos = nullptr;
-  uint2 *d_ev = nullptr;
-  int64_t *d_starts = nullptr;
-  NpResult *d_res = nullptr;
-  int64_t cap_fin = 0, cap_ev = 0, cap_starts = 0;
-  int64_t entry_lds = 0, tup_lds = 0;
-  int cus = 256;  // compute units of the context's device
-};
-
-namespace rs {
-
-void np_work_free(rs_ctx *c) {
-  rs_np_work *w = c->np_work;
-  if (!w) return;
-  void *ptrs[] = {w->d_bits, w->d_win, w->d_stream, w->d_fin, w->d_fin_m, w->d_ev_n,
-                  w->d_ent,  w->d_vcnt, w->d_off,   w->d_err, w->d_ev,    w->d_starts,
-                  w->d_tpos, w->d_res};
-  for (void *p : ptrs)
-    if (p) (void)hipFree(p);
-  delete w;
-  c->np_work = nullptr;
-}
-
-template <class T>
-static int grow(T *&p, int64_t &cap, int64_t need) {
-  if (need <= cap) return RS_OK;
-  if (p) (void)hipFree(p);
-  p = nullptr;
-  cap = 0;
-  if (hipMalloc(reinterpret_cast<void **>(&p), sizeof(T) * static_cast<size_t>(need)) != hipSuccess)
-    return fail(RS_ENOMEM, "np sampler: device allocation failed");
-  cap = need;
-  return RS_OK;
-}
-
-bool np_gpu_supported(int64_t n, int32_t k) { return k >= 1 && k <= 8 && k <= n && n - 1 <= kMaxN1; }
-
-// The numpy stream's next `count` choice(n, k) tuples into device memory (count * k int32),
-// on the context stream; advances (key, pos).  Synchronous.
-int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t k,
-                     int64_t count, int32_t *d_out, bool py, int64_t skip, int64_t take) {
-  if (take < 0) take = count - skip;
-  if (skip < 0 || skip + take > count) return fail(RS_EINVAL, "np sampler: slice out of range");
-  if (k < 1 || k > 8) return fail(RS_EINVAL, "np sampler: k must be in 1..8");
-  if (k > n)
-    return fail(RS_EINVAL, py ? "Cannot generate more indices than the amount of values in the set "
-                                "from which they are extracted. n should therefore be smaller or "
-                                "equal to set_length"
-                              : "Cannot take a larger sample than population when 'replace=False'");
-  if (n - 1 > kMaxN1) return fail(RS_EINVAL, "np sampler: population too large for the GPU parse");
-  if (*pos < 0 || *pos > kN) return fail(RS_EINVAL, "bad MT19937 position");
-  if (count == 0) return RS_OK;
-  HIP_TRY(hipSetDevice(c->device));
-  hipStream_t s = c->stream;
-  if (n <= 1) {  // a one-element shuffle draws nothing: every tuple is (0)
-    HIP_TRY(hipMemsetAsync(d_out, 0, sizeof(int32_t) * static_cast<size_t>(count) * k, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    return RS_OK;
-  }
-  if (!c->np_work) c->np_work = new rs_np_work();
-  rs_np_work &w = *c->np_work;
-  int st;
-  const int n1 = static_cast<int>(n - 1);
-  const int64_t Gmax = (kSegWords / kN + kJB - 1) / kJB + 1;
-  // RSAMD_NP_KW fixes the chunk length (kWmin .. kWmax draws); else automatic (below)
-  static const int kWenv = [] {
-    const char *e = std::getenv("RSAMD_NP_KW");
-    const int v = e ? std::atoi(e) : 0;
-    return v >= kWmin && v <= kWmax ? v : 0;
-  }();
-  const int64_t Cmax = kSegWords / kWmin + 1;
-  const int64_t tup_lds = (static_cast<int64_t>(sizeof(uint32_t)) * kTupRing + static_cast<int64_t>(sizeof(uint16_t)) * ((n1 + 1) & ~1)) * kTupWaves;
-  if (tup_lds > w.tup_lds) {
-    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_np_tuples_wave<false>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(tup_lds)));
-    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_np_tuples_wave<true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(tup_lds)));
-    w.tup_lds = tup_lds;
-  }
-  if (!w.d_bits) {
-    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_mt_jump),
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                static_cast<int>(sizeof(uint32_t) * kPrefix)));
-    const JumpPolys &jp = jump_polys();
-    std::vector<int32_t> all;
-    for (const auto &b : jp.bits) {
-      w.bit_off.push_back(static_cast<int>(all.size()));
-      w.bit_n.push_back(static_cast<int>(b.size()));
-      all.insert(all.end(), b.begin(), b.end());
-    }
-    int64_t cap = 0;
-    if ((st = grow(w.d_bits, cap, static_cast<int64_t>(all.size())))) return st;
-    HIP_TRY(hipMemcpy(w.d_bits, all.data(), sizeof(int32_t) * all.size(), hipMemcpyHostToDevice));
-    int64_t c1 = 0, c2 = 0, c3 = 0, c4 = 0, c5 = 0, c6 = 0, c7 = 0, c8 = 0, c9 = 0;
-    if ((st = grow(w.d_win, c1, Gmax * kN)) || (st = grow(w.d_stream, c2, kSegWords)) ||
-        (st = grow(w.d_fin_m, c3, Cmax)) || (st = grow(w.d_ev_n, c4, Cmax)) ||
-        (st = grow(w.d_ent, c5, Cmax)) || (st = grow(w.d_vcnt, c6, Cmax)) ||
-        (st = grow(w.d_off, c7, Cmax)) || (st = grow(w.d_err, c8, 1)) ||
-        (st = grow(w.d_tpos, c9, Cmax)))
-      return st;
-    int64_t c10 = 0;
-    if ((st = grow(w.d_res, c10, 1))) return st;
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && cus > 0)
-      w.cus = cus;
-  }
-  const double E = expected_draws(n1, py);
-  const int64_t dmax = seg_words() - 3 * kN;
-  const int64_t hcap = std::max<int64_t>(1, static_cast<int64_t>((dmax - 16 * n) / (E * 1.03)));
-  int ecap_shift = 0;  // wrap-log doublings after an overflow
-  const int64_t lds = 8 * static_cast<int64_t>((n1 + 1) & ~1);
-  if (lds > w.entry_lds) {
-    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_np_entry<false>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_np_entry<true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-    w.entry_lds = lds;
-  }
-  int64_t done = 0;
-  while (done < count) {
-    const int64_t hs = std::min<int64_t>(count - done, hcap);
-    const int64_t D = std::min<int64_t>(dmax, static_cast<int64_t>(std::ceil(hs * E * 1.03)) + 16 * n + 4096);
-    // automatic chunk length: every chunk in one resident round of k_np_track (16-wave
-    // workgroups, two per CU) with equal lengths: C = 2 x CUs chunks for N - 1 < 4096; for
-    // larger N the dense entry phase (cost ~ N per chunk) favours one chunk per CU.  Measured
-    // (C2, 1e5 tuples): 274 chunks of 2^20 9.9 ms, 508 of 565 248 8.3 ms, 765 of 376 832 9.9 ms.
-    int kWr = kWenv;
-    if (!kWr) {
-      const int64_t C0 = static_cast<int64_t>(w.cus) * (n1 < 4096 ? 2 : 1);
-      const int64_t L = ((D + C0 - 1) / C0 + 4095) / 4096 * 4096;
-      kWr = static_cast<int>(std::max<int64_t>(kWmin, std::min<int64_t>(kW, L)));
-    }
-    const int ecap = static_cast<int>(std::min<int64_t>(
-        kWr + 2 * n1, (static_cast<int64_t>(70.0 * kWr / E) + 4 * n1 + 4096) << ecap_shift));
-    const int C = static_cast<int>((D + kWr - 1) / kWr);
-    if ((st = grow(w.d_fin, w.cap_fin, static_cast<int64_t>(C) * n1))) return st;
-    const int64_t Lb = (*pos + D + kN - 1) / kN;
-    const int G = static_cast<int>((Lb + kJB - 1) / kJB);
-    if ((st = grow(w.d_ev, w.cap_ev, static_cast<int64_t>(C) * ecap)) ||
-        (st = grow(w.d_starts, w.cap_starts, hs + 1)))
-      return st;
-    // 1-2: the word stream from (key, pos): block 0 is the key itself
-    HIP_TRY(hipMemcpyAsync(w.d_win, key, sizeof(uint32_t) * kN, hipMemcpyHostToDevice, s));
-    if (G > 1)
-      HIP_TRY(hipMemsetAsync(w.d_win + kN, 0, sizeof(uint32_t) * kN * static_cast<size_t>(G - 1), s));
-    for (int half = 1, lv = 0; half < G; half *= 2, ++lv) {
-      if (lv >= kLevels) return fail(RS_EINVAL, "np sampler: segment too long");
-      // parts per jump: about 512 workgroups per level (two per CU)
-      const int S = std::max(1, std::min(64, 512 / half));
-      k_mt_jump<<<half * S, 256 * kJumpGroups, sizeof(uint32_t) * kPrefix, s>>>(
-          w.d_win, half, G, w.d_bits + w.bit_off[lv], w.bit_n[lv], S);
-      HIP_TRY(hipGetLastError());
-    }
-    k_mt_stream<<<G, 256, 0, s>>>(w.d_win, w.d_stream, Lb);
-    HIP_TRY(hipGetLastError());
-    // 3: all-entry parse per chunk
-    HIP_TRY(hipMemsetAsync(w.d_err, 0, sizeof(int), s));
-    long long *d_stats = nullptr;
-#ifdef RSAMD_DIAG
-    static const char *stats_path = std::getenv("RSAMD_NP_STATS");
-    if (stats_path) HIP_TRY(hipMalloc(&d_stats, sizeof(long long) * 128 * C));
-    if (d_stats) HIP_TRY(hipMemsetAsync(d_stats, 0, sizeof(long long) * 128 * C, s));
-#endif
-    EntryArgs ea{w.d_stream + *pos, D, kWr, n1, w.d_fin, w.d_fin_m, w.d_ev, w.d_ev_n, w.d_tpos,
-                 ecap, w.d_err, d_stats};
-    const bool small = n1 < 64;  // several hypothesis ends in one tracking window
-    if (py) {
-      k_np_entry<true><<<C, kEntryThreads, static_cast<size_t>(lds), s>>>(ea, ea.draws);
-      HIP_TRY(hipGetLastError());
-      (small ? k_np_track<true, true> : k_np_track<true, false>)<<<C, 64 * kTrackWaves, 0, s>>>(ea, ea.draws);
-    } else {
-      k_np_entry<false><<<C, kEntryThreads, static_cast<size_t>(lds), s>>>(ea, ea.draws);
-      HIP_TRY(hipGetLastError());
-      (small ? k_np_track<false, true> : k_np_track<false, false>)<<<C, 64 * kTrackWaves, 0, s>>>(ea, ea.draws);
-    }
-    HIP_TRY(hipGetLastError());
-    // 4-5: compose the chunk maps, keep the true wraps (= hypothesis starts), gather them
-    k_np_compose<<<1, 1024, 0, s>>>(w.d_fin, w.d_fin_m, n1, C, w.d_ent, nullptr);
-    HIP_TRY(hipGetLastError());
-    k_np_filter<<<C, 64, 0, s>>>(w.d_ev, w.d_ev_n, w.d_ent, w.d_vcnt, ecap);
-    HIP_TRY(hipGetLastError());
-    k_np_scan<<<1, 1024, 0, s>>>(w.d_vcnt, C, w.d_off, hs, &w.d_res->got);
-    HIP_TRY(hipGetLastError());
-    k_np_starts<<<C, 256, 0, s>>>(w.d_ev, w.d_vcnt, w.d_off, w.d_starts, &w.d_res->got, ecap, kWr);
-    HIP_TRY(hipGetLastError());
-    // 6: tuples of the requested slice [skip, skip + take) within this segment's hypotheses
-    // [done, done + hs) (waves beyond the delivered count exit)
-    const int64_t lo = std::max<int64_t>(skip - done, 0), hi = std::min<int64_t>(skip + take - done, hs);
-    if (hi > lo) {
-      const int n1p = (n1 + 1) & ~1;
-      (py ? k_np_tuples_wave<true> : k_np_tuples_wave<false>)<<<static_cast<unsigned>((hi - lo + kTupWaves - 1) / kTupWaves), 64 * kTupWaves,
-                         static_cast<size_t>(tup_lds), s>>>(
-          w.d_stream + *pos, w.d_starts, &w.d_res->got, lo, hi, n1, n1p, k,
-          d_out + (done + lo - skip) * k, w.d_err, kSegWords - *pos);
-      HIP_TRY(hipGetLastError());
-    }
-    // 7: delivered count, draws used, errors and the stream block holding the next word
-    k_np_result<<<1, 64, 0, s>>>(w.d_stream, w.d_starts, *pos, w.d_err, w.d_res);
-    HIP_TRY(hipGetLastError());
-    NpResult res;
-    HIP_TRY(hipMemcpyAsync(&res, w.d_res, sizeof(res), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-#ifdef RSAMD_DIAG
-    if (d_stats) {
-      std::vector<long long> hst(static_cast<size_t>(128) * C);
-      HIP_TRY(hipMemcpy(hst.data(), d_stats, sizeof(long long) * hst.size(), hipMemcpyDeviceToHost));
-      if (FILE *f = std::fopen(stats_path, "ab")) {
-        const int64_t hdr[4] = {n1, C, kWr, D};
-        std::fwrite(hdr, sizeof(hdr), 1, f);
-        std::fwrite(hst.data(), sizeof(long long), hst.size(), f);
-        std::fclose(f);
-      }
-      (void)hipFree(d_stats);
-    }
-#endif
-    if (res.err & 1) {  // wrap log overflow: a larger log and the same segment again
-      if (ecap >= kWr + 2 * n1) return fail(RS_EDEVICE, "np sampler: wrap log overflow");
-      ++ecap_shift;
-      continue;
-    }
-    if (res.err) return fail(RS_EDEVICE, "np sampler: hypothesis parse mismatch");
-    const int64_t got = res.got;
-    if (got < 1) return fail(RS_EDEVICE, "np sampler: segment holds no complete hypothesis");
-    // state after `used` draws: the block holding the next word (rs_mt_jump's convention)
-    const int64_t W = *pos + res.used;
-    if (W > kN) {
-      const int64_t b = (W - 1) / kN;
-      for (int i = 0; i < kN; ++i) key[i] = untemper(res.blk[i]);
-      *pos = static_cast<int32_t>(W - b * kN);
-    } else {
-      *pos = static_cast<int32_t>(W);
-    }
-    done += got;
-  }
-  return RS_OK;
-}
-
-}  // namespace rs
-
-namespace {
-// Tuples of either stream into host memory through the context's scratch buffer.
-int choice_tuples_gpu(rs_ctx *c, uint32_t *mt_key, int32_t *mt_pos, int64_t n, int32_t k,
-                      int64_t count, int32_t *out, bool py) {
-  if (!c || !mt_key || !mt_pos || (count > 0 && !out))
-    return rs::fail(RS_EINVAL, "tuples_gpu: null pointer");
-  if (count < 0 || k < 0) return rs::fail(RS_EINVAL, "negative dimensions are not allowed");
-  if (count == 0) return RS_OK;
-  int st;
-  if ((st = rs::ensure_scratch(c, sizeof(int32_t) * static_cast<size_t>(count) * k))) return st;
-  uint32_t key[kN];
-  int32_t pos = *mt_pos;
-  std::memcpy(key, mt_key, sizeof(key));
-  if ((st = rs::np_choice_device(c, key, &pos, n, k, count, static_cast<int32_t *>(c->scratch),
-                                 py)))
-    return st;
-  HIP_TRY(hipMemcpy(out, c->scratch, sizeof(int32_t) * static_cast<size_t>(count) * k,
-                    hipMemcpyDeviceToHost));
-  std::memcpy(mt_key, key, sizeof(key));
-  *mt_pos = pos;
-  return RS_OK;
-}
-}  // namespace
-
-extern "C" int rs_np_choice_tuples_gpu(rs_ctx *c, uint32_t *mt_key, int32_t *mt_pos, int64_t n,
-                                       int32_t k, int64_t count, int32_t *out) {
-  return choice_tuples_gpu(c, mt_key, mt_pos, n, k, count, out, false);
-}
-
-extern "C" int rs_py_shuffle_tuples_gpu(rs_ctx *c, uint32_t *mt_key, int32_t *mt_pos, int64_t n,
-                                        int32_t k, int64_t count, int32_t *out) {
-  return choice_tuples_gpu(c, mt_key, mt_pos, n, k, count, out, true);
-}
 
 // ==== sharded parse: the chunks of one stream split across ranks ==========
 //
@@ -1522,6 +1216,32 @@ extern "C" int rs_py_shuffle_tuples_gpu(rs_ctx *c, uint32_t *mt_key, int32_t *mt
 namespace {
 
 constexpr int64_t kShardSegWords = int64_t(1) << 31;  // own words per rank and segment (8 GiB)
+
+// test / tuning knobs, read once per process: RSAMD_NP_SEGWORDS caps a rank's words per
+// segment (tests of the multi-segment path), RSAMD_NP_KW fixes the chunk length (kWmin ..
+// kWmax draws), RSAMD_NP_CPR the chunks per rank
+int64_t env_i64(const char *name) {
+  const char *e = std::getenv(name);
+  return e ? std::atoll(e) : 0;
+}
+int64_t seg_words() {
+  static const int64_t v = [] {
+    const int64_t x = env_i64("RSAMD_NP_SEGWORDS");
+    return x > 0 ? std::max<int64_t>(int64_t(1) << 16, std::min(x, kShardSegWords)) : kShardSegWords;
+  }();
+  return v;
+}
+int knob_kw() {
+  static const int v = [] {
+    const int64_t x = env_i64("RSAMD_NP_KW");
+    return x >= kWmin && x <= kWmax ? static_cast<int>(x) : 0;
+  }();
+  return v;
+}
+int64_t knob_cpr() {
+  static const int64_t v = std::max<int64_t>(0, env_i64("RSAMD_NP_CPR"));
+  return v;
+}
 constexpr int64_t kMapsMagic = 0x5253485044414d53LL;   // blob header tag
 
 // start draw (relative to the rank's draw 0) of every kept wrap, in order; lead = 1 puts the
@@ -1575,6 +1295,7 @@ struct rs_np_shard {
       *d_vcnt = nullptr, *d_off = nullptr, *d_err = nullptr, *d_tpos = nullptr;
   int64_t *d_row_off = nullptr, *d_starts = nullptr, *d_got = nullptr;
   uint2 *d_ev = nullptr;
+  NpResult *d_res = nullptr;  // world 1 (np_choice_device): the segment's outcome in one copy
   int64_t cap_win = 0, cap_chain = 0, cap_stream = 0, cap_fin = 0, cap_fin_all = 0, cap_fm = 0,
           cap_fm_all = 0, cap_ev = 0, cap_evn = 0, cap_ent = 0, cap_vcnt = 0, cap_off = 0,
           cap_tpos = 0, cap_row = 0, cap_starts = 0;
@@ -1585,7 +1306,8 @@ namespace {
 void shard_free(rs_np_shard *w) {
   void *ptrs[] = {w->d_bits, w->d_win,   w->d_chain, w->d_stream, w->d_fin,     w->d_fin_all,
                   w->d_fin_m, w->d_fin_m_all, w->d_ev_n, w->d_ent, w->d_vcnt, w->d_off,
-                  w->d_err,  w->d_tpos,  w->d_row_off, w->d_starts, w->d_got, w->d_ev};
+                  w->d_err,  w->d_tpos,  w->d_row_off, w->d_starts, w->d_got, w->d_ev,
+                  w->d_res};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
 }
@@ -1629,16 +1351,19 @@ int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 int shard_layout(rs_np_shard &w, int32_t pos, int64_t count) {
   const double E = expected_draws(w.n1, w.py);
   const int64_t margin = 16 * w.n + 4096 + 8 * static_cast<int64_t>(std::ceil(E)) + kN;
-  const int64_t own_cap = kShardSegWords - margin - 2 * kJ;
+  const int64_t own_cap = std::max<int64_t>(seg_words() - margin, 1 << 16);
   const int64_t hcap = std::max<int64_t>(
       1, static_cast<int64_t>(static_cast<double>(own_cap * w.world - 16 * w.n - 4096) / (E * 1.03)));
   const int64_t hs = std::min<int64_t>(count, hcap);
   const int64_t need = static_cast<int64_t>(std::ceil(hs * E * 1.03)) + 16 * w.n + 4096;
   const int64_t Dr = cdiv(need, w.world);
-  // chunk length as np_choice_device: 2 x CUs chunks per rank for N - 1 < 4096, else 1 x CUs
-  const int64_t C0 = static_cast<int64_t>(w.cus) * (w.n1 < 4096 ? 2 : 1);
+  // chunk length: every chunk in one resident round of k_np_track (16-wave workgroups, two
+  // per CU) with equal lengths -- 2 x CUs chunks per rank for N - 1 < 4096; for larger N the
+  // dense entry phase (cost ~ N per chunk) favours 1 x CUs.  Measured (C2, 1e5 tuples, one
+  // GPU): 274 chunks of 2^20 9.9 ms, 508 of 565 248 8.3 ms, 765 of 376 832 9.9 ms.
+  const int64_t C0 = knob_cpr() ? knob_cpr() : static_cast<int64_t>(w.cus) * (w.n1 < 4096 ? 2 : 1);
   const int64_t L = cdiv(cdiv(Dr, C0), 4096) * 4096;
-  w.Wc = std::max<int64_t>(kWmin, std::min<int64_t>(kW, L));
+  w.Wc = knob_kw() ? knob_kw() : std::max<int64_t>(kWmin, std::min<int64_t>(kW, L));
   w.Cr = cdiv(Dr, w.Wc);
   w.C = w.Cr * w.world;
   w.D = w.C * w.Wc;
@@ -1695,10 +1420,9 @@ int shard_windows(rs_np_shard &w, const uint32_t *key, hipStream_t s) {
   return RS_OK;
 }
 
-int shard_parse(rs_np_shard &w, const uint32_t *key, int32_t pos, int64_t count) {
-  rs_ctx *c = w.ctx;
-  HIP_TRY(hipSetDevice(c->device));
-  hipStream_t s = c->stream;
+// device set-up shared by both drivers: kernel attributes, the jump polynomials, counters
+int shard_init(rs_np_shard &w) {
+  HIP_TRY(hipSetDevice(w.ctx->device));
   int st;
   if ((st = shard_kernel_attrs(w.n1))) return st;
   if (!w.d_bits) {
@@ -1712,42 +1436,94 @@ int shard_parse(rs_np_shard &w, const uint32_t *key, int32_t pos, int64_t count)
     int64_t cap = 0;
     if ((st = sgrow(w.d_bits, cap, static_cast<int64_t>(all.size())))) return st;
     HIP_TRY(hipMemcpy(w.d_bits, all.data(), sizeof(int32_t) * all.size(), hipMemcpyHostToDevice));
-    int64_t c1 = 0, c2 = 0;
-    if ((st = sgrow(w.d_err, c1, 1)) || (st = sgrow(w.d_got, c2, 1))) return st;
+    int64_t c1 = 0, c2 = 0, c3 = 0;
+    if ((st = sgrow(w.d_err, c1, 1)) || (st = sgrow(w.d_got, c2, 1)) || (st = sgrow(w.d_res, c3, 1)))
+      return st;
   }
-  if ((st = shard_layout(w, pos, count))) return st;
-  // 1: own words (+ margin)
+  return RS_OK;
+}
+
+// 1: the rank's own words (+ margin) for the segment laid out by shard_layout
+int shard_stream(rs_np_shard &w, const uint32_t *key) {
+  hipStream_t s = w.ctx->stream;
+  int st;
   if ((st = sgrow(w.d_stream, w.cap_stream, w.Lb * kN))) return st;
   if ((st = shard_windows(w, key, s))) return st;
   k_mt_stream<<<static_cast<unsigned>(w.G), 256, 0, s>>>(w.d_win, w.d_stream, w.Lb);
   HIP_TRY(hipGetLastError());
-  // 1: all-entry parse of own chunks
-  const int Cr = static_cast<int>(w.Cr), Wc = static_cast<int>(w.Wc);
   if ((st = sgrow(w.d_fin, w.cap_fin, w.Cr * w.n1)) || (st = sgrow(w.d_fin_m, w.cap_fm, w.Cr)) ||
       (st = sgrow(w.d_ev_n, w.cap_evn, w.Cr)) || (st = sgrow(w.d_tpos, w.cap_tpos, w.Cr)) ||
-      (st = sgrow(w.d_vcnt, w.cap_vcnt, w.Cr)) || (st = sgrow(w.d_off, w.cap_off, w.Cr)))
+      (st = sgrow(w.d_vcnt, w.cap_vcnt, w.Cr)) || (st = sgrow(w.d_off, w.cap_off, w.Cr)) ||
+      (st = sgrow(w.d_ent, w.cap_ent, w.Cr)) ||
+      // every hypothesis spans at least n1 draws: a bound on the own starts
+      (st = sgrow(w.d_starts, w.cap_starts, w.Cr * w.Wc / std::max(1, w.n1) + 4)))
     return st;
+  return RS_OK;
+}
+
+// 1: the all-entry parse of the rank's chunks, enqueued (wrap log of the current capacity)
+int shard_enqueue_parse(rs_np_shard &w) {
+  hipStream_t s = w.ctx->stream;
+  int st;
   const double E = expected_draws(w.n1, w.py);
-  const uint32_t *own = w.d_stream + (w.s_lo - w.wbase);
+  w.ecap = static_cast<int>(std::min<int64_t>(
+      w.Wc + 2 * w.n1, (static_cast<int64_t>(70.0 * w.Wc / E) + 4 * w.n1 + 4096) << w.ecap_shift));
+  if ((st = sgrow(w.d_ev, w.cap_ev, w.Cr * w.ecap))) return st;
+  HIP_TRY(hipMemsetAsync(w.d_err, 0, sizeof(int), s));
+  const int Cr = static_cast<int>(w.Cr), Wc = static_cast<int>(w.Wc);
   const int64_t lds = 8 * static_cast<int64_t>((w.n1 + 1) & ~1);
-  for (;;) {
-    w.ecap = static_cast<int>(std::min<int64_t>(
-        w.Wc + 2 * w.n1, (static_cast<int64_t>(70.0 * w.Wc / E) + 4 * w.n1 + 4096) << w.ecap_shift));
-    if ((st = sgrow(w.d_ev, w.cap_ev, w.Cr * w.ecap))) return st;
-    HIP_TRY(hipMemsetAsync(w.d_err, 0, sizeof(int), s));
-    EntryArgs ea{own, w.Cr * w.Wc, Wc, w.n1, w.d_fin, w.d_fin_m, w.d_ev, w.d_ev_n, w.d_tpos,
-                 w.ecap, w.d_err, nullptr};
-    const bool small = w.n1 < 64;
-    if (w.py) {
-      k_np_entry<true><<<Cr, kEntryThreads, static_cast<size_t>(lds), s>>>(ea, ea.draws);
-      HIP_TRY(hipGetLastError());
-      (small ? k_np_track<true, true> : k_np_track<true, false>)<<<Cr, 64 * kTrackWaves, 0, s>>>(ea, ea.draws);
-    } else {
-      k_np_entry<false><<<Cr, kEntryThreads, static_cast<size_t>(lds), s>>>(ea, ea.draws);
-      HIP_TRY(hipGetLastError());
-      (small ? k_np_track<false, true> : k_np_track<false, false>)<<<Cr, 64 * kTrackWaves, 0, s>>>(ea, ea.draws);
-    }
+  EntryArgs ea{w.d_stream + (w.s_lo - w.wbase), w.Cr * w.Wc, Wc, w.n1, w.d_fin, w.d_fin_m,
+               w.d_ev, w.d_ev_n, w.d_tpos, w.ecap, w.d_err, nullptr};
+  const bool small = w.n1 < 64;  // several hypothesis ends in one tracking window
+  if (w.py) {
+    k_np_entry<true><<<Cr, kEntryThreads, static_cast<size_t>(lds), s>>>(ea, ea.draws);
     HIP_TRY(hipGetLastError());
+    (small ? k_np_track<true, true> : k_np_track<true, false>)<<<Cr, 64 * kTrackWaves, 0, s>>>(ea, ea.draws);
+  } else {
+    k_np_entry<false><<<Cr, kEntryThreads, static_cast<size_t>(lds), s>>>(ea, ea.draws);
+    HIP_TRY(hipGetLastError());
+    (small ? k_np_track<false, true> : k_np_track<false, false>)<<<Cr, 64 * kTrackWaves, 0, s>>>(ea, ea.draws);
+  }
+  HIP_TRY(hipGetLastError());
+  return RS_OK;
+}
+
+// 3 (the true entry states in d_ent): the rank's wraps of the true trajectory, their count
+// (scan into *got, at most cap) and start draws (d_starts, relative to the rank's draw 0)
+int shard_enqueue_starts(rs_np_shard &w, int64_t cap, int64_t *got) {
+  hipStream_t s = w.ctx->stream;
+  const int Cr = static_cast<int>(w.Cr);
+  k_np_filter<<<Cr, 64, 0, s>>>(w.d_ev, w.d_ev_n, w.d_ent + w.rank * w.Cr, w.d_vcnt, w.ecap);
+  HIP_TRY(hipGetLastError());
+  k_np_scan<<<1, 1024, 0, s>>>(w.d_vcnt, Cr, w.d_off, cap, got);
+  HIP_TRY(hipGetLastError());
+  k_np_starts_local<<<Cr, 256, 0, s>>>(w.d_ev, w.d_vcnt, w.d_off, w.d_starts, w.ecap,
+                                       static_cast<int>(w.Wc), w.rank == 0 ? 1 : 0);
+  HIP_TRY(hipGetLastError());
+  return RS_OK;
+}
+
+// 4: the tuples of hypotheses [lo, hi) (rank-local start indices; waves at or beyond *got exit)
+void shard_launch_tuples(rs_np_shard &w, int64_t lo, int64_t hi, const int64_t *got,
+                         int32_t *d_out) {
+  const int n1p = (w.n1 + 1) & ~1;
+  const int64_t tl = (static_cast<int64_t>(sizeof(uint32_t)) * kTupRing +
+                      static_cast<int64_t>(sizeof(uint16_t)) * n1p) * kTupWaves;
+  (w.py ? k_np_tuples_wave<true> : k_np_tuples_wave<false>)<<<static_cast<unsigned>(cdiv(hi - lo, kTupWaves)),
+                                                               64 * kTupWaves, static_cast<size_t>(tl),
+                                                               w.ctx->stream>>>(
+      w.d_stream + (w.s_lo - w.wbase), w.d_starts, got, lo, hi, w.n1, n1p, w.k, d_out, w.d_err,
+      w.nwords);
+}
+
+int shard_parse(rs_np_shard &w, const uint32_t *key, int32_t pos, int64_t count) {
+  hipStream_t s = w.ctx->stream;
+  int st;
+  if ((st = shard_init(w)) || (st = shard_layout(w, pos, count)) || (st = shard_stream(w, key)))
+    return st;
+  const int Cr = static_cast<int>(w.Cr);
+  for (;;) {
+    if ((st = shard_enqueue_parse(w))) return st;
     int err = 0;
     HIP_TRY(hipMemcpyAsync(&err, w.d_err, sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -1835,17 +1611,8 @@ int shard_compose(rs_np_shard &w, const uint8_t *blobs, int64_t stride) {
   k_np_compose<<<1, 1024, 0, s>>>(w.d_fin_all, w.d_fin_m_all, w.n1, static_cast<int>(w.C), w.d_ent,
                                   w.d_row_off);
   HIP_TRY(hipGetLastError());
-  const int Cr = static_cast<int>(w.Cr);
-  k_np_filter<<<Cr, 64, 0, s>>>(w.d_ev, w.d_ev_n, w.d_ent + w.rank * w.Cr, w.d_vcnt, w.ecap);
-  HIP_TRY(hipGetLastError());
-  k_np_scan<<<1, 1024, 0, s>>>(w.d_vcnt, Cr, w.d_off, std::numeric_limits<int64_t>::max(), w.d_got);
-  HIP_TRY(hipGetLastError());
-  // every hypothesis spans at least n1 draws: a bound on the own starts
+  if ((st = shard_enqueue_starts(w, std::numeric_limits<int64_t>::max(), w.d_got))) return st;
   const int lead = w.rank == 0 ? 1 : 0;
-  if ((st = sgrow(w.d_starts, w.cap_starts, w.Cr * w.Wc / std::max(1, w.n1) + 4))) return st;
-  k_np_starts_local<<<Cr, 256, 0, s>>>(w.d_ev, w.d_vcnt, w.d_off, w.d_starts, w.ecap,
-                                       static_cast<int>(w.Wc), lead);
-  HIP_TRY(hipGetLastError());
   int64_t got = 0, first = -1;
   HIP_TRY(hipMemcpyAsync(&got, w.d_got, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
@@ -1873,7 +1640,6 @@ int shard_tuples(rs_np_shard &w, int64_t base, int64_t hi, int64_t next_start, i
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = c->stream;
   const int64_t own0 = static_cast<int64_t>(w.rank) * w.Cr * w.Wc;
-  const uint32_t *own = w.d_stream + (w.s_lo - w.wbase);
   if (cnt > 0) {
     if (cnt == w.nstarts) {  // the last own hypothesis ends at the next rank's first start
       if (next_start < 0) return rs::fail(RS_EINVAL, "np shard: the last hypothesis needs the next start");
@@ -1884,12 +1650,7 @@ int shard_tuples(rs_np_shard &w, int64_t base, int64_t hi, int64_t next_start, i
     }
     HIP_TRY(hipMemcpy(w.d_got, &cnt, sizeof(int64_t), hipMemcpyHostToDevice));
     HIP_TRY(hipMemsetAsync(w.d_err, 0, sizeof(int), s));
-    const int n1p = (w.n1 + 1) & ~1;
-    const int64_t tl = (static_cast<int64_t>(sizeof(uint32_t)) * kTupRing +
-                        static_cast<int64_t>(sizeof(uint16_t)) * n1p) * kTupWaves;
-    (w.py ? k_np_tuples_wave<true> : k_np_tuples_wave<false>)<<<static_cast<unsigned>(cdiv(cnt, kTupWaves)),
-                                                                 64 * kTupWaves, static_cast<size_t>(tl), s>>>(
-        own, w.d_starts, w.d_got, 0, cnt, w.n1, n1p, w.k, d_out, w.d_err, w.nwords);
+    shard_launch_tuples(w, 0, cnt, w.d_got, d_out);
     HIP_TRY(hipGetLastError());
     int err = 0;
     HIP_TRY(hipMemcpyAsync(&err, w.d_err, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -1918,6 +1679,54 @@ int shard_tuples(rs_np_shard &w, int64_t base, int64_t hi, int64_t next_start, i
   return RS_OK;
 }
 
+// World 1, all on the device (np_choice_device): one segment of at most `count` hypotheses
+// from (key, pos) -- the same steps with the compose read straight from the device maps and
+// one host synchronisation; its hypotheses [lo, hi) go to d_out as k-tuples; *got and
+// (key, pos) advance.
+int shard_run_local(rs_np_shard &w, uint32_t *key, int32_t *pos, int64_t count, int64_t lo,
+                    int64_t hi, int32_t *d_out, int64_t *got_out) {
+  int st;
+  if ((st = shard_init(w)) || (st = shard_layout(w, *pos, count)) || (st = shard_stream(w, key)))
+    return st;
+  hipStream_t s = w.ctx->stream;
+  NpResult res;
+  for (;;) {
+    if ((st = shard_enqueue_parse(w))) return st;
+    k_np_compose<<<1, 1024, 0, s>>>(w.d_fin, w.d_fin_m, w.n1, static_cast<int>(w.Cr), w.d_ent,
+                                    nullptr);
+    HIP_TRY(hipGetLastError());
+    if ((st = shard_enqueue_starts(w, w.count, &w.d_res->got))) return st;
+    if (hi > lo) {  // waves beyond the delivered count exit
+      shard_launch_tuples(w, lo, hi, &w.d_res->got, d_out);
+      HIP_TRY(hipGetLastError());
+    }
+    // delivered count, draws used, errors and the stream block holding the next word
+    k_np_result<<<1, 64, 0, s>>>(w.d_stream, w.d_starts, *pos, w.d_err, w.d_res);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(&res, w.d_res, sizeof(res), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (res.err & 1) {  // wrap log overflow: a larger log, the same chunks again
+      if (w.ecap >= w.Wc + 2 * w.n1) return rs::fail(RS_EDEVICE, "np sampler: wrap log overflow");
+      ++w.ecap_shift;
+      continue;
+    }
+    break;
+  }
+  if (res.err) return rs::fail(RS_EDEVICE, "np sampler: hypothesis parse mismatch");
+  if (res.got < 1) return rs::fail(RS_EDEVICE, "np sampler: segment holds no complete hypothesis");
+  // state after `used` draws: the block holding the last word drawn (rs_mt_jump's convention)
+  const int64_t W = *pos + res.used;
+  if (W > kN) {
+    const int64_t b = (W - 1) / kN;
+    for (int i = 0; i < kN; ++i) key[i] = untemper(res.blk[i]);
+    *pos = static_cast<int32_t>(W - b * kN);
+  } else {
+    *pos = static_cast<int32_t>(W);
+  }
+  *got_out = res.got;
+  return RS_OK;
+}
+
 }  // namespace
 
 namespace rs {
@@ -1926,7 +1735,96 @@ int np_shard_tuples_device(rs_np_shard *w, int64_t base, int64_t hi, int64_t nex
   if (!w) return fail(RS_EINVAL, "null shard");
   return shard_tuples(*w, base, hi, next_start, final_idx, d_out, key_out, pos_out);
 }
+
+bool np_gpu_supported(int64_t n, int32_t k) { return k >= 1 && k <= 8 && k <= n && n - 1 <= kMaxN1; }
+
+void np_shard_free(rs_ctx *c) {
+  if (c->np_shard) {
+    (void)rs_np_shard_destroy(c->np_shard);
+    c->np_shard = nullptr;
+  }
+}
+
+// The numpy (py: CPython) stream's next `count` choice(n, k) tuples, rows [skip, skip + take)
+// into device memory, on the context stream; advances (key, pos).  Synchronous.  The
+// context's world-1 session carries the buffers from call to call.
+int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t k,
+                     int64_t count, int32_t *d_out, bool py, int64_t skip, int64_t take) {
+  if (take < 0) take = count - skip;
+  if (skip < 0 || skip + take > count) return fail(RS_EINVAL, "np sampler: slice out of range");
+  if (k < 1 || k > 8) return fail(RS_EINVAL, "np sampler: k must be in 1..8");
+  if (k > n)
+    return fail(RS_EINVAL, py ? "Cannot generate more indices than the amount of values in the set "
+                                "from which they are extracted. n should therefore be smaller or "
+                                "equal to set_length"
+                              : "Cannot take a larger sample than population when 'replace=False'");
+  if (n - 1 > kMaxN1) return fail(RS_EINVAL, "np sampler: population too large for the GPU parse");
+  if (*pos < 0 || *pos > kN) return fail(RS_EINVAL, "bad MT19937 position");
+  if (count == 0) return RS_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  if (n <= 1) {  // a one-element shuffle draws nothing: every tuple is (0)
+    HIP_TRY(hipMemsetAsync(d_out, 0, sizeof(int32_t) * static_cast<size_t>(take) * k, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RS_OK;
+  }
+  rs_np_shard *w = c->np_shard;
+  if (w && (w->n != n || w->k != k || w->py != py)) {
+    np_shard_free(c);
+    w = nullptr;
+  }
+  int st;
+  if (!w) {
+    if ((st = rs_np_shard_create(c, n, k, 1, 0, py ? 1 : 0, &w))) return st;
+    c->np_shard = w;
+  }
+  int64_t done = 0;
+  while (done < count) {
+    // this segment's hypotheses [done, done + got) against the slice [skip, skip + take)
+    const int64_t lo = std::max<int64_t>(skip - done, 0);
+    const int64_t hi = std::max(lo, std::min<int64_t>(skip + take - done, count - done));
+    int64_t got = 0;
+    if ((st = shard_run_local(*w, key, pos, count - done, lo, hi,
+                              hi > lo ? d_out + (done + lo - skip) * k : nullptr, &got)))
+      return st;
+    done += got;
+  }
+  return RS_OK;
+}
 }  // namespace rs
+
+namespace {
+// Tuples of either stream into host memory through the context's scratch buffer.
+int choice_tuples_gpu(rs_ctx *c, uint32_t *mt_key, int32_t *mt_pos, int64_t n, int32_t k,
+                      int64_t count, int32_t *out, bool py) {
+  if (!c || !mt_key || !mt_pos || (count > 0 && !out))
+    return rs::fail(RS_EINVAL, "tuples_gpu: null pointer");
+  if (count < 0 || k < 0) return rs::fail(RS_EINVAL, "negative dimensions are not allowed");
+  if (count == 0) return RS_OK;
+  int st;
+  if ((st = rs::ensure_scratch(c, sizeof(int32_t) * static_cast<size_t>(count) * k))) return st;
+  uint32_t key[kN];
+  int32_t pos = *mt_pos;
+  std::memcpy(key, mt_key, sizeof(key));
+  if ((st = rs::np_choice_device(c, key, &pos, n, k, count, static_cast<int32_t *>(c->scratch),
+                                 py)))
+    return st;
+  HIP_TRY(hipMemcpy(out, c->scratch, sizeof(int32_t) * static_cast<size_t>(count) * k,
+                    hipMemcpyDeviceToHost));
+  std::memcpy(mt_key, key, sizeof(key));
+  *mt_pos = pos;
+  return RS_OK;
+}
+}  // namespace
+
+extern "C" int rs_np_choice_tuples_gpu(rs_ctx *c, uint32_t *mt_key, int32_t *mt_pos, int64_t n,
+                                       int32_t k, int64_t count, int32_t *out) {
+  return choice_tuples_gpu(c, mt_key, mt_pos, n, k, count, out, false);
+}
+
+extern "C" int rs_py_shuffle_tuples_gpu(rs_ctx *c, uint32_t *mt_key, int32_t *mt_pos, int64_t n,
+                                        int32_t k, int64_t count, int32_t *out) {
+  return choice_tuples_gpu(c, mt_key, mt_pos, n, k, count, out, true);
+}
 
 extern "C" int rs_np_shard_create(rs_ctx *c, int64_t n, int32_t k, int32_t world, int32_t rank,
                                   int32_t py, rs_np_shard **out) {

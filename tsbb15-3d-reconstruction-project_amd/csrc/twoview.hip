@@ -344,13 +344,21 @@ struct GsInfo {  // == rs_gs_info
 // ---- reference-faithful gold standard (fun.py:358 as scipy runs it) ------------------------
 // Residuals of lab3.fmatrix_residuals_gs (lab3.py:228-266) for one point k of the parameter
 // vector (C1 row-major, X_k): left = pl - project(X_k, C1), right = pr - project(X_k, [I|0]).
+// project (lab3.py:52-72) is np.dot(C, [X; 1]): OpenBLAS dgemm, whose microkernel accumulates
+// over k = 0..3 with FMAs from zero, so row i is fma(c_i3, 1, fma(c_i2, x2, fma(c_i1, x1,
+// c_i0 x0))) = fma(c_i2, x2, fma(c_i1, x1, c_i0 x0)) + c_i3 -- the same bits (checked against
+// numpy in tests/test_gpu_twoview.py; tools/gs_trace_cpu.py shows that with these bits and
+// the Jacobian's column-major layout scipy's TRF retraces the reference's path exactly).
+__device__ __forceinline__ double dgemm_row(const double *c, double X0, double X1, double X2) {
+  return __builtin_fma(c[2], X2, __builtin_fma(c[1], X1, c[0] * X0)) + c[3];
+}
 __device__ __forceinline__ void gs_res4(const double *C, double X0, double X1, double X2,
                                         double plx, double ply, double prx, double pry,
                                         double r[4]) {
 #pragma clang fp contract(off)
-  const double y0 = ((C[0] * X0 + C[1] * X1) + C[2] * X2) + C[3];
-  const double y1 = ((C[4] * X0 + C[5] * X1) + C[6] * X2) + C[7];
-  const double y2 = ((C[8] * X0 + C[9] * X1) + C[10] * X2) + C[11];
+  const double y0 = dgemm_row(C, X0, X1, X2);
+  const double y1 = dgemm_row(C + 4, X0, X1, X2);
+  const double y2 = dgemm_row(C + 8, X0, X1, X2);
   r[0] = plx - y0 / y2;
   r[1] = ply - y1 / y2;
   r[2] = prx - X0 / X2;
@@ -360,8 +368,9 @@ __device__ __forceinline__ void gs_res4(const double *C, double X0, double X1, d
 // Thread per point k: the residual f(x) (rows k, n+k, 2n+k, 3n+k) and the 2-point forward
 // differences scipy's approx_derivative forms for least_squares(jac='2-point'): column j is
 // (f(x with x_j -> xp_j) - f(x)) / dx_j, xp and dx computed by the caller exactly as scipy
-// does.  Entries a parameter cannot reach are left as the caller zeroed them (their forward
-// differences are exactly 0: the same inputs give the same values).
+// does.  J is stored column-major (Jt[col][row], as scipy returns J_transposed.T): LSMR's
+// products with J then run in the reference's order.  Entries a parameter cannot reach are
+// left as the caller zeroed them (their forward differences are exactly 0).
 __global__ __launch_bounds__(128) void k_gs_fd(const double *__restrict__ x,
                                                const double *__restrict__ xp,
                                                const double *__restrict__ dx,
@@ -371,7 +380,7 @@ __global__ __launch_bounds__(128) void k_gs_fd(const double *__restrict__ x,
 #pragma clang fp contract(off)
   const int64_t k = static_cast<int64_t>(blockIdx.x) * 128 + threadIdx.x;
   if (k >= n) return;
-  const int64_t nc = 12 + 3 * n;
+  const int64_t nr = 4 * n;
   double C[12];
 #pragma unroll
   for (int j = 0; j < 12; ++j) C[j] = x[j];
@@ -390,8 +399,8 @@ __global__ __launch_bounds__(128) void k_gs_fd(const double *__restrict__ x,
     double r[4];
     gs_res4(C, X0, X1, X2, plx, ply, prx, pry, r);
     C[j] = keep;
-    J[row[0] * nc + j] = (r[0] - r0[0]) / dx[j];
-    J[row[1] * nc + j] = (r[1] - r0[1]) / dx[j];
+    J[j * nr + row[0]] = (r[0] - r0[0]) / dx[j];
+    J[j * nr + row[1]] = (r[1] - r0[1]) / dx[j];
   }
 #pragma unroll
   for (int c = 0; c < 3; ++c) {  // this point's coordinates: its four residuals
@@ -400,7 +409,7 @@ __global__ __launch_bounds__(128) void k_gs_fd(const double *__restrict__ x,
     gs_res4(C, c == 0 ? xp[col] : X0, c == 1 ? xp[col] : X1, c == 2 ? xp[col] : X2, plx, ply,
             prx, pry, r);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) J[row[q] * nc + col] = (r[q] - r0[q]) / dx[col];
+    for (int q = 0; q < 4; ++q) J[col * nr + row[q]] = (r[q] - r0[q]) / dx[col];
   }
 }
 

@@ -255,12 +255,14 @@ def gs_jacobian_2point(x, pl, pr, ctx=None):
     xp = x + h
     dx = xp - x
     f = np.empty(4 * n)
-    J = np.empty((4 * n, 12 + 3 * n))
+    Jt = np.empty((12 + 3 * n, 4 * n))
     _ffi.check(_ffi.lib().rs_gs_residuals_fd(_ctx(ctx), _ffi.ptr(x, _d), _ffi.ptr(xp, _d),
                                              _ffi.ptr(dx, _d), _ffi.ptr(pl, _d),
                                              _ffi.ptr(pr, _d), n, _ffi.ptr(f, _d),
-                                             _ffi.ptr(J, _d)))
-    return J
+                                             _ffi.ptr(Jt, _d)))
+    # scipy's approx_derivative returns J_transposed.T (Fortran order); LSMR's BLAS products
+    # with J depend on that layout, and so does the TRF path (tools/gs_trace_cpu.py)
+    return Jt.T
 
 
 @dataclass
@@ -274,13 +276,23 @@ class GoldStandardTRF:
     status: int   # scipy least_squares status (1 gtol, 2 ftol, 3 xtol, 4 ftol and xtol, 0 max_nfev)
 
 
+def gs_trf(params, pl, pr, ctx=None):
+    """fun.py:358 from a given start: scipy.optimize.least_squares(fmatrix_residuals_gs,
+    params, xtol=2.22e-14, tr_solver='lsmr') with the residual and the 2-point Jacobian
+    computed on the GPU in the reference's bits and layout; returns scipy's result.  From the
+    reference's start it retraces the reference's path evaluation for evaluation
+    (tests/test_gpu_twoview.py against tests/golden/gs_trace.npz)."""
+    from scipy.optimize import least_squares
+    return least_squares(gs_residuals, _ffi.f64c(params), jac=gs_jacobian_2point,
+                         xtol=2.22e-14, tr_solver='lsmr', args=(pl, pr), kwargs={"ctx": ctx})
+
+
 def gold_standard_trf_full(F, pl, pr, ctx=None):
     """fun.py:343-369 as the reference runs it.  Cameras from F_RANSAC and the optimal
     triangulation of the inliers on the GPU, then scipy.optimize.least_squares with the
     reference's options (fun.py:358: method 'trf', xtol=2.22e-14, tr_solver='lsmr', default
     ftol / gtol / x_scale / max_nfev) over a residual and a forward-difference Jacobian
     computed on the GPU, then F from the refined cameras on the GPU."""
-    from scipy.optimize import least_squares
     pl = _ffi.f64c(pl)
     pr = _ffi.f64c(pr)
     if pl.shape != pr.shape or pl.ndim != 2 or pl.shape[0] != 2:
@@ -289,8 +301,7 @@ def gold_standard_trf_full(F, pl, pr, ctx=None):
     X = triangulate_optimal_batch(C1, C2, pl, pr, ctx=ctx)      # fun.py:352
     params = np.hstack((C1.ravel(), X.ravel()))                  # fun.py:355
     f0 = gs_residuals(params, pl, pr, ctx)
-    res = least_squares(gs_residuals, params, jac=gs_jacobian_2point, xtol=2.22e-14,
-                        tr_solver='lsmr', args=(pl, pr), kwargs={"ctx": ctx})
+    res = gs_trf(params, pl, pr, ctx)
     C1g = res.x[:12].reshape(3, 4)
     Fg = fmatrix_from_cameras(C1g, I34, ctx)                     # fun.py:362-368
     return GoldStandardTRF(Fg, C1g, res.x[12:].reshape(-1, 3), 0.5 * float(f0 @ f0),
