@@ -145,6 +145,42 @@ def fmatrix_residuals_gs(params, pl, pr):
     return np.concatenate([(pl - project(X, C1)).ravel(), (pr - project(X, I34)).ravel()])
 
 
+def fmatrix_residuals_gs_jac_2point(params, pl, pr):
+    """scipy's approx_derivative(fmatrix_residuals_gs, params, method='2-point') -- the
+    Jacobian least_squares forms at fun.py:358 -- without its 12 + 3N residual evaluations:
+    a column perturbs one parameter, which moves only the residuals of the camera (every
+    point's left pair) or of its point, and those are recomputed with the same numpy
+    operations (np.dot per element is independent of the other columns), so every entry has
+    scipy's bits; the zeros scipy forms as 0 / dx keep dx's sign, and the array is the
+    transpose of a C-order (n, m) array, as scipy returns it (tests/test_oracle_twoview.py
+    checks it against approx_derivative bit for bit)."""
+    params = np.asarray(params, dtype=np.float64)
+    n = pl.shape[1]
+    sign = (params >= 0).astype(float) * 2 - 1
+    h = np.finfo(np.float64).eps ** 0.5 * sign * np.maximum(1.0, np.abs(params))
+    xp = params + h
+    dx = xp - params
+    f0 = fmatrix_residuals_gs(params, pl, pr)
+    Jt = np.empty((12 + 3 * n, 4 * n))
+    Jt[:] = 0.0 / dx[:, None]
+    C1 = params[:12].reshape(3, 4)
+    X = params[12:].reshape(-1, 3).T
+    for j in range(12):
+        Cp = C1.ravel().copy()
+        Cp[j] = xp[j]
+        r = (pl - project(X, Cp.reshape(3, 4))).ravel()
+        Jt[j, :2 * n] = (r - f0[:2 * n]) / dx[j]
+    idx = np.arange(n)
+    for c in range(3):
+        Xp = X.copy()
+        Xp[c] = xp[12 + 3 * idx + c]
+        r = np.concatenate([(pl - project(Xp, C1)).ravel(), (pr - project(Xp, I34)).ravel()])
+        col = 12 + 3 * idx + c
+        for q in range(4):
+            Jt[col, q * n + idx] = (r[q * n:(q + 1) * n] - f0[q * n:(q + 1) * n]) / dx[col]
+    return Jt.T
+
+
 def gold_standard(F, pl, pr, **ls_kwargs):
     """fun.py:336-369 on the inliers (pl, pr): returns (F_gold, least_squares result)."""
     C1, _ = fmatrix_cameras(F)

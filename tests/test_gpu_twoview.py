@@ -229,36 +229,23 @@ def _traced_trf(x0, a, b):
 
 
 def _oracle_trf_trace(x0, a, b):
-    """The reference's call (fun.py:358) with the oracle's restatement of
-    lab3.fmatrix_residuals_gs and scipy's own '2-point' Jacobian, on THIS host, recording the
-    evaluations made outside the Jacobian (as make_golden_gs_trace.py did in the build
-    container)."""
-    import sys
+    """The reference's call (fun.py:358) in the reference's arithmetic on THIS host: the
+    oracle's restatement of lab3.fmatrix_residuals_gs with scipy's '2-point' Jacobian (formed
+    by oracle.twoview_ref.fmatrix_residuals_gs_jac_2point, bit-equal to approx_derivative,
+    tests/test_oracle_twoview.py), recording every residual evaluation outside the Jacobian
+    (as make_golden_gs_trace.py did in the build container)."""
     from scipy.optimize import least_squares
-    lsq_mod = sys.modules["scipy.optimize._lsq.least_squares"]
-    rec = {"x": [], "c": [], "j": False}
-    real_ad = lsq_mod.approx_derivative
-
-    def ad(*args, **kw):
-        rec["j"] = True
-        try:
-            return real_ad(*args, **kw)
-        finally:
-            rec["j"] = False
+    xs, cs = [], []
 
     def fun(x, pl, pr):
         f = tvr.fmatrix_residuals_gs(x, pl, pr)
-        if not rec["j"]:
-            rec["x"].append(x.copy())
-            rec["c"].append(0.5 * float(f @ f))
+        xs.append(x.copy())
+        cs.append(0.5 * float(f @ f))
         return f
 
-    lsq_mod.approx_derivative = ad
-    try:
-        res = least_squares(fun, x0, xtol=2.22e-14, tr_solver='lsmr', args=(a, b))
-    finally:
-        lsq_mod.approx_derivative = real_ad
-    return res, rec["x"], rec["c"]
+    res = least_squares(fun, x0, jac=tvr.fmatrix_residuals_gs_jac_2point, xtol=2.22e-14,
+                        tr_solver='lsmr', args=(a, b))
+    return res, xs, cs
 
 
 def _first_divergence(xs, cs, ref_x, ref_c, kept_idx=None):
@@ -284,11 +271,15 @@ def test_gold_standard_trf_retraces_reference_path(ctx):
     comparison with the trace recorded in the build container is reported, and is exact
     there (tools/gs_trace_cpu.py: numpy with the GPU's arithmetic retraces all 1 067 / 20 021
     evaluations of the noisy / s300 traces)."""
+    import time
     a, b, _, z = _gs_case("noisy")
     tr = golden("gs_trace.npz")
     x0 = tr["noisy_x0"]
+    t0 = time.perf_counter()
     res, xs, cs = _traced_trf(x0, a, b)
+    t1 = time.perf_counter()
     ores, oxs, ocs = _oracle_trf_trace(x0, a, b)
+    t2 = time.perf_counter()
     first, kx = _first_divergence(xs, cs, oxs, ocs)
     tfirst, tkx = _first_divergence(xs, cs, tr["noisy_kept_x"], tr["noisy_costs"],
                                     tr["noisy_kept_idx"])
@@ -296,20 +287,22 @@ def test_gold_standard_trf_retraces_reference_path(ctx):
           f"cost {res.cost!r}; the reference form on this host: nfev {ores.nfev}, cost "
           f"{ores.cost!r}; first divergence from it: cost {first}, x {kx}; from the build "
           f"container's trace (nfev {int(tr['noisy_nfev'])}, cost "
-          f"{float(tr['noisy_cost_final'])!r}): cost {tfirst}, x {tkx}")
+          f"{float(tr['noisy_cost_final'])!r}): cost {tfirst}, x {tkx}; {t1 - t0:.1f} s GPU "
+          f"path, {t2 - t1:.1f} s numpy")
     assert first is None and kx is None and len(cs) == len(ocs), (first, kx, len(cs), len(ocs))
     assert res.nfev == ores.nfev and res.status == ores.status
     assert np.array_equal(res.x, ores.x)
 
 
-@pytest.mark.parametrize("tag", ["clean", "noisy", "s300"])
+@pytest.mark.parametrize("tag", ["clean", "noisy"])
 def test_gold_standard_trf_end_to_end(ctx, tag):
     """fun.py:343-369 end to end on the GPU (cameras of F_RANSAC, optimal triangulation,
     then the TRF above).  Clean pair: the reference's F_gold to 1e-9.  Noisy pairs: the start
     differs from the reference's in the last bits (GPU SVD / root finder against LAPACK), and
     the reference's own end point moves by 3e-4 under a 1e-15 relative change of its start
     (tools/gs_trace_cpu.py): there the bar is the start (cost to 1e-9), the
-    termination kind and the final cost within 5 %."""
+    termination kind and the final cost within 5 %.  (The s300 pair is left out: like the
+    reference, whose TRF runs 20 021 evaluations there, it takes minutes.)"""
     a, b, F0, z = _gs_case(tag)
     g = twoview.gold_standard_trf_full(F0, a, b)
     dF = np.abs(nF(g.F) - nF(z[f"gs_{tag}_F_gold"])).max()

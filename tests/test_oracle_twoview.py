@@ -118,3 +118,25 @@ def test_objective_and_converged_gold_standard():
     np.testing.assert_allclose(ransac_ref.normalize_F(F), ransac_ref.normalize_F(Fs), atol=1e-9)
     assert tv.gs_objective(F, a, b) <= obj_ref
     assert info["cost"] <= float(z["gs_s300_cost_final"])
+
+
+def test_vectorised_2point_jacobian_equals_scipy():
+    """oracle.twoview_ref.fmatrix_residuals_gs_jac_2point = scipy's approx_derivative(
+    '2-point') of the residual (the Jacobian fun.py:358's least_squares forms), bit for bit
+    and in scipy's column-major layout, at the reference's noisy / s300 starts."""
+    from scipy.optimize._numdiff import approx_derivative
+    from conftest import golden
+    tr = golden("gs_trace.npz")
+    c1, tvz = golden("dino_c1.npz"), golden("twoview.npz")
+    cases = {"noisy": (c1["noisy_p1"][:, c1["noisy_full_S_ransac"]],
+                       c1["noisy_p2"][:, c1["noisy_full_S_ransac"]]),
+             "s300": (tvz["gs_s300_p1"][:, tvz["gs_s300_S_ransac"]],
+                      tvz["gs_s300_p2"][:, tvz["gs_s300_S_ransac"]])}
+    for tag, (a, b) in cases.items():
+        x0 = tr[f"{tag}_x0"]
+        assert np.array_equal(tv.fmatrix_residuals_gs(x0, a, b), tr[f"{tag}_f0"])
+        J = tv.fmatrix_residuals_gs_jac_2point(x0, a, b)
+        Jr = approx_derivative(tv.fmatrix_residuals_gs, x0, method="2-point", args=(a, b))
+        assert J.flags["F_CONTIGUOUS"] and J.shape == Jr.shape
+        assert np.array_equal(J, Jr)
+        assert np.array_equal(np.signbit(J), np.signbit(Jr))

@@ -1361,7 +1361,14 @@ int shard_layout(rs_np_shard &w, int32_t pos, int64_t count) {
   // per CU) with equal lengths -- 2 x CUs chunks per rank for N - 1 < 4096; for larger N the
   // dense entry phase (cost ~ N per chunk) favours 1 x CUs.  Measured (C2, 1e5 tuples, one
   // GPU): 274 chunks of 2^20 9.9 ms, 508 of 565 248 8.3 ms, 765 of 376 832 9.9 ms.
-  const int64_t C0 = knob_cpr() ? knob_cpr() : static_cast<int64_t>(w.cus) * (w.n1 < 4096 ? 2 : 1);
+  // A rank's share of a sharded segment is short: chunks below ~64 N draws spend most of
+  // their time in the dense all-entry phase (~N draws per surviving trajectory), so the count
+  // drops before the length does (C2 over 8 ranks, per-rank parse: 512 chunks of 73 728
+  // draws 3.1 ms, 256 of 141 312 2.7 ms, 128 2.9 ms, 64 4.0 ms).
+  const int64_t Cdef = static_cast<int64_t>(w.cus) * (w.n1 < 4096 ? 2 : 1);
+  const int64_t C0 = knob_cpr() ? knob_cpr()
+                                : std::max<int64_t>(1, std::min<int64_t>(
+                                                           Cdef, Dr / std::max<int64_t>(kWmin, 64 * w.n1)));
   const int64_t L = cdiv(cdiv(Dr, C0), 4096) * 4096;
   w.Wc = knob_kw() ? knob_kw() : std::max<int64_t>(kWmin, std::min<int64_t>(kW, L));
   w.Cr = cdiv(Dr, w.Wc);
