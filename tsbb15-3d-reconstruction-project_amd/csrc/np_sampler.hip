@@ -61,8 +61,8 @@ constexpr int kPrefix = kDeg + kN - 1;       // words of a window's sequence a j
 constexpr int kJB = 1024;                    // stream blocks per generator
 constexpr int64_t kJ = int64_t(kN) * kJB;    // words per generator
 constexpr int kLevels = 16;                  // jump levels: windows up to 2^16 generators apart
-constexpr int kW = 1 << 21;                  // longest automatic parse chunk (draws)
-constexpr int kWmax = 1 << 21;               // longest chunk (RSAMD_NP_KW)
+constexpr int kW = 1 << 24;                  // longest automatic parse chunk (draws)
+constexpr int kWmax = 1 << 24;               // longest chunk (RSAMD_NP_KW)
 constexpr int kWmin = 8192;                  // shortest parse chunk
 constexpr int kEntryThreads = 512;
 constexpr int kR = 20;                       // slots per thread: N - 1 <= 10240
@@ -1010,53 +1010,57 @@ constexpr int kTupWaves = RSAMD_TUP_WAVES;  // waves (hypotheses) per tuple work
 // / 744 / 906 / 1099 us (the larger rings cost occupancy)
 constexpr int kTupBlk = RSAMD_TUP_BLK;
 constexpr int kTupRing = 2 * kTupBlk;       // words staged per wave
+// u16 entries per wave after the ring: the swap partners J[s - 1] of the states s = 1..n1
+__host__ __device__ constexpr int tup_table(int n1) { return (n1 + 1) & ~1; }
+__host__ __device__ constexpr int64_t tup_lds_bytes(int n1) {
+  return (static_cast<int64_t>(sizeof(uint32_t)) * kTupRing +
+          static_cast<int64_t>(sizeof(uint16_t)) * tup_table(n1)) * kTupWaves;
+}
+// ring blocks held in registers ahead of the one being parsed: the stream comes from HBM (far
+// larger than the caches), and at large N the LDS table leaves one wave per SIMD, so one block
+// ahead (two 64-draw windows) waited a full HBM round trip per block
+#ifndef RSAMD_TUP_AHEAD
+#define RSAMD_TUP_AHEAD 6
+#endif
+constexpr int kTupAhead = RSAMD_TUP_AHEAD;
+
 template <bool PY>
 __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
     const uint32_t *__restrict__ draws, const int64_t *__restrict__ starts,
-    const int64_t *__restrict__ got, int64_t lo, int64_t hi, int n1, int n1p, int kk,
+    const int64_t *__restrict__ got, int64_t lo, int64_t hi, int n1, int kk,
     int32_t *__restrict__ out, int *err, int64_t nwords) {
-  // per wave: a ring of kTupRing words of the hypothesis (blocks of kTupBlk words loaded one
-  // block ahead, so the window reads wait on LDS, not on HBM: the stream is far larger than
-  // the caches), then the swap partners J (uint16 x n1p)
+  // per wave: a ring of kTupRing words of the hypothesis (blocks of kTupBlk words, kTupAhead
+  // blocks in flight in registers), then the swap partners J (uint16 x tup_table(n1))
   extern __shared__ uint32_t tup_lds[];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
   // hypotheses [lo, hi) of the segment (those the caller asked for), out row h - lo
   const int64_t h = lo + static_cast<int64_t>(blockIdx.x) * kTupWaves + wv;
   if (h >= hi || h >= *got) return;  // wave-uniform; the kernel has no workgroup barrier
-  uint32_t *ring = tup_lds + static_cast<size_t>(wv) * (kTupRing + n1p / 2);
+  uint32_t *ring = tup_lds + static_cast<size_t>(wv) * (kTupRing + tup_table(n1) / 2);
   uint16_t *J = reinterpret_cast<uint16_t *>(ring + kTupRing);
   const int64_t a = starts[h], b = starts[h + 1];
   const uint32_t *__restrict__ src = draws + a;
-  // read-ahead never leaves the stream allocation (nwords words from draws[0])
+  // read-ahead never leaves the stream allocation (nwords words from draws[0]), nor the
+  // hypothesis by more than the queue
   const int64_t lim = nwords - 1 - a;
   auto ld = [&](int64_t x) { return src[x < lim ? x : lim]; };
   constexpr int kPerLane = kTupBlk / 64;
-  uint32_t nb[kPerLane];
+  uint32_t nb[kTupAhead][kPerLane];  // blocks 1 .. kTupAhead after the ring's newest
 #pragma unroll
-  for (int k = 0; k < kPerLane; ++k) nb[k] = ld(64 * k + l);
+  for (int k = 0; k < kPerLane; ++k) ring[64 * k + l] = ld(64 * k + l);
 #pragma unroll
-  for (int k = 0; k < kPerLane; ++k) ring[64 * k + l] = nb[k];
+  for (int q = 0; q < kTupAhead; ++q)
 #pragma unroll
-  for (int k = 0; k < kPerLane; ++k) nb[k] = ld(kTupBlk + 64 * k + l);
-  int filled = kTupBlk;  // words of the hypothesis in the ring (relative to a); one block in flight
+    for (int k = 0; k < kPerLane; ++k) nb[q][k] = ld((q + 1) * kTupBlk + 64 * k + l);
+  int filled = kTupBlk;  // words of the hypothesis in the ring (relative to a)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const uint64_t below = (1ull << l) - 1ull;
   uint32_t i = static_cast<uint32_t>(n1);
   int o = 0;  // words parsed
-  while (i > 0) {
-    if (o + 64 > filled) {  // the block in flight lands in the ring; the next one is issued
-#pragma unroll
-      for (int k = 0; k < kPerLane; ++k) ring[(filled + 64 * k + l) & (kTupRing - 1)] = nb[k];
-#pragma unroll
-      for (int k = 0; k < kPerLane; ++k) nb[k] = ld(filled + kTupBlk + 64 * k + l);
-      filled += kTupBlk;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    // states i .. i - L + 1 share the draw rule's mask / shift
+  // one 64-draw window (states i .. i - W + 1 share the draw rule's mask / shift)
+  auto window = [&]() {
     uint32_t L, msk = 0, sh = 0;
     if constexpr (PY) {
       sh = static_cast<uint32_t>(__builtin_clz(i + 1u));
@@ -1083,6 +1087,25 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
       J[i - static_cast<uint32_t>(__popcll(acc & below)) - 1u] = static_cast<uint16_t>(u);
     i -= static_cast<uint32_t>(__popcll(acc));
     o += W;
+  };
+  // The register queue rotates by unrolling (slot q is refilled in turn), never by moving a
+  // register: a move of a load's destination would wait for that load.
+  while (i > 0) {
+#pragma unroll
+    for (int q = 0; q < kTupAhead; ++q) {
+      while (i > 0 && o + 64 <= filled) window();
+      if (i > 0) {  // the oldest block in flight lands in the ring; its slot loads the next
+#pragma unroll
+        for (int k = 0; k < kPerLane; ++k) ring[(filled + 64 * k + l) & (kTupRing - 1)] = nb[q][k];
+#pragma unroll
+        for (int k = 0; k < kPerLane; ++k)
+          nb[q][k] = ld(filled + kTupAhead * kTupBlk + 64 * k + l);
+        filled += kTupBlk;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+    }
   }
   const int64_t d = a + o;
   if (d != b) {
@@ -1092,6 +1115,10 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // Trace positions 0..7 through the swaps in the order the shuffle's effect unwinds: states
+  // 1..7 by the full transposition rule, then for s >= 8 ascending a position p < s moves to s
+  // exactly when J[s - 1] == p.  64 states per step; one ballot per step tests all eight
+  // positions at once (a hit is rare once s is large), and only a hit is resolved per position.
   uint32_t p[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) p[k] = static_cast<uint32_t>(k);
@@ -1104,6 +1131,10 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
   for (int s0 = 8; s0 <= n1; s0 += 64) {
     const int s = s0 + l;
     const uint32_t jv = s <= n1 ? static_cast<uint32_t>(J[s - 1]) : 0xffffffffu;
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) any |= jv == p[k];
+    if (!__ballot(any)) continue;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       uint64_t bb = __ballot(jv == p[k]);
@@ -1215,7 +1246,11 @@ double expected_draws(int64_t n1, bool py) {
 // depends on the transport.  World 1 gives the np_choice_device result, bit for bit.
 namespace {
 
-constexpr int64_t kShardSegWords = int64_t(1) << 31;  // own words per rank and segment (8 GiB)
+// own words per rank and segment (32 GiB, allocated by need).  C5 (N = 10 000, 1e6 hypotheses,
+// 1.44e10 draws), measured per run: 2^31-word segments of 2^21-draw chunks 918 ms, 2^22 675,
+// 2^23 612; 2^33-word segments of 2^23-draw chunks 442, of 2^24 368 (fewer chunks: the dense
+// all-entry phase costs ~N per chunk; fewer segments: fewer rounds that drain)
+constexpr int64_t kShardSegWords = int64_t(1) << 33;
 
 // test / tuning knobs, read once per process: RSAMD_NP_SEGWORDS caps a rank's words per
 // segment (tests of the multi-segment path), RSAMD_NP_KW fixes the chunk length (kWmin ..
@@ -1227,7 +1262,7 @@ int64_t env_i64(const char *name) {
 int64_t seg_words() {
   static const int64_t v = [] {
     const int64_t x = env_i64("RSAMD_NP_SEGWORDS");
-    return x > 0 ? std::max<int64_t>(int64_t(1) << 16, std::min(x, kShardSegWords)) : kShardSegWords;
+    return x > 0 ? std::max<int64_t>(int64_t(1) << 16, std::min(x, int64_t(1) << 34)) : kShardSegWords;
   }();
   return v;
 }
@@ -1332,8 +1367,7 @@ int shard_kernel_attrs(int n1) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
     entry_lds = lds;
   }
-  const int64_t tl = (static_cast<int64_t>(sizeof(uint32_t)) * kTupRing +
-                      static_cast<int64_t>(sizeof(uint16_t)) * ((n1 + 1) & ~1)) * kTupWaves;
+  const int64_t tl = tup_lds_bytes(n1);
   if (tl > tup_lds) {
     HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_np_tuples_wave<false>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(tl)));
@@ -1513,13 +1547,11 @@ int shard_enqueue_starts(rs_np_shard &w, int64_t cap, int64_t *got) {
 // 4: the tuples of hypotheses [lo, hi) (rank-local start indices; waves at or beyond *got exit)
 void shard_launch_tuples(rs_np_shard &w, int64_t lo, int64_t hi, const int64_t *got,
                          int32_t *d_out) {
-  const int n1p = (w.n1 + 1) & ~1;
-  const int64_t tl = (static_cast<int64_t>(sizeof(uint32_t)) * kTupRing +
-                      static_cast<int64_t>(sizeof(uint16_t)) * n1p) * kTupWaves;
   (w.py ? k_np_tuples_wave<true> : k_np_tuples_wave<false>)<<<static_cast<unsigned>(cdiv(hi - lo, kTupWaves)),
-                                                               64 * kTupWaves, static_cast<size_t>(tl),
+                                                               64 * kTupWaves,
+                                                               static_cast<size_t>(tup_lds_bytes(w.n1)),
                                                                w.ctx->stream>>>(
-      w.d_stream + (w.s_lo - w.wbase), w.d_starts, got, lo, hi, w.n1, n1p, w.k, d_out, w.d_err,
+      w.d_stream + (w.s_lo - w.wbase), w.d_starts, got, lo, hi, w.n1, w.k, d_out, w.d_err,
       w.nwords);
 }
 
