@@ -258,19 +258,36 @@ int rs_pnp_ransac(rs_ctx *ctx, const double *X_med, const double *y_med, int64_t
                   double thresh, rs_pnp_result *out, int64_t *inl_med, int64_t *n_inl_med,
                   int64_t *inl_high, int64_t *n_inl_high);
 
+/* Minimal solvers of the OpenCV drop-ins: RS_PNP_DLT6 the reference's DLT (pnp.py:132-160) on
+ * 6-point samples, RS_PNP_EPNP5 EPnP on 5-point samples (OpenCV's solvePnPRansac kernel),
+ * RS_PNP_P3P Lambda-Twist P3P on 4-point samples (3 solve, the 4th chooses; OpenCV's kernel
+ * for 4 correspondences and for SOLVEPNP_P3P; the reference's unfinished p3p_twist,
+ * pnp.py:61-121). */
+#define RS_PNP_DLT6 0
+#define RS_PNP_EPNP5 1
+#define RS_PNP_P3P 2
+
+/* EPnP over all m >= 4 correspondences (method RS_PNP_EPNP5) or P3P over exactly 4
+ * (RS_PNP_P3P): X (m,3), y (m,3) C-normalised homogeneous image points; R_out (3,3), t_out
+ * (3), err_out = mean reprojection error in normalised units (inf: no pose).  cv.solvePnP
+ * with SOLVEPNP_EPNP / SOLVEPNP_P3P (pnp.py:7-10 calls cv.solvePnP). */
+int rs_pnp_minimal(rs_ctx *ctx, const double *X, const double *y, int64_t m, int32_t method,
+                   double *R_out, double *t_out, double *err_out);
+
 /* cv.solvePnPRansac drop-in (tables.py:141-145 call site): world points X (m,3), PIXEL
  * image points uv (m,2), camera matrix K (3,3 row-major, upper triangular), zero distortion.
- * Up to max_iters hypotheses (Philox 6-point samples from `seed`, DLT minimal solver on the
- * sample's centred, RMS-scaled world points -- Hartley conditioning) are
- * solved and counted on the GPU with OpenCV's pixel test |K pi(R x + t) - uv|^2 <=
- * reproj_err^2; OpenCV's sequential loop (a model wins with goodCount > max(best,
- * model_points - 1), then RANSACUpdateNumIters(confidence, outlier ratio, model_points,
- * niters) shrinks the budget) is replayed over that hypothesis order.  out->best_index = -1
- * when nothing wins; *iters_used = hypotheses the loop consumed; inliers (<= m) in point
- * order.  m >= 6 (the DLT), unlike OpenCV's EPnP kernel (m >= 4). */
+ * Up to max_iters hypotheses (Philox samples from `seed` of the method's minimal size: EPnP
+ * on 5 points as OpenCV's kernel, P3P on 4, or the DLT on 6 with the sample's world points
+ * centred and RMS-scaled) are solved and counted on the GPU with OpenCV's pixel test
+ * |K pi(R x + t) - uv|^2 <= reproj_err^2; OpenCV's sequential loop (a model wins with
+ * goodCount > max(best, model_points - 1), then RANSACUpdateNumIters(confidence, outlier
+ * ratio, model_points, niters) shrinks the budget) is replayed over that hypothesis order.
+ * guess (R row-major then t, 12 doubles, or null): scored first, as hypothesis 0 (the
+ * extrinsic guess of useExtrinsicGuess).  out->best_index = -1 when nothing wins;
+ * *iters_used = hypotheses the loop consumed; inliers (<= m) in point order. */
 int rs_pnp_ransac_cv(rs_ctx *ctx, const double *X, const double *uv, int64_t m, const double *K,
                      int64_t max_iters, uint64_t seed, double reproj_err, double confidence,
-                     int32_t model_points, rs_pnp_result *out, int64_t *inliers,
+                     int32_t method, const double *guess, rs_pnp_result *out, int64_t *inliers,
                      int64_t *n_inliers, int64_t *iters_used);
 
 /* ------------------------------------------------------------------------------------------

@@ -148,7 +148,10 @@ def test_solvepnpransac_pixel_threshold_through_K(ctx):
     rr = cv.last_ransac
     e = np.linalg.norm(cv.project_points(X, cv.Rodrigues(rr["R"])[0], rr["t"], K) - uv, axis=1)
     np.testing.assert_array_equal(inl, np.flatnonzero(e <= 8.0))
-    np.testing.assert_array_equal(inl, np.arange(110))
+    # the winner holds at least the true pose's 110 (a 5-point EPnP pose fitted through some
+    # of the 7 px points may trade a few of those for 9 px ones and count more), every exact
+    # point and no gross outlier
+    assert len(inl) >= 110 and set(range(100)) <= set(inl) and inl.max() < 120, inl
     # LM refinement on the consensus set: no worse than the RANSAC pose, near the truth
     R, _ = cv.Rodrigues(rvec)
     e2 = np.linalg.norm(cv.project_points(X[inl], rvec, tvec[:, 0], K) - uv[inl], axis=1)
@@ -170,10 +173,11 @@ def test_solvepnpransac_adaptive_iterations_and_determinism(ctx):
         used.append(cv.last_ransac["iterations"])
         best.append((cv.last_ransac["best_index"], len(inl)))
     assert used == sorted(used) and used[-1] < 1000, used
-    # OpenCV's budget at the winner's outlier ratio (m = 6): log(1 - p) / log(1 - (1 - ep)^6);
-    # the loop stops at that budget, or right after the winner when it came later
+    # OpenCV's budget at the winner's outlier ratio (EPnP kernel, m = 5):
+    # log(1 - p) / log(1 - (1 - ep)^5); the loop stops at that budget, or right after the
+    # winner when it came later
     ep = 1 - best[1][1] / 140
-    bound = int(np.ceil(np.log(0.01) / np.log(1 - (1 - ep) ** 6))) + 1
+    bound = int(np.ceil(np.log(0.01) / np.log(1 - (1 - ep) ** 5))) + 1
     assert used[1] <= max(bound, best[1][0] + 1), (used, best, bound)
     # equal inputs, equal outputs, whatever ran in between
     a = cv.solvePnPRansac(X, uv, K, None)
@@ -185,7 +189,10 @@ def test_solvepnpransac_adaptive_iterations_and_determinism(ctx):
 
 def test_solvepnpransac_rejects_bad_input(ctx):
     X, uv, K, _, _ = _aniso_scene()
-    assert cv.solvePnPRansac(X[:5], uv[:5], K, None) == (False, None, None, None)
+    with pytest.raises(ValueError, match="at least 4"):
+        cv.solvePnPRansac(X[:3], uv[:3], K, None)
+    with pytest.raises(ValueError, match="flags"):
+        cv.solvePnPRansac(X, uv, K, None, flags=7)     # e.g. SOLVEPNP_SQPNP: not provided
     with pytest.raises(ValueError):
         cv.solvePnPRansac(X, uv, K, np.array([0.1, 0, 0, 0]))
     Kb = K.copy()
@@ -234,4 +241,83 @@ def test_p3p_solvepnp_iterative(ctx):
     ok, rv2, tv2 = cv.solvePnP(X, uvn, K, None, rv, tv, useExtrinsicGuess=True)
     assert ok and np.allclose(rv2, rv, atol=1e-6) and np.allclose(tv2, tv, atol=1e-6)
     with pytest.raises(ValueError):
-        cv.solvePnP(X[:5], uvn[:5], K, None)
+        cv.solvePnP(X[:3], uvn[:3], K, None)
+
+
+def test_minimal_pnp_known_answers_badino2(ctx):
+    """The OpenCV kernels on noise-free BAdino2 views (poses from the reference's
+    camera_resectioning): EPnP on 5 points and on all of a view's points, P3P on 4 (three
+    solve, the fourth chooses), through cv.solvePnP(flags) and through cv.solvePnPRansac's
+    direct path (as many correspondences as the kernel's sample: every point an inlier)."""
+    z = golden("dino_pnp_kat.npz")
+    K0 = None
+    for v in (1, 7, 20, 33):
+        X, uv, _ = _view(z, v)
+        K = z["K"][v]
+        rs = np.random.RandomState(v)
+        for trial in range(3):
+            s = rs.choice(len(X), 5, replace=False)
+            ok, rv, tv = cv.solvePnP(X[s], uv[s], K, None, flags=cv.SOLVEPNP_EPNP)
+            assert ok
+            np.testing.assert_allclose(cv.Rodrigues(rv)[0], z["R"][v], atol=1e-6)
+            np.testing.assert_allclose(tv[:, 0], z["t"][v], rtol=1e-6, atol=1e-6)
+            ok, rv, tv, inl = cv.solvePnPRansac(X[s], uv[s], K, None)
+            assert ok and np.array_equal(inl[:, 0], np.arange(5))
+            np.testing.assert_allclose(cv.Rodrigues(rv)[0], z["R"][v], atol=1e-6)
+            s4 = s[:4]
+            for call in (lambda: cv.solvePnP(X[s4], uv[s4], K, None, flags=cv.SOLVEPNP_P3P),
+                         lambda: cv.solvePnPRansac(X[s4], uv[s4], K, None)[:3]):
+                ok, rv, tv = call()
+                assert ok
+                np.testing.assert_allclose(cv.Rodrigues(rv)[0], z["R"][v], atol=1e-6)
+                np.testing.assert_allclose(tv[:, 0], z["t"][v], rtol=1e-6, atol=1e-6)
+        ok, rv, tv = cv.solvePnP(X, uv, K, None, flags=cv.SOLVEPNP_EPNP)
+        np.testing.assert_allclose(cv.Rodrigues(rv)[0], z["R"][v], atol=1e-8)
+        K0 = K
+    with pytest.raises(ValueError):
+        cv.solvePnP(X[:5], uv[:5], K0, None, flags=cv.SOLVEPNP_P3P)   # P3P takes exactly 4
+
+
+def test_solvepnpransac_kernels_and_guess(ctx):
+    """RANSAC with the EPnP (5-point) and P3P (4-point, flags=SOLVEPNP_P3P) kernels on the
+    anisotropic scene: each keeps every exact point and no gross outlier; the extrinsic guess (useExtrinsicGuess) is
+    scored first, so a correct guess wins at hypothesis 0."""
+    X, uv, K, Rt, tt = _aniso_scene()
+    for flags in (cv.SOLVEPNP_ITERATIVE, cv.SOLVEPNP_EPNP, cv.SOLVEPNP_P3P):
+        ok, rv, tv, inl = cv.solvePnPRansac(X, uv, K, None, iterationsCount=2000,
+                                            confidence=0.999999, flags=flags)
+        inl = inl[:, 0]
+        assert ok and len(inl) >= 110 and set(range(100)) <= set(inl) and inl.max() < 120, flags
+        np.testing.assert_allclose(cv.Rodrigues(rv)[0], Rt, atol=5e-3)
+    # exact points and gross outliers only: the true pose's 100 is the maximum consensus, and a
+    # later hypothesis needs strictly more to replace hypothesis 0
+    sel = np.r_[0:100, 120:140]
+    rg, _ = cv.Rodrigues(Rt)
+    ok, rv, tv, inl = cv.solvePnPRansac(X[sel], uv[sel], K, None, rg, tt.reshape(3, 1),
+                                        useExtrinsicGuess=True, iterationsCount=50)
+    assert ok and cv.last_ransac["best_index"] == 0
+    assert np.array_equal(inl[:, 0], np.arange(100))
+    # a wrong guess is just one more hypothesis
+    ok, rv, tv, inl = cv.solvePnPRansac(X[sel], uv[sel], K, None, -rg, tt.reshape(3, 1) + 1.0,
+                                        useExtrinsicGuess=True, iterationsCount=200)
+    assert ok and cv.last_ransac["best_index"] > 0 and np.array_equal(inl[:, 0], np.arange(100))
+
+
+def test_c3_full_size_exact_stream_equals_oracle_fixture(ctx):
+    """C3 at full size (500 points, 50 000 trials) on random.seed(0)'s CPython stream: the
+    winner, its consensus count, both consensus sets, R, t and the advanced stream state equal
+    tests/golden/full_c3.npz (the oracle restatement of the intended ransac.py:37-113,
+    make_golden_c3.py; the reference's own loop raises at ransac.py:77, so this is the pinned
+    oracle, not a run of the reference)."""
+    z = golden("full_c3.npz")
+    rng = random.Random(0)
+    R, t, im, ih, best, cnt = ransac.ransac_pnp(z["X"], z["y"], z["X"], z["y"], int(z["r"]),
+                                                float(z["thresh"]), 6, rng=rng)
+    assert best == int(z["best"])
+    assert cnt == int(z["counts"].max()) == len(z["inl_med"])
+    assert np.array_equal(im, z["inl_med"]) and np.array_equal(ih, z["inl_high"])
+    np.testing.assert_allclose(R, z["R"], atol=1e-6)
+    np.testing.assert_allclose(t, z["t"], rtol=1e-6, atol=1e-6)
+    st = rng.getstate()
+    assert int(st[1][624]) == int(z["py_pos_out"])
+    assert np.array_equal(np.array(st[1][:624], np.uint32), z["py_key_out"])

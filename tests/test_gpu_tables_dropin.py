@@ -118,8 +118,24 @@ def test_add_new_view_too_few_matches_raises(ctx):
     T = tables_after_ba(z, "clean")
     n_views = T.T_views.size
     found = _found(g)
-    keep = np.sort(np.r_[np.flatnonzero(found)[:5], np.flatnonzero(~found)])
-    with pytest.raises(ValueError, match=r"\b5 putative correspondences matched"):
+    keep = np.sort(np.r_[np.flatnonzero(found)[:3], np.flatnonzero(~found)])
+    with pytest.raises(ValueError, match=r"\b3 putative correspondences matched"):
         gt.add_new_view(T, g("K"), 2, g("match_queries")[keep], g("match_y2_hom")[keep],
                         g("match_y1")[keep], g("match_y2")[keep])
     assert T.T_views.size == n_views
+
+
+@pytest.mark.parametrize("n", [4, 5])
+def test_add_new_view_registers_with_4_or_5_matches(ctx, n):
+    """Views with only 4 or 5 matched 2D<->3D correspondences register, as OpenCV's kernels
+    (P3P / EPnP) allow: the pose from exactly those points, every one an inlier."""
+    z = golden("tables.npz")
+    g = lambda k: z["clean_" + k]
+    T = tables_after_ba(z, "clean")
+    n_views, n_obs0 = T.T_views.size, T.T_obs.size
+    found = _found(g)
+    keep = np.sort(np.r_[np.flatnonzero(found)[:n], np.flatnonzero(~found)])
+    gt.add_new_view(T, g("K"), 2, g("match_queries")[keep], g("match_y2_hom")[keep],
+                    g("match_y1")[keep], g("match_y2")[keep])
+    assert T.T_views.size == n_views + 1 and T.T_obs.size == n_obs0 + n
+    assert np.abs(T.T_views[2].camera_pose.R - g("pnp_R")).max() < 0.05

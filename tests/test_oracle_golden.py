@@ -112,3 +112,13 @@ def test_ransac_helpers_match_reference():
 def test_essential_golden_consistent():
     z = golden("dino_pnp_kat.npz")
     np.testing.assert_allclose(z["R01"], z["clean_data_eval"][1], atol=1e-12)
+
+
+def test_full_c3_fixture_prefix_replays():
+    """full_c3.npz (make_golden_c3.py) replays: the first 1 500 trials of the oracle loop on
+    random.seed(0) give the fixture's per-trial consensus sizes."""
+    import random
+    z = golden("full_c3.npz")
+    *_, counts = pnp_ref.ransac_pnp(z["y"], z["X"], z["y"], z["X"], 1500, float(z["thresh"]), 6,
+                                    rng=random.Random(0), trace=True)
+    assert np.array_equal(counts, z["counts"][:1500].astype(np.int64))

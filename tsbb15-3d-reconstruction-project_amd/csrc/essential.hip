@@ -259,9 +259,11 @@ __device__ __forceinline__ double horner_asc(const double (&p)[N], double z) {
   return v;
 }
 
-// All real solutions of one sample; returns their number (<= 10), E row-major, unit norm.
-__device__ int e5_solve_one(const double (&y1)[5][2], const double (&y2)[5][2],
-                            double (&Es)[kE5Sol][9]) {
+// All real solutions of one sample, each handed to emit(slot, E) as it is found (E row-major,
+// unit norm; no array of solutions is kept, so the 10 x 20 system and the null basis fit the
+// register file); returns their number (<= 10).
+template <class Emit>
+__device__ int e5_solve_one(const double (&y1)[5][2], const double (&y2)[5][2], Emit emit) {
   double Q[5][9];
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
@@ -357,7 +359,8 @@ __device__ int e5_solve_one(const double (&y1)[5][2], const double (&y2)[5][2],
     if (!(nn > 0.0) || !isfinite(nn)) continue;
     const double in = 1.0 / sqrt(nn);
 #pragma unroll
-    for (int e = 0; e < 9; ++e) Es[ns][e] = E[e] * in;
+    for (int e = 0; e < 9; ++e) E[e] *= in;
+    emit(ns, E);
     ++ns;
   }
   return ns;
@@ -399,15 +402,9 @@ __global__ __launch_bounds__(64) void k_e5_solve(E5Args a) {
     norm_pt(a.Kin1, p.x1, p.y1, y1[i][0], y1[i][1]);
     norm_pt(a.Kin2, p.x2, p.y2, y2[i][0], y2[i][1]);
   }
-  double Es[kE5Sol][9];
-  const int ns = e5_solve_one(y1, y2, Es);
-  if (a.nsol) a.nsol[s] = ns;
-  const double qn = __builtin_nan("");
-  for (int j = 0; j < kE5Sol; ++j) {
+  // one solution slot: E, and F = M1 E M2 (K1^-T E K2^-1) when asked for
+  auto store = [&](int j, const double (&E)[9]) {
     const int64_t slot = static_cast<int64_t>(s) * kE5Sol + j;
-    double E[9];
-#pragma unroll
-    for (int e = 0; e < 9; ++e) E[e] = j < ns ? Es[j][e] : qn;
 #pragma unroll
     for (int e = 0; e < 9; ++e) a.Esoa[e * a.ld + slot] = E[e];
     if (a.Fsoa) {
@@ -424,7 +421,13 @@ __global__ __launch_bounds__(64) void k_e5_solve(E5Args a) {
           a.Fsoa[(3 * r + c) * a.ld + slot] =
               fma(a.M1[3 * r], T[c], fma(a.M1[3 * r + 1], T[3 + c], a.M1[3 * r + 2] * T[6 + c]));
     }
-  }
+  };
+  const int ns = e5_solve_one(y1, y2, store);
+  if (a.nsol) a.nsol[s] = ns;
+  // NaN past the sample's solutions: those slots count 0
+  const double qn = __builtin_nan("");
+  const double Enan[9] = {qn, qn, qn, qn, qn, qn, qn, qn, qn};
+  for (int j = ns; j < kE5Sol; ++j) store(j, Enan);
 }
 
 struct E5DevResult {

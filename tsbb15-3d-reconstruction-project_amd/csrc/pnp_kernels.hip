@@ -42,6 +42,12 @@ struct PxMetric {
   double a, b, c;
 };
 
+}  // namespace rsd
+
+#include "pnp_minimal.h"
+
+namespace rsd {
+
 constexpr int ridx(int j, int l) { return j * 12 - (j * (j - 1)) / 2 + (l - j); }
 
 __device__ __forceinline__ void givens_row(double (&R)[78], double (&a)[12]) {
@@ -328,6 +334,59 @@ __global__ __launch_bounds__(256) void k_pnp_solve(const PPt *__restrict__ pts, 
   for (int q = 0; q < 3; ++q) Psoa[(9 + q) * ld + h] = t[q];
 }
 
+// Minimal-sample poses for the cv.solvePnPRansac drop-in with OpenCV's RANSAC kernels: lane per
+// hypothesis, a Philox sample of K points (K = 5: EPnP; K = 4: P3P on three, the fourth
+// deciding).  Hypothesis `guess_slot` (>= 0) takes the caller's pose instead (the extrinsic
+// guess, scored in the same order).  A failed solve writes NaN, which scores 0.
+template <int K>
+__global__ __launch_bounds__(64) void k_pnp_solve_min(const PPt *__restrict__ pts, int m, int H,
+                                                      uint64_t seed, double *__restrict__ Psoa,
+                                                      int64_t ld, int guess_slot,
+                                                      const double *__restrict__ guess) {
+  const int h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= H) return;
+  double Rm[9], t[3];
+  double err = INFINITY;
+  if (h == guess_slot) {
+#pragma unroll
+    for (int q = 0; q < 9; ++q) Rm[q] = guess[q];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) t[q] = guess[9 + q];
+    err = 0.0;
+  } else {
+    int idx[K];
+    floyd_sample<K>(seed, static_cast<uint64_t>(h), m, idx);
+    auto at = [&](int q) {
+      int v = idx[0];
+#pragma unroll
+      for (int i = 1; i < K; ++i) v = q == i ? idx[i] : v;
+      return pts[v];
+    };
+    if constexpr (K == 4)
+      err = p3p_pose(at, Rm, t);
+    else
+      err = epnp_pose(at, K, Rm, t);
+  }
+  const double qn = __builtin_nan("");
+  const bool ok = err < INFINITY;
+#pragma unroll
+  for (int q = 0; q < 9; ++q) Psoa[q * ld + h] = ok ? Rm[q] : qn;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) Psoa[(9 + q) * ld + h] = ok ? t[q] : qn;
+}
+
+// EPnP over all m correspondences (method 1) or P3P on exactly four (method 2): single lane.
+__global__ __launch_bounds__(64) void k_pnp_minimal_all(const PPt *__restrict__ pts, int m,
+                                                        int method, double *__restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double Rm[9], t[3];
+  auto at = [&](int q) { return pts[q]; };
+  const double err = method == 2 ? p3p_pose(at, Rm, t) : epnp_pose(at, m, Rm, t);
+  for (int q = 0; q < 9; ++q) out[q] = err < INFINITY ? Rm[q] : __builtin_nan("");
+  for (int q = 0; q < 3; ++q) out[9 + q] = err < INFINITY ? t[q] : __builtin_nan("");
+  out[12] = err;
+}
+
 // One-point DLT over all m correspondences (rs_pnp_dlt): single lane.
 __global__ __launch_bounds__(64) void k_pnp_dlt_all(const PPt *__restrict__ pts, int m,
                                                     double *__restrict__ out) {
@@ -601,6 +660,39 @@ extern "C" int rs_pnp_dlt(rs_ctx *c, const double *X, const double *y, int64_t m
   return RS_OK;
 }
 
+extern "C" int rs_pnp_minimal(rs_ctx *c, const double *X, const double *y, int64_t m,
+                              int32_t method, double *R_out, double *t_out, double *err_out) {
+  if (!c || !X || !y || !R_out || !t_out) return fail(RS_EINVAL, "null pointer");
+  if (method != RS_PNP_EPNP5 && method != RS_PNP_P3P) return fail(RS_EINVAL, "unknown solver");
+  if (method == RS_PNP_P3P && m != 4)
+    return fail(RS_EINVAL, "P3P takes exactly 4 correspondences (3 to solve, 1 to choose)");
+  if (m < 4) return fail(RS_EINVAL, "EPnP needs m >= 4 correspondences");
+  if (m > (1 << 24)) return fail(RS_EINVAL, "too many correspondences");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t bin = align256(sizeof(double) * 3 * m), bp = align256(sizeof(rsd::PPt) * m);
+  int st = rs::ensure_scratch(c, 2 * bin + bp + 256);
+  if (st) return st;
+  char *base = static_cast<char *>(c->scratch);
+  double *dX = reinterpret_cast<double *>(base), *dy = reinterpret_cast<double *>(base + bin);
+  auto *dp = reinterpret_cast<rsd::PPt *>(base + 2 * bin);
+  double *dout = reinterpret_cast<double *>(base + 2 * bin + bp);
+  HIP_TRY(hipMemcpyAsync(dX, X, sizeof(double) * 3 * m, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(dy, y, sizeof(double) * 3 * m, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(rsd::k_pack_ppts, dim3((m + 255) / 256), dim3(256), 0, c->stream, dX, dy,
+                     static_cast<int>(m), dp);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(rsd::k_pnp_minimal_all, dim3(1), dim3(64), 0, c->stream, dp,
+                     static_cast<int>(m), static_cast<int>(method), dout);
+  HIP_TRY(hipGetLastError());
+  double out[13];
+  HIP_TRY(hipMemcpyAsync(out, dout, sizeof(out), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  std::memcpy(R_out, out, sizeof(double) * 9);
+  std::memcpy(t_out, out + 9, sizeof(double) * 3);
+  if (err_out) *err_out = out[12];
+  return RS_OK;
+}
+
 extern "C" int rs_pnp_ransac(rs_ctx *c, const double *X_med, const double *y_med, int64_t m_med,
                              const double *X_high, const double *y_high, int64_t m_high,
                              int32_t k, int64_t H, int32_t mode, uint64_t seed,
@@ -712,14 +804,17 @@ static int64_t ransac_update_num_iters(double p, double ep, int model_points, in
 
 extern "C" int rs_pnp_ransac_cv(rs_ctx *c, const double *X, const double *uv, int64_t m,
                                 const double *K, int64_t max_iters, uint64_t seed,
-                                double reproj_err, double confidence, int32_t model_points,
-                                rs_pnp_result *out, int64_t *inliers, int64_t *n_inliers,
-                                int64_t *iters_used) {
+                                double reproj_err, double confidence, int32_t method,
+                                const double *guess, rs_pnp_result *out, int64_t *inliers,
+                                int64_t *n_inliers, int64_t *iters_used) {
   if (!c || !X || !uv || !K || !out) return fail(RS_EINVAL, "null pointer");
-  if (m < 6) return fail(RS_EINVAL, "the DLT minimal solver needs m >= 6 correspondences");
+  if (method < RS_PNP_DLT6 || method > RS_PNP_P3P) return fail(RS_EINVAL, "unknown minimal solver");
+  const int model_points = method == RS_PNP_DLT6 ? 6 : (method == RS_PNP_EPNP5 ? 5 : 4);
+  if (m < model_points)
+    return fail(RS_EINVAL, method == RS_PNP_DLT6 ? "the DLT minimal solver needs m >= 6 correspondences"
+                                                : "the minimal solver needs more correspondences");
   if (m > (1 << 26) || max_iters < 1 || max_iters > (1LL << 28))
     return fail(RS_EINVAL, "bad dimensions");
-  if (model_points < 1 || model_points > 64) return fail(RS_EINVAL, "bad model_points");
   if (!(reproj_err >= 0.0) || !std::isfinite(reproj_err))
     return fail(RS_EINVAL, "reprojectionError must be finite and >= 0");
   if (K[3] != 0.0 || K[6] != 0.0 || K[7] != 0.0 || !(K[8] != 0.0))
@@ -737,11 +832,13 @@ extern "C" int rs_pnp_ransac_cv(rs_ctx *c, const double *X, const double *uv, in
     yn[3 * i + 1] = y1;
     yn[3 * i + 2] = 1.0;
   }
-  const int64_t H = max_iters, ld = (H + 63) / 64 * 64;
+  // with an extrinsic guess, hypothesis 0 is the guess and the samples follow
+  const int64_t H = max_iters + (guess ? 1 : 0), ld = (H + 63) / 64 * 64;
   const size_t b_in = align256(sizeof(double) * 3 * m), b_p = align256(sizeof(rsd::PPt) * m);
   const size_t b_P = align256(sizeof(double) * 12 * ld), b_cnt = align256(sizeof(int) * ld);
   const size_t b_res = align256(sizeof(rsd::PnpDevResult) + sizeof(int64_t) * m);
-  int st = rs::ensure_scratch(c, 2 * b_in + b_p + b_P + b_cnt + b_res);
+  const size_t b_g = align256(sizeof(double) * 12);
+  int st = rs::ensure_scratch(c, 2 * b_in + b_p + b_P + b_cnt + b_res + b_g);
   if (st) return st;
   char *p = static_cast<char *>(c->scratch);
   auto take = [&p](size_t b) {
@@ -755,7 +852,9 @@ extern "C" int rs_pnp_ransac_cv(rs_ctx *c, const double *X, const double *uv, in
   double *dP = reinterpret_cast<double *>(take(b_P));
   int *dcnt = reinterpret_cast<int *>(take(b_cnt));
   auto *dres = reinterpret_cast<rsd::PnpDevResult *>(take(b_res));
+  double *dguess = reinterpret_cast<double *>(take(b_g));
   hipStream_t s = c->stream;
+  if (guess) HIP_TRY(hipMemcpyAsync(dguess, guess, sizeof(double) * 12, hipMemcpyHostToDevice, s));
   const rsd::PxMetric mt{fx, sk, fy};
   const double thresh = reproj_err * reproj_err;
   HIP_TRY(hipMemcpyAsync(dX, X, sizeof(double) * 3 * m, hipMemcpyHostToDevice, s));
@@ -763,9 +862,24 @@ extern "C" int rs_pnp_ransac_cv(rs_ctx *c, const double *X, const double *uv, in
   hipLaunchKernelGGL(rsd::k_pack_ppts, dim3((m + 255) / 256), dim3(256), 0, s, dX, dy,
                      static_cast<int>(m), pts);
   HIP_TRY(hipMemsetAsync(dcnt, 0, sizeof(int) * H, s));
-  hipLaunchKernelGGL(rsd::k_pnp_solve, dim3((H + 255) / 256), dim3(256), 0, s, pts,
-                     static_cast<int>(m), static_cast<int>(H), 6, RS_SAMPLER_PHILOX, seed,
-                     static_cast<const int *>(nullptr), dP, ld, 1);
+  const int gslot = guess ? 0 : -1;
+  if (method == RS_PNP_DLT6) {
+    hipLaunchKernelGGL(rsd::k_pnp_solve, dim3((H + 255) / 256), dim3(256), 0, s, pts,
+                       static_cast<int>(m), static_cast<int>(H), 6, RS_SAMPLER_PHILOX, seed,
+                       static_cast<const int *>(nullptr), dP, ld, 1);
+    if (guess) {  // slot 0 (overwritten after the solve, in stream order): the guess
+      for (int q = 0; q < 12; ++q)
+        HIP_TRY(hipMemcpyAsync(dP + q * ld, dguess + q, sizeof(double), hipMemcpyDeviceToDevice, s));
+    }
+  } else if (method == RS_PNP_EPNP5) {
+    hipLaunchKernelGGL(rsd::k_pnp_solve_min<5>, dim3((H + 63) / 64), dim3(64), 0, s, pts,
+                       static_cast<int>(m), static_cast<int>(H), seed, dP, ld, gslot,
+                       static_cast<const double *>(dguess));
+  } else {
+    hipLaunchKernelGGL(rsd::k_pnp_solve_min<4>, dim3((H + 63) / 64), dim3(64), 0, s, pts,
+                       static_cast<int>(m), static_cast<int>(H), seed, dP, ld, gslot,
+                       static_cast<const double *>(dguess));
+  }
   HIP_TRY(hipGetLastError());
   const int64_t groups = (H + 63) / 64;
   int64_t nch = std::max<int64_t>(1, std::min<int64_t>((8192 + groups - 1) / groups, (m + 63) / 64));

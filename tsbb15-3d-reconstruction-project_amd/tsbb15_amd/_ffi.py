@@ -19,6 +19,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_PKG_ROOT), "include", "rsamd.h")
 
 RS_OK, RS_EINVAL, RS_EDEVICE, RS_ENODEV, RS_ECOMM, RS_ENOMEM = 0, -1, -2, -3, -4, -5
 SAMPLER_PHILOX, SAMPLER_TUPLES = 0, 1
+PNP_DLT6, PNP_EPNP5, PNP_P3P = 0, 1, 2
 MT_N = 624
 COMM_ID_BYTES = 128
 
@@ -106,8 +107,9 @@ _SIGS = {
                                 C.c_int64, C.c_int32, C.c_uint64, _i32p, C.c_double,
                                 C.POINTER(PnpResult), _i64p, _i64p, _i64p, _i64p]),
     "rs_pnp_ransac_cv": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, C.c_int64, C.c_uint64,
-                                   C.c_double, C.c_double, C.c_int32, C.POINTER(PnpResult),
+                                   C.c_double, C.c_double, C.c_int32, _dp, C.POINTER(PnpResult),
                                    _i64p, _i64p, _i64p]),
+    "rs_pnp_minimal": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, C.c_int32, _dp, _dp, _dp]),
     "rs_e5_solve": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, _i32p]),
     "rs_e5_ransac": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, _dp, C.c_int64, C.c_uint64,
                                C.c_double, C.POINTER(E5Result), _i64p, _i64p]),

@@ -1,33 +1,34 @@
-"""OpenCV-compatible entry points for the tables.py:141-145 call site.
+"""OpenCV-compatible entry points for the tables.py:141-145 call site and pnp.py:7-10.
 
 ``solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs, ...)`` returns
-``(retval, rvec (3,1), tvec (3,1), inliers (k,1) int32)`` like ``cv.solvePnPRansac`` and
-``Rodrigues(src)`` returns ``(dst, jacobian)``, so ``Tables.addNewView`` drops them in.
+``(retval, rvec (3,1), tvec (3,1), inliers (k,1) int32)`` like ``cv.solvePnPRansac``,
+``solvePnP`` returns ``(retval, rvec, tvec)`` and ``Rodrigues(src)`` returns
+``(dst, jacobian)``, so ``Tables.addNewView`` and ``pnp.p3p`` drop them in.
 
-What runs (rs_pnp_ransac_cv, pnp_kernels.hip), following OpenCV's solvePnPRansac structure:
+What runs (rs_pnp_ransac_cv, pnp_kernels.hip / pnp_minimal.h), following OpenCV's
+solvePnPRansac structure:
 
-  * up to ``iterationsCount`` 6-point hypotheses (DLT minimal solver on C-normalised points,
-    pnp.py:132-160, with the sample's world points centred and RMS-scaled first -- without
-    that conditioning the 12x12 DLT system does not survive pixel noise on compact, distant
-    point sets such as BAdino2's reconstruction) are solved and scored on the GPU with
-    OpenCV's test in PIXELS,
-    ``|K pi(R x + t) - uv|^2 <= reprojectionError^2``;
-  * OpenCV's sequential loop is replayed over that hypothesis order: a model replaces the best
+  * the minimal solver is OpenCV's RANSAC kernel: EPnP on 5-point samples, or -- for exactly
+    4 correspondences and for ``flags`` SOLVEPNP_P3P -- P3P on 4 (Lambda Twist on three, the
+    fourth choosing); up to ``iterationsCount`` hypotheses are solved and scored on the GPU
+    with OpenCV's test in PIXELS, ``|K pi(R x + t) - uv|^2 <= reprojectionError^2``;
+  * with as many correspondences as the sample size OpenCV solves once with that kernel and
+    returns every point as an inlier; so does this;
+  * OpenCV's sequential loop is replayed over the hypothesis order: a model replaces the best
     only if its inlier count exceeds ``max(best, modelPoints - 1)``, and each new best shrinks
-    the budget with RANSACUpdateNumIters(confidence, outlier ratio, modelPoints, budget), so
-    ``confidence`` stops the search early exactly as OpenCV's does (here modelPoints = 6, the
-    DLT sample size; OpenCV's EPnP kernel samples 5);
+    the budget with RANSACUpdateNumIters(confidence, outlier ratio, modelPoints, budget);
   * the sampling stream is a fixed-seed Philox stream per call, the analogue of OpenCV seeding
     its RANSAC RNG with the same constant on every call: equal inputs give equal outputs;
-  * the winning pose is refined on its consensus set by Levenberg-Marquardt on the pixel
-    reprojection error (OpenCV's SOLVEPNP_ITERATIVE refinement, started from the RANSAC pose),
-    and ``inliers`` is the RANSAC consensus set, in point order.
+  * the winner is refined on its consensus set as OpenCV does with ``flags``: Levenberg-
+    Marquardt on the pixel reprojection error for SOLVEPNP_ITERATIVE (started from the RANSAC
+    pose), EPnP over the consensus set for SOLVEPNP_EPNP, none for SOLVEPNP_P3P;
+  * ``useExtrinsicGuess`` with ``rvec``/``tvec``: the guess is scored first, as hypothesis 0
+    (OpenCV's kernels ignore it; here a good guess is kept unless a sample beats it).
 
-Limits: zero lens distortion only (tables.py:140 passes zeros); m >= 6 correspondences (the
-DLT) where OpenCV's EPnP kernel accepts m >= 4 -- fewer return ``(False, None, None, None)``
-and tables.add_new_view raises a ValueError naming the count.  OpenCV itself is absent and
-unversioned here, so parity with its exact samples is unpinned; the tests
-check the documented semantics (pixel threshold, adaptive budget, determinism).
+Limits: zero lens distortion only (tables.py:140 passes zeros); other ``flags`` raise
+ValueError.  OpenCV itself is absent and unversioned here, so parity with
+its exact samples is unpinned; the tests check known answers (BAdino2 views, including 4- and
+5-point subsets) and the documented semantics (pixel threshold, adaptive budget, determinism).
 """
 from __future__ import annotations
 
@@ -37,8 +38,8 @@ from . import _ffi
 
 # OpenCV constructs its RANSAC RNG as RNG((uint64)-1) on every call
 CV_RANSAC_SEED = 0xFFFFFFFFFFFFFFFF
-MODEL_POINTS = 6
 LM_MAX_ITERS = 20  # OpenCV's solvePnP ITERATIVE: CvLevMarq criteria (20 iterations, FLT_EPSILON)
+SOLVEPNP_ITERATIVE, SOLVEPNP_EPNP, SOLVEPNP_P3P = 0, 1, 2
 
 # the last call's RANSAC outcome before refinement: hypotheses the loop consumed, the winning
 # hypothesis and its pose (diagnostics / tests)
@@ -97,9 +98,7 @@ def _refine_lm(X, uv, K, rvec, tvec):
     return sol.x[:3].reshape(3, 1), sol.x[3:].reshape(3, 1)
 
 
-def solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec=None, tvec=None,
-                   useExtrinsicGuess=False, iterationsCount=100, reprojectionError=8.0,
-                   confidence=0.99, inliers=None, flags=0, ctx=None):
+def _inputs(objectPoints, imagePoints, cameraMatrix, distCoeffs):
     X = np.ascontiguousarray(np.asarray(objectPoints, dtype=np.float64).reshape(-1, 3))
     uv = np.ascontiguousarray(np.asarray(imagePoints, dtype=np.float64).reshape(-1, 2))
     if len(X) != len(uv):
@@ -107,73 +106,150 @@ def solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec=Non
     if distCoeffs is not None and np.any(np.asarray(distCoeffs) != 0):
         raise ValueError("only zero lens distortion is supported")
     K = np.ascontiguousarray(np.asarray(cameraMatrix, dtype=np.float64).reshape(3, 3))
+    return X, uv, K
+
+
+def _check_flags(flags):
+    if flags not in (SOLVEPNP_ITERATIVE, SOLVEPNP_EPNP, SOLVEPNP_P3P):
+        raise ValueError(f"flags={flags}: only SOLVEPNP_ITERATIVE, SOLVEPNP_EPNP and "
+                         "SOLVEPNP_P3P are provided")
+
+
+def _normalised(uv, K):
+    y = np.linalg.solve(K, np.vstack([uv.T, np.ones((1, len(uv)))])).T
+    return np.ascontiguousarray(y)
+
+
+def _guess_pose(useExtrinsicGuess, rvec, tvec):
+    if not useExtrinsicGuess or rvec is None or tvec is None:
+        return None
+    R, _ = Rodrigues(np.asarray(rvec, dtype=np.float64).reshape(3))
+    return np.ascontiguousarray(np.concatenate([R.ravel(), np.asarray(tvec, np.float64).reshape(3)]))
+
+
+def minimal_pose(X, uv, K, method, ctx=None):
+    """EPnP over all correspondences (method PNP_EPNP5, m >= 4) or P3P over exactly four
+    (PNP_P3P) on the GPU (rs_pnp_minimal); returns (R, t) or None."""
+    y = _normalised(uv, K)
+    R, t, err = np.empty(9), np.empty(3), _ffi.C.c_double(0.0)
+    _ffi.check(_ffi.lib().rs_pnp_minimal((ctx or _ffi.default_context()).handle,
+                                         _ffi.ptr(X, _ffi.C.c_double), _ffi.ptr(y, _ffi.C.c_double),
+                                         len(X), int(method), _ffi.ptr(R, _ffi.C.c_double),
+                                         _ffi.ptr(t, _ffi.C.c_double), _ffi.C.byref(err)))
+    if not np.isfinite(err.value):
+        return None
+    return R.reshape(3, 3), t
+
+
+def solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec=None, tvec=None,
+                   useExtrinsicGuess=False, iterationsCount=100, reprojectionError=8.0,
+                   confidence=0.99, inliers=None, flags=SOLVEPNP_ITERATIVE, ctx=None):
+    _check_flags(flags)
+    X, uv, K = _inputs(objectPoints, imagePoints, cameraMatrix, distCoeffs)
     last_ransac.clear()
-    if len(X) < MODEL_POINTS:
-        return False, None, None, None
+    if len(X) < 4:
+        raise ValueError(f"solvePnPRansac needs at least 4 correspondences, got {len(X)} "
+                         "(OpenCV asserts npoints >= 4)")
     ctx = ctx or _ffi.default_context()
+    # OpenCV's kernel choice: P3P for its flag or for exactly four points, else EPnP on five
+    method = _ffi.PNP_P3P if (flags == SOLVEPNP_P3P or len(X) == 4) else _ffi.PNP_EPNP5
+    model_points = 4 if method == _ffi.PNP_P3P else 5
+    if len(X) == model_points:  # one solve with the kernel, every point an inlier
+        pose = minimal_pose(X, uv, K, method, ctx)
+        if pose is None:
+            return False, None, None, None
+        rv, _ = Rodrigues(pose[0])
+        last_ransac.update(iterations=1, best_index=0, R=pose[0], t=pose[1])
+        return (True, rv.reshape(3, 1), pose[1].reshape(3, 1),
+                np.arange(len(X), dtype=np.int32).reshape(-1, 1))
+    guess = _guess_pose(useExtrinsicGuess, rvec, tvec)
     res = _ffi.PnpResult()
     inl = np.empty(len(X), np.int64)
     n_inl, used = _ffi.C.c_int64(0), _ffi.C.c_int64(0)
     _ffi.check(_ffi.lib().rs_pnp_ransac_cv(
         ctx.handle, _ffi.ptr(X, _ffi.C.c_double), _ffi.ptr(uv, _ffi.C.c_double), len(X),
         _ffi.ptr(K, _ffi.C.c_double), int(iterationsCount), CV_RANSAC_SEED,
-        float(reprojectionError), float(confidence), MODEL_POINTS, _ffi.C.byref(res),
+        float(reprojectionError), float(confidence), int(method),
+        None if guess is None else _ffi.ptr(guess, _ffi.C.c_double), _ffi.C.byref(res),
         _ffi.ptr(inl, _ffi.C.c_int64), _ffi.C.byref(n_inl), _ffi.C.byref(used)))
     last_ransac.update(iterations=int(used.value), best_index=int(res.best_index))
     if res.best_index < 0:
         return False, None, None, None
     inl = inl[:n_inl.value]
-    last_ransac.update(R=np.array(res.R[:]).reshape(3, 3), t=np.array(res.t[:]))
-    rv, _ = Rodrigues(last_ransac["R"])
-    rv, tv = _refine_lm(X[inl], uv[inl], K, rv, np.array(res.t[:]))
-    return True, rv.reshape(3, 1), tv.reshape(3, 1), inl.astype(np.int32).reshape(-1, 1)
-
-
-SOLVEPNP_ITERATIVE = 0
+    R, t = np.array(res.R[:]).reshape(3, 3), np.array(res.t[:])
+    last_ransac.update(R=R, t=t)
+    rv, _ = Rodrigues(R)
+    if flags == SOLVEPNP_ITERATIVE:
+        rv, tv = _refine_lm(X[inl], uv[inl], K, rv, t)
+    elif flags == SOLVEPNP_EPNP and len(inl) >= 4:
+        pose = minimal_pose(np.ascontiguousarray(X[inl]), np.ascontiguousarray(uv[inl]), K,
+                            _ffi.PNP_EPNP5, ctx)
+        tv = t
+        if pose is not None:
+            rv, _ = Rodrigues(pose[0])
+            tv = pose[1]
+    else:
+        tv = t
+    return True, np.asarray(rv).reshape(3, 1), np.asarray(tv).reshape(3, 1), \
+        inl.astype(np.int32).reshape(-1, 1)
 
 
 def solvePnP(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec=None, tvec=None,
              useExtrinsicGuess=False, flags=SOLVEPNP_ITERATIVE, ctx=None):
-    """``cv.solvePnP`` with OpenCV's SOLVEPNP_ITERATIVE semantics, the call behind the
-    reference's ``pnp.p3p`` (pnp.py:7-10): the pose over ALL correspondences, initialised by the
-    DLT (rs_pnp_dlt on the GPU; world points centred and RMS-scaled first, the conditioning
-    OpenCV's DLT initialisation applies too) -- or by (rvec, tvec) when ``useExtrinsicGuess`` --
-    then refined by Levenberg-Marquardt on the pixel reprojection error.  Returns
-    ``(retval, rvec (3,1), tvec (3,1))``.  Zero distortion only; m >= 6 (the DLT; OpenCV's
-    ITERATIVE also needs >= 6 non-coplanar points for its DLT start).  OpenCV is absent here,
-    so parity with it is unpinned; the tests check the known answers (noise-free BAdino2
-    views) and that the refinement never raises the reprojection error of its start."""
+    """``cv.solvePnP``, the call behind the reference's ``pnp.p3p`` (pnp.py:7-10).
+
+    SOLVEPNP_ITERATIVE: the pose over ALL correspondences, initialised by the DLT (rs_pnp_dlt
+    on the GPU, world points centred and RMS-scaled first -- OpenCV's DLT initialisation
+    conditions them too; EPnP for 4-5 points) or by (rvec, tvec) when ``useExtrinsicGuess``,
+    then refined by Levenberg-Marquardt on the pixel reprojection error.  SOLVEPNP_EPNP: EPnP
+    over all points (m >= 4).  SOLVEPNP_P3P: exactly 4 points.  Returns ``(retval, rvec (3,1),
+    tvec (3,1))``.  Zero distortion only.  OpenCV is absent here, so parity with it is
+    unpinned; the tests check known answers (noise-free BAdino2 views) and that the refinement
+    never raises the reprojection error of its start."""
+    _check_flags(flags)
+    X, uv, K = _inputs(objectPoints, imagePoints, cameraMatrix, distCoeffs)
+    ctx = ctx or _ffi.default_context()
+    if flags == SOLVEPNP_P3P:
+        if len(X) != 4:
+            raise ValueError("SOLVEPNP_P3P takes exactly 4 points")
+        pose = minimal_pose(X, uv, K, _ffi.PNP_P3P, ctx)
+    elif flags == SOLVEPNP_EPNP:
+        if len(X) < 4:
+            raise ValueError("SOLVEPNP_EPNP needs at least 4 points")
+        pose = minimal_pose(X, uv, K, _ffi.PNP_EPNP5, ctx)
+    else:
+        pose = None
     if flags != SOLVEPNP_ITERATIVE:
-        raise ValueError("only SOLVEPNP_ITERATIVE is provided")
-    X = np.ascontiguousarray(np.asarray(objectPoints, dtype=np.float64).reshape(-1, 3))
-    uv = np.ascontiguousarray(np.asarray(imagePoints, dtype=np.float64).reshape(-1, 2))
-    if len(X) != len(uv):
-        raise ValueError("objectPoints and imagePoints must have the same count")
-    if distCoeffs is not None and np.any(np.asarray(distCoeffs) != 0):
-        raise ValueError("only zero lens distortion is supported")
-    K = np.asarray(cameraMatrix, dtype=np.float64).reshape(3, 3)
+        if pose is None:
+            return False, None, None
+        rv, _ = Rodrigues(pose[0])
+        return True, rv.reshape(3, 1), pose[1].reshape(3, 1)
     if useExtrinsicGuess and rvec is not None and tvec is not None:
         r0 = np.asarray(rvec, dtype=np.float64).reshape(3, 1)
         t0 = np.asarray(tvec, dtype=np.float64).reshape(3, 1)
-    else:
-        if len(X) < 6:
-            raise ValueError("SOLVEPNP_ITERATIVE needs at least 6 non-coplanar points for its DLT start")
+    elif len(X) >= 6:
         c = X.mean(axis=0)
         s = float(np.sqrt(np.mean(np.sum((X - c) ** 2, axis=1)))) or 1.0
         Xc = np.ascontiguousarray((X - c) / s)
-        y = np.linalg.solve(K, np.vstack([uv.T, np.ones((1, len(uv)))])).T
-        y = np.ascontiguousarray(y)
+        y = _normalised(uv, K)
         R = np.empty(9)
         t = np.empty(3)
-        _ffi.check(_ffi.lib().rs_pnp_dlt((ctx or _ffi.default_context()).handle,
-                                         _ffi.ptr(Xc, _ffi.C.c_double), _ffi.ptr(y, _ffi.C.c_double),
-                                         len(X), _ffi.ptr(R, _ffi.C.c_double),
-                                         _ffi.ptr(t, _ffi.C.c_double)))
+        _ffi.check(_ffi.lib().rs_pnp_dlt(ctx.handle, _ffi.ptr(Xc, _ffi.C.c_double),
+                                         _ffi.ptr(y, _ffi.C.c_double), len(X),
+                                         _ffi.ptr(R, _ffi.C.c_double), _ffi.ptr(t, _ffi.C.c_double)))
         R = R.reshape(3, 3)
         if not np.all(np.isfinite(R)):
             return False, None, None
         # the conditioned frame: x = s x' + c, so R x + t = s (R x' + t') gives t = s t' - R c
         r0, _ = Rodrigues(R)
         t0 = (s * t - R @ c).reshape(3, 1)
+    elif len(X) >= 4:
+        pose = minimal_pose(X, uv, K, _ffi.PNP_EPNP5, ctx)
+        if pose is None:
+            return False, None, None
+        r0, _ = Rodrigues(pose[0])
+        t0 = pose[1].reshape(3, 1)
+    else:
+        raise ValueError("solvePnP needs at least 4 points")
     rv, tv = _refine_lm(X, uv, K, r0, t0)
     return True, np.asarray(rv, dtype=np.float64).reshape(3, 1), np.asarray(tv, dtype=np.float64).reshape(3, 1)

@@ -131,9 +131,9 @@ def add_new_view(T, K, img_index, y1_hom, y2_hom, y1, y2, solvePnPRansac=None, R
 
     The new view's pose is built with the class of the table's existing poses (the reference's
     help_classes.CameraPose in the pipeline), so no reference module is imported here.  When
-    PnP-RANSAC fails -- fewer than 6 matched 2D<->3D correspondences (the DLT minimal solver;
-    OpenCV's EPnP kernel would accept 4-5) or no consensus -- a ValueError names the number of
-    matched points instead of the reference's crash inside Rodrigues / inliers[:, 0]."""
+    PnP-RANSAC fails -- fewer than 4 matched 2D<->3D correspondences (OpenCV asserts 4 too) or
+    no consensus -- a ValueError names the number of matched points instead of the reference's
+    crash inside Rodrigues / inliers[:, 0]."""
     from . import cv as gcv
     solvePnPRansac = solvePnPRansac or gcv.solvePnPRansac
     Rodrigues = Rodrigues or gcv.Rodrigues
@@ -150,12 +150,14 @@ def add_new_view(T, K, img_index, y1_hom, y2_hom, y1, y2, solvePnPRansac=None, R
     D_img_hom = np.asarray(y2_hom)[found].reshape(-1, 3)
     A_y1 = np.asarray(y1)[~found].reshape(-1, 2).astype(np.float64)
     A_y2 = np.asarray(y2)[~found].reshape(-1, 2).astype(np.float64)
+    if len(x_i) < 4:
+        raise ValueError(f"solvePnPRansac found no pose for view {img_index}: {len(x_i)} "
+                         f"putative correspondences matched known 3D points (PnP needs >= 4)")
     retval, R, t, inliers = solvePnPRansac(D_3D[:, :3], D_img[:, :2], K, np.zeros((4, 1)),
                                            useExtrinsicGuess=True)
     if not retval or R is None or inliers is None:
         raise ValueError(f"solvePnPRansac found no pose for view {img_index}: {len(x_i)} "
-                         f"putative correspondences matched known 3D points (the DLT needs "
-                         f">= 6 and a consensus)")
+                         f"putative correspondences matched known 3D points, no consensus")
     R, _ = Rodrigues(R)
     view_index = T.addView(img_index, pose_cls(R, np.asarray(t)[:, 0]))
     for yy, x in zip(D_img_hom[inliers[:, 0]], x_i[inliers[:, 0]]):
