@@ -106,6 +106,27 @@ def _cpu_worker(args):
             return done, el
 
 
+def host_cores():
+    """The host cores this process may use: the CPU affinity mask, bounded by the cgroup CPU
+    quota and by OMP_NUM_THREADS (the box exports its CPU share there; nproc and
+    os.cpu_count() show the whole machine).  Returns (cores, evidence)."""
+    ev = {"affinity": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count()}
+    n = ev["affinity"]
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            ev["cgroup_quota"] = float(q) / float(per)
+            n = min(n, max(1, int(ev["cgroup_quota"])))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        ev["omp_num_threads"] = int(omp)
+        n = min(n, int(omp))
+    return n, ev
+
+
 def cpu_baseline(p1, p2, budget_s, procs):
     """Oracle CPU baseline on the box's host cores, bounded sample: one process per core
     (independent seeds, BLAS threads = 1), forked BEFORE the GPU is initialised; plus the
@@ -115,7 +136,9 @@ def cpu_baseline(p1, p2, budget_s, procs):
     with mp.get_context("fork").Pool(procs) as pool:
         res = pool.map(_cpu_worker, [(p1, p2, 1 + k, budget_s) for k in range(procs)])
     agg = sum(d / e for d, e in res)
+    cores, ev = host_cores()
     return {"value": agg, "unit": "hypotheses/s", "cores": procs, "kind": "port",
+            "host_cores": ev,
             "single_core_value": one[0] / one[1],
             "sample": f"{sum(d for d, _ in res)} hypotheses of the same C2 pair "
                       f"(N={p1.shape[1]}) through oracle/ransac_ref.ransac_f (numpy, OpenBLAS "
@@ -314,8 +337,10 @@ def extras(ctx, rank, world, dist, comm):
         out["e5_ransac_c2"] = {"metric": "five-point E-RANSAC minimal samples/s", "value": S / el,
                                "ms": el * 1e3, "samples": S, "hypotheses": 10 * S,
                                "consensus": r.count,
-                               "note": "k_e5_solve (all real roots of each sample) + k_f8_count "
-                                       "over 10 slots per sample + selection, N = 2000"}
+                               "round2_value": E5_ROUND2[0], "round2_source": E5_ROUND2[1],
+                               "note": "k_e5_solve (all real roots of each sample, stored as "
+                                       "found: no per-lane solution array) + k_f8_count over 10 "
+                                       "slots per sample + selection, N = 2000"}
     except Exception as e:  # noqa: BLE001
         out["e5_ransac_c2"] = {"error": repr(e)}
     # ---- per-view table steps (tables.py:116-175, 260-380) at the reference's noisy sizes ----
@@ -353,6 +378,13 @@ def extras(ctx, rank, world, dist, comm):
 COUNT_KERNEL = {"fp32": "k_f8_count32q", "fp64": "k_f8_count"}
 
 
+COUNT_BYTES_PER_HYP, COUNT_BYTES_PER_POINT = 9 * 4 + 16 + 4, 16
+
+# e5_ransac_c2 before the scratch cut (k_e5_solve kept all ten solutions in a per-lane array:
+# 1664 B of scratch per lane), as the round-2 driver bench measured it
+E5_ROUND2 = (13389928.829414358, "BENCH_r02.json extras.e5_ransac_c2.value (1.494 ms / 20000)")
+
+
 def load_pmc(n_corr, hyps):
     """HBM bytes per counting launch from the newest committed rocprofv3 PMC summary."""
     import glob
@@ -378,8 +410,8 @@ def main():
     ap.add_argument("--hyps", type=int, default=HYPS)
     ap.add_argument("--n", type=int, default=N_CORR)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-procs", type=int,
-                    default=int(os.environ.get("RSAMD_CPU_PROCS", "16")))  # the box's CPU share
+    ap.add_argument("--cpu-procs", type=int, default=0,
+                    help="oracle worker processes (default: host_cores())")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity-mode", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
@@ -395,7 +427,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # before any HIP call: the worker processes are forked from this one
         cp1, cp2, _ = synth.two_view(args.n, OUTLIERS, seed=1)
-        cpu = cpu_baseline(cp1, cp2, args.cpu_seconds, args.cpu_procs)
+        cpu = cpu_baseline(cp1, cp2, args.cpu_seconds, args.cpu_procs or host_cores()[0])
     # RSAMD_BENCH_DEVICE pins every rank to one device: a multi-rank rehearsal on a one-GPU
     # box (RCCL refuses two ranks on one GPU, so that run exercises the TCP-hub exchange)
     ctx = _ffi.Context(int(os.environ.get("RSAMD_BENCH_DEVICE", local_rank)))
@@ -509,6 +541,12 @@ def main():
                      "achieved": achieved, "peak": PEAK_FP32_VALU_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_FP32_VALU_TFLOPS,
                      "traffic": pmc,
+                     # algorithmic HBM bytes of one counting launch: per hypothesis the fp32
+                     # model (36 B) + its guard-band float4 (16 B) + the count (4 B); the packed
+                     # points once (16 B each); PMC traffic / this = re-read factor
+                     "algorithmic_bytes": H * COUNT_BYTES_PER_HYP + args.n * COUNT_BYTES_PER_POINT,
+                     "traffic_over_algorithmic": (pmc / (H * COUNT_BYTES_PER_HYP + args.n * COUNT_BYTES_PER_POINT)
+                                                  if pmc else None),
                      "per_launch": {"hypotheses": H, "flop": H * FLOP_PER_CORR * args.n,
                                     "avg_ms": c_ms, "timed_launches_every": TIMING_EVERY},
                      "whole_run_nominal": {

@@ -21,4 +21,6 @@ B="python3 bench.py --steps 50 --warmup 200 --no-cpu-baseline --no-parity-mode -
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o pmc -- $B > $OUT/pmc_fetch.log 2>&1 || { echo pmc fetch failed; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_write -o pmc -- $B > $OUT/pmc_write.log 2>&1 || { echo pmc write failed; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU_FMA_F64 --output-format csv -d $OUT/pmc_sq -o pmc -- $B > $OUT/pmc_sq.log 2>&1 || echo "pmc sq failed"
+# scalar / instruction cache pass: the count kernel reads its points through the scalar cache
+timeout -s KILL 300 rocprofv3 --pmc SQC_DCACHE_REQ SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_ICACHE_REQ SQC_ICACHE_MISSES SQC_TC_DATA_READ_REQ SQC_TC_INST_REQ GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_sqc -o pmc -- $B > $OUT/pmc_sqc.log 2>&1 || echo "pmc sqc failed"
 find $OUT -name "*.csv" | head -50

@@ -39,7 +39,7 @@ def main():
                 os.path.join(prof, f"{tag}_kernel_stats.csv"))
     bench = json.load(open(os.path.join(src, "bench.json")))
     counters, launches = {}, {}
-    for sub in ("pmc_fetch", "pmc_write", "pmc_sq"):
+    for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sqc"):
         p = os.path.join(src, sub, "pmc_counter_collection.csv")
         if os.path.exists(p):
             c, n = per_launch(p, KERNEL)
@@ -68,6 +68,12 @@ def main():
         "ambiguous_pair_rate_est": (counters.get("SQ_INSTS_VALU_FMA_F64", 0.0) / FMA64_PER_RETEST /
                                     (bench["config"]["hypotheses_per_step"] / 64.0 *
                                      bench["config"]["n_corr"] / 2.0)),
+        "sqc_dcache_hit_rate": (counters["SQC_DCACHE_HITS"] / counters["SQC_DCACHE_REQ"]
+                                if counters.get("SQC_DCACHE_REQ") else None),
+        "sqc_dcache_req_per_wave_point": (counters.get("SQC_DCACHE_REQ", 0.0) /
+                                          (bench["config"]["hypotheses_per_step"] *
+                                           bench["config"]["n_corr"] / 64.0)),
+        "algorithmic_bytes_per_launch": bench["roofline"].get("algorithmic_bytes"),
         "pmc_run": "50 counted launches after 200 warm-up launches (clock ramped)",
         "source": f"rocprofv3 --pmc passes of bench.py (tools/gpu_round.sh), {src}",
     }

@@ -235,6 +235,10 @@ __global__ __launch_bounds__(256) void k_f8_count(const Pt *__restrict__ pts, in
 // 0.098-0.101 for equal slices, interleaved runs on one box (round 2).  Points loaded four at a
 // time (16 SGPRs per load group: 90 SGPRs, 7-8 waves per SIMD) were not faster either:
 // 97.0-99.3 us against 96.9-97.1 us, with 6 144 / 7 168 / 8 192 resident-wave launch shapes.
+// A scalar-load double buffer (block i+8's two s_load_dwordx16 issued right after block i's
+// data arrived, 16 s_mov_b64 per block to rotate) was not faster either (round 3, interleaved
+// A/B: 98.1-103.4 us against 97.5-99.3 us; profiles/r03b_count_ab.txt): six resident waves
+// per SIMD already cover the scalar cache's misses (SQC_DCACHE hit rate 36 %).
 // ----------------------------------------------------------------------------------------
 
 // The float64 test of k_f8_count (pixel units) for one (hypothesis, point).
