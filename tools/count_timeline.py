@@ -48,6 +48,21 @@ def main():
                "end_min_p10_p50_max": [round(q(en, x), 1) for x in (0, 10, 50, 100)],
                "dur_p10_p50_p90": [round(q(dur, x), 1) for x in (10, 50, 90)],
                "retest_p10_p50_p90_max": [int(q(nre, x)) for x in (10, 50, 90, 100)]})
+        # resident waves per SIMD over the launch: the drain is the SIMD-time with few waves
+        sid = ((xcc * 8 + se) * 16 + cu) * 4 + simd
+        grid = np.arange(0.0, en.max(), 0.25)
+        occ = np.zeros((int(sid.max()) + 1, len(grid)), np.int16)
+        for a, b, k in zip(st, en, sid):
+            occ[k, (grid >= a) & (grid < b)] += 1
+        used = occ[np.unique(sid)]
+        tot = used.size
+        print({"simds": int(len(used)),
+               "simd_time_frac_by_resident_waves": {str(w): round(float((used == w).sum()) / tot, 3)
+                                                    for w in range(0, 7)},
+               "simd_time_frac_7plus": round(float((used >= 7).sum()) / tot, 3),
+               "simd_last_wave_end_p10_p50_p90_us": [
+                   round(float(np.percentile([en[sid == k].max() for k in np.unique(sid)], x)), 1)
+                   for x in (10, 50, 90)]})
         first = st < 2.0  # the first round (all resident at once)
         if first.sum() > 10:
             d, k = dur[first], nre[first]

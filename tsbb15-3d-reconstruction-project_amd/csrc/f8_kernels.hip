@@ -238,7 +238,23 @@ __global__ __launch_bounds__(256) void k_f8_count(const Pt *__restrict__ pts, in
 // A scalar-load double buffer (block i+8's two s_load_dwordx16 issued right after block i's
 // data arrived, 16 s_mov_b64 per block to rotate) was not faster either (round 3, interleaved
 // A/B: 98.1-103.4 us against 97.5-99.3 us; profiles/r03b_count_ab.txt): six resident waves
-// per SIMD already cover the scalar cache's misses (SQC_DCACHE hit rate 36 %).
+// per SIMD already cover the scalar cache's misses (SQC_DCACHE hit rate 36 %).  Two instruction-
+// count variants, bit-exact against the full-size goldens, did not move it either (round 3,
+// profiles/r03_count_variants.txt): sure-inlier counts as scalar bit planes (two v_addc fewer
+// per pair, ~12 scalar ops more: 103-106 us, slower), and signed margins per point (E1 = P -
+// alpha m, E2 = beta m - Q by one fma each, ambiguity iff E1 E2 >= 0 tested once per block by a
+// running max3: no scalar work per pair, 30.75 instead of ~38 instructions per pair, in plain C
+// or behind this asm core: 98-103 us against 98-100 us).  PMC of the product kernel
+// (profiles/r03c_count_stall.txt): VALU instructions 79 % of the SIMD time at one quad-cycle
+// each, 89 % of the SIMDs' time with waves resident; neither the total instruction count nor the
+// scalar loads set the launch time -- the drain of unequal waves does (timeline, r03f: 26 % of
+// the SIMD-time has <= 3 resident waves; the last ~20 us run on a falling fraction of them).
+// Two ways to share the work dynamically, both bit-exact and both slower (round 3, same file):
+// persistent 12-wave workgroups taking whole hypothesis groups from per-XCD heads, sub-chunks
+// from an LDS counter, counts summed in LDS (109 us: the last groups leave one workgroup per CU
+// running alone), and static slices over 75 % of the plane with the rest claimed in 32-128-point
+// chunks from per-XCD heads (431-570 us: tens of thousands of returning device-scope atomics on
+// eight words serialise).
 // ----------------------------------------------------------------------------------------
 
 // The float64 test of k_f8_count (pixel units) for one (hypothesis, point).
