@@ -356,7 +356,14 @@ __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ p
 #pragma clang fp contract(off)
   typedef float f2 __attribute__((ext_vector_type(2)));
   const int lane = threadIdx.x & 63;
-  const int64_t w = wave_uniform(blockIdx.x * (BT / 64) + (threadIdx.x >> 6));
+  // XCD-aware slice order: workgroups are dealt to the 8 XCDs round-robin, so workgroup b runs
+  // on XCD b % 8; it takes slice block base(b % 8) + b / 8, which gives every XCD one contiguous
+  // run of slices -- a hypothesis group's slices, and so its fp32 models and decision constants,
+  // stay in one XCD's L2 instead of being fetched into two
+  const int nb = static_cast<int>(gridDim.x), bx = static_cast<int>(blockIdx.x);
+  const int xq = nb >> 3, xr = nb & 7, xc = bx & 7;
+  const int bslot = xc * xq + min(xc, xr) + (bx >> 3);
+  const int64_t w = wave_uniform(bslot * (BT / 64) + (threadIdx.x >> 6));
   const int npad = (n + 7) / 8 * 8;
   const int64_t total = static_cast<int64_t>((H + 63) >> 6) * npad;
   int64_t pos = w * per_wave;
