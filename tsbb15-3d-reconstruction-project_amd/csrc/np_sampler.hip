@@ -58,6 +58,7 @@ constexpr uint32_t kLower = 0x7fffffffu;
 constexpr uint32_t kMatA = 0x9908b0dfu;
 constexpr int kDeg = 19937;
 constexpr int kPrefix = kDeg + kN - 1;       // words of a window's sequence a jump reads
+constexpr int kPrefixAlloc = kN * ((kPrefix + kN - 1) / kN);  // generated in whole blocks
 constexpr int kJB = 1024;                    // stream blocks per generator
 constexpr int64_t kJ = int64_t(kN) * kJB;    // words per generator
 constexpr int kLevels = 16;                  // jump levels: windows up to 2^16 generators apart
@@ -108,107 +109,157 @@ __device__ __forceinline__ uint32_t draw_of(uint32_t w, uint32_t i) {
 // word 0 of a jumped window may carry wrong low bits: it is never emitted (k_mt_stream) and
 // the recurrence reads only its top bit.
 // Each jump is split into S parts over the (sorted) set bits, so that every level of the tree
-// runs on all CUs: part q regenerates in LDS only the prefix y_0 .. y_{hi-1} its bits read, XORs
-// its share (four groups of 256 threads a quarter of the bits each, three output words per
-// thread), and XOR-adds the partial window into the destination (zeroed beforehand) with
-// vector atomics; a single part stores it.
-constexpr int kJumpGroups = 4;
-__global__ __launch_bounds__(256 * kJumpGroups) void k_mt_jump(uint32_t *__restrict__ win, int half,
-                                                               int G, const int32_t *__restrict__ bits,
-                                                               int nbits, int S) {
-  extern __shared__ uint32_t y[];  // up to kPrefix words
-  __shared__ uint32_t part[kJumpGroups - 1][kN];
+// runs on all CUs: part q regenerates in LDS only the prefix y_0 .. y_{hi-1} its bits read,
+// XORs its share (kJumpGroups groups of kJumpGroupThreads threads, a third of the bits each),
+// and XOR-adds the partial window into the destination (zeroed beforehand) with vector atomics;
+// a single part stores it.
+// The XOR phase is LDS-bandwidth bound, so it reads aligned word PAIRS (ds_read_b64: 256 B per
+// clock against 128 for ds_read_b32): thread l of a group owns the pair (2l, 2l + 1) for an even
+// bit i, reading y_{i+2l}, y_{i+2l+1}; for an odd bit the aligned pair at i + 2l - 1 holds
+// y_{i+2l-1}, y_{i+2l}, which belong to words 2l - 1 and 2l.  The four accumulators per thread
+// are recombined through LDS at the end.  (b32 reads, three words per thread: C2 levels 7 / 8
+// 85 / 155 us.)
+constexpr int kJumpGroups = 3;
+constexpr int kJumpGroupThreads = 320;   // >= 313 pair owners (l = 0 .. 312)
+constexpr int kJumpThreads = kJumpGroups * kJumpGroupThreads;
+__global__ __launch_bounds__(kJumpThreads) void k_mt_jump(uint32_t *__restrict__ win, int half,
+                                                         int G, const int32_t *__restrict__ bits,
+                                                         int nbits, int ne, int S) {
+  // bits: the level's even set bits (ne of them, ascending), then its odd ones
+  extern __shared__ uint32_t y[];  // up to kPrefixAlloc words (8-byte aligned)
+  __shared__ uint32_t pe[kJumpGroups][kN], po[kJumpGroups][kN];
   const int g = blockIdx.x / S, q = blockIdx.x % S, dst = g + half;
   if (dst >= G) return;
-  const int p0 = static_cast<int>(static_cast<int64_t>(nbits) * q / S);
-  const int p1 = static_cast<int>(static_cast<int64_t>(nbits) * (q + 1) / S);
-  if (p0 >= p1) return;
-  const int hi = bits[p1 - 1] + kN;  // words y_0 .. y_{hi-1} are read
-  const int tid = threadIdx.x, grp = tid >> 8, lt = tid & 255;
-  for (int t = tid; t < kN; t += 256 * kJumpGroups) y[t] = win[static_cast<size_t>(g) * kN + t];
+  const int no = nbits - ne;
+  const int e0 = static_cast<int>(static_cast<int64_t>(ne) * q / S);
+  const int e1 = static_cast<int>(static_cast<int64_t>(ne) * (q + 1) / S);
+  const int q0 = ne + static_cast<int>(static_cast<int64_t>(no) * q / S);
+  const int q1 = ne + static_cast<int>(static_cast<int64_t>(no) * (q + 1) / S);
+  if (e0 >= e1 && q0 >= q1) return;
+  // words y_0 .. y_{hi-1} are read
+  const int hi = max(e1 > e0 ? bits[e1 - 1] : 0, q1 > q0 ? bits[q1 - 1] : 0) + kN;
+  const int tid = threadIdx.x;
+  const int grp = __builtin_amdgcn_readfirstlane(tid / kJumpGroupThreads), lt = tid - grp * kJumpGroupThreads;
+  for (int t = tid; t < kN; t += kJumpThreads) y[t] = win[static_cast<size_t>(g) * kN + t];
   __syncthreads();
-  for (int t0 = kN; t0 < hi; t0 += 227) {
-    const int t = t0 + tid;
-    if (tid < 227 && t < hi) y[t] = y[t - 227] ^ twist(y[t - kN], y[t - kN + 1]);
+  // the prefix a block of 624 words at a time, one barrier per block (the three dependent runs
+  // of the recurrence are one thread's chain, as in k_mt_stream; 88 -> 33 barriers at most)
+  for (int b0 = 0; b0 + kN < hi; b0 += kN) {
+    if (tid < 227) {
+      const uint32_t *o = y + b0;
+      uint32_t *n = y + b0 + kN;
+      const uint32_t n0 = o[tid + kM] ^ twist(o[tid], o[tid + 1]);
+      const uint32_t n1 = n0 ^ twist(o[tid + 227], o[tid + 228]);
+      n[tid] = n0;
+      n[tid + 227] = n1;
+      if (tid < 170) {
+        const uint32_t nx = tid + 455 < kN ? o[tid + 455] : (o[kM] ^ twist(o[0], o[1]));
+        n[tid + 454] = n1 ^ twist(o[tid + 454], nx);
+      }
+    }
     __syncthreads();
   }
-  const int w0 = lt, w1 = lt + 256, w2 = lt + 512 < kN ? lt + 512 : kN - 1;
-  const int per = (p1 - p0 + kJumpGroups - 1) / kJumpGroups;
-  const int b0 = p0 + grp * per, b1 = min(p1, b0 + per);
-  uint32_t a0 = 0, a1 = 0, a2 = 0;
-  int b = b0;
-  for (; b + 16 <= b1; b += 16) {  // 16 bit indices per scalar load batch
-    int ix[16];
+  // pair owner l = lt (0 .. 312); reads stay below hi + 1 <= kPrefixAlloc (lane 312 of an even
+  // bit reads y_{i+624}, y_{i+625}: words of the last generated block)
+  const bool act = lt <= kN / 2;
+  uint32_t a0 = 0, a1 = 0, c0 = 0, c1 = 0;  // even bits: words 2l, 2l+1; odd: 2l-1, 2l
+  const uint2 *y2 = reinterpret_cast<const uint2 *>(y);
+  // the group's share of a sorted run of bits of one parity, 16 indices per scalar load batch
+  auto run = [&](int r0, int r1, uint32_t &x0, uint32_t &x1) {
+    const int per = (r1 - r0 + kJumpGroups - 1) / kJumpGroups;
+    const int b0 = r0 + grp * per, b1 = min(r1, b0 + per);
+    int b = b0;
+    for (; b + 16 <= b1; b += 16) {
+      int ix[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) ix[k] = bits[b + k];
+      for (int k = 0; k < 16; ++k) ix[k] = bits[b + k];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      a0 ^= y[ix[k] + w0];
-      a1 ^= y[ix[k] + w1];
-      a2 ^= y[ix[k] + w2];
+      for (int k = 0; k < 16; ++k) {
+        const uint2 v = y2[(ix[k] >> 1) + lt];  // pair at i - (i & 1) + 2l
+        x0 ^= v.x;
+        x1 ^= v.y;
+      }
     }
-  }
-  for (; b < b1; ++b) {
-    const int i = bits[b];
-    a0 ^= y[i + w0];
-    a1 ^= y[i + w1];
-    a2 ^= y[i + w2];
-  }
-  if (grp > 0) {
-    part[grp - 1][w0] = a0;
-    part[grp - 1][w1] = a1;
-    if (lt + 512 < kN) part[grp - 1][w2] = a2;
+    for (; b < b1; ++b) {
+      const uint2 v = y2[(bits[b] >> 1) + lt];
+      x0 ^= v.x;
+      x1 ^= v.y;
+    }
+  };
+  if (act) {
+    run(e0, e1, a0, a1);
+    run(q0, q1, c0, c1);
+    const uint32_t o0 = c0, o1 = c1;
+    // word 2l: e0 ^ o1; word 2l+1: e1 (+ the next owner's o0); word 2l-1: o0
+    const int w = 2 * lt;
+    if (w < kN) pe[grp][w] = a0 ^ o1;
+    if (w + 1 < kN) pe[grp][w + 1] = a1;
+    if (w >= 1 && w - 1 < kN) po[grp][w - 1] = o0;
   }
   __syncthreads();
-  if (grp == 0) {
+  // combine: word t = XOR over groups of pe[.][t] ^ po[.][t] (po[.][t] for odd t only)
+  uint32_t *out = win + static_cast<size_t>(dst) * kN;
+  for (int t = tid; t < kN; t += kJumpThreads) {
+    uint32_t v = 0;
 #pragma unroll
-    for (int k = 0; k < kJumpGroups - 1; ++k) {
-      a0 ^= part[k][w0];
-      a1 ^= part[k][w1];
-      a2 ^= part[k][w2];
-    }
-    uint32_t *out = win + static_cast<size_t>(dst) * kN;
-    if (S == 1) {
-      out[w0] = a0;
-      out[w1] = a1;
-      if (lt + 512 < kN) out[w2] = a2;
-    } else {
-      atomicXor(out + w0, a0);
-      atomicXor(out + w1, a1);
-      if (lt + 512 < kN) atomicXor(out + w2, a2);
-    }
+    for (int k = 0; k < kJumpGroups; ++k) v ^= pe[k][t] ^ ((t & 1) ? po[k][t] : 0u);
+    if (S == 1) out[t] = v;
+    else atomicXor(out + t, v);
   }
 }
 
 // ---- 2. stream: generator g owns blocks (g kJB, (g+1) kJB] plus words 1..623 of its window --
-// 256 threads: a block is the three dependent runs of the recurrence (227, 227, 170 words),
-// one word per thread each, then tempered and stored; the two LDS blocks alternate.  (One wave
-// per generator with wave-level fences instead of barriers: 1.45 ms against 0.61 at C2.)
+// Thread l < 227 owns the words l, l + 227 and (l < 170) l + 454 of every block, in registers:
+//   new[l]       = old[l + 397] ^ twist(old[l], old[l + 1])
+//   new[l + 227] = new[l]       ^ twist(old[l + 227], old[l + 228])
+//   new[l + 454] = new[l + 227] ^ twist(old[l + 454], old[l + 455])   (new[0] for word 623)
+// so the three dependent runs of the recurrence are one thread's sequential chain and a block
+// needs ONE barrier: the old block is published in LDS (two buffers alternate), every thread
+// reads the four neighbour words it needs (thread 169 also recomputes new[0]).  (Three runs of
+// 227 / 227 / 170 threads with a barrier after each: 0.61 ms at C2; one wave per generator
+// with wave-level fences: 1.45 ms.)
 __global__ __launch_bounds__(256) void k_mt_stream(const uint32_t *__restrict__ win,
                                                    uint32_t *__restrict__ stream, int64_t Lb) {
   __shared__ uint32_t bb[2][kN];
   const int g = blockIdx.x, l = threadIdx.x;
+  const bool own = l < 227, own2 = l < 170;
   const int64_t b0 = static_cast<int64_t>(g) * kJB;
-  uint32_t *ob = bb[0], *nb = bb[1];
-  for (int t = l; t < kN; t += 256) {
-    const uint32_t v = win[static_cast<size_t>(g) * kN + t];
-    ob[t] = v;
-    if (t > 0 || g == 0) stream[b0 * kN + t] = temper(v);
+  const uint32_t *wg = win + static_cast<size_t>(g) * kN;
+  uint32_t o0 = 0, o1 = 0, o2 = 0;
+  if (own) {
+    o0 = wg[l];
+    o1 = wg[l + 227];
+    if (own2) o2 = wg[l + 454];
+    uint32_t *o = stream + b0 * kN;
+    if (l > 0 || g == 0) o[l] = temper(o0);
+    o[l + 227] = temper(o1);
+    if (own2) o[l + 454] = temper(o2);
   }
-  __syncthreads();
   const int64_t bend = std::min<int64_t>(b0 + kJB, Lb - 1);
+  int buf = 0;
   for (int64_t b = b0 + 1; b <= bend; ++b) {
-    if (l < 227) nb[l] = ob[l + kM] ^ twist(ob[l], ob[l + 1]);
+    uint32_t *ob = bb[buf];
+    if (own) {
+      ob[l] = o0;
+      ob[l + 227] = o1;
+      if (own2) ob[l + 454] = o2;
+    }
     __syncthreads();
-    if (l < 227) nb[227 + l] = nb[l] ^ twist(ob[227 + l], ob[228 + l]);
-    __syncthreads();
-    if (l < 170) nb[454 + l] = nb[227 + l] ^ twist(ob[454 + l], l + 1 < 170 ? ob[455 + l] : nb[0]);
-    __syncthreads();
-    uint32_t *o = stream + b * kN;
-    for (int t = l; t < kN; t += 256) o[t] = temper(nb[t]);
-    uint32_t *x = ob;
-    ob = nb;
-    nb = x;
+    if (own) {
+      const uint32_t n0 = ob[l + kM] ^ twist(o0, ob[l + 1]);
+      const uint32_t n1 = n0 ^ twist(o1, ob[l + 228]);
+      uint32_t *o = stream + b * kN;
+      o[l] = temper(n0);
+      o[l + 227] = temper(n1);
+      if (own2) {
+        const uint32_t nx = l + 455 < kN ? ob[l + 455] : (ob[kM] ^ twist(ob[0], ob[1]));
+        o2 = n1 ^ twist(o2, nx);
+        o[l + 454] = temper(o2);
+      }
+      o0 = n0;
+      o1 = n1;
+    }
+    buf ^= 1;
   }
 }
 
@@ -1181,7 +1232,8 @@ __global__ __launch_bounds__(64) void k_np_result(const uint32_t *__restrict__ s
 
 // ---- host ------------------------------------------------------------------------------------
 struct JumpPolys {
-  std::vector<std::vector<int32_t>> bits;  // level k: set bits of x^(2^k kJ) mod phi
+  std::vector<std::vector<int32_t>> bits;  // level k: set bits of x^(2^k kJ) mod phi, the even
+  std::vector<int> ne;                     // ones first (ne[k] of them), then the odd ones
 };
 
 const JumpPolys &jump_polys() {
@@ -1193,8 +1245,11 @@ const JumpPolys &jump_polys() {
     for (int k = 0; k < kLevels; ++k) {
       if (k) rs::mt_poly_square(p);
       std::vector<int32_t> b;
-      for (int i = 0; i < kDeg; ++i)
-        if ((p[static_cast<size_t>(i) >> 6] >> (i & 63)) & 1u) b.push_back(i);
+      for (int par = 0; par < 2; ++par) {
+        for (int i = par; i < kDeg; i += 2)
+          if ((p[static_cast<size_t>(i) >> 6] >> (i & 63)) & 1u) b.push_back(i);
+        if (par == 0) jp.ne.push_back(static_cast<int>(b.size()));
+      }
       jp.bits.push_back(std::move(b));
     }
   });
@@ -1323,7 +1378,7 @@ struct rs_np_shard {
   std::vector<uint8_t> maps;  // this rank's chunk-map blob
   // device
   int32_t *d_bits = nullptr;
-  std::vector<int> bit_off, bit_n;
+  std::vector<int> bit_off, bit_n, bit_ne;
   uint32_t *d_win = nullptr, *d_chain = nullptr, *d_stream = nullptr, *d_fin = nullptr,
            *d_fin_all = nullptr;
   int *d_fin_m = nullptr, *d_fin_m_all = nullptr, *d_ev_n = nullptr, *d_ent = nullptr,
@@ -1356,7 +1411,7 @@ int shard_kernel_attrs(int n1) {
   if (!jump) {
     HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_mt_jump),
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                static_cast<int>(sizeof(uint32_t) * kPrefix)));
+                                static_cast<int>(sizeof(uint32_t) * kPrefixAlloc)));
     jump = true;
   }
   const int64_t lds = 8 * static_cast<int64_t>((n1 + 1) & ~1);
@@ -1442,8 +1497,8 @@ int shard_windows(rs_np_shard &w, const uint32_t *key, hipStream_t s) {
     int j = 0;
     for (int lv = 0; lv < kLevels; ++lv) {
       if (!((w.g0 >> lv) & 1)) continue;
-      k_mt_jump<<<64, 256 * kJumpGroups, sizeof(uint32_t) * kPrefix, s>>>(
-          w.d_chain + static_cast<size_t>(j) * kN, 1, 2, w.d_bits + w.bit_off[lv], w.bit_n[lv], 64);
+      k_mt_jump<<<64, kJumpThreads, sizeof(uint32_t) * kPrefixAlloc, s>>>(
+          w.d_chain + static_cast<size_t>(j) * kN, 1, 2, w.d_bits + w.bit_off[lv], w.bit_n[lv], w.bit_ne[lv], 64);
       HIP_TRY(hipGetLastError());
       ++j;
     }
@@ -1452,10 +1507,13 @@ int shard_windows(rs_np_shard &w, const uint32_t *key, hipStream_t s) {
   }
   if (w.G > 1)
     HIP_TRY(hipMemsetAsync(w.d_win + kN, 0, sizeof(uint32_t) * kN * static_cast<size_t>(w.G - 1), s));
+  // S parts per jump so that a level is one round of workgroups (one per CU: the prefix takes
+  // 82 KB of LDS); two rounds cost a second prefix generation (C2 levels 3..8: 30 .. 168 us)
   for (int half = 1, lv = 0; half < w.G; half *= 2, ++lv) {
-    const int S = std::max(1, std::min(64, 512 / half));
-    k_mt_jump<<<half * S, 256 * kJumpGroups, sizeof(uint32_t) * kPrefix, s>>>(
-        w.d_win, half, static_cast<int>(w.G), w.d_bits + w.bit_off[lv], w.bit_n[lv], S);
+    const int jumps = static_cast<int>(std::min<int64_t>(half, w.G - half));
+    const int S = std::max(1, std::min(64, w.cus / jumps));
+    k_mt_jump<<<half * S, kJumpThreads, sizeof(uint32_t) * kPrefixAlloc, s>>>(
+        w.d_win, half, static_cast<int>(w.G), w.d_bits + w.bit_off[lv], w.bit_n[lv], w.bit_ne[lv], S);
     HIP_TRY(hipGetLastError());
   }
   return RS_OK;
@@ -1472,6 +1530,7 @@ int shard_init(rs_np_shard &w) {
     for (const auto &b : jp.bits) {
       w.bit_off.push_back(static_cast<int>(all.size()));
       w.bit_n.push_back(static_cast<int>(b.size()));
+      w.bit_ne.push_back(jp.ne[w.bit_ne.size()]);
       all.insert(all.end(), b.begin(), b.end());
     }
     int64_t cap = 0;
@@ -1513,8 +1572,19 @@ int shard_enqueue_parse(rs_np_shard &w) {
   HIP_TRY(hipMemsetAsync(w.d_err, 0, sizeof(int), s));
   const int Cr = static_cast<int>(w.Cr), Wc = static_cast<int>(w.Wc);
   const int64_t lds = 8 * static_cast<int64_t>((w.n1 + 1) & ~1);
+  long long *d_stats = nullptr;
+#ifdef RSAMD_DIAG
+  // RSAMD_NP_STATS=<file>: per-chunk statistics of the entry kernel appended to <file>
+  static int64_t cap_stats = 0;
+  static long long *stats_buf = nullptr;
+  if (std::getenv("RSAMD_NP_STATS")) {
+    if ((st = sgrow(stats_buf, cap_stats, w.Cr * 128))) return st;
+    HIP_TRY(hipMemsetAsync(stats_buf, 0, sizeof(long long) * w.Cr * 128, s));
+    d_stats = stats_buf;
+  }
+#endif
   EntryArgs ea{w.d_stream + (w.s_lo - w.wbase), w.Cr * w.Wc, Wc, w.n1, w.d_fin, w.d_fin_m,
-               w.d_ev, w.d_ev_n, w.d_tpos, w.ecap, w.d_err, nullptr};
+               w.d_ev, w.d_ev_n, w.d_tpos, w.ecap, w.d_err, d_stats};
   const bool small = w.n1 < 64;  // several hypothesis ends in one tracking window
   if (w.py) {
     k_np_entry<true><<<Cr, kEntryThreads, static_cast<size_t>(lds), s>>>(ea, ea.draws);
@@ -1526,6 +1596,21 @@ int shard_enqueue_parse(rs_np_shard &w) {
     (small ? k_np_track<false, true> : k_np_track<false, false>)<<<Cr, 64 * kTrackWaves, 0, s>>>(ea, ea.draws);
   }
   HIP_TRY(hipGetLastError());
+#ifdef RSAMD_DIAG
+  if (d_stats) {
+    std::vector<long long> hs(static_cast<size_t>(w.Cr) * 128 + 4);
+    hs[0] = w.n1;
+    hs[1] = w.Cr;
+    hs[2] = w.Wc;
+    hs[3] = w.Cr * w.Wc;
+    HIP_TRY(hipMemcpyAsync(hs.data() + 4, d_stats, sizeof(long long) * w.Cr * 128, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (FILE *f = std::fopen(std::getenv("RSAMD_NP_STATS"), "ab")) {
+      std::fwrite(hs.data(), sizeof(long long), hs.size(), f);
+      std::fclose(f);
+    }
+  }
+#endif
   return RS_OK;
 }
 
