@@ -1126,13 +1126,20 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
     const uint32_t u = in ? (PY ? (wd >> sh) : (wd & msk)) : 0xffffffffu;
     const uint32_t lo_s = i - static_cast<uint32_t>(l);
     uint64_t acc = __ballot(in && u <= lo_s);
-    uint64_t amb = __ballot(in && u > lo_s && u <= i);
-    while (amb) {
-      const int f = __ffsll(static_cast<long long>(amb)) - 1;
-      const uint32_t uf = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(u), f));
-      const uint32_t sf = i - static_cast<uint32_t>(__popcll(acc & ((1ull << f) - 1ull)));
-      if (uf <= sf) acc |= 1ull << f;
-      amb &= amb - 1ull;
+    const bool am = in && u > lo_s && u <= i;
+    const uint64_t amb = __ballot(am);
+    if (amb) {
+      // the ambiguous lanes by the fixed point acc <- ballot(u_l <= i - rank_l(acc)) (only they
+      // can change; lanes < l right => lane l right, so it ends at the sequential answer), from
+      // "every ambiguous lane accepts".  (One lane at a time on the scalar unit made the kernel
+      // scalar-issue bound: 4.2e8 SALU per C2 launch.)
+      const uint64_t sure = acc;
+      uint64_t a = sure | amb, prev;
+      do {
+        prev = a;
+        a = sure | __ballot(am && u <= i - lane_rank(prev));
+      } while (a != prev);
+      acc = a;
     }
     if ((acc >> l) & 1ull)
       J[i - static_cast<uint32_t>(__popcll(acc & below)) - 1u] = static_cast<uint16_t>(u);
