@@ -274,6 +274,16 @@ int rs_pnp_ransac(rs_ctx *ctx, const double *X_med, const double *y_med, int64_t
 int rs_pnp_minimal(rs_ctx *ctx, const double *X, const double *y, int64_t m, int32_t method,
                    double *R_out, double *t_out, double *err_out);
 
+/* Levenberg-Marquardt refinement of a pose (R row-major 3x3, t) on the PIXEL reprojection error
+ * |K pi(R x + t) - uv|^2 over m correspondences: the refinement stage of cv.solvePnP with
+ * SOLVEPNP_ITERATIVE (pnp.py:7-10) and of cv.solvePnPRansac (tables.py:141-147).  One GPU
+ * workgroup; left-multiplied rotation steps, Marquardt damping, only cost-lowering steps taken,
+ * at most max_jac Jacobians (OpenCV's CvLevMarq: 20), stop at a relative step below FLT_EPSILON.
+ * R_io / t_io are updated in place; cost_out (4 doubles, may be null): initial and final
+ * 0.5 |r|^2, Jacobians evaluated, steps taken. */
+int rs_pnp_refine_lm(rs_ctx *ctx, const double *X, const double *uv, int64_t m, const double *K,
+                     double *R_io, double *t_io, int32_t max_jac, double *cost_out);
+
 /* cv.solvePnPRansac drop-in (tables.py:141-145 call site): world points X (m,3), PIXEL
  * image points uv (m,2), camera matrix K (3,3 row-major, upper triangular), zero distortion.
  * Up to max_iters hypotheses (Philox samples from `seed` of the method's minimal size: EPnP

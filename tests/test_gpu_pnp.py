@@ -321,3 +321,45 @@ def test_c3_full_size_exact_stream_equals_oracle_fixture(ctx):
     st = rng.getstate()
     assert int(st[1][624]) == int(z["py_pos_out"])
     assert np.array_equal(np.array(st[1][:624], np.uint32), z["py_key_out"])
+
+
+def test_refine_lm_gpu_reaches_the_least_squares_pose(ctx):
+    """rs_pnp_refine_lm (the SOLVEPNP_ITERATIVE refinement, one GPU workgroup) against scipy's
+    MINPACK LM on the same pixel residual from the same perturbed start, on noisy BAdino2 views:
+    equal final cost (1e-9 relative), equal pose (1e-6), never above the start's cost."""
+    from scipy.optimize import least_squares
+    z = golden("dino_pnp_kat.npz")
+    rs = np.random.RandomState(11)
+    for v in (2, 7, 13):
+        X, uv, _ = _view(z, v)
+        K = z["K"][v]
+        uvn = uv + rs.normal(0.0, 1.0, uv.shape)
+        r_true, _ = cv.Rodrigues(z["R"][v])
+        r0 = r_true + rs.normal(0.0, 0.02, (3, 1))
+        t0 = z["t"][v].reshape(3, 1) * (1.0 + rs.normal(0.0, 0.02, (3, 1)))
+
+        def res(x):
+            return (cv.project_points(X, x[:3], x[3:], K) - uvn).ravel()
+
+        x0 = np.concatenate((r0.ravel(), t0.ravel()))
+        ref = least_squares(res, x0, method="lm", xtol=1e-15, ftol=1e-15, gtol=1e-15)
+        rv, tv = cv._refine_lm(X, uvn, K, r0, t0)
+        c_gpu = 0.5 * float(np.sum(res(np.concatenate((rv.ravel(), tv.ravel()))) ** 2))
+        assert c_gpu <= 0.5 * float(res(x0) @ res(x0))
+        assert cv.last_lm["cost"] == pytest.approx(c_gpu, rel=1e-9)
+        assert c_gpu == pytest.approx(ref.cost, rel=1e-9), (v, c_gpu, ref.cost)
+        np.testing.assert_allclose(rv.ravel(), ref.x[:3], atol=1e-6)
+        np.testing.assert_allclose(tv.ravel(), ref.x[3:], rtol=1e-6, atol=1e-6)
+    with pytest.raises(ValueError):  # fewer than 3 correspondences
+        _ffi_refine_short(X, uvn, K)
+
+
+def _ffi_refine_short(X, uv, K):
+    from tsbb15_amd import _ffi
+    R, t, c = np.eye(3), np.zeros(3), np.zeros(4)
+    _ffi.check(_ffi.lib().rs_pnp_refine_lm(_ffi.default_context().handle,
+                                           _ffi.ptr(np.ascontiguousarray(X[:2]), _ffi.C.c_double),
+                                           _ffi.ptr(np.ascontiguousarray(uv[:2]), _ffi.C.c_double),
+                                           2, _ffi.ptr(np.ascontiguousarray(K), _ffi.C.c_double),
+                                           _ffi.ptr(R, _ffi.C.c_double), _ffi.ptr(t, _ffi.C.c_double),
+                                           20, _ffi.ptr(c, _ffi.C.c_double)))

@@ -792,7 +792,6 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_np_track(EntryArgs a,
   constexpr int kStride = 64 * kTrackWaves;
   constexpr int kPer = (kCheck + kStride - 1) / kStride;  // draws per thread per interval
   const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = uni(tid >> 6);
-  const int wq = wv;  // (rotating the busy wave across SIMDs by chunk: measured, no change)
   int m = a.fin_m[c];
   if (m > 64) return;  // the chunk ended while dense: final already
   const int n1 = a.n1;
@@ -800,6 +799,11 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_np_track(EntryArgs a,
   const int T = static_cast<int>(std::min<int64_t>(a.W, a.D - t0));
   int t = a.tpos[c];
   if (t >= T) return;
+  // (the busy wave is wave q % kTrackWaves for trajectory q; placing the trajectories by the
+  // waves' hardware SIMD ids, the two chunks of a CU on opposite SIMDs: no gain, 6.46 vs 6.40 ms
+  // at C2 with the SGPRs capped at 70 -- this kernel must stay within ~80 SGPRs, at 84-86 it
+  // loses its second 16-wave workgroup per CU, +1.3 ms)
+  const int wq = wv;
   const uint32_t *__restrict__ wp = draws + t0;
   uint2 *ev = a.ev + static_cast<size_t>(c) * a.ecap;
   // RSAMD_DIAG: windows (multi-slot path), cycles with one / several trajectories, wave-intervals

@@ -617,6 +617,225 @@ __global__ __launch_bounds__(256) void k_pack_ppts(const double *__restrict__ X,
   out[i] = p;
 }
 
+
+// ---- Levenberg-Marquardt on the pixel reprojection error (cv.solvePnP SOLVEPNP_ITERATIVE's
+// refinement stage, pnp.py:7-10 and the tables.py:141-147 call site) -------------------------
+// One workgroup: every pass maps the points over the threads, each accumulating its share of
+// J^T J (21 terms), J^T r (6) and the cost, reduced by wave shuffles and LDS; thread 0 solves the
+// damped 6 x 6 system (Marquardt scaling, Cholesky) and steps.  The pose is updated on the left,
+// R <- exp([d]x) R, t <- t + dt, so dq/dd = -[R x]x and dq/dt = I for q = R x + t; the pixel
+// residual is K pi(q) - uv with K's fx, skew, cx, fy, cy (K / K[2][2], as projectPoints).  Only
+// steps that lower the cost are taken (CvLevMarq), at most `max_jac` Jacobians and 8x as many
+// trial passes; the loop ends when a taken step moves the parameters by less than eps relative.
+struct LmK {
+  double fx, s, cx, fy, cy;
+};
+
+constexpr int kLmThreads = 256;
+constexpr int kLmAcc = 28;  // J^T J upper triangle (21), J^T r (6), |r|^2
+
+__device__ void lm_block_sum(double (&v)[kLmAcc], double (*sh)[kLmAcc]) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < kLmAcc; ++k) {
+    double x = v[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    v[k] = x;
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < kLmAcc; ++k) sh[wv][k] = v[k];
+  __syncthreads();
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int k = 0; k < kLmAcc; ++k) {
+      double x = 0.0;
+      for (int w = 0; w < kLmThreads / 64; ++w) x += sh[w][k];
+      v[k] = x;
+    }
+}
+
+// io: R (9), t (3), then scratch / results (4)
+__global__ __launch_bounds__(kLmThreads) void k_pnp_lm(const double *__restrict__ X,
+                                                        const double *__restrict__ uv, int n, LmK K,
+                                                        double *__restrict__ io, int max_jac,
+                                                        double eps) {
+  __shared__ double sR[9], st[3], tR[9], tt[3];
+  __shared__ double sh[kLmThreads / 64][kLmAcc];
+  __shared__ int s_cmd;  // 0 Jacobian pass at the current pose, 1 trial pass, 2 stop
+  const int tid = threadIdx.x;
+  if (tid < 9) sR[tid] = io[tid];
+  if (tid < 3) st[tid] = io[9 + tid];
+  if (tid == 0) s_cmd = 0;
+  __syncthreads();
+  // thread 0's LM state
+  double A[21] = {}, g[6] = {}, cost = 0.0, cost0 = 0.0, lambda = 1e-3, step2 = 0.0;
+  int njac = 0, ntrial = 0, taken = 0;
+  for (;;) {
+    const int cmd = s_cmd;
+    if (cmd == 2) break;
+    double R[9], t[3];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) R[k] = cmd == 0 ? sR[k] : tR[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) t[k] = cmd == 0 ? st[k] : tt[k];
+    double acc[kLmAcc];
+#pragma unroll
+    for (int k = 0; k < kLmAcc; ++k) acc[k] = 0.0;
+    for (int i = tid; i < n; i += kLmThreads) {
+      const double *x = X + 3 * i;
+      const double p0 = fma(R[0], x[0], fma(R[1], x[1], R[2] * x[2]));
+      const double p1 = fma(R[3], x[0], fma(R[4], x[1], R[5] * x[2]));
+      const double p2 = fma(R[6], x[0], fma(R[7], x[1], R[8] * x[2]));
+      const double q0 = p0 + t[0], q1 = p1 + t[1], q2 = p2 + t[2];
+      const double iz = 1.0 / q2, a = q0 * iz, b = q1 * iz;
+      const double ru = fma(K.fx, a, fma(K.s, b, K.cx)) - uv[2 * i];
+      const double rv = fma(K.fy, b, K.cy) - uv[2 * i + 1];
+      acc[27] = fma(ru, ru, fma(rv, rv, acc[27]));
+      if (cmd != 0) continue;
+      // du/dq, dv/dq
+      const double du0 = K.fx * iz, du1 = K.s * iz, du2 = -(K.fx * a + K.s * b) * iz;
+      const double dv1 = K.fy * iz, dv2 = -K.fy * b * iz;
+      // J = dres/dq [ -[p]x | I ],  -[p]x = [[0, p2, -p1], [-p2, 0, p0], [p1, -p0, 0]]
+      double ju[6], jv[6];
+      ju[0] = -du1 * p2 + du2 * p1;
+      ju[1] = du0 * p2 - du2 * p0;
+      ju[2] = -du0 * p1 + du1 * p0;
+      ju[3] = du0;
+      ju[4] = du1;
+      ju[5] = du2;
+      jv[0] = -dv1 * p2 + dv2 * p1;
+      jv[1] = -dv2 * p0;
+      jv[2] = dv1 * p0;
+      jv[3] = 0.0;
+      jv[4] = dv1;
+      jv[5] = dv2;
+      int k = 0;
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c2 = r; c2 < 6; ++c2) acc[k++] += ju[r] * ju[c2] + jv[r] * jv[c2];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) acc[21 + r] += ju[r] * ru + jv[r] * rv;
+    }
+    lm_block_sum(acc, sh);
+    if (tid == 0) {
+      const double c = 0.5 * acc[27];
+      bool solve = false;
+      if (cmd == 0) {  // the Jacobian at the current pose
+        if (njac == 0) cost0 = c;
+        cost = c;
+#pragma unroll
+        for (int k = 0; k < 21; ++k) A[k] = acc[k];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) g[k] = acc[21 + k];
+        ++njac;
+        solve = isfinite(c);
+        if (!solve) s_cmd = 2;
+      } else {  // a trial pose
+        ++ntrial;
+        if (c < cost && isfinite(c)) {  // taken
+          for (int k = 0; k < 9; ++k) sR[k] = tR[k];
+          double pn = 0.0;
+          for (int k = 0; k < 3; ++k) {
+            st[k] = tt[k];
+            pn += tt[k] * tt[k];
+          }
+          cost = c;
+          lambda = fmax(lambda * 0.1, 1e-12);
+          ++taken;
+          // converged when the step is below eps relative to the parameters (|t| + rotation)
+          s_cmd = (njac < max_jac && step2 > eps * eps * (pn + 1.0)) ? 0 : 2;
+        } else {
+          lambda *= 10.0;
+          solve = lambda < 1e16 && ntrial < 8 * max_jac;
+          if (!solve) s_cmd = 2;
+        }
+      }
+      // (A + lambda diag(A)) d = -g by Cholesky; trial R' = exp([d0..2]x) R, t' = t + d3..5
+      while (solve) {
+        // (fully unrolled: every index static, the 6 x 6 stays in registers)
+        double M[6][6], d[6];
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+          for (int c2 = 0; c2 < 6; ++c2) {
+            const int lo = r < c2 ? r : c2, hi = r < c2 ? c2 : r;
+            M[r][c2] = A[lo * 6 - lo * (lo - 1) / 2 + (hi - lo)];
+          }
+#pragma unroll
+        for (int r = 0; r < 6; ++r) M[r][r] *= 1.0 + lambda;
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+          double sj = M[j][j];
+#pragma unroll
+          for (int l = 0; l < j; ++l) sj -= M[j][l] * M[j][l];
+          ok = ok && sj > 0.0;
+          M[j][j] = sqrt(sj > 0.0 ? sj : 1.0);
+#pragma unroll
+          for (int r = j + 1; r < 6; ++r) {
+            double sr = M[r][j];
+#pragma unroll
+            for (int l = 0; l < j; ++l) sr -= M[r][l] * M[j][l];
+            M[r][j] = sr / M[j][j];
+          }
+        }
+        if (!ok) {  // singular even with damping: more damping, or stop
+          lambda *= 10.0;
+          if (!(lambda < 1e16)) {
+            s_cmd = 2;
+            solve = false;
+          }
+          continue;
+        }
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {  // L y = -g
+          double sr = -g[r];
+#pragma unroll
+          for (int l = 0; l < r; ++l) sr -= M[r][l] * d[l];
+          d[r] = sr / M[r][r];
+        }
+#pragma unroll
+        for (int r = 5; r >= 0; --r) {  // L^T d = y
+          double sr = d[r];
+#pragma unroll
+          for (int l = r + 1; l < 6; ++l) sr -= M[l][r] * d[l];
+          d[r] = sr / M[r][r];
+        }
+        const double th2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2], th = sqrt(th2);
+        const double sa = th2 < 1e-16 ? 1.0 - th2 / 6.0 : sin(th) / th;
+        const double cb = th2 < 1e-16 ? 0.5 - th2 / 24.0 : (1.0 - cos(th)) / th2;
+        const double W[9] = {0.0, -d[2], d[1], d[2], 0.0, -d[0], -d[1], d[0], 0.0};
+        double E[9];
+        for (int r = 0; r < 3; ++r)
+          for (int c2 = 0; c2 < 3; ++c2) {
+            double w2 = 0.0;
+            for (int l = 0; l < 3; ++l) w2 += W[3 * r + l] * W[3 * l + c2];
+            E[3 * r + c2] = (r == c2 ? 1.0 : 0.0) + sa * W[3 * r + c2] + cb * w2;
+          }
+        for (int r = 0; r < 3; ++r)
+          for (int c2 = 0; c2 < 3; ++c2)
+            tR[3 * r + c2] = E[3 * r] * sR[c2] + E[3 * r + 1] * sR[3 + c2] + E[3 * r + 2] * sR[6 + c2];
+        for (int r = 0; r < 3; ++r) tt[r] = st[r] + d[3 + r];
+        step2 = th2 + d[3] * d[3] + d[4] * d[4] + d[5] * d[5];
+        s_cmd = 1;
+        solve = false;
+      }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    for (int k = 0; k < 9; ++k) io[k] = sR[k];
+    for (int k = 0; k < 3; ++k) io[9 + k] = st[k];
+    io[12] = cost0;
+    io[13] = cost;
+    io[14] = njac;
+    io[15] = taken;
+  }
+}
+
 }  // namespace rsd
 
 // ------------------------------------------------------------------------------------------
@@ -927,5 +1146,40 @@ extern "C" int rs_pnp_ransac_cv(rs_ctx *c, const double *X, const double *uv, in
   out->best_count = good;
   if (n_inliers) *n_inliers = r->n_med;
   if (inliers) std::memcpy(inliers, r->inliers, sizeof(int64_t) * r->n_med);
+  return RS_OK;
+}
+
+extern "C" int rs_pnp_refine_lm(rs_ctx *c, const double *X, const double *uv, int64_t m,
+                                const double *K, double *R_io, double *t_io, int32_t max_jac,
+                                double *cost_out) {
+  if (!c || !X || !uv || !K || !R_io || !t_io) return fail(RS_EINVAL, "null pointer");
+  if (m < 3) return fail(RS_EINVAL, "the refinement needs m >= 3 correspondences");
+  if (m > (1 << 24)) return fail(RS_EINVAL, "too many correspondences");
+  if (max_jac < 1) return fail(RS_EINVAL, "max_jac must be >= 1");
+  if (!(K[8] != 0.0)) return fail(RS_EINVAL, "K[2][2] must be nonzero");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t bx = align256(sizeof(double) * 3 * m), bu = align256(sizeof(double) * 2 * m);
+  int st = rs::ensure_scratch(c, bx + bu + 256);
+  if (st) return st;
+  char *base = static_cast<char *>(c->scratch);
+  double *dX = reinterpret_cast<double *>(base), *du = reinterpret_cast<double *>(base + bx);
+  double *dio = reinterpret_cast<double *>(base + bx + bu);
+  double io[16] = {};
+  std::memcpy(io, R_io, sizeof(double) * 9);
+  std::memcpy(io + 9, t_io, sizeof(double) * 3);
+  HIP_TRY(hipMemcpyAsync(dX, X, sizeof(double) * 3 * m, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(du, uv, sizeof(double) * 2 * m, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(dio, io, sizeof(io), hipMemcpyHostToDevice, c->stream));
+  const double k22 = K[8];
+  const rsd::LmK kk{K[0] / k22, K[1] / k22, K[2] / k22, K[4] / k22, K[5] / k22};
+  hipLaunchKernelGGL(rsd::k_pnp_lm, dim3(1), dim3(rsd::kLmThreads), 0, c->stream, dX, du,
+                     static_cast<int>(m), kk, dio, static_cast<int>(max_jac),
+                     static_cast<double>(std::numeric_limits<float>::epsilon()));
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(io, dio, sizeof(io), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  std::memcpy(R_io, io, sizeof(double) * 9);
+  std::memcpy(t_io, io + 9, sizeof(double) * 3);
+  if (cost_out) std::memcpy(cost_out, io + 12, sizeof(double) * 4);
   return RS_OK;
 }

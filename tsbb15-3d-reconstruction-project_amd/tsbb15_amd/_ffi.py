@@ -110,6 +110,7 @@ _SIGS = {
                                    C.c_double, C.c_double, C.c_int32, _dp, C.POINTER(PnpResult),
                                    _i64p, _i64p, _i64p]),
     "rs_pnp_minimal": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, C.c_int32, _dp, _dp, _dp]),
+    "rs_pnp_refine_lm": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, _dp, _dp, C.c_int32, _dp]),
     "rs_e5_solve": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, _i32p]),
     "rs_e5_ransac": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, _dp, C.c_int64, C.c_uint64,
                                C.c_double, C.POINTER(E5Result), _i64p, _i64p]),

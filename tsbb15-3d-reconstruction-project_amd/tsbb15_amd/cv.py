@@ -21,7 +21,8 @@ solvePnPRansac structure:
     its RANSAC RNG with the same constant on every call: equal inputs give equal outputs;
   * the winner is refined on its consensus set as OpenCV does with ``flags``: Levenberg-
     Marquardt on the pixel reprojection error for SOLVEPNP_ITERATIVE (started from the RANSAC
-    pose), EPnP over the consensus set for SOLVEPNP_EPNP, none for SOLVEPNP_P3P;
+    pose; one GPU workgroup, rs_pnp_refine_lm), EPnP over the consensus set for SOLVEPNP_EPNP,
+    none for SOLVEPNP_P3P;
   * ``useExtrinsicGuess`` with ``rvec``/``tvec``: the guess is scored first, as hypothesis 0
     (OpenCV's kernels ignore it; here a good guess is kept unless a sample beats it).
 
@@ -42,8 +43,9 @@ LM_MAX_ITERS = 20  # OpenCV's solvePnP ITERATIVE: CvLevMarq criteria (20 iterati
 SOLVEPNP_ITERATIVE, SOLVEPNP_EPNP, SOLVEPNP_P3P = 0, 1, 2
 
 # the last call's RANSAC outcome before refinement: hypotheses the loop consumed, the winning
-# hypothesis and its pose (diagnostics / tests)
+# hypothesis and its pose (diagnostics / tests); the last LM refinement's costs and steps
 last_ransac = {}
+last_lm = {}
 
 
 def Rodrigues(src, dst=None, jacobian=None):
@@ -81,21 +83,33 @@ def project_points(X, rvec, tvec, K):
                      K[1, 1] * p[:, 1] + K[1, 2]), axis=1)
 
 
-def _refine_lm(X, uv, K, rvec, tvec):
-    from scipy.optimize import least_squares
-
-    def res(x):
-        return (project_points(X, x[:3], x[3:], K) - uv).ravel()
-
-    x0 = np.concatenate((np.ravel(rvec), np.ravel(tvec)))
-    r0 = res(x0)
-    if not np.all(np.isfinite(r0)) or len(r0) < 6:
+def _refine_lm(X, uv, K, rvec, tvec, ctx=None):
+    """Levenberg-Marquardt on the pixel reprojection error, on the GPU (rs_pnp_refine_lm):
+    left-multiplied rotation steps, Marquardt damping, only steps that lower the error
+    (CvLevMarq), at most LM_MAX_ITERS Jacobians.  Returns (rvec, tvec), never worse than the
+    start."""
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    uv = np.ascontiguousarray(uv, dtype=np.float64)
+    if len(X) < 3:
         return rvec, tvec
-    sol = least_squares(res, x0, method="lm", max_nfev=LM_MAX_ITERS * 7,
-                        xtol=np.finfo(np.float32).eps, ftol=np.finfo(np.float32).eps)
-    if not np.all(np.isfinite(sol.x)) or sol.cost > 0.5 * float(r0 @ r0):
-        return rvec, tvec  # CvLevMarq only accepts steps that lower the error
-    return sol.x[:3].reshape(3, 1), sol.x[3:].reshape(3, 1)
+    R, _ = Rodrigues(np.ravel(rvec))
+    R = np.ascontiguousarray(R, dtype=np.float64)
+    t = np.ascontiguousarray(np.ravel(tvec), dtype=np.float64).copy()
+    if not (np.all(np.isfinite(R)) and np.all(np.isfinite(t))):
+        return rvec, tvec
+    cost = np.zeros(4)
+    Kc = np.ascontiguousarray(K, dtype=np.float64)
+    _ffi.check(_ffi.lib().rs_pnp_refine_lm(
+        (ctx or _ffi.default_context()).handle, _ffi.ptr(X, _ffi.C.c_double),
+        _ffi.ptr(uv, _ffi.C.c_double), len(X), _ffi.ptr(Kc, _ffi.C.c_double),
+        _ffi.ptr(R, _ffi.C.c_double), _ffi.ptr(t, _ffi.C.c_double), LM_MAX_ITERS,
+        _ffi.ptr(cost, _ffi.C.c_double)))
+    last_lm.update(cost_init=float(cost[0]), cost=float(cost[1]), jacobians=int(cost[2]),
+                   steps=int(cost[3]))
+    if not (np.all(np.isfinite(R)) and np.all(np.isfinite(t))):
+        return rvec, tvec
+    rv, _ = Rodrigues(R)
+    return rv.reshape(3, 1), t.reshape(3, 1)
 
 
 def _inputs(objectPoints, imagePoints, cameraMatrix, distCoeffs):
@@ -180,7 +194,7 @@ def solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec=Non
     last_ransac.update(R=R, t=t)
     rv, _ = Rodrigues(R)
     if flags == SOLVEPNP_ITERATIVE:
-        rv, tv = _refine_lm(X[inl], uv[inl], K, rv, t)
+        rv, tv = _refine_lm(X[inl], uv[inl], K, rv, t, ctx)
     elif flags == SOLVEPNP_EPNP and len(inl) >= 4:
         pose = minimal_pose(np.ascontiguousarray(X[inl]), np.ascontiguousarray(uv[inl]), K,
                             _ffi.PNP_EPNP5, ctx)
@@ -251,5 +265,5 @@ def solvePnP(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec=None, tve
         t0 = pose[1].reshape(3, 1)
     else:
         raise ValueError("solvePnP needs at least 4 points")
-    rv, tv = _refine_lm(X, uv, K, r0, t0)
+    rv, tv = _refine_lm(X, uv, K, r0, t0, ctx)
     return True, np.asarray(rv, dtype=np.float64).reshape(3, 1), np.asarray(tv, dtype=np.float64).reshape(3, 1)
