@@ -76,6 +76,12 @@ constexpr int kK = 64;                       // draws between compactions (<= N 
 __host__ __device__ constexpr int fast_batches(int n1) { return n1 >= 4096 ? 32 : 16; }
 __host__ __device__ constexpr int fast_batches_multi(int n1) { return n1 >= 4096 ? 4 : 1; }
 constexpr int kRFast = 8;                    // slots per thread of the branch-free multi-slot path
+// Trajectories left when the dense parse hands a chunk to the tracking kernel, also the tracking
+// kernel's list capacity (a template argument, <= 8 per wave of its 16).  The
+// one-slot dense path costs ~N per draw and chunk, so large N hands over earlier: measured
+// (probe, C2 / N = 10 000): 64 -> 6.40 / 36.6 ms, 128 -> 6.48 / 34.2 ms.
+__host__ __device__ constexpr int hand_of(int n1) { return n1 >= 4096 ? 128 : 64; }
+
 constexpr uint32_t kSentinel = 0x80000000u;  // an empty slot: never reaches 0 within kW steps
 
 __device__ __forceinline__ uint32_t twist(uint32_t a, uint32_t b) {
@@ -335,6 +341,7 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
   if (tid == 0) sh_evn = 0;
   __syncthreads();
   int m = n1, t = 0;
+  const int hand = hand_of(n1);
   const int nfast = fast_batches(n1), nfastm = fast_batches_multi(n1);
 #ifdef RSAMD_DIAG
   // per path: cycles [0..2] (several slots / multi-slot fast / one-slot), compaction [3], draws [4..6]
@@ -353,7 +360,7 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
   do {                         \
   } while (0)
 #endif
-  if (m > 64) {
+  if (m > hand) {
     // dense phase: the whole workgroup, slots q = tid + r * kEntryThreads
     uint32_t s[kR];
 #pragma unroll
@@ -365,7 +372,7 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
     // batch ahead in every wave: the stream comes from HBM, and a load issued where it is
     // used cost ~40 cycles per draw (one HBM round trip per batch)
     uint32_t wa = lane < T ? wp[lane] : 0u, wb = 64 + lane < T ? wp[64 + lane] : 0u;
-    while (m > 64 && t < T) {
+    while (m > hand && t < T) {
       const int kk = min(kK, T - t);
       const int nr = (m + kEntryThreads - 1) / kEntryThreads;
       if (nr == 1 && kk == 64) {
@@ -529,7 +536,7 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
       o[9] = m;
     }
 #endif
-    if (m > 64) {  // chunk done while still dense
+    if (m > hand) {  // chunk done while still dense
       for (int q = tid; q < m; q += kEntryThreads)
         a.fin[static_cast<size_t>(c) * n1 + q] = lo[q] | (static_cast<uint32_t>(st[q]) << 16);
       if (tid == 0) {
@@ -540,7 +547,7 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
       return;
     }
   }
-  // hand over to k_np_sparse: the (<= 64) live slots, the wrap count and the position
+  // hand over to k_np_track: the (<= hand) live slots, the wrap count and the position
   __syncthreads();
   for (int q = tid; q < m; q += kEntryThreads)
     a.fin[static_cast<size_t>(c) * n1 + q] = lo[q] | (static_cast<uint32_t>(st[q]) << 16);
@@ -781,19 +788,18 @@ __device__ __forceinline__ void track_interval(const EntryArgs &a, const uint32_
     if (r < nq && lane == 0) s_st[wv + r * kTrackWaves] = i[r];
 }
 
-template <bool PY, bool SMALL>
-__global__ __launch_bounds__(64 * kTrackWaves) void k_np_track(EntryArgs a,
-                                                                const uint32_t *__restrict__ draws) {
+template <bool PY, bool SMALL, int CAP>  // CAP: list capacity = hand_of(n1)
+__device__ __forceinline__ void np_track_body(const EntryArgs &a, const uint32_t *__restrict__ draws) {
   // the draws of the current checkpoint interval in LDS (all trajectories of the chunk read
   // them; a window's read is issued one window ahead), the next interval in flight in VGPRs
   __shared__ uint32_t s_w[2][kCheck];
-  __shared__ uint32_t s_st[64], s_lo[64];
+  __shared__ uint32_t s_st[CAP], s_lo[CAP];
   __shared__ int s_m, s_evn;
   constexpr int kStride = 64 * kTrackWaves;
   constexpr int kPer = (kCheck + kStride - 1) / kStride;  // draws per thread per interval
   const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = uni(tid >> 6);
   int m = a.fin_m[c];
-  if (m > 64) return;  // the chunk ended while dense: final already
+  if (m > CAP) return;  // the chunk ended while dense: final already
   const int n1 = a.n1;
   const int64_t t0 = static_cast<int64_t>(c) * a.W;
   const int T = static_cast<int>(std::min<int64_t>(a.W, a.D - t0));
@@ -863,22 +869,41 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_np_track(EntryArgs a,
 #endif
     __syncthreads();
     if (wv == 0) {  // merge equal states (runs are contiguous in cyclic order)
-      const bool v = lane < m;
-      const uint32_t sq = v ? s_st[lane] : 0u;
-      const uint32_t sp = v ? s_st[lane == 0 ? m - 1 : lane - 1] : 0u;
-      const uint32_t lq = v ? s_lo[lane] : 0u;
-      const uint64_t vm = m >= 64 ? ~0ull : ((1ull << m) - 1ull);
-      const uint64_t eq = __ballot(v && m > 1 && sq == sp);
-      bool keep = v && !((eq >> lane) & 1ull);
-      if (eq == vm) keep = lane == 0;  // one trajectory left
-      const uint64_t kb = __ballot(keep);
-      __builtin_amdgcn_wave_barrier();
-      if (keep) {
-        const int dst = static_cast<int>(lane_rank(kb));
-        s_st[dst] = sq;
-        s_lo[dst] = lq;
+      constexpr int kH = CAP / 64;
+      uint32_t sq[kH], lq[kH];
+      uint64_t eq[kH];
+      int neq = 0;
+#pragma unroll
+      for (int h = 0; h < kH; ++h) {
+        const int q = lane + 64 * h;
+        const bool v = q < m;
+        sq[h] = v ? s_st[q] : 0u;
+        const uint32_t sp = v ? s_st[q == 0 ? m - 1 : q - 1] : 0u;
+        lq[h] = v ? s_lo[q] : 0u;
+        eq[h] = __ballot(v && m > 1 && sq[h] == sp);
+        neq += static_cast<int>(__popcll(eq[h]));
       }
-      if (lane == 0) s_m = static_cast<int>(__popcll(kb));
+      const bool one = neq == m;  // every entry equals its predecessor: one trajectory left
+      uint64_t kb[kH];
+      bool keep[kH];
+#pragma unroll
+      for (int h = 0; h < kH; ++h) {
+        const int q = lane + 64 * h;
+        keep[h] = one ? q == 0 : (q < m && !((eq[h] >> lane) & 1ull));
+        kb[h] = __ballot(keep[h]);
+      }
+      __builtin_amdgcn_wave_barrier();
+      int base = 0;
+#pragma unroll
+      for (int h = 0; h < kH; ++h) {
+        if (keep[h]) {
+          const int dst = base + static_cast<int>(lane_rank(kb[h]));
+          s_st[dst] = sq[h];
+          s_lo[dst] = lq[h];
+        }
+        base += static_cast<int>(__popcll(kb[h]));
+      }
+      if (lane == 0) s_m = base;
     }
     __syncthreads();
     m = uni(s_m);
@@ -904,6 +929,20 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_np_track(EntryArgs a,
 #else
   (void)dg;
 #endif
+}
+
+// The tracking kernel must stay within ~80 SGPRs: at 84-86 it loses its second 16-wave
+// workgroup per CU (+1.3 ms at C2).  The 64-entry kernel needs 70; the 128-entry one (large N)
+// is capped at 72 (spilling ~20 SGPRs to VGPR lanes: 86 uncapped).
+template <bool PY, bool SMALL>
+__global__ __launch_bounds__(64 * kTrackWaves) void k_np_track(EntryArgs a,
+                                                                const uint32_t *__restrict__ draws) {
+  np_track_body<PY, SMALL, 64>(a, draws);
+}
+template <bool PY>
+__global__ __launch_bounds__(64 * kTrackWaves) __attribute__((amdgpu_num_sgpr(72))) void
+k_np_track128(EntryArgs a, const uint32_t *__restrict__ draws) {
+  np_track_body<PY, false, 128>(a, draws);
 }
 
 // ---- 5. keep the wraps of the true trajectory (in place, order preserved) -----------------
@@ -1600,11 +1639,13 @@ int shard_enqueue_parse(rs_np_shard &w) {
   if (w.py) {
     k_np_entry<true><<<Cr, kEntryThreads, static_cast<size_t>(lds), s>>>(ea, ea.draws);
     HIP_TRY(hipGetLastError());
-    (small ? k_np_track<true, true> : k_np_track<true, false>)<<<Cr, 64 * kTrackWaves, 0, s>>>(ea, ea.draws);
+    (small ? k_np_track<true, true>
+           : (hand_of(w.n1) > 64 ? k_np_track128<true> : k_np_track<true, false>))<<<Cr, 64 * kTrackWaves, 0, s>>>(ea, ea.draws);
   } else {
     k_np_entry<false><<<Cr, kEntryThreads, static_cast<size_t>(lds), s>>>(ea, ea.draws);
     HIP_TRY(hipGetLastError());
-    (small ? k_np_track<false, true> : k_np_track<false, false>)<<<Cr, 64 * kTrackWaves, 0, s>>>(ea, ea.draws);
+    (small ? k_np_track<false, true>
+           : (hand_of(w.n1) > 64 ? k_np_track128<false> : k_np_track<false, false>))<<<Cr, 64 * kTrackWaves, 0, s>>>(ea, ea.draws);
   }
   HIP_TRY(hipGetLastError());
 #ifdef RSAMD_DIAG
