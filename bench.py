@@ -338,9 +338,10 @@ def extras(ctx, rank, world, dist, comm):
                                "ms": el * 1e3, "samples": S, "hypotheses": 10 * S,
                                "consensus": r.count,
                                "round2_value": E5_ROUND2[0], "round2_source": E5_ROUND2[1],
-                               "note": "k_e5_solve (all real roots of each sample, stored as "
-                                       "found: no per-lane solution array) + k_f8_count over 10 "
-                                       "slots per sample + selection, N = 2000"}
+                               "note": "k_e5_build (null basis, ten cubics) + k_e5_gj (Gauss-"
+                                       "Jordan, 32 lanes per sample) + k_e5_roots (all real "
+                                       "roots, stored as found) + k_f8_count over 10 slots per "
+                                       "sample + selection, N = 2000"}
     except Exception as e:  # noqa: BLE001
         out["e5_ransac_c2"] = {"error": repr(e)}
     # ---- per-view table steps (tables.py:116-175, 260-380) at the reference's noisy sizes ----

@@ -6,12 +6,16 @@
 // C-normalised points y1 (left) and y2 (right), E = R^T [t]_x for x2 = R x1 + t; pixel
 // points x = K y, so F = K1^-T E K2^-1 satisfies x1^T F x2 = 0.
 //
-//   k_e5_solve   lane per minimal sample of 5 correspondences:
+//   solve        three kernels per batch of minimal samples of 5 correspondences:
+//                k_e5_build (lane per sample)
 //                  1. Q (5 x 9), row i = vec(y1_i y2_i^T); Householder LQ of its rows, null
-//                     basis {X, Y, Z, W} = H_0 .. H_4 e_{5..8}: E = x X + y Y + z Z + W;
+//                     basis {X, Y, Z, W} = H_0 .. H_4 e_{5..8}: E = x X + y Y + z Z + W
+//                     (to memory);
 //                  2. the ten cubics det E = 0 and 2 E E^T E - tr(E E^T) E = 0 over the 20
-//                     monomials (Nister's order, kT3), Gauss-Jordan with partial pivoting on the
-//                     first ten columns -> [I | B];
+//                     monomials (Nister's order, kT3), to memory row by row;
+//                k_e5_gj (32 lanes per sample, a column per lane): Gauss-Jordan with partial
+//                  pivoting on the first ten columns -> [I | B];
+//                k_e5_roots (lane per sample)
 //                  3. k = row(x^2 z) - z row(x^2), l = row(y^2 z) - z row(y^2),
 //                     m = row(x y z) - z row(x y): linear in (x, y, 1), polynomial in z;
 //                     det [k; l; m](z) has degree 10;
@@ -19,7 +23,8 @@
 //                     polished by Newton; (x, y, 1) = the null vector of [k; l; m](z) (the
 //                     row cross product with the largest third component);
 //                writes up to 10 unit-norm E per sample, their F = K1^-T E K2^-1 (NaN slots
-//                past the sample's count, so they count 0).
+//                past the sample's count, so they count 0).  (One lane per sample for all of it
+//                held the 10 x 20 system in 256 VGPRs + 256 AGPRs + 752 B of scratch.)
 //   counting     k_f8_count (f8_kernels.hip) over the S x 10 slots: the reference's residual
 //                test d = max(|r1|, |r2|) < thresh of lab3.fmatrix_residuals in pixels.
 //   k_e5_select  c* = the largest count; among the slots with c* the smallest residual norm
@@ -123,8 +128,10 @@ __device__ __forceinline__ void e5_null_basis(double (&A)[5][9], double (&basis)
   }
 }
 
-// The ten cubic constraints (rows 0-8: 2 E E^T E - tr(E E^T) E, row 9: det E).
-__device__ __forceinline__ void e5_constraints(const double (&basis)[4][9], double (&M)[10][20]) {
+// The ten cubic constraints (rows 0-8: 2 E E^T E - tr(E E^T) E, row 9: det E), each row of 20
+// coefficients handed to sink(row, coefficients) as it is formed.
+template <class Sink>
+__device__ __forceinline__ void e5_constraints(const double (&basis)[4][9], Sink sink) {
   P1 E[9];
 #pragma unroll
   for (int e = 0; e < 9; ++e) {
@@ -159,8 +166,7 @@ __device__ __forceinline__ void e5_constraints(const double (&basis)[4][9], doub
 #pragma unroll
       for (int k = 0; k < 3; ++k) fma21(acc, 2.0, EEt[i][k], E[3 * k + j]);
       fma21(acc, -1.0, tr, E[3 * i + j]);
-#pragma unroll
-      for (int q = 0; q < 20; ++q) M[3 * i + j][q] = acc[q];
+      sink(3 * i + j, acc);
     }
   double det[20];
 #pragma unroll
@@ -174,50 +180,7 @@ __device__ __forceinline__ void e5_constraints(const double (&basis)[4][9], doub
   fma21(det, 1.0, c1b, E[1]);
   fma21(det, 1.0, c2, E[2]);
   fma21(det, -1.0, c2b, E[2]);
-#pragma unroll
-  for (int q = 0; q < 20; ++q) M[9][q] = det[q];
-}
-
-// Gauss-Jordan on the first ten columns with partial pivoting (row swaps as selects, so every
-// index stays static); returns false for a singular leading block.
-__device__ __forceinline__ bool e5_reduce(double (&M)[10][20]) {
-#pragma unroll
-  for (int c = 0; c < 10; ++c) {
-    int piv = c;
-    double best = fabs(M[c][c]);
-#pragma unroll
-    for (int r = c + 1; r < 10; ++r) {
-      const double v = fabs(M[r][c]);
-      if (v > best) {
-        best = v;
-        piv = r;
-      }
-    }
-    if (!(best > 0.0)) return false;
-#pragma unroll
-    for (int r = c + 1; r < 10; ++r) {
-      const bool sw = r == piv;
-#pragma unroll
-      for (int j = c; j < 20; ++j) {
-        const double a = M[c][j], b = M[r][j];
-        M[c][j] = sw ? b : a;
-        M[r][j] = sw ? a : b;
-      }
-    }
-    const double inv = 1.0 / M[c][c];
-#pragma unroll
-    for (int j = c + 1; j < 20; ++j) M[c][j] *= inv;
-    M[c][c] = 1.0;
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-      if (r == c) continue;
-      const double f = M[r][c];
-#pragma unroll
-      for (int j = c + 1; j < 20; ++j) M[r][j] = fma(-f, M[c][j], M[r][j]);
-      M[r][c] = 0.0;
-    }
-  }
-  return true;
+  sink(9, det);
 }
 
 template <int A, int B>
@@ -231,11 +194,11 @@ __device__ __forceinline__ void polymul(const double (&a)[A], const double (&b)[
     for (int j = 0; j < B; ++j) r[i + j] = fma(a[i], b[j], r[i + j]);
 }
 
-// row(a) - z row(b) of the reduced system (B rows a, b; columns 10..19): coefficients of x,
+// row(a) - z row(b) of the reduced system [I | B] (Bm holds B's rows 4..9): coefficients of x,
 // y and 1, ascending in z
-__device__ __forceinline__ void e5_row(const double (&M)[10][20], int a, int b, double (&px)[4],
+__device__ __forceinline__ void e5_row(const double (&Bm)[6][10], int a, int b, double (&px)[4],
                                        double (&py)[4], double (&p1)[5]) {
-  const double *A = &M[a][10], *Bb = &M[b][10];
+  const double *A = Bm[a - 4], *Bb = Bm[b - 4];
   px[0] = A[2];
   px[1] = A[1] - Bb[2];
   px[2] = A[0] - Bb[1];
@@ -259,34 +222,15 @@ __device__ __forceinline__ double horner_asc(const double (&p)[N], double z) {
   return v;
 }
 
-// All real solutions of one sample, each handed to emit(slot, E) as it is found (E row-major,
-// unit norm; no array of solutions is kept, so the 10 x 20 system and the null basis fit the
-// register file); returns their number (<= 10).
+// All real solutions of one sample from its reduced system (B rows 4..9) and its null basis
+// (read back from memory per solution), each handed to emit(slot, E) as it is found (E
+// row-major, unit norm); returns their number (<= 10).
 template <class Emit>
-__device__ int e5_solve_one(const double (&y1)[5][2], const double (&y2)[5][2], Emit emit) {
-  double Q[5][9];
-#pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    const double a0 = y1[i][0], a1 = y1[i][1], b0 = y2[i][0], b1 = y2[i][1];
-    Q[i][0] = a0 * b0;
-    Q[i][1] = a0 * b1;
-    Q[i][2] = a0;
-    Q[i][3] = a1 * b0;
-    Q[i][4] = a1 * b1;
-    Q[i][5] = a1;
-    Q[i][6] = b0;
-    Q[i][7] = b1;
-    Q[i][8] = 1.0;
-  }
-  double basis[4][9];
-  e5_null_basis(Q, basis);
-  double M[10][20];
-  e5_constraints(basis, M);
-  if (!e5_reduce(M)) return 0;
+__device__ int e5_solve_tail(const double (&Bm)[6][10], const double *bas, int64_t ldb, Emit emit) {
   double kx[4], ky[4], k1[5], lx[4], ly[4], l1[5], mx[4], my[4], m1[5];
-  e5_row(M, 4, 5, kx, ky, k1);
-  e5_row(M, 6, 7, lx, ly, l1);
-  e5_row(M, 8, 9, mx, my, m1);
+  e5_row(Bm, 4, 5, kx, ky, k1);
+  e5_row(Bm, 6, 7, lx, ly, l1);
+  e5_row(Bm, 8, 9, mx, my, m1);
   // det [k; l; m] = kx (ly m1 - l1 my) - ky (lx m1 - l1 mx) + k1 (lx my - ly mx)
   double t7a[8], t7b[8], t7[8], d[11], u[11];
   polymul(ly, m1, t7a);
@@ -319,7 +263,10 @@ __device__ int e5_solve_one(const double (&y1)[5][2], const double (&y2)[5][2], 
   int trailing = 0;
   const int deg = aberth_roots<10>(g, zr, zi, trailing);
   int ns = 0;
-  for (int r = 0; r < deg + trailing && ns < kE5Sol; ++r) {
+  // (unrolled: every root index static, no array of roots addressed at run time)
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r >= deg + trailing || ns >= kE5Sol) continue;
     double z = r < deg ? zr[r] : 0.0;
     if (r < deg && !(fabs(zi[r]) <= 1e-6 * fmax(1.0, fabs(z)))) continue;
     // Newton polish on the real axis (the complex iteration may stop at its rounding floor)
@@ -333,27 +280,28 @@ __device__ int e5_solve_one(const double (&y1)[5][2], const double (&y2)[5][2], 
     const double A0[3] = {horner_asc(kx, z), horner_asc(ky, z), horner_asc(k1, z)};
     const double A1[3] = {horner_asc(lx, z), horner_asc(ly, z), horner_asc(l1, z)};
     const double A2[3] = {horner_asc(mx, z), horner_asc(my, z), horner_asc(m1, z)};
-    double v[3][3];
-    const double *rows[3][2] = {{A0, A1}, {A0, A2}, {A1, A2}};
-    int bi = 0;
-    double bz = -1.0;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const double *a = rows[c][0], *b = rows[c][1];
-      v[c][0] = a[1] * b[2] - a[2] * b[1];
-      v[c][1] = a[2] * b[0] - a[0] * b[2];
-      v[c][2] = a[0] * b[1] - a[1] * b[0];
-      if (fabs(v[c][2]) > bz) {
-        bz = fabs(v[c][2]);
-        bi = c;
+    // the row cross product with the largest third component (first on ties), kept as it goes
+    double v0 = 0.0, v1 = 0.0, v2 = 0.0, bz = -1.0;
+    auto cand = [&](const double (&a)[3], const double (&b)[3]) {
+      const double c0 = a[1] * b[2] - a[2] * b[1];
+      const double c1 = a[2] * b[0] - a[0] * b[2];
+      const double c2 = a[0] * b[1] - a[1] * b[0];
+      if (fabs(c2) > bz) {
+        bz = fabs(c2);
+        v0 = c0;
+        v1 = c1;
+        v2 = c2;
       }
-    }
+    };
+    cand(A0, A1);
+    cand(A0, A2);
+    cand(A1, A2);
     if (!(bz > 0.0)) continue;
-    const double x = v[bi][0] / v[bi][2], y = v[bi][1] / v[bi][2];
+    const double x = v0 / v2, y = v1 / v2;
     double E[9], nn = 0.0;
 #pragma unroll
     for (int e = 0; e < 9; ++e) {
-      E[e] = fma(x, basis[0][e], fma(y, basis[1][e], fma(z, basis[2][e], basis[3][e])));
+      E[e] = fma(x, bas[e * ldb], fma(y, bas[(9 + e) * ldb], fma(z, bas[(18 + e) * ldb], bas[(27 + e) * ldb])));
       nn = fma(E[e], E[e], nn);
     }
     if (!(nn > 0.0) || !isfinite(nn)) continue;
@@ -376,6 +324,12 @@ struct E5Args {
   double *Fsoa;             // 9 x ld (may be null)
   int *nsol;                // per sample (may be null)
   int64_t ld;
+  // work between the three solve kernels (ldw >= S, sample-minor so each kernel's loads and
+  // stores coalesce over its lanes): the 10 x 20 system (200 x ldw), the null basis
+  // (36 x ldw), B's rows 4..9 (60 x ldw), Gauss-Jordan success (ldw)
+  double *Mg, *Bas, *Bg;
+  int *okg;
+  int64_t ldw;
 };
 
 __device__ __forceinline__ void norm_pt(const double (&K)[9], double u, double v, double &x,
@@ -385,7 +339,10 @@ __device__ __forceinline__ void norm_pt(const double (&K)[9], double u, double v
   y = fma(K[3], u, fma(K[4], v, K[5])) / w;
 }
 
-__global__ __launch_bounds__(64) void k_e5_solve(E5Args a) {
+// (A) lane per sample: the sample, its 5 x 9 constraint matrix, the null basis (to memory) and
+// the ten cubic constraints (to memory, row by row: the 10 x 20 system is 400 of the 512
+// registers a lane has, so it is never held by one lane)
+__global__ __launch_bounds__(64) void k_e5_build(E5Args a) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= a.S) return;
   int idx[5];
@@ -395,13 +352,102 @@ __global__ __launch_bounds__(64) void k_e5_solve(E5Args a) {
 #pragma unroll
     for (int i = 0; i < 5; ++i) idx[i] = 5 * s + i;
   }
-  double y1[5][2], y2[5][2];
+  double Q[5][9];
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
     const Pt p = a.pts[idx[i]];
-    norm_pt(a.Kin1, p.x1, p.y1, y1[i][0], y1[i][1]);
-    norm_pt(a.Kin2, p.x2, p.y2, y2[i][0], y2[i][1]);
+    double a0, a1, b0, b1;
+    norm_pt(a.Kin1, p.x1, p.y1, a0, a1);
+    norm_pt(a.Kin2, p.x2, p.y2, b0, b1);
+    Q[i][0] = a0 * b0;
+    Q[i][1] = a0 * b1;
+    Q[i][2] = a0;
+    Q[i][3] = a1 * b0;
+    Q[i][4] = a1 * b1;
+    Q[i][5] = a1;
+    Q[i][6] = b0;
+    Q[i][7] = b1;
+    Q[i][8] = 1.0;
   }
+  double basis[4][9];
+  e5_null_basis(Q, basis);
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int e = 0; e < 9; ++e) a.Bas[(9 * b + e) * a.ldw + s] = basis[b][e];
+  double *M = a.Mg + s;
+  const int64_t ldw = a.ldw;
+  e5_constraints(basis, [&](int r, const double (&row)[20]) {
+#pragma unroll
+    for (int q = 0; q < 20; ++q) M[(20 * r + q) * ldw] = row[q];
+  });
+}
+
+// (B) Gauss-Jordan on the first ten columns with partial pivoting, two samples per wave: lane j
+// (< 20) of a 32-lane half holds column j of its sample's system; the pivot column's lane finds
+// the pivot (the first largest |M[r][c]|, r >= c), and its column (the multipliers) and 1 /
+// pivot are broadcast by shuffles.  Every element sees the same operations as a one-lane
+// elimination: M[c][j] *= 1 / M[c][c], M[r][j] = fma(-M[r][c], M[c][j], M[r][j]).
+__global__ __launch_bounds__(64) void k_e5_gj(E5Args a) {
+  const int lane = threadIdx.x & 63, g = lane >> 5, j = lane & 31;
+  const int s = blockIdx.x * 2 + g;
+  const bool own = s < a.S && j < 20;
+  const int64_t ldw = a.ldw;
+  double col[10];
+#pragma unroll
+  for (int r = 0; r < 10; ++r) col[r] = own ? a.Mg[(20 * r + j) * ldw + s] : 0.0;
+  bool ok = true;
+#pragma unroll
+  for (int c = 0; c < 10; ++c) {
+    const int src = (g << 5) + c;
+    int piv = c;
+    double best = fabs(col[c]);
+#pragma unroll
+    for (int r = c + 1; r < 10; ++r) {
+      const double v = fabs(col[r]);
+      if (v > best) {
+        best = v;
+        piv = r;
+      }
+    }
+    piv = __shfl(piv, src);
+    best = __shfl(best, src);
+    ok = ok && best > 0.0;
+    // swap rows c and piv (a no-op on the reduced columns j < c, zero in both rows)
+    double pc = col[c];
+#pragma unroll
+    for (int r = c + 1; r < 10; ++r) {
+      const bool sw = r == piv;
+      const double x = col[r];
+      col[r] = sw ? pc : x;
+      pc = sw ? x : pc;
+    }
+    col[c] = pc;
+    const double inv = __shfl(1.0 / col[c], src);
+    double f[10];
+#pragma unroll
+    for (int r = 0; r < 10; ++r) f[r] = __shfl(col[r], src);
+    if (j > c) {
+      col[c] *= inv;
+#pragma unroll
+      for (int r = 0; r < 10; ++r)
+        if (r != c) col[r] = fma(-f[r], col[c], col[r]);
+    } else if (j == c) {
+#pragma unroll
+      for (int r = 0; r < 10; ++r) col[r] = r == c ? 1.0 : 0.0;
+    }
+  }
+  if (own && j >= 10)
+#pragma unroll
+    for (int r = 4; r < 10; ++r) a.Bg[(10 * (r - 4) + (j - 10)) * ldw + s] = col[r];
+  if (own && j == 0) a.okg[s] = ok ? 1 : 0;
+}
+
+// (C) lane per sample: the degree-10 polynomial of B's rows 4..9, its real roots, the solutions
+// (E from the null basis in memory, F = M1 E M2), NaN slots past the sample's count
+__global__ __launch_bounds__(64) void k_e5_roots(E5Args a) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= a.S) return;
   // one solution slot: E, and F = M1 E M2 (K1^-T E K2^-1) when asked for
   auto store = [&](int j, const double (&E)[9]) {
     const int64_t slot = static_cast<int64_t>(s) * kE5Sol + j;
@@ -422,7 +468,15 @@ __global__ __launch_bounds__(64) void k_e5_solve(E5Args a) {
               fma(a.M1[3 * r], T[c], fma(a.M1[3 * r + 1], T[3 + c], a.M1[3 * r + 2] * T[6 + c]));
     }
   };
-  const int ns = e5_solve_one(y1, y2, store);
+  int ns = 0;
+  if (a.okg[s]) {
+    double Bm[6][10];
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+      for (int q = 0; q < 10; ++q) Bm[r][q] = a.Bg[(10 * r + q) * a.ldw + s];
+    ns = e5_solve_tail(Bm, a.Bas + s, a.ldw, store);
+  }
   if (a.nsol) a.nsol[s] = ns;
   // NaN past the sample's solutions: those slots count 0
   const double qn = __builtin_nan("");
@@ -595,6 +649,28 @@ using rs::hip_fail;
 
 static size_t e5_align(size_t b) { return (b + 255) / 256 * 256; }
 
+// bytes of the three solve kernels' work buffers for S samples
+static size_t e5_work_bytes(int64_t S) {
+  return e5_align(sizeof(double) * 296 * static_cast<size_t>(S)) + e5_align(sizeof(int) * S);
+}
+
+// the solve (k_e5_build, k_e5_gj, k_e5_roots) into a.Esoa / a.Fsoa, work buffers from `work`
+static int launch_e5_solve(rsd::E5Args &a, char *work, hipStream_t s) {
+  const int64_t S = a.S;
+  a.ldw = S;
+  a.Mg = reinterpret_cast<double *>(work);
+  a.Bas = a.Mg + 200 * S;
+  a.Bg = a.Bas + 36 * S;
+  a.okg = reinterpret_cast<int *>(work + e5_align(sizeof(double) * 296 * static_cast<size_t>(S)));
+  hipLaunchKernelGGL(rsd::k_e5_build, dim3((S + 63) / 64), dim3(64), 0, s, a);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(rsd::k_e5_gj, dim3((S + 1) / 2), dim3(64), 0, s, a);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(rsd::k_e5_roots, dim3((S + 63) / 64), dim3(64), 0, s, a);
+  HIP_TRY(hipGetLastError());
+  return RS_OK;
+}
+
 static bool inv3(const double *K, double *Ki) {
   const double det = K[0] * (K[4] * K[8] - K[5] * K[7]) - K[1] * (K[3] * K[8] - K[5] * K[6]) +
                      K[2] * (K[3] * K[7] - K[4] * K[6]);
@@ -627,12 +703,13 @@ extern "C" int rs_e5_solve(rs_ctx *c, const double *y1, const double *y2, int64_
   }
   const size_t bp = e5_align(sizeof(rsd::Pt) * m), bE = e5_align(sizeof(double) * 9 * ld),
                bn = e5_align(sizeof(int) * S);
-  int st = rs::ensure_scratch(c, bp + bE + bn);
+  int st = rs::ensure_scratch(c, bp + bE + bn + e5_work_bytes(S));
   if (st) return st;
   char *base = static_cast<char *>(c->scratch);
   auto *dp = reinterpret_cast<rsd::Pt *>(base);
   auto *dE = reinterpret_cast<double *>(base + bp);
   auto *dn = reinterpret_cast<int *>(base + bp + bE);
+  char *work = base + bp + bE + bn;
   hipStream_t s = c->stream;
   HIP_TRY(hipMemcpyAsync(dp, hp.data(), sizeof(rsd::Pt) * m, hipMemcpyHostToDevice, s));
   rsd::E5Args a{};
@@ -648,8 +725,7 @@ extern "C" int rs_e5_solve(rs_ctx *c, const double *y1, const double *y2, int64_
   a.Esoa = dE;
   a.nsol = dn;
   a.ld = ld;
-  hipLaunchKernelGGL(rsd::k_e5_solve, dim3((S + 63) / 64), dim3(64), 0, s, a);
-  HIP_TRY(hipGetLastError());
+  if ((st = launch_e5_solve(a, work, s))) return st;
   std::vector<double> soa(static_cast<size_t>(9 * ld));
   HIP_TRY(hipMemcpyAsync(soa.data(), dE, sizeof(double) * 9 * ld, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(nsol, dn, sizeof(int) * S, hipMemcpyDeviceToHost, s));
@@ -680,7 +756,7 @@ extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64
   const size_t bE = e5_align(sizeof(double) * 9 * ld), bc = e5_align(sizeof(int) * ld);
   const size_t br = e5_align(sizeof(rsd::E5DevResult) + sizeof(int64_t) * n);
   const size_t bnorm = e5_align(sizeof(double) * ld);
-  int st = rs::ensure_scratch(c, 2 * bin + bp + 2 * bE + bc + br + bnorm + 256);
+  int st = rs::ensure_scratch(c, 2 * bin + bp + 2 * bE + bc + br + bnorm + 256 + e5_work_bytes(S));
   if (st) return st;
   char *ptr = static_cast<char *>(c->scratch);
   auto take = [&ptr](size_t b) {
@@ -697,6 +773,7 @@ extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64
   auto *dr = reinterpret_cast<rsd::E5DevResult *>(take(br));
   double *dnorm = reinterpret_cast<double *>(take(bnorm));
   int *dcmax = reinterpret_cast<int *>(take(256));
+  char *work = take(e5_work_bytes(S));
   hipStream_t s = c->stream;
   HIP_TRY(hipMemcpyAsync(d1, p1, sizeof(double) * 2 * n, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(d2, p2, sizeof(double) * 2 * n, hipMemcpyHostToDevice, s));
@@ -709,8 +786,7 @@ extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64
   a.Esoa = dE;
   a.Fsoa = dF;
   a.ld = ld;
-  hipLaunchKernelGGL(rsd::k_e5_solve, dim3((S + 63) / 64), dim3(64), 0, s, a);
-  HIP_TRY(hipGetLastError());
+  if ((st = launch_e5_solve(a, work, s))) return st;
   HIP_TRY(hipMemsetAsync(dc, 0, sizeof(int) * H, s));
   // chunking of k_f8_count: >= 8 units of work per SIMD, chunks of >= 64 points
   const int64_t groups = (H + 63) / 64;
