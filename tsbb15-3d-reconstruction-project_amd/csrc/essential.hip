@@ -509,38 +509,65 @@ __global__ __launch_bounds__(1024) void k_e5_max(const int *__restrict__ counts,
 
 // ||d||^2 of every slot with count c* (lane per slot, +inf elsewhere), reference-order d_i:
 // max(|x1^T F x2| / |l1|, |x1^T F x2| / |l2|) (lab3.fmatrix_residuals, fun.py:315).
-__global__ __launch_bounds__(256) void k_e5_norms(const Pt *__restrict__ pts, int n, int64_t H,
-                                                  const int *__restrict__ counts,
-                                                  const int *__restrict__ cmax,
-                                                  const double *__restrict__ Fsoa, int64_t ld,
-                                                  double *__restrict__ norms) {
-  const int64_t h = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (h >= H) return;
+// The slots with the largest count c* (the candidates), appended in any order: one ballot and
+// one atomic per wave.
+__global__ __launch_bounds__(256) void k_e5_cands(const int *__restrict__ counts, int64_t H,
+                                                  const int *__restrict__ cmax, int *__restrict__ cand,
+                                                  int *__restrict__ ncand) {
   const int c = *cmax;
-  if (c <= 0 || counts[h] != c) {
-    norms[h] = __builtin_inf();
-    return;
+  const int lane = threadIdx.x & 63;
+  for (int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x; b < H;
+       b += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t h = b + threadIdx.x;
+    const bool take = c > 0 && h < H && counts[h] == c;
+    const uint64_t bal = __ballot(take);
+    if (!bal) continue;
+    int base = 0;
+    if (lane == 0) base = atomicAdd(ncand, static_cast<int>(__popcll(bal)));
+    base = __shfl(base, 0);
+    if (take) cand[base + __popcll(bal & ((1ull << lane) - 1ull))] = static_cast<int>(h);
   }
-  double f[9];
-#pragma unroll
-  for (int q = 0; q < 9; ++q) f[q] = Fsoa[q * ld + h];
-  double ss = 0.0;
-  for (int i = 0; i < n; ++i) {
-    const Pt p = pts[i];
-    const double l10 = fma(f[0], p.x2, fma(f[1], p.y2, f[2]));
-    const double l11 = fma(f[3], p.x2, fma(f[4], p.y2, f[5]));
-    const double l12 = fma(f[6], p.x2, fma(f[7], p.y2, f[8]));
-    const double l20 = fma(f[0], p.x1, fma(f[3], p.y1, f[6]));
-    const double l21 = fma(f[1], p.x1, fma(f[4], p.y1, f[7]));
-    const double e = fabs(fma(l10, p.x1, fma(l11, p.y1, l12)));
-    const double d = fmax(e / sqrt(fma(l10, l10, l11 * l11)), e / sqrt(fma(l20, l20, l21 * l21)));
-    ss = fma(d, d, ss);
-  }
-  norms[h] = ss == ss ? ss : __builtin_inf();
 }
 
-// The slot with count c* and the smallest norm (first on ties).
-__global__ __launch_bounds__(1024) void k_e5_select(const double *__restrict__ norms, int64_t H,
+// ||d||^2 of every candidate, d_i = max(|r1_i|, |r2_i|) over all points (the quantity the
+// reference's F loop compares on ties, fun.py:317-325): a wave per candidate, the points over
+// the lanes, partial sums combined by a fixed butterfly (deterministic).  (A lane per slot
+// summed 2 000 points serially: 476 us of the C2 E-RANSAC run.)
+__global__ __launch_bounds__(256) void k_e5_norms(const Pt *__restrict__ pts, int n,
+                                                  const int *__restrict__ cand,
+                                                  const int *__restrict__ ncand,
+                                                  const double *__restrict__ Fsoa, int64_t ld,
+                                                  double *__restrict__ norms) {
+  const int lane = threadIdx.x & 63;
+  const int nw = static_cast<int>(gridDim.x) * (blockDim.x >> 6);
+  const int nc = *ncand;
+  for (int k = static_cast<int>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6); k < nc; k += nw) {
+    const int64_t h = cand[k];
+    double f[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) f[q] = Fsoa[q * ld + h];
+    double ss = 0.0;
+    for (int i = lane; i < n; i += 64) {
+      const Pt p = pts[i];
+      const double l10 = fma(f[0], p.x2, fma(f[1], p.y2, f[2]));
+      const double l11 = fma(f[3], p.x2, fma(f[4], p.y2, f[5]));
+      const double l12 = fma(f[6], p.x2, fma(f[7], p.y2, f[8]));
+      const double l20 = fma(f[0], p.x1, fma(f[3], p.y1, f[6]));
+      const double l21 = fma(f[1], p.x1, fma(f[4], p.y1, f[7]));
+      const double e = fabs(fma(l10, p.x1, fma(l11, p.y1, l12)));
+      const double d = fmax(e / sqrt(fma(l10, l10, l11 * l11)), e / sqrt(fma(l20, l20, l21 * l21)));
+      ss = fma(d, d, ss);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+    if (lane == 0) norms[k] = ss == ss ? ss : __builtin_inf();
+  }
+}
+
+// the winner among the candidates: the smallest norm, the smallest slot on equal norms
+__global__ __launch_bounds__(1024) void k_e5_select(const double *__restrict__ norms,
+                                                    const int *__restrict__ cand,
+                                                    const int *__restrict__ ncand,
                                                     const int *__restrict__ cmax,
                                                     const double *__restrict__ Esoa,
                                                     const double *__restrict__ Fsoa, int64_t ld,
@@ -548,11 +575,13 @@ __global__ __launch_bounds__(1024) void k_e5_select(const double *__restrict__ n
   __shared__ double sv[16];
   __shared__ int64_t si[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nc = *ncand;
   double bv = __builtin_inf();
   int64_t bi = INT64_MAX;
-  for (int64_t i = tid; i < H; i += 1024) {
-    const double v = norms[i];
-    if (v < bv) {
+  for (int k = tid; k < nc; k += 1024) {
+    const double v = norms[k];
+    const int64_t i = cand[k];
+    if (v < bv || (v == bv && i < bi)) {
       bv = v;
       bi = i;
     }
@@ -588,7 +617,6 @@ __global__ __launch_bounds__(1024) void k_e5_select(const double *__restrict__ n
   }
 }
 
-// The winner's consensus set, in point order (the k_f8_count test in pixels).
 __global__ __launch_bounds__(1024) void k_e5_inliers(const Pt *__restrict__ pts, int n,
                                                      double thr2, E5DevResult *res) {
   __shared__ int woff[16];
@@ -756,7 +784,8 @@ extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64
   const size_t bE = e5_align(sizeof(double) * 9 * ld), bc = e5_align(sizeof(int) * ld);
   const size_t br = e5_align(sizeof(rsd::E5DevResult) + sizeof(int64_t) * n);
   const size_t bnorm = e5_align(sizeof(double) * ld);
-  int st = rs::ensure_scratch(c, 2 * bin + bp + 2 * bE + bc + br + bnorm + 256 + e5_work_bytes(S));
+  int st = rs::ensure_scratch(c, 2 * bin + bp + 2 * bE + bc + br + bnorm + 256 +
+                                     e5_align(sizeof(int) * ld) + e5_work_bytes(S));
   if (st) return st;
   char *ptr = static_cast<char *>(c->scratch);
   auto take = [&ptr](size_t b) {
@@ -772,7 +801,8 @@ extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64
   int *dc = reinterpret_cast<int *>(take(bc));
   auto *dr = reinterpret_cast<rsd::E5DevResult *>(take(br));
   double *dnorm = reinterpret_cast<double *>(take(bnorm));
-  int *dcmax = reinterpret_cast<int *>(take(256));
+  int *dcmax = reinterpret_cast<int *>(take(256));  // c* (int 0), candidate count (int 1)
+  int *dcand = reinterpret_cast<int *>(take(e5_align(sizeof(int) * ld)));
   char *work = take(e5_work_bytes(S));
   hipStream_t s = c->stream;
   HIP_TRY(hipMemcpyAsync(d1, p1, sizeof(double) * 2 * n, hipMemcpyHostToDevice, s));
@@ -794,11 +824,14 @@ extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64
   const int chunk = static_cast<int>((n + nch - 1) / nch);
   HIP_TRY(rsd::launch_f8_count(dp, static_cast<int>(n), static_cast<int>(H), dF, ld, chunk,
                                thresh * thresh, dc, s));
+  HIP_TRY(hipMemsetAsync(dcmax + 1, 0, sizeof(int), s));
   hipLaunchKernelGGL(rsd::k_e5_max, dim3(1), dim3(1024), 0, s, dc, H, dcmax);
-  hipLaunchKernelGGL(rsd::k_e5_norms, dim3((H + 255) / 256), dim3(256), 0, s, dp,
-                     static_cast<int>(n), H, dc, dcmax, dF, ld, dnorm);
-  hipLaunchKernelGGL(rsd::k_e5_select, dim3(1), dim3(1024), 0, s, dnorm, H, dcmax, dE, dF, ld,
-                     dr);
+  hipLaunchKernelGGL(rsd::k_e5_cands, dim3(static_cast<unsigned>(std::min<int64_t>((H + 255) / 256, 1024))),
+                     dim3(256), 0, s, dc, H, dcmax, dcand, dcmax + 1);
+  hipLaunchKernelGGL(rsd::k_e5_norms, dim3(256), dim3(256), 0, s, dp, static_cast<int>(n), dcand,
+                     dcmax + 1, dF, ld, dnorm);
+  hipLaunchKernelGGL(rsd::k_e5_select, dim3(1), dim3(1024), 0, s, dnorm, dcand, dcmax + 1, dcmax,
+                     dE, dF, ld, dr);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(rsd::k_e5_inliers, dim3(1), dim3(1024), 0, s, dp, static_cast<int>(n),
                      thresh * thresh, dr);
