@@ -339,9 +339,10 @@ def extras(ctx, rank, world, dist, comm):
                                "consensus": r.count,
                                "round2_value": E5_ROUND2[0], "round2_source": E5_ROUND2[1],
                                "note": "k_e5_build (null basis, ten cubics) + k_e5_gj (Gauss-"
-                                       "Jordan, 32 lanes per sample) + k_e5_roots (all real "
-                                       "roots, stored as found) + k_f8_count over 10 slots per "
-                                       "sample + selection, N = 2000"}
+                                       "Jordan, 32 lanes per sample) + k_e5_roots (16 lanes per "
+                                       "sample, a lane per root) + k_e5_pack (the real "
+                                       "solutions' slots) + k_f8_count over those + selection, "
+                                       "N = 2000"}
     except Exception as e:  # noqa: BLE001
         out["e5_ransac_c2"] = {"error": repr(e)}
     # ---- per-view table steps (tables.py:116-175, 260-380) at the reference's noisy sizes ----

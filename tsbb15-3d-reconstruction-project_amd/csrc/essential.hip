@@ -15,17 +15,19 @@
 //                     monomials (Nister's order, kT3), to memory row by row;
 //                k_e5_gj (32 lanes per sample, a column per lane): Gauss-Jordan with partial
 //                  pivoting on the first ten columns -> [I | B];
-//                k_e5_roots (lane per sample)
+//                k_e5_roots (16 lanes per sample, lane r owns root r)
 //                  3. k = row(x^2 z) - z row(x^2), l = row(y^2 z) - z row(y^2),
 //                     m = row(x y z) - z row(x y): linear in (x, y, 1), polynomial in z;
 //                     det [k; l; m](z) has degree 10;
-//                  4. its roots by Aberth-Ehrlich (twoview_math.h aberth_roots<10>), real ones
-//                     polished by Newton; (x, y, 1) = the null vector of [k; l; m](z) (the
-//                     row cross product with the largest third component);
+//                  4. its roots by Aberth-Ehrlich (the start points and freeze tests of
+//                     twoview_math.h aberth_roots, the other roots read across the row by DPP),
+//                     real ones polished by Newton; (x, y, 1) = the null vector of
+//                     [k; l; m](z) (the row cross product with the largest third component);
 //                writes up to 10 unit-norm E per sample, their F = K1^-T E K2^-1 (NaN slots
 //                past the sample's count, so they count 0).  (One lane per sample for all of it
 //                held the 10 x 20 system in 256 VGPRs + 256 AGPRs + 752 B of scratch.)
-//   counting     k_f8_count (f8_kernels.hip) over the S x 10 slots: the reference's residual
+//   counting     k_e5_pack: a dense list of the real solutions' slots; k_f8_count
+//                (f8_kernels.hip) over the models it names: the reference's residual
 //                test d = max(|r1|, |r2|) < thresh of lab3.fmatrix_residuals in pixels.
 //   k_e5_select  c* = the largest count; among the slots with c* the smallest residual norm
 //                ||d||, d_i = max(|r1_i|, |r2_i|) over all points (the quantity the
@@ -222,96 +224,122 @@ __device__ __forceinline__ double horner_asc(const double (&p)[N], double z) {
   return v;
 }
 
-// All real solutions of one sample from its reduced system (B rows 4..9) and its null basis
-// (read back from memory per solution), each handed to emit(slot, E) as it is found (E
-// row-major, unit norm); returns their number (<= 10).
-template <class Emit>
-__device__ int e5_solve_tail(const double (&Bm)[6][10], const double *bas, int64_t ldb, Emit emit) {
+// The three rows k, l, m of one sample (linear in (x, y, 1), polynomial in z) from B's rows
+// 4..9, and d(z) = det [k; l; m] (degree 10, ascending).
+struct E5Polys {
   double kx[4], ky[4], k1[5], lx[4], ly[4], l1[5], mx[4], my[4], m1[5];
-  e5_row(Bm, 4, 5, kx, ky, k1);
-  e5_row(Bm, 6, 7, lx, ly, l1);
-  e5_row(Bm, 8, 9, mx, my, m1);
+};
+
+__device__ __forceinline__ void e5_polys(const double (&Bm)[6][10], E5Polys &P, double (&d)[11]) {
+  e5_row(Bm, 4, 5, P.kx, P.ky, P.k1);
+  e5_row(Bm, 6, 7, P.lx, P.ly, P.l1);
+  e5_row(Bm, 8, 9, P.mx, P.my, P.m1);
   // det [k; l; m] = kx (ly m1 - l1 my) - ky (lx m1 - l1 mx) + k1 (lx my - ly mx)
-  double t7a[8], t7b[8], t7[8], d[11], u[11];
-  polymul(ly, m1, t7a);
-  polymul(l1, my, t7b);
+  double t7a[8], t7b[8], t7[8], u[11];
+  polymul(P.ly, P.m1, t7a);
+  polymul(P.l1, P.my, t7b);
 #pragma unroll
   for (int i = 0; i < 8; ++i) t7[i] = t7a[i] - t7b[i];
-  polymul(kx, t7, d);
-  polymul(lx, m1, t7a);
-  polymul(l1, mx, t7b);
+  polymul(P.kx, t7, d);
+  polymul(P.lx, P.m1, t7a);
+  polymul(P.l1, P.mx, t7b);
 #pragma unroll
   for (int i = 0; i < 8; ++i) t7[i] = t7a[i] - t7b[i];
-  polymul(ky, t7, u);
+  polymul(P.ky, t7, u);
 #pragma unroll
   for (int i = 0; i < 11; ++i) d[i] -= u[i];
   double t6a[7], t6b[7], t6[7];
-  polymul(lx, my, t6a);
-  polymul(ly, mx, t6b);
+  polymul(P.lx, P.my, t6a);
+  polymul(P.ly, P.mx, t6b);
 #pragma unroll
   for (int i = 0; i < 7; ++i) t6[i] = t6a[i] - t6b[i];
-  polymul(k1, t6, u);
+  polymul(P.k1, t6, u);
 #pragma unroll
   for (int i = 0; i < 11; ++i) d[i] += u[i];
-  double g[11];  // descending for aberth_roots
-#pragma unroll
-  for (int i = 0; i < 11; ++i) g[i] = d[10 - i];
+}
+
+// The solution of one root z of d (Newton-polished on the real axis): (x, y, 1) = the row cross
+// product of [k; l; m](z) with the largest third component (first on ties), E = x X + y Y +
+// z Z + W from the null basis in memory, unit norm.  False when it degenerates.
+__device__ __forceinline__ bool e5_solution(const E5Polys &P, const double (&d)[11], double z,
+                                            const double *bas, int64_t ldb, double (&E)[9]) {
   double dp[10];  // derivative, ascending
 #pragma unroll
   for (int i = 0; i < 10; ++i) dp[i] = (i + 1) * d[i + 1];
-  double zr[10], zi[10];
-  int trailing = 0;
-  const int deg = aberth_roots<10>(g, zr, zi, trailing);
-  int ns = 0;
-  // (unrolled: every root index static, no array of roots addressed at run time)
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    if (r >= deg + trailing || ns >= kE5Sol) continue;
-    double z = r < deg ? zr[r] : 0.0;
-    if (r < deg && !(fabs(zi[r]) <= 1e-6 * fmax(1.0, fabs(z)))) continue;
-    // Newton polish on the real axis (the complex iteration may stop at its rounding floor)
-    for (int it = 0; it < 3; ++it) {
-      const double f = horner_asc(d, z), fp = horner_asc(dp, z);
-      if (!(fp != 0.0)) break;
-      const double step = f / fp;
-      if (!(fabs(step) <= 1e-3 * fmax(1.0, fabs(z)))) break;
-      z -= step;
-    }
-    const double A0[3] = {horner_asc(kx, z), horner_asc(ky, z), horner_asc(k1, z)};
-    const double A1[3] = {horner_asc(lx, z), horner_asc(ly, z), horner_asc(l1, z)};
-    const double A2[3] = {horner_asc(mx, z), horner_asc(my, z), horner_asc(m1, z)};
-    // the row cross product with the largest third component (first on ties), kept as it goes
-    double v0 = 0.0, v1 = 0.0, v2 = 0.0, bz = -1.0;
-    auto cand = [&](const double (&a)[3], const double (&b)[3]) {
-      const double c0 = a[1] * b[2] - a[2] * b[1];
-      const double c1 = a[2] * b[0] - a[0] * b[2];
-      const double c2 = a[0] * b[1] - a[1] * b[0];
-      if (fabs(c2) > bz) {
-        bz = fabs(c2);
-        v0 = c0;
-        v1 = c1;
-        v2 = c2;
-      }
-    };
-    cand(A0, A1);
-    cand(A0, A2);
-    cand(A1, A2);
-    if (!(bz > 0.0)) continue;
-    const double x = v0 / v2, y = v1 / v2;
-    double E[9], nn = 0.0;
-#pragma unroll
-    for (int e = 0; e < 9; ++e) {
-      E[e] = fma(x, bas[e * ldb], fma(y, bas[(9 + e) * ldb], fma(z, bas[(18 + e) * ldb], bas[(27 + e) * ldb])));
-      nn = fma(E[e], E[e], nn);
-    }
-    if (!(nn > 0.0) || !isfinite(nn)) continue;
-    const double in = 1.0 / sqrt(nn);
-#pragma unroll
-    for (int e = 0; e < 9; ++e) E[e] *= in;
-    emit(ns, E);
-    ++ns;
+  // Newton polish on the real axis (the complex iteration may stop at its rounding floor)
+  for (int it = 0; it < 3; ++it) {
+    const double f = horner_asc(d, z), fp = horner_asc(dp, z);
+    if (!(fp != 0.0)) break;
+    const double step = f / fp;
+    if (!(fabs(step) <= 1e-3 * fmax(1.0, fabs(z)))) break;
+    z -= step;
   }
-  return ns;
+  const double A0[3] = {horner_asc(P.kx, z), horner_asc(P.ky, z), horner_asc(P.k1, z)};
+  const double A1[3] = {horner_asc(P.lx, z), horner_asc(P.ly, z), horner_asc(P.l1, z)};
+  const double A2[3] = {horner_asc(P.mx, z), horner_asc(P.my, z), horner_asc(P.m1, z)};
+  double v0 = 0.0, v1 = 0.0, v2 = 0.0, bz = -1.0;
+  auto cand = [&](const double (&a)[3], const double (&b)[3]) {
+    const double c0 = a[1] * b[2] - a[2] * b[1];
+    const double c1 = a[2] * b[0] - a[0] * b[2];
+    const double c2 = a[0] * b[1] - a[1] * b[0];
+    if (fabs(c2) > bz) {
+      bz = fabs(c2);
+      v0 = c0;
+      v1 = c1;
+      v2 = c2;
+    }
+  };
+  cand(A0, A1);
+  cand(A0, A2);
+  cand(A1, A2);
+  if (!(bz > 0.0)) return false;
+  const double x = v0 / v2, y = v1 / v2;
+  double nn = 0.0;
+#pragma unroll
+  for (int e = 0; e < 9; ++e) {
+    E[e] = fma(x, bas[e * ldb], fma(y, bas[(9 + e) * ldb], fma(z, bas[(18 + e) * ldb], bas[(27 + e) * ldb])));
+    nn = fma(E[e], E[e], nn);
+  }
+  if (!(nn > 0.0) || !isfinite(nn)) return false;
+  const double in = 1.0 / sqrt(nn);
+#pragma unroll
+  for (int e = 0; e < 9; ++e) E[e] *= in;
+  return true;
+}
+
+// (x, y) of the 16-lane row neighbour k to the left (DPP row_ror:k; every lane of the row
+// must be active)
+template <int K>
+__device__ __forceinline__ void row_ror_pair(double xr, double xi, double &yr, double &yi) {
+  auto rot = [](double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const unsigned lo = __builtin_amdgcn_update_dpp(0u, static_cast<unsigned>(b), 0x120 + K, 0xf, 0xf, false);
+    const unsigned hi = __builtin_amdgcn_update_dpp(0u, static_cast<unsigned>(b >> 32), 0x120 + K, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, (static_cast<uint64_t>(hi) << 32) | lo);
+  };
+  yr = rot(xr);
+  yi = rot(xi);
+}
+
+// sum over the other 15 lanes of the row of 1 / (z - z_j); lanes without a root hold NaN, which
+// fails dd > 0 (as a coincident root does in aberth_roots)
+template <int K>
+__device__ __forceinline__ void aberth_sum(double xr, double xi, double &sr, double &si) {
+  if constexpr (K < 16) {
+    double yr, yi;
+    row_ror_pair<K>(xr, xi, yr, yi);
+    const double ur = xr - yr, ui = xi - yi;
+    const double dd = ur * ur + ui * ui;
+    if (dd > 0.0) {
+      // the sum only shapes the step (the fixed point is p(z) = 0): v_rcp_f64 and one
+      // Newton step instead of two IEEE divisions
+      const double r0 = __builtin_amdgcn_rcp(dd);
+      const double inv = r0 * fma(-dd, r0, 2.0);
+      sr = fma(ur, inv, sr);
+      si = fma(-ui, inv, si);
+    }
+    aberth_sum<K + 1>(xr, xi, sr, si);
+  }
 }
 
 struct E5Args {
@@ -443,45 +471,190 @@ __global__ __launch_bounds__(64) void k_e5_gj(E5Args a) {
   if (own && j == 0) a.okg[s] = ok ? 1 : 0;
 }
 
-// (C) lane per sample: the degree-10 polynomial of B's rows 4..9, its real roots, the solutions
-// (E from the null basis in memory, F = M1 E M2), NaN slots past the sample's count
-__global__ __launch_bounds__(64) void k_e5_roots(E5Args a) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= a.S) return;
-  // one solution slot: E, and F = M1 E M2 (K1^-T E K2^-1) when asked for
-  auto store = [&](int j, const double (&E)[9]) {
+// (C) 16 lanes per sample (a DPP row), lane r owns root r: the degree-10 polynomial of B's rows
+// 4..9 (every lane of the row), its roots by Aberth-Ehrlich with the Newton-polygon start points
+// of twoview_math.h aberth_roots (same start points, Horner steps and freeze tests, but every
+// root of a sweep updated from the previous sweep's roots, read across the row by DPP), then
+// lane r's real root to its solution (E from the null basis in memory, F = M1 E M2).  A sample's
+// solutions take slots in root order; NaN in the slots past its count.  (A lane per sample:
+// 346 us at C2 -- 313 waves for 1 024 SIMDs, each a serial chain of 10 roots.)
+#ifndef RSD_E5_ROOTS_WAVES
+#define RSD_E5_ROOTS_WAVES 2  // minimum waves per SIMD (157 VGPRs: 3; a cap at 4 spills and is slower) (A/B builds: tools/build_ab.sh)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSD_E5_ROOTS_WAVES))) void k_e5_roots(E5Args a) {
+  const int r = threadIdx.x & 15;
+  const int s = blockIdx.x * (blockDim.x >> 4) + (threadIdx.x >> 4);
+  const bool live = s < a.S;  // the whole row runs the sweeps (DPP), dead rows are masked out
+  const int sc = live ? s : a.S - 1;
+  const bool ok = live && a.okg[sc];
+  double Bm[6][10];
+  const double *bg = a.Bg + sc;
+#pragma unroll
+  for (int rr = 0; rr < 6; ++rr)
+#pragma unroll
+    for (int q = 0; q < 10; ++q) Bm[rr][q] = bg[(10 * rr + q) * a.ldw];
+  double d[11];
+  {
+    E5Polys P;
+    e5_polys(Bm, P, d);
+  }
+  // monic descending coefficients padded to degree 10: zero roots (trailing zeros of the
+  // ascending d) shifted out, leading zeros kept (they add exact zeros in Horner)
+  double g[11];
+#pragma unroll
+  for (int i = 0; i < 11; ++i) g[i] = ok ? d[10 - i] : 0.0;
+  int trailing = 0;
+#pragma unroll
+  for (int i = 10; i >= 0; --i)
+    if (g[i] == 0.0 && trailing == 10 - i) ++trailing;
+  bool any = false;
+#pragma unroll
+  for (int i = 0; i < 11; ++i) any = any || g[i] != 0.0;
+  if (!any) trailing = 0;
+  for (int t = 0; t < trailing; ++t) {
+#pragma unroll
+    for (int i = 10; i > 0; --i) g[i] = g[i - 1];
+    g[0] = 0.0;
+  }
+  double lead = 0.0;
+  int lo = 11;
+#pragma unroll
+  for (int i = 10; i >= 0; --i)
+    if (g[i] != 0.0) {
+      lead = g[i];
+      lo = i;
+    }
+  const int deg = any ? 10 - lo : 0;
+  double am[11];
+#pragma unroll
+  for (int i = 0; i < 11; ++i) am[i] = any ? g[i] / lead : 0.0;
+  // start point of root r: edge e of the Newton polygon (upper hull of (k, log |b_k|), b_k =
+  // am[10 - k]) with m = k2 - k1 points on |z| = (|b_k1| / |b_k2|)^(1/m)
+  double zr = __builtin_nan(""), zi = __builtin_nan("");
+  if (r < deg) {
+    double lg[11];
+#pragma unroll
+    for (int k = 0; k < 11; ++k) {
+      const double v = fabs(am[10 - k]);
+      lg[k] = v > 0.0 ? log(v) : -1.0e300;
+    }
+    int hull[11], nh = 0;
+    hull[nh++] = 0;
+    for (int k = 1; k <= deg; ++k) {
+      if (lg[k] == -1.0e300) continue;
+      while (nh >= 2) {
+        const int k1 = hull[nh - 2], k2 = hull[nh - 1];
+        if ((lg[k2] - lg[k1]) * (k - k1) <= (lg[k] - lg[k1]) * (k2 - k1))
+          --nh;
+        else
+          break;
+      }
+      hull[nh++] = k;
+    }
+    int q = 0;
+    for (int e = 0; e + 1 < nh; ++e) {
+      const int m = hull[e + 1] - hull[e];
+      if (r < q + m) {
+        const double rad = exp((lg[hull[e]] - lg[hull[e + 1]]) / m);
+        const double ang = 6.283185307179586 * (r - q) / m + 6.283185307179586 * e / deg + 0.4;
+        zr = rad * cos(ang);
+        zi = rad * sin(ang);
+        break;
+      }
+      q += m;
+    }
+  }
+  bool conv = !(r < deg);
+  for (int it = 0; it < 100; ++it) {
+    if (!__ballot(!conv)) break;  // wave-uniform: every row keeps sweeping while one root moves
+    double sr = 0.0, si = 0.0;  // sum_{j != r} 1 / (z_r - z_j), the previous sweep's z_j
+    aberth_sum<1>(zr, zi, sr, si);
+    if (!conv) {
+      const double xr = zr, xi = zi;
+      const double az = sqrt(xr * xr + xi * xi);
+      double pr = 0.0, pi = 0.0, dr = 0.0, di = 0.0, S = 0.0;
+#pragma unroll
+      for (int j = 0; j < 11; ++j) {
+        const double ndr = dr * xr - di * xi + pr, ndi = dr * xi + di * xr + pi;
+        dr = ndr;
+        di = ndi;
+        const double npr = pr * xr - pi * xi + am[j], npi = pr * xi + pi * xr;
+        pr = npr;
+        pi = npi;
+        S = S * az + fabs(am[j]);
+      }
+      if (sqrt(pr * pr + pi * pi) <= 8.0 * 2.220446049250313e-16 * S) {
+        conv = true;
+      } else {
+        double rr_, ri_;  // p / p'
+        const double den = dr * dr + di * di;
+        if (den == 0.0) {
+          rr_ = pr;
+          ri_ = pi;
+        } else {
+          rr_ = (pr * dr + pi * di) / den;
+          ri_ = (pi * dr - pr * di) / den;
+        }
+        const double qr = 1.0 - (rr_ * sr - ri_ * si), qi = -(rr_ * si + ri_ * sr);
+        const double qd = qr * qr + qi * qi;
+        double wr = rr_, wi = ri_;
+        if (qd != 0.0) {
+          wr = (rr_ * qr + ri_ * qi) / qd;
+          wi = (ri_ * qr - rr_ * qi) / qd;
+        }
+        zr = xr - wr;
+        zi = xi - wi;
+        if (fabs(wr) + fabs(wi) <= 2.0 * 2.220446049250313e-16 * (fabs(zr) + fabs(zi))) conv = true;
+      }
+    }
+  }
+  // lane r's solution: real iterated roots (|Im| <= 1e-6 max(1, |Re|)) and the zero roots
+  double E[9];
+  bool valid = false;
+  if (ok && r < deg + trailing && (r >= deg || fabs(zi) <= 1e-6 * fmax(1.0, fabs(zr)))) {
+    // the row polynomials again, from memory (not kept live through the sweeps)
+    const double *bg2 = bg;
+    asm volatile("" : "+v"(bg2));
+#pragma unroll
+    for (int rr = 0; rr < 6; ++rr)
+#pragma unroll
+      for (int q = 0; q < 10; ++q) Bm[rr][q] = bg2[(10 * rr + q) * a.ldw];
+    E5Polys P;
+    double d2[11];
+    e5_polys(Bm, P, d2);
+    valid = e5_solution(P, d2, r < deg ? zr : 0.0, a.Bas + sc, a.ldw, E);
+  }
+  const uint64_t row = 0xffffull << (threadIdx.x & 48);
+  const uint64_t vb = __ballot(valid) & row;
+  const int ns = __popcll(vb);
+  const int lane = threadIdx.x & 63;
+  if (!live) return;
+  if (r == 0 && a.nsol) a.nsol[s] = ns;
+  auto store = [&](int j, const double (&V)[9]) {
     const int64_t slot = static_cast<int64_t>(s) * kE5Sol + j;
 #pragma unroll
-    for (int e = 0; e < 9; ++e) a.Esoa[e * a.ld + slot] = E[e];
+    for (int e = 0; e < 9; ++e) a.Esoa[e * a.ld + slot] = V[e];
     if (a.Fsoa) {
       double T[9];  // E M2
 #pragma unroll
-      for (int r = 0; r < 3; ++r)
+      for (int rr = 0; rr < 3; ++rr)
 #pragma unroll
         for (int c = 0; c < 3; ++c)
-          T[3 * r + c] = fma(E[3 * r], a.M2[c], fma(E[3 * r + 1], a.M2[3 + c], E[3 * r + 2] * a.M2[6 + c]));
+          T[3 * rr + c] = fma(V[3 * rr], a.M2[c], fma(V[3 * rr + 1], a.M2[3 + c], V[3 * rr + 2] * a.M2[6 + c]));
 #pragma unroll
-      for (int r = 0; r < 3; ++r)
+      for (int rr = 0; rr < 3; ++rr)
 #pragma unroll
         for (int c = 0; c < 3; ++c)
-          a.Fsoa[(3 * r + c) * a.ld + slot] =
-              fma(a.M1[3 * r], T[c], fma(a.M1[3 * r + 1], T[3 + c], a.M1[3 * r + 2] * T[6 + c]));
+          a.Fsoa[(3 * rr + c) * a.ld + slot] =
+              fma(a.M1[3 * rr], T[c], fma(a.M1[3 * rr + 1], T[3 + c], a.M1[3 * rr + 2] * T[6 + c]));
     }
   };
-  int ns = 0;
-  if (a.okg[s]) {
-    double Bm[6][10];
-#pragma unroll
-    for (int r = 0; r < 6; ++r)
-#pragma unroll
-      for (int q = 0; q < 10; ++q) Bm[r][q] = a.Bg[(10 * r + q) * a.ldw + s];
-    ns = e5_solve_tail(Bm, a.Bas + s, a.ldw, store);
+  if (valid) store(__popcll(vb & ((1ull << lane) - 1ull)), E);  // slots in root order
+  if (r >= ns && r < kE5Sol) {  // NaN past the sample's solutions: those slots count 0
+    const double qn = __builtin_nan("");
+    const double Enan[9] = {qn, qn, qn, qn, qn, qn, qn, qn, qn};
+    store(r, Enan);
   }
-  if (a.nsol) a.nsol[s] = ns;
-  // NaN past the sample's solutions: those slots count 0
-  const double qn = __builtin_nan("");
-  const double Enan[9] = {qn, qn, qn, qn, qn, qn, qn, qn, qn};
-  for (int j = ns; j < kE5Sol; ++j) store(j, Enan);
 }
 
 struct E5DevResult {
@@ -491,30 +664,72 @@ struct E5DevResult {
 };
 
 // c* = max count (one workgroup; strict ">" against 0: no consensus, no winner).
-__global__ __launch_bounds__(1024) void k_e5_max(const int *__restrict__ counts, int64_t H,
-                                                 int *cmax) {
-  __shared__ int sm[16];
+__global__ __launch_bounds__(256) void k_e5_max(const int *__restrict__ counts, int64_t H,
+                                                const int *__restrict__ hc, int *cmax) {
+  __shared__ int sm[4];
   const int tid = threadIdx.x;
+  H = hc ? min<int64_t>(H, *hc) : H;
   int bm = 0;
-  for (int64_t i = tid; i < H; i += 1024) bm = max(bm, counts[i]);
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + tid; i < H;
+       i += static_cast<int64_t>(gridDim.x) * 256)
+    bm = max(bm, counts[i]);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) bm = max(bm, __shfl_xor(bm, o));
   if ((tid & 63) == 0) sm[tid >> 6] = bm;
   __syncthreads();
-  if (tid == 0) {
-    for (int q = 1; q < 16; ++q) bm = max(bm, sm[q]);
-    *cmax = bm;
-  }
+  if (tid == 0) atomicMax(cmax, max(max(sm[0], sm[1]), max(sm[2], sm[3])));  // *cmax zeroed first
 }
 
-// ||d||^2 of every slot with count c* (lane per slot, +inf elsewhere), reference-order d_i:
-// max(|x1^T F x2| / |l1|, |x1^T F x2| / |l2|) (lab3.fmatrix_residuals, fun.py:315).
+// Counting only the real solutions: the map dense index -> slot of the real ones (*hc of
+// them), so the counting and the tie-break read F through it.  A workgroup per 256 samples:
+// the solutions of all earlier samples (int4 loads, a reduction; no device-wide scan pass),
+// its samples' offsets by a block scan.  The dense order keeps the slot order, so "the smallest
+// slot on equal norms" is "the smallest dense index".
+constexpr int kPackSamples = 256;
+__global__ __launch_bounds__(kPackSamples) void k_e5_pack(const int *__restrict__ nsol, int S,
+                                                          int *__restrict__ slot_of,
+                                                          int *__restrict__ hc) {
+  __shared__ int sw[kPackSamples / 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b0 = blockIdx.x * kPackSamples;  // a multiple of 4: int4 loads below b0
+  int pre = 0;
+#pragma unroll 4
+  for (int k = 4 * tid; k < b0; k += 4 * kPackSamples) {
+    const int4 q = *reinterpret_cast<const int4 *>(nsol + k);
+    pre += (q.x + q.y) + (q.z + q.w);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
+  if (lane == 0) sw[w] = pre;
+  __syncthreads();
+  int base = 0;
+#pragma unroll
+  for (int q = 0; q < kPackSamples / 64; ++q) base += sw[q];
+  __syncthreads();
+  const int sidx = b0 + tid;
+  const int v = sidx < S ? nsol[sidx] : 0;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sw[w] = x;
+  __syncthreads();
+  for (int q = 0; q < w; ++q) base += sw[q];
+  const int o = base + x - v;
+  for (int j = 0; j < v; ++j) slot_of[o + j] = sidx * kE5Sol + j;
+  if (blockIdx.x == gridDim.x - 1 && tid == kPackSamples - 1) *hc = base + x;
+}
+
 // The slots with the largest count c* (the candidates), appended in any order: one ballot and
 // one atomic per wave.
 __global__ __launch_bounds__(256) void k_e5_cands(const int *__restrict__ counts, int64_t H,
+                                                  const int *__restrict__ hc,
                                                   const int *__restrict__ cmax, int *__restrict__ cand,
                                                   int *__restrict__ ncand) {
   const int c = *cmax;
+  H = hc ? min<int64_t>(H, *hc) : H;
   const int lane = threadIdx.x & 63;
   for (int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x; b < H;
        b += static_cast<int64_t>(gridDim.x) * blockDim.x) {
@@ -536,13 +751,14 @@ __global__ __launch_bounds__(256) void k_e5_cands(const int *__restrict__ counts
 __global__ __launch_bounds__(256) void k_e5_norms(const Pt *__restrict__ pts, int n,
                                                   const int *__restrict__ cand,
                                                   const int *__restrict__ ncand,
+                                                  const int *__restrict__ slot_of,
                                                   const double *__restrict__ Fsoa, int64_t ld,
                                                   double *__restrict__ norms) {
   const int lane = threadIdx.x & 63;
   const int nw = static_cast<int>(gridDim.x) * (blockDim.x >> 6);
   const int nc = *ncand;
   for (int k = static_cast<int>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6); k < nc; k += nw) {
-    const int64_t h = cand[k];
+    const int64_t h = slot_of[cand[k]];  // dense index -> slot
     double f[9];
 #pragma unroll
     for (int q = 0; q < 9; ++q) f[q] = Fsoa[q * ld + h];
@@ -569,6 +785,7 @@ __global__ __launch_bounds__(1024) void k_e5_select(const double *__restrict__ n
                                                     const int *__restrict__ cand,
                                                     const int *__restrict__ ncand,
                                                     const int *__restrict__ cmax,
+                                                    const int *__restrict__ slot_of,
                                                     const double *__restrict__ Esoa,
                                                     const double *__restrict__ Fsoa, int64_t ld,
                                                     E5DevResult *res) {
@@ -608,11 +825,12 @@ __global__ __launch_bounds__(1024) void k_e5_select(const double *__restrict__ n
       }
     const int c = *cmax;
     const bool ok = c > 0 && bi != INT64_MAX;
-    res->best_slot = ok ? bi : -1;
+    const int64_t slot = ok ? (slot_of ? slot_of[bi] : bi) : -1;  // dense index -> slot
+    res->best_slot = slot;
     res->best_count = ok ? c : 0;
     for (int q = 0; q < 9; ++q) {
-      res->E[q] = ok ? Esoa[q * ld + bi] : 0.0;
-      res->F[q] = ok ? Fsoa[q * ld + bi] : 0.0;
+      res->E[q] = ok ? Esoa[q * ld + slot] : 0.0;
+      res->F[q] = ok ? Fsoa[q * ld + slot] : 0.0;
     }
   }
 }
@@ -694,7 +912,7 @@ static int launch_e5_solve(rsd::E5Args &a, char *work, hipStream_t s) {
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(rsd::k_e5_gj, dim3((S + 1) / 2), dim3(64), 0, s, a);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(rsd::k_e5_roots, dim3((S + 63) / 64), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(rsd::k_e5_roots, dim3((S + 15) / 16), dim3(256), 0, s, a);
   HIP_TRY(hipGetLastError());
   return RS_OK;
 }
@@ -785,7 +1003,8 @@ extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64
   const size_t br = e5_align(sizeof(rsd::E5DevResult) + sizeof(int64_t) * n);
   const size_t bnorm = e5_align(sizeof(double) * ld);
   int st = rs::ensure_scratch(c, 2 * bin + bp + 2 * bE + bc + br + bnorm + 256 +
-                                     e5_align(sizeof(int) * ld) + e5_work_bytes(S));
+                                     2 * e5_align(sizeof(int) * ld) + e5_align(sizeof(int) * S) +
+                                     e5_work_bytes(S));
   if (st) return st;
   char *ptr = static_cast<char *>(c->scratch);
   auto take = [&ptr](size_t b) {
@@ -801,8 +1020,10 @@ extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64
   int *dc = reinterpret_cast<int *>(take(bc));
   auto *dr = reinterpret_cast<rsd::E5DevResult *>(take(br));
   double *dnorm = reinterpret_cast<double *>(take(bnorm));
-  int *dcmax = reinterpret_cast<int *>(take(256));  // c* (int 0), candidate count (int 1)
+  int *dcmax = reinterpret_cast<int *>(take(256));  // c* (0), candidates (1), real solutions (2)
   int *dcand = reinterpret_cast<int *>(take(e5_align(sizeof(int) * ld)));
+  int *dnsol = reinterpret_cast<int *>(take(e5_align(sizeof(int) * S)));
+  int *dslot = reinterpret_cast<int *>(take(e5_align(sizeof(int) * ld)));
   char *work = take(e5_work_bytes(S));
   hipStream_t s = c->stream;
   HIP_TRY(hipMemcpyAsync(d1, p1, sizeof(double) * 2 * n, hipMemcpyHostToDevice, s));
@@ -815,23 +1036,29 @@ extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64
   a.seed = seed;
   a.Esoa = dE;
   a.Fsoa = dF;
+  a.nsol = dnsol;
   a.ld = ld;
   if ((st = launch_e5_solve(a, work, s))) return st;
+  // only the real solutions are counted: the map dslot (dense index -> slot, *hc entries)
+  hipLaunchKernelGGL(rsd::k_e5_pack, dim3(static_cast<unsigned>((S + rsd::kPackSamples - 1) / rsd::kPackSamples)),
+                     dim3(rsd::kPackSamples), 0, s, dnsol, static_cast<int>(S), dslot, dcmax + 2);
   HIP_TRY(hipMemsetAsync(dc, 0, sizeof(int) * H, s));
-  // chunking of k_f8_count: >= 8 units of work per SIMD, chunks of >= 64 points
-  const int64_t groups = (H + 63) / 64;
+  // chunking of k_f8_count: >= 8 units of work per SIMD, chunks of >= 64 points (sized for the
+  // expected ~4 real solutions per sample; the kernel stops at the device count)
+  const int64_t groups = (std::max<int64_t>(1, 4 * S) + 63) / 64;
   int64_t nch = std::max<int64_t>(1, std::min<int64_t>((8192 + groups - 1) / groups, (n + 63) / 64));
   const int chunk = static_cast<int>((n + nch - 1) / nch);
   HIP_TRY(rsd::launch_f8_count(dp, static_cast<int>(n), static_cast<int>(H), dF, ld, chunk,
-                               thresh * thresh, dc, s));
-  HIP_TRY(hipMemsetAsync(dcmax + 1, 0, sizeof(int), s));
-  hipLaunchKernelGGL(rsd::k_e5_max, dim3(1), dim3(1024), 0, s, dc, H, dcmax);
+                               thresh * thresh, dc, s, dcmax + 2, dslot));
+  HIP_TRY(hipMemsetAsync(dcmax, 0, 2 * sizeof(int), s));
+  hipLaunchKernelGGL(rsd::k_e5_max, dim3(static_cast<unsigned>(std::min<int64_t>((H + 255) / 256, 64))),
+                     dim3(256), 0, s, dc, H, dcmax + 2, dcmax);
   hipLaunchKernelGGL(rsd::k_e5_cands, dim3(static_cast<unsigned>(std::min<int64_t>((H + 255) / 256, 1024))),
-                     dim3(256), 0, s, dc, H, dcmax, dcand, dcmax + 1);
+                     dim3(256), 0, s, dc, H, dcmax + 2, dcmax, dcand, dcmax + 1);
   hipLaunchKernelGGL(rsd::k_e5_norms, dim3(256), dim3(256), 0, s, dp, static_cast<int>(n), dcand,
-                     dcmax + 1, dF, ld, dnorm);
+                     dcmax + 1, dslot, dF, ld, dnorm);
   hipLaunchKernelGGL(rsd::k_e5_select, dim3(1), dim3(1024), 0, s, dnorm, dcand, dcmax + 1, dcmax,
-                     dE, dF, ld, dr);
+                     dslot, dE, dF, ld, dr);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(rsd::k_e5_inliers, dim3(1), dim3(1024), 0, s, dp, static_cast<int>(n),
                      thresh * thresh, dr);

@@ -92,7 +92,8 @@ hipError_t launch_f8_count32q(const float4 *ptsq, const Pt *pts, int n, int H,
                               const Count32qShape &sh, const GuardW &g, int *counts,
                               hipStream_t s, int *gdone, int *status, const float4 *G4);
 hipError_t launch_f8_count(const Pt *pts, int n, int H, const double *Fsoa, int64_t ld,
-                           int chunk, double thr2, int *counts, hipStream_t s);
+                           int chunk, double thr2, int *counts, hipStream_t s,
+                           const int *Hdev = nullptr, const int *Hmap = nullptr);
 // Selection tail: c* (k_f8_max, unless the counting kernel fused it), candidates + reference
 // statistics + (last block) replay and S_RANSAC.  Candidates live in per-block segments of
 // `cand`.

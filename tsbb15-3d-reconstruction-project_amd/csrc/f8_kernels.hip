@@ -143,9 +143,12 @@ __global__ __launch_bounds__(256) void k_f8_solve(SolveArgs a) {
 __global__ __launch_bounds__(256) void k_f8_count(const Pt *__restrict__ pts, int n, int H,
                                                   const double *__restrict__ Fsoa, int64_t ld,
                                                   int chunk, int nchunks, double thr2,
-                                                  int *__restrict__ counts) {
+                                                  int *__restrict__ counts,
+                                                  const int *__restrict__ Hdev,
+                                                  const int *__restrict__ Hmap) {
   const int lane = threadIdx.x & 63;
   const int u = wave_uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (Hdev) H = min(H, *Hdev);  // a count known on the device only (grid sized for the bound H)
   const int ngroups = (H + 63) >> 6;
   if (u >= ngroups * nchunks) return;
   const int g = u / nchunks;
@@ -153,7 +156,8 @@ __global__ __launch_bounds__(256) void k_f8_count(const Pt *__restrict__ pts, in
   const int p0 = c * chunk;
   const int p1 = min(n, p0 + chunk);
   const int h = g * 64 + lane;
-  const int hl = h < H ? h : H - 1;
+  const int hl0 = h < H ? h : H - 1;
+  const int hl = Hmap ? Hmap[hl0] : hl0;  // counts[h] of model Hmap[h] (a dense list of models)
   double f[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) f[k] = Fsoa[k * ld + hl];
@@ -940,11 +944,12 @@ hipError_t launch_f8_solve(const Pt *pts, int n, int H, int mode, uint64_t seed,
 }
 
 hipError_t launch_f8_count(const Pt *pts, int n, int H, const double *Fsoa, int64_t ld,
-                           int chunk, double thr2, int *counts, hipStream_t s) {
+                           int chunk, double thr2, int *counts, hipStream_t s, const int *Hdev,
+                           const int *Hmap) {
   const int nchunks = (n + chunk - 1) / chunk;
   const int units = ((H + 63) / 64) * nchunks;
   hipLaunchKernelGGL(k_f8_count, dim3((units + 3) / 4), dim3(256), 0, s, pts, n, H, Fsoa, ld,
-                     chunk, nchunks, thr2, counts);
+                     chunk, nchunks, thr2, counts, Hdev, Hmap);
   return hipGetLastError();
 }
 
