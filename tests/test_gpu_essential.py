@@ -114,6 +114,22 @@ def test_ransac_e_synthetic_outliers(ctx):
     assert r2.best_sample == r.best_sample and np.array_equal(r2.inliers, r.inliers)
 
 
+def test_ransac_e_many_samples_two_level_scan(ctx):
+    """Past 128 x 256 samples the real solutions are listed through per-workgroup sums and a
+    scan (k_e5_bsum / k_e5_bscan) instead of the inline reduction.  Sample s depends only on
+    (seed, s), so 40 000 samples contain the 20 000-sample run's hypotheses: the consensus can
+    only grow, and the winner's count is its own recount."""
+    p1, p2, _ = synth.two_view(2000, 0.3, seed=6)
+    K = synth.K_SYNTH
+    small = essential.ransac_e(p1, p2, K, samples=20000, seed=3)
+    big = essential.ransac_e(p1, p2, K, samples=40000, seed=3)
+    assert big.count >= small.count > 0
+    d = ransac_ref.inlier_distance(big.F, p1, p2)
+    assert big.count == int((d < 1.5).sum()) == len(big.inliers)
+    if big.best_sample < 20000:  # the same winner when it lies in the shared prefix
+        assert big.best_sample == small.best_sample and big.count == small.count
+
+
 def test_ransac_e_rejects_bad_input(ctx):
     p1, p2, _ = synth.two_view(20, 0.0, seed=1)
     with pytest.raises(ValueError):

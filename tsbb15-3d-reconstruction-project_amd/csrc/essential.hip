@@ -685,18 +685,25 @@ __global__ __launch_bounds__(256) void k_e5_max(const int *__restrict__ counts, 
 // the solutions of all earlier samples (int4 loads, a reduction; no device-wide scan pass),
 // its samples' offsets by a block scan.  The dense order keeps the slot order, so "the smallest
 // slot on equal norms" is "the smallest dense index".
-constexpr int kPackSamples = 256;
+// (Past kPackInline workgroups the earlier counts come from k_e5_bsum / k_e5_bscan instead:
+// the inline reduction reads O(S^2 / 256) words.)
+constexpr int kPackSamples = 256, kPackInline = 128;
 __global__ __launch_bounds__(kPackSamples) void k_e5_pack(const int *__restrict__ nsol, int S,
+                                                          const int *__restrict__ bbase,
                                                           int *__restrict__ slot_of,
                                                           int *__restrict__ hc) {
   __shared__ int sw[kPackSamples / 64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int b0 = blockIdx.x * kPackSamples;  // a multiple of 4: int4 loads below b0
   int pre = 0;
+  if (bbase) {
+    pre = tid == 0 ? bbase[blockIdx.x] : 0;
+  } else {
 #pragma unroll 4
-  for (int k = 4 * tid; k < b0; k += 4 * kPackSamples) {
-    const int4 q = *reinterpret_cast<const int4 *>(nsol + k);
-    pre += (q.x + q.y) + (q.z + q.w);
+    for (int k = 4 * tid; k < b0; k += 4 * kPackSamples) {
+      const int4 q = *reinterpret_cast<const int4 *>(nsol + k);
+      pre += (q.x + q.y) + (q.z + q.w);
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
@@ -720,6 +727,48 @@ __global__ __launch_bounds__(kPackSamples) void k_e5_pack(const int *__restrict_
   const int o = base + x - v;
   for (int j = 0; j < v; ++j) slot_of[o + j] = sidx * kE5Sol + j;
   if (blockIdx.x == gridDim.x - 1 && tid == kPackSamples - 1) *hc = base + x;
+}
+
+// solutions per workgroup of kPackSamples samples
+__global__ __launch_bounds__(kPackSamples) void k_e5_bsum(const int *__restrict__ nsol, int S,
+                                                          int *__restrict__ bsum) {
+  __shared__ int sw[kPackSamples / 64];
+  const int tid = threadIdx.x, sidx = blockIdx.x * kPackSamples + tid;
+  int v = sidx < S ? nsol[sidx] : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((tid & 63) == 0) sw[tid >> 6] = v;
+  __syncthreads();
+  if (tid == 0) {
+    int t = 0;
+#pragma unroll
+    for (int q = 0; q < kPackSamples / 64; ++q) t += sw[q];
+    bsum[blockIdx.x] = t;
+  }
+}
+
+// exclusive scan of the nb workgroup sums in place (one workgroup, a run per thread)
+__global__ __launch_bounds__(1024) void k_e5_bscan(int *__restrict__ bsum, int nb) {
+  __shared__ int sw[16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int per = (nb + 1023) / 1024, lo = min(nb, tid * per), hi = min(nb, lo + per);
+  int v = 0;
+  for (int k = lo; k < hi; ++k) v += bsum[k];
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sw[w] = x;
+  __syncthreads();
+  int base = x - v;
+  for (int q = 0; q < w; ++q) base += sw[q];
+  for (int k = lo; k < hi; ++k) {
+    const int t = bsum[k];
+    bsum[k] = base;
+    base += t;
+  }
 }
 
 // The slots with the largest count c* (the candidates), appended in any order: one ballot and
@@ -1003,7 +1052,7 @@ extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64
   const size_t br = e5_align(sizeof(rsd::E5DevResult) + sizeof(int64_t) * n);
   const size_t bnorm = e5_align(sizeof(double) * ld);
   int st = rs::ensure_scratch(c, 2 * bin + bp + 2 * bE + bc + br + bnorm + 256 +
-                                     2 * e5_align(sizeof(int) * ld) + e5_align(sizeof(int) * S) +
+                                     2 * e5_align(sizeof(int) * ld) + 2 * e5_align(sizeof(int) * S) +
                                      e5_work_bytes(S));
   if (st) return st;
   char *ptr = static_cast<char *>(c->scratch);
@@ -1024,6 +1073,7 @@ extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64
   int *dcand = reinterpret_cast<int *>(take(e5_align(sizeof(int) * ld)));
   int *dnsol = reinterpret_cast<int *>(take(e5_align(sizeof(int) * S)));
   int *dslot = reinterpret_cast<int *>(take(e5_align(sizeof(int) * ld)));
+  int *doff = reinterpret_cast<int *>(take(e5_align(sizeof(int) * S)));  // workgroup bases
   char *work = take(e5_work_bytes(S));
   hipStream_t s = c->stream;
   HIP_TRY(hipMemcpyAsync(d1, p1, sizeof(double) * 2 * n, hipMemcpyHostToDevice, s));
@@ -1040,8 +1090,16 @@ extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64
   a.ld = ld;
   if ((st = launch_e5_solve(a, work, s))) return st;
   // only the real solutions are counted: the map dslot (dense index -> slot, *hc entries)
-  hipLaunchKernelGGL(rsd::k_e5_pack, dim3(static_cast<unsigned>((S + rsd::kPackSamples - 1) / rsd::kPackSamples)),
-                     dim3(rsd::kPackSamples), 0, s, dnsol, static_cast<int>(S), dslot, dcmax + 2);
+  const int npack = static_cast<int>((S + rsd::kPackSamples - 1) / rsd::kPackSamples);
+  int *dbsum = nullptr;
+  if (npack > rsd::kPackInline) {
+    dbsum = doff;
+    hipLaunchKernelGGL(rsd::k_e5_bsum, dim3(npack), dim3(rsd::kPackSamples), 0, s, dnsol,
+                       static_cast<int>(S), dbsum);
+    hipLaunchKernelGGL(rsd::k_e5_bscan, dim3(1), dim3(1024), 0, s, dbsum, npack);
+  }
+  hipLaunchKernelGGL(rsd::k_e5_pack, dim3(npack), dim3(rsd::kPackSamples), 0, s, dnsol,
+                     static_cast<int>(S), dbsum, dslot, dcmax + 2);
   HIP_TRY(hipMemsetAsync(dc, 0, sizeof(int) * H, s));
   // chunking of k_f8_count: >= 8 units of work per SIMD, chunks of >= 64 points (sized for the
   // expected ~4 real solutions per sample; the kernel stops at the device count)
