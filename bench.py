@@ -341,7 +341,7 @@ def extras(ctx, rank, world, dist, comm):
                                "note": "k_e5_build (null basis, ten cubics) + k_e5_gj (Gauss-"
                                        "Jordan, 32 lanes per sample) + k_e5_roots (16 lanes per "
                                        "sample, a lane per root) + k_e5_pack (the real "
-                                       "solutions' slots) + k_f8_count over those + selection, "
+                                       "solutions' slots) + k_f8_count32q over those + selection, "
                                        "N = 2000"}
     except Exception as e:  # noqa: BLE001
         out["e5_ransac_c2"] = {"error": repr(e)}

@@ -104,6 +104,53 @@ __device__ __forceinline__ double rcp_fast(double x) {
   return fma(y, e, y);
 }
 
+// fp32 model of the counting kernel k_f8_count32q for the float64 F of hypothesis h: F~ = T1^T
+// F T2 (T_i = [[s,0,cx_i],[0,s,cy_i],[0,0,1]]) scaled to max |F~_ij| = 1, into F32soa (9 x ld),
+// and (G4 non-null) its decision constants from the guard bounds (T, De, Dn) of the frame
+// (f8_kernels.hip above k_f8_count32q).
+__device__ __forceinline__ void f32_model(const double (&F)[9], const Frame &fr, double gT,
+                                          double gDe, double gDn, float *__restrict__ F32soa,
+                                          float4 *__restrict__ G4, int64_t ld, int64_t h) {
+  double G[9];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    G[3 * r + 0] = F[3 * r + 0] * fr.s;
+    G[3 * r + 1] = F[3 * r + 1] * fr.s;
+    G[3 * r + 2] = F[3 * r + 0] * fr.cx2 + F[3 * r + 1] * fr.cy2 + F[3 * r + 2];
+  }
+  double Ft[9];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    Ft[0 + c] = fr.s * G[0 + c];
+    Ft[3 + c] = fr.s * G[3 + c];
+    Ft[6 + c] = fr.cx1 * G[0 + c] + fr.cy1 * G[3 + c] + G[6 + c];
+  }
+  double mx = 0.0;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) mx = fmax(mx, fabs(Ft[k]));
+  const double kap = 1.0 / mx;  // F = 0 or non-finite -> NaN model, counts 0 on both paths
+#pragma unroll
+  for (int k = 0; k < 9; ++k) F32soa[k * ld + h] = static_cast<float>(Ft[k] * kap);
+  if (G4) {
+    // decision constants, AM-GM split point c = t~ sqrt(m at the frame centre) (any c > 0 is
+    // rigorous; this one keeps the band near the exact-|e| band)
+    const double u = 0x1p-24, T = gT, De = gDe, Dn = gDn;
+    const double f02 = Ft[2] * kap, f12 = Ft[5] * kap, f20 = Ft[6] * kap, f21 = Ft[7] * kap;
+    const double mc = fmin(f02 * f02 + f12 * f12, f20 * f20 + f21 * f21);
+    // (rsqrt_fast / rcp_fast: a few ulp, far inside the 1 -/+ 4u and 1.02 margins)
+    const double tm = T * fmax(mc, 1e-12);
+    const double c = fmax(tm * rsqrt_fast(tm), 100.0 * De);
+    const double r = De * rcp_fast(c);
+    const double ip = rcp_fast(1.0 + r), im = rcp_fast(1.0 - r);
+    const double alpha = T * (1.0 - u) * rcp_fast(1.0 + u) * ip * (1.0 - 4.0 * u);
+    const double beta = T * (1.0 + u) * rcp_fast(1.0 - u) * im * (1.0 + 4.0 * u);
+    const double ki = 1.02 * (De * c + De * De + T * Dn) * ip + 1e-30;
+    const double ko = 1.02 * (T * Dn + De * c) * im + 1e-30;
+    G4[h] = make_float4(static_cast<float>(ki), -static_cast<float>(ko), static_cast<float>(alpha),
+                        static_cast<float>(beta));
+  }
+}
+
 // ----------------------------------------------------------------------------------------
 // One-sided Jacobi SVD of a 3x3 matrix (row-major M).  On exit the columns of B = M V are
 // mutually orthogonal (their norms are the singular values) and V holds the right

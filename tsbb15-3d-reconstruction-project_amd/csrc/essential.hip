@@ -729,6 +729,27 @@ __global__ __launch_bounds__(kPackSamples) void k_e5_pack(const int *__restrict_
   if (blockIdx.x == gridDim.x - 1 && tid == kPackSamples - 1) *hc = base + x;
 }
 
+// The counting models of the real solutions (dense index h -> slot): the float64 F for the
+// guard re-test (Fd) and the fp32 unit-frame model with its decision constants (f32_model, as
+// the F-RANSAC solve writes them)
+__global__ __launch_bounds__(256) void k_e5_models(const int *__restrict__ slot_of, int Hc,
+                                                   const double *__restrict__ Fsoa, int64_t ld,
+                                                   Frame fr, double gT, double gDe, double gDn,
+                                                   double *__restrict__ Fd,
+                                                   float *__restrict__ F32soa,
+                                                   float4 *__restrict__ G4) {
+  const int h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= Hc) return;
+  const int64_t slot = slot_of[h];
+  double F[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) {
+    F[q] = Fsoa[q * ld + slot];
+    Fd[q * ld + h] = F[q];
+  }
+  f32_model(F, fr, gT, gDe, gDn, F32soa, G4, ld, h);
+}
+
 // solutions per workgroup of kPackSamples samples
 __global__ __launch_bounds__(kPackSamples) void k_e5_bsum(const int *__restrict__ nsol, int S,
                                                           int *__restrict__ bsum) {
@@ -943,6 +964,7 @@ using rs::hip_fail;
   } while (0)
 
 static size_t e5_align(size_t b) { return (b + 255) / 256 * 256; }
+constexpr int kE5CountWaves = 6144;  // resident waves of k_f8_count32q (as the F-RANSAC plan)
 
 // bytes of the three solve kernels' work buffers for S samples
 static size_t e5_work_bytes(int64_t S) {
@@ -1051,7 +1073,9 @@ extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64
   const size_t bE = e5_align(sizeof(double) * 9 * ld), bc = e5_align(sizeof(int) * ld);
   const size_t br = e5_align(sizeof(rsd::E5DevResult) + sizeof(int64_t) * n);
   const size_t bnorm = e5_align(sizeof(double) * ld);
-  int st = rs::ensure_scratch(c, 2 * bin + bp + 2 * bE + bc + br + bnorm + 256 +
+  const size_t bpq = e5_align(sizeof(float) * 4 * ((n + 7) / 8 * 8));
+  const size_t bF32 = e5_align(sizeof(float) * 9 * ld), bG4 = e5_align(sizeof(float4) * ld);
+  int st = rs::ensure_scratch(c, 2 * bin + bp + 3 * bE + bc + br + bnorm + 256 + bpq + bF32 + bG4 +
                                      2 * e5_align(sizeof(int) * ld) + 2 * e5_align(sizeof(int) * S) +
                                      e5_work_bytes(S));
   if (st) return st;
@@ -1074,11 +1098,21 @@ extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64
   int *dnsol = reinterpret_cast<int *>(take(e5_align(sizeof(int) * S)));
   int *dslot = reinterpret_cast<int *>(take(e5_align(sizeof(int) * ld)));
   int *doff = reinterpret_cast<int *>(take(e5_align(sizeof(int) * S)));  // workgroup bases
+  // fp32 counting: point-pair layout, dense float64 / fp32 models, decision constants
+  auto *dpq = reinterpret_cast<float4 *>(take(bpq));
+  double *dFd = reinterpret_cast<double *>(take(bE));
+  float *dF32 = reinterpret_cast<float *>(take(bF32));
+  auto *dG4 = reinterpret_cast<float4 *>(take(bG4));
   char *work = take(e5_work_bytes(S));
   hipStream_t s = c->stream;
   HIP_TRY(hipMemcpyAsync(d1, p1, sizeof(double) * 2 * n, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(d2, p2, sizeof(double) * 2 * n, hipMemcpyHostToDevice, s));
   HIP_TRY(rsd::launch_pack_points(d1, d2, static_cast<int>(n), dp, s));
+  // counting in fp32 with the float64 guard band (k_f8_count32q, the F-RANSAC product kernel:
+  // counts identical to the float64 test's) unless the points give no unit frame
+  rsd::Frame fr{};
+  const bool fp32 = rsd::unit_frame(p1, p2, n, fr);
+  if (fp32) HIP_TRY(rsd::launch_pack_points32q(dp, static_cast<int>(n), fr, dpq, s));
   a.pts = dp;
   a.n = static_cast<int>(n);
   a.S = static_cast<int>(S);
@@ -1100,14 +1134,30 @@ extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64
   }
   hipLaunchKernelGGL(rsd::k_e5_pack, dim3(npack), dim3(rsd::kPackSamples), 0, s, dnsol,
                      static_cast<int>(S), dbsum, dslot, dcmax + 2);
-  HIP_TRY(hipMemsetAsync(dc, 0, sizeof(int) * H, s));
-  // chunking of k_f8_count: >= 8 units of work per SIMD, chunks of >= 64 points (sized for the
-  // expected ~4 real solutions per sample; the kernel stops at the device count)
-  const int64_t groups = (std::max<int64_t>(1, 4 * S) + 63) / 64;
-  int64_t nch = std::max<int64_t>(1, std::min<int64_t>((8192 + groups - 1) / groups, (n + 63) / 64));
-  const int chunk = static_cast<int>((n + nch - 1) / nch);
-  HIP_TRY(rsd::launch_f8_count(dp, static_cast<int>(n), static_cast<int>(H), dF, ld, chunk,
-                               thresh * thresh, dc, s, dcmax + 2, dslot));
+  if (fp32) {
+    // the launch shape of k_f8_count32q needs the number of real solutions on the host
+    int Hc = 0;
+    HIP_TRY(hipMemcpyAsync(&Hc, dcmax + 2, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (Hc > 0) {
+      const rsd::Bounds gb = rsd::fp32_bounds(fr, thresh);
+      hipLaunchKernelGGL(rsd::k_e5_models, dim3((Hc + 255) / 256), dim3(256), 0, s, dslot, Hc, dF,
+                         ld, fr, gb.thr2, gb.De, gb.Dn, dFd, dF32, dG4);
+      HIP_TRY(hipMemsetAsync(dc, 0, sizeof(int) * Hc, s));
+      const rsd::Count32qShape sh = rsd::count32q_shape(static_cast<int>(n), Hc, kE5CountWaves);
+      HIP_TRY(rsd::launch_f8_count32q(dpq, dp, static_cast<int>(n), Hc, dF32, dFd, ld, sh,
+                                      rsd::GuardW{thresh * thresh}, dc, s, nullptr, nullptr, dG4));
+    }
+  } else {
+    HIP_TRY(hipMemsetAsync(dc, 0, sizeof(int) * H, s));
+    // chunking of k_f8_count: >= 8 units of work per SIMD, chunks of >= 64 points (sized for
+    // the expected ~4 real solutions per sample; the kernel stops at the device count)
+    const int64_t groups = (std::max<int64_t>(1, 4 * S) + 63) / 64;
+    int64_t nch = std::max<int64_t>(1, std::min<int64_t>((8192 + groups - 1) / groups, (n + 63) / 64));
+    const int chunk = static_cast<int>((n + nch - 1) / nch);
+    HIP_TRY(rsd::launch_f8_count(dp, static_cast<int>(n), static_cast<int>(H), dF, ld, chunk,
+                                 thresh * thresh, dc, s, dcmax + 2, dslot));
+  }
   HIP_TRY(hipMemsetAsync(dcmax, 0, 2 * sizeof(int), s));
   hipLaunchKernelGGL(rsd::k_e5_max, dim3(static_cast<unsigned>(std::min<int64_t>((H + 255) / 256, 64))),
                      dim3(256), 0, s, dc, H, dcmax + 2, dcmax);

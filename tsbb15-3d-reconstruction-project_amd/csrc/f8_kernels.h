@@ -86,6 +86,12 @@ struct Count32qShape {
   int64_t blocks;    // 256-thread workgroups launched
 };
 int count32q_resident_waves(int device);
+// fp32 counting set-up (host): guard bounds of the unit frame, and the frame of the points
+struct Bounds {
+  double u, De, Dn, thr2;
+};
+Bounds fp32_bounds(const Frame &fr, double thresh);
+bool unit_frame(const double *p1, const double *p2, int64_t n, Frame &fr);
 Count32qShape count32q_shape(int n, int H, int waves, int slices_per_wave = 0);
 hipError_t launch_f8_count32q(const float4 *ptsq, const Pt *pts, int n, int H,
                               const float *F32soa, const double *Fsoa, int64_t ld,

@@ -86,47 +86,7 @@ __device__ __forceinline__ void solve_one(const SolveArgs &a, int h) {
   fmatrix8(xl, yl, xr, yr, F);
 #pragma unroll
   for (int k = 0; k < 9; ++k) Fsoa[k * ld + h] = F[k];
-  if (F32soa) {
-    // F~ = T1^T F T2 (T_i = [[s,0,cx_i],[0,s,cy_i],[0,0,1]]), scaled to max |F~_ij| = 1
-    double G[9];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      G[3 * r + 0] = F[3 * r + 0] * fr.s;
-      G[3 * r + 1] = F[3 * r + 1] * fr.s;
-      G[3 * r + 2] = F[3 * r + 0] * fr.cx2 + F[3 * r + 1] * fr.cy2 + F[3 * r + 2];
-    }
-    double Ft[9];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      Ft[0 + c] = fr.s * G[0 + c];
-      Ft[3 + c] = fr.s * G[3 + c];
-      Ft[6 + c] = fr.cx1 * G[0 + c] + fr.cy1 * G[3 + c] + G[6 + c];
-    }
-    double mx = 0.0;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) mx = fmax(mx, fabs(Ft[k]));
-    const double kap = 1.0 / mx;  // F = 0 or non-finite -> NaN model, counts 0 on both paths
-#pragma unroll
-    for (int k = 0; k < 9; ++k) F32soa[k * ld + h] = static_cast<float>(Ft[k] * kap);
-    if (a.G4) {
-      // k_f8_count32q decision constants, AM-GM split point c = t~ sqrt(m at the frame centre)
-      // (any c > 0 is rigorous; this one keeps the band near the exact-|e| band)
-      const double u = 0x1p-24, T = a.gT, De = a.gDe, Dn = a.gDn;
-      const double f02 = Ft[2] * kap, f12 = Ft[5] * kap, f20 = Ft[6] * kap, f21 = Ft[7] * kap;
-      const double mc = fmin(f02 * f02 + f12 * f12, f20 * f20 + f21 * f21);
-      // (rsqrt_fast / rcp_fast: a few ulp, far inside the 1 -/+ 4u and 1.02 margins)
-      const double tm = T * fmax(mc, 1e-12);
-      const double c = fmax(tm * rsqrt_fast(tm), 100.0 * De);
-      const double r = De * rcp_fast(c);
-      const double ip = rcp_fast(1.0 + r), im = rcp_fast(1.0 - r);
-      const double alpha = T * (1.0 - u) * rcp_fast(1.0 + u) * ip * (1.0 - 4.0 * u);
-      const double beta = T * (1.0 + u) * rcp_fast(1.0 - u) * im * (1.0 + 4.0 * u);
-      const double ki = 1.02 * (De * c + De * De + T * Dn) * ip + 1e-30;
-      const double ko = 1.02 * (T * Dn + De * c) * im + 1e-30;
-      a.G4[h] = make_float4(static_cast<float>(ki), -static_cast<float>(ko),
-                            static_cast<float>(alpha), static_cast<float>(beta));
-    }
-  }
+  if (F32soa) f32_model(F, fr, a.gT, a.gDe, a.gDn, F32soa, a.G4, ld, h);
 }
 
 __global__ __launch_bounds__(256) void k_f8_solve(SolveArgs a) {
@@ -972,6 +932,46 @@ int count32q_resident_waves(int device) {
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     cus = 256;
   return cus * 4 * 6;
+}
+
+// Absolute error bounds of the fp32 test in the unit frame (|x~| <= R); derivation above
+// k_f8_count32q.  Dl: a line component, De: e, Dn: a squared length.
+Bounds fp32_bounds(const Frame &fr, double thresh) {
+  const double u = std::ldexp(1.0, -24), R = 1.0 + 1e-6, Lm = 2.0 * R + 1.0;
+  const double Dl = 1.1 * u * (7.0 * R + 3.0);
+  const double De =
+      1.1 * (2.0 * (Dl * R * 1.001 + Lm * u * R) + Dl + u * (Lm + Dl) * (3.0 * R + 2.0) * 1.001);
+  const double Dn = 1.1 * (2.0 * Dl * (2.0 * Lm + Dl) + 3.0 * u * (Lm + Dl) * (Lm + Dl) * 1.001);
+  return {u, De, Dn, (thresh / fr.s) * (thresh / fr.s)};
+}
+
+// The unit frame of the fp32 counting kernel from the (2, n) pixel points: per-image centres,
+// one common scale; false (no fp32 counting) for non-finite points or a degenerate frame.
+bool unit_frame(const double *p1, const double *p2, int64_t n, Frame &fr) {
+  double lo[4], hi[4];
+  bool finite = true;
+  for (int k = 0; k < 4; ++k) {
+    lo[k] = INFINITY;
+    hi[k] = -INFINITY;
+  }
+  for (int64_t i = 0; i < n; ++i) {
+    const double v[4] = {p1[i], p1[n + i], p2[i], p2[n + i]};
+    for (int k = 0; k < 4; ++k) {
+      finite &= std::isfinite(v[k]);
+      lo[k] = std::min(lo[k], v[k]);
+      hi[k] = std::max(hi[k], v[k]);
+    }
+  }
+  fr = Frame{0.0, 0.5 * (lo[0] + hi[0]), 0.5 * (lo[1] + hi[1]), 0.5 * (lo[2] + hi[2]),
+             0.5 * (lo[3] + hi[3])};
+  const double cen[4] = {fr.cx1, fr.cy1, fr.cx2, fr.cy2};
+  for (int64_t i = 0; finite && i < n; ++i) {
+    const double v[4] = {p1[i], p1[n + i], p2[i], p2[n + i]};
+    for (int k = 0; k < 4; ++k) fr.s = std::max(fr.s, std::fabs(v[k] - cen[k]));
+  }
+  if (!(finite && fr.s > 0.0 && std::isfinite(fr.s))) return false;
+  fr.s *= 1.0 + 1e-12;  // |x~| <= 1 after the fp64 division
+  return true;
 }
 
 Count32qShape count32q_shape(int n, int H, int waves, int slices_per_wave) {

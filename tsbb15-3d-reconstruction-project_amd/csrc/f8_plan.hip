@@ -57,21 +57,6 @@ struct RunBufs {
   bool copy_pending = false;
 };
 
-// Absolute error bounds of the fp32 test in the unit frame (|x~| <= R); derivation in
-// f8_kernels.hip above k_f8_count32.  Dl: a line component, De: e, Dn: a squared length.
-struct Bounds {
-  double u, De, Dn, thr2;
-};
-
-Bounds fp32_bounds(const rsd::Frame &fr, double thresh) {
-  const double u = std::ldexp(1.0, -24), R = 1.0 + 1e-6, Lm = 2.0 * R + 1.0;
-  const double Dl = 1.1 * u * (7.0 * R + 3.0);
-  const double De =
-      1.1 * (2.0 * (Dl * R * 1.001 + Lm * u * R) + Dl + u * (Lm + Dl) * (3.0 * R + 2.0) * 1.001);
-  const double Dn = 1.1 * (2.0 * Dl * (2.0 * Lm + Dl) + 3.0 * u * (Lm + Dl) * (Lm + Dl) * 1.001);
-  return {u, De, Dn, (thresh / fr.s) * (thresh / fr.s)};
-}
-
 int env_int(const char *name, int dflt) {
   const char *v = std::getenv(name);
   return v ? std::atoi(v) : dflt;
@@ -264,31 +249,9 @@ extern "C" int rs_f8_plan_set_points(rs_f8_plan *p, const double *p1, const doub
   HIP_TRY(hipMemcpyAsync(p->d_p12 + 2 * n, p2, b, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(rsd::launch_pack_points(p->d_p12, p->d_p12 + 2 * n, static_cast<int>(n), p->d_pts,
                                   c->stream));
-  // unit frame of the fp32 counting kernel: per-image centres, one common scale
-  double lo[4], hi[4];
-  bool finite = true;
-  for (int k = 0; k < 4; ++k) {
-    lo[k] = INFINITY;
-    hi[k] = -INFINITY;
-  }
-  for (int64_t i = 0; i < n; ++i) {
-    const double v[4] = {p1[i], p1[n + i], p2[i], p2[n + i]};
-    for (int k = 0; k < 4; ++k) {
-      finite &= std::isfinite(v[k]);
-      lo[k] = std::min(lo[k], v[k]);
-      hi[k] = std::max(hi[k], v[k]);
-    }
-  }
-  rsd::Frame fr{0.0, 0.5 * (lo[0] + hi[0]), 0.5 * (lo[1] + hi[1]), 0.5 * (lo[2] + hi[2]),
-                0.5 * (lo[3] + hi[3])};
-  const double cen[4] = {fr.cx1, fr.cy1, fr.cx2, fr.cy2};
-  for (int64_t i = 0; finite && i < n; ++i) {
-    const double v[4] = {p1[i], p1[n + i], p2[i], p2[n + i]};
-    for (int k = 0; k < 4; ++k) fr.s = std::max(fr.s, std::fabs(v[k] - cen[k]));
-  }
-  p->fp32_ok = finite && fr.s > 0.0 && std::isfinite(fr.s);
+  rsd::Frame fr{};
+  p->fp32_ok = rsd::unit_frame(p1, p2, n, fr);
   if (p->fp32_ok) {
-    fr.s *= 1.0 + 1e-12;  // |x~| <= 1 after the fp64 division
     p->frame = fr;
     HIP_TRY(rsd::launch_pack_points32q(p->d_pts, static_cast<int>(n), fr, p->d_pts32q,
                                        c->stream));
@@ -370,7 +333,7 @@ static int plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t seed, uint6
   sa.frame = fp32 ? p->frame : rsd::Frame{1.0, 0.0, 0.0, 0.0, 0.0};
   sa.gdone = b.d_gdone;
   if (fp32) {
-    const Bounds gb = fp32_bounds(p->frame, thresh);
+    const rsd::Bounds gb = rsd::fp32_bounds(p->frame, thresh);
     sa.G4 = b.d_G4;
     sa.gT = gb.thr2;
     sa.gDe = gb.De;
