@@ -130,6 +130,19 @@ def test_ransac_e_many_samples_two_level_scan(ctx):
         assert big.best_sample == small.best_sample and big.count == small.count
 
 
+def test_ransac_e_fp32_counting_equals_float64(ctx, monkeypatch):
+    """The real solutions are counted by the fp32 guard-band kernel (k_f8_count32q); the plain
+    float64 kernel (RSAMD_E5_FP64=1) gives the same winner, count and consensus set."""
+    p1, p2, _ = synth.two_view(2000, 0.3, seed=6)
+    K = synth.K_SYNTH
+    r32 = essential.ransac_e(p1, p2, K, samples=3000, seed=11)
+    monkeypatch.setenv("RSAMD_E5_FP64", "1")
+    r64 = essential.ransac_e(p1, p2, K, samples=3000, seed=11)
+    assert (r32.best_sample, r32.best_solution, r32.count) == (r64.best_sample, r64.best_solution, r64.count)
+    assert np.array_equal(r32.inliers, r64.inliers)
+    assert np.array_equal(r32.F, r64.F)
+
+
 def test_ransac_e_rejects_bad_input(ctx):
     p1, p2, _ = synth.two_view(20, 0.0, seed=1)
     with pytest.raises(ValueError):

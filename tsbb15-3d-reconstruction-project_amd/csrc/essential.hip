@@ -37,6 +37,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -1111,7 +1112,9 @@ extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64
   // counting in fp32 with the float64 guard band (k_f8_count32q, the F-RANSAC product kernel:
   // counts identical to the float64 test's) unless the points give no unit frame
   rsd::Frame fr{};
-  const bool fp32 = rsd::unit_frame(p1, p2, n, fr);
+  // (RSAMD_E5_FP64=1, a test hook: the plain float64 kernel, for the equal-counts test)
+  const char *f64 = std::getenv("RSAMD_E5_FP64");
+  const bool fp32 = rsd::unit_frame(p1, p2, n, fr) && !(f64 && f64[0] == '1');
   if (fp32) HIP_TRY(rsd::launch_pack_points32q(dp, static_cast<int>(n), fr, dpq, s));
   a.pts = dp;
   a.n = static_cast<int>(n);
