@@ -57,6 +57,8 @@ struct RunBufs {
   bool copy_pending = false;
 };
 
+constexpr int kOverlapDefault = 0;  // rs_f8_plan::overlap unless RSAMD_OVERLAP is set
+
 int env_int(const char *name, int dflt) {
   const char *v = std::getenv(name);
   return v ? std::atoi(v) : dflt;
@@ -82,6 +84,13 @@ struct rs_f8_plan {
   int64_t runs = 0, last_H = 0;
   bool pending = false;              // stream work not yet waited for
   bool tail_pending = false;         // the last run's tail is not enqueued yet
+  // Overlap mode (RSAMD_OVERLAP=1; kOverlapDefault otherwise): run k's solve on ss, its
+  // count on the context stream, its tail on ts, chained by events, so the next run's solve and
+  // this run's tail fill the CUs the counting kernel's drain leaves idle.  A buffer set's solve
+  // waits for the tail of the run that used the set before (kBufs runs back).
+  bool overlap = true;
+  hipStream_t ss = nullptr, ts = nullptr;
+  hipEvent_t ev_solve[kBufs] = {}, ev_count[kBufs] = {}, ev_tail[kBufs] = {};
   rsd::TailArgs tail{};              // ... its arguments
   // counting kernel: fp32 point-pair kernel with the float64 guard re-test (default), or the
   // plain float64 kernel (rs_f8_plan_set_count_precision; both give identical counts)
@@ -135,6 +144,13 @@ static void plan_free(rs_f8_plan *p) {
     if (b.h_tuples) (void)hipHostFree(b.h_tuples);
     if (b.ev_copy) (void)hipEventDestroy(b.ev_copy);
   }
+  for (int k = 0; k < rs_f8_plan::kBufs; ++k) {
+    if (p->ev_solve[k]) (void)hipEventDestroy(p->ev_solve[k]);
+    if (p->ev_count[k]) (void)hipEventDestroy(p->ev_count[k]);
+    if (p->ev_tail[k]) (void)hipEventDestroy(p->ev_tail[k]);
+  }
+  if (p->ss) (void)hipStreamDestroy(p->ss);
+  if (p->ts) (void)hipStreamDestroy(p->ts);
   for (auto &h : p->h_slot)
     if (h) (void)hipHostFree(h);
   for (auto &r : p->ring)
@@ -200,6 +216,16 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
   for (auto &r : p->ring)
     for (auto &ev : r)
       if (e == hipSuccess) e = hipEventCreate(&ev);
+  p->overlap = env_int("RSAMD_OVERLAP", kOverlapDefault) != 0;
+  if (p->overlap) {
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->ss, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->ts, hipStreamNonBlocking);
+    for (int k = 0; k < rs_f8_plan::kBufs; ++k) {
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&p->ev_solve[k], hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&p->ev_count[k], hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&p->ev_tail[k], hipEventDisableTiming);
+    }
+  }
   p->nospec = env_int("RSAMD_NOSPEC", 0) != 0;
   p->ts_path = std::getenv("RSAMD_TSTAMP");
   if (p->ts_path) {
@@ -224,6 +250,10 @@ static int plan_flush(rs_f8_plan *p) {
   if (p->tail_pending) {
     HIP_TRY(rsd::launch_f8_tail_solve(&p->tail, nullptr, p->ctx->stream));
     p->tail_pending = false;
+  }
+  if (p->overlap) {
+    HIP_TRY(hipStreamSynchronize(p->ss));
+    HIP_TRY(hipStreamSynchronize(p->ts));
   }
   HIP_TRY(hipStreamSynchronize(p->ctx->stream));
   p->pending = false;
@@ -293,6 +323,10 @@ static int plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t seed, uint6
   const int slot = static_cast<int>(p->runs % rs_f8_plan::kSlots);
   const bool fp32 = p->use_fp32 && p->fp32_ok;
   hipStream_t ms = c->stream;
+  const int bi = static_cast<int>(p->runs % rs_f8_plan::kBufs);
+  // the solve's stream: ss in overlap mode, after the tail of this buffer set's previous run
+  hipStream_t sv = p->overlap ? p->ss : ms;
+  if (p->overlap) HIP_TRY(hipStreamWaitEvent(sv, p->ev_tail[bi], 0));
 
   if (mode == RS_SAMPLER_TUPLES && !dev_tuples) {
     // stage through the set's pinned buffer: the copy no longer reads caller memory after
@@ -311,8 +345,8 @@ static int plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t seed, uint6
     if (!b.ev_copy) HIP_TRY(hipEventCreateWithFlags(&b.ev_copy, hipEventDisableTiming));
     std::memcpy(b.h_tuples, host_tuples, sizeof(int) * 8 * H);
     HIP_TRY(hipMemcpyAsync(b.d_tuples, b.h_tuples, sizeof(int) * 8 * H, hipMemcpyHostToDevice,
-                           ms));
-    HIP_TRY(hipEventRecord(b.ev_copy, ms));
+                           sv));
+    HIP_TRY(hipEventRecord(b.ev_copy, sv));
     b.copy_pending = true;
   }
   // [tail of the previous run | solve of this run]: buffer set b was last read by run k-2,
@@ -339,10 +373,14 @@ static int plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t seed, uint6
     sa.gDe = gb.De;
     sa.gDn = gb.Dn;
   }
-  if (tl >= 2) HIP_TRY(hipEventRecord(ev[2], ms));
-  HIP_TRY(rsd::launch_f8_tail_solve(p->tail_pending ? &p->tail : nullptr, &sa, ms, p->tail_cus));
+  if (tl >= 2) HIP_TRY(hipEventRecord(ev[2], sv));
+  HIP_TRY(rsd::launch_f8_tail_solve(p->tail_pending ? &p->tail : nullptr, &sa, sv, p->tail_cus));
   p->tail_pending = false;
-  if (tl >= 2) HIP_TRY(hipEventRecord(ev[3], ms));
+  if (tl >= 2) HIP_TRY(hipEventRecord(ev[3], sv));
+  if (p->overlap) {
+    HIP_TRY(hipEventRecord(p->ev_solve[bi], sv));
+    HIP_TRY(hipStreamWaitEvent(ms, p->ev_solve[bi], 0));
+  }
 
   // counts of this run
   if (tl >= 1) HIP_TRY(hipEventRecord(ev[0], ms));
@@ -381,7 +419,15 @@ static int plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t seed, uint6
   ta.cnorm = b.d_cnorm;
   ta.res = b.d_res;
   ta.hres = p->h_slot_dev[slot];
-  p->tail_pending = true;
+  if (p->overlap) {
+    // the tail on ts right after this run's count; the next run's count does not wait for it
+    HIP_TRY(hipEventRecord(p->ev_count[bi], ms));
+    HIP_TRY(hipStreamWaitEvent(p->ts, p->ev_count[bi], 0));
+    HIP_TRY(rsd::launch_f8_tail_solve(&ta, nullptr, p->ts, p->tail_cus));
+    HIP_TRY(hipEventRecord(p->ev_tail[bi], p->ts));
+  } else {
+    p->tail_pending = true;
+  }
   ++p->runs;
   p->last_H = H;
   p->pending = true;
@@ -407,6 +453,7 @@ extern "C" int rs_f8_plan_run_np_slice(rs_f8_plan *p, int64_t H, int64_t start, 
   int st;
   if (rs::np_gpu_supported(p->n, 8) && std::getenv("RSAMD_NP_HOST") == nullptr) {
     RunBufs &b = p->buf[p->runs % rs_f8_plan::kBufs];
+    if (p->overlap) HIP_TRY(hipEventSynchronize(p->ev_solve[p->runs % rs_f8_plan::kBufs]));
     if ((st = rs::np_choice_device(p->ctx, key, pos, p->n, 8, H, b.d_tuples, false, start, count)))
       return st;
     return plan_run(p, count, RS_SAMPLER_TUPLES, 0, static_cast<uint64_t>(start), nullptr, thresh,
@@ -428,6 +475,7 @@ extern "C" int rs_f8_plan_run_np_shard(rs_f8_plan *p, rs_np_shard *sh, int64_t b
   const int64_t count = hi - base;
   if (count > p->max_hyp) return fail(RS_EINVAL, "hypothesis count out of plan range");
   RunBufs &b = p->buf[p->runs % rs_f8_plan::kBufs];
+  if (p->overlap) HIP_TRY(hipEventSynchronize(p->ev_solve[p->runs % rs_f8_plan::kBufs]));
   int st;
   if ((st = rs::np_shard_tuples_device(sh, base, hi, next_start, final_idx,
                                        count > 0 ? b.d_tuples : nullptr, key_out, pos_out)))
