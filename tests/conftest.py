@@ -20,6 +20,21 @@ def golden(name):
     return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
 
 
+def trace_blas_matches():
+    """(same, description): whether this host's numpy BLAS is the one tests/golden/gs_trace.npz
+    was recorded with (gs_trace_blas.json).  A TRF path is bit-reproducible only under the same
+    OpenBLAS kernel choice, so bit-equality against that trace is asserted only then."""
+    import json
+    import threadpoolctl
+    with open(os.path.join(GOLDEN, "gs_trace_blas.json")) as f:
+        rec = json.load(f)
+    here = [d for d in threadpoolctl.threadpool_info() if d.get("user_api") == "blas"]
+    here = here[0] if here else {}
+    keys = ("internal_api", "version", "architecture")
+    same = all(here.get(k) == rec[k] for k in keys)
+    return same, (f"this host: {[here.get(k) for k in keys]}, trace: {[rec[k] for k in keys]}")
+
+
 @pytest.fixture(scope="session")
 def ctx():
     from tsbb15_amd import _ffi

@@ -92,6 +92,19 @@ def main():
             out[f"{tag}_{k}"] = v
         print(tag, "nfev", r["nfev"], "njev", r["njev"], "cost", r["cost_final"], flush=True)
     np.savez_compressed(os.path.join(HERE, "gs_trace.npz"), **out)
+    # the TRF path depends on the OpenBLAS kernels picked for this CPU: record them, so the
+    # bit-equality tests can tell a different host from a regression
+    import json
+    import scipy
+    import threadpoolctl
+    blas = [d for d in threadpoolctl.threadpool_info() if d.get("user_api") == "blas"][0]
+    with open(os.path.join(HERE, "gs_trace_blas.json"), "w") as f:
+        json.dump({"note": "BLAS that tests/golden/gs_trace.npz was recorded and retraced with "
+                           "(the build container); the bit-equality of a TRF path holds only "
+                           "under the same OpenBLAS kernel choice",
+                   "internal_api": blas["internal_api"], "version": blas["version"],
+                   "architecture": blas["architecture"], "numpy": np.__version__,
+                   "scipy": scipy.__version__}, f, indent=1)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,59 @@
+"""bench.py's own rank launcher (``bench.py --gpus N`` with no torch.distributed.run) and the
+TcpHub harness, on the CPU: ``--harness-only`` never opens a device."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(REPO, "bench.py")
+
+
+def _run(args, env_extra=None, timeout=120):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                        "RSAMD_BENCH_FAIL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, BENCH] + args, env=env, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_launcher_spawns_n_ranks_and_prints_one_line(n):
+    p = _run(["--gpus", str(n), "--harness-only"])
+    assert p.returncode == 0, p.stderr
+    lines = [s for s in p.stdout.splitlines() if s.strip()]
+    assert len(lines) == 1, p.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == n and rec["harness_only"]
+    assert [r["rank"] for r in rec["ranks"]] == list(range(n))
+    assert [r["local_rank"] for r in rec["ranks"]] == list(range(n))
+    assert all(r["launched"] for r in rec["ranks"])
+    assert len({r["pid"] for r in rec["ranks"]}) == n       # n distinct processes
+    assert rec["max_rank"] == n - 1                          # the hub's max-reduce
+    assert rec["harness"].startswith("tcp hub")
+
+
+def test_single_rank_runs_in_process():
+    p = _run(["--gpus", "1", "--harness-only"])
+    assert p.returncode == 0, p.stderr
+    rec = json.loads(p.stdout.strip())
+    assert rec["n_gpus"] == 1 and not rec["ranks"][0]["launched"]
+
+
+def test_failing_rank_fails_the_launcher():
+    p = _run(["--gpus", "3", "--harness-only"], {"RSAMD_BENCH_FAIL_RANK": "1"})
+    assert p.returncode != 0
+    assert "rank 1 of 3 exited with status 3" in p.stderr
+    assert not p.stdout.strip()
+
+
+def test_world_mismatch_is_an_error():
+    # an external launcher that formed a different world than --gpus asks for
+    p = _run(["--gpus", "4", "--harness-only"],
+             {"WORLD_SIZE": "2", "RANK": "0", "MASTER_ADDR": "127.0.0.1",
+              "MASTER_PORT": "29777"})
+    assert p.returncode != 0
+    assert "WORLD_SIZE=2 but --gpus=4" in p.stderr

@@ -102,6 +102,23 @@ def test_split_ransac_equals_reference_golden(full, base, worlds):
             assert p2_ == int(z["mt_pos_out"]) and np.array_equal(k2, z["mt_key_out"])
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_split_projection_computes_the_golden_run(ctx, world):
+    # bench.py's parity_mode.split_projection: every emulated rank's steps run alone on this
+    # GPU; the merged result must be the exact run it claims to time
+    z, b = golden("full_c2.npz"), golden("synth_c2.npz")
+    key, pos = _ffi.np_seed(0)
+    rep, best, k2, p2_ = parallel.project_split_np(ctx, b["p1"], b["p2"], int(z["H"]), key,
+                                                   pos, world)
+    assert int(best["index"]) == int(z["best"])
+    assert np.array_equal(parallel.inliers_of(best, b["p1"], b["p2"]),
+                          z["S_ransac"].astype(np.int64))
+    assert p2_ == int(z["mt_pos_out"]) and np.array_equal(k2, z["mt_key_out"])
+    assert rep["world"] == world and len(rep["rank_total_ms"]) == world
+    assert rep["projected_ms"] == max(rep["rank_total_ms"]) > 0
+    assert all(len(v) == world for v in rep["per_rank_ms"].values())
+
+
 def test_split_shard_argument_errors(ctx):
     with pytest.raises(ValueError):
         _ffi.NpShard(ctx, 10, 8, 2, 2)          # rank outside the world

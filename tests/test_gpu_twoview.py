@@ -12,7 +12,7 @@ Bars (BASELINE.json north_star: "within 1e-6 relative on recovered F/R/t"):
 import numpy as np
 import pytest
 
-from conftest import golden
+from conftest import golden, trace_blas_matches
 from oracle import ransac_ref
 from oracle import twoview_ref as tvr
 from tsbb15_amd import fun, lab3, twoview
@@ -275,11 +275,13 @@ def test_gold_standard_trf_retraces_reference_path(ctx):
     a, b, _, z = _gs_case("noisy")
     tr = golden("gs_trace.npz")
     x0 = tr["noisy_x0"]
-    t0 = time.perf_counter()
-    res, xs, cs = _traced_trf(x0, a, b)
-    t1 = time.perf_counter()
-    ores, oxs, ocs = _oracle_trf_trace(x0, a, b)
-    t2 = time.perf_counter()
+    from threadpoolctl import threadpool_limits
+    with threadpool_limits(limits=1, user_api="blas"):   # as the trace was recorded
+        t0 = time.perf_counter()
+        res, xs, cs = _traced_trf(x0, a, b)
+        t1 = time.perf_counter()
+        ores, oxs, ocs = _oracle_trf_trace(x0, a, b)
+        t2 = time.perf_counter()
     first, kx = _first_divergence(xs, cs, oxs, ocs)
     tfirst, tkx = _first_divergence(xs, cs, tr["noisy_kept_x"], tr["noisy_costs"],
                                     tr["noisy_kept_idx"])
@@ -292,6 +294,12 @@ def test_gold_standard_trf_retraces_reference_path(ctx):
     assert first is None and kx is None and len(cs) == len(ocs), (first, kx, len(cs), len(ocs))
     assert res.nfev == ores.nfev and res.status == ores.status
     assert np.array_equal(res.x, ores.x)
+    same, desc = trace_blas_matches()
+    if same:   # the build container's BLAS: the recorded reference trace itself, bit for bit
+        assert tfirst is None and tkx is None and res.nfev == int(tr["noisy_nfev"]), (tfirst, tkx)
+        assert np.array_equal(res.x, tr["noisy_x_final"])
+    else:
+        print(f"[noisy] recorded-trace equality not asserted: another BLAS ({desc})")
 
 
 @pytest.mark.parametrize("tag", ["clean", "noisy"])
@@ -315,7 +323,7 @@ def test_gold_standard_trf_end_to_end(ctx, tag):
           f"|dF| {dF:.3g}")
     assert g.status in (2, 4) and int(z[f"gs_{tag}_status"]) in (2, 4)
     assert g.cost == pytest.approx(float(z[f"gs_{tag}_cost_final"]), rel=5e-2)
-    assert dF <= 1e-3, dF
+    assert dF <= 1e-4, dF      # measured 3.7e-5 (the reference itself moves 3e-4, above)
 
 
 def test_getFFromLabCode_dropin_noisy_pair_trf(ctx):
@@ -325,4 +333,4 @@ def test_getFFromLabCode_dropin_noisy_pair_trf(ctx):
     c1 = golden("dino_c1.npz")
     np.random.seed(0)
     Fg = fun.getFFromLabCode(c1["noisy_p1"], c1["noisy_p2"])
-    assert np.abs(nF(Fg) - nF(c1["noisy_full_F_gold"])).max() <= 1e-3
+    assert np.abs(nF(Fg) - nF(c1["noisy_full_F_gold"])).max() <= 1e-4

@@ -318,6 +318,35 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t bits) {
                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bits), 0u));
 }
 
+// Chunk timeline of the parse (RSAMD_NP_TSTAMP=<file>, tools/np_timeline.py): per chunk
+// kTs words of stamps -- 100 MHz real-time counter and shader-clock cycles at the entry kernel's
+// start / end, the tracking kernel's start / end and the moment the chunk's trajectories are
+// down to one per wave, with the draw positions and hardware ids.  Null in production: the
+// product kernels carry the stamps (read through a relaxed load at each point, so no register
+// holds the pointer), and a stamp never feeds a computed value.
+__device__ unsigned long long *g_np_ts = nullptr;
+constexpr int kTs = 16;
+enum : int {
+  kTsEntryR0 = 0, kTsEntryC0, kTsEntryR1, kTsEntryC1, kTsEntryT, kTsEntryM, kTsEntryHw,
+  kTsTrackR0 = 8, kTsTrackC0, kTsSingleR, kTsSingleT, kTsTrackR1, kTsTrackC1, kTsTrackHw, kTsSingleC
+};
+__device__ __forceinline__ unsigned long long *np_ts() {
+  return __atomic_load_n(&g_np_ts, __ATOMIC_RELAXED);
+}
+__device__ __forceinline__ unsigned long long hw_where() {  // HW_ID (wave, SIMD, CU, SE) | XCC_ID
+  return (static_cast<unsigned long long>(__builtin_amdgcn_s_getreg((31 << 11) | 4)) << 8) |
+         static_cast<unsigned long long>(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7);
+}
+__device__ __forceinline__ void np_stamp(int c, int slot_r, int slot_c) {
+  if (unsigned long long *ts = np_ts()) {
+    ts[static_cast<size_t>(c) * kTs + slot_r] = __builtin_amdgcn_s_memrealtime();
+    ts[static_cast<size_t>(c) * kTs + slot_c] = __builtin_amdgcn_s_memtime();
+  }
+}
+__device__ __forceinline__ void np_stamp_val(int c, int slot, unsigned long long v) {
+  if (unsigned long long *ts = np_ts()) ts[static_cast<size_t>(c) * kTs + slot] = v;
+}
+
 template <bool PY>
 __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
                                                              const uint32_t *__restrict__ draws) {
@@ -334,6 +363,10 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
   const uint32_t *__restrict__ wp = draws + t0;
   uint2 *ev = a.ev + static_cast<size_t>(c) * a.ecap;
   const uint32_t N1 = static_cast<uint32_t>(n1);
+  if (tid == 0) {
+    np_stamp(c, kTsEntryR0, kTsEntryC0);
+    np_stamp_val(c, kTsEntryHw, hw_where());
+  }
   for (int q = tid; q < n1; q += kEntryThreads) {
     st[q] = static_cast<uint16_t>(n1 - q);
     lo[q] = static_cast<uint16_t>(q);
@@ -543,6 +576,9 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
         a.fin_m[c] = m;
         a.ev_n[c] = min(sh_evn, a.ecap);
         if (sh_evn > a.ecap) atomicOr(a.err, 1);
+        np_stamp(c, kTsEntryR1, kTsEntryC1);
+        np_stamp_val(c, kTsEntryT, static_cast<unsigned long long>(t));
+        np_stamp_val(c, kTsEntryM, static_cast<unsigned long long>(m));
       }
       return;
     }
@@ -555,6 +591,9 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
     a.fin_m[c] = m;
     a.ev_n[c] = sh_evn;
     a.tpos[c] = t;
+    np_stamp(c, kTsEntryR1, kTsEntryC1);
+    np_stamp_val(c, kTsEntryT, static_cast<unsigned long long>(t));
+    np_stamp_val(c, kTsEntryM, static_cast<unsigned long long>(m));
   }
 }
 
@@ -824,7 +863,15 @@ __device__ __forceinline__ void np_track_body(const EntryArgs &a, const uint32_t
     s_st[tid] = f >> 16;
     s_lo[tid] = f & 0xffffu;
   }
-  if (tid == 0) s_evn = a.ev_n[c];
+  if (tid == 0) {
+    s_evn = a.ev_n[c];
+    np_stamp(c, kTsTrackR0, kTsTrackC0);
+    np_stamp_val(c, kTsTrackHw, hw_where());
+    if (m <= kTrackWaves) {  // one trajectory per wave from the start
+      np_stamp(c, kTsSingleR, kTsSingleC);
+      np_stamp_val(c, kTsSingleT, static_cast<unsigned long long>(t));
+    }
+  }
   uint32_t nx[kPer];
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
@@ -906,6 +953,10 @@ __device__ __forceinline__ void np_track_body(const EntryArgs &a, const uint32_t
       if (lane == 0) s_m = base;
     }
     __syncthreads();
+    if (tid == 0 && m > kTrackWaves && s_m <= kTrackWaves) {  // down to one per wave
+      np_stamp(c, kTsSingleR, kTsSingleC);
+      np_stamp_val(c, kTsSingleT, static_cast<unsigned long long>(cp));
+    }
     m = uni(s_m);
     t = cp;
     buf ^= 1;
@@ -915,6 +966,7 @@ __device__ __forceinline__ void np_track_body(const EntryArgs &a, const uint32_t
     a.fin_m[c] = m;
     a.ev_n[c] = min(s_evn, a.ecap);
     if (s_evn > a.ecap) atomicOr(a.err, 1);
+    np_stamp(c, kTsTrackR1, kTsTrackC1);
   }
 #ifdef RSAMD_DIAG
   if (a.stats && lane == 0) {
@@ -1633,6 +1685,16 @@ int shard_enqueue_parse(rs_np_shard &w) {
     d_stats = stats_buf;
   }
 #endif
+  // RSAMD_NP_TSTAMP=<file>: the chunk timeline of this parse (g_np_ts), appended to <file>
+  static const char *ts_path = std::getenv("RSAMD_NP_TSTAMP");
+  static unsigned long long *ts_buf = nullptr;
+  static int64_t ts_cap = 0;
+  if (ts_path) {
+    if ((st = sgrow(ts_buf, ts_cap, w.Cr * kTs))) return st;
+    HIP_TRY(hipMemsetAsync(ts_buf, 0, sizeof(unsigned long long) * w.Cr * kTs, s));
+    HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_np_ts), &ts_buf, sizeof(ts_buf), 0,
+                                   hipMemcpyHostToDevice, s));
+  }
   EntryArgs ea{w.d_stream + (w.s_lo - w.wbase), w.Cr * w.Wc, Wc, w.n1, w.d_fin, w.d_fin_m,
                w.d_ev, w.d_ev_n, w.d_tpos, w.ecap, w.d_err, d_stats};
   const bool small = w.n1 < 64;  // several hypothesis ends in one tracking window
@@ -1648,6 +1710,19 @@ int shard_enqueue_parse(rs_np_shard &w) {
            : (hand_of(w.n1) > 64 ? k_np_track128<false> : k_np_track<false, false>))<<<Cr, 64 * kTrackWaves, 0, s>>>(ea, ea.draws);
   }
   HIP_TRY(hipGetLastError());
+  if (ts_path) {
+    // header: n1, chunks, chunk length, draws, rank, world, then kTs words per chunk
+    std::vector<unsigned long long> h(static_cast<size_t>(w.Cr) * kTs + 8, 0ull);
+    const int64_t hd[8] = {w.n1, w.Cr, w.Wc, w.Cr * w.Wc, w.rank, w.world, kTs, 0};
+    for (int k = 0; k < 8; ++k) h[k] = static_cast<unsigned long long>(hd[k]);
+    HIP_TRY(hipMemcpyAsync(h.data() + 8, ts_buf, sizeof(unsigned long long) * w.Cr * kTs,
+                           hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (FILE *f = std::fopen(ts_path, "ab")) {
+      std::fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
+      std::fclose(f);
+    }
+  }
 #ifdef RSAMD_DIAG
   if (d_stats) {
     std::vector<long long> hs(static_cast<size_t>(w.Cr) * 128 + 4);

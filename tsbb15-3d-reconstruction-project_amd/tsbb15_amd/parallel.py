@@ -512,6 +512,93 @@ def ransac_f_split_np(comm, ctx, p1, p2, H, key, pos, thresh=1.5, plan=None, sha
     return best, key2, pos2
 
 
+def project_split_np(ctx, p1, p2, H, key, pos, world, thresh=1.5, plans=None, shards=None):
+    """One-GPU PROJECTION of :func:`ransac_f_split_np` at ``world`` ranks: every rank's steps
+    run one after another on this GPU (nothing else on the device while a step runs), each
+    timed alone, with the exchanges done in host memory.  Per rank: ``parse`` (its chunks'
+    jump / stream / entry / track), ``maps`` (its blob to the host), ``compose`` (all blobs ->
+    its start count), ``evaluate`` (its hypotheses' tuples + solve / count / select, result
+    header).  A rank's projected time is the sum of its steps; the job's is the slowest rank's
+    plus the collectives (not timed here: per segment two all-gathers of a few KB and two of
+    8 B / 2.5 KB, and the final c* all-reduce + candidate all-gather).
+
+    ``plans`` / ``shards`` (one per rank) may be passed in so that a second call times warm
+    buffers.  Returns (report dict, winner record, key', pos'); the winner and state equal
+    the serial run's (the caller checks), so the projection times the exact computation."""
+    import time
+    p1, p2 = _ffi.f64c(p1), _ffi.f64c(p2)
+    W = int(world)
+    own_sh, own = shards is None, plans is None
+    if own_sh:
+        shards = [_ffi.NpShard(ctx, p1.shape[1], 8, W, r) for r in range(W)]
+    if own:
+        plans = []
+    try:
+        if own:
+            for _ in range(W):
+                pl = _ffi.F8Plan(ctx, p1.shape[1], max(1, int(H)))
+                pl.set_points(p1, p2)
+                plans.append(pl)
+        steps = {s: [0.0] * W for s in ("parse", "maps", "compose", "evaluate")}
+        blob_bytes = [0] * W
+        cands = [[] for _ in range(W)]
+        key = np.array(key, dtype=np.uint32, copy=True)
+        pos, done, segments = int(pos), 0, 0
+
+        def timed(step, r, f):
+            ctx.synchronize()
+            t = time.perf_counter()
+            out = f()
+            ctx.synchronize()
+            steps[step][r] += time.perf_counter() - t
+            return out
+
+        while done < H:
+            segments += 1
+            blobs = []
+            for r in range(W):
+                timed("parse", r, lambda: shards[r].parse(key, pos, H - done))
+                blobs.append(timed("maps", r, shards[r].maps))
+                blob_bytes[r] = max(blob_bytes[r], len(blobs[-1]))
+            width = max(len(b) for b in blobs)
+            blobs = [b + bytes(width - len(b)) for b in blobs]
+            stats = [timed("compose", r, lambda: shards[r].compose(blobs)) for r in range(W)]
+            fin = None
+            for r in range(W):
+                got, base, hi, nxt, final_rank = shard_schedule(stats, H - done, r)
+                fidx = got if final_rank == r else -1
+
+                def ev():
+                    f = plans[r].run_np_shard(shards[r], base, hi, nxt, fidx, key, thresh)
+                    if hi > base:
+                        plans[r].result()
+                    return f
+                f = timed("evaluate", r, ev)
+                if hi > base:
+                    cands[r].append(candidates_from_plan(plans[r], done + base))
+                if fidx >= 0:
+                    fin = f
+            key, pos = fin[0].copy(), int(fin[1])
+            done += got
+        local = [np.concatenate(c) if c else np.zeros(0, CAND_DTYPE) for c in cands]
+        allc = np.concatenate(local)
+        cstar = int(allc["count"].max()) if len(allc) else 0
+        best = replay_rule(allc[allc["count"] == cstar] if cstar > 0 else allc[:0])
+    finally:
+        if own_sh:
+            for s in shards:
+                s.close()
+        if own:
+            for pl in plans:
+                pl.close()
+    per_rank = [sum(steps[s][r] for s in steps) * 1e3 for r in range(W)]
+    rep = {"world": W, "segments": segments,
+           "per_rank_ms": {s: [v * 1e3 for v in steps[s]] for s in steps},
+           "rank_total_ms": per_rank, "projected_ms": max(per_rank),
+           "slowest_rank": int(np.argmax(per_rank)), "blob_bytes": blob_bytes}
+    return rep, best, key, pos
+
+
 def inliers_of(best, p1, p2, thresh=1.5):
     """S_RANSAC of a merged winner record (fun.py:316-317, reference-order residuals)."""
     if best is None:
