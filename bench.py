@@ -137,8 +137,25 @@ def cpu_baseline(p1, p2, budget_s, procs):
         res = pool.map(_cpu_worker, [(p1, p2, 1 + k, budget_s) for k in range(procs)])
     agg = sum(d / e for d, e in res)
     cores, ev = host_cores()
+    ref = None
+    try:   # the reference loop itself, measured where it can run (tests/golden/make_ref_rate.py)
+        with open(os.path.join(REPO, "tests", "golden", "ref_rate_c2.json")) as f:
+            rr = json.load(f)
+        ratio = rr["reference_over_port_single_core"]
+        ref = {"measured_in": rr["where"], "what": rr["what"],
+               "single_core_hyp_per_s": rr["single_core_hyp_per_s"],
+               "all_cores_hyp_per_s": rr["all_cores_hyp_per_s"], "all_cores": rr["all_cores"],
+               "port_single_core_hyp_per_s_same_host": rr["port_single_core_hyp_per_s"],
+               "reference_over_port": ratio,
+               "estimated_on_this_host": {"single_core": ratio * one[0] / one[1],
+                                          "all_cores": ratio * agg, "cores": procs},
+               "note": "the reference modules cannot run on the GPU box; their rate here is the "
+                       "port's measured on-box rate times the reference/port ratio measured "
+                       "side by side in the build container"}
+    except (OSError, KeyError, ValueError):
+        pass
     return {"value": agg, "unit": "hypotheses/s", "cores": procs, "kind": "port",
-            "host_cores": ev,
+            "host_cores": ev, "reference_loop": ref,
             "single_core_value": one[0] / one[1],
             "sample": f"{sum(d for d, _ in res)} hypotheses of the same C2 pair "
                       f"(N={p1.shape[1]}) through oracle/ransac_ref.ransac_f (numpy, OpenBLAS "

@@ -249,9 +249,12 @@ typedef struct rs_pnp_result {
 int rs_pnp_dlt(rs_ctx *ctx, const double *X, const double *y, int64_t m, double *R_out,
                double *t_out);
 
-/* RANSAC over DLT minimal samples.  Tuples (H, k) index the `high` set; consensus
- * e = |pi(y) - pi(R x + t)|^2 <= thresh is counted on the `med` set.  mode as for F;
- * in tuple mode host_tuples come from rs_py_shuffle_tuples. */
+/* RANSAC over minimal samples (ransac.py:37-113).  Tuples (H, k) index the `high` set;
+ * consensus e = |pi(y) - pi(R x + t)|^2 <= thresh is counted on the `med` set.  mode as for
+ * F; in tuple mode host_tuples come from rs_py_shuffle_tuples.  k in [6, 16]: the DLT
+ * (pnp.py:132-160).  k = 3: the reference's p3p branch (ransac.py:81-82, 91-111), Lambda
+ * Twist P3P with every pose of a trial scored (trial-major, pose-minor first occurrence;
+ * best_index is the trial).  Replaces ransac.ransac_robust's loop (ransac.py:72-111). */
 int rs_pnp_ransac(rs_ctx *ctx, const double *X_med, const double *y_med, int64_t m_med,
                   const double *X_high, const double *y_high, int64_t m_high, int32_t k,
                   int64_t H, int32_t mode, uint64_t seed, const int32_t *host_tuples,
@@ -401,9 +404,13 @@ typedef struct rs_gs_info {
  * least_squares(jac='2-point') forms (fun.py:358): the (4n, 12 + 3n) Jacobian stored
  * column-major (J[j * 4n + i] = dF_i / dx_j, scipy's Fortran-ordered J_transposed.T), column
  * j = (f(x with x_j -> xp[j]) - f(x)) / dx[j]; xp and dx are the caller's (scipy's step rule).
- * The projection uses numpy's dgemm bits (FMA chain over k), so f equals the reference's
- * residual bit for bit.  The host-side TRF iteration of the reference-faithful gold standard
- * calls this. */
+ * The projection copies the FMA chain of one OpenBLAS dgemm microkernel (the one
+ * OpenBLAS 0.3.29 DYNAMIC_ARCH picks on the build container's SkylakeX cores,
+ * tests/golden/gs_trace_blas.json), so f equals the reference's residual bit for bit where
+ * numpy runs that kernel; under another BLAS kernel (another CPU type, MKL, a threaded or
+ * small-matrix path) the reference's own bits differ and the equality is not guaranteed --
+ * the tests then skip the bit-equality assertions.  The host-side TRF iteration of the
+ * reference-faithful gold standard calls this. */
 int rs_gs_residuals_fd(rs_ctx *ctx, const double *x, const double *xp, const double *dx,
                        const double *pl, const double *pr, int64_t n, double *f, double *J);
 

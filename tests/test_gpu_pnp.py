@@ -91,7 +91,59 @@ def test_ransac_robust_surface(ctx):
     with pytest.raises(ValueError, match="Not implemented yet"):
         ransac.ransac_robust(D, D, 10, 1e-5, 4)
     with pytest.raises(ValueError, match="No PnP algorithm"):
-        ransac.ransac_robust(D, D, 10, 1e-5, 3)
+        ransac.ransac_robust(D, D, 10, 1e-5, 5)
+
+
+def test_ransac_robust_p3p_branch_equals_oracle(ctx):
+    """The n = 3 branch (ransac.py:81-82, 91-111): P3P poses per trial, each scored on D_med,
+    strict ">" over (trial, pose).  Parity unpinned (the reference raises at ransac.py:77 and
+    its p3p is OpenCV): against the oracle restatement at r = 400 on the CPython stream --
+    winner trial and pose, every per-pose count, both consensus sets, R, t -- and the stream
+    advanced as gen_rnd_indices would."""
+    X, _, y, Rt, tt, truth = synth.pnp_scene(300, 0.30, seed=8)
+    thr = (2.0 / 800.0) ** 2
+    r = 400
+    rng_g, rng_o = random.Random(0), random.Random(0)
+    R, t, im, ih, best, cnt = ransac.ransac_pnp(X, y, X, y, r, thr, 3, rng=rng_g)
+    Ro, to, imo, iho, besto, poseo, counts = pnp_ref.ransac_pnp_p3p(y, X, y, X, r, thr,
+                                                                    rng=rng_o, trace=True)
+    assert best == besto and cnt == counts.max()
+    assert np.array_equal(im, imo) and np.array_equal(ih, iho)
+    np.testing.assert_allclose(R, Ro, atol=1e-9)
+    np.testing.assert_allclose(t, to, rtol=1e-9, atol=1e-9)
+    assert rng_g.getstate() == rng_o.getstate()
+    assert truth[im].mean() > 0.95
+    np.testing.assert_allclose(R, Rt, atol=2e-2)
+    # the drop-in surface: lists as ransac.py:109-113 builds them
+    D = np.stack([y, X], axis=1)
+    random.seed(0)
+    R_est, t_est, C_est = ransac.ransac_robust(D, D, r, thr, 3)
+    np.testing.assert_allclose(R_est[0], Ro, atol=1e-9)
+    assert np.array_equal(C_est[0][0], D[imo]) and np.array_equal(C_est[0][1], D[iho])
+
+
+def test_ransac_robust_p3p_known_answers_badino2(ctx):
+    """Noise-free BAdino2 views (negative-scale cameras: the mirrored-depth P3P twin carries
+    the pose): the winner is the reference's camera_resectioning pose and every point agrees."""
+    z = golden("dino_pnp_kat.npz")
+    for v in (3, 17, 30):
+        X, _, y = _view(z, v)
+        D = np.stack([y, X], axis=1)
+        random.seed(v)
+        R_est, t_est, C_est = ransac.ransac_robust(D, D, 50, 1e-10, 3)
+        np.testing.assert_allclose(R_est[0], z["R"][v], atol=1e-6)
+        np.testing.assert_allclose(t_est[0], z["t"][v], rtol=1e-6, atol=1e-6)
+        assert len(C_est[0][0]) == len(X)
+
+
+def test_p3p_philox_sampler(ctx):
+    X, _, y, Rt, tt, truth = synth.pnp_scene(500, 0.30, seed=3)
+    thr = (1.5 / 800.0) ** 2
+    R, t, im, ih, best, cnt = ransac.ransac_pnp(X, y, X, y, 20_000, thr, 3, sampler="philox",
+                                                seed=4)
+    assert np.array_equal(im, np.flatnonzero(thr >= pnp_ref.pose_errors(R, t, X, y)))
+    assert cnt == len(im) and truth[im].mean() > 0.99
+    np.testing.assert_allclose(R, Rt, atol=5e-3)
 
 
 def test_full_size_c3_properties(ctx):
@@ -276,6 +328,35 @@ def test_minimal_pnp_known_answers_badino2(ctx):
         K0 = K
     with pytest.raises(ValueError):
         cv.solvePnP(X[:5], uv[:5], K0, None, flags=cv.SOLVEPNP_P3P)   # P3P takes exactly 4
+
+
+def test_minimal_poses_are_front_facing_on_positive_depth_data(ctx):
+    """OpenCV's EPnP / P3P return front-facing poses only.  The kernels also score the mirrored
+    solution (every depth negated: BAdino2's negative-scale cameras need it), which the pixel
+    error x / z alone cannot tell apart on near-degenerate samples; a mirrored pose must be
+    clearly better to win (pnp_minimal.h kMirrorWins).  On ordinary positive-depth scenes with
+    noisy pixels every returned pose puts all its inliers at z > 0."""
+    rs = np.random.RandomState(11)
+    K = np.array([[700.0, 0.0, 640.0], [0.0, 700.0, 480.0], [0.0, 0.0, 1.0]])
+    for trial in range(40):
+        R, _ = cv.Rodrigues(rs.normal(0, 0.3, 3))
+        t = np.array([rs.uniform(-0.5, 0.5), rs.uniform(-0.5, 0.5), rs.uniform(4, 8)])
+        X = rs.uniform(-1.5, 1.5, (60, 3))
+        uv = cv.project_points(X, cv.Rodrigues(R)[0], t, K) + rs.normal(0, 0.8, (60, 2))
+        s = rs.choice(60, 5, replace=False)
+        for flags, sel in ((cv.SOLVEPNP_EPNP, s), (cv.SOLVEPNP_P3P, s[:4]),
+                           (cv.SOLVEPNP_EPNP, np.arange(60))):
+            ok, rv, tv = cv.solvePnP(X[sel], uv[sel], K, None, flags=flags)
+            if not ok:
+                continue
+            Rm, _ = cv.Rodrigues(rv)
+            z = (X[sel] @ Rm.T + tv[:, 0])[:, 2]
+            assert np.all(z > 0), (trial, flags, z)
+        ok, rv, tv, inl = cv.solvePnPRansac(X, uv, K, None, iterationsCount=200,
+                                            flags=cv.SOLVEPNP_EPNP)
+        assert ok
+        Rm, _ = cv.Rodrigues(rv)
+        assert np.all((X[inl[:, 0]] @ Rm.T + tv[:, 0])[:, 2] > 0), trial
 
 
 def test_solvepnpransac_kernels_and_guess(ctx):

@@ -1,0 +1,49 @@
+"""The oracle's P3P restatement (oracle/pnp_ref.py p3p_lambda_twist, the n = 3 branch of
+ransac.py:81-82) on the CPU: exact poses recovered from noise-free triples, the mirrored twins
+put the three points behind the camera, and the RANSAC restatement finds the pose."""
+import random
+
+import numpy as np
+
+from oracle import pnp_ref
+
+
+def _rot(w):
+    th = np.linalg.norm(w)
+    k = w / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+
+
+def test_p3p_recovers_the_pose():
+    rs = np.random.RandomState(0)
+    found = 0
+    for _ in range(200):
+        R = _rot(rs.normal(0, 0.5, 3))
+        t = np.array([rs.uniform(-1, 1), rs.uniform(-1, 1), rs.uniform(4, 9)])
+        X = rs.uniform(-1.5, 1.5, (3, 3))
+        Y = X @ R.T + t
+        sols = pnp_ref.p3p_lambda_twist(X, pnp_ref.bearings(Y / Y[:, 2:]))
+        assert len(sols) <= 8
+        for Rs, ts, mirrored in sols:
+            assert np.allclose(Rs @ Rs.T, np.eye(3), atol=1e-8) and np.linalg.det(Rs) > 0
+            z = (X @ Rs.T + ts)[:, 2]
+            assert np.all(z < 0) if mirrored else np.all(z > 0)
+        err = min(np.abs(Rs - R).max() + np.abs(ts - t).max() for Rs, ts, m in sols if not m)
+        found += err < 1e-8
+    assert found >= 198, found
+
+
+def test_ransac_p3p_restatement():
+    rs = np.random.RandomState(2)
+    R = _rot(np.array([0.1, 0.3, -0.2]))
+    t = np.array([0.2, -0.1, 6.0])
+    X = rs.uniform(-2, 2, (150, 3))
+    Y = X @ R.T + t
+    y = Y / Y[:, 2:]
+    y[100:, :2] += rs.uniform(-0.2, 0.2, (50, 2))
+    Rb, tb, im, ih, best, pose, counts = pnp_ref.ransac_pnp_p3p(
+        y, X, y, X, 60, 1e-12, rng=random.Random(1), trace=True)
+    assert best >= 0 and counts.max() == len(im) == 100
+    assert np.array_equal(im, np.arange(100))
+    np.testing.assert_allclose(Rb, R, atol=1e-8)

@@ -27,7 +27,7 @@ def main():
     for r in range(runs):
         plan.run(H, mode=_ffi.SAMPLER_PHILOX, seed=r)
         plan.result()
-    raw = np.fromfile(path, dtype=np.uint64).reshape(runs, -1, 4)
+    raw = np.fromfile(path, dtype=np.uint64).reshape(runs, -1, 6)
     for r in (runs - 2, runs - 1):
         rec = raw[r]
         rec = rec[rec[:, 0] > 0]
@@ -37,6 +37,8 @@ def main():
         dur = en - st
         nre = rec[:, 2].astype(np.int64)
         hw = rec[:, 3].astype(np.int64)
+        cyc = (rec[:, 5] - rec[:, 4]).astype(np.float64)      # shader-clock cycles of the wave
+        ghz = cyc / np.maximum(1.0, (rec[:, 1] - rec[:, 0]).astype(np.float64)) * 0.1
         xcc = hw & 7
         hwid = hw >> 8
         simd = (hwid >> 4) & 3
@@ -63,9 +65,23 @@ def main():
                "simd_last_wave_end_p10_p50_p90_us": [
                    round(float(np.percentile([en[sid == k].max() for k in np.unique(sid)], x)), 1)
                    for x in (10, 50, 90)]})
+        # is the spread of equal-work waves a clock effect or a cycle effect?
+        print({"wave_clock_ghz_p10_p50_p90": [round(q(ghz, x), 3) for x in (10, 50, 90)],
+               "wave_cycles_p10_p50_p90": [int(q(cyc, x)) for x in (10, 50, 90)],
+               "corr(duration, cycles)": round(float(np.corrcoef(dur, cyc)[0, 1]), 3),
+               "corr(duration, clock)": round(float(np.corrcoef(dur, ghz)[0, 1]), 3),
+               "corr(end, cycles)": round(float(np.corrcoef(en, cyc)[0, 1]), 3)})
+        for x in range(8):
+            m = xcc == x
+            if m.any():
+                print("  xcc %d: clock p50 %.3f GHz, cycles p50 %d, dur p50 %.1f us"
+                      % (x, np.median(ghz[m]), int(np.median(cyc[m])), np.median(dur[m])))
         first = st < 2.0  # the first round (all resident at once)
         if first.sum() > 10:
             d, k = dur[first], nre[first]
+            cy = cyc[first]
+            print("first round: cycles p10/p50/p90 %d / %d / %d, corr(cycles, retests) %.2f"
+                  % (q(cy, 10), q(cy, 50), q(cy, 90), np.corrcoef(cy, k)[0, 1] if k.std() > 0 else 0.0))
             c = np.corrcoef(d, k)[0, 1] if k.std() > 0 else 0.0
             print("first round: corr(duration, retests) = %.2f" % c)
             for x in range(8):

@@ -33,7 +33,9 @@ def records(path):
 
 
 def pct(a, ps=(0, 10, 50, 90, 100)):
-    return [round(float(np.percentile(a, p)), 3) for p in ps]
+    a = np.asarray(a, dtype=np.float64)
+    a = a[~np.isnan(a)]
+    return [round(float(np.percentile(a, p)), 3) for p in ps] if a.size else None
 
 
 def analyse(h, r):
@@ -68,9 +70,10 @@ def analyse(h, r):
         "entry_hand_m": pct(r[:, E_M]),
         "entry_clock_ghz": pct(clk_e),
         "entry_cycles_per_draw": pct((r[:, E_C1] - r[:, E_C0]) / np.maximum(1, r[:, E_T])),
-        "gap_entry_end_to_track_start_us": round(float(tr0[tracked].min() - e1.max()), 2),
-        "track_start_skew_us": pct(tr0[tracked] - tr0[tracked].min()),
-        "track_kernel_us": round(float(tr1[tracked].max() - tr0[tracked].min()), 1),
+        "gap_entry_end_to_track_start_us": round(float(tr0[tracked].min() - e1.max()), 2) if tracked.any() else None,
+        "track_start_skew_us": pct(tr0[tracked] - tr0[tracked].min()) if tracked.any() else None,
+        "track_kernel_us": round(float(tr1[tracked].max() - tr0[tracked].min()), 1) if tracked.any() else 0.0,
+        "chunks_tracked": int(tracked.sum()),
         "track_dur_us": pct((tr1 - tr0)[tracked]),
         "track_clock_ghz": pct(clk_t[tracked]),
         "multi_phase_us": pct(multi_us[tracked & ~np.isnan(sr)]),
@@ -91,7 +94,7 @@ def analyse(h, r):
     }
     # what the critical path would be at the measured per-phase rates with no skew:
     # entry max + track max, against the sum of per-chunk means
-    out["sum_of_maxima_us"] = round(float((e1 - e0).max() + (tr1 - tr0)[tracked].max()), 1)
+    out["sum_of_maxima_us"] = round(float((e1 - e0).max() + ((tr1 - tr0)[tracked].max() if tracked.any() else 0)), 1)
     out["max_of_sums_us"] = round(float(((e1 - e0) + np.where(tracked, tr1 - tr0, 0)).max()), 1)
     return out
 

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Overlap mode A/B: the GPU tests with RSAMD_OVERLAP=1, then the C2 bench line with RSAMD_OVERLAP=1 (default) and 0.
+# Overlap mode A/B: the GPU tests with RSAMD_OVERLAP=1, then the C2 bench line with RSAMD_OVERLAP=1 and 0 (the default).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/${1:-ovl}

@@ -818,7 +818,11 @@ __global__ __launch_bounds__(256) void k_e5_cands(const int *__restrict__ counts
 // ||d||^2 of every candidate, d_i = max(|r1_i|, |r2_i|) over all points (the quantity the
 // reference's F loop compares on ties, fun.py:317-325): a wave per candidate, the points over
 // the lanes, partial sums combined by a fixed butterfly (deterministic).  (A lane per slot
-// summed 2 000 points serially: 476 us of the C2 E-RANSAC run.)
+// summed 2 000 points serially: 476 us of the C2 E-RANSAC run.)  The summation order is NOT
+// numpy's (np.linalg.norm's pairwise sum over the points) nor the earlier per-slot
+// sequential one, so two candidates whose norms differ by a few ulp can rank differently
+// from a numpy restatement; the E path has no reference counterpart (SURVEY a-15), so the
+// tie-break is deterministic but unpinned at that level.
 __global__ __launch_bounds__(256) void k_e5_norms(const Pt *__restrict__ pts, int n,
                                                   const int *__restrict__ cand,
                                                   const int *__restrict__ ncand,

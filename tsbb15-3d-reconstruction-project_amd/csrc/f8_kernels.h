@@ -79,6 +79,9 @@ hipError_t launch_f8_solve(const Pt *pts, int n, int H, int mode, uint64_t seed,
 // Point-pair packed fp32 counting (guard band + float64 re-test: counts bit-identical to
 // launch_f8_count); ptsq in the k_pack_points32q layout.
 hipError_t set_count_timeline(uint64_t *buf);  // RSAMD_TSTAMP diagnostics (null: off)
+// words per wave of that timeline: real-time start / end, re-tests, HW_ID | XCC_ID,
+// shader-clock start / end
+constexpr int kCountTsWords = 6;
 hipError_t launch_pack_points32q(const Pt *pts, int n, const Frame &fr, float4 *ptsq,
                                  hipStream_t s);
 struct Count32qShape {

@@ -334,6 +334,7 @@ __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ p
   const int64_t end = min(total, pos + per_wave);
   uint64_t *ts = g_count_ts;  // diagnostic wave timeline (RSAMD_TSTAMP), null in production
   const uint64_t t_start = ts ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  const uint64_t c_start = ts ? __builtin_amdgcn_s_memtime() : 0ull;  // shader clock
   int n_retest = 0;  // re-test branches taken (timeline diagnostics)
   while (pos < end) {
     const int grp = static_cast<int>(pos / npad);
@@ -385,12 +386,16 @@ __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ p
     if (gdone) group_done_max(counts, gdone, status, grp, p1 - p0, npad, h, H);
   }
   if (ts && lane == 0) {
-    ts[4 * w] = t_start;
-    ts[4 * w + 1] = __builtin_amdgcn_s_memrealtime();
-    ts[4 * w + 2] = static_cast<uint64_t>(n_retest);
+    uint64_t *o = ts + kCountTsWords * w;
+    o[0] = t_start;
+    o[1] = __builtin_amdgcn_s_memrealtime();
+    o[2] = static_cast<uint64_t>(n_retest);
     // where it ran: HW_ID (wave, SIMD, CU, SE fields) and XCC_ID
-    ts[4 * w + 3] = (static_cast<uint64_t>(__builtin_amdgcn_s_getreg((31 << 11) | 4)) << 8) |
-                    static_cast<uint64_t>(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7);
+    o[3] = (static_cast<uint64_t>(__builtin_amdgcn_s_getreg((31 << 11) | 4)) << 8) |
+           static_cast<uint64_t>(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7);
+    // shader-clock cycles over the wave: with o[0..1] the wave's own clock (cycles / real time)
+    o[4] = c_start;
+    o[5] = __builtin_amdgcn_s_memtime();
   }
 }
 

@@ -2,7 +2,8 @@
 // hypotheses issued back to back.  Replaces the fun.getFFromLabCode hypothesis loop
 // (fun.py:298-328).
 //
-// One HIP stream, two alternating per-run buffer sets.  rs_f8_plan_run(k) enqueues
+// Per-run buffer sets (kBufs) used in rotation.  By default everything runs on the context's
+// HIP stream: rs_f8_plan_run(k) enqueues
 //
 //   k_f8_tail_solve  [selection tail of run k-1 | solve of run k]   (one launch)
 //   k_f8_count32x    counts of run k (+ fused c*)
@@ -13,6 +14,12 @@
 // ~1.5 waves per SIMD) thus share the machine instead of running back to back, with no
 // cross-stream events (each event or wait is a packet the command processor retires
 // between kernels; r01: ~3.5 us each).
+//
+// Optional overlap mode (RSAMD_OVERLAP=1, off by default: measured 2-4 % slower, DESIGN.md
+// "Next"): run k's solve on a side stream ss, its count on the context stream and its tail
+// on a third stream ts, chained by per-buffer-set events (ev_solve / ev_count / ev_tail); a
+// set's solve waits for the tail of the run that used the set kBufs runs back, and the
+// parity samplers wait for the set's last solve before they refill its tuples.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -88,7 +95,7 @@ struct rs_f8_plan {
   // count on the context stream, its tail on ts, chained by events, so the next run's solve and
   // this run's tail fill the CUs the counting kernel's drain leaves idle.  A buffer set's solve
   // waits for the tail of the run that used the set before (kBufs runs back).
-  bool overlap = true;
+  bool overlap = kOverlapDefault != 0;
   hipStream_t ss = nullptr, ts = nullptr;
   hipEvent_t ev_solve[kBufs] = {}, ev_count[kBufs] = {}, ev_tail[kBufs] = {};
   rsd::TailArgs tail{};              // ... its arguments
@@ -229,7 +236,7 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
   p->nospec = env_int("RSAMD_NOSPEC", 0) != 0;
   p->ts_path = std::getenv("RSAMD_TSTAMP");
   if (p->ts_path) {
-    const size_t tsb = sizeof(uint64_t) * 4 * (static_cast<size_t>(p->q_waves) * 64 + 1024);
+    const size_t tsb = sizeof(uint64_t) * rsd::kCountTsWords * (static_cast<size_t>(p->q_waves) * 64 + 1024);
     if (hipMalloc(&p->d_ts, tsb) == hipSuccess) {
       (void)hipMemset(p->d_ts, 0, tsb);
       (void)rsd::set_count_timeline(p->d_ts);
@@ -511,7 +518,7 @@ extern "C" int rs_f8_plan_result(rs_f8_plan *p, rs_f8_result *out, int64_t *inli
   out->n_candidates = r->n_candidates;
   out->guard_mismatch = r->guard_mismatch;
   if (p->d_ts && p->ts_path) {  // diagnostics: append this run's wave timeline
-    std::vector<uint64_t> t(4 * (static_cast<size_t>(p->q_waves) * 64 + 1024));
+    std::vector<uint64_t> t(rsd::kCountTsWords * (static_cast<size_t>(p->q_waves) * 64 + 1024));
     if (hipMemcpy(t.data(), p->d_ts, sizeof(uint64_t) * t.size(), hipMemcpyDeviceToHost) ==
         hipSuccess) {
       if (FILE *f = std::fopen(p->ts_path, "ab")) {

@@ -375,6 +375,53 @@ __global__ __launch_bounds__(64) void k_pnp_solve_min(const PPt *__restrict__ pt
   for (int q = 0; q < 3; ++q) Psoa[(9 + q) * ld + h] = ok ? t[q] : qn;
 }
 
+// The n = 3 branch of ransac_robust (ransac.py:81-82, 91-111): lane per trial, Lambda Twist
+// P3P on the trial's three D_high correspondences (bearings (u, v, 1) / |.|), every pose it
+// yields a hypothesis of its own, as the reference loops over p3p's poses (ransac.py:92) --
+// slot j of trial i is model kP3pSlots i + j, so the strict-">" first-occurrence winner is the
+// reference's trial-major, pose-minor order.  Up to four front-facing solutions, each followed
+// by its mirrored-depth twin (the pose of a negative-scale camera, BAdino2's); empty slots are
+// NaN, which scores no consensus.
+constexpr int kP3pSlots = 8;
+__global__ __launch_bounds__(64) void k_pnp_solve_p3p(const PPt *__restrict__ pts, int m, int H,
+                                                      int mode, uint64_t seed,
+                                                      const int *__restrict__ tuples,
+                                                      double *__restrict__ Psoa, int64_t ld) {
+  const int h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= H) return;
+  int idx[3];
+  if (mode == RSD_SAMPLER_PHILOX) {
+    floyd_sample<3>(seed, static_cast<uint64_t>(h), m, idx);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) idx[i] = tuples[3 * static_cast<int64_t>(h) + i];
+  }
+  double X[3][3], y[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const PPt p = pts[idx[i]];
+    X[i][0] = p.X;
+    X[i][1] = p.Y;
+    X[i][2] = p.Z;
+    const double in = 1.0 / sqrt(p.u * p.u + p.v * p.v + 1.0);
+    y[i][0] = p.u * in;
+    y[i][1] = p.v * in;
+    y[i][2] = in;
+  }
+  double Rs[kP3pSlots][9], ts[kP3pSlots][3];
+  bool mir[kP3pSlots];
+  const int ns = p3p_lambda_twist(X, y, Rs, ts, mir);
+  const double qn = __builtin_nan("");
+  const int64_t base = static_cast<int64_t>(kP3pSlots) * h;
+  for (int s = 0; s < kP3pSlots; ++s) {
+    const bool ok = s < ns;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) Psoa[q * ld + base + s] = ok ? Rs[s][q] : qn;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) Psoa[(9 + q) * ld + base + s] = ok ? ts[s][q] : qn;
+  }
+}
+
 // EPnP over all m correspondences (method 1) or P3P on exactly four (method 2): single lane.
 __global__ __launch_bounds__(64) void k_pnp_minimal_all(const PPt *__restrict__ pts, int m,
                                                         int method, double *__restrict__ out) {
@@ -919,14 +966,18 @@ extern "C" int rs_pnp_ransac(rs_ctx *c, const double *X_med, const double *y_med
                              int64_t *inl_med, int64_t *n_inl_med, int64_t *inl_high,
                              int64_t *n_inl_high) {
   if (!c || !X_med || !y_med || !X_high || !y_high || !out) return fail(RS_EINVAL, "null pointer");
-  if (k < 6 || k > rsd::kMaxK) return fail(RS_EINVAL, "sample size must be in [6, 16] for the DLT");
-  if (mode == RS_SAMPLER_PHILOX && k != 6) return fail(RS_EINVAL, "Philox sampler draws k = 6");
+  if (k != 3 && (k < 6 || k > rsd::kMaxK))
+    return fail(RS_EINVAL, "sample size must be 3 (P3P) or in [6, 16] (the DLT)");
+  if (mode == RS_SAMPLER_PHILOX && k != 6 && k != 3)
+    return fail(RS_EINVAL, "Philox sampler draws k = 6 or k = 3");
   if (mode != RS_SAMPLER_PHILOX && mode != RS_SAMPLER_TUPLES) return fail(RS_EINVAL, "bad mode");
   if (m_high < k)
     return fail(RS_EINVAL,
                 "Cannot generate more indices than the amount of values in the set from which "
                 "they are extracted. n should therefore be smaller or equal to set_length");
-  if (m_med < 1 || H < 1 || H > (1LL << 28) || m_med > (1 << 26) || m_high > (1 << 26))
+  // n = 3: every P3P pose of a trial is a model of its own (k_pnp_solve_p3p)
+  const int64_t Hm = k == 3 ? H * rsd::kP3pSlots : H;
+  if (m_med < 1 || H < 1 || Hm > (1LL << 28) || m_med > (1 << 26) || m_high > (1 << 26))
     return fail(RS_EINVAL, "bad dimensions");
   if (mode == RS_SAMPLER_TUPLES) {
     if (!host_tuples) return fail(RS_EINVAL, "tuples required");
@@ -935,7 +986,7 @@ extern "C" int rs_pnp_ransac(rs_ctx *c, const double *X_med, const double *y_med
         return fail(RS_EINVAL, "tuple index out of range");
   }
   HIP_TRY(hipSetDevice(c->device));
-  const int64_t ld = (H + 63) / 64 * 64;
+  const int64_t ld = (Hm + 63) / 64 * 64;
   const size_t b_in_m = align256(sizeof(double) * 3 * m_med), b_in_h = align256(sizeof(double) * 3 * m_high);
   const size_t b_pm = align256(sizeof(rsd::PPt) * m_med), b_ph = align256(sizeof(rsd::PPt) * m_high);
   const size_t b_tup = align256(sizeof(int) * (mode == RS_SAMPLER_TUPLES ? H * k : 1));
@@ -970,21 +1021,25 @@ extern "C" int rs_pnp_ransac(rs_ctx *c, const double *X_med, const double *y_med
                      static_cast<int>(m_med), pm);
   hipLaunchKernelGGL(rsd::k_pack_ppts, dim3((m_high + 255) / 256), dim3(256), 0, s, dXh, dyh,
                      static_cast<int>(m_high), ph);
-  HIP_TRY(hipMemsetAsync(dcnt, 0, sizeof(int) * H, s));
-  hipLaunchKernelGGL(rsd::k_pnp_solve, dim3((H + 255) / 256), dim3(256), 0, s, ph,
-                     static_cast<int>(m_high), static_cast<int>(H), k, mode, seed, dtup, dP, ld,
-                     0);
+  HIP_TRY(hipMemsetAsync(dcnt, 0, sizeof(int) * Hm, s));
+  if (k == 3)
+    hipLaunchKernelGGL(rsd::k_pnp_solve_p3p, dim3((H + 63) / 64), dim3(64), 0, s, ph,
+                       static_cast<int>(m_high), static_cast<int>(H), mode, seed, dtup, dP, ld);
+  else
+    hipLaunchKernelGGL(rsd::k_pnp_solve, dim3((H + 255) / 256), dim3(256), 0, s, ph,
+                       static_cast<int>(m_high), static_cast<int>(H), k, mode, seed, dtup, dP,
+                       ld, 0);
   HIP_TRY(hipGetLastError());
-  const int64_t groups = (H + 63) / 64;
+  const int64_t groups = (Hm + 63) / 64;
   int64_t nch = std::max<int64_t>(1, std::min<int64_t>((8192 + groups - 1) / groups, (m_med + 63) / 64));
   const int chunk = static_cast<int>((m_med + nch - 1) / nch);
   nch = (m_med + chunk - 1) / chunk;
   const int64_t units = groups * nch;
   hipLaunchKernelGGL(rsd::k_pnp_count, dim3((units + 3) / 4), dim3(256), 0, s, pm,
-                     static_cast<int>(m_med), static_cast<int>(H), dP, ld, chunk,
+                     static_cast<int>(m_med), static_cast<int>(Hm), dP, ld, chunk,
                      static_cast<int>(nch), thresh, rsd::PxMetric{1.0, 0.0, 1.0}, dcnt);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(rsd::k_pnp_select, dim3(1), dim3(1024), 0, s, dcnt, static_cast<int>(H), dP,
+  hipLaunchKernelGGL(rsd::k_pnp_select, dim3(1), dim3(1024), 0, s, dcnt, static_cast<int>(Hm), dP,
                      ld, dres);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(rsd::k_pnp_inliers, dim3(1), dim3(1024), 0, s, pm, static_cast<int>(m_med),
@@ -996,7 +1051,8 @@ extern "C" int rs_pnp_ransac(rs_ctx *c, const double *X_med, const double *y_med
   const auto *r = reinterpret_cast<const rsd::PnpDevResult *>(host.data());
   std::memcpy(out->R, r->R, sizeof(out->R));
   std::memcpy(out->t, r->t, sizeof(out->t));
-  out->best_index = r->best_index;
+  // n = 3: the trial of the winning pose (its slot: best_index % kP3pSlots on the device)
+  out->best_index = k == 3 && r->best_index >= 0 ? r->best_index / rsd::kP3pSlots : r->best_index;
   out->best_count = r->best_count;
   if (n_inl_med) *n_inl_med = r->n_med;
   if (n_inl_high) *n_inl_high = r->n_high;

@@ -28,6 +28,15 @@
 
 namespace rsd {
 
+// A mirrored minimal pose (all depths negated) replaces the best front-facing one only when
+// its error is below kMirrorWins times the front-facing error: OpenCV's EPnP / P3P return
+// front-facing poses only, and the reprojection error x / z cannot tell the two apart on a
+// near-degenerate sample.
+constexpr double kMirrorWins = 0.5;
+__device__ inline bool mirror_wins(double e_mirror, double e_front) {
+  return e_mirror < kMirrorWins * e_front || (e_front != e_front && e_mirror == e_mirror);
+}
+
 // cyclic Jacobi eigen-decomposition of a symmetric N x N matrix (row-major; destroyed):
 // eigenvalues on the diagonal of A, eigenvectors in the columns of V
 template <int N>
@@ -318,7 +327,11 @@ __device__ inline double epnp_pose(PtAt pt, int n, double (&R)[9], double (&t)[3
     err /= n;
     return err == err ? err : INFINITY;
   };
-  double best = INFINITY;
+  // front-facing candidates (every point at z > 0 for the sign OpenCV picks) and mirrored ones
+  // (the points behind the camera: a P = K [R | t] with a negative scale, BAdino2) are kept
+  // apart; a mirrored pose wins only if clearly better (kMirrorWins), so on ordinary
+  // positive-depth data the solver returns what OpenCV's EPnP returns
+  double best = INFINITY, best_m = INFINITY, Rm[9], tm[3];
   for (int N = 1; N <= 3; ++N) {
     double b[4] = {0.0, 0.0, 0.0, 0.0};
     if (N == 1) {  // all four null vectors: b11 b12 b13 b14
@@ -376,12 +389,18 @@ __device__ inline double epnp_pose(PtAt pt, int n, double (&R)[9], double (&t)[3
     for (int mirror = 0; mirror < 2; ++mirror) {
       double Rc[9], tc[3];
       const double e = pose_of(b, mirror != 0, Rc, tc);
-      if (e < best) {
-        best = e;
-        for (int i = 0; i < 9; ++i) R[i] = Rc[i];
-        for (int i = 0; i < 3; ++i) t[i] = tc[i];
+      double &bb = mirror ? best_m : best;
+      if (e < bb) {
+        bb = e;
+        for (int i = 0; i < 9; ++i) (mirror ? Rm : R)[i] = Rc[i];
+        for (int i = 0; i < 3; ++i) (mirror ? tm : t)[i] = tc[i];
       }
     }
+  }
+  if (mirror_wins(best_m, best)) {
+    for (int i = 0; i < 9; ++i) R[i] = Rm[i];
+    for (int i = 0; i < 3; ++i) t[i] = tm[i];
+    return best_m;
   }
   return best;
 }
@@ -435,7 +454,8 @@ __device__ inline void null3(const double (&A)[9], double (&v)[3]) {
 // Up to four poses from three correspondences (world X[i], unit bearings y[i]), each with its
 // mirror (all depths negated); returns their number.
 __device__ inline int p3p_lambda_twist(const double (&X)[3][3], const double (&y)[3][3],
-                                       double (&Rs)[8][9], double (&ts)[8][3]) {
+                                       double (&Rs)[8][9], double (&ts)[8][3],
+                                       bool (&mirrored)[8]) {
   const double b01 = dot3(y[0], y[1]), b02 = dot3(y[0], y[2]), b12 = dot3(y[1], y[2]);
   double d01[3], d02[3], d12[3];
   for (int k = 0; k < 3; ++k) {
@@ -577,6 +597,7 @@ __device__ inline int p3p_lambda_twist(const double (&X)[3][3], const double (&y
             Rs[ns][3 * r + c] = (Pm[3 * r] * Xi[c] + Pm[3 * r + 1] * Xi[3 + c] + Pm[3 * r + 2] * Xi[6 + c]) / dx;
         for (int r = 0; r < 3; ++r)
           ts[ns][r] = P[0][r] - (Rs[ns][3 * r] * X[0][0] + Rs[ns][3 * r + 1] * X[0][1] + Rs[ns][3 * r + 2] * X[0][2]);
+        mirrored[ns] = mirror != 0;
         ++ns;
         }
       }
@@ -602,22 +623,28 @@ __device__ inline double p3p_pose(PtAt pt, double (&R)[9], double (&t)[3]) {
     y[i][2] = in;
   }
   double Rs[8][9], ts[8][3];
-  const int ns = p3p_lambda_twist(X, y, Rs, ts);
+  bool mir[8];
+  const int ns = p3p_lambda_twist(X, y, Rs, ts, mir);
   const PPt p3 = pt(3);
-  double best = INFINITY;
+  double best[2] = {INFINITY, INFINITY};  // front-facing, mirrored (see kMirrorWins)
+  int arg[2] = {-1, -1};
   for (int s = 0; s < ns; ++s) {
     const double x = Rs[s][0] * p3.X + Rs[s][1] * p3.Y + Rs[s][2] * p3.Z + ts[s][0];
     const double yy = Rs[s][3] * p3.X + Rs[s][4] * p3.Y + Rs[s][5] * p3.Z + ts[s][1];
     const double z = Rs[s][6] * p3.X + Rs[s][7] * p3.Y + Rs[s][8] * p3.Z + ts[s][2];
     const double du = p3.u - x / z, dv = p3.v - yy / z;
     const double e = sqrt(du * du + dv * dv);
-    if (e < best) {
-      best = e;
-      for (int i = 0; i < 9; ++i) R[i] = Rs[s][i];
-      for (int i = 0; i < 3; ++i) t[i] = ts[s][i];
+    const int k = mir[s] ? 1 : 0;
+    if (e < best[k]) {
+      best[k] = e;
+      arg[k] = s;
     }
   }
-  return best;
+  const int k = mirror_wins(best[1], best[0]) ? 1 : 0;
+  if (arg[k] < 0) return INFINITY;
+  for (int i = 0; i < 9; ++i) R[i] = Rs[arg[k]][i];
+  for (int i = 0; i < 3; ++i) t[i] = ts[arg[k]][i];
+  return best[k];
 }
 
 }  // namespace rsd

@@ -7,15 +7,17 @@
                                                stream is advanced exactly as the reference
   * ``norm_p``, ``cart``, ``dpp``, ``dpp_squared``, ``calc_y_prim``  ransac.py:21-35
   * ``ransac_robust(D_med, D_high, r, thresh, n)``  ransac.py:37-113 with its intended
-    semantics on the GPU: r trials sampling n >= 6 correspondences of D_high (CPython
-    stream), the DLT of pnp.py:132-160 as the minimal solver, consensus
-    ``thresh >= |pi(y) - pi(R x + t)|^2`` on D_med and D_high, largest D_med consensus wins
-    (strict ">", first occurrence).
+    semantics on the GPU: r trials sampling n correspondences of D_high (CPython stream);
+    n = 3 is the reference's own branch (ransac.py:81-82): P3P (Lambda Twist) with every pose
+    it yields scored (ransac.py:91-111, trial-major, pose-minor), n >= 6 the DLT of
+    pnp.py:132-160; consensus ``thresh >= |pi(y) - pi(R x + t)|^2`` on D_med and D_high,
+    largest D_med consensus wins (strict ">", first occurrence).
 
 Data layout of D_med / D_high: (N, 2, 3) float arrays, D[:, 0] = y (C-normalised homogeneous
 image point), D[:, 1] = x (3D point), the pairs ``ransac.py:68-69,96-97`` index.  The
-reference's own loop raises before its first trial (ransac.py:77, SURVEY.md 8(a) a-10);
-n == 3 (p3p through OpenCV) and n == 4 are not provided, as there.
+reference's own loop raises before its first trial (ransac.py:77), so
+every result here is parity-unpinned (tests: the oracle restatement and BAdino2 known
+answers); n == 4 raises "Not implemented yet", as there.
 """
 from __future__ import annotations
 
@@ -125,9 +127,9 @@ def ransac_pnp(X_med, y_med, X_high, y_high, r, thresh, n=6, rng=None, sampler="
     for X, y in ((X_med, y_med), (X_high, y_high)):
         if X.ndim != 2 or X.shape[1] != 3 or y.shape != X.shape:
             raise ValueError("X must be (m, 3) and y (m, 3)")
-    if n < 6:
-        raise ValueError("No PnP algorithm with the given n is implemented (the DLT needs "
-                         "n >= 6; p3p wraps OpenCV in the reference)")
+    if n != 3 and n < 6:
+        raise ValueError("No PnP algorithm with the given n is implemented (P3P takes n = 3, "
+                         "the DLT n >= 6)")
     r = int(r)
     ctx = ctx or _ffi.default_context()
     if sampler == "exact":
@@ -136,6 +138,8 @@ def ransac_pnp(X_med, y_med, X_high, y_high, r, thresh, n=6, rng=None, sampler="
     else:
         if len(X_high) < n:
             raise ValueError("Cannot generate more indices than the amount of values in the set")
+        if n not in (3, 6):
+            raise ValueError("the Philox sampler draws n = 3 or n = 6")
         mode, tp = _ffi.SAMPLER_PHILOX, None
     res = _ffi.PnpResult()
     im = np.empty(len(X_med), np.int64)
