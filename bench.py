@@ -542,6 +542,21 @@ def harness_only(rank, world, dist):
                           else "one process"}), flush=True)
 
 
+def load_clock():
+    """The clock the counting kernel holds (newest committed profiles/r*_count_clock.json)."""
+    import glob
+    found = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_count_clock.json")))
+    if not found:
+        return None
+    try:
+        with open(found[-1]) as f:
+            d = json.load(f)
+        return {"held_clock_ghz": d["held_clock_ghz"], "source": os.path.relpath(found[-1], REPO),
+                "valu_bound_us_at_held_clock": d.get("valu_bound_us_at_held_clock")}
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -720,6 +735,13 @@ def main():
         "kernels_ms": {"k_f8_count32q": c_ms, "k_f8_solve": km["solve_ms"],
                        "run_device_total": km["total_ms"]},
     }
+    clk = load_clock()
+    if clk:
+        # DVFS: under this launch the chip holds ~1.95 GHz, not the 2.4 GHz of the nominal
+        # peak; the fraction of the peak at the held clock (measured in-kernel, committed)
+        peak_held = PEAK_FP32_VALU_TFLOPS * clk["held_clock_ghz"] / 2.4
+        line["roofline"]["held_clock"] = dict(clk, peak_at_held_clock=peak_held,
+                                              frac_at_held_clock=achieved / peak_held)
     if pmc:
         line["hbm_roofline"] = {"bound": "hbm", "achieved": pmc / (c_ms * 1e-3) / 1e9,
                                 "peak": PEAK_HBM_GBS, "unit": "GB/s",

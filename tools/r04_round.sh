@@ -15,6 +15,7 @@ tail -4 $OUT/pytest_gpu.log
 RSAMD_TSTAMP=/tmp/cts.bin timeout -k 10 200 python tools/count_timeline.py > $OUT/count_timeline.txt 2>&1 || { echo count timeline failed; tail $OUT/count_timeline.txt; exit 1; }
 cat $OUT/count_timeline.txt
 timeout -k 10 200 python tools/np_timeline.py 10000 20000 3 > $OUT/np_timeline_n10k.json 2> $OUT/np_timeline.err || { echo timeline failed; tail $OUT/np_timeline.err; exit 1; }
+bash tools/e5_split_ab.sh $TAG/e5 || exit 1
 timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; tail -20 $OUT/bench.err; exit 1; }
 python - <<PY
 import json

@@ -359,6 +359,12 @@ struct E5Args {
   double *Mg, *Bas, *Bg;
   int *okg;
   int64_t ldw;
+  // two-phase root finding (k_e5_roots): after `split` sweeps the samples whose roots are still
+  // moving leave their root state (zr, zi, converged per lane: 3 x 16 doubles) in zst and their
+  // index in defer_list; phase 2 resumes them packed four to a wave (split = 0: one phase)
+  int split;
+  int *defer_list, *defer_n;
+  double *zst;
 };
 
 __device__ __forceinline__ void norm_pt(const double (&K)[9], double u, double v, double &x,
@@ -482,10 +488,22 @@ __global__ __launch_bounds__(64) void k_e5_gj(E5Args a) {
 #ifndef RSD_E5_ROOTS_WAVES
 #define RSD_E5_ROOTS_WAVES 2  // minimum waves per SIMD (157 VGPRs: 3; a cap at 4 spills and is slower) (A/B builds: tools/build_ab.sh)
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSD_E5_ROOTS_WAVES))) void k_e5_roots(E5Args a) {
+// Two phases (a.split > 0): four samples share a wave and the wave sweeps until the slowest
+// of them converges, so phase 1 stops after a.split sweeps and hands the rows still moving to
+// phase 2, which resumes them from their saved roots packed densely (rows never interact --
+// the sweep reads only its own row, converged roots stay frozen -- so the roots, and every
+// solution, are the same as one phase's).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSD_E5_ROOTS_WAVES))) void k_e5_roots(E5Args a, int phase) {
   const int r = threadIdx.x & 15;
-  const int s = blockIdx.x * (blockDim.x >> 4) + (threadIdx.x >> 4);
-  const bool live = s < a.S;  // the whole row runs the sweeps (DPP), dead rows are masked out
+  const int row_id = blockIdx.x * (blockDim.x >> 4) + (threadIdx.x >> 4);
+  int s = row_id;
+  bool live = s < a.S;  // the whole row runs the sweeps (DPP), dead rows are masked out
+  if (phase == 2) {     // a deferred sample, or a dead row
+    const int nd = *a.defer_n;
+    if (static_cast<int>(blockIdx.x) * static_cast<int>(blockDim.x >> 4) >= nd) return;  // all dead
+    live = row_id < nd;
+    s = live ? a.defer_list[row_id] : a.S - 1;
+  }
   const int sc = live ? s : a.S - 1;
   const bool ok = live && a.okg[sc];
   double Bm[6][10];
@@ -566,7 +584,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSD_E5_ROOT
     }
   }
   bool conv = !(r < deg);
-  for (int it = 0; it < 100; ++it) {
+  int it0 = 0, it1 = 100;
+  double *zs = a.zst + (static_cast<int64_t>(sc) * 16 + r) * 3;
+  if (phase == 1) it1 = a.split;
+  if (phase == 2) {  // resume the saved sweep state
+    zr = zs[0];
+    zi = zs[1];
+    conv = !live || zs[2] != 0.0;
+    it0 = a.split;
+  }
+  for (int it = it0; it < it1; ++it) {
     if (!__ballot(!conv)) break;  // wave-uniform: every row keeps sweeping while one root moves
     double sr = 0.0, si = 0.0;  // sum_{j != r} 1 / (z_r - z_j), the previous sweep's z_j
     aberth_sum<1>(zr, zi, sr, si);
@@ -607,6 +634,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSD_E5_ROOT
         zi = xi - wi;
         if (fabs(wr) + fabs(wi) <= 2.0 * 2.220446049250313e-16 * (fabs(zr) + fabs(zi))) conv = true;
       }
+    }
+  }
+  if (phase == 1) {  // rows still moving go to phase 2 with their state
+    const uint64_t rowm = 0xffffull << (threadIdx.x & 48);
+    if (live && (__ballot(!conv) & rowm)) {
+      zs[0] = zr;
+      zs[1] = zi;
+      zs[2] = conv ? 1.0 : 0.0;
+      if (r == 0) a.defer_list[atomicAdd(a.defer_n, 1)] = s;
+      return;
     }
   }
   // lane r's solution: real iterated roots (|Im| <= 1e-6 max(1, |Re|)) and the zero roots
@@ -970,10 +1007,27 @@ using rs::hip_fail;
 
 static size_t e5_align(size_t b) { return (b + 255) / 256 * 256; }
 constexpr int kE5CountWaves = 6144;  // resident waves of k_f8_count32q (as the F-RANSAC plan)
+// sweeps of the root finder's first phase (0: one phase).  Measured at C2 (20 000 samples,
+// profiles/r04b_e5_split_ab.txt, two passes): one phase 0.440 / 0.446 ms per E-RANSAC run;
+// split after 5 / 6 / 8 / 10 / 12 sweeps 0.52 / 0.52-0.54 / 0.50 / 0.46-0.47 / 0.48 ms -- the
+// second phase's set-up (B rows, polynomial, start state) costs more than the drained sweeps
+constexpr int kE5SplitDefault = 0;
 
-// bytes of the three solve kernels' work buffers for S samples
+// bytes of the three solve kernels' work buffers for S samples: the 10 x 20 system, null
+// basis and B rows (296 doubles), Gauss-Jordan flags, the deferred list + count and the
+// deferred rows' root state (48 doubles) of the two-phase root finder
 static size_t e5_work_bytes(int64_t S) {
-  return e5_align(sizeof(double) * 296 * static_cast<size_t>(S)) + e5_align(sizeof(int) * S);
+  return e5_align(sizeof(double) * 296 * static_cast<size_t>(S)) + e5_align(sizeof(int) * S) +
+         e5_align(sizeof(int) * (S + 1)) + e5_align(sizeof(double) * 48 * static_cast<size_t>(S));
+}
+
+// sweeps before the root finder's rows still moving are repacked (RSAMD_E5_SPLIT; 0: one phase)
+static int e5_split() {
+  static const int v = [] {
+    const char *e = std::getenv("RSAMD_E5_SPLIT");
+    return e ? std::max(0, std::min(99, std::atoi(e))) : kE5SplitDefault;
+  }();
+  return v;
 }
 
 // the solve (k_e5_build, k_e5_gj, k_e5_roots) into a.Esoa / a.Fsoa, work buffers from `work`
@@ -983,12 +1037,28 @@ static int launch_e5_solve(rsd::E5Args &a, char *work, hipStream_t s) {
   a.Mg = reinterpret_cast<double *>(work);
   a.Bas = a.Mg + 200 * S;
   a.Bg = a.Bas + 36 * S;
-  a.okg = reinterpret_cast<int *>(work + e5_align(sizeof(double) * 296 * static_cast<size_t>(S)));
+  char *w2 = work + e5_align(sizeof(double) * 296 * static_cast<size_t>(S));
+  a.okg = reinterpret_cast<int *>(w2);
+  w2 += e5_align(sizeof(int) * S);
+  a.defer_n = reinterpret_cast<int *>(w2);
+  a.defer_list = a.defer_n + 1;
+  w2 += e5_align(sizeof(int) * (S + 1));
+  a.zst = reinterpret_cast<double *>(w2);
+  a.split = e5_split();
   hipLaunchKernelGGL(rsd::k_e5_build, dim3((S + 63) / 64), dim3(64), 0, s, a);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(rsd::k_e5_gj, dim3((S + 1) / 2), dim3(64), 0, s, a);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(rsd::k_e5_roots, dim3((S + 15) / 16), dim3(256), 0, s, a);
+  if (a.split > 0) {
+    HIP_TRY(hipMemsetAsync(a.defer_n, 0, sizeof(int), s));
+    hipLaunchKernelGGL(rsd::k_e5_roots, dim3((S + 15) / 16), dim3(256), 0, s, a, 1);
+    HIP_TRY(hipGetLastError());
+    // every row may have been deferred: the grid covers S rows, the rows past the deferred
+    // count exit at once
+    hipLaunchKernelGGL(rsd::k_e5_roots, dim3((S + 15) / 16), dim3(256), 0, s, a, 2);
+  } else {
+    hipLaunchKernelGGL(rsd::k_e5_roots, dim3((S + 15) / 16), dim3(256), 0, s, a, 0);
+  }
   HIP_TRY(hipGetLastError());
   return RS_OK;
 }

@@ -29,10 +29,12 @@
 namespace rsd {
 
 // A mirrored minimal pose (all depths negated) replaces the best front-facing one only when
-// its error is below kMirrorWins times the front-facing error: OpenCV's EPnP / P3P return
+// its error is below kMirrorWins times the front-facing error (on noise-free negative-scale
+// views the ratio is ~1e-10; with noisy pixels a 4-point P3P mirror reached 0.27 of the
+// front-facing error on positive-depth data, tests/test_gpu_pnp.py): OpenCV's EPnP / P3P return
 // front-facing poses only, and the reprojection error x / z cannot tell the two apart on a
 // near-degenerate sample.
-constexpr double kMirrorWins = 0.5;
+constexpr double kMirrorWins = 1e-2;
 __device__ inline bool mirror_wins(double e_mirror, double e_front) {
   return e_mirror < kMirrorWins * e_front || (e_front != e_front && e_mirror == e_mirror);
 }
