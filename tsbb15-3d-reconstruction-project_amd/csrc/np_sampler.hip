@@ -619,6 +619,14 @@ constexpr int kTrackWaves = RSAMD_TRACK_WAVES;  // waves per chunk workgroup, >=
 #define RSAMD_KCHECK 4096
 #endif
 constexpr int kCheck = RSAMD_KCHECK;  // draws per checkpoint interval (A/B builds may override)
+// multi-trajectory windows through fast_window (bucket constants on the vector unit) before
+// window_step; single-trajectory windows too with RSAMD_ONE_VALU (A/B builds may override)
+#ifndef RSAMD_MULTI_VALU
+#define RSAMD_MULTI_VALU 1
+#endif
+#ifndef RSAMD_ONE_VALU
+#define RSAMD_ONE_VALU 0
+#endif
 
 template <bool PY, bool SMALL>
 __device__ __forceinline__ uint32_t wrap_state(int si, int n1) {
@@ -683,6 +691,47 @@ __device__ __forceinline__ uint64_t window_step(uint32_t w, uint64_t wm, uint32_
   sl_out = sl;
   i = wrap_state<PY, SMALL>(static_cast<int>(i) - static_cast<int>(__popcll(acc)), n1);
   return acc;
+}
+
+// The fast two-bucket window of window_step for a FULL window (64 draws), with the bucket
+// constants computed on the VECTOR unit: i is copied into a VGPR, the mask, the bucket's lowest
+// state and the fast-path test are VALU, and the test reaches the scalar unit as one ballot.  A
+// CU runs 16-32 busy tracking waves that share ONE scalar unit (1 instruction per cycle)
+// against four SIMD-32 vector units (2 cycles per wave64 instruction each), and window_step
+// spends ~35 scalar instructions per window against ~17 vector ones (ISA of the round-3
+// kernel), so the scalar unit bounds the multi-trajectory phase; this form spends ~8 scalar and
+// ~25 vector instructions.  Returns false (and leaves i alone) where the fast path does not
+// hold; the caller then runs window_step.  Same fixed point, so the same accept mask.
+template <bool PY>
+__device__ __forceinline__ bool fast_window(uint32_t w, uint32_t &i) {
+  uint32_t iv;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(iv) : "s"(i));  // a vector copy of the uniform state
+  uint32_t lowest, lowest2, sh = 0, M = 0;
+  if constexpr (PY) {
+    sh = static_cast<uint32_t>(__builtin_clz(iv + 1u));
+    lowest = (1u << (31u - sh)) - 1u;
+    lowest2 = sh < 30u ? (1u << (30u - sh)) - 1u : 0x7fffffffu;
+  } else {
+    M = 0xffffffffu >> __builtin_clz(iv);
+    lowest = (M >> 1) + 1u;
+    lowest2 = M > 1u ? (M >> 2) + 1u : 0x7fffffffu;
+  }
+  const bool fast = iv >= lowest2 + 63u && lowest2 >= 1u && lowest2 != 0x7fffffffu;
+  if (__builtin_amdgcn_ballot_w64(fast) == 0ull) return false;  // uniform: all lanes agree
+  const int c = static_cast<int>(iv) - static_cast<int>(lowest);
+  const int vh = static_cast<int>(iv) - static_cast<int>(PY ? (w >> sh) : (w & M));
+  const int vl = static_cast<int>(iv) - static_cast<int>(PY ? (w >> (sh + 1u)) : (w & (M >> 1)));
+  // convergence checked every second round (a fixed point is stable)
+  uint64_t a0 = __ballot(vh >= 0), a1, a2;
+  do {
+    int rk = static_cast<int>(lane_rank(a0));
+    a1 = __ballot(rk <= (rk <= c ? vh : vl));
+    rk = static_cast<int>(lane_rank(a1));
+    a2 = __ballot(rk <= (rk <= c ? vh : vl));
+    a0 = a2;
+  } while (a2 != a1);
+  i -= static_cast<uint32_t>(__popcll(a2));
+  return true;
 }
 
 // One checkpoint interval [t, cp) of a single trajectory (the common case once a chunk's
@@ -750,6 +799,11 @@ __device__ __forceinline__ uint32_t track_one(const EntryArgs &a, const uint32_t
       const uint32_t w = q[k];
       q[k] = sw[(d - t + 64 * (kAhead + k) + lane) & (kCheck - 1)];
       const int dk = d + 64 * k;
+#if RSAMD_ONE_VALU
+      if (dk + 64 <= cp && fast_window<PY>(w, i)) continue;
+      if (dk < cp) track_window<PY, SMALL>(n1, ecap, w, s_evn, ev, i, range, dk, cp);
+      continue;
+#endif
       if (dk + 64 <= cp) {
         if (i < lowest || i > (PY ? (lowest << 1) : (lowest << 1) - 1u)) set_bucket();  // left it
         if (i >= fast_min) {
@@ -786,13 +840,18 @@ __device__ __forceinline__ void track_interval(const EntryArgs &a, const uint32_
                                                long long *dg) {
   const int lane = threadIdx.x & 63;
   const int n1 = a.n1;
-  uint32_t i[R], range[R];
+  uint32_t i[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int q = wv + (r < nq ? r : nq - 1) * kTrackWaves;
     i[r] = uni(s_st[q]);
-    range[r] = uni(s_lo[q] | (s_lo[q + 1 == m ? 0 : q + 1] << 16));
   }
+  // the member range of chain r, read from LDS only where a wrap is logged (rare): SGPRs are
+  // what limits this kernel's residency (two 16-wave workgroups per CU need <= ~84)
+  auto range_of = [&](int r) {
+    const int q = wv + r * kTrackWaves;
+    return s_lo[q] | (s_lo[q + 1 == m ? 0 : q + 1] << 16);
+  };
   int d = t;
   uint32_t wn = sw[lane];  // draws beyond cp are never accepted (lanes >= Wn)
   while (d < cp) {
@@ -800,9 +859,85 @@ __device__ __forceinline__ void track_interval(const EntryArgs &a, const uint32_
     const uint64_t wm = Wn == 64 ? ~0ull : ((1ull << Wn) - 1ull);
     const uint32_t w = wn;
     if (d + 64 < cp) wn = sw[(d + 64 - t + lane) & (kCheck - 1)];
+#if RSAMD_LOCKSTEP
+    if (R <= 4 && Wn == 64) {
+      // the chains' fast windows in lockstep: their fixed-point rounds interleaved instruction
+      // by instruction, so one chain's dependency latency is another's issue slot (a chain
+      // alone is latency bound, ~8 cycles per instruction).  A chain outside the fast path (or
+      // r >= nq) gets "always accept" thresholds, converges at once and is run by window_step
+      // afterwards; each chain's own fixed point is the sequential answer as before.
+      int cc[R], vh[R], vl[R];
+      bool fv[R];  // per lane (all lanes agree): kept in VGPRs, balloted at the end
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        uint32_t iv;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(iv) : "s"(i[r]));
+        uint32_t lowest, lowest2, sh = 0, M = 0;
+        if constexpr (PY) {
+          sh = static_cast<uint32_t>(__builtin_clz(iv + 1u));
+          lowest = (1u << (31u - sh)) - 1u;
+          lowest2 = sh < 30u ? (1u << (30u - sh)) - 1u : 0x7fffffffu;
+        } else {
+          M = 0xffffffffu >> __builtin_clz(iv);
+          lowest = (M >> 1) + 1u;
+          lowest2 = M > 1u ? (M >> 2) + 1u : 0x7fffffffu;
+        }
+        const bool f = r < nq && iv >= lowest2 + 63u && lowest2 >= 1u && lowest2 != 0x7fffffffu;
+        fv[r] = f;
+        cc[r] = static_cast<int>(iv) - static_cast<int>(lowest);
+        vh[r] = f ? static_cast<int>(iv) - static_cast<int>(PY ? (w >> sh) : (w & M)) : 64;
+        vl[r] = f ? static_cast<int>(iv) - static_cast<int>(PY ? (w >> (sh + 1u)) : (w & (M >> 1))) : 64;
+      }
+      uint64_t a1[R], a2[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) a2[r] = __ballot(vh[r] >= 0);
+      uint64_t diff;
+      do {
+        diff = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          int rk = static_cast<int>(lane_rank(a2[r]));
+          a1[r] = __ballot(rk <= (rk <= cc[r] ? vh[r] : vl[r]));
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int rk = static_cast<int>(lane_rank(a1[r]));
+          a2[r] = __ballot(rk <= (rk <= cc[r] ? vh[r] : vl[r]));
+          diff |= a1[r] ^ a2[r];
+        }
+      } while (diff);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (__builtin_amdgcn_ballot_w64(fv[r]) != 0ull) {
+          i[r] -= static_cast<uint32_t>(__popcll(a2[r]));
+        } else if (r < nq) {
+          uint64_t wr;
+          uint32_t sl;
+          (void)window_step<PY, SMALL>(w, wm, i[r], n1, wr, sl);
+          if (wr) {
+            int eb = 0;
+            if (lane == 0) eb = atomicAdd(s_evn, __popcll(wr));
+            eb = __shfl(eb, 0);
+            if (((wr >> lane) & 1ull)) {
+              const int e = eb + static_cast<int>(lane_rank(wr));
+              if (e < a.ecap) ev[e] = make_uint2(static_cast<uint32_t>(d + lane + 1), range_of(r));
+            }
+          }
+        }
+      }
+#ifdef RSAMD_DIAG
+      dg[0] += 1;
+#endif
+      d += 64;
+      continue;
+    }
+#endif
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (r < nq) {
+#if RSAMD_MULTI_VALU
+        if (Wn == 64 && fast_window<PY>(w, i[r])) continue;
+#endif
         uint64_t wr;
         uint32_t sl;
         (void)window_step<PY, SMALL>(w, wm, i[r], n1, wr, sl);
@@ -812,7 +947,7 @@ __device__ __forceinline__ void track_interval(const EntryArgs &a, const uint32_
           eb = __shfl(eb, 0);
           if (((wr >> lane) & 1ull)) {
             const int e = eb + static_cast<int>(lane_rank(wr));
-            if (e < a.ecap) ev[e] = make_uint2(static_cast<uint32_t>(d + lane + 1), range[r]);
+            if (e < a.ecap) ev[e] = make_uint2(static_cast<uint32_t>(d + lane + 1), range_of(r));
           }
         }
       }
@@ -905,7 +1040,9 @@ __device__ __forceinline__ void np_track_body(const EntryArgs &a, const uint32_t
     }
     else if (nq == 2) track_interval<2, PY, SMALL>(a, sw, s_st, s_lo, &s_evn, ev, m, wq, 2, t, cp, dg);
     else if (nq > 2 && nq <= 4) track_interval<4, PY, SMALL>(a, sw, s_st, s_lo, &s_evn, ev, m, wq, nq, t, cp, dg);
-    else if (nq > 4) track_interval<8, PY, SMALL>(a, sw, s_st, s_lo, &s_evn, ev, m, wq, nq, t, cp, dg);
+    else if constexpr (CAP > 4 * kTrackWaves) {  // more than four per wave: the 128-entry list
+      if (nq > 4) track_interval<8, PY, SMALL>(a, sw, s_st, s_lo, &s_evn, ev, m, wq, nq, t, cp, dg);
+    }
 #ifdef RSAMD_DIAG
     {
       const long long dc = __builtin_amdgcn_s_memtime() - c0;  // busy cycles of this wave
@@ -986,8 +1123,15 @@ __device__ __forceinline__ void np_track_body(const EntryArgs &a, const uint32_t
 // The tracking kernel must stay within ~80 SGPRs: at 84-86 it loses its second 16-wave
 // workgroup per CU (+1.3 ms at C2).  The 64-entry kernel needs 70; the 128-entry one (large N)
 // is capped at 72 (spilling ~20 SGPRs to VGPR lanes: 86 uncapped).
+#ifndef RSAMD_TRACK_SGPR
+#define RSAMD_TRACK_SGPR 0  // >0: cap the 64-entry tracking kernel's SGPRs (A/B builds)
+#endif
 template <bool PY, bool SMALL>
-__global__ __launch_bounds__(64 * kTrackWaves) void k_np_track(EntryArgs a,
+__global__ __launch_bounds__(64 * kTrackWaves)
+#if RSAMD_TRACK_SGPR
+__attribute__((amdgpu_num_sgpr(RSAMD_TRACK_SGPR)))
+#endif
+void k_np_track(EntryArgs a,
                                                                 const uint32_t *__restrict__ draws) {
   np_track_body<PY, SMALL, 64>(a, draws);
 }
