@@ -9,10 +9,10 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd $R
-RSAMD_LIB=$R/tsbb15-3d-reconstruction-project_amd/lib_ab/ls80/librsamd.so timeout -k 10 400 python -u -m pytest tests/test_gpu_np_sampler.py tests/test_gpu_full_parity.py tests/test_gpu_np_shard.py -x -q --timeout 200 --timeout-method thread > $OUT/pytest_np.log 2>&1 || { echo np tests failed; tail -30 $OUT/pytest_np.log; exit 1; }
+RSAMD_LIB=$R/tsbb15-3d-reconstruction-project_amd/lib_ab/w14ls/librsamd.so timeout -k 10 400 python -u -m pytest tests/test_gpu_np_sampler.py tests/test_gpu_full_parity.py tests/test_gpu_np_shard.py -x -q --timeout 200 --timeout-method thread > $OUT/pytest_np.log 2>&1 || { echo np tests failed; tail -30 $OUT/pytest_np.log; exit 1; }
 tail -2 $OUT/pytest_np.log
 for pass in 1 2; do
-for v in prod ls80 ls84; do
+for v in prod w14ls w12ls; do
   if [ $v = prod ]; then unset RSAMD_LIB; else export RSAMD_LIB=$R/tsbb15-3d-reconstruction-project_amd/lib_ab/$v/librsamd.so; fi
   echo "== $v pass $pass" | tee -a $OUT/probe.txt
   timeout -k 10 150 python tools/np_kw_probe.py >> $OUT/probe.txt 2>&1 || { echo probe failed; tail $OUT/probe.txt; exit 1; }
@@ -23,7 +23,7 @@ unset RSAMD_LIB
 cat $OUT/probe.txt
 python - <<PY
 import json
-for v in ("prod", "ls80", "ls84"):
+for v in ("prod", "w14ls", "w12ls"):
     r = json.load(open("$OUT/tl_%s.json" % v))["last_run"]
     print(v, "entry", r["entry_kernel_us"], "track", r["track_kernel_us"], "multi", r["multi_phase_us"], "single", r["single_phase_us"], "cpd", r["single_cycles_per_draw"])
 PY
