@@ -627,14 +627,9 @@ constexpr int kCheck = RSAMD_KCHECK;  // draws per checkpoint interval (A/B buil
 #ifndef RSAMD_MULTI_VALU
 #define RSAMD_MULTI_VALU 1
 #endif
-// lockstep group size (chains interleaved per fixed point)
-#ifndef RSAMD_LOCKSTEP_G
-#define RSAMD_LOCKSTEP_G 2
-#endif
-// single-trajectory windows of 128 draws (one Jacobi fixed point over two 64-draw halves)
-#ifndef RSAMD_ONE128
-#define RSAMD_ONE128 0
-#endif
+// (Measured and removed, round 4, commit "Parse A/B: lockstep chain groups": the chains of a
+// wave in lockstep -- fixed-point rounds interleaved -- and 128-draw single-trajectory
+// windows; DESIGN.md §5 "Round 4".)
 
 template <bool PY, bool SMALL>
 __device__ __forceinline__ uint32_t wrap_state(int si, int n1) {
@@ -786,7 +781,7 @@ __device__ __forceinline__ uint32_t track_one(const EntryArgs &a, const uint32_t
   // second round (a fixed point is stable, so an extra round changes nothing).  C2 stream
   // 7.49 -> 6.82 ms (the same fixed point with per-window constants, window mask and a check
   // every round: window_step)
-  uint32_t M = 0, sh = 0, lowest = 0, fast_min = 0xffffffffu, fast_min128 = 0xffffffffu;
+  uint32_t M = 0, sh = 0, lowest = 0, fast_min = 0xffffffffu;
   auto set_bucket = [&]() {
     uint32_t lowest2;
     if constexpr (PY) {
@@ -799,76 +794,8 @@ __device__ __forceinline__ uint32_t track_one(const EntryArgs &a, const uint32_t
       lowest2 = M > 1u ? (M >> 2) + 1u : 0x7fffffffu;
     }
     fast_min = lowest2 >= 1u && lowest2 < 0x7fffffffu ? lowest2 + 63u : 0xffffffffu;
-    fast_min128 = lowest2 >= 1u && lowest2 < 0x7fffffffu ? lowest2 + 127u : 0xffffffffu;
   };
   set_bucket();
-#if RSAMD_ONE128
-  // 128-draw windows: two 64-draw windows in one Jacobi fixed point (lane l holds draws l and
-  // 64 + l; the second half's ranks start at the first half's accept count of the SAME round),
-  // so a round covers 128 draws for about the latency of one 64-draw round.  Lanes < k of the
-  // 128 are right after k rounds from any start, and a fixed point is the sequential answer.
-  // Valid while every state the window can reach lies in i's bucket or the one below
-  // (i - 127 >= the lower bucket's lowest state); otherwise the two windows run one by one.
-  auto one_window = [&](uint32_t w, int dk) {
-    if (dk + 64 <= cp) {
-      if (i < lowest || i > (PY ? (lowest << 1) : (lowest << 1) - 1u)) set_bucket();
-      if (i >= fast_min) {
-        const int c = static_cast<int>(i) - static_cast<int>(lowest);
-        const int vh = static_cast<int>(i) - static_cast<int>(PY ? (w >> sh) : (w & M));
-        const int vl = static_cast<int>(i) - static_cast<int>(PY ? (w >> (sh + 1u)) : (w & (M >> 1)));
-        uint64_t a0 = __ballot(vh >= 0), a1, a2;
-        do {
-          int rk = static_cast<int>(lane_rank(a0));
-          a1 = __ballot(rk <= (rk <= c ? vh : vl));
-          rk = static_cast<int>(lane_rank(a1));
-          a2 = __ballot(rk <= (rk <= c ? vh : vl));
-          a0 = a2;
-        } while (a2 != a1);
-        i -= static_cast<uint32_t>(__popcll(a2));
-        return;
-      }
-    }
-    if (dk < cp) {
-      track_window<PY, SMALL>(n1, ecap, w, s_evn, ev, i, range, dk, cp);
-      set_bucket();
-    }
-  };
-  for (int d = t; d < cp; d += 64 * kAhead) {
-#pragma unroll
-    for (int k = 0; k < kAhead; k += 2) {
-      const uint32_t w0 = q[k], w1 = q[k + 1];
-      q[k] = sw[(d - t + 64 * (kAhead + k) + lane) & (kCheck - 1)];
-      q[k + 1] = sw[(d - t + 64 * (kAhead + k + 1) + lane) & (kCheck - 1)];
-      const int dk = d + 64 * k;
-      if (dk + 128 <= cp) {
-        if (i < lowest || i > (PY ? (lowest << 1) : (lowest << 1) - 1u)) set_bucket();
-        if (i >= fast_min128) {
-          const int c = static_cast<int>(i) - static_cast<int>(lowest);
-          const int vh0 = static_cast<int>(i) - static_cast<int>(PY ? (w0 >> sh) : (w0 & M));
-          const int vl0 = static_cast<int>(i) - static_cast<int>(PY ? (w0 >> (sh + 1u)) : (w0 & (M >> 1)));
-          const int vh1 = static_cast<int>(i) - static_cast<int>(PY ? (w1 >> sh) : (w1 & M));
-          const int vl1 = static_cast<int>(i) - static_cast<int>(PY ? (w1 >> (sh + 1u)) : (w1 & (M >> 1)));
-          uint64_t a = __ballot(vh0 >= 0), b = __ballot(vh1 >= 0), a1, b1;
-          do {
-            int r0 = static_cast<int>(lane_rank(a));
-            int r1 = __popcll(a) + static_cast<int>(lane_rank(b));
-            a1 = __ballot(r0 <= (r0 <= c ? vh0 : vl0));
-            b1 = __ballot(r1 <= (r1 <= c ? vh1 : vl1));
-            r0 = static_cast<int>(lane_rank(a1));
-            r1 = __popcll(a1) + static_cast<int>(lane_rank(b1));
-            a = __ballot(r0 <= (r0 <= c ? vh0 : vl0));
-            b = __ballot(r1 <= (r1 <= c ? vh1 : vl1));
-          } while (a != a1 || b != b1);
-          i -= static_cast<uint32_t>(__popcll(a) + __popcll(b));
-          continue;
-        }
-      }
-      one_window(w0, dk);
-      one_window(w1, dk + 64);
-    }
-  }
-  return i;
-#endif
   for (int d = t; d < cp; d += 64 * kAhead) {
 #pragma unroll
     for (int k = 0; k < kAhead; ++k) {
@@ -930,86 +857,6 @@ __device__ __forceinline__ void track_interval(const EntryArgs &a, const uint32_
     const uint64_t wm = Wn == 64 ? ~0ull : ((1ull << Wn) - 1ull);
     const uint32_t w = wn;
     if (d + 64 < cp) wn = sw[(d + 64 - t + lane) & (kCheck - 1)];
-#if RSAMD_LOCKSTEP
-    if (R <= 4 && Wn == 64) {  // (the 8-per-wave path of the 128-entry list stays sequential)
-      // the chains' fast windows in lockstep groups of G: their fixed-point rounds interleaved
-      // instruction by instruction, so one chain's dependency latency is another's issue slot
-      // (a chain alone is latency bound, ~8 cycles per instruction).  A chain outside the fast
-      // path (or r >= nq) gets "always accept" thresholds, converges at once and is run by
-      // window_step afterwards; each chain's own fixed point is the sequential answer as before.
-      constexpr int G = R < RSAMD_LOCKSTEP_G ? R : RSAMD_LOCKSTEP_G;
-#pragma unroll
-      for (int g = 0; g < R; g += G) {
-        if (g >= nq) break;
-        int cc[G], vh[G], vl[G];
-        bool fv[G];  // per lane (all lanes agree): kept in VGPRs, balloted at the end
-#pragma unroll
-        for (int j = 0; j < G; ++j) {
-          const int r = g + j;
-          uint32_t iv;
-          asm volatile("v_mov_b32 %0, %1" : "=v"(iv) : "s"(i[r]));
-          uint32_t lowest, lowest2, sh = 0, M = 0;
-          if constexpr (PY) {
-            sh = static_cast<uint32_t>(__builtin_clz(iv + 1u));
-            lowest = (1u << (31u - sh)) - 1u;
-            lowest2 = sh < 30u ? (1u << (30u - sh)) - 1u : 0x7fffffffu;
-          } else {
-            M = 0xffffffffu >> __builtin_clz(iv);
-            lowest = (M >> 1) + 1u;
-            lowest2 = M > 1u ? (M >> 2) + 1u : 0x7fffffffu;
-          }
-          const bool f = r < nq && iv >= lowest2 + 63u && lowest2 >= 1u && lowest2 != 0x7fffffffu;
-          fv[j] = f;
-          cc[j] = static_cast<int>(iv) - static_cast<int>(lowest);
-          vh[j] = f ? static_cast<int>(iv) - static_cast<int>(PY ? (w >> sh) : (w & M)) : 64;
-          vl[j] = f ? static_cast<int>(iv) - static_cast<int>(PY ? (w >> (sh + 1u)) : (w & (M >> 1))) : 64;
-        }
-        uint64_t a1[G], a2[G];
-#pragma unroll
-        for (int j = 0; j < G; ++j) a2[j] = __ballot(vh[j] >= 0);
-        bool more;
-        do {
-#pragma unroll
-          for (int j = 0; j < G; ++j) {
-            const int rk = static_cast<int>(lane_rank(a2[j]));
-            a1[j] = __ballot(rk <= (rk <= cc[j] ? vh[j] : vl[j]));
-          }
-          more = false;
-#pragma unroll
-          for (int j = 0; j < G; ++j) {
-            const int rk = static_cast<int>(lane_rank(a1[j]));
-            a2[j] = __ballot(rk <= (rk <= cc[j] ? vh[j] : vl[j]));
-            more = more || a1[j] != a2[j];
-          }
-        } while (more);
-#pragma unroll
-        for (int j = 0; j < G; ++j) {
-          const int r = g + j;
-          if (__builtin_amdgcn_ballot_w64(fv[j]) != 0ull) {
-            i[r] -= static_cast<uint32_t>(__popcll(a2[j]));
-          } else if (r < nq) {
-            uint64_t wr;
-            uint32_t sl;
-            (void)window_step<PY, SMALL>(w, wm, i[r], n1, wr, sl);
-            if (wr) {
-              int eb = 0;
-              if (lane == 0) eb = atomicAdd(s_evn, __popcll(wr));
-              eb = __shfl(eb, 0);
-              if (((wr >> lane) & 1ull)) {
-                const int e = eb + static_cast<int>(lane_rank(wr));
-                if (e < a.ecap) ev[e] = make_uint2(static_cast<uint32_t>(d + lane + 1), range_of(r));
-              }
-            }
-          }
-        }
-      }
-#ifdef RSAMD_DIAG
-      dg[0] += 1;
-#endif
-      d += 64;
-      continue;
-    }
-#endif
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (r < nq) {
