@@ -101,11 +101,6 @@ int rs_np_choice_tuples_gpu(rs_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int6
 int rs_py_shuffle_tuples_gpu(rs_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int64_t n,
                              int32_t k, int64_t count, int32_t *out);
 
-/* Process-wide counters of the GPU stream parse (diagnostics, no reference counterpart):
- * out[0] segment parses with seeded chunks, out[1] of them failed over to the all-entry parse
- * (a carry met none of a chunk's records), out[2] all-entry segment parses. */
-int rs_np_parse_stats(int64_t *out);
-
 /* Sharded parity stream ("the host sampler must emit tuples in stream order
  * and hand each GPU its slice; that serial step is the scaling limiter").  The numpy (py = 0)
  * or CPython (py = 1) stream of fun.py:305-306 / ransac.py:12-19 is cut into world x Cr

@@ -48,38 +48,6 @@ def test_gpu_stream_c2_size(ctx):
     _same(2000, 8, 100000, seed=11)
 
 
-def _parse_delta(fn):
-    a = _ffi.np_parse_stats()
-    fn()
-    b = _ffi.np_parse_stats()
-    return {k: b[k] - a[k] for k in a}
-
-
-@pytest.mark.parametrize("n,count", [(1000, 20000), (2000, 30000), (3000, 20000)])
-def test_gpu_stream_seeded_chunks(ctx, monkeypatch, n, count):
-    """Seeded chunks (512 evenly spread entries, the previous chunk's trajectories carried in
-    until they meet a recorded list) give the host replay's tuples and state -- by default, with
-    few seeds, and when every carry misses the records (two records per chunk: the parse fails
-    over to every entry state) -- and so does the all-entry parse."""
-    d = _parse_delta(lambda: _same(n, 8, count, seed=n + 1))
-    assert d["seeded"] >= 1 and d["fallbacks"] == 0, d
-    monkeypatch.setenv("RSAMD_NP_SEEDS", "0")
-    d = _parse_delta(lambda: _same(n, 8, count, seed=n + 2))
-    assert d["seeded"] == 0 and d["all_entry"] >= 1, d
-    monkeypatch.setenv("RSAMD_NP_SEEDS", "96")
-    _same(n, 8, count, seed=n + 3)
-    monkeypatch.setenv("RSAMD_NP_SEEDS", "512")
-    monkeypatch.setenv("RSAMD_NP_SEEDREC", "1")
-    d = _parse_delta(lambda: _same(n, 8, count, seed=n + 4))
-    assert d["fallbacks"] >= 1, d
-
-
-def test_gpu_stream_c2_size_is_seeded(ctx):
-    """The C2 parse runs seeded chunks without a fall-back."""
-    d = _parse_delta(lambda: _same(2000, 8, 100000, seed=12))
-    assert d["seeded"] == 1 and d["fallbacks"] == 0 and d["all_entry"] == 0, d
-
-
 def test_gpu_stream_reference_goldens(ctx):
     z = golden("synth_c2.npz")
     tup, key, pos = _ffi.np_choice_tuples_gpu(z["mt_key_in"], z["mt_pos_in"], 2000, 8,

@@ -12,13 +12,8 @@
 //                   states are i in 1..N-1, trajectories that meet merge, and they stay in
 //                   cyclic order, so a sorted list with member ranges (lo) describes the map
 //                   entry -> exit state.  Every wrap (hypothesis end) of every trajectory is
-//                   logged with the member range it belongs to.  Seeded chunks (large N and
-//                   long chunks) start from K evenly spread entry states instead of all N - 1
-//                   and record their list every few thousand draws;
-//   3c. k_np_extend the previous chunk's surviving trajectories continue into a seeded chunk
-//                   until each meets one of its recorded lists: from there on it IS that seed's
-//                   trajectory (exact), and its wraps before the meeting are logged on the side;
-//   4. compose      the per-chunk maps (C lookups) -> the true entry state per chunk;
+//                   logged with the member range it belongs to;
+//   4. host         compose the per-chunk maps (C lookups) -> the true entry state per chunk;
 //   5. k_np_filter  keep the logged wraps whose member range holds the true entry: these are
 //                   exactly the hypothesis starts; k_np_starts gathers them in order;
 //   6. k_np_tuples  one lane per hypothesis: re-parse its own words, keep the swap partners
@@ -36,7 +31,6 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
-#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -89,19 +83,6 @@ constexpr int kRFast = 8;                    // slots per thread of the branch-f
 __host__ __device__ constexpr int hand_of(int n1) { return n1 >= 4096 ? 128 : 64; }
 
 constexpr uint32_t kSentinel = 0x80000000u;  // an empty slot: never reaches 0 within kW steps
-
-// Seeded chunks.  From all N - 1 entries the dense parse spends most of its time while more
-// than 512 trajectories are alive (C2: the multi-slot path and its compactions, 1.35e6 of
-// 2.4e6 cycles per chunk); a chunk that starts from K = 512 evenly spread entries is in the
-// one-slot path from its first draw and reaches the hand-over at the same draw count
-// (simulation, tools/seed_sim.c: 66 trajectories after 2^14 draws from 512 seeds, 69 from all
-// 1 999).  Its map is then exact only at the seeds, so the previous chunk's final trajectories
-// are carried into it (k_np_extend) until they meet one of its recorded lists -- at most a few
-// ten thousand draws (2^13 in 99 % of 4 000 simulated carries at N = 2 000, 47 104 at most).
-// A carry that meets none of the records fails the segment over to the all-entry parse.
-constexpr int kRec = 128;                    // recorded lists per seeded chunk
-constexpr int kSeeds = 512;                  // default seeds per chunk (N - 1 > kSeeds)
-constexpr int kExtSlots = 16;                // carry waves per chunk (each takes g = j, j + 16, ..)
 
 __device__ __forceinline__ uint32_t twist(uint32_t a, uint32_t b) {
   const uint32_t y = (a & kUpper) | (b & kLower);
@@ -302,27 +283,7 @@ struct EntryArgs {
   int ecap;
   int *err;
   long long *stats;       // RSAMD_DIAG builds only: per-chunk tracking statistics (else null)
-  // seeded chunks (K > 0): chunk c starts from K seeds unless c == 0 && first_all; its list is
-  // recorded (rec: [C][kRec][RW] entries lo | state << 16, rec_tm: [C][kRec] (draw, count),
-  // rec_n: [C] records) at t = 0, at the entry kernel's compactions every rec_stride draws and
-  // at every tracking checkpoint
-  int K, first_all, RW, rec_stride, nrec_max;
-  uint32_t *rec;
-  int2 *rec_tm;
-  int *rec_n;
-  // carries (k_np_track, at a chunk's end, into the next seeded chunk up to that chunk's entry
-  // records; k_np_extend takes the rest): rec_ne [C] the entry kernel's record count, mode [C],
-  // ext [C][gcap] (0xffffffff: unresolved), ext_n [C][gcap], ext_ev [C][gcap][ecx]
-  int *rec_ne;
-  const int *mode;
-  uint32_t *ext;
-  int *ext_n;
-  uint32_t *ext_ev;
-  int gcap, ecx, Cl;      // Cl: chunks of the (rank's) segment
 };
-__device__ __forceinline__ bool seeded_chunk(const EntryArgs &a, int c) {
-  return a.K > 0 && !(c == 0 && a.first_all);
-}
 
 __device__ __forceinline__ int block_excl_scan(int v, int *sh, int *total) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -406,37 +367,13 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
     np_stamp(c, kTsEntryR0, kTsEntryC0);
     np_stamp_val(c, kTsEntryHw, hw_where());
   }
-  // a seeded chunk starts from K evenly spread entries (entry 0, state n1, among them) and
-  // records its list (the seeds, then at compactions every rec_stride draws).  The record
-  // state lives in LDS, read inside a compaction and advanced by thread 0 after its last
-  // barrier: as registers it stays live through the parse loop (15 more SGPR spills)
-  __shared__ uint32_t *s_rb;
-  __shared__ int2 *s_rt;
-  __shared__ int *s_rn, *s_rne;  // this chunk's record counts (read at the exits)
-  __shared__ int s_nrec, s_rnext, s_rstride, s_rmax, s_rw;
-  const bool sd = seeded_chunk(a, c);
-  const int m0 = sd ? min(a.K, n1) : n1;
-  for (int q = tid; q < m0; q += kEntryThreads) {
-    const int e = sd ? static_cast<int>(static_cast<int64_t>(q) * n1 / m0) : q;
-    st[q] = static_cast<uint16_t>(n1 - e);
-    lo[q] = static_cast<uint16_t>(e);
-    if (sd) a.rec[static_cast<size_t>(c) * kRec * a.RW + q] = static_cast<uint32_t>(e) | (static_cast<uint32_t>(n1 - e) << 16);
+  for (int q = tid; q < n1; q += kEntryThreads) {
+    st[q] = static_cast<uint16_t>(n1 - q);
+    lo[q] = static_cast<uint16_t>(q);
   }
-  if (tid == 0) {
-    sh_evn = 0;
-    s_rb = sd ? a.rec + static_cast<size_t>(c) * kRec * a.RW : nullptr;
-    s_rt = a.rec_tm + static_cast<size_t>(c) * kRec;
-    if (sd) s_rt[0] = make_int2(0, m0);
-    s_nrec = sd ? 1 : 0;
-    s_rnext = a.rec_stride;
-    s_rstride = a.rec_stride;
-    s_rmax = a.nrec_max;
-    s_rw = a.RW;
-    s_rn = a.rec_n + c;
-    s_rne = a.rec_ne + c;
-  }
+  if (tid == 0) sh_evn = 0;
   __syncthreads();
-  int m = m0, t = 0;
+  int m = n1, t = 0;
   const int hand = hand_of(n1);
   const int nfast = fast_batches(n1), nfastm = fast_batches_multi(n1);
 #ifdef RSAMD_DIAG
@@ -594,13 +531,10 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
       for (int p = k0; p < k1; ++p) cnt += st[p] != st[p == 0 ? m - 1 : p - 1] ? 1 : 0;
       int total;
       int o = block_excl_scan(cnt, sh_red, &total);
-      // this compaction's list goes to the next record (seeded chunks, every rec_stride draws)
-      uint32_t *rb = s_rb && s_nrec < s_rmax && t >= s_rnext ? s_rb + static_cast<size_t>(s_nrec) * s_rw : nullptr;
       for (int p = k0; p < k1; ++p) {
         if (st[p] != st[p == 0 ? m - 1 : p - 1]) {
           st2[o] = st[p];
           lo2[o] = lo[p];
-          if (rb) rb[o] = lo[p] | (static_cast<uint32_t>(st[p]) << 16);
           ++o;
         }
       }
@@ -608,16 +542,10 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
         if (tid == 0) {
           st2[0] = st[0];
           lo2[0] = lo[0];
-          if (rb) rb[0] = lo[0] | (static_cast<uint32_t>(st[0]) << 16);
         }
         total = 1;
       }
-      if (rb && tid == 0) s_rt[s_nrec] = make_int2(t, total);
       __syncthreads();
-      if (rb && tid == 0) {
-        ++s_nrec;
-        s_rnext = t + s_rstride;
-      }
       uint16_t *x = st;
       st = st2;
       st2 = x;
@@ -647,8 +575,6 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
       if (tid == 0) {
         a.fin_m[c] = m;
         a.ev_n[c] = min(sh_evn, a.ecap);
-        *s_rn = s_nrec;
-        *s_rne = s_nrec;
         if (sh_evn > a.ecap) atomicOr(a.err, 1);
         np_stamp(c, kTsEntryR1, kTsEntryC1);
         np_stamp_val(c, kTsEntryT, static_cast<unsigned long long>(t));
@@ -665,8 +591,6 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
     a.fin_m[c] = m;
     a.ev_n[c] = sh_evn;
     a.tpos[c] = t;
-    *s_rn = s_nrec;
-    *s_rne = s_nrec;
     np_stamp(c, kTsEntryR1, kTsEntryC1);
     np_stamp_val(c, kTsEntryT, static_cast<unsigned long long>(t));
     np_stamp_val(c, kTsEntryM, static_cast<unsigned long long>(m));
@@ -705,7 +629,10 @@ constexpr int kCheck = RSAMD_KCHECK;  // draws per checkpoint interval (A/B buil
 #endif
 // (Measured and removed, round 4, commit "Parse A/B: lockstep chain groups": the chains of a
 // wave in lockstep -- fixed-point rounds interleaved -- and 128-draw single-trajectory
-// windows; DESIGN.md §5 "Round 4".)
+// windows; commit "Parse A/B: seeded chunks": chunks parsed from 512 spread entries with the
+// previous chunk's trajectories carried in -- entry 1.23 -> 0.85 ms at C2, but the carries'
+// heavy tail (tools/seed_sim.c) cost 0.21-0.27 ms more and the parse stayed at 6.25-6.32 ms;
+// DESIGN.md §5 "Round 4".)
 
 template <bool PY, bool SMALL>
 __device__ __forceinline__ uint32_t wrap_state(int si, int n1) {
@@ -969,17 +896,7 @@ __device__ __forceinline__ void np_track_body(const EntryArgs &a, const uint32_t
   // them; a window's read is issued one window ahead), the next interval in flight in VGPRs
   __shared__ uint32_t s_w[2][kCheck];
   __shared__ uint32_t s_st[CAP], s_lo[CAP];
-  __shared__ int s_m, s_evn, s_nrec, s_rw, s_rslot, s_rmax;
-  // this chunk's records (null: not seeded), read from LDS where used: kernel arguments the
-  // compiler would hoist into SGPRs for the whole kernel (its residency needs <= ~80)
-  __shared__ uint32_t *s_rec;
-  __shared__ int2 *s_rtm;
-  // the carries at the chunk's end (null s_cxr: none), read from LDS where used
-  __shared__ const uint32_t *s_cxr;  // the next chunk's records
-  __shared__ const int2 *s_cxt;
-  __shared__ uint32_t *s_cxo, *s_cxe;
-  __shared__ int *s_cxn;
-  __shared__ int s_cxne, s_cxecx;
+  __shared__ int s_m, s_evn;
   constexpr int kStride = 64 * kTrackWaves;
   constexpr int kPer = (kCheck + kStride - 1) / kStride;  // draws per thread per interval
   const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = uni(tid >> 6);
@@ -1011,19 +928,6 @@ __device__ __forceinline__ void np_track_body(const EntryArgs &a, const uint32_t
   }
   if (tid == 0) {
     s_evn = a.ev_n[c];
-    s_nrec = a.rec_n[c];
-    s_rec = seeded_chunk(a, c) ? a.rec + static_cast<size_t>(c) * kRec * a.RW : nullptr;
-    s_rtm = a.rec_tm + static_cast<size_t>(c) * kRec;
-    s_rw = a.RW;
-    s_rmax = a.nrec_max;
-    const bool cx = a.ext && c + 1 < a.Cl && a.mode[c + 1];
-    s_cxr = cx ? a.rec + static_cast<size_t>(c + 1) * kRec * a.RW : nullptr;
-    s_cxt = a.rec_tm + static_cast<size_t>(c + 1) * kRec;
-    s_cxo = a.ext + static_cast<size_t>(c + 1) * a.gcap;
-    s_cxn = a.ext_n + static_cast<size_t>(c + 1) * a.gcap;
-    s_cxe = a.ext_ev + static_cast<size_t>(c + 1) * a.gcap * a.ecx;
-    s_cxne = cx ? a.rec_ne[c + 1] : 0;
-    s_cxecx = a.ecx;
     np_stamp(c, kTsTrackR0, kTsTrackC0);
     np_stamp_val(c, kTsTrackHw, hw_where());
     if (m <= kTrackWaves) {  // one trajectory per wave from the start
@@ -1111,11 +1015,7 @@ __device__ __forceinline__ void np_track_body(const EntryArgs &a, const uint32_t
         }
         base += static_cast<int>(__popcll(kb[h]));
       }
-      if (lane == 0) {
-        s_m = base;
-        // seeded chunks record the merged list at cp (for the carries of k_np_extend)
-        s_rslot = s_rec && s_nrec < s_rmax ? s_nrec++ : -1;
-      }
+      if (lane == 0) s_m = base;
     }
     __syncthreads();
     if (tid == 0 && m > kTrackWaves && s_m <= kTrackWaves) {  // down to one per wave
@@ -1123,71 +1023,12 @@ __device__ __forceinline__ void np_track_body(const EntryArgs &a, const uint32_t
       np_stamp_val(c, kTsSingleT, static_cast<unsigned long long>(cp));
     }
     m = uni(s_m);
-    if (const int rs = s_rslot; rs >= 0) {
-      if (tid < m) s_rec[static_cast<size_t>(rs) * s_rw + tid] = s_lo[tid] | (s_st[tid] << 16);
-      if (tid == 0) s_rtm[rs] = make_int2(cp, m);
-    }
     t = cp;
     buf ^= 1;
-  }
-  // The carries into the next chunk (seeded): each final trajectory g continues through the next
-  // chunk's draws up to its entry records (written by the previous launch); one that meets a
-  // record resolves here, the others stay unresolved for k_np_extend.  (The simulation puts 99 %
-  // of them within 2^13 draws; the next chunk's entry kernel recorded its list every 1 024.)
-  if (const uint32_t *xr = s_cxr; xr && s_cxne > 0) {
-    const int nre = s_cxne, ecx = s_cxecx, rw = s_rw;
-    const int2 *xt = s_cxt;
-    const uint32_t *__restrict__ wq = wp + T;  // the next chunk's draw 0 (T = W here)
-    for (int g = wv; g < m; g += kTrackWaves) {
-      uint32_t i = uni(s_st[g]);
-      uint32_t *evx = s_cxe + static_cast<size_t>(g) * ecx;
-      int ne = 0, d = 0;
-      uint32_t res = 0xffffffffu;
-      uint32_t wn = wq[lane];
-      for (int r = 0; r < nre; ++r) {
-        const int2 tm = xt[r];
-        const int tr = uni(tm.x), mr = uni(tm.y);
-        while (d < tr) {
-          const int Wn = min(64, tr - d);
-          const uint64_t wm = Wn == 64 ? ~0ull : ((1ull << Wn) - 1ull);
-          const uint32_t w = wn;
-          wn = wq[d + Wn + lane];
-          uint64_t wr;
-          uint32_t sl;
-          (void)window_step<PY, SMALL>(w, wm, i, n1, wr, sl);
-          if (wr) {
-            if ((wr >> lane) & 1ull) {
-              const int e = ne + static_cast<int>(lane_rank(wr));
-              if (e < ecx) evx[e] = static_cast<uint32_t>(d + lane + 1);
-            }
-            ne += static_cast<int>(__popcll(wr));
-          }
-          d += Wn;
-        }
-        const uint32_t *rr = xr + static_cast<size_t>(r) * rw;
-        for (int q0 = 0; q0 < mr; q0 += 64) {
-          const int q = q0 + lane;
-          const uint32_t x = q < mr ? rr[q] : 0u;
-          const uint64_t b = __ballot(q < mr && (x >> 16) == i);
-          if (b) {
-            const int f = __ffsll(static_cast<long long>(b)) - 1;
-            res = (static_cast<uint32_t>(r) << 16) |
-                  (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), f)) & 0xffffu);
-            break;
-          }
-        }
-        if (res != 0xffffffffu) break;
-      }
-      if (lane == 0 && res != 0xffffffffu && ne <= ecx) {
-        s_cxo[g] = res;
-        s_cxn[g] = ne;
-      }
-    }
   }
   if (tid < m) a.fin[static_cast<size_t>(c) * n1 + tid] = s_lo[tid] | (s_st[tid] << 16);
   if (tid == 0) {
     a.fin_m[c] = m;
-    a.rec_n[c] = s_nrec;
     a.ev_n[c] = min(s_evn, a.ecap);
     if (s_evn > a.ecap) atomicOr(a.err, 1);
     np_stamp(c, kTsTrackR1, kTsTrackC1);
@@ -1211,10 +1052,7 @@ __device__ __forceinline__ void np_track_body(const EntryArgs &a, const uint32_t
 // workgroup per CU (+1.3 ms at C2).  The 64-entry kernel needs 70; the 128-entry one (large N)
 // is capped at 72 (spilling ~20 SGPRs to VGPR lanes: 86 uncapped).
 #ifndef RSAMD_TRACK_SGPR
-// the cap of the 64-entry tracking kernel's SGPRs (0: none): the seeded-chunk records took it
-// from 78 to 82 uncapped (7 waves per SIMD: one 16-wave workgroup per CU); at 78 it spills two
-// to VGPR lanes
-#define RSAMD_TRACK_SGPR 78
+#define RSAMD_TRACK_SGPR 0  // >0: cap the 64-entry tracking kernel's SGPRs (A/B builds)
 #endif
 template <bool PY, bool SMALL>
 __global__ __launch_bounds__(64 * kTrackWaves)
@@ -1231,123 +1069,12 @@ k_np_track128(EntryArgs a, const uint32_t *__restrict__ draws) {
   np_track_body<PY, false, 128>(a, draws);
 }
 
-// ---- 3c. carries into seeded chunks -----------------------------------------------------------
-// Seeded chunk c's map is exact at its K seeds only.  Every final trajectory g of chunk c - 1
-// (its state at chunk c's draw 0) is carried on through chunk c's draws, one wave per carry, a
-// window of 64 draws at a time (window_step), up to each recorded list of chunk c in turn; at
-// the first record holding the carry's state the carry IS that list entry's trajectory from
-// then on (trajectories that meet merge), so the carry resolves to (record r, entry lo).  Its
-// wraps before the record are logged apart (ext_ev, relative draw after the wrap).  A carry that
-// meets no record sets err bit 8: the host parses the segment again from every entry state.
-struct ExtArgs {
-  const uint32_t *draws;  // draw 0 of the (rank's) segment
-  int W, n1, Cr, gcap, ecx, RW;
-  const uint32_t *fin;
-  const int *fin_m;
-  const uint32_t *rec;
-  const int2 *rec_tm;
-  const int *rec_n;
-  const int *mode;        // [Cr] 1: seeded chunk entered by a carry
-  uint32_t *ext;          // [Cr][gcap] record index << 16 | lo
-  int *ext_n;             // [Cr][gcap] wraps logged
-  uint32_t *ext_ev;       // [Cr][gcap][ecx]
-  int *err;
-};
-
-template <bool PY>
-__global__ __launch_bounds__(64) void k_np_extend(ExtArgs a) {
-  const int c = static_cast<int>(blockIdx.x) / kExtSlots, j = static_cast<int>(blockIdx.x) % kExtSlots;
-  const int l = threadIdx.x;
-  if (c < 1 || c >= a.Cr || !a.mode[c]) return;
-  const int mp = a.fin_m[c - 1];
-  if (mp > a.gcap) {  // the previous chunk ended with more trajectories than a carry row holds
-    if (j == 0 && l == 0) atomicOr(a.err, 8);
-    return;
-  }
-  const int n1 = a.n1, nrec = a.rec_n[c];
-  const uint32_t *__restrict__ wp = a.draws + static_cast<int64_t>(c) * a.W;
-  for (int g = j; g < mp; g += kExtSlots) {
-    const size_t slot = static_cast<size_t>(c) * a.gcap + g;
-    if (a.ext[slot] != 0xffffffffu) continue;  // resolved at the end of chunk c - 1's tracking
-    uint32_t i = uni(a.fin[static_cast<size_t>(c - 1) * n1 + g] >> 16);
-    uint32_t *ev = a.ext_ev + slot * a.ecx;
-    int ne = 0, d = 0;
-    uint32_t res = 0xffffffffu;
-    uint32_t wn = wp[l];  // the next window's words (the stream has a margin past the segment)
-    for (int r = 0; r < nrec; ++r) {
-      const int2 tm = a.rec_tm[c * kRec + r];
-      const int tr = uni(tm.x), mr = uni(tm.y);
-      while (d < tr) {
-        const int Wn = min(64, tr - d);
-        const uint64_t wm = Wn == 64 ? ~0ull : ((1ull << Wn) - 1ull);
-        const uint32_t w = wn;
-        wn = wp[d + Wn + l];
-        uint64_t wr;
-        uint32_t sl;
-        (void)window_step<PY, false>(w, wm, i, n1, wr, sl);
-        if (wr) {
-          if ((wr >> l) & 1ull) {
-            const int e = ne + static_cast<int>(lane_rank(wr));
-            if (e < a.ecx) ev[e] = static_cast<uint32_t>(d + l + 1);
-          }
-          ne += static_cast<int>(__popcll(wr));
-        }
-        d += Wn;
-      }
-      const uint32_t *rr = a.rec + (static_cast<size_t>(c) * kRec + r) * a.RW;
-      for (int q0 = 0; q0 < mr; q0 += 64) {
-        const int q = q0 + l;
-        const uint32_t x = q < mr ? rr[q] : 0u;
-        const uint64_t b = __ballot(q < mr && (x >> 16) == i);
-        if (b) {
-          const int f = __ffsll(static_cast<long long>(b)) - 1;
-          res = (static_cast<uint32_t>(r) << 16) |
-                (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), f)) & 0xffffu);
-          break;
-        }
-      }
-      if (res != 0xffffffffu) break;
-    }
-    if (l == 0) {
-      a.ext[slot] = res;
-      a.ext_n[slot] = ne;
-      if (res == 0xffffffffu || ne > a.ecx) atomicOr(a.err, 8);
-    }
-  }
-}
-
 // ---- 5. keep the wraps of the true trajectory (in place, order preserved) -----------------
-// Carry selection of a seeded chunk c (c > 0 in the whole stream): the true trajectory enters
-// it as the carry of the previous chunk's chosen final entry gch[c - 1]; that carry's logged
-// wraps come first (sel.x of them, carry row sel.y), then the chunk's own wraps after the
-// carry's meeting draw p whose member range holds the true entry.  Otherwise sel = (0, -1)
-// and p = 0.
-struct CarrySel {
-  const int *mode;        // [Cr] local chunks
-  const int *gch;         // chosen final entry per chunk, offset to the rank's chunk 0
-  const uint32_t *ext;    // [Cr][gcap]
-  const int *ext_n;       // [Cr][gcap]
-  const int2 *rec_tm;     // [Cr][kRec]
-  int gcap, coff;         // coff: global index of local chunk 0
-  int2 *sel;              // [Cr] out
-};
-
 __global__ __launch_bounds__(64) void k_np_filter(uint2 *__restrict__ ev, const int *ev_n,
-                                                  const int *ent, int *vcnt, int ecap, CarrySel f) {
+                                                  const int *ent, int *vcnt, int ecap) {
   const int c = blockIdx.x, l = threadIdx.x;
   const uint32_t a = static_cast<uint32_t>(ent[c]);
   const int n = ev_n[c];
-  uint32_t p = 0;
-  int nx = 0, xs = -1;
-  if (f.mode && f.mode[c] && f.coff + c > 0) {
-    const int g = min(max(f.gch[c - 1], 0), f.gcap - 1);
-    const uint32_t e = f.ext[static_cast<size_t>(c) * f.gcap + g];
-    if (e != 0xffffffffu) {  // (a failed carry fails the segment: err bit 8)
-      p = static_cast<uint32_t>(f.rec_tm[c * kRec + min(static_cast<int>(e >> 16), kRec - 1)].x);
-      xs = c * f.gcap + g;
-      nx = f.ext_n[xs];
-    }
-  }
   uint2 *e = ev + static_cast<size_t>(c) * ecap;
   int cnt = 0;
   for (int b = 0; b < n; b += 64) {
@@ -1358,16 +1085,13 @@ __global__ __launch_bounds__(64) void k_np_filter(uint2 *__restrict__ ev, const 
       const uint2 x = e[i];
       tv = x.x;
       const uint32_t lo = x.y & 0xffffu, hi = x.y >> 16;
-      ok = tv > p && (lo < hi ? (a >= lo && a < hi) : (a >= lo || a < hi));
+      ok = lo < hi ? (a >= lo && a < hi) : (a >= lo || a < hi);
     }
     const uint64_t bl = __ballot(ok);
     if (ok) e[cnt + static_cast<int>(lane_rank(bl))].x = tv;
     cnt += __popcll(bl);
   }
-  if (l == 0) {
-    vcnt[c] = nx + cnt;
-    f.sel[c] = make_int2(nx, xs);
-  }
+  if (l == 0) vcnt[c] = cnt;
 }
 
 // ---- 4. compose the chunk maps on the GPU ------------------------------------------------
@@ -1381,23 +1105,17 @@ constexpr int kComposeBlock = 256;
 // along the lanes; the serial walk of wave 0 is then one ballot per chunk: the wanted entry is
 // the highest lane with lo <= a (none: the last lane, the largest lo).  Longer lists (chunks
 // that ended dense) take the key-maximum scan from HBM.
-// Where chunk c + 1 is seeded (mode), the next entry is not n1 - state but the lo its carry
-// met: the staged row carries n1 - that lo in the state field, so the walk is the same.  The
-// chosen entry of every chunk (index in its final list) goes to gch.
 // row_off (optional): where chunk c's list starts in fin (the gathered, packed maps of a
 // sharded parse); null: row c at c * n1.
 __global__ __launch_bounds__(1024) void k_np_compose(const uint32_t *__restrict__ fin,
                                                      const int *__restrict__ fin_m, int n1, int C,
                                                      int *__restrict__ ent,
-                                                     const int64_t *__restrict__ row_off,
-                                                     const int *__restrict__ mode,
-                                                     const uint32_t *__restrict__ ext, int gcap,
-                                                     int *__restrict__ gch) {
+                                                     const int64_t *__restrict__ row_off) {
   auto row = [&](int c) -> const uint32_t * {
     return fin + (row_off ? row_off[c] : static_cast<int64_t>(c) * n1);
   };
   __shared__ uint32_t rows[kComposeBlock][64];
-  __shared__ int ms[kComposeBlock], es[kComposeBlock], rot[kComposeBlock], ei[kComposeBlock];
+  __shared__ int ms[kComposeBlock], es[kComposeBlock];
   const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
   int a = 0;
   for (int c0 = 0; c0 < C; c0 += kComposeBlock) {
@@ -1405,13 +1123,9 @@ __global__ __launch_bounds__(1024) void k_np_compose(const uint32_t *__restrict_
     for (int k = tid; k < nb; k += 1024) ms[k] = fin_m[c0 + k];
     __syncthreads();
     for (int r = wv; r < nb; r += 16) {
-      const int m = ms[r], c = c0 + r;
+      const int m = ms[r];
       if (m > 64) continue;
-      uint32_t x = l < m ? row(c)[l] : 0xffffffffu;
-      if (mode && c + 1 < C && mode[c + 1] && l < m && l < gcap) {  // the carry's meeting lo
-        const uint32_t e = ext[static_cast<size_t>(c + 1) * gcap + l];
-        x = (x & 0xffffu) | ((static_cast<uint32_t>(n1) - (e & 0xffffu)) << 16);
-      }
+      const uint32_t x = l < m ? row(c0 + r)[l] : 0xffffffffu;
       // the lane holding the smallest lo starts the rotated row
       uint32_t mn = x & 0xffffu;
 #pragma unroll
@@ -1419,7 +1133,6 @@ __global__ __launch_bounds__(1024) void k_np_compose(const uint32_t *__restrict_
       const uint64_t at = __ballot(l < m && (x & 0xffffu) == mn);
       const int p0 = __ffsll(static_cast<long long>(at)) - 1;
       if (l < m) rows[r][l - p0 >= 0 ? l - p0 : l - p0 + m] = x;
-      if (l == 0) rot[r] = p0;
     }
     __syncthreads();
     if (wv == 0) {
@@ -1438,47 +1151,30 @@ __global__ __launch_bounds__(1024) void k_np_compose(const uint32_t *__restrict_
           const uint32_t x = l < m ? xr : 0xffffffffu;
           const uint64_t le = __ballot(l < m && static_cast<int>(x & 0xffffu) <= a);
           const int idx = le ? 63 - __builtin_clzll(le) : m - 1;
-          ei[r] = idx;
           a = n1 - static_cast<int>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), idx)) >> 16);
           continue;
         }
-        // (key, index) maxima: the largest lo <= a, else the largest lo overall
-        uint64_t kb = 0, kt = 0;
+        uint32_t kb = 0, kt = 0;
         bool hb = false, ht = false;
         for (int k = l; k < m; k += 64) {
           const uint32_t x = row(c)[k];
           const uint32_t lo = x & 0xffffu, key = (lo << 16) | (x >> 16);
-          const uint64_t kk = (static_cast<uint64_t>(key) << 32) | static_cast<uint32_t>(k);
-          if (static_cast<int>(lo) <= a && (!hb || kk > kb)) kb = kk, hb = true;
-          if (!ht || kk > kt) kt = kk, ht = true;
+          if (static_cast<int>(lo) <= a && (!hb || key > kb)) kb = key, hb = true;
+          if (!ht || key > kt) kt = key, ht = true;
         }
         const uint64_t anyb = __ballot(hb);
         // keys of valid rows are distinct; invalid lanes hold 0 and lose every max below
-        uint64_t mb = hb ? kb : 0ull, mt = ht ? kt : 0ull;
+        uint32_t mb = hb ? kb : 0u, mt = ht ? kt : 0u;
 #pragma unroll
         for (int o = 32; o; o >>= 1) {
-          const uint64_t yb = __shfl_xor(static_cast<unsigned long long>(mb), o);
-          const uint64_t yt = __shfl_xor(static_cast<unsigned long long>(mt), o);
-          mb = mb > yb ? mb : yb;
-          mt = mt > yt ? mt : yt;
+          mb = max(mb, static_cast<uint32_t>(__shfl_xor(static_cast<int>(mb), o)));
+          mt = max(mt, static_cast<uint32_t>(__shfl_xor(static_cast<int>(mt), o)));
         }
-        const uint64_t win = anyb ? mb : mt;
-        const int k = static_cast<int>(win & 0xffffffffu);
-        ei[r] = k | 0x40000000;  // an index in the final list itself
-        int nx = n1 - static_cast<int>((win >> 32) & 0xffffu);
-        if (mode && c + 1 < C && mode[c + 1] && k < gcap)
-          nx = static_cast<int>(ext[static_cast<size_t>(c + 1) * gcap + k] & 0xffffu);
-        a = nx;
+        a = n1 - static_cast<int>((anyb ? mb : mt) & 0xffffu);
       }
     }
     __syncthreads();
-    for (int k = tid; k < nb; k += 1024) {
-      ent[c0 + k] = es[k];
-      if (gch) {
-        const int e = ei[k], m = ms[k];
-        gch[c0 + k] = (e & 0x40000000) ? (e & 0x3fffffff) : (e + rot[k]) % max(m, 1);
-      }
-    }
+    for (int k = tid; k < nb; k += 1024) ent[c0 + k] = es[k];
   }
 }
 
@@ -1549,6 +1245,7 @@ __host__ __device__ constexpr int64_t tup_lds_bytes(int n1) {
 #endif
 constexpr int kTupAhead = RSAMD_TUP_AHEAD;
 
+
 template <bool PY>
 __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
     const uint32_t *__restrict__ draws, const int64_t *__restrict__ starts,
@@ -1587,8 +1284,8 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
   // A full 64-draw window in i's bucket and the one below (every state it can reach is at
   // least the lower bucket's lowest): the two-bucket fixed point of the tracking kernel
   // (fast_window), the bucket constants on the vector unit, the swap partners stored by every
-  // lane (rejected lanes into their dummy slot).  The kernel was scalar-issue bound (PMC, C2:
-  // 3.3e8 SALU per launch against 3.7e8 VALU, ~38 per window): this form spends ~10.
+  // lane (rejected lanes into their dummy slot).  PMC per C2 launch (r04d_pmc / r04d_pmc2):
+  // SALU 3.28e8 -> 1.83e8, VALU 3.74e8 -> 4.03e8; 668 -> 591-611 us (profiles/r04d_tuples_ab.txt).
   const uint32_t jdummy = static_cast<uint32_t>(tup_jpad(n1)) + static_cast<uint32_t>(l);
   auto window2 = [&]() -> bool {
     uint32_t iv;
@@ -1619,10 +1316,8 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
       a2 = __ballot(rk <= (rk <= c ? vh : vl));
       a0 = a2;
     } while (a2 != a1);
-    // the accepted lanes' states and draws from the fixed point itself (opaque to the compiler,
-    // so that the loop does not carry the lanes' predicates as exec-masked scalar copies)
-    asm volatile("" : "+s"(a2));
-    rk = static_cast<int>(lane_rank(a2));
+    // (rk = rank_l(a1) = rank_l(a2); recomputing it from an opaque a2 so that the loop does not
+    // carry the lanes' predicates as exec-masked scalar copies measured the same, 604 vs 591 us)
     const bool hb = rk <= c;
     const bool ac = rk <= (hb ? vh : vl);
     J[ac ? iv - static_cast<uint32_t>(rk) - 1u : jdummy] = static_cast<uint16_t>(hb ? uh : ul);
@@ -1669,7 +1364,9 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
   };
   // The register queue rotates by unrolling (slot q is refilled in turn), never by moving a
   // register: a move of a load's destination would wait for that load.
-  // (a two-bucket window never ends the hypothesis: only the general one is followed by the test)
+  // (a two-bucket window never ends the hypothesis: only the general one is followed by the
+  // test; unconditional refills let the compiler's wait counts keep five of six blocks in flight
+  // -- the guarded form waited for every load at every refill -- which measured the same)
   for (;;) {
 #pragma unroll
     for (int q = 0; q < kTupAhead; ++q) {
@@ -1866,45 +1563,20 @@ int64_t knob_cpr() {
   static const int64_t v = std::max<int64_t>(0, env_i64("RSAMD_NP_CPR"));
   return v;
 }
-constexpr int64_t kMapsMagic = 0x5253485044414d54LL;   // blob header tag (v2: seeded chunks)
-// seeds per chunk for a segment of chunks of Wc draws: kSeeds where they pay (N - 1 > kSeeds and
-// chunks long enough that the dense phase ends well inside them); RSAMD_NP_SEEDS=<K> forces K
-// (0: every chunk from all entries), read at every call (tests switch it)
-int seeds_for(int n1, int64_t Wc) {
-  if (const char *e = std::getenv("RSAMD_NP_SEEDS")) {
-    const int k = std::atoi(e);
-    return k <= 0 || k >= n1 ? 0 : k;
-  }
-  return n1 > kSeeds && n1 < 4096 && Wc >= 32 * static_cast<int64_t>(n1) ? kSeeds : 0;
-}
-// records a seeded chunk keeps (RSAMD_NP_SEEDREC, tests of the fall-back: few records, carries
-// that meet none)
-std::atomic<int64_t> g_parse_seeded{0}, g_parse_fallback{0}, g_parse_all{0};
-int seed_records() {
-  if (const char *e = std::getenv("RSAMD_NP_SEEDREC")) return std::max(1, std::min(kRec, std::atoi(e)));
-  return kRec;
-}
+constexpr int64_t kMapsMagic = 0x5253485044414d53LL;   // blob header tag
 
 // start draw (relative to the rank's draw 0) of every kept wrap, in order; lead = 1 puts the
 // segment's first hypothesis (draw 0, rank 0 only) in front
-// (a seeded chunk's carry wraps first: sel = (count, carry row), k_np_filter)
 __global__ __launch_bounds__(256) void k_np_starts_local(const uint2 *__restrict__ ev,
                                                          const int *__restrict__ vcnt,
                                                          const int *__restrict__ off,
                                                          int64_t *__restrict__ starts, int ecap,
-                                                         int W, int lead,
-                                                         const int2 *__restrict__ sel,
-                                                         const uint32_t *__restrict__ ext_ev,
-                                                         int ecx) {
+                                                         int W, int lead) {
   const int c = blockIdx.x;
   const int n = vcnt[c];
-  const int2 sx = sel ? sel[c] : make_int2(0, -1);
-  const int nx = sx.y >= 0 ? sx.x : 0;
-  const int64_t base = lead + off[c], c0 = static_cast<int64_t>(c) * W;
-  for (int i = threadIdx.x; i < nx; i += 256)
-    starts[base + i] = c0 + ext_ev[static_cast<size_t>(sx.y) * ecx + i];
-  for (int i = threadIdx.x; i < n - nx; i += 256)
-    starts[base + nx + i] = c0 + ev[static_cast<size_t>(c) * ecap + i].x;
+  const int64_t base = lead + off[c];
+  for (int i = threadIdx.x; i < n; i += 256)
+    starts[base + i] = static_cast<int64_t>(c) * W + ev[static_cast<size_t>(c) * ecap + i].x;
   if (lead && c == 0 && threadIdx.x == 0) starts[0] = 0;
 }
 
@@ -1932,8 +1604,6 @@ struct rs_np_shard {
   int64_t count = 0, Wc = 0, Cr = 0, C = 0, D = 0;
   int64_t s_lo = 0, g0 = 0, wbase = 0, Lb = 0, G = 0, nwords = 0;
   int ecap = 0, ecap_shift = 0;
-  // seeded chunks of the current segment (K = 0: all-entry; set to 0 when a carry fails)
-  int K = 0, gcap = 64, RW = 0, ecx = 0, rec_stride = 1024, nrec_max = kRec;
   int state = 0;  // 0 idle, 1 parsed, 2 composed
   int64_t nstarts = 0, first_start = -1;
   std::vector<uint8_t> maps;  // this rank's chunk-map blob
@@ -1946,12 +1616,6 @@ struct rs_np_shard {
       *d_vcnt = nullptr, *d_off = nullptr, *d_err = nullptr, *d_tpos = nullptr;
   int64_t *d_row_off = nullptr, *d_starts = nullptr, *d_got = nullptr;
   uint2 *d_ev = nullptr;
-  uint32_t *d_rec = nullptr, *d_ext = nullptr, *d_ext_ev = nullptr, *d_ext_all = nullptr;
-  int2 *d_rec_tm = nullptr, *d_sel = nullptr;
-  int *d_rec_n = nullptr, *d_mode = nullptr, *d_ext_n = nullptr, *d_gch = nullptr,
-      *d_mode_all = nullptr, *d_rec_ne = nullptr;
-  int64_t cap_rec = 0, cap_ext = 0, cap_ext_ev = 0, cap_ext_all = 0, cap_rec_tm = 0, cap_sel = 0,
-          cap_rec_n = 0, cap_mode = 0, cap_ext_n = 0, cap_gch = 0, cap_mode_all = 0, cap_rec_ne = 0;
   NpResult *d_res = nullptr;  // world 1 (np_choice_device): the segment's outcome in one copy
   int64_t cap_win = 0, cap_chain = 0, cap_stream = 0, cap_fin = 0, cap_fin_all = 0, cap_fm = 0,
           cap_fm_all = 0, cap_ev = 0, cap_evn = 0, cap_ent = 0, cap_vcnt = 0, cap_off = 0,
@@ -1964,9 +1628,7 @@ void shard_free(rs_np_shard *w) {
   void *ptrs[] = {w->d_bits, w->d_win,   w->d_chain, w->d_stream, w->d_fin,     w->d_fin_all,
                   w->d_fin_m, w->d_fin_m_all, w->d_ev_n, w->d_ent, w->d_vcnt, w->d_off,
                   w->d_err,  w->d_tpos,  w->d_row_off, w->d_starts, w->d_got, w->d_ev,
-                  w->d_res,  w->d_rec,   w->d_ext,   w->d_ext_ev, w->d_ext_all, w->d_rec_tm,
-                  w->d_sel,  w->d_rec_n, w->d_mode,  w->d_ext_n,  w->d_gch,     w->d_mode_all,
-                  w->d_rec_ne};
+                  w->d_res};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
 }
@@ -2046,12 +1708,6 @@ int shard_layout(rs_np_shard &w, int32_t pos, int64_t count) {
   if (w.G > (int64_t(1) << kLevels)) return rs::fail(RS_EINVAL, "np shard: segment too long");
   w.nwords = w.Lb * kN - (w.s_lo - w.wbase);
   w.ecap_shift = 0;
-  w.K = seeds_for(w.n1, w.Wc);
-  w.gcap = hand_of(w.n1);
-  w.RW = std::max(w.K, w.gcap);
-  w.ecx = static_cast<int>(w.Wc / w.n1) + 4;
-  w.rec_stride = w.n1 < 4096 ? 1024 : 8192;
-  w.nrec_max = seed_records();
   return RS_OK;
 }
 
@@ -2131,17 +1787,7 @@ int shard_stream(rs_np_shard &w, const uint32_t *key) {
       (st = sgrow(w.d_vcnt, w.cap_vcnt, w.Cr)) || (st = sgrow(w.d_off, w.cap_off, w.Cr)) ||
       (st = sgrow(w.d_ent, w.cap_ent, w.Cr)) ||
       // every hypothesis spans at least n1 draws: a bound on the own starts
-      (st = sgrow(w.d_starts, w.cap_starts, w.Cr * w.Wc / std::max(1, w.n1) + 4)) ||
-      (st = sgrow(w.d_rec_n, w.cap_rec_n, w.Cr)) || (st = sgrow(w.d_mode, w.cap_mode, w.Cr)) ||
-      (st = sgrow(w.d_sel, w.cap_sel, w.Cr)) || (st = sgrow(w.d_gch, w.cap_gch, w.C)) ||
-      (st = sgrow(w.d_rec_ne, w.cap_rec_ne, w.Cr)))
-    return st;
-  if (w.K > 0 &&
-      ((st = sgrow(w.d_rec, w.cap_rec, w.Cr * kRec * w.RW)) ||
-       (st = sgrow(w.d_rec_tm, w.cap_rec_tm, w.Cr * kRec)) ||
-       (st = sgrow(w.d_ext, w.cap_ext, w.Cr * w.gcap)) ||
-       (st = sgrow(w.d_ext_n, w.cap_ext_n, w.Cr * w.gcap)) ||
-       (st = sgrow(w.d_ext_ev, w.cap_ext_ev, w.Cr * w.gcap * static_cast<int64_t>(w.ecx)))))
+      (st = sgrow(w.d_starts, w.cap_starts, w.Cr * w.Wc / std::max(1, w.n1) + 4)))
     return st;
   return RS_OK;
 }
@@ -2178,23 +1824,8 @@ int shard_enqueue_parse(rs_np_shard &w) {
     HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_np_ts), &ts_buf, sizeof(ts_buf), 0,
                                    hipMemcpyHostToDevice, s));
   }
-  // seeded chunks: every local chunk but a later rank's first (its entry comes from another
-  // rank's chunk: all entries); K = 0 after a failed carry
-  (w.K > 0 ? g_parse_seeded : g_parse_all).fetch_add(1);
-  {
-    std::vector<int> mode(static_cast<size_t>(w.Cr), 0);
-    if (w.K > 0)
-      for (int q = 0; q < Cr; ++q) mode[static_cast<size_t>(q)] = (q == 0 && w.rank > 0) ? 0 : 1;
-    HIP_TRY(hipMemcpyAsync(w.d_mode, mode.data(), sizeof(int) * mode.size(), hipMemcpyHostToDevice, s));
-  }
   EntryArgs ea{w.d_stream + (w.s_lo - w.wbase), w.Cr * w.Wc, Wc, w.n1, w.d_fin, w.d_fin_m,
-               w.d_ev, w.d_ev_n, w.d_tpos, w.ecap, w.d_err, d_stats,
-               w.K, w.rank > 0 ? 1 : 0, w.RW, w.rec_stride, w.nrec_max,
-               w.K > 0 ? w.d_rec : nullptr, w.K > 0 ? w.d_rec_tm : nullptr, w.d_rec_n,
-               w.d_rec_ne, w.d_mode, w.K > 0 ? w.d_ext : nullptr, w.d_ext_n, w.d_ext_ev, w.gcap,
-               w.ecx, Cr};
-  if (w.K > 0)  // every carry unresolved until a kernel resolves it
-    HIP_TRY(hipMemsetAsync(w.d_ext, 0xff, sizeof(uint32_t) * static_cast<size_t>(w.Cr) * w.gcap, s));
+               w.d_ev, w.d_ev_n, w.d_tpos, w.ecap, w.d_err, d_stats};
   const bool small = w.n1 < 64;  // several hypothesis ends in one tracking window
   if (w.py) {
     k_np_entry<true><<<Cr, kEntryThreads, static_cast<size_t>(lds), s>>>(ea, ea.draws);
@@ -2208,12 +1839,6 @@ int shard_enqueue_parse(rs_np_shard &w) {
            : (hand_of(w.n1) > 64 ? k_np_track128<false> : k_np_track<false, false>))<<<Cr, 64 * kTrackWaves, 0, s>>>(ea, ea.draws);
   }
   HIP_TRY(hipGetLastError());
-  if (w.K > 0 && Cr > 1) {  // the carries into seeded chunks
-    ExtArgs xa{ea.draws, Wc, w.n1, Cr, w.gcap, w.ecx, w.RW, w.d_fin, w.d_fin_m, w.d_rec,
-               w.d_rec_tm, w.d_rec_n, w.d_mode, w.d_ext, w.d_ext_n, w.d_ext_ev, w.d_err};
-    (w.py ? k_np_extend<true> : k_np_extend<false>)<<<static_cast<unsigned>(Cr) * kExtSlots, 64, 0, s>>>(xa);
-    HIP_TRY(hipGetLastError());
-  }
   if (ts_path) {
     // header: n1, chunks, chunk length, draws, rank, world, then kTs words per chunk
     std::vector<unsigned long long> h(static_cast<size_t>(w.Cr) * kTs + 8, 0ull);
@@ -2250,16 +1875,12 @@ int shard_enqueue_parse(rs_np_shard &w) {
 int shard_enqueue_starts(rs_np_shard &w, int64_t cap, int64_t *got) {
   hipStream_t s = w.ctx->stream;
   const int Cr = static_cast<int>(w.Cr);
-  const int coff = static_cast<int>(w.rank * w.Cr);
-  const CarrySel cs{w.K > 0 ? w.d_mode : nullptr, w.d_gch + coff, w.d_ext, w.d_ext_n, w.d_rec_tm,
-                    w.gcap, coff, w.d_sel};
-  k_np_filter<<<Cr, 64, 0, s>>>(w.d_ev, w.d_ev_n, w.d_ent + coff, w.d_vcnt, w.ecap, cs);
+  k_np_filter<<<Cr, 64, 0, s>>>(w.d_ev, w.d_ev_n, w.d_ent + w.rank * w.Cr, w.d_vcnt, w.ecap);
   HIP_TRY(hipGetLastError());
   k_np_scan<<<1, 1024, 0, s>>>(w.d_vcnt, Cr, w.d_off, cap, got);
   HIP_TRY(hipGetLastError());
   k_np_starts_local<<<Cr, 256, 0, s>>>(w.d_ev, w.d_vcnt, w.d_off, w.d_starts, w.ecap,
-                                       static_cast<int>(w.Wc), w.rank == 0 ? 1 : 0, w.d_sel,
-                                       w.d_ext_ev, w.ecx);
+                                       static_cast<int>(w.Wc), w.rank == 0 ? 1 : 0);
   HIP_TRY(hipGetLastError());
   return RS_OK;
 }
@@ -2286,12 +1907,6 @@ int shard_parse(rs_np_shard &w, const uint32_t *key, int32_t pos, int64_t count)
     int err = 0;
     HIP_TRY(hipMemcpyAsync(&err, w.d_err, sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    if (err & 8) {  // a carry met no record: this rank's chunks from every entry state
-      if (w.K == 0) return rs::fail(RS_EDEVICE, "np shard: carry failure without seeds");
-      g_parse_fallback.fetch_add(1);
-      w.K = 0;
-      continue;
-    }
     if (err & 1) {  // wrap log overflow: a larger log, the same chunks again
       if (w.ecap >= w.Wc + 2 * w.n1) return rs::fail(RS_EDEVICE, "np shard: wrap log overflow");
       ++w.ecap_shift;
@@ -2312,30 +1927,12 @@ int shard_parse(rs_np_shard &w, const uint32_t *key, int32_t pos, int64_t count)
     if (fm[q] < 1 || fm[q] > w.n1) return rs::fail(RS_EDEVICE, "np shard: bad chunk map");
     nent += fm[q];
   }
-  // seeded chunks: mode per chunk and, for every local chunk q >= 1 that is seeded, the carry
-  // result of each of chunk q - 1's final entries
-  std::vector<int> mode(static_cast<size_t>(Cr), 0);
-  std::vector<uint32_t> xr;
-  if (w.K > 0) {
-    HIP_TRY(hipMemcpy(mode.data(), w.d_mode, sizeof(int) * mode.size(), hipMemcpyDeviceToHost));
-    std::vector<uint32_t> all(static_cast<size_t>(Cr) * w.gcap);
-    HIP_TRY(hipMemcpy(all.data(), w.d_ext, sizeof(uint32_t) * all.size(), hipMemcpyDeviceToHost));
-    for (int q = 1; q < Cr; ++q)
-      if (mode[q]) {
-        if (fm[q - 1] > w.gcap) return rs::fail(RS_EDEVICE, "np shard: carry row overflow");
-        xr.insert(xr.end(), all.begin() + static_cast<int64_t>(q) * w.gcap,
-                  all.begin() + static_cast<int64_t>(q) * w.gcap + fm[q - 1]);
-      }
-  }
-  const int64_t nx = static_cast<int64_t>(xr.size());
-  const int64_t hdr[10] = {kMapsMagic, w.rank, w.Cr, w.Wc, w.D, w.n1, nent, w.C, w.gcap, nx};
-  w.maps.assign(sizeof(hdr) + 2 * sizeof(int32_t) * Cr + sizeof(uint32_t) * (nent + nx), 0);
+  const int64_t hdr[8] = {kMapsMagic, w.rank, w.Cr, w.Wc, w.D, w.n1, nent, w.C};
+  w.maps.assign(sizeof(hdr) + sizeof(int32_t) * Cr + sizeof(uint32_t) * nent, 0);
   uint8_t *o = w.maps.data();
   std::memcpy(o, hdr, sizeof(hdr));
   std::memcpy(o + sizeof(hdr), fm.data(), sizeof(int32_t) * Cr);
-  std::memcpy(o + sizeof(hdr) + sizeof(int32_t) * Cr, mode.data(), sizeof(int32_t) * Cr);
-  uint32_t *e = reinterpret_cast<uint32_t *>(o + sizeof(hdr) + 2 * sizeof(int32_t) * Cr);
-  if (nx) std::memcpy(e + nent, xr.data(), sizeof(uint32_t) * nx);
+  uint32_t *e = reinterpret_cast<uint32_t *>(o + sizeof(hdr) + sizeof(int32_t) * Cr);
   for (int q = 0; q < Cr; ++q) {
     if (fm[q] <= width) {
       std::memcpy(e, rows.data() + static_cast<size_t>(q) * width, sizeof(uint32_t) * fm[q]);
@@ -2355,28 +1952,24 @@ int shard_compose(rs_np_shard &w, const uint8_t *blobs, int64_t stride) {
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = c->stream;
   int st;
-  std::vector<int> fm_all(static_cast<size_t>(w.C)), mode_all(static_cast<size_t>(w.C), 0);
+  std::vector<int> fm_all(static_cast<size_t>(w.C));
   std::vector<int64_t> row(static_cast<size_t>(w.C));
-  std::vector<uint32_t> ent, ext_all(static_cast<size_t>(w.C) * w.gcap, 0xffffffffu);
-  bool any_seed = false;
+  std::vector<uint32_t> ent;
   for (int r = 0; r < w.world; ++r) {
     const uint8_t *b = blobs + static_cast<size_t>(r) * stride;
-    int64_t hdr[10];
+    int64_t hdr[8];
     if (stride < static_cast<int64_t>(sizeof(hdr))) return rs::fail(RS_EINVAL, "np shard: short map blob");
     std::memcpy(hdr, b, sizeof(hdr));
     if (hdr[0] != kMapsMagic || hdr[1] != r)
       return rs::fail(RS_EINVAL, "np shard: map blobs must be the ranks' own, in rank order");
-    if (hdr[2] != w.Cr || hdr[3] != w.Wc || hdr[4] != w.D || hdr[5] != w.n1 || hdr[7] != w.C ||
-        hdr[8] != w.gcap)
+    if (hdr[2] != w.Cr || hdr[3] != w.Wc || hdr[4] != w.D || hdr[5] != w.n1 || hdr[7] != w.C)
       return rs::fail(RS_EINVAL, "np shard: ranks disagree on the segment layout");
-    const int64_t nent = hdr[6], nx = hdr[9];
-    if (nent < 0 || nx < 0 ||
-        static_cast<int64_t>(sizeof(hdr) + 2 * sizeof(int32_t) * w.Cr + sizeof(uint32_t) * (nent + nx)) > stride)
+    const int64_t nent = hdr[6];
+    if (static_cast<int64_t>(sizeof(hdr) + sizeof(int32_t) * w.Cr + sizeof(uint32_t) * nent) > stride)
       return rs::fail(RS_EINVAL, "np shard: truncated map blob");
     const int32_t *fm = reinterpret_cast<const int32_t *>(b + sizeof(hdr));
-    const int32_t *md = fm + w.Cr;
-    const uint32_t *e = reinterpret_cast<const uint32_t *>(b + sizeof(hdr) + 2 * sizeof(int32_t) * w.Cr);
-    int64_t o = 0, ox = 0;
+    const uint32_t *e = reinterpret_cast<const uint32_t *>(b + sizeof(hdr) + sizeof(int32_t) * w.Cr);
+    int64_t o = 0;
     for (int64_t q = 0; q < w.Cr; ++q) {
       const int m = fm[q];
       if (m < 1 || m > w.n1 || o + m > nent) return rs::fail(RS_EINVAL, "np shard: corrupt map blob");
@@ -2385,33 +1978,18 @@ int shard_compose(rs_np_shard &w, const uint8_t *blobs, int64_t stride) {
       row[static_cast<size_t>(cg)] = static_cast<int64_t>(ent.size());
       ent.insert(ent.end(), e + o, e + o + m);
       o += m;
-      if (md[q]) {
-        if (q == 0 && r > 0) return rs::fail(RS_EINVAL, "np shard: corrupt map blob");
-        mode_all[static_cast<size_t>(cg)] = 1;
-        any_seed = true;
-        if (q >= 1) {
-          const int mp = fm[q - 1];
-          if (mp > w.gcap || ox + mp > nx) return rs::fail(RS_EINVAL, "np shard: corrupt map blob");
-          std::memcpy(ext_all.data() + cg * w.gcap, e + nent + ox, sizeof(uint32_t) * mp);
-          ox += mp;
-        }
-      }
     }
   }
   if ((st = sgrow(w.d_fin_all, w.cap_fin_all, static_cast<int64_t>(ent.size()))) ||
       (st = sgrow(w.d_fin_m_all, w.cap_fm_all, w.C)) || (st = sgrow(w.d_row_off, w.cap_row, w.C)) ||
-      (st = sgrow(w.d_ent, w.cap_ent, w.C)) || (st = sgrow(w.d_mode_all, w.cap_mode_all, w.C)) ||
-      (st = sgrow(w.d_ext_all, w.cap_ext_all, w.C * w.gcap)))
+      (st = sgrow(w.d_ent, w.cap_ent, w.C)))
     return st;
   HIP_TRY(hipMemcpyAsync(w.d_fin_all, ent.data(), sizeof(uint32_t) * ent.size(), hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(w.d_fin_m_all, fm_all.data(), sizeof(int) * fm_all.size(), hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(w.d_row_off, row.data(), sizeof(int64_t) * row.size(), hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(w.d_mode_all, mode_all.data(), sizeof(int) * mode_all.size(), hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(w.d_ext_all, ext_all.data(), sizeof(uint32_t) * ext_all.size(), hipMemcpyHostToDevice, s));
   // 3: true entry state of every chunk, then this rank's wraps of the true trajectory
   k_np_compose<<<1, 1024, 0, s>>>(w.d_fin_all, w.d_fin_m_all, w.n1, static_cast<int>(w.C), w.d_ent,
-                                  w.d_row_off, any_seed ? w.d_mode_all : nullptr, w.d_ext_all, w.gcap,
-                                  w.d_gch);
+                                  w.d_row_off);
   HIP_TRY(hipGetLastError());
   if ((st = shard_enqueue_starts(w, std::numeric_limits<int64_t>::max(), w.d_got))) return st;
   const int lead = w.rank == 0 ? 1 : 0;
@@ -2495,7 +2073,7 @@ int shard_run_local(rs_np_shard &w, uint32_t *key, int32_t *pos, int64_t count, 
   for (;;) {
     if ((st = shard_enqueue_parse(w))) return st;
     k_np_compose<<<1, 1024, 0, s>>>(w.d_fin, w.d_fin_m, w.n1, static_cast<int>(w.Cr), w.d_ent,
-                                    nullptr, w.K > 0 ? w.d_mode : nullptr, w.d_ext, w.gcap, w.d_gch);
+                                    nullptr);
     HIP_TRY(hipGetLastError());
     if ((st = shard_enqueue_starts(w, w.count, &w.d_res->got))) return st;
     if (hi > lo) {  // waves beyond the delivered count exit
@@ -2507,12 +2085,6 @@ int shard_run_local(rs_np_shard &w, uint32_t *key, int32_t *pos, int64_t count, 
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(&res, w.d_res, sizeof(res), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    if (res.err & 8) {  // a carry met no record: the same segment from every entry state
-      if (w.K == 0) return rs::fail(RS_EDEVICE, "np sampler: carry failure without seeds");
-      g_parse_fallback.fetch_add(1);
-      w.K = 0;
-      continue;
-    }
     if (res.err & 1) {  // wrap log overflow: a larger log, the same chunks again
       if (w.ecap >= w.Wc + 2 * w.n1) return rs::fail(RS_EDEVICE, "np sampler: wrap log overflow");
       ++w.ecap_shift;
@@ -2722,13 +2294,5 @@ extern "C" int rs_np_shard_tuples(rs_np_shard *w, int64_t base, int64_t hi, int6
   if ((st = shard_tuples(*w, base, hi, next_start, final_idx, d, key_out, pos_out))) return st;
   if (cnt > 0)
     HIP_TRY(hipMemcpy(out, d, sizeof(int32_t) * static_cast<size_t>(cnt) * w->k, hipMemcpyDeviceToHost));
-  return RS_OK;
-}
-
-extern "C" int rs_np_parse_stats(int64_t *out) {
-  if (!out) return rs::fail(RS_EINVAL, "null pointer");
-  out[0] = g_parse_seeded.load();
-  out[1] = g_parse_fallback.load();
-  out[2] = g_parse_all.load();
   return RS_OK;
 }

@@ -140,7 +140,6 @@ _SIGS = {
     "rs_np_shard_create": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
                                      C.c_int32, C.POINTER(C.c_void_p)]),
     "rs_np_shard_destroy": (C.c_int, [C.c_void_p]),
-    "rs_np_parse_stats": (C.c_int, [_i64p]),
     "rs_np_shard_parse": (C.c_int, [C.c_void_p, _u32p, C.c_int32, C.c_int64, _i64p]),
     "rs_np_shard_maps": (C.c_int, [C.c_void_p, _u8p, C.c_int64, _i64p]),
     "rs_np_shard_compose": (C.c_int, [C.c_void_p, _u8p, C.c_int64, _i64p, _i64p]),
@@ -284,14 +283,6 @@ def np_choice_tuples_gpu(key, pos, n, k, count, ctx=None):
     check(lib().rs_np_choice_tuples_gpu(ctx.handle, ptr(key, C.c_uint32), C.byref(p), int(n),
                                         int(k), int(count), ptr(out, C.c_int32)))
     return out, key, p.value
-
-
-def np_parse_stats():
-    """Process-wide GPU stream-parse counters (rs_np_parse_stats): {"seeded", "fallbacks",
-    "all_entry"} segment parses."""
-    out = np.zeros(3, np.int64)
-    check(lib().rs_np_parse_stats(ptr(out, C.c_int64)))
-    return {"seeded": int(out[0]), "fallbacks": int(out[1]), "all_entry": int(out[2])}
 
 
 def np_choice_tuples_multi(keys, poss, ns, k, count, threads=0, seeds=None):
