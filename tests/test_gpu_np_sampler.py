@@ -48,6 +48,18 @@ def test_gpu_stream_c2_size(ctx):
     _same(2000, 8, 100000, seed=11)
 
 
+@pytest.mark.parametrize("n,count", [(2000, 30000), (1000, 20000), (300, 40000)])
+def test_gpu_stream_two_pass_and_pauses(ctx, monkeypatch, n, count):
+    """Chunk-aligned generators with the stream in two passes (the entry kernel beside the
+    second), chunks that pause at the first pass's end and resume (RSAMD_NP_XDRAWS: a short
+    first pass), and the single-pass layout (RSAMD_NP_SPLIT=0) all give the host replay."""
+    _same(n, 8, count, seed=n + 5)
+    monkeypatch.setenv("RSAMD_NP_XDRAWS", "700")
+    _same(n, 8, count, seed=n + 6)
+    monkeypatch.setenv("RSAMD_NP_SPLIT", "0")
+    _same(n, 8, count, seed=n + 7)
+
+
 def test_gpu_stream_reference_goldens(ctx):
     z = golden("synth_c2.npz")
     tup, key, pos = _ffi.np_choice_tuples_gpu(z["mt_key_in"], z["mt_pos_in"], 2000, 8,

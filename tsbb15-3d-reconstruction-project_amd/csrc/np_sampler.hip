@@ -59,8 +59,7 @@ constexpr uint32_t kMatA = 0x9908b0dfu;
 constexpr int kDeg = 19937;
 constexpr int kPrefix = kDeg + kN - 1;       // words of a window's sequence a jump reads
 constexpr int kPrefixAlloc = kN * ((kPrefix + kN - 1) / kN);  // generated in whole blocks
-constexpr int kJB = 1024;                    // stream blocks per generator
-constexpr int64_t kJ = int64_t(kN) * kJB;    // words per generator
+constexpr int kJB = 1024;                    // stream blocks per generator (unless chunk-aligned)
 constexpr int kLevels = 16;                  // jump levels: windows up to 2^16 generators apart
 constexpr int kW = 1 << 24;                  // longest automatic parse chunk (draws)
 constexpr int kWmax = 1 << 24;               // longest chunk (RSAMD_NP_KW)
@@ -224,26 +223,41 @@ __global__ __launch_bounds__(kJumpThreads) void k_mt_jump(uint32_t *__restrict__
 // reads the four neighbour words it needs (thread 169 also recomputes new[0]).  (Three runs of
 // 227 / 227 / 170 threads with a barrier after each: 0.61 ms at C2; one wave per generator
 // with wave-level fences: 1.45 ms.)
+// Chunk-aligned layouts split a generator's run in two launches (k_mt_stream over blocks
+// 1..XB of every generator, then XB+1.. on a second stream while the entry kernel parses the
+// chunks' first draws): blo / bhi bound the blocks (relative to the window) this launch
+// writes, and the raw words of block blo (pass 2) / bhi (pass 1) go through io.  G generators
+// of JB blocks; with `ext` the last one runs on to the segment's end (Lb - 1).
 __global__ __launch_bounds__(256) void k_mt_stream(const uint32_t *__restrict__ win,
-                                                   uint32_t *__restrict__ stream, int64_t Lb) {
+                                                   uint32_t *__restrict__ stream, int64_t Lb,
+                                                   int JB, int G, int ext, int blo, int bhi,
+                                                   uint32_t *__restrict__ io) {
   __shared__ uint32_t bb[2][kN];
   const int g = blockIdx.x, l = threadIdx.x;
   const bool own = l < 227, own2 = l < 170;
-  const int64_t b0 = static_cast<int64_t>(g) * kJB;
-  const uint32_t *wg = win + static_cast<size_t>(g) * kN;
+  const int64_t b0 = static_cast<int64_t>(g) * JB;
   uint32_t o0 = 0, o1 = 0, o2 = 0;
-  if (own) {
-    o0 = wg[l];
-    o1 = wg[l + 227];
-    if (own2) o2 = wg[l + 454];
-    uint32_t *o = stream + b0 * kN;
-    if (l > 0 || g == 0) o[l] = temper(o0);
-    o[l + 227] = temper(o1);
-    if (own2) o[l + 454] = temper(o2);
+  if (blo == 0) {
+    const uint32_t *wg = win + static_cast<size_t>(g) * kN;
+    if (own) {
+      o0 = wg[l];
+      o1 = wg[l + 227];
+      if (own2) o2 = wg[l + 454];
+      uint32_t *o = stream + b0 * kN;
+      if (l > 0 || g == 0) o[l] = temper(o0);
+      o[l + 227] = temper(o1);
+      if (own2) o[l + 454] = temper(o2);
+    }
+  } else if (own) {
+    const uint32_t *ig = io + static_cast<size_t>(g) * kN;
+    o0 = ig[l];
+    o1 = ig[l + 227];
+    if (own2) o2 = ig[l + 454];
   }
-  const int64_t bend = std::min<int64_t>(b0 + kJB, Lb - 1);
+  const int64_t gend = ext && g == G - 1 ? Lb - 1 : std::min<int64_t>(b0 + JB, Lb - 1);
+  const int64_t bend = std::min<int64_t>(gend, b0 + bhi);
   int buf = 0;
-  for (int64_t b = b0 + 1; b <= bend; ++b) {
+  for (int64_t b = b0 + blo + 1; b <= bend; ++b) {
     uint32_t *ob = bb[buf];
     if (own) {
       ob[l] = o0;
@@ -267,6 +281,12 @@ __global__ __launch_bounds__(256) void k_mt_stream(const uint32_t *__restrict__ 
     }
     buf ^= 1;
   }
+  if (bend < gend && own) {  // pass 1 stopped early: the raw block for pass 2
+    uint32_t *ig = io + static_cast<size_t>(g) * kN;
+    ig[l] = o0;
+    ig[l + 227] = o1;
+    if (own2) ig[l + 454] = o2;
+  }
 }
 
 // ---- 3. all-entry parse of one chunk ---------------------------------------------------------
@@ -283,6 +303,12 @@ struct EntryArgs {
   int ecap;
   int *err;
   long long *stats;       // RSAMD_DIAG builds only: per-chunk tracking statistics (else null)
+  // split stream (chunk-aligned generators): the first launch of k_np_entry reads only the
+  // chunk's first xlim draws (the first stream pass); a chunk still dense there pauses (its list
+  // in fin, position in tpos, pause[c] = 1) and the resume launch (after the second pass)
+  // carries it on
+  int xlim, resume;
+  int *pause;
 };
 
 __device__ __forceinline__ int block_excl_scan(int v, int *sh, int *total) {
@@ -360,6 +386,8 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
   const int c = blockIdx.x;
   const int64_t t0 = static_cast<int64_t>(c) * a.W;
   const int T = static_cast<int>(std::min<int64_t>(a.W, a.D - t0));
+  const int TL = min(T, a.xlim);  // draws this launch may read
+  if (a.resume && !a.pause[c]) return;
   const uint32_t *__restrict__ wp = draws + t0;
   uint2 *ev = a.ev + static_cast<size_t>(c) * a.ecap;
   const uint32_t N1 = static_cast<uint32_t>(n1);
@@ -367,13 +395,24 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
     np_stamp(c, kTsEntryR0, kTsEntryC0);
     np_stamp_val(c, kTsEntryHw, hw_where());
   }
-  for (int q = tid; q < n1; q += kEntryThreads) {
-    st[q] = static_cast<uint16_t>(n1 - q);
-    lo[q] = static_cast<uint16_t>(q);
-  }
-  if (tid == 0) sh_evn = 0;
-  __syncthreads();
   int m = n1, t = 0;
+  if (a.resume) {  // the paused list, draw position and wrap count
+    m = a.fin_m[c];
+    t = a.tpos[c];
+    for (int q = tid; q < m; q += kEntryThreads) {
+      const uint32_t x = a.fin[static_cast<size_t>(c) * n1 + q];
+      st[q] = static_cast<uint16_t>(x >> 16);
+      lo[q] = static_cast<uint16_t>(x & 0xffffu);
+    }
+    if (tid == 0) sh_evn = a.ev_n[c];
+  } else {
+    for (int q = tid; q < n1; q += kEntryThreads) {
+      st[q] = static_cast<uint16_t>(n1 - q);
+      lo[q] = static_cast<uint16_t>(q);
+    }
+    if (tid == 0) sh_evn = 0;
+  }
+  __syncthreads();
   const int hand = hand_of(n1);
   const int nfast = fast_batches(n1), nfastm = fast_batches_multi(n1);
 #ifdef RSAMD_DIAG
@@ -404,9 +443,9 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
     // the words of the next two 64-draw batches, lane l holding draw l of each, loaded one
     // batch ahead in every wave: the stream comes from HBM, and a load issued where it is
     // used cost ~40 cycles per draw (one HBM round trip per batch)
-    uint32_t wa = lane < T ? wp[lane] : 0u, wb = 64 + lane < T ? wp[64 + lane] : 0u;
-    while (m > hand && t < T) {
-      const int kk = min(kK, T - t);
+    uint32_t wa = t + lane < TL ? wp[t + lane] : 0u, wb = t + 64 + lane < TL ? wp[t + 64 + lane] : 0u;
+    while (m > hand && t < TL) {
+      const int kk = min(kK, TL - t);
       const int nr = (m + kEntryThreads - 1) / kEntryThreads;
       if (nr == 1 && kk == 64) {
         // one slot per thread (the common case after the first ~n1 draws): the 64 words in a
@@ -414,7 +453,7 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
         // as n1 > 64) logged after the batch with one LDS atomic per wave
         // up to nfast batches between compactions (a slot's list neighbours, used by the wrap
         // log, change only at a compaction)
-        for (int fb = 0; fb < nfast && T - t >= 64; ++fb) {
+        for (int fb = 0; fb < nfast && TL - t >= 64; ++fb) {
           // (waves holding only empty slots skip the batch: sentinels stay sentinels)
           uint32_t sv = s[0], wk = 0xffffffffu;
           if ((tid & ~63) < m) {
@@ -442,14 +481,14 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
           }
           t += 64;
           wa = wb;
-          wb = t + 64 + lane < T ? wp[t + 64 + lane] : 0u;
+          wb = t + 64 + lane < TL ? wp[t + 64 + lane] : 0u;
           RSD_ETICK(2, 64);
         }
       } else if (kk == 64 && nr <= kRFast) {
         // several slots per thread: branch-free steps, each slot's wrap (at most one in 64
         // draws, as n1 > 64) logged after the batch; up to nfastm batches between compactions
         // (member ranges change only at a compaction)
-        for (int fb = 0; fb < nfastm && T - t >= 64; ++fb) {
+        for (int fb = 0; fb < nfastm && TL - t >= 64; ++fb) {
           uint32_t wk[kRFast];
 #pragma unroll
           for (int r = 0; r < kRFast; ++r) wk[r] = 0xffffffffu;
@@ -485,7 +524,7 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
           }
           t += 64;
           wa = wb;
-          wb = t + 64 + lane < T ? wp[t + 64 + lane] : 0u;
+          wb = t + 64 + lane < TL ? wp[t + 64 + lane] : 0u;
           RSD_ETICK(1, 64);
         }
       } else {
@@ -511,7 +550,7 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
       }
       t += kk;
       wa = wb;
-      wb = t + 64 + lane < T ? wp[t + 64 + lane] : 0u;
+      wb = t + 64 + lane < TL ? wp[t + 64 + lane] : 0u;
       RSD_ETICK(0, kk);
       }
       // compaction: equal cyclic neighbours merge, the first of a run keeps its lo (the list
@@ -569,10 +608,22 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
       o[9] = m;
     }
 #endif
+    if (m > hand && t < T) {  // paused at the first stream pass's end: resumed after the second
+      for (int q = tid; q < m; q += kEntryThreads)
+        a.fin[static_cast<size_t>(c) * n1 + q] = lo[q] | (static_cast<uint32_t>(st[q]) << 16);
+      if (tid == 0) {
+        a.fin_m[c] = m;
+        a.ev_n[c] = sh_evn;
+        a.tpos[c] = t;
+        a.pause[c] = 1;
+      }
+      return;
+    }
     if (m > hand) {  // chunk done while still dense
       for (int q = tid; q < m; q += kEntryThreads)
         a.fin[static_cast<size_t>(c) * n1 + q] = lo[q] | (static_cast<uint32_t>(st[q]) << 16);
       if (tid == 0) {
+        if (!a.resume) a.pause[c] = 0;
         a.fin_m[c] = m;
         a.ev_n[c] = min(sh_evn, a.ecap);
         if (sh_evn > a.ecap) atomicOr(a.err, 1);
@@ -591,6 +642,7 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
     a.fin_m[c] = m;
     a.ev_n[c] = sh_evn;
     a.tpos[c] = t;
+    if (!a.resume) a.pause[c] = 0;
     np_stamp(c, kTsEntryR1, kTsEntryC1);
     np_stamp_val(c, kTsEntryT, static_cast<unsigned long long>(t));
     np_stamp_val(c, kTsEntryM, static_cast<unsigned long long>(m));
@@ -1463,28 +1515,33 @@ __global__ __launch_bounds__(64) void k_np_result(const uint32_t *__restrict__ s
 
 // ---- host ------------------------------------------------------------------------------------
 struct JumpPolys {
-  std::vector<std::vector<int32_t>> bits;  // level k: set bits of x^(2^k kJ) mod phi, the even
+  std::vector<std::vector<int32_t>> bits;  // level k: set bits of x^(2^k J) mod phi, the even
   std::vector<int> ne;                     // ones first (ne[k] of them), then the odd ones
 };
 
-const JumpPolys &jump_polys() {
-  static JumpPolys jp;
-  static std::once_flag once;
-  std::call_once(once, [] {
-    std::vector<uint64_t> p;
-    rs::mt_jump_poly(static_cast<uint64_t>(kJ), p);
-    for (int k = 0; k < kLevels; ++k) {
-      if (k) rs::mt_poly_square(p);
-      std::vector<int32_t> b;
-      for (int par = 0; par < 2; ++par) {
-        for (int i = par; i < kDeg; i += 2)
-          if ((p[static_cast<size_t>(i) >> 6] >> (i & 63)) & 1u) b.push_back(i);
-        if (par == 0) jp.ne.push_back(static_cast<int>(b.size()));
-      }
-      jp.bits.push_back(std::move(b));
+// the level polynomials for generators of JB blocks (J = 624 JB words), built once per JB
+// (~0.1 s of host arithmetic; chunk-aligned layouts use the chunk length)
+const JumpPolys &jump_polys(int JB) {
+  static std::mutex mu;
+  static std::vector<std::pair<int, JumpPolys *>> cache;
+  std::lock_guard<std::mutex> g(mu);
+  for (auto &e : cache)
+    if (e.first == JB) return *e.second;
+  auto *jp = new JumpPolys();
+  std::vector<uint64_t> p;
+  rs::mt_jump_poly(static_cast<uint64_t>(kN) * static_cast<uint64_t>(JB), p);
+  for (int k = 0; k < kLevels; ++k) {
+    if (k) rs::mt_poly_square(p);
+    std::vector<int32_t> b;
+    for (int par = 0; par < 2; ++par) {
+      for (int i = par; i < kDeg; i += 2)
+        if ((p[static_cast<size_t>(i) >> 6] >> (i & 63)) & 1u) b.push_back(i);
+      if (par == 0) jp->ne.push_back(static_cast<int>(b.size()));
     }
-  });
-  return jp;
+    jp->bits.push_back(std::move(b));
+  }
+  cache.emplace_back(JB, jp);
+  return *jp;
 }
 
 uint32_t untemper(uint32_t z) {
@@ -1563,6 +1620,11 @@ int64_t knob_cpr() {
   static const int64_t v = std::max<int64_t>(0, env_i64("RSAMD_NP_CPR"));
   return v;
 }
+// chunk-aligned generators and the two-pass stream (RSAMD_NP_SPLIT=0: off), read at every call
+bool split_knob() {
+  const char *e = std::getenv("RSAMD_NP_SPLIT");
+  return !e || std::atoi(e) != 0;
+}
 constexpr int64_t kMapsMagic = 0x5253485044414d53LL;   // blob header tag
 
 // start draw (relative to the rank's draw 0) of every kept wrap, in order; lead = 1 puts the
@@ -1603,6 +1665,10 @@ struct rs_np_shard {
   // layout of the current segment (shard_layout)
   int64_t count = 0, Wc = 0, Cr = 0, C = 0, D = 0;
   int64_t s_lo = 0, g0 = 0, wbase = 0, Lb = 0, G = 0, nwords = 0;
+  // generators of JB stream blocks (kJB, or the chunk length for chunk-aligned layouts, whose
+  // last generator runs on to the segment's end: gext); xb > 0: the stream in two passes (blocks
+  // 1..xb of every generator first), the entry kernel reading the first xlim draws of a chunk
+  int JB = kJB, gext = 0, xb = 0, xlim = 0, bits_JB = 0;
   int ecap = 0, ecap_shift = 0;
   int state = 0;  // 0 idle, 1 parsed, 2 composed
   int64_t nstarts = 0, first_start = -1;
@@ -1613,13 +1679,16 @@ struct rs_np_shard {
   uint32_t *d_win = nullptr, *d_chain = nullptr, *d_stream = nullptr, *d_fin = nullptr,
            *d_fin_all = nullptr;
   int *d_fin_m = nullptr, *d_fin_m_all = nullptr, *d_ev_n = nullptr, *d_ent = nullptr,
-      *d_vcnt = nullptr, *d_off = nullptr, *d_err = nullptr, *d_tpos = nullptr;
+      *d_vcnt = nullptr, *d_off = nullptr, *d_err = nullptr, *d_tpos = nullptr, *d_pause = nullptr;
+  uint32_t *d_io = nullptr;  // raw block of every generator between the two stream passes
+  hipStream_t s2 = nullptr;  // the second stream pass
+  hipEvent_t ev_a = nullptr, ev_b = nullptr;
   int64_t *d_row_off = nullptr, *d_starts = nullptr, *d_got = nullptr;
   uint2 *d_ev = nullptr;
   NpResult *d_res = nullptr;  // world 1 (np_choice_device): the segment's outcome in one copy
   int64_t cap_win = 0, cap_chain = 0, cap_stream = 0, cap_fin = 0, cap_fin_all = 0, cap_fm = 0,
           cap_fm_all = 0, cap_ev = 0, cap_evn = 0, cap_ent = 0, cap_vcnt = 0, cap_off = 0,
-          cap_tpos = 0, cap_row = 0, cap_starts = 0;
+          cap_tpos = 0, cap_row = 0, cap_starts = 0, cap_pause = 0, cap_io = 0;
 };
 
 namespace {
@@ -1631,6 +1700,11 @@ void shard_free(rs_np_shard *w) {
                   w->d_res};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
+  if (w->d_pause) (void)hipFree(w->d_pause);
+  if (w->d_io) (void)hipFree(w->d_io);
+  if (w->ev_a) (void)hipEventDestroy(w->ev_a);
+  if (w->ev_b) (void)hipEventDestroy(w->ev_b);
+  if (w->s2) (void)hipStreamDestroy(w->s2);
 }
 
 // kernel attributes for populations up to n1 (dynamic LDS of the entry and tuple kernels)
@@ -1689,7 +1763,14 @@ int shard_layout(rs_np_shard &w, int32_t pos, int64_t count) {
   const int64_t C0 = knob_cpr() ? knob_cpr()
                                 : std::max<int64_t>(1, std::min<int64_t>(
                                                            Cdef, Dr / std::max<int64_t>(kWmin, 64 * w.n1)));
-  const int64_t L = cdiv(cdiv(Dr, C0), 4096) * 4096;
+  // Chunk-aligned generators (N - 1 < 4096, chunks of at most two default generators): every
+  // chunk starts a generator (J = the chunk length, a whole number of blocks), so the chunks'
+  // first draws are generated in a short first pass and the rest on a second stream while the
+  // entry kernel parses them (the stream's 0.33 ms beside the entry kernel at C2)
+  const int64_t Lraw = cdiv(Dr, C0);
+  const bool aligned = !knob_kw() && split_knob() && w.n1 < 4096 && Lraw >= kWmin &&
+                       cdiv(Lraw, kN) <= 2 * kJB;
+  const int64_t L = aligned ? cdiv(Lraw, kN) * kN : cdiv(Lraw, 4096) * 4096;
   w.Wc = knob_kw() ? knob_kw() : std::max<int64_t>(kWmin, std::min<int64_t>(kW, L));
   w.Cr = cdiv(Dr, w.Wc);
   w.C = w.Cr * w.world;
@@ -1700,12 +1781,31 @@ int shard_layout(rs_np_shard &w, int32_t pos, int64_t count) {
   const int64_t s_end = w.s_lo + w.Cr * w.Wc + margin;
   // the first generator: every word the rank reads lies in a block it writes whole (a jumped
   // window's word 0 carries only its top bit)
-  w.g0 = w.rank == 0 ? 0 : (w.s_lo - kN) / kJ;
+  w.JB = aligned ? static_cast<int>(w.Wc / kN) : kJB;
+  const int64_t J = static_cast<int64_t>(kN) * w.JB;
+  w.g0 = w.rank == 0 ? 0 : (w.s_lo - kN) / J;
   if (w.g0 >> kLevels) return rs::fail(RS_EINVAL, "np shard: stream offset beyond the jump table");
-  w.wbase = w.g0 * kJ;
-  w.Lb = cdiv(s_end, kN) - w.g0 * kJB;
-  w.G = cdiv(w.Lb, kJB);
+  w.wbase = w.g0 * J;
+  w.Lb = cdiv(s_end, kN) - w.g0 * w.JB;
+  w.gext = aligned ? 1 : 0;
+  w.G = aligned ? std::max<int64_t>(1, w.Lb / w.JB) : cdiv(w.Lb, w.JB);
   if (w.G > (int64_t(1) << kLevels)) return rs::fail(RS_EINVAL, "np shard: segment too long");
+  // the first pass: every generator's blocks 1..xb, so that each chunk's first xlim draws
+  // (offset oq into its generator) exist; a chunk whose dense phase goes further pauses
+  const int64_t oq = (w.s_lo - w.wbase) % J;
+  w.xb = 0;
+  w.xlim = std::numeric_limits<int>::max();
+  if (aligned && oq >= 1) {
+    // (the dense phase ends within 23 360 draws at C2; RSAMD_NP_XDRAWS overrides: tests of the
+    // pause / resume path)
+    const int64_t xd = env_i64("RSAMD_NP_XDRAWS");
+    const int64_t want = xd > 0 ? xd : 16 * static_cast<int64_t>(w.n1) + 8192;
+    const int64_t xb = cdiv(want + oq, kN);
+    if (xb < w.JB) {
+      w.xb = static_cast<int>(xb);
+      w.xlim = static_cast<int>((xb + 1) * kN - oq);
+    }
+  }
   w.nwords = w.Lb * kN - (w.s_lo - w.wbase);
   w.ecap_shift = 0;
   return RS_OK;
@@ -1715,8 +1815,25 @@ int shard_layout(rs_np_shard &w, int32_t pos, int64_t count) {
 int shard_windows(rs_np_shard &w, const uint32_t *key, hipStream_t s) {
   int st;
   if ((st = sgrow(w.d_win, w.cap_win, w.G * kN))) return st;
-  const JumpPolys &jp = jump_polys();
-  (void)jp;
+  if (w.bits_JB != w.JB) {  // the level polynomials of this generator length
+    const JumpPolys &jp = jump_polys(w.JB);
+    std::vector<int32_t> all;
+    w.bit_off.clear();
+    w.bit_n.clear();
+    w.bit_ne.clear();
+    for (size_t k = 0; k < jp.bits.size(); ++k) {
+      w.bit_off.push_back(static_cast<int>(all.size()));
+      w.bit_n.push_back(static_cast<int>(jp.bits[k].size()));
+      w.bit_ne.push_back(jp.ne[k]);
+      all.insert(all.end(), jp.bits[k].begin(), jp.bits[k].end());
+    }
+    int64_t cap = 0;
+    if (w.d_bits) (void)hipFree(w.d_bits);
+    w.d_bits = nullptr;
+    if ((st = sgrow(w.d_bits, cap, static_cast<int64_t>(all.size())))) return st;
+    HIP_TRY(hipMemcpy(w.d_bits, all.data(), sizeof(int32_t) * all.size(), hipMemcpyHostToDevice));
+    w.bits_JB = w.JB;
+  }
   if (w.g0 == 0) {
     HIP_TRY(hipMemcpyAsync(w.d_win, key, sizeof(uint32_t) * kN, hipMemcpyHostToDevice, s));
   } else {
@@ -1755,21 +1872,13 @@ int shard_init(rs_np_shard &w) {
   HIP_TRY(hipSetDevice(w.ctx->device));
   int st;
   if ((st = shard_kernel_attrs(w.n1))) return st;
-  if (!w.d_bits) {
-    const JumpPolys &jp = jump_polys();
-    std::vector<int32_t> all;
-    for (const auto &b : jp.bits) {
-      w.bit_off.push_back(static_cast<int>(all.size()));
-      w.bit_n.push_back(static_cast<int>(b.size()));
-      w.bit_ne.push_back(jp.ne[w.bit_ne.size()]);
-      all.insert(all.end(), b.begin(), b.end());
-    }
-    int64_t cap = 0;
-    if ((st = sgrow(w.d_bits, cap, static_cast<int64_t>(all.size())))) return st;
-    HIP_TRY(hipMemcpy(w.d_bits, all.data(), sizeof(int32_t) * all.size(), hipMemcpyHostToDevice));
+  if (!w.d_err) {
     int64_t c1 = 0, c2 = 0, c3 = 0;
     if ((st = sgrow(w.d_err, c1, 1)) || (st = sgrow(w.d_got, c2, 1)) || (st = sgrow(w.d_res, c3, 1)))
       return st;
+    HIP_TRY(hipStreamCreateWithFlags(&w.s2, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&w.ev_a, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&w.ev_b, hipEventDisableTiming));
   }
   return RS_OK;
 }
@@ -1780,12 +1889,27 @@ int shard_stream(rs_np_shard &w, const uint32_t *key) {
   int st;
   if ((st = sgrow(w.d_stream, w.cap_stream, w.Lb * kN))) return st;
   if ((st = shard_windows(w, key, s))) return st;
-  k_mt_stream<<<static_cast<unsigned>(w.G), 256, 0, s>>>(w.d_win, w.d_stream, w.Lb);
-  HIP_TRY(hipGetLastError());
+  const int G = static_cast<int>(w.G), JB = w.JB;
+  if (w.xb > 0) {  // blocks 1..xb here, the rest on s2 beside the entry kernel (event ev_b)
+    if ((st = sgrow(w.d_io, w.cap_io, w.G * kN))) return st;
+    k_mt_stream<<<static_cast<unsigned>(G), 256, 0, s>>>(w.d_win, w.d_stream, w.Lb, JB, G, w.gext, 0,
+                                                         w.xb, w.d_io);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(w.ev_a, s));
+    HIP_TRY(hipStreamWaitEvent(w.s2, w.ev_a, 0));
+    k_mt_stream<<<static_cast<unsigned>(G), 256, 0, w.s2>>>(w.d_win, w.d_stream, w.Lb, JB, G, w.gext,
+                                                            w.xb, std::numeric_limits<int>::max(), w.d_io);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(w.ev_b, w.s2));
+  } else {
+    k_mt_stream<<<static_cast<unsigned>(G), 256, 0, s>>>(w.d_win, w.d_stream, w.Lb, JB, G, w.gext, 0,
+                                                         std::numeric_limits<int>::max(), nullptr);
+    HIP_TRY(hipGetLastError());
+  }
   if ((st = sgrow(w.d_fin, w.cap_fin, w.Cr * w.n1)) || (st = sgrow(w.d_fin_m, w.cap_fm, w.Cr)) ||
       (st = sgrow(w.d_ev_n, w.cap_evn, w.Cr)) || (st = sgrow(w.d_tpos, w.cap_tpos, w.Cr)) ||
       (st = sgrow(w.d_vcnt, w.cap_vcnt, w.Cr)) || (st = sgrow(w.d_off, w.cap_off, w.Cr)) ||
-      (st = sgrow(w.d_ent, w.cap_ent, w.Cr)) ||
+      (st = sgrow(w.d_ent, w.cap_ent, w.Cr)) || (st = sgrow(w.d_pause, w.cap_pause, w.Cr)) ||
       // every hypothesis spans at least n1 draws: a bound on the own starts
       (st = sgrow(w.d_starts, w.cap_starts, w.Cr * w.Wc / std::max(1, w.n1) + 4)))
     return st;
@@ -1825,16 +1949,28 @@ int shard_enqueue_parse(rs_np_shard &w) {
                                    hipMemcpyHostToDevice, s));
   }
   EntryArgs ea{w.d_stream + (w.s_lo - w.wbase), w.Cr * w.Wc, Wc, w.n1, w.d_fin, w.d_fin_m,
-               w.d_ev, w.d_ev_n, w.d_tpos, w.ecap, w.d_err, d_stats};
+               w.d_ev, w.d_ev_n, w.d_tpos, w.ecap, w.d_err, d_stats, w.xlim, 0, w.d_pause};
   const bool small = w.n1 < 64;  // several hypothesis ends in one tracking window
-  if (w.py) {
-    k_np_entry<true><<<Cr, kEntryThreads, static_cast<size_t>(lds), s>>>(ea, ea.draws);
+  // (split stream: the first launch reads the first pass's words; the second pass joins before
+  // the resume launch, which carries on the chunks that paused)
+  auto entry = [&](bool py) -> int {
+    EntryArgs e2 = ea;
+    (py ? k_np_entry<true> : k_np_entry<false>)<<<Cr, kEntryThreads, static_cast<size_t>(lds), s>>>(e2, e2.draws);
     HIP_TRY(hipGetLastError());
+    if (w.xb > 0) {
+      HIP_TRY(hipStreamWaitEvent(s, w.ev_b, 0));
+      e2.resume = 1;
+      e2.xlim = std::numeric_limits<int>::max();
+      (py ? k_np_entry<true> : k_np_entry<false>)<<<Cr, kEntryThreads, static_cast<size_t>(lds), s>>>(e2, e2.draws);
+      HIP_TRY(hipGetLastError());
+    }
+    return RS_OK;
+  };
+  if ((st = entry(w.py))) return st;
+  if (w.py) {
     (small ? k_np_track<true, true>
            : (hand_of(w.n1) > 64 ? k_np_track128<true> : k_np_track<true, false>))<<<Cr, 64 * kTrackWaves, 0, s>>>(ea, ea.draws);
   } else {
-    k_np_entry<false><<<Cr, kEntryThreads, static_cast<size_t>(lds), s>>>(ea, ea.draws);
-    HIP_TRY(hipGetLastError());
     (small ? k_np_track<false, true>
            : (hand_of(w.n1) > 64 ? k_np_track128<false> : k_np_track<false, false>))<<<Cr, 64 * kTrackWaves, 0, s>>>(ea, ea.draws);
   }
@@ -2046,7 +2182,7 @@ int shard_tuples(rs_np_shard &w, int64_t base, int64_t hi, int64_t next_start, i
     const int64_t W = w.s_lo + used;  // global word index of the next draw
     if (W > kN) {
       const int64_t b = (W - 1) / kN;
-      const int64_t lb = b - w.g0 * kJB;
+      const int64_t lb = b - w.g0 * w.JB;
       if (lb < (w.g0 ? 1 : 0) || lb >= w.Lb) return rs::fail(RS_EDEVICE, "np shard: final block outside the rank's stream");
       uint32_t blk[kN];
       HIP_TRY(hipMemcpy(blk, w.d_stream + lb * kN, sizeof(blk), hipMemcpyDeviceToHost));
