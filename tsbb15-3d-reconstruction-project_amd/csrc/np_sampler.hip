@@ -75,6 +75,12 @@ constexpr int kK = 64;                       // draws between compactions (<= N 
 __host__ __device__ constexpr int fast_batches(int n1) { return n1 >= 4096 ? 32 : 16; }
 __host__ __device__ constexpr int fast_batches_multi(int n1) { return n1 >= 4096 ? 4 : 1; }
 constexpr int kRFast = 8;                    // slots per thread of the branch-free multi-slot path
+#ifndef RSAMD_ONESLOT2
+#define RSAMD_ONESLOT2 1  // two-bucket batches in the one-slot dense path (A/B builds: 0)
+#endif
+#ifndef RSAMD_MULTI2
+#define RSAMD_MULTI2 1    // the same per slot in the multi-slot dense path (A/B builds: 0)
+#endif
 // Trajectories left when the dense parse hands a chunk to the tracking kernel, also the tracking
 // kernel's list capacity (a template argument, <= 8 per wave of its 16).  The
 // one-slot dense path costs ~N per draw and chunk, so large N hands over earlier: measured
@@ -457,13 +463,41 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
           // (waves holding only empty slots skip the batch: sentinels stay sentinels)
           uint32_t sv = s[0], wk = 0xffffffffu;
           if ((tid & ~63) < m) {
+#if RSAMD_ONESLOT2
+            // Two-bucket batch: when every lane's state stays within its bucket and the one
+            // below for the 64 draws (and so cannot wrap), both draw rules are taken off the
+            // chain and a step is select / compare / subtract (the general step: clz, shift,
+            // and, compare, subtract, wrap test and select).  Sentinel slots qualify.
+            uint32_t lw, lw2, sh = 0, M = 0;
+            if constexpr (PY) {
+              sh = static_cast<uint32_t>(__builtin_clz(sv + 1u));
+              lw = (1u << (31u - sh)) - 1u;
+              lw2 = sh < 30u ? (1u << (30u - sh)) - 1u : 0x7fffffffu;
+            } else {
+              M = 0xffffffffu >> __builtin_clz(sv);
+              lw = (M >> 1) + 1u;
+              lw2 = M > 1u ? (M >> 2) + 1u : 0x7fffffffu;
+            }
+            const bool fast = sv >= lw2 + 64u && lw2 >= 1u && lw2 != 0x7fffffffu;
+            if (__ballot(!fast) == 0ull) {
 #pragma unroll
-            for (int k = 0; k < 64; ++k) {
-              const uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wa), k));
-              sv -= draw_of<PY>(w, sv) <= sv ? 1u : 0u;
-              const bool z = sv == 0;
-              sv = z ? N1 : sv;
-              wk = z ? static_cast<uint32_t>(k) : wk;
+              for (int k = 0; k < 64; ++k) {
+                const uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wa), k));
+                const uint32_t uh = PY ? (w >> sh) : (w & M), ul = PY ? (w >> (sh + 1u)) : (w & (M >> 1));
+                const uint32_t u = sv >= lw ? uh : ul;
+                sv -= u <= sv ? 1u : 0u;
+              }
+            } else
+#endif
+            {
+#pragma unroll
+              for (int k = 0; k < 64; ++k) {
+                const uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wa), k));
+                sv -= draw_of<PY>(w, sv) <= sv ? 1u : 0u;
+                const bool z = sv == 0;
+                sv = z ? N1 : sv;
+                wk = z ? static_cast<uint32_t>(k) : wk;
+              }
             }
           }
           s[0] = sv;
@@ -492,6 +526,46 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
           uint32_t wk[kRFast];
 #pragma unroll
           for (int r = 0; r < kRFast; ++r) wk[r] = 0xffffffffu;
+#if RSAMD_MULTI2
+          // slot by slot: a slot whose states all stay within their bucket and the one below
+          // for the batch takes the two-bucket step (as the one-slot path), else the general one
+#pragma unroll
+          for (int r = 0; r < kRFast; ++r) {
+            if (r >= nr) break;
+            uint32_t sv = s[r], wkr = 0xffffffffu;
+            uint32_t lw, lw2, sh = 0, M = 0;
+            if constexpr (PY) {
+              sh = static_cast<uint32_t>(__builtin_clz(sv + 1u));
+              lw = (1u << (31u - sh)) - 1u;
+              lw2 = sh < 30u ? (1u << (30u - sh)) - 1u : 0x7fffffffu;
+            } else {
+              M = 0xffffffffu >> __builtin_clz(sv);
+              lw = (M >> 1) + 1u;
+              lw2 = M > 1u ? (M >> 2) + 1u : 0x7fffffffu;
+            }
+            const bool fast = sv >= lw2 + 64u && lw2 >= 1u && lw2 != 0x7fffffffu;
+            if (__ballot(!fast) == 0ull) {
+#pragma unroll 16
+              for (int k = 0; k < 64; ++k) {
+                const uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wa), k));
+                const uint32_t uh = PY ? (w >> sh) : (w & M), ul = PY ? (w >> (sh + 1u)) : (w & (M >> 1));
+                const uint32_t u = sv >= lw ? uh : ul;
+                sv -= u <= sv ? 1u : 0u;
+              }
+            } else {
+#pragma unroll 16
+              for (int k = 0; k < 64; ++k) {
+                const uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wa), k));
+                sv -= draw_of<PY>(w, sv) <= sv ? 1u : 0u;
+                const bool z = sv == 0;
+                sv = z ? N1 : sv;
+                wkr = z ? static_cast<uint32_t>(k) : wkr;
+              }
+            }
+            s[r] = sv;
+            wk[r] = wkr;
+          }
+#else
 #pragma unroll 1
           for (int k = 0; k < 64; ++k) {
             const uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wa), k));
@@ -505,6 +579,7 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
               wk[r] = z ? static_cast<uint32_t>(k) : wk[r];
             }
           }
+#endif
 #pragma unroll
           for (int r = 0; r < kRFast; ++r) {
             if (r >= nr) break;
