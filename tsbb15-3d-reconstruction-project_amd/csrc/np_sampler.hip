@@ -317,14 +317,21 @@ struct EntryArgs {
   int *pause;
 };
 
+// inclusive wave scan by DPP (row shifts, then the row broadcasts into the upper rows): six
+// vector ops instead of six LDS permutes
+__device__ __forceinline__ int wave_incl_scan(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return x;
+}
+
 __device__ __forceinline__ int block_excl_scan(int v, int *sh, int *total) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  int x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
+  const int x = wave_incl_scan(v);  // (by LDS permutes: +4 us per C2 entry launch)
   if (lane == 63) sh[wid] = x;
   __syncthreads();
   int base = 0, tot = 0;
