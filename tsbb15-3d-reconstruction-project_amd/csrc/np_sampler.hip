@@ -1231,14 +1231,28 @@ __global__ __launch_bounds__(64) void k_np_filter(uint2 *__restrict__ ev, const 
 // ---- 4. compose the chunk maps on the GPU ------------------------------------------------
 // Chunk c's final list maps entry list index a (state n1 - a) to the state of the entry with the
 // largest start lo <= a (cyclically: the largest lo overall if none); chunk 0 starts a
-// hypothesis (a = 0).  The whole workgroup stages kComposeBlock chunks at a time in LDS
-// (coalesced), then wave 0 walks them serially.  (C2, 512 chunks: 187 us with a key-maximum
-// shuffle reduction per chunk, 101 us with the rotated rows and one ballot per chunk.)
+// hypothesis (a = 0).  A map is thus a step function of a: its entries rotated so that lo
+// ascends, value v = n1 - state, below the first lo the last value.  Two maps compose on the
+// first one's steps (g o f has f's steps, values g(v)), so a composition of consecutive chunks
+// holds <= 64 steps at every level.  Per block of kComposeBlock chunks, all in LDS: the rows
+// are staged (coalesced, every load in flight) and rotated, an up-sweep composes sibling pairs
+// (a wave per node, a lane per step, a binary search of the sibling's steps), the down-sweep
+// hands each node's entry to its left child and the left child's value of it to the right
+// one; the block's root carries the entry to the next block.  (The serial walk of wave 0 --
+// one ballot / find-last / readlane per chunk -- took 104 us for C2's 512 chunks and
+// 0.3-0.6 ms for the 1 000-4 000 chunks of a split parse; it remains for blocks holding a
+// chunk that ended dense, whose list may exceed 64 entries.)
 constexpr int kComposeBlock = 256;
-// Rows of <= 64 entries are first rotated (by all 16 waves, in parallel) so that lo ascends
-// along the lanes; the serial walk of wave 0 is then one ballot per chunk: the wanted entry is
-// the highest lane with lo <= a (none: the last lane, the largest lo).  Longer lists (chunks
-// that ended dense) take the key-maximum scan from HBM.
+constexpr int kComposeNodes = 2 * kComposeBlock + 8;  // all levels of a block's tree
+__device__ __forceinline__ int step_eval(const uint32_t *node, int m, int e) {
+  int lo = 0, hi = m;  // the largest k with lo_k <= e (lo ascending), else m - 1
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (static_cast<int>(node[mid] & 0xffffu) <= e) lo = mid + 1;
+    else hi = mid;
+  }
+  return static_cast<int>(node[lo > 0 ? lo - 1 : m - 1] >> 16);
+}
 // row_off (optional): where chunk c's list starts in fin (the gathered, packed maps of a
 // sharded parse); null: row c at c * n1.
 __global__ __launch_bounds__(1024) void k_np_compose(const uint32_t *__restrict__ fin,
@@ -1248,67 +1262,129 @@ __global__ __launch_bounds__(1024) void k_np_compose(const uint32_t *__restrict_
   auto row = [&](int c) -> const uint32_t * {
     return fin + (row_off ? row_off[c] : static_cast<int64_t>(c) * n1);
   };
-  __shared__ uint32_t rows[kComposeBlock][64];
-  __shared__ int ms[kComposeBlock], es[kComposeBlock];
+  __shared__ uint32_t pool[kComposeNodes * 64];  // tree nodes (the serial walk: its rows)
+  __shared__ int nm[kComposeNodes], ne[kComposeNodes];  // steps and entry per node
+  __shared__ int big, carry;
   const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
-  int a = 0;
+  if (tid == 0) carry = 0;
   for (int c0 = 0; c0 < C; c0 += kComposeBlock) {
     const int nb = min(kComposeBlock, C - c0);
-    for (int k = tid; k < nb; k += 1024) ms[k] = fin_m[c0 + k];
+    if (tid == 0) big = 0;
     __syncthreads();
+    for (int k = tid; k < nb; k += 1024) {
+      nm[k] = fin_m[c0 + k];
+      if (nm[k] > 64) big = 1;
+    }
+    __syncthreads();
+    // the block's rows, every load of a thread in flight at once
+    {
+      constexpr int kPer = kComposeBlock * 64 / 1024;
+      uint32_t v[kPer];
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const int k = tid + j * 1024, r = k >> 6, q = k & 63;
+        v[j] = r < nb && q < nm[r] && nm[r] <= 64 ? row(c0 + r)[q] : 0xffffffffu;
+      }
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) pool[tid + j * 1024] = v[j];
+    }
+    __syncthreads();
+    // rotated so that lo ascends (a wave per row); tree rows hold lo | v << 16
     for (int r = wv; r < nb; r += 16) {
-      const int m = ms[r];
+      const int m = nm[r];
       if (m > 64) continue;
-      const uint32_t x = l < m ? row(c0 + r)[l] : 0xffffffffu;
-      // the lane holding the smallest lo starts the rotated row
+      const uint32_t x = l < m ? pool[r * 64 + l] : 0xffffffffu;
       uint32_t mn = x & 0xffffu;
 #pragma unroll
       for (int o = 32; o; o >>= 1) mn = min(mn, static_cast<uint32_t>(__shfl_xor(static_cast<int>(mn), o)));
       const uint64_t at = __ballot(l < m && (x & 0xffffu) == mn);
       const int p0 = __ffsll(static_cast<long long>(at)) - 1;
-      if (l < m) rows[r][l - p0 >= 0 ? l - p0 : l - p0 + m] = x;
+      __builtin_amdgcn_wave_barrier();
+      if (l < m)
+        pool[r * 64 + (l - p0 >= 0 ? l - p0 : l - p0 + m)] =
+            big ? x : ((x & 0xffffu) | ((static_cast<uint32_t>(n1) - (x >> 16)) << 16));
     }
     __syncthreads();
-    if (wv == 0) {
-      // the next row is read while the current one is walked (the walk is the serial chain)
-      uint32_t xn = rows[0][l];
-      int mn = ms[0];
-      for (int r = 0; r < nb; ++r) {
-        const int c = c0 + r, m = mn;
-        const uint32_t xr = xn;
-        if (r + 1 < nb) {
-          xn = rows[r + 1][l];
-          mn = ms[r + 1];
-        }
-        es[r] = a;  // (every lane writes the same value)
-        if (m <= 64) {
-          const uint32_t x = l < m ? xr : 0xffffffffu;
-          const uint64_t le = __ballot(l < m && static_cast<int>(x & 0xffffu) <= a);
-          const int idx = le ? 63 - __builtin_clzll(le) : m - 1;
-          a = n1 - static_cast<int>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), idx)) >> 16);
-          continue;
-        }
-        uint32_t kb = 0, kt = 0;
-        bool hb = false, ht = false;
-        for (int k = l; k < m; k += 64) {
-          const uint32_t x = row(c)[k];
-          const uint32_t lo = x & 0xffffu, key = (lo << 16) | (x >> 16);
-          if (static_cast<int>(lo) <= a && (!hb || key > kb)) kb = key, hb = true;
-          if (!ht || key > kt) kt = key, ht = true;
-        }
-        const uint64_t anyb = __ballot(hb);
-        // keys of valid rows are distinct; invalid lanes hold 0 and lose every max below
-        uint32_t mb = hb ? kb : 0u, mt = ht ? kt : 0u;
+    if (big) {  // the serial walk (rows: lo | state << 16)
+      if (wv == 0) {
+        int a = carry;
+        for (int r = 0; r < nb; ++r) {
+          const int c = c0 + r, m = nm[r];
+          ne[r] = a;
+          if (m <= 64) {
+            const uint32_t x = l < m ? pool[r * 64 + l] : 0xffffffffu;
+            const uint64_t le = __ballot(l < m && static_cast<int>(x & 0xffffu) <= a);
+            const int idx = le ? 63 - __builtin_clzll(le) : m - 1;
+            a = n1 - static_cast<int>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), idx)) >> 16);
+            continue;
+          }
+          uint32_t kb = 0, kt = 0;
+          bool hb = false, ht = false;
+          for (int k = l; k < m; k += 64) {
+            const uint32_t x = row(c)[k];
+            const uint32_t lo = x & 0xffffu, key = (lo << 16) | (x >> 16);
+            if (static_cast<int>(lo) <= a && (!hb || key > kb)) kb = key, hb = true;
+            if (!ht || key > kt) kt = key, ht = true;
+          }
+          const uint64_t anyb = __ballot(hb);
+          // keys of valid rows are distinct; invalid lanes hold 0 and lose every max below
+          uint32_t mb = hb ? kb : 0u, mt = ht ? kt : 0u;
 #pragma unroll
-        for (int o = 32; o; o >>= 1) {
-          mb = max(mb, static_cast<uint32_t>(__shfl_xor(static_cast<int>(mb), o)));
-          mt = max(mt, static_cast<uint32_t>(__shfl_xor(static_cast<int>(mt), o)));
+          for (int o = 32; o; o >>= 1) {
+            mb = max(mb, static_cast<uint32_t>(__shfl_xor(static_cast<int>(mb), o)));
+            mt = max(mt, static_cast<uint32_t>(__shfl_xor(static_cast<int>(mt), o)));
+          }
+          a = n1 - static_cast<int>((anyb ? mb : mt) & 0xffffu);
         }
-        a = n1 - static_cast<int>((anyb ? mb : mt) & 0xffffu);
+        if (l == 0) carry = a;
       }
+      __syncthreads();
+      for (int k = tid; k < nb; k += 1024) ent[c0 + k] = ne[k];
+      __syncthreads();
+      continue;
+    }
+    // up-sweep: node j of a level composes nodes 2j (first) and 2j + 1 of the level below
+    int nodes = nb, base = 0;
+    while (nodes > 1) {
+      const int nn = (nodes + 1) >> 1, nbase = base + nodes;
+      for (int j = wv; j < nn; j += 16) {
+        const int f = base + 2 * j, g = f + 1, mf = nm[f];
+        if (l < mf) {
+          const uint32_t x = pool[f * 64 + l];
+          pool[(nbase + j) * 64 + l] =
+              g < nbase ? (x & 0xffffu) | (static_cast<uint32_t>(step_eval(pool + g * 64, nm[g], static_cast<int>(x >> 16))) << 16)
+                        : x;
+        }
+        if (l == 0) nm[nbase + j] = mf;
+      }
+      __syncthreads();
+      base = nbase;
+      nodes = nn;
+    }
+    // down-sweep from the root (at base) with the carried entry
+    if (tid == 0) {
+      ne[base] = carry;
+      carry = step_eval(pool + base * 64, nm[base], carry);  // the next block's entry
     }
     __syncthreads();
-    for (int k = tid; k < nb; k += 1024) ent[c0 + k] = es[k];
+    while (base > 0) {
+      // the level below the current one: find its base and size by walking up from 0
+      int cb = 0, cn = nb;
+      while (cb + cn < base) {
+        cb += cn;
+        cn = (cn + 1) >> 1;
+      }
+      const int pn = (cn + 1) >> 1;
+      for (int j = tid; j < pn; j += 1024) {
+        const int e = ne[base + j], f = cb + 2 * j;
+        ne[f] = e;
+        if (2 * j + 1 < cn) ne[f + 1] = step_eval(pool + f * 64, nm[f], e);
+      }
+      __syncthreads();
+      base = cb;
+    }
+    for (int k = tid; k < nb; k += 1024) ent[c0 + k] = ne[k];
+    __syncthreads();
   }
 }
 
