@@ -81,6 +81,27 @@ constexpr int kRFast = 8;                    // slots per thread of the branch-f
 #ifndef RSAMD_MULTI2
 #define RSAMD_MULTI2 1    // the same per slot in the multi-slot dense path (A/B builds: 0)
 #endif
+// numpy draw rule inside a two-bucket batch (s in [M/4 + 1, M], M = mask of the batch's first
+// state): mask(s) = s | (M >> 1) -- M where s has the top bit of M, M >> 1 below it -- so a step
+// is one v_bitop3 (w & (s | M/2)), a compare and a subtract-with-borrow instead of compare /
+// select / and / compare / subtract.  Entry kernel at C2 (rocprofv3, two interleaved passes,
+// profiles/r04_np_ab3): 550 -> 489 us per launch (A/B builds: 0)
+#ifndef RSAMD_ORMASK
+#define RSAMD_ORMASK 1
+#endif
+// the batch's 64 words broadcast from a per-wave LDS copy (ds_read_b128, four draws per read)
+// instead of one v_readlane per draw: three vector instructions per draw.  489 -> 437 us
+// (A/B builds: 0)
+#ifndef RSAMD_WLDS
+#define RSAMD_WLDS 1
+#endif
+// (Measured and not kept: the same broadcast in the one-slot path's general batches, 433 ->
+// 441 us, and with the wrap bookkeeping skipped where no state is <= 64, 450 us.)
+// the dense phase's compaction specialised for one slot per thread (a ballot rank and the wave
+// counts instead of the block scan; three barriers instead of five): 437 -> 432 us (A/B builds: 0)
+#ifndef RSAMD_CMP1
+#define RSAMD_CMP1 1
+#endif
 // Trajectories left when the dense parse hands a chunk to the tracking kernel, also the tracking
 // kernel's list capacity (a template argument, <= 8 per wave of its 16).  The
 // one-slot dense path costs ~N per draw and chunk, so large N hands over earlier: measured
@@ -391,6 +412,10 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
                                                              const uint32_t *__restrict__ draws) {
   extern __shared__ uint16_t dyn[];
   __shared__ uint32_t wbuf[kK];
+#if RSAMD_WLDS
+  __shared__ __attribute__((aligned(16))) uint32_t wl[kEntryThreads];  // per-wave word copies
+  const uint4 *wq = reinterpret_cast<const uint4 *>(wl + (threadIdx.x & ~63u));
+#endif
   __shared__ int sh_red[kEntryThreads / 64];
   __shared__ int sh_evn;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -487,12 +512,35 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
             }
             const bool fast = sv >= lw2 + 64u && lw2 >= 1u && lw2 != 0x7fffffffu;
             if (__ballot(!fast) == 0ull) {
+              if (!PY && RSAMD_ORMASK) {
+                const uint32_t M2 = M >> 1;
+#if RSAMD_WLDS
+                wl[tid] = wa;
+                __builtin_amdgcn_wave_barrier();
 #pragma unroll
-              for (int k = 0; k < 64; ++k) {
-                const uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wa), k));
-                const uint32_t uh = PY ? (w >> sh) : (w & M), ul = PY ? (w >> (sh + 1u)) : (w & (M >> 1));
-                const uint32_t u = sv >= lw ? uh : ul;
-                sv -= u <= sv ? 1u : 0u;
+                for (int j = 0; j < 16; ++j) {
+                  const uint4 q4 = wq[j];
+                  sv -= (q4.x & (sv | M2)) <= sv ? 1u : 0u;
+                  sv -= (q4.y & (sv | M2)) <= sv ? 1u : 0u;
+                  sv -= (q4.z & (sv | M2)) <= sv ? 1u : 0u;
+                  sv -= (q4.w & (sv | M2)) <= sv ? 1u : 0u;
+                }
+                __builtin_amdgcn_wave_barrier();
+#else
+#pragma unroll
+                for (int k = 0; k < 64; ++k) {
+                  const uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wa), k));
+                  sv -= (w & (sv | M2)) <= sv ? 1u : 0u;
+                }
+#endif
+              } else {
+#pragma unroll
+                for (int k = 0; k < 64; ++k) {
+                  const uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wa), k));
+                  const uint32_t uh = PY ? (w >> sh) : (w & M), ul = PY ? (w >> (sh + 1u)) : (w & (M >> 1));
+                  const uint32_t u = sv >= lw ? uh : ul;
+                  sv -= u <= sv ? 1u : 0u;
+                }
               }
             } else
 #endif
@@ -552,12 +600,35 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
             }
             const bool fast = sv >= lw2 + 64u && lw2 >= 1u && lw2 != 0x7fffffffu;
             if (__ballot(!fast) == 0ull) {
+              if (!PY && RSAMD_ORMASK) {
+                const uint32_t M2 = M >> 1;
+#if RSAMD_WLDS
+                wl[tid] = wa;
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll 4
+                for (int j = 0; j < 16; ++j) {
+                  const uint4 q4 = wq[j];
+                  sv -= (q4.x & (sv | M2)) <= sv ? 1u : 0u;
+                  sv -= (q4.y & (sv | M2)) <= sv ? 1u : 0u;
+                  sv -= (q4.z & (sv | M2)) <= sv ? 1u : 0u;
+                  sv -= (q4.w & (sv | M2)) <= sv ? 1u : 0u;
+                }
+                __builtin_amdgcn_wave_barrier();
+#else
 #pragma unroll 16
-              for (int k = 0; k < 64; ++k) {
-                const uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wa), k));
-                const uint32_t uh = PY ? (w >> sh) : (w & M), ul = PY ? (w >> (sh + 1u)) : (w & (M >> 1));
-                const uint32_t u = sv >= lw ? uh : ul;
-                sv -= u <= sv ? 1u : 0u;
+                for (int k = 0; k < 64; ++k) {
+                  const uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wa), k));
+                  sv -= (w & (sv | M2)) <= sv ? 1u : 0u;
+                }
+#endif
+              } else {
+#pragma unroll 16
+                for (int k = 0; k < 64; ++k) {
+                  const uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wa), k));
+                  const uint32_t uh = PY ? (w >> sh) : (w & M), ul = PY ? (w >> (sh + 1u)) : (w & (M >> 1));
+                  const uint32_t u = sv >= lw ? uh : ul;
+                  sv -= u <= sv ? 1u : 0u;
+                }
               }
             } else {
 #pragma unroll 16
@@ -638,6 +709,50 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
       // compaction: equal cyclic neighbours merge, the first of a run keeps its lo (the list
       // stays in cyclic order; where it starts does not matter, so no rotation to a run head:
       // two barriers and a block reduction fewer per compaction); all equal: one survivor
+#if RSAMD_CMP1
+      if (nr == 1) {
+        // one slot per thread (m <= 512): a thread's own slot is its list entry, so the
+        // neighbour test is one LDS read and the offsets a ballot rank plus the wave counts
+        // (three barriers: the batches read no st entry of another thread)
+        const uint32_t sv = s[0];
+        if (tid < m) st[tid] = static_cast<uint16_t>(sv);
+        __syncthreads();
+        const bool keep = tid < m && static_cast<uint16_t>(sv) != st[tid == 0 ? m - 1 : tid - 1];
+        const uint64_t kb = __ballot(keep);
+        if (lane == 0) sh_red[tid >> 6] = __popcll(kb);
+        __syncthreads();
+        int base = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < kEntryThreads / 64; ++w) {
+          const int cw = sh_red[w];
+          base += w < (tid >> 6) ? cw : 0;
+          total += cw;
+        }
+        if (keep) {
+          const int o = base + static_cast<int>(lane_rank(kb));
+          st2[o] = static_cast<uint16_t>(sv);
+          lo2[o] = lo[tid];
+        }
+        if (total == 0) {  // every trajectory in one state: one survivor covering every entry
+          if (tid == 0) {
+            st2[0] = static_cast<uint16_t>(sv);
+            lo2[0] = lo[0];
+          }
+          total = 1;
+        }
+        __syncthreads();
+        uint16_t *x = st;
+        st = st2;
+        st2 = x;
+        x = lo;
+        lo = lo2;
+        lo2 = x;
+        m = total;
+        s[0] = tid < m ? st[tid] : kSentinel;
+        RSD_ETICK(3, 0);
+        continue;
+      }
+#endif
       __syncthreads();
 #pragma unroll
       for (int r = 0; r < kR; ++r) {
