@@ -1556,8 +1556,15 @@ constexpr int kTupRing = 2 * kTupBlk;       // words staged per wave
 // u16 entries per wave after the ring: the swap partners J[s - 1] of the states s = 1..n1, then
 // one dummy slot per lane (the rejected lanes of a two-bucket window store there, so the store
 // needs no exec-mask change on the scalar unit)
-__host__ __device__ constexpr int tup_jpad(int n1) { return (n1 + 1) & ~1; }
-__host__ __device__ constexpr int tup_table(int n1) { return tup_jpad(n1) + 64; }
+// (RSAMD_TUPF: the table holds, instead of J, the first later state F[v] = min{s >= 8, s > v :
+// J[s - 1] = v} for every partner value v -- the trace then follows F from each position, a
+// few dependent reads instead of a ballot per 64 states -- plus J for the states 1..7.)
+#ifndef RSAMD_TUPF
+#define RSAMD_TUPF 1
+#endif
+// (entries 0..n1: the trace reads F at every state it reaches, n1 included)
+__host__ __device__ constexpr int tup_jpad(int n1) { return (n1 + 2) & ~1; }
+__host__ __device__ constexpr int tup_table(int n1) { return tup_jpad(n1) + 64 + (RSAMD_TUPF ? 8 : 0); }
 __host__ __device__ constexpr int64_t tup_lds_bytes(int n1) {
   return (static_cast<int64_t>(sizeof(uint32_t)) * kTupRing +
           static_cast<int64_t>(sizeof(uint16_t)) * tup_table(n1)) * kTupWaves;
@@ -1612,6 +1619,24 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
   // lane (rejected lanes into their dummy slot).  PMC per C2 launch (r04d_pmc / r04d_pmc2):
   // SALU 3.28e8 -> 1.83e8, VALU 3.74e8 -> 4.03e8; 668 -> 591-611 us (profiles/r04d_tuples_ab.txt).
   const uint32_t jdummy = static_cast<uint32_t>(tup_jpad(n1)) + static_cast<uint32_t>(l);
+#if RSAMD_TUPF
+  uint16_t *F = J, *J7 = J + tup_jpad(n1) + 64;  // F[v] (0xffff: none), then J of states 1..7
+  for (int x = l; x < tup_jpad(n1) / 2; x += 64) reinterpret_cast<uint32_t *>(F)[x] = 0xffffffffu;
+  // F[v] = s for the lanes that store: the parse runs the states downwards, so a later window
+  // simply overwrites; inside one window equal partners are resolved to the smallest state
+  // (read back, the losers that should have won store again)
+  auto fstore = [&](bool st, uint32_t v, uint32_t sl) {
+    const uint32_t fi = st ? v : jdummy;
+    F[fi] = static_cast<uint16_t>(sl);
+    __builtin_amdgcn_wave_barrier();
+    uint64_t bad = __ballot(st && F[fi] > sl);
+    for (int r = 0; bad && r < 64; ++r) {  // each round settles at least one lane
+      if ((bad >> l) & 1ull) F[fi] = static_cast<uint16_t>(sl);
+      __builtin_amdgcn_wave_barrier();
+      bad = __ballot(st && F[fi] > sl);
+    }
+  };
+#endif
   auto window2 = [&]() -> bool {
     uint32_t iv;
     asm volatile("v_mov_b32 %0, %1" : "=v"(iv) : "s"(i));
@@ -1645,7 +1670,14 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
     // carry the lanes' predicates as exec-masked scalar copies measured the same, 604 vs 591 us)
     const bool hb = rk <= c;
     const bool ac = rk <= (hb ? vh : vl);
+#if RSAMD_TUPF
+    {
+      const uint32_t sl = iv - static_cast<uint32_t>(rk), v = hb ? uh : ul;  // sl >= 32 here
+      fstore(ac && v < sl, v, sl);
+    }
+#else
     J[ac ? iv - static_cast<uint32_t>(rk) - 1u : jdummy] = static_cast<uint16_t>(hb ? uh : ul);
+#endif
     i -= static_cast<uint32_t>(__popcll(a2));
     o += 64;
     return true;
@@ -1682,8 +1714,17 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
       } while (a != prev);
       acc = a;
     }
+#if RSAMD_TUPF
+    {
+      const bool ap = (acc >> l) & 1ull;
+      const uint32_t sl = i - static_cast<uint32_t>(__popcll(acc & below));
+      if (ap && sl <= 7u) J7[sl - 1u] = static_cast<uint16_t>(u);
+      fstore(ap && sl >= 8u && u < sl, u, sl);
+    }
+#else
     if ((acc >> l) & 1ull)
       J[i - static_cast<uint32_t>(__popcll(acc & below)) - 1u] = static_cast<uint16_t>(u);
+#endif
     i -= static_cast<uint32_t>(__popcll(acc));
     o += W;
   };
@@ -1730,10 +1771,34 @@ parsed:
   for (int k = 0; k < 8; ++k) p[k] = static_cast<uint32_t>(k);
   const int s1 = n1 < 7 ? n1 : 7;
   for (int s = 1; s <= s1; ++s) {  // states below 8: the full transposition rule
+#if RSAMD_TUPF
+    const uint32_t j = J7[s - 1], us = static_cast<uint32_t>(s);
+#else
     const uint32_t j = J[s - 1], us = static_cast<uint32_t>(s);
+#endif
 #pragma unroll
     for (int k = 0; k < 8; ++k) p[k] = p[k] == us ? j : (p[k] == j ? us : p[k]);
   }
+#if RSAMD_TUPF
+  // position k moves to F[p] (the first later state whose partner it is), then on from there;
+  // lane k follows its chain (~ln(n1 / 8) steps)
+  if (l < kk) {
+    uint32_t v = p[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) v = l == k ? p[k] : v;
+    for (;;) {  // F[v] > v, so at most n1 steps; anything else is a corrupt table: loud
+      const uint32_t nx = F[v];
+      if (nx == 0xffffu) break;
+      if (nx <= v || nx > static_cast<uint32_t>(n1)) {
+        atomicOr(err, 4);
+        break;
+      }
+      v = nx;
+    }
+    out[(h - lo) * kk + l] = static_cast<int32_t>(v);
+  }
+  return;
+#endif
   for (int s0 = 8; s0 <= n1; s0 += 64) {
     const int s = s0 + l;
     const uint32_t jv = s <= n1 ? static_cast<uint32_t>(J[s - 1]) : 0xffffffffu;
