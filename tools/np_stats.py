@@ -22,13 +22,14 @@ if len(sys.argv) > 2 and sys.argv[1] == "--read":
         print(f"  one-trajectory wave-intervals {i1.sum()/C:.0f} per chunk, {c1.sum()/max(i1.sum(),1):.3g} cycles each")
         print(f"  multi-trajectory wave-intervals {iN.sum()/C:.0f} per chunk, {cN.sum()/max(iN.sum(),1):.3g} cycles each")
         print(f"  busiest wave per chunk: one {c1.max(1).mean():.3g} multi {cN.max(1).mean():.3g} cycles; intervals {w[:,0,5].mean():.0f}")
-        e = st[:, 100:110].astype(float)
+        e = st[:, 100:111].astype(float)
         if e[:, 7].any():
             cyc = e[:, 0:4].mean(0)
             dr = e[:, 4:7].mean(0)
             print(f"  entry: total {e[:,7].mean():.3g} cycles; several-slot {cyc[0]:.3g} ({dr[0]:.0f} draws), "
                   f"multi-slot fast {cyc[1]:.3g} ({dr[1]:.0f}), one-slot {cyc[2]:.3g} ({dr[2]:.0f}), "
-                  f"compaction {cyc[3]:.3g}; exits at t {e[:,8].mean():.0f} with m {e[:,9].mean():.1f}")
+                  f"compaction {cyc[3]:.3g}; exits at t {e[:,8].mean():.0f} with m {e[:,9].mean():.1f}; "
+                  f"wave 0 general one-slot batches {e[:,10].mean():.0f} of {dr[2] / 64:.0f}")
         r0, r1 = st[:, 121], st[:, 122]
         if r0.any():
             rel0, rel1 = (r0 - r0.min()) / 100.0, (r1 - r0.min()) / 100.0  # us

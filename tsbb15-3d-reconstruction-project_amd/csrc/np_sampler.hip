@@ -70,10 +70,24 @@ constexpr int kMaxN1 = kEntryThreads * kR;
 constexpr int kK = 64;                       // draws between compactions (<= N - 1 when dense)
 // dense-phase batches of 64 draws between compactions (the one-slot and the multi-slot paths):
 // a compaction costs ~8k cycles (block scans, barriers), merges are slow at large N.  Measured
-// (C2 / N = 10 000 ms): one-slot 4 / 16 / 32 batches 7.90 / 7.75 / - and 41.4 / 38.6 / 36.6;
-// multi-slot 1 / 4 / 8 batches 7.78 / 8.17 / 8.22 and 38.0 / 37.1 / 36.9.
-__host__ __device__ constexpr int fast_batches(int n1) { return n1 >= 4096 ? 32 : 16; }
-__host__ __device__ constexpr int fast_batches_multi(int n1) { return n1 >= 4096 ? 4 : 1; }
+// (round 2, C2 / N = 10 000 ms): one-slot 4 / 16 / 32 batches 7.90 / 7.75 / - and 41.4 / 38.6 /
+// 36.6; multi-slot 1 / 4 / 8 batches 7.78 / 8.17 / 8.22 and 38.0 / 37.1 / 36.9 (re-measured in
+// round 4 below).
+#ifndef RSAMD_NFAST
+#define RSAMD_NFAST 0   // A/B builds: batches between the one-slot path's compactions at C2 sizes
+#endif
+#ifndef RSAMD_NFASTM
+#define RSAMD_NFASTM 0  // A/B builds: the same for the multi-slot path
+#endif
+__host__ __device__ constexpr int fast_batches(int n1) {
+  return n1 >= 4096 ? 32 : (RSAMD_NFAST ? RSAMD_NFAST : 16);
+}
+// (with the one-instruction draw masks the multi-slot batches got cheap against a compaction:
+// C2 entry kernel per launch, compaction every 1 / 2 / 4 / 8 / 16 batches: 430 / 412 / 406 /
+// 409 / 410 us; one-slot every 8 / 16 / 32: 442 / 430 / 433, profiles/r04_np_ab3)
+__host__ __device__ constexpr int fast_batches_multi(int n1) {
+  return n1 >= 4096 ? 4 : (RSAMD_NFASTM ? RSAMD_NFASTM : 4);
+}
 constexpr int kRFast = 8;                    // slots per thread of the branch-free multi-slot path
 #ifndef RSAMD_ONESLOT2
 #define RSAMD_ONESLOT2 1  // two-bucket batches in the one-slot dense path (A/B builds: 0)
@@ -494,6 +508,9 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
         for (int fb = 0; fb < nfast && TL - t >= 64; ++fb) {
           // (waves holding only empty slots skip the batch: sentinels stay sentinels)
           uint32_t sv = s[0], wk = 0xffffffffu;
+#ifdef RSAMD_DIAG
+          bool gen = false;  // this wave took the general (wrap-capable) batch
+#endif
           if ((tid & ~63) < m) {
 #if RSAMD_ONESLOT2
             // Two-bucket batch: when every lane's state stays within its bucket and the one
@@ -545,6 +562,9 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
             } else
 #endif
             {
+#ifdef RSAMD_DIAG
+              gen = true;
+#endif
 #pragma unroll
               for (int k = 0; k < 64; ++k) {
                 const uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wa), k));
@@ -571,6 +591,9 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
           t += 64;
           wa = wb;
           wb = t + 64 + lane < TL ? wp[t + 64 + lane] : 0u;
+#ifdef RSAMD_DIAG
+          if (gen) eg[7] += 1;  // general batches of this wave (thread 0's wave reports)
+#endif
           RSD_ETICK(2, 64);
         }
       } else if (kk == 64 && nr <= kRFast) {
@@ -803,6 +826,7 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
       o[7] = __builtin_amdgcn_s_memtime() - e0;
       o[8] = t;
       o[9] = m;
+      o[10] = eg[7];
     }
 #endif
     if (m > hand && t < T) {  // paused at the first stream pass's end: resumed after the second
