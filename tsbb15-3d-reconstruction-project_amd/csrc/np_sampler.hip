@@ -981,6 +981,31 @@ __device__ __forceinline__ uint64_t window_step(uint32_t w, uint64_t wm, uint32_
 // kernel), so the scalar unit bounds the multi-trajectory phase; this form spends ~8 scalar and
 // ~25 vector instructions.  Returns false (and leaves i alone) where the fast path does not
 // hold; the caller then runs window_step.  Same fixed point, so the same accept mask.
+// The two-bucket fixed point on REJECT masks (numpy rule): lane l's state is s_l = i - (accepts
+// below l) = (i - l) + (rejects below l) -- one v_mbcnt pair with i - l as the addend -- and its
+// draw is w_l & mask(s_l) = w_l & (s_l | M/2) inside the two buckets (one v_bitop3), so a round
+// is mbcnt / mbcnt / bitop3 / compare with one hazard wait, against mbcnt / mbcnt / compare /
+// select / compare with two.  From "every lane at state i" (rejects of the rank-0 guess); the
+// same fixed point as the accept-mask form.  base = i - l (per lane), iu = i (uniform or its
+// vector copy).  Returns the window's reject mask.
+#ifndef RSAMD_REJFP
+#define RSAMD_REJFP 1
+#endif
+__device__ __forceinline__ uint64_t rej_fixed_point(uint32_t w, uint32_t iu, uint32_t base,
+                                                    uint32_t M2) {
+  uint64_t r0 = __ballot((w & (iu | M2)) > iu), r1, r2;
+  do {  // convergence checked every second round (a fixed point is stable)
+    uint32_t sl = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(r0 >> 32),
+                                            __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(r0), base));
+    r1 = __ballot((w & (sl | M2)) > sl);
+    sl = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(r1 >> 32),
+                                   __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(r1), base));
+    r2 = __ballot((w & (sl | M2)) > sl);
+    r0 = r2;
+  } while (r2 != r1);
+  return r2;
+}
+
 template <bool PY>
 __device__ __forceinline__ bool fast_window(uint32_t w, uint32_t &i) {
   uint32_t iv;
@@ -997,6 +1022,12 @@ __device__ __forceinline__ bool fast_window(uint32_t w, uint32_t &i) {
   }
   const bool fast = iv >= lowest2 + 63u && lowest2 >= 1u && lowest2 != 0x7fffffffu;
   if (__builtin_amdgcn_ballot_w64(fast) == 0ull) return false;  // uniform: all lanes agree
+  if constexpr (!PY && RSAMD_REJFP) {
+    const uint32_t rej = static_cast<uint32_t>(__popcll(
+        rej_fixed_point(w, iv, iv - static_cast<uint32_t>(threadIdx.x & 63), M >> 1)));
+    i -= 64u - rej;
+    return true;
+  }
   const int c = static_cast<int>(iv) - static_cast<int>(lowest);
   const int vh = static_cast<int>(iv) - static_cast<int>(PY ? (w >> sh) : (w & M));
   const int vl = static_cast<int>(iv) - static_cast<int>(PY ? (w >> (sh + 1u)) : (w & (M >> 1)));
@@ -1081,6 +1112,12 @@ __device__ __forceinline__ uint32_t track_one(const EntryArgs &a, const uint32_t
       if (dk + 64 <= cp) {
         if (i < lowest || i > (PY ? (lowest << 1) : (lowest << 1) - 1u)) set_bucket();  // left it
         if (i >= fast_min) {
+          if constexpr (!PY && RSAMD_REJFP) {
+            const uint32_t rej = static_cast<uint32_t>(__popcll(
+                rej_fixed_point(w, i, i - static_cast<uint32_t>(lane), M >> 1)));
+            i -= 64u - rej;
+            continue;
+          }
           const int c = static_cast<int>(i) - static_cast<int>(lowest);
           const int vh = static_cast<int>(i) - static_cast<int>(PY ? (w >> sh) : (w & M));
           const int vl = static_cast<int>(i) - static_cast<int>(PY ? (w >> (sh + 1u)) : (w & (M >> 1)));
@@ -1677,6 +1714,19 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
     const bool ok = iv >= lowest2 + 63u && lowest2 >= 1u && lowest2 != 0x7fffffffu;
     if (__builtin_amdgcn_ballot_w64(ok) == 0ull) return false;  // uniform
     const uint32_t wd = ring[(o + l) & (kTupRing - 1)];
+#if RSAMD_TUPF
+    if constexpr (!PY && RSAMD_REJFP) {
+      const uint32_t M2 = M >> 1, base = iv - static_cast<uint32_t>(l);
+      const uint64_t rj = rej_fixed_point(wd, iv, base, M2);
+      const uint32_t sl = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(rj >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(rj), base));
+      const uint32_t v = wd & (sl | M2);  // the lane's draw = its swap partner when accepted
+      fstore(v < sl, v, sl);              // (rejected lanes: v > sl)
+      i -= 64u - static_cast<uint32_t>(__popcll(rj));
+      o += 64;
+      return true;
+    }
+#endif
     const uint32_t uh = PY ? (wd >> sh) : (wd & M), ul = PY ? (wd >> (sh + 1u)) : (wd & (M >> 1));
     const int c = static_cast<int>(iv) - static_cast<int>(lowest);
     const int vh = static_cast<int>(iv) - static_cast<int>(uh);
