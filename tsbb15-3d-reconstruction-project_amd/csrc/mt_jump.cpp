@@ -174,6 +174,24 @@ void mt_jump_poly(uint64_t J, std::vector<uint64_t> &out) {
 // p = p^2 mod phi (x^J -> x^(2J))
 void mt_poly_square(std::vector<uint64_t> &p) { square_mod(p, charpoly()); }
 
+// r = a * b mod phi (x^A, x^B -> x^(A+B)): carry-less product by shifted XORs over a's set
+// bits, then the reduction of square_mod
+void mt_poly_mulmod(const std::vector<uint64_t> &a, const std::vector<uint64_t> &b,
+                    std::vector<uint64_t> &r) {
+  const Poly &phi = charpoly();
+  Poly pr(2 * kWords + 2, 0), bb(b.begin(), b.end());
+  bb.resize(kWords, 0);
+  for (int64_t i = 0; i < kWords; ++i) {
+    const uint64_t v = i < static_cast<int64_t>(a.size()) ? a[i] : 0;
+    if (!v) continue;
+    for (int t = 0; t < 64; ++t)
+      if ((v >> t) & 1u) xor_shifted(pr, bb, 64 * i + t);
+  }
+  for (int64_t i = 2 * (kDeg - 1); i >= kDeg; --i)
+    if (getbit(pr, i)) xor_shifted(pr, phi, i - kDeg);
+  r.assign(pr.begin(), pr.begin() + kWords);
+}
+
 // Window (y_0..y_623) advanced by the polynomial p: out[w] = XOR_{i: p_i} y_{i+w}.
 void mt_apply_poly(const uint32_t *win, const std::vector<uint64_t> &p, uint32_t *out) {
   std::vector<uint32_t> y(static_cast<size_t>(kDeg + kN + 1));

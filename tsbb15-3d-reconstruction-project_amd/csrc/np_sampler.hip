@@ -41,6 +41,8 @@ namespace rs {
 int hip_fail(hipError_t e, const char *what);
 void mt_jump_poly(uint64_t J, std::vector<uint64_t> &out);
 void mt_poly_square(std::vector<uint64_t> &p);
+void mt_poly_mulmod(const std::vector<uint64_t> &a, const std::vector<uint64_t> &b,
+                    std::vector<uint64_t> &r);
 }  // namespace rs
 
 #define HIP_TRY(expr)                                     \
@@ -168,14 +170,25 @@ __device__ __forceinline__ uint32_t draw_of(uint32_t w, uint32_t i) {
 constexpr int kJumpGroups = 3;
 constexpr int kJumpGroupThreads = 320;   // >= 313 pair owners (l = 0 .. 312)
 constexpr int kJumpThreads = kJumpGroups * kJumpGroupThreads;
+// One launch per tree level: multiplier m = 1 .. nm of the level's base distance B (`half`),
+// window[g + m B] = x^(m B J) applied to window[g] (radix nm + 1; the g0 chain uses nm = 1).
+struct JumpSet {
+  int nm;
+  int off[7], nb[7], ne[7];  // per multiplier: offset into the bit lists, set bits, even ones
+};
 __global__ __launch_bounds__(kJumpThreads) void k_mt_jump(uint32_t *__restrict__ win, int half,
-                                                         int G, const int32_t *__restrict__ bits,
-                                                         int nbits, int ne, int S) {
+                                                         int G,
+                                                         const int32_t *__restrict__ bits_base,
+                                                         JumpSet js, int S) {
   // bits: the level's even set bits (ne of them, ascending), then its odd ones
   extern __shared__ uint32_t y[];  // up to kPrefixAlloc words (8-byte aligned)
   __shared__ uint32_t pe[kJumpGroups][kN], po[kJumpGroups][kN];
-  const int g = blockIdx.x / S, q = blockIdx.x % S, dst = g + half;
-  if (dst >= G) return;
+  const int per_m = half * S, mi = static_cast<int>(blockIdx.x) / per_m;
+  const int rem = static_cast<int>(blockIdx.x) - mi * per_m;
+  const int g = rem / S, q = rem % S, dst = g + (mi + 1) * half;
+  if (mi >= js.nm || dst >= G) return;
+  const int32_t *__restrict__ bits = bits_base + js.off[mi];
+  const int nbits = js.nb[mi], ne = js.ne[mi];
   const int no = nbits - ne;
   const int e0 = static_cast<int>(static_cast<int64_t>(ne) * q / S);
   const int e1 = static_cast<int>(static_cast<int64_t>(ne) * (q + 1) / S);
@@ -991,6 +1004,9 @@ __device__ __forceinline__ uint64_t window_step(uint32_t w, uint64_t wm, uint32_
 #ifndef RSAMD_REJFP
 #define RSAMD_REJFP 1
 #endif
+#ifndef RSAMD_FWPRE
+#define RSAMD_FWPRE 1  // fast_window's two-bucket test by leading-zero counts (A/B builds: 0)
+#endif
 __device__ __forceinline__ uint64_t rej_fixed_point(uint32_t w, uint32_t iu, uint32_t base,
                                                     uint32_t M2) {
   uint64_t r0 = __ballot((w & (iu | M2)) > iu), r1, r2;
@@ -1020,6 +1036,19 @@ __device__ __forceinline__ bool fast_window(uint32_t w, uint32_t &i) {
     lowest = (M >> 1) + 1u;
     lowest2 = M > 1u ? (M >> 2) + 1u : 0x7fffffffu;
   }
+#if RSAMD_FWPRE
+  if constexpr (!PY && RSAMD_REJFP) {
+    // two buckets hold the window iff i >= 64 and i - 63 lies in i's bucket or the next lower
+    // one: clz(i - 63) <= clz(i) + 1 (the same test as i >= M/4 + 1 + 63, fewer instructions)
+    const uint32_t cz = static_cast<uint32_t>(__builtin_clz(iv));
+    const bool two = iv >= 64u && static_cast<uint32_t>(__builtin_clz((iv - 63u) | 1u)) <= cz + 1u;
+    if (__builtin_amdgcn_ballot_w64(two) == 0ull) return false;  // uniform: all lanes agree
+    const uint32_t rej = static_cast<uint32_t>(__popcll(
+        rej_fixed_point(w, iv, iv - static_cast<uint32_t>(threadIdx.x & 63), 0x7fffffffu >> cz)));
+    i -= 64u - rej;
+    return true;
+  }
+#endif
   const bool fast = iv >= lowest2 + 63u && lowest2 >= 1u && lowest2 != 0x7fffffffu;
   if (__builtin_amdgcn_ballot_w64(fast) == 0ull) return false;  // uniform: all lanes agree
   if constexpr (!PY && RSAMD_REJFP) {
@@ -1167,7 +1196,6 @@ __device__ __forceinline__ void track_interval(const EntryArgs &a, const uint32_
   uint32_t wn = sw[lane];  // draws beyond cp are never accepted (lanes >= Wn)
   while (d < cp) {
     const int Wn = min(64, cp - d);
-    const uint64_t wm = Wn == 64 ? ~0ull : ((1ull << Wn) - 1ull);
     const uint32_t w = wn;
     if (d + 64 < cp) wn = sw[(d + 64 - t + lane) & (kCheck - 1)];
 #pragma unroll
@@ -1176,6 +1204,12 @@ __device__ __forceinline__ void track_interval(const EntryArgs &a, const uint32_
 #if RSAMD_MULTI_VALU
         if (Wn == 64 && fast_window<PY>(w, i[r])) continue;
 #endif
+        // (the window mask only where the general step runs -- the opaque copy keeps the
+        // compiler from hoisting it into every window: scalar instructions on the CU's shared
+        // scalar unit)
+        int wn_ = Wn;
+        asm volatile("" : "+s"(wn_));
+        const uint64_t wm = wn_ == 64 ? ~0ull : ((1ull << wn_) - 1ull);
         uint64_t wr;
         uint32_t sl;
         (void)window_step<PY, SMALL>(w, wm, i[r], n1, wr, sl);
@@ -1956,6 +1990,55 @@ const JumpPolys &jump_polys(int JB) {
   return *jp;
 }
 
+// Radix-R tree levels (RSAMD_JRADIX, R <= 8): level k's multipliers m = 1 .. R-1 are
+// x^(m R^k J) mod phi, products of the level base x^(R^k J) (~5 ms of host arithmetic each);
+// built up to the levels a call needs and cached per JB
+#ifndef RSAMD_JRADIX
+#define RSAMD_JRADIX 8
+#endif
+constexpr int kJumpRadix = RSAMD_JRADIX;
+static_assert(kJumpRadix >= 2 && kJumpRadix <= 8, "jump radix");
+struct JumpPolysR {
+  std::vector<std::vector<int32_t>> bits;  // index k (R-1) + m - 1, even bits first
+  std::vector<int> ne;
+  std::vector<uint64_t> next;              // x^(R^levels J): the next level's base
+  int levels = 0;
+};
+const JumpPolysR &jump_polys_r(int JB, int levels) {
+  static std::mutex mu;
+  static std::vector<std::pair<int, JumpPolysR *>> cache;
+  std::lock_guard<std::mutex> g(mu);
+  JumpPolysR *jp = nullptr;
+  for (auto &e : cache)
+    if (e.first == JB) jp = e.second;
+  if (!jp) {
+    jp = new JumpPolysR();
+    rs::mt_jump_poly(static_cast<uint64_t>(kN) * static_cast<uint64_t>(JB), jp->next);
+    cache.emplace_back(JB, jp);
+  }
+  while (jp->levels < levels) {
+    const std::vector<uint64_t> base = jp->next;
+    std::vector<uint64_t> p = base, t;
+    for (int m = 1; m < kJumpRadix; ++m) {
+      if (m > 1) {
+        rs::mt_poly_mulmod(p, base, t);
+        p.swap(t);
+      }
+      std::vector<int32_t> b;
+      for (int par = 0; par < 2; ++par) {
+        for (int i = par; i < kDeg; i += 2)
+          if ((p[static_cast<size_t>(i) >> 6] >> (i & 63)) & 1u) b.push_back(i);
+        if (par == 0) jp->ne.push_back(static_cast<int>(b.size()));
+      }
+      jp->bits.push_back(std::move(b));
+    }
+    rs::mt_poly_mulmod(p, base, t);  // x^(R^(k+1) J)
+    jp->next.swap(t);
+    ++jp->levels;
+  }
+  return *jp;
+}
+
 uint32_t untemper(uint32_t z) {
   uint32_t y = z ^ (z >> 18);
   y ^= (y << 15) & 0xefc60000u;
@@ -2088,6 +2171,9 @@ struct rs_np_shard {
   // device
   int32_t *d_bits = nullptr;
   std::vector<int> bit_off, bit_n, bit_ne;
+  int32_t *d_rbits = nullptr;  // radix-tree level polynomials (jump_polys_r)
+  std::vector<int> rbit_off, rbit_n, rbit_ne;
+  int rbits_JB = 0, rlevels = 0;
   uint32_t *d_win = nullptr, *d_chain = nullptr, *d_stream = nullptr, *d_fin = nullptr,
            *d_fin_all = nullptr;
   int *d_fin_m = nullptr, *d_fin_m_all = nullptr, *d_ev_n = nullptr, *d_ent = nullptr,
@@ -2106,7 +2192,7 @@ struct rs_np_shard {
 namespace {
 
 void shard_free(rs_np_shard *w) {
-  void *ptrs[] = {w->d_bits, w->d_win,   w->d_chain, w->d_stream, w->d_fin,     w->d_fin_all,
+  void *ptrs[] = {w->d_bits, w->d_rbits, w->d_win,   w->d_chain, w->d_stream, w->d_fin,     w->d_fin_all,
                   w->d_fin_m, w->d_fin_m_all, w->d_ev_n, w->d_ent, w->d_vcnt, w->d_off,
                   w->d_err,  w->d_tpos,  w->d_row_off, w->d_starts, w->d_got, w->d_ev,
                   w->d_res};
@@ -2257,8 +2343,13 @@ int shard_windows(rs_np_shard &w, const uint32_t *key, hipStream_t s) {
     int j = 0;
     for (int lv = 0; lv < kLevels; ++lv) {
       if (!((w.g0 >> lv) & 1)) continue;
+      JumpSet js{};
+      js.nm = 1;
+      js.off[0] = w.bit_off[lv];
+      js.nb[0] = w.bit_n[lv];
+      js.ne[0] = w.bit_ne[lv];
       k_mt_jump<<<64, kJumpThreads, sizeof(uint32_t) * kPrefixAlloc, s>>>(
-          w.d_chain + static_cast<size_t>(j) * kN, 1, 2, w.d_bits + w.bit_off[lv], w.bit_n[lv], w.bit_ne[lv], 64);
+          w.d_chain + static_cast<size_t>(j) * kN, 1, 2, w.d_bits, js, 64);
       HIP_TRY(hipGetLastError());
       ++j;
     }
@@ -2269,11 +2360,60 @@ int shard_windows(rs_np_shard &w, const uint32_t *key, hipStream_t s) {
     HIP_TRY(hipMemsetAsync(w.d_win + kN, 0, sizeof(uint32_t) * kN * static_cast<size_t>(w.G - 1), s));
   // S parts per jump so that a level is one round of workgroups (one per CU: the prefix takes
   // 82 KB of LDS); two rounds cost a second prefix generation (C2 levels 3..8: 30 .. 168 us)
+  if (kJumpRadix > 2) {
+    // radix-R tree: level k sends window g < R^k to g + m R^k (m = 1 .. R-1) in one launch,
+    // ceil(log_R G) levels instead of ceil(log2 G) (the small levels are latency, not work)
+    int need = 0;
+    for (int64_t B = 1; B < w.G; B *= kJumpRadix) ++need;
+    if (w.rbits_JB != w.JB || w.rlevels < need) {
+      const JumpPolysR &jr = jump_polys_r(w.JB, need);
+      std::vector<int32_t> all;
+      w.rbit_off.clear();
+      w.rbit_n.clear();
+      w.rbit_ne.clear();
+      for (size_t k = 0; k < jr.bits.size(); ++k) {
+        w.rbit_off.push_back(static_cast<int>(all.size()));
+        w.rbit_n.push_back(static_cast<int>(jr.bits[k].size()));
+        w.rbit_ne.push_back(jr.ne[k]);
+        all.insert(all.end(), jr.bits[k].begin(), jr.bits[k].end());
+      }
+      int64_t cap = 0;
+      if (w.d_rbits) (void)hipFree(w.d_rbits);
+      w.d_rbits = nullptr;
+      if ((st = sgrow(w.d_rbits, cap, static_cast<int64_t>(all.size())))) return st;
+      HIP_TRY(hipMemcpy(w.d_rbits, all.data(), sizeof(int32_t) * all.size(), hipMemcpyHostToDevice));
+      w.rbits_JB = w.JB;
+      w.rlevels = jr.levels;
+    }
+    int lv = 0;
+    for (int64_t B = 1; B < w.G; B *= kJumpRadix, ++lv) {
+      JumpSet js{};
+      js.nm = kJumpRadix - 1;
+      int64_t jumps = 0;
+      for (int m = 1; m < kJumpRadix; ++m) {
+        const size_t x = static_cast<size_t>(lv) * (kJumpRadix - 1) + (m - 1);
+        js.off[m - 1] = w.rbit_off[x];
+        js.nb[m - 1] = w.rbit_n[x];
+        js.ne[m - 1] = w.rbit_ne[x];
+        jumps += std::max<int64_t>(0, std::min<int64_t>(B, w.G - m * B));
+      }
+      const int S = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(64, w.cus / std::max<int64_t>(1, jumps))));
+      k_mt_jump<<<static_cast<unsigned>(js.nm * B * S), kJumpThreads, sizeof(uint32_t) * kPrefixAlloc, s>>>(
+          w.d_win, static_cast<int>(B), static_cast<int>(w.G), w.d_rbits, js, S);
+      HIP_TRY(hipGetLastError());
+    }
+    return RS_OK;
+  }
   for (int half = 1, lv = 0; half < w.G; half *= 2, ++lv) {
     const int jumps = static_cast<int>(std::min<int64_t>(half, w.G - half));
     const int S = std::max(1, std::min(64, w.cus / jumps));
+    JumpSet js{};
+    js.nm = 1;
+    js.off[0] = w.bit_off[lv];
+    js.nb[0] = w.bit_n[lv];
+    js.ne[0] = w.bit_ne[lv];
     k_mt_jump<<<half * S, kJumpThreads, sizeof(uint32_t) * kPrefixAlloc, s>>>(
-        w.d_win, half, static_cast<int>(w.G), w.d_bits + w.bit_off[lv], w.bit_n[lv], w.bit_ne[lv], S);
+        w.d_win, half, static_cast<int>(w.G), w.d_bits, js, S);
     HIP_TRY(hipGetLastError());
   }
   return RS_OK;
