@@ -111,6 +111,9 @@ constexpr int kRFast = 8;                    // slots per thread of the branch-f
 #ifndef RSAMD_WLDS
 #define RSAMD_WLDS 1
 #endif
+#ifndef RSAMD_GEN2
+#define RSAMD_GEN2 0  // the one-slot general batch with the wrap test off the chain (A/B builds: 1)
+#endif
 // (Measured and not kept: the same broadcast in the one-slot path's general batches, 433 ->
 // 441 us, and with the wrap bookkeeping skipped where no state is <= 64, 450 us.)
 // the dense phase's compaction specialised for one slot per thread (a ballot rank and the wave
@@ -434,6 +437,110 @@ __device__ __forceinline__ void np_stamp_val(int c, int slot, unsigned long long
   if (unsigned long long *ts = np_ts()) ts[static_cast<size_t>(c) * kTs + slot] = v;
 }
 
+// The one-slot path's general (wrap-capable) batch as one instruction stream (RSAMD_GEN3): per
+// draw the next word's v_readlane and the wrap select sit where the compiler placed hazard waits
+// (the wrap test reads the step's INPUT state: state 1 always accepts and wraps), so a draw is
+// nine vector instructions and no s_nop.  Operand rules kept by hand: one scalar source per
+// instruction (N1 in a VGPR), >= 2 instructions between an SGPR / VCC write and its read.
+#ifndef RSAMD_GEN3
+#define RSAMD_GEN3 1
+#endif
+#define RSD_S_(x) #x
+#define RSD_S(x) RSD_S_(x)
+#define RSD_GSTEP_BODY(K, SA)                                      \
+  "v_cmp_eq_u32_e64 %[one], 1, %[sv]\n\t"                           \
+  "v_ffbh_u32_e32 %[t], %[sv]\n\t"                                  \
+  "v_lshrrev_b32_e64 %[t], %[t], -1\n\t"                            \
+  "v_and_b32_e32 %[t], %[" SA "], %[t]\n\t"                         \
+  "v_cmp_le_u32_e32 vcc, %[t], %[sv]\n\t"                           \
+  "v_cndmask_b32_e64 %[wk], %[wk], " RSD_S(K) ", %[one]\n\t"
+#define RSD_GSTEP(K, KN, SA, SB)                                   \
+  RSD_GSTEP_BODY(K, SA)                                            \
+  "v_readlane_b32 %[" SB "], %[wa], " RSD_S(KN) "\n\t"               \
+  "v_subbrev_co_u32_e32 %[s2], vcc, 0, %[sv], vcc\n\t"              \
+  "v_cndmask_b32_e64 %[sv], %[s2], %[n1], %[one]\n\t"
+#define RSD_GSTEP_LAST(K, SA)                                      \
+  RSD_GSTEP_BODY(K, SA)                                            \
+  "s_nop 1\n\t"                                                    \
+  "v_subbrev_co_u32_e32 %[s2], vcc, 0, %[sv], vcc\n\t"              \
+  "v_cndmask_b32_e64 %[sv], %[s2], %[n1], %[one]\n\t"
+__device__ __forceinline__ void general_batch_asm(uint32_t wa, uint32_t n1v, uint32_t &sv,
+                                                  uint32_t &wk) {
+  uint32_t t, s2, w0, w1;
+  uint64_t one;
+  asm volatile(
+    "v_readlane_b32 %[w0], %[wa], 0\n\t"
+    "s_nop 1\n\t"
+    RSD_GSTEP(0, 1, "w0", "w1")
+    RSD_GSTEP(1, 2, "w1", "w0")
+    RSD_GSTEP(2, 3, "w0", "w1")
+    RSD_GSTEP(3, 4, "w1", "w0")
+    RSD_GSTEP(4, 5, "w0", "w1")
+    RSD_GSTEP(5, 6, "w1", "w0")
+    RSD_GSTEP(6, 7, "w0", "w1")
+    RSD_GSTEP(7, 8, "w1", "w0")
+    RSD_GSTEP(8, 9, "w0", "w1")
+    RSD_GSTEP(9, 10, "w1", "w0")
+    RSD_GSTEP(10, 11, "w0", "w1")
+    RSD_GSTEP(11, 12, "w1", "w0")
+    RSD_GSTEP(12, 13, "w0", "w1")
+    RSD_GSTEP(13, 14, "w1", "w0")
+    RSD_GSTEP(14, 15, "w0", "w1")
+    RSD_GSTEP(15, 16, "w1", "w0")
+    RSD_GSTEP(16, 17, "w0", "w1")
+    RSD_GSTEP(17, 18, "w1", "w0")
+    RSD_GSTEP(18, 19, "w0", "w1")
+    RSD_GSTEP(19, 20, "w1", "w0")
+    RSD_GSTEP(20, 21, "w0", "w1")
+    RSD_GSTEP(21, 22, "w1", "w0")
+    RSD_GSTEP(22, 23, "w0", "w1")
+    RSD_GSTEP(23, 24, "w1", "w0")
+    RSD_GSTEP(24, 25, "w0", "w1")
+    RSD_GSTEP(25, 26, "w1", "w0")
+    RSD_GSTEP(26, 27, "w0", "w1")
+    RSD_GSTEP(27, 28, "w1", "w0")
+    RSD_GSTEP(28, 29, "w0", "w1")
+    RSD_GSTEP(29, 30, "w1", "w0")
+    RSD_GSTEP(30, 31, "w0", "w1")
+    RSD_GSTEP(31, 32, "w1", "w0")
+    RSD_GSTEP(32, 33, "w0", "w1")
+    RSD_GSTEP(33, 34, "w1", "w0")
+    RSD_GSTEP(34, 35, "w0", "w1")
+    RSD_GSTEP(35, 36, "w1", "w0")
+    RSD_GSTEP(36, 37, "w0", "w1")
+    RSD_GSTEP(37, 38, "w1", "w0")
+    RSD_GSTEP(38, 39, "w0", "w1")
+    RSD_GSTEP(39, 40, "w1", "w0")
+    RSD_GSTEP(40, 41, "w0", "w1")
+    RSD_GSTEP(41, 42, "w1", "w0")
+    RSD_GSTEP(42, 43, "w0", "w1")
+    RSD_GSTEP(43, 44, "w1", "w0")
+    RSD_GSTEP(44, 45, "w0", "w1")
+    RSD_GSTEP(45, 46, "w1", "w0")
+    RSD_GSTEP(46, 47, "w0", "w1")
+    RSD_GSTEP(47, 48, "w1", "w0")
+    RSD_GSTEP(48, 49, "w0", "w1")
+    RSD_GSTEP(49, 50, "w1", "w0")
+    RSD_GSTEP(50, 51, "w0", "w1")
+    RSD_GSTEP(51, 52, "w1", "w0")
+    RSD_GSTEP(52, 53, "w0", "w1")
+    RSD_GSTEP(53, 54, "w1", "w0")
+    RSD_GSTEP(54, 55, "w0", "w1")
+    RSD_GSTEP(55, 56, "w1", "w0")
+    RSD_GSTEP(56, 57, "w0", "w1")
+    RSD_GSTEP(57, 58, "w1", "w0")
+    RSD_GSTEP(58, 59, "w0", "w1")
+    RSD_GSTEP(59, 60, "w1", "w0")
+    RSD_GSTEP(60, 61, "w0", "w1")
+    RSD_GSTEP(61, 62, "w1", "w0")
+    RSD_GSTEP(62, 63, "w0", "w1")
+    RSD_GSTEP_LAST(63, "w1")
+      : [sv] "+v"(sv), [wk] "+v"(wk), [t] "=&v"(t), [s2] "=&v"(s2), [w0] "=&s"(w0),
+        [w1] "=&s"(w1), [one] "=&s"(one)
+      : [wa] "v"(wa), [n1] "v"(n1v)
+      : "vcc");
+}
+
 template <bool PY>
 __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
                                                              const uint32_t *__restrict__ draws) {
@@ -577,6 +684,28 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
             {
 #ifdef RSAMD_DIAG
               gen = true;
+#endif
+#if RSAMD_GEN3
+              if constexpr (!PY) {
+                uint32_t n1v;
+                asm volatile("v_mov_b32 %0, %1" : "=v"(n1v) : "s"(N1));
+                general_batch_asm(wa, n1v, sv, wk);
+              } else
+#endif
+#if RSAMD_GEN2
+              if constexpr (!PY) {
+                // the wrap test off the chain: state 1 always accepts (mask 1) and wraps, so
+                // the select reads a compare of the step's INPUT state, written instructions
+                // earlier (no dependent hazard wait)
+#pragma unroll
+                for (int k = 0; k < 64; ++k) {
+                  const uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wa), k));
+                  const bool one = sv == 1u;
+                  const uint32_t s2 = sv - (masked(w, sv) <= sv ? 1u : 0u);
+                  sv = one ? N1 : s2;
+                  wk = one ? static_cast<uint32_t>(k) : wk;
+                }
+              } else
 #endif
 #pragma unroll
               for (int k = 0; k < 64; ++k) {
@@ -1038,11 +1167,11 @@ __device__ __forceinline__ bool fast_window(uint32_t w, uint32_t &i) {
   }
 #if RSAMD_FWPRE
   if constexpr (!PY && RSAMD_REJFP) {
-    // two buckets hold the window iff i >= 64 and i - 63 lies in i's bucket or the next lower
-    // one: clz(i - 63) <= clz(i) + 1 (the same test as i >= M/4 + 1 + 63, fewer instructions)
+    // two buckets hold the window iff i - 63 >= M/4 + 1 = 2^30 >> clz(i) (signed: i < 63 fails
+    // too), tested by one compare whose ballot is the branch condition
     const uint32_t cz = static_cast<uint32_t>(__builtin_clz(iv));
-    const bool two = iv >= 64u && static_cast<uint32_t>(__builtin_clz((iv - 63u) | 1u)) <= cz + 1u;
-    if (__builtin_amdgcn_ballot_w64(two) == 0ull) return false;  // uniform: all lanes agree
+    const int lw2 = static_cast<int>(0x40000000u >> cz);
+    if (__ballot(static_cast<int>(iv) - 63 >= lw2) == 0ull) return false;  // uniform
     const uint32_t rej = static_cast<uint32_t>(__popcll(
         rej_fixed_point(w, iv, iv - static_cast<uint32_t>(threadIdx.x & 63), 0x7fffffffu >> cz)));
     i -= 64u - rej;
@@ -1735,6 +1864,23 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
   auto window2 = [&]() -> bool {
     uint32_t iv;
     asm volatile("v_mov_b32 %0, %1" : "=v"(iv) : "s"(i));
+#if RSAMD_TUPF && RSAMD_FWPRE
+    if constexpr (!PY && RSAMD_REJFP) {  // the tracking kernel's fast_window test and rounds
+      const uint32_t cz = static_cast<uint32_t>(__builtin_clz(iv));
+      if (__ballot(static_cast<int>(iv) - 63 >= static_cast<int>(0x40000000u >> cz)) == 0ull)
+        return false;  // uniform
+      const uint32_t wd = ring[(o + l) & (kTupRing - 1)];
+      const uint32_t M2 = 0x7fffffffu >> cz, base = iv - static_cast<uint32_t>(l);
+      const uint64_t rj = rej_fixed_point(wd, iv, base, M2);
+      const uint32_t sl = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(rj >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(rj), base));
+      const uint32_t v = wd & (sl | M2);
+      fstore(v < sl, v, sl);
+      i -= 64u - static_cast<uint32_t>(__popcll(rj));
+      o += 64;
+      return true;
+    }
+#endif
     uint32_t lowest, lowest2, sh = 0, M = 0;
     if constexpr (PY) {
       sh = static_cast<uint32_t>(__builtin_clz(iv + 1u));
