@@ -111,6 +111,11 @@ constexpr int kRFast = 8;                    // slots per thread of the branch-f
 #ifndef RSAMD_WLDS
 #define RSAMD_WLDS 1
 #endif
+#ifndef RSAMD_STREAM_PRIO
+#define RSAMD_STREAM_PRIO 0  // k_mt_stream's waves at issue priority 3 (A/B knob: the second
+                             // pass sped up, the entry beside it slowed 389 -> 450 us per
+                             // launch; C2 parse 4.98 vs 4.97 ms: not kept)
+#endif
 #ifndef RSAMD_GEN2
 #define RSAMD_GEN2 0  // the one-slot general batch with the wrap test off the chain (A/B builds: 1)
 #endif
@@ -290,6 +295,12 @@ __global__ __launch_bounds__(256) void k_mt_stream(const uint32_t *__restrict__ 
                                                    int JB, int G, int ext, int blo, int bhi,
                                                    uint32_t *__restrict__ io) {
   __shared__ uint32_t bb[2][kN];
+#if RSAMD_STREAM_PRIO
+  // the second pass runs beside the entry kernel and, with the entry's steps down to three
+  // instructions a draw, became the longer of the two (854 vs 765 us at C2): its waves are a
+  // barrier-bound chain, so they take the SIMDs' issue first
+  __builtin_amdgcn_s_setprio(3);
+#endif
   const int g = blockIdx.x, l = threadIdx.x;
   const bool own = l < 227, own2 = l < 170;
   const int64_t b0 = static_cast<int64_t>(g) * JB;
