@@ -2458,9 +2458,12 @@ int shard_layout(rs_np_shard &w, int32_t pos, int64_t count) {
   w.xlim = std::numeric_limits<int>::max();
   if (aligned && oq >= 1) {
     // (the dense phase ends within 23 360 draws at C2; RSAMD_NP_XDRAWS overrides: tests of the
-    // pause / resume path)
+    // pause / resume path.  The first pass runs alone, the second beside the entry kernel, which
+    // waits for it before its resume launch: since the entry kernel got faster, a first pass of
+    // 72 (N - 1) + 8 192 draws balances the two -- C2 parse 4.97-5.00 ms with 16 (N - 1) + 8 192,
+    // 4.94 with 120k and 160k draws, profiles/r04_np_ab3)
     const int64_t xd = env_i64("RSAMD_NP_XDRAWS");
-    const int64_t want = xd > 0 ? xd : 16 * static_cast<int64_t>(w.n1) + 8192;
+    const int64_t want = xd > 0 ? xd : 72 * static_cast<int64_t>(w.n1) + 8192;
     const int64_t xb = cdiv(want + oq, kN);
     if (xb < w.JB) {
       w.xb = static_cast<int>(xb);
