@@ -76,6 +76,12 @@ int rs_py_shuffle_tuples(uint32_t *mt_key, int32_t *mt_pos, int64_t n, int32_t k
 int rs_mt_jump(const uint32_t *mt_key, int32_t mt_pos, int64_t steps, uint32_t *key_out,
                int32_t *pos_out);
 
+/* Self-test of the GF(2)[x] product mod phi behind the parity parse's radix-8 jump tree (level
+ * polynomials x^(m 8^k J) as products, np_sampler.hip jump_polys_r): 1 iff
+ * x^j1 * x^j2 mod phi == x^(j1 + j2) mod phi, 0 if not, RS_EINVAL for a negative exponent.
+ * Host only; exported for the CPU test suite. */
+int rs_mt_poly_selftest(int64_t j1, int64_t j2);
+
 /* ------------------------------------------------------------------------------------------
  * Context: one per host thread; owns the device buffers, stream and RCCL communicator
  * ---------------------------------------------------------------------------------------- */

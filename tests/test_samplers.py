@@ -129,6 +129,14 @@ def test_mt_jump_matches_sequential_draws(seed, pre):
         assert np.array_equal(key, np.array(ref[:624], np.uint32)), steps
 
 
+@pytest.mark.parametrize("j1,j2", [(0, 1), (624, 565_248), (3 * 565_248, 4 * 565_248),
+                                   (7 * 64 * 565_248, 64 * 565_248)])
+def test_mt_poly_product_is_the_jump_sum(j1, j2):
+    """The radix-8 jump tree's level polynomials x^(m 8^k J) are products mod phi
+    (mt_poly_mulmod): x^j1 * x^j2 = x^(j1 + j2) mod phi, at C2's chunk length J."""
+    assert _ffi.lib().rs_mt_poly_selftest(j1, j2) == 1
+
+
 def test_np_choice_tuples_multi_equals_single_streams():
     """Threaded replay of many independent numpy streams (config C4's per-pair seeds) = one
     rs_np_choice_tuples call per stream, state included; streams with n < k stay zero."""

@@ -210,6 +210,18 @@ void mt_apply_poly(const uint32_t *win, const std::vector<uint64_t> &p, uint32_t
 
 // numpy / CPython state after `steps` more outputs: (key, pos) of the block holding the next
 // word.  The jumped window starts one word early so that key[0] comes out whole.
+// Self-test of the polynomial product the radix-8 jump tree's level polynomials come from
+// (np_sampler.hip jump_polys_r): 1 iff x^j1 * x^j2 mod phi equals x^(j1 + j2) mod phi.
+extern "C" int rs_mt_poly_selftest(int64_t j1, int64_t j2) {
+  if (j1 < 0 || j2 < 0) return rs::fail(RS_EINVAL, "rs_mt_poly_selftest: negative exponent");
+  std::vector<uint64_t> a, b, c, r;
+  rs::mt_jump_poly(static_cast<uint64_t>(j1), a);
+  rs::mt_jump_poly(static_cast<uint64_t>(j2), b);
+  rs::mt_jump_poly(static_cast<uint64_t>(j1) + static_cast<uint64_t>(j2), c);
+  rs::mt_poly_mulmod(a, b, r);
+  return r == c ? 1 : 0;
+}
+
 extern "C" int rs_mt_jump(const uint32_t *key, int32_t pos, int64_t steps, uint32_t *key_out,
                           int32_t *pos_out) {
   if (!key || !key_out || !pos_out) return rs::fail(RS_EINVAL, "rs_mt_jump: null pointer");

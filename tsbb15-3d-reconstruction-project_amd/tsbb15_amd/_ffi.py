@@ -77,6 +77,7 @@ _SIGS = {
     "rs_py_shuffle_tuples_gpu": (C.c_int, [C.c_void_p, _u32p, _i32p, C.c_int64, C.c_int32,
                                            C.c_int64, _i32p]),
     "rs_mt_jump": (C.c_int, [_u32p, C.c_int32, C.c_int64, _u32p, _i32p]),
+    "rs_mt_poly_selftest": (C.c_int, [C.c_int64, C.c_int64]),
     "rs_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "rs_ctx_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
     "rs_ctx_destroy": (C.c_int, [C.c_void_p]),
