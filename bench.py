@@ -524,9 +524,24 @@ def launch_ranks(n, argv):
     return 0
 
 
-def harness_only(rank, world, dist):
+def exchange_policy(rccl_ok, pinned):
+    """The per-pair record exchange of a multi-rank bench, decided on every rank alike.
+    RCCL when its communicator came up on every rank.  Otherwise: a one-device rehearsal
+    (RSAMD_BENCH_DEVICE pins every rank to one GPU, which RCCL refuses) exchanges over the TCP
+    hub and says so; ranks on distinct GPUs raise instead -- a multi-GPU line must be an RCCL
+    measurement or no line at all."""
+    if rccl_ok:
+        return "rccl all-gather"
+    if pinned:
+        return "tcp-hub all-gather (RCCL init failed; one-device rehearsal)"
+    raise RuntimeError("RCCL communicator init failed on some rank while the ranks hold distinct "
+                       "GPUs: refusing to report a multi-GPU line without RCCL")
+
+
+def harness_only(rank, world, dist, args, cpu):
     """--harness-only: the launcher + TcpHub handshake, barrier, max-reduce and all-gather
-    with no device opened (the CPU test of the multi-rank harness)."""
+    with no device opened (the CPU test of the multi-rank harness).  RSAMD_BENCH_FAKE_RCCL
+    ("fail" / "ok") runs the transport decision of a real run on a simulated RCCL init."""
     import platform
     dist.barrier()
     t = dist.max(float(rank))
@@ -534,12 +549,22 @@ def harness_only(rank, world, dist):
             "host": platform.node(), "launched": os.environ.get("RSAMD_BENCH_LAUNCHED") == "1"}
     recs = [json.loads(b) for b in dist.hub.allgather_bytes(json.dumps(info).encode())] \
         if dist.hub else [info]
+    line = {"harness_only": True, "n_gpus": world, "max_rank": t, "ranks": recs,
+            "harness": "tcp hub (no torch.distributed)" if world > 1 else "one process"}
+    fake = os.environ.get("RSAMD_BENCH_FAKE_RCCL")
+    if fake and world > 1:
+        ok = dist.max(0.0 if fake == "ok" else 1.0) == 0.0
+        try:
+            line["exchange"] = exchange_policy(ok, "RSAMD_BENCH_DEVICE" in os.environ)
+        except RuntimeError as e:
+            print(f"error: {e}", file=sys.stderr, flush=True)
+            dist.close()
+            sys.exit(4)
+    if cpu is not None:
+        line["cpu_baseline"] = cpu
     dist.barrier()
     if rank == 0:
-        print(json.dumps({"harness_only": True, "n_gpus": world, "max_rank": t,
-                          "ranks": recs,
-                          "harness": "tcp hub (no torch.distributed)" if world > 1
-                          else "one process"}), flush=True)
+        print(json.dumps(line), flush=True)
 
 
 def load_clock():
@@ -589,13 +614,19 @@ def main():
         if os.environ.get("RSAMD_BENCH_FAIL_RANK") == str(rank):
             sys.exit(3)   # before the hub handshake: the other ranks would wait on it
         dist = Dist(world)
-        harness_only(rank, world, dist)
+        cpu = None
+        if rank == 0 and not args.no_cpu_baseline:
+            cp1, cp2, _ = synth.two_view(args.n, OUTLIERS, seed=1)
+            cpu = cpu_baseline(cp1, cp2, args.cpu_seconds, args.cpu_procs or host_cores()[0])
+        harness_only(rank, world, dist, args, cpu)
         dist.close()
         return
     dist = Dist(world)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        # before any HIP call: the worker processes are forked from this one
+    if rank == 0 and not args.no_cpu_baseline:
+        # before any HIP call of this process: the worker processes are forked from it.  At
+        # world > 1 the other ranks wait for rank 0 at the first hub exchange meanwhile (their
+        # GPUs idle: nothing of the timed region overlaps the CPU baseline)
         cp1, cp2, _ = synth.two_view(args.n, OUTLIERS, seed=1)
         cpu = cpu_baseline(cp1, cp2, args.cpu_seconds, args.cpu_procs or host_cores()[0])
     # RSAMD_BENCH_DEVICE pins every rank to one device: a multi-rank rehearsal on a one-GPU
@@ -614,6 +645,7 @@ def main():
 
     comm = world > 1
     exchange = "none (one GPU)"
+    comm_ranks = [{"rank": 0, "device": ctx.device}]
     if comm:
         uid = np.zeros(_ffi.COMM_ID_BYTES, np.uint8)
         st = 0
@@ -625,19 +657,34 @@ def main():
             with _stdout_to_stderr():
                 st = _ffi.lib().rs_comm_init(ctx.handle, world, rank, _ffi.ptr(uid, ctypes.c_uint8))
         ok = dist.max(0.0 if st == 0 else 1.0) == 0.0   # every rank agrees on the transport
+        try:
+            exchange = exchange_policy(ok, "RSAMD_BENCH_DEVICE" in os.environ)
+        except RuntimeError as e:
+            print(f"error: {e} (this rank: status {st}: "
+                  f"{_ffi.lib().rs_last_error().decode(errors='replace')})", file=sys.stderr,
+                  flush=True)
+            if st == 0:
+                _ffi.lib().rs_comm_destroy(ctx.handle)
+            dist.close()
+            sys.exit(4)
         if ok:
-            exchange = "rccl all-gather"
             xcomm = _CtxComm(ctx, rank, world)
         else:
             if st == 0:
                 _ffi.lib().rs_comm_destroy(ctx.handle)
             print(f"warning: RCCL communicator init failed on some rank (status {st}: {_ffi.lib().rs_last_error().decode(errors='replace')}); "
                   "exchanging the per-pair records over the TCP hub", file=sys.stderr)
-            exchange = "tcp-hub all-gather (RCCL init failed)"
             xcomm = _HubComm(dist, rank, world)
         # the first collective on a communicator sets up its channels (lazy, can take far
-        # longer than the timed steps): do it before the timed region
-        xcomm.allgather_bytes(np.zeros(96, np.uint8).tobytes())
+        # longer than the timed steps): do it before the timed region.  Its payload is every
+        # rank's (rank, device): the communicator's own world and device map, in the line
+        me = np.zeros(12, np.int64)
+        me[0], me[1] = rank, ctx.device
+        got = np.frombuffer(b"".join(xcomm.allgather_bytes(me.tobytes())), np.int64).reshape(-1, 12)
+        comm_ranks = [{"rank": int(g[0]), "device": int(g[1])} for g in got]
+        if [r["rank"] for r in comm_ranks] != list(range(world)):
+            sys.exit(f"error: the communicator's all-gather returned ranks "
+                     f"{[r['rank'] for r in comm_ranks]}, expected 0..{world - 1}")
 
     rccl_lib = None
     if comm:
@@ -709,6 +756,7 @@ def main():
                    "n_corr": args.n, "hypotheses_per_step": H, "sampler": "philox (throughput)",
                    "parallelism": f"pairs sharded, {world} pair(s) on {world} GPU(s)",
                    "exchange": exchange, "exchange_library": rccl_lib,
+                   "comm_world": len(comm_ranks), "rank_devices": comm_ranks,
                    "harness": "tcp hub (no torch.distributed)" if world > 1 else "one process"},
         "roofline": {"bound": "valu", "kernel": COUNT_KERNEL["fp64" if os.environ.get("RSAMD_COUNT") == "fp64"
                                                          else "fp32"],

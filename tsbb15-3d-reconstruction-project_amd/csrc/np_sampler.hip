@@ -23,6 +23,8 @@
 // host.  Exactness does not depend on any tuning constant; tests compare against the host
 // replay (tests/test_gpu_np_sampler.py).
 #include <hip/hip_runtime.h>
+#include <array>
+#include <memory>
 
 #include <algorithm>
 #include <cmath>
@@ -1162,6 +1164,62 @@ __device__ __forceinline__ uint64_t rej_fixed_point(uint32_t w, uint32_t iu, uin
   return r2;
 }
 
+// The same two-bucket fixed point from "all accept" (lane l at state base_l = i - l), with the
+// state per lane in a VGPR: returns the window's reject mask.  Converged when two successive
+// rounds agree, checked every second round.
+#ifndef RSAMD_BLOCK4
+#define RSAMD_BLOCK4 1  // single-trajectory blocks of four windows under one test (A/B: 0)
+#endif
+#ifndef RSAMD_PARTIAL
+#define RSAMD_PARTIAL 0  // blocks run their first windows fast when only those stay in two buckets
+                         // (A/B: 1; measured 4.52 against 4.44-4.46 ms per C2 parse, not kept)
+#endif
+#ifndef RSAMD_BLOCK4M
+#define RSAMD_BLOCK4M 1  // the same blocks in the multi-trajectory intervals (A/B: 0)
+#endif
+#ifndef RSAMD_SINGLE_PRIO
+#define RSAMD_SINGLE_PRIO 0  // s_setprio of the single-trajectory wave (A/B; measured: no gain)
+#endif
+__device__ __forceinline__ uint64_t rej_fixed_point_aa(uint32_t w, uint32_t base, uint32_t M2) {
+  uint64_t r = __ballot((w & (base | M2)) > base), r1, r2;
+  do {
+    uint32_t sl = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(r >> 32),
+                                            __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(r), base));
+    r1 = __ballot((w & (sl | M2)) > sl);
+    sl = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(r1 >> 32),
+                                   __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(r1), base));
+    r2 = __ballot((w & (sl | M2)) > sl);
+    r = r2;
+  } while (r2 != r1);
+  return r2;
+}
+// The same fixed point checked after every round: fewer vector instructions per window where
+// the waves are issue-bound (the multi-trajectory phase) rather than latency-bound
+__device__ __forceinline__ uint64_t rej_fixed_point_aa1(uint32_t w, uint32_t base, uint32_t M2) {
+  uint64_t r = __ballot((w & (base | M2)) > base), rn;
+  for (;;) {
+    const uint32_t sl = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(r >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(r), base));
+    rn = __ballot((w & (sl | M2)) > sl);
+    if (rn == r) return rn;
+    r = rn;
+  }
+}
+#ifndef RSAMD_MULTI_FP
+#define RSAMD_MULTI_FP rej_fixed_point_aa  // multi-trajectory blocks (A/B: rej_fixed_point_aa1)
+#endif
+// add + popcount(r) on the vector unit: the mask comes from a vector compare, so the count never
+// takes the vector -> scalar -> vector round trip (s_bcnt1 then a VGPR operand: ~20 cycles more
+// per window, tools/ubench/lat_bench.hip).  The s_nop pair covers the SGPR read after the VALU
+// write, as the compiler places it before v_mbcnt.
+__device__ __forceinline__ uint32_t vbcnt_add(uint64_t r, uint32_t add) {
+  uint32_t o;
+  asm volatile("s_nop 1\n v_bcnt_u32_b32 %0, %1, %2\n v_bcnt_u32_b32 %0, %3, %0"
+               : "=&v"(o)
+               : "s"(static_cast<uint32_t>(r)), "v"(add), "s"(static_cast<uint32_t>(r >> 32)));
+  return o;
+}
+
 template <bool PY>
 __device__ __forceinline__ bool fast_window(uint32_t w, uint32_t &i) {
   uint32_t iv;
@@ -1273,8 +1331,42 @@ __device__ __forceinline__ uint32_t track_one(const EntryArgs &a, const uint32_t
   };
   set_bucket();
   for (int d = t; d < cp; d += 64 * kAhead) {
+    int kf = 0;  // windows of this block run with the state in a VGPR
+#if RSAMD_BLOCK4
+    if constexpr (!PY && RSAMD_REJFP) {
+      // A block of kAhead full windows under ONE two-bucket test: every state the block can
+      // reach (i .. i - 64 kAhead + 1) lies in i's bucket or the one below, where numpy's mask is
+      // s | M/2, so no per-window bucket test is needed.  The state lives in a VGPR as
+      // base = i - lane and advances by v_bcnt of the window's reject mask, so a window never
+      // waits for a vector -> scalar round trip; the fixed point starts from "all accept" and
+      // is checked every second round (tools/ubench/single_bench.hip, one wave alone: 5.6 ->
+      // 3.9 cycles per draw; with the other chunk's waves beside it and s_setprio: 7.5 -> 3.8)
+      // (a block whose lower states leave the two buckets runs its first kf windows so, where
+      // kf = the full windows above the lower bucket's floor, then the rest window by window)
+      const uint32_t Mb = 0xffffffffu >> __builtin_clz(i);
+      const uint32_t l2b = Mb > 3u ? (Mb >> 2) + 1u : 0xffffffffu;
+      kf = l2b != 0xffffffffu && i >= l2b + 63u ? static_cast<int>((i - l2b + 1u) >> 6) : 0;
+      kf = min(min(kf, kAhead), (cp - d) >> 6);
+      if (!RSAMD_PARTIAL && kf < kAhead) kf = 0;
+      if (kf > 0) {
+        const uint32_t M2 = Mb >> 1;
+        uint32_t base = i - static_cast<uint32_t>(lane);
+#pragma unroll
+        for (int k = 0; k < kAhead; ++k) {
+          if (k < kf) {
+            const uint32_t w = q[k];
+            q[k] = sw[(d - t + 64 * (kAhead + k) + lane) & (kCheck - 1)];
+            base = vbcnt_add(rej_fixed_point_aa(w, base, M2), base - 64u);
+          }
+        }
+        i = uni(base);  // lane 0's base is i
+        if (kf == kAhead) continue;
+      }
+    }
+#endif
 #pragma unroll
     for (int k = 0; k < kAhead; ++k) {
+      if (k < kf) continue;  // run above in the block's fast part
       const uint32_t w = q[k];
       q[k] = sw[(d - t + 64 * (kAhead + k) + lane) & (kCheck - 1)];
       const int dk = d + 64 * k;
@@ -1332,38 +1424,72 @@ __device__ __forceinline__ void track_interval(const EntryArgs &a, const uint32_
     const int q = wv + r * kTrackWaves;
     return s_lo[q] | (s_lo[q + 1 == m ? 0 : q + 1] << 16);
   };
+  // one window of chain r at draw dk (Wn draws)
+  auto one_window = [&](uint32_t w, int Wn, int dk, int r) {
+#if RSAMD_MULTI_VALU
+    if (Wn == 64 && fast_window<PY>(w, i[r])) return;
+#endif
+    // (the window mask only where the general step runs -- the opaque copy keeps the
+    // compiler from hoisting it into every window: scalar instructions on the CU's shared
+    // scalar unit)
+    int wn_ = Wn;
+    asm volatile("" : "+s"(wn_));
+    const uint64_t wm = wn_ == 64 ? ~0ull : ((1ull << wn_) - 1ull);
+    uint64_t wr;
+    uint32_t sl;
+    (void)window_step<PY, SMALL>(w, wm, i[r], n1, wr, sl);
+    if (wr) {  // hypothesis ends: the next hypothesis starts at the following draw
+      int eb = 0;
+      if (lane == 0) eb = atomicAdd(s_evn, __popcll(wr));
+      eb = __shfl(eb, 0);
+      if (((wr >> lane) & 1ull)) {
+        const int e = eb + static_cast<int>(lane_rank(wr));
+        if (e < a.ecap) ev[e] = make_uint2(static_cast<uint32_t>(dk + lane + 1), range_of(r));
+      }
+    }
+  };
   int d = t;
-  uint32_t wn = sw[lane];  // draws beyond cp are never accepted (lanes >= Wn)
+#if RSAMD_BLOCK4 && RSAMD_BLOCK4M
+  if constexpr (!PY && RSAMD_REJFP) {
+    // blocks of four full windows: a chain whose block stays within its bucket and the one below
+    // runs the four windows with its state in a VGPR (as track_one; no scalar work per window on
+    // the CU's shared scalar unit), the others window by window
+    for (; d + 256 <= cp; d += 256) {
+      uint32_t q[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) q[k] = sw[(d - t + 64 * k + lane) & (kCheck - 1)];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (r < nq) {
+          const uint32_t Mb = 0xffffffffu >> __builtin_clz(i[r]);
+          const uint32_t l2b = Mb > 3u ? (Mb >> 2) + 1u : 0xffffffffu;
+          int kf = l2b != 0xffffffffu && i[r] >= l2b + 63u
+                             ? min(4, static_cast<int>((i[r] - l2b + 1u) >> 6)) : 0;
+          if (!RSAMD_PARTIAL && kf < 4) kf = 0;
+          if (kf > 0) {
+            const uint32_t M2 = Mb >> 1;
+            uint32_t base = i[r] - static_cast<uint32_t>(lane);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              if (k < kf) base = vbcnt_add(RSAMD_MULTI_FP(q[k], base, M2), base - 64u);
+            i[r] = uni(base);
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (k >= kf) one_window(q[k], 64, d + 64 * k, r);
+        }
+      }
+    }
+  }
+#endif
+  uint32_t wn = sw[(d - t + lane) & (kCheck - 1)];  // draws beyond cp are never accepted (lanes >= Wn)
   while (d < cp) {
     const int Wn = min(64, cp - d);
     const uint32_t w = wn;
     if (d + 64 < cp) wn = sw[(d + 64 - t + lane) & (kCheck - 1)];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (r < nq) {
-#if RSAMD_MULTI_VALU
-        if (Wn == 64 && fast_window<PY>(w, i[r])) continue;
-#endif
-        // (the window mask only where the general step runs -- the opaque copy keeps the
-        // compiler from hoisting it into every window: scalar instructions on the CU's shared
-        // scalar unit)
-        int wn_ = Wn;
-        asm volatile("" : "+s"(wn_));
-        const uint64_t wm = wn_ == 64 ? ~0ull : ((1ull << wn_) - 1ull);
-        uint64_t wr;
-        uint32_t sl;
-        (void)window_step<PY, SMALL>(w, wm, i[r], n1, wr, sl);
-        if (wr) {  // hypothesis ends: the next hypothesis starts at the following draw
-          int eb = 0;
-          if (lane == 0) eb = atomicAdd(s_evn, __popcll(wr));
-          eb = __shfl(eb, 0);
-          if (((wr >> lane) & 1ull)) {
-            const int e = eb + static_cast<int>(lane_rank(wr));
-            if (e < a.ecap) ev[e] = make_uint2(static_cast<uint32_t>(d + lane + 1), range_of(r));
-          }
-        }
-      }
-    }
+    for (int r = 0; r < R; ++r)
+      if (r < nq) one_window(w, Wn, d, r);
 #ifdef RSAMD_DIAG
     dg[0] += 1;
 #endif
@@ -1445,9 +1571,14 @@ __device__ __forceinline__ void np_track_body(const EntryArgs &a, const uint32_t
     const long long c0 = __builtin_amdgcn_s_memtime();
 #endif
     if (nq == 1) {
+      // the single trajectory's wave is its chunk's critical path: issue priority over the
+      // other chunk's waves on the SIMD (tools/ubench/single_bench.hip: a parse wave beside a
+      // busy one 7.5 -> 5.2 cycles per draw at priority 3)
+      if (RSAMD_SINGLE_PRIO) __builtin_amdgcn_s_setprio(RSAMD_SINGLE_PRIO);
       const uint32_t i1 = track_one<PY, SMALL>(
           a, sw, &s_evn, ev, uni(s_st[wq]), uni(s_lo[wq] | (s_lo[wq + 1 == m ? 0 : wq + 1] << 16)),
           t, cp);
+      if (RSAMD_SINGLE_PRIO) __builtin_amdgcn_s_setprio(0);
       if (lane == 0) s_st[wq] = i1;
     }
     else if (nq == 2) track_interval<2, PY, SMALL>(a, sw, s_st, s_lo, &s_evn, ev, m, wq, 2, t, cp, dg);
@@ -2123,84 +2254,74 @@ __global__ __launch_bounds__(64) void k_np_result(const uint32_t *__restrict__ s
 }
 
 // ---- host ------------------------------------------------------------------------------------
-struct JumpPolys {
-  std::vector<std::vector<int32_t>> bits;  // level k: set bits of x^(2^k J) mod phi, the even
-  std::vector<int> ne;                     // ones first (ne[k] of them), then the odd ones
-};
-
-// the level polynomials for generators of JB blocks (J = 624 JB words), built once per JB
-// (~0.1 s of host arithmetic; chunk-aligned layouts use the chunk length)
-const JumpPolys &jump_polys(int JB) {
-  static std::mutex mu;
-  static std::vector<std::pair<int, JumpPolys *>> cache;
-  std::lock_guard<std::mutex> g(mu);
-  for (auto &e : cache)
-    if (e.first == JB) return *e.second;
-  auto *jp = new JumpPolys();
-  std::vector<uint64_t> p;
-  rs::mt_jump_poly(static_cast<uint64_t>(kN) * static_cast<uint64_t>(JB), p);
-  for (int k = 0; k < kLevels; ++k) {
-    if (k) rs::mt_poly_square(p);
-    std::vector<int32_t> b;
+// Level polynomials as the jump kernel reads them: per polynomial its set bits below kDeg, the
+// even ones first (ne of them), then the odd ones; all polynomials' lists concatenated.
+struct JumpBits {
+  std::vector<int32_t> all;
+  std::vector<int> off, n, ne;
+  void add(const std::vector<uint64_t> &p) {
+    off.push_back(static_cast<int>(all.size()));
+    const size_t n0 = all.size();
     for (int par = 0; par < 2; ++par) {
       for (int i = par; i < kDeg; i += 2)
-        if ((p[static_cast<size_t>(i) >> 6] >> (i & 63)) & 1u) b.push_back(i);
-      if (par == 0) jp->ne.push_back(static_cast<int>(b.size()));
+        if ((p[static_cast<size_t>(i) >> 6] >> (i & 63)) & 1u) all.push_back(i);
+      if (par == 0) ne.push_back(static_cast<int>(all.size() - n0));
     }
-    jp->bits.push_back(std::move(b));
+    n.push_back(static_cast<int>(all.size() - n0));
   }
-  cache.emplace_back(JB, jp);
-  return *jp;
+};
+
+// A small process-wide cache of level polynomials, keyed by (kind, JB, levels).  Entries are
+// immutable once built and are copied out under the mutex, so thread ranks of one process
+// (ThreadComm) may ask concurrently; at most kJumpCache entries are kept (oldest dropped).
+// With the fast arithmetic of mt_jump.cpp a new generator length costs a few ms of host time
+// (x^(624 JB) from cached powers of x^624, then the tree's products).
+constexpr size_t kJumpCache = 8;
+void jump_bits_cached(int kind, int JB, int levels, JumpBits &out) {
+  static std::mutex mu;
+  static std::vector<std::pair<std::array<int, 3>, std::shared_ptr<const JumpBits>>> cache;
+  std::lock_guard<std::mutex> g(mu);
+  const std::array<int, 3> key{kind, JB, levels};
+  for (auto &e : cache)
+    if (e.first == key) {
+      out = *e.second;
+      return;
+    }
+  auto jb = std::make_shared<JumpBits>();
+  std::vector<uint64_t> p;
+  rs::mt_jump_poly(static_cast<uint64_t>(kN) * static_cast<uint64_t>(JB), p);
+  if (kind == 0) {
+    // radix 2: level k is x^(2^k J), k < kLevels
+    for (int k = 0; k < levels; ++k) {
+      if (k) rs::mt_poly_square(p);
+      jb->add(p);
+    }
+  } else {
+    // radix R: level k's multipliers m = 1 .. R-1 are x^(m R^k J), index k (R-1) + m - 1
+    for (int k = 0; k < levels; ++k) {
+      const std::vector<uint64_t> base = p;
+      std::vector<uint64_t> q = base, t;
+      for (int m = 1; m < kind; ++m) {
+        if (m > 1) {
+          rs::mt_poly_mulmod(q, base, t);
+          q.swap(t);
+        }
+        jb->add(q);
+      }
+      rs::mt_poly_mulmod(q, base, p);  // x^(R^(k+1) J)
+    }
+  }
+  if (cache.size() >= kJumpCache) cache.erase(cache.begin());
+  cache.emplace_back(key, jb);
+  out = *jb;
 }
 
-// Radix-R tree levels (RSAMD_JRADIX, R <= 8): level k's multipliers m = 1 .. R-1 are
-// x^(m R^k J) mod phi, products of the level base x^(R^k J) (~5 ms of host arithmetic each);
-// built up to the levels a call needs and cached per JB
+// Radix-R tree levels (RSAMD_JRADIX, R <= 8): level k sends window g < R^k to g + m R^k
 #ifndef RSAMD_JRADIX
 #define RSAMD_JRADIX 8
 #endif
 constexpr int kJumpRadix = RSAMD_JRADIX;
 static_assert(kJumpRadix >= 2 && kJumpRadix <= 8, "jump radix");
-struct JumpPolysR {
-  std::vector<std::vector<int32_t>> bits;  // index k (R-1) + m - 1, even bits first
-  std::vector<int> ne;
-  std::vector<uint64_t> next;              // x^(R^levels J): the next level's base
-  int levels = 0;
-};
-const JumpPolysR &jump_polys_r(int JB, int levels) {
-  static std::mutex mu;
-  static std::vector<std::pair<int, JumpPolysR *>> cache;
-  std::lock_guard<std::mutex> g(mu);
-  JumpPolysR *jp = nullptr;
-  for (auto &e : cache)
-    if (e.first == JB) jp = e.second;
-  if (!jp) {
-    jp = new JumpPolysR();
-    rs::mt_jump_poly(static_cast<uint64_t>(kN) * static_cast<uint64_t>(JB), jp->next);
-    cache.emplace_back(JB, jp);
-  }
-  while (jp->levels < levels) {
-    const std::vector<uint64_t> base = jp->next;
-    std::vector<uint64_t> p = base, t;
-    for (int m = 1; m < kJumpRadix; ++m) {
-      if (m > 1) {
-        rs::mt_poly_mulmod(p, base, t);
-        p.swap(t);
-      }
-      std::vector<int32_t> b;
-      for (int par = 0; par < 2; ++par) {
-        for (int i = par; i < kDeg; i += 2)
-          if ((p[static_cast<size_t>(i) >> 6] >> (i & 63)) & 1u) b.push_back(i);
-        if (par == 0) jp->ne.push_back(static_cast<int>(b.size()));
-      }
-      jp->bits.push_back(std::move(b));
-    }
-    rs::mt_poly_mulmod(p, base, t);  // x^(R^(k+1) J)
-    jp->next.swap(t);
-    ++jp->levels;
-  }
-  return *jp;
-}
 
 uint32_t untemper(uint32_t z) {
   uint32_t y = z ^ (z >> 18);
@@ -2334,7 +2455,7 @@ struct rs_np_shard {
   // device
   int32_t *d_bits = nullptr;
   std::vector<int> bit_off, bit_n, bit_ne;
-  int32_t *d_rbits = nullptr;  // radix-tree level polynomials (jump_polys_r)
+  int32_t *d_rbits = nullptr;  // radix-tree level polynomials (jump_bits_cached)
   std::vector<int> rbit_off, rbit_n, rbit_ne;
   int rbits_JB = 0, rlevels = 0;
   uint32_t *d_win = nullptr, *d_chain = nullptr, *d_stream = nullptr, *d_fin = nullptr,
@@ -2479,23 +2600,19 @@ int shard_layout(rs_np_shard &w, int32_t pos, int64_t count) {
 int shard_windows(rs_np_shard &w, const uint32_t *key, hipStream_t s) {
   int st;
   if ((st = sgrow(w.d_win, w.cap_win, w.G * kN))) return st;
-  if (w.bits_JB != w.JB) {  // the level polynomials of this generator length
-    const JumpPolys &jp = jump_polys(w.JB);
-    std::vector<int32_t> all;
-    w.bit_off.clear();
-    w.bit_n.clear();
-    w.bit_ne.clear();
-    for (size_t k = 0; k < jp.bits.size(); ++k) {
-      w.bit_off.push_back(static_cast<int>(all.size()));
-      w.bit_n.push_back(static_cast<int>(jp.bits[k].size()));
-      w.bit_ne.push_back(jp.ne[k]);
-      all.insert(all.end(), jp.bits[k].begin(), jp.bits[k].end());
-    }
+  // the radix-2 level polynomials of this generator length: only for a rank's first window
+  // (g0 > 0: a chain of level jumps) or a radix-2 tree; world 1 (g0 = 0) never needs them
+  if ((w.g0 != 0 || kJumpRadix == 2) && w.bits_JB != w.JB) {
+    JumpBits jb;
+    jump_bits_cached(0, w.JB, kLevels, jb);
+    w.bit_off = jb.off;
+    w.bit_n = jb.n;
+    w.bit_ne = jb.ne;
     int64_t cap = 0;
     if (w.d_bits) (void)hipFree(w.d_bits);
     w.d_bits = nullptr;
-    if ((st = sgrow(w.d_bits, cap, static_cast<int64_t>(all.size())))) return st;
-    HIP_TRY(hipMemcpy(w.d_bits, all.data(), sizeof(int32_t) * all.size(), hipMemcpyHostToDevice));
+    if ((st = sgrow(w.d_bits, cap, static_cast<int64_t>(jb.all.size())))) return st;
+    HIP_TRY(hipMemcpy(w.d_bits, jb.all.data(), sizeof(int32_t) * jb.all.size(), hipMemcpyHostToDevice));
     w.bits_JB = w.JB;
   }
   if (w.g0 == 0) {
@@ -2532,24 +2649,18 @@ int shard_windows(rs_np_shard &w, const uint32_t *key, hipStream_t s) {
     int need = 0;
     for (int64_t B = 1; B < w.G; B *= kJumpRadix) ++need;
     if (w.rbits_JB != w.JB || w.rlevels < need) {
-      const JumpPolysR &jr = jump_polys_r(w.JB, need);
-      std::vector<int32_t> all;
-      w.rbit_off.clear();
-      w.rbit_n.clear();
-      w.rbit_ne.clear();
-      for (size_t k = 0; k < jr.bits.size(); ++k) {
-        w.rbit_off.push_back(static_cast<int>(all.size()));
-        w.rbit_n.push_back(static_cast<int>(jr.bits[k].size()));
-        w.rbit_ne.push_back(jr.ne[k]);
-        all.insert(all.end(), jr.bits[k].begin(), jr.bits[k].end());
-      }
+      JumpBits jr;
+      jump_bits_cached(kJumpRadix, w.JB, need, jr);
+      w.rbit_off = jr.off;
+      w.rbit_n = jr.n;
+      w.rbit_ne = jr.ne;
       int64_t cap = 0;
       if (w.d_rbits) (void)hipFree(w.d_rbits);
       w.d_rbits = nullptr;
-      if ((st = sgrow(w.d_rbits, cap, static_cast<int64_t>(all.size())))) return st;
-      HIP_TRY(hipMemcpy(w.d_rbits, all.data(), sizeof(int32_t) * all.size(), hipMemcpyHostToDevice));
+      if ((st = sgrow(w.d_rbits, cap, static_cast<int64_t>(jr.all.size())))) return st;
+      HIP_TRY(hipMemcpy(w.d_rbits, jr.all.data(), sizeof(int32_t) * jr.all.size(), hipMemcpyHostToDevice));
       w.rbits_JB = w.JB;
-      w.rlevels = jr.levels;
+      w.rlevels = need;
     }
     int lv = 0;
     for (int64_t B = 1; B < w.G; B *= kJumpRadix, ++lv) {
