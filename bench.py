@@ -424,20 +424,22 @@ E5_ROUND2 = (13389928.829414358, "BENCH_r02.json extras.e5_ransac_c2.value (1.49
 
 
 def load_pmc(n_corr, hyps):
-    """HBM bytes per counting launch from the newest committed rocprofv3 PMC summary."""
+    """The newest committed rocprofv3 summary of the counting kernel (profiles/r*_pmc_k_f8_count
+    .json, tools/pmc_summary.py) for this workload: HBM bytes per launch from the PMC passes and
+    the C2-only kernel-trace average.  Returns (hbm_bytes, record) or (None, None)."""
     import glob
     found = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_k_f8_count.json")))
     if not found:
-        return None
+        return None, None
     path = found[-1]
     try:
         with open(path) as f:
             d = json.load(f)
         if d.get("n_corr") == n_corr and d.get("hypotheses") == hyps:
-            return d.get("hbm_bytes_per_launch")
+            return d.get("hbm_bytes_per_launch"), dict(d, source=os.path.relpath(path, REPO))
     except Exception:
-        return None
-    return None
+        return None, None
+    return None, None
 
 
 def _free_port_pair():
@@ -736,7 +738,7 @@ def main():
     # score; the kernel computes it in fp32 with an exact fp64 guard band, so the bounding
     # peak is the FP32 vector rate (its FP64 fraction is reported beside it)
     achieved = H * FLOP_PER_CORR * args.n / (c_ms * 1e-3) / 1e12
-    pmc = load_pmc(args.n, H)
+    pmc, pmc_rec = load_pmc(args.n, H)
     line = {
         "metric": METRIC,
         "value": value,
@@ -771,6 +773,14 @@ def main():
                                                   if pmc else None),
                      "per_launch": {"hypotheses": H, "flop": H * FLOP_PER_CORR * args.n,
                                     "avg_ms": c_ms, "timed_launches_every": TIMING_EVERY},
+                     # the same kernel in the committed C2-only rocprofv3 kernel trace (a
+                     # profiled run on the profiling box: DVFS and the box set both figures)
+                     "rocprof_c2_avg_us": (pmc_rec["rocprof_c2_avg_ns"] / 1e3
+                                           if pmc_rec and pmc_rec.get("rocprof_c2_avg_ns") else None),
+                     "rocprof_c2_frac": (H * FLOP_PER_CORR * args.n / (pmc_rec["rocprof_c2_avg_ns"] * 1e-9)
+                                         / 1e12 / PEAK_FP32_VALU_TFLOPS
+                                         if pmc_rec and pmc_rec.get("rocprof_c2_avg_ns") else None),
+                     "rocprof_source": pmc_rec["source"] if pmc_rec else None,
                      "whole_run_nominal": {
                          "flop_per_hypothesis": FLOP_PER_CORR * args.n + FLOP_SOLVE,
                          "tflops": value * (FLOP_PER_CORR * args.n + FLOP_SOLVE) / 1e12,
@@ -824,8 +834,20 @@ def main():
         # GPU (rs_f8_plan_run_np).  Weak: every rank its own pair's run.  Sharded: ONE pair's
         # H hypotheses split over the ranks (rs_f8_plan_run_np_slice + c* all-reduce and
         # candidate all-gather), the fun.py:320-328 decision replayed on every rank.
-        from tsbb15_amd import parallel
+        from tsbb15_amd import fun, parallel
         key0, pos0 = _ffi.np_seed(0)
+        # the drop-in's first call (fun.ransac_f, the loop of getFFromLabCode) at this N in this
+        # process: a fresh context -- new plan, new parse buffers -- and jump polynomials not
+        # built yet; then the same call warm
+        hs0 = _ffi.np_host_stats()
+        cnew = _ffi.Context(ctx.device)
+        t = time.perf_counter()
+        fun.ransac_f(p1, p2, r=H, rng=np.random.RandomState(0), ctx=cnew)
+        first_call = time.perf_counter() - t
+        hs1 = _ffi.np_host_stats()
+        warm_call, _ = _best_of(lambda: fun.ransac_f(p1, p2, r=H, rng=np.random.RandomState(0),
+                                                     ctx=cnew), 3)
+        cnew.close()
         tg = []
         for _ in range(6):
             dist.barrier()
@@ -835,6 +857,12 @@ def main():
             tg.append(dist.max(time.perf_counter() - t))
         pm = {"value": world * H / min(tg[1:]), "unit": "hypotheses/s",
               "ms": 1e3 * min(tg[1:]), "scaling": "weak", "n_gpus": world,
+              "first_call_ms": first_call * 1e3, "warm_call_ms": warm_call * 1e3,
+              "first_call_host_jump_ms": hs1[0] - hs0[0],
+              "first_call_note": "fun.ransac_f (getFFromLabCode's RANSAC, fun.py:298-328) on a "
+                                 "fresh context at this N: plan and parse buffers allocated, MT "
+                                 "jump polynomials built on the host (host_jump_ms); warm = best "
+                                 "of 3 of the same call",
               "note": "np.random legacy stream (seed 0) reproduced bit-exactly on the GPU "
                       "(MT19937 jump-ahead windows, all-entry-state chunk parse + windowed "
                       "tracking, per-hypothesis swap trace), then the same GPU pipeline; one "

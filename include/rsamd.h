@@ -125,6 +125,11 @@ int rs_py_shuffle_tuples_gpu(rs_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int
  *                        when the state stays in the caller's block).
  * tsbb15_amd.parallel.np_sharded_segments runs the exchange; world 1 reproduces
  * rs_np_choice_tuples_gpu bit for bit. */
+/* Host milliseconds this process has spent building MT19937 jump polynomials for the GPU parse
+ * (once per new generator length; mt_jump.cpp's carry-less products), and the level sets built.
+ * No reference counterpart: it accounts for the first-call cost of getFFromLabCode (fun.py:291). */
+int rs_np_host_stats(double *jump_ms, int64_t *builds);
+
 typedef struct rs_np_shard rs_np_shard;
 int rs_np_shard_create(rs_ctx *ctx, int64_t n, int32_t k, int32_t world, int32_t rank, int32_t py,
                        rs_np_shard **out);

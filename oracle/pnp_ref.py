@@ -252,19 +252,26 @@ def bearings(y):
 
 def ransac_pnp_p3p(y_med, X_med, y_high, X_high, r, thresh, rng=None, trace=False):
     """ransac_robust with n = 3 (ransac.py:72-111): per trial the P3P poses in order, each
-    scored on D_med; strict ">" over (trial, pose).  Returns (R, t, inl_med, inl_high,
+    scored on D_med; strict ">" over (trial, pose) within the front-facing and within the
+    mirrored-depth poses, a mirrored winner only at more than twice the front-facing count.  Returns (R, t, inl_med, inl_high,
     best_trial, best_pose, counts (r, 8) or None)."""
-    best, best_pose, best_count, R_best, t_best = -1, -1, 0, None, None
+    # per class (front-facing, mirrored-depth): the first pose of largest count, strict ">"
+    cls = [[-1, -1, 0, None, None], [-1, -1, 0, None, None]]
     counts = np.zeros((r, 8), np.int64) if trace else None
     for i in range(r):
         T = gen_rnd_indices(len(X_high), 3, rng)
         sols = p3p_lambda_twist(X_high[T], bearings(y_high[T]))
-        for j, (R, t, _) in enumerate(sols):
+        for j, (R, t, mirrored) in enumerate(sols):
             c_med = int(np.count_nonzero(thresh >= pose_errors(R, t, X_med, y_med)))
             if trace:
                 counts[i, j] = c_med
-            if c_med > best_count:
-                best, best_pose, best_count, R_best, t_best = i, j, c_med, R, t
+            b = cls[1 if mirrored else 0]
+            if c_med > b[2]:
+                b[:] = [i, j, c_med, R, t]
+    # a mirrored pose reprojects like its front-facing twin (the scene behind the camera); it
+    # wins only when its count is more than twice the best front-facing count (the kernel's
+    # kMirrorCountWins; OpenCV's p3p never returns it, a negative-scale view needs it)
+    best, best_pose, best_count, R_best, t_best = cls[1] if cls[1][2] > 2 * cls[0][2] else cls[0]
     if best < 0:
         return None, None, None, None, -1, -1, counts
     inl_med = np.flatnonzero(thresh >= pose_errors(R_best, t_best, X_med, y_med))

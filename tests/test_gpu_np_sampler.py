@@ -135,6 +135,59 @@ def test_plan_run_np_equals_host_tuple_run(ctx, n, H, seed, out):
     assert np.array_equal(np.array(g[0].F[:]), np.array(h[0].F[:]))
 
 
+@pytest.mark.parametrize("n", [129, 257, 513, 1025, 2049])
+def test_gpu_stream_pow2_populations_with_pauses(ctx, monkeypatch, n):
+    """N - 1 = 2^k (the top state alone in its mask bucket, the two-bucket batches' edge) with
+    the stream in two passes and many chunks pausing at the first pass's end (RSAMD_NP_XDRAWS,
+    read at every call): the r04d_tree1 fault's parameters (N = 257, 1e4 hypotheses, seed 3)
+    among them.  The parse fails loudly on a corrupt hand-over (err bits 4 / 8) and the host
+    checks the segment layout, so an out-of-range index cannot pass silently."""
+    count = max(2000, 2_600_000 // n)
+    _same(n, 8, count, seed=3)
+    for xd in ("700", "5000"):
+        monkeypatch.setenv("RSAMD_NP_XDRAWS", xd)
+        _same(n, 8, count, seed=n)
+    monkeypatch.setenv("RSAMD_NP_XDRAWS", "700")
+    key, pos = _state(3)
+    from tsbb15_amd import synth
+    p1, p2, _ = synth.two_view(n, 0.3, seed=4)
+    plan = _ffi.F8Plan(ctx, n, 10000)
+    try:
+        plan.set_points(p1, p2)
+        gkey, gpos = plan.run_np(10000, key, pos)
+        g = plan.result()
+        tup, rkey, rpos = _ffi.np_choice_tuples(key, pos, n, 8, 10000)
+        plan.run(10000, mode=_ffi.SAMPLER_TUPLES, tuples=tup)
+        h = plan.result()
+    finally:
+        plan.close()
+    assert gpos == rpos and np.array_equal(gkey, rkey)
+    assert g[0].best_index == h[0].best_index and np.array_equal(g[1], h[1])
+
+
+def test_drop_in_session_across_populations():
+    """fun.ransac_f on ONE context for pairs of different N, growing and shrinking (the plan and
+    the parse session are retargeted, their buffers kept): every call equals the oracle loop
+    (fun.py:303-328 restated) on its own RandomState -- winner, inlier set, F, MT state."""
+    from oracle import ransac_ref
+    from tsbb15_amd import fun, synth
+    c = _ffi.Context(0)
+    try:
+        for j, n in enumerate((300, 2000, 257, 1500, 2000, 64, 4097)):
+            p1, p2, _ = synth.two_view(n, 0.3, seed=20 + j)
+            rg, rc = np.random.RandomState(j), np.random.RandomState(j)
+            res = fun.ransac_f(p1, p2, r=400, rng=rg, ctx=c)
+            F, S, _, best, _ = ransac_ref.ransac_f(p1, p2, r=400, rng=rc)
+            assert res.best_index == best, (n, res.best_index, best)
+            assert np.array_equal(res.inliers, S), n
+            d = np.abs(ransac_ref.normalize_F(res.F) - ransac_ref.normalize_F(F)).max()
+            assert d < 1e-6, (n, d)
+            assert np.array_equal(rg.get_state()[1], rc.get_state()[1]) and \
+                rg.get_state()[2] == rc.get_state()[2], n
+    finally:
+        c.close()
+
+
 # ---- the CPython stream (ransac.gen_rnd_indices: random.shuffle, getrandbits rejection) ----
 def _py_state(seed, skip=0):
     import random

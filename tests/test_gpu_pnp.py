@@ -107,7 +107,7 @@ def test_ransac_robust_p3p_branch_equals_oracle(ctx):
     R, t, im, ih, best, cnt = ransac.ransac_pnp(X, y, X, y, r, thr, 3, rng=rng_g)
     Ro, to, imo, iho, besto, poseo, counts = pnp_ref.ransac_pnp_p3p(y, X, y, X, r, thr,
                                                                     rng=rng_o, trace=True)
-    assert best == besto and cnt == counts.max()
+    assert best == besto and cnt == counts[besto, poseo]
     assert np.array_equal(im, imo) and np.array_equal(ih, iho)
     np.testing.assert_allclose(R, Ro, atol=1e-9)
     np.testing.assert_allclose(t, to, rtol=1e-9, atol=1e-9)
@@ -120,6 +120,32 @@ def test_ransac_robust_p3p_branch_equals_oracle(ctx):
     R_est, t_est, C_est = ransac.ransac_robust(D, D, r, thr, 3)
     np.testing.assert_allclose(R_est[0], Ro, atol=1e-9)
     assert np.array_equal(C_est[0][0], D[imo]) and np.array_equal(C_est[0][1], D[iho])
+
+
+def test_ransac_robust_p3p_noisy_near_planar_keeps_depths_positive(ctx):
+    """on a noisy near-planar scene the mirrored-depth twin of the true pose (a turn
+    about the plane's normal, the scene behind the camera) reprojects almost like it and can
+    out-count it by a few points; the winner must still put every inlier in front of the
+    camera (OpenCV's p3p, the reference's, never returns a mirrored pose).  GPU = oracle."""
+    from tsbb15_amd import synth as sy
+    for seed in range(6):
+        rs = np.random.RandomState(100 + seed)
+        m = 200
+        X = np.column_stack([rs.uniform(-1.0, 1.0, m), rs.uniform(-1.0, 1.0, m),
+                             6.0 + rs.normal(0.0, 0.01, m)])   # a plane 6 units ahead
+        R0, t0 = sy.rot_y(0.15), np.array([0.1, -0.05, 0.3])
+        P = (R0 @ X.T).T + t0
+        y = np.column_stack([P[:, 0] / P[:, 2], P[:, 1] / P[:, 2], np.ones(m)])
+        y[:, :2] += rs.normal(0.0, 1.5 / 800.0, (m, 2))          # ~1.5 px of noise
+        out = rs.permutation(m)[:40]
+        y[out, :2] = rs.uniform(-0.4, 0.4, (40, 2))
+        thr = (3.0 / 800.0) ** 2
+        rg, ro = random.Random(seed), random.Random(seed)
+        R, t, im, ih, best, cnt = ransac.ransac_pnp(X, y, X, y, 300, thr, 3, rng=rg)
+        Ro, to, imo, iho, besto, poseo, _ = pnp_ref.ransac_pnp_p3p(y, X, y, X, 300, thr, rng=ro)
+        assert best == besto and np.array_equal(im, imo)
+        z = (np.asarray(R) @ X[im].T).T[:, 2] + np.asarray(t)[2]
+        assert len(im) > 100 and (z > 0).all(), (seed, len(im), z.min())
 
 
 def test_ransac_robust_p3p_known_answers_badino2(ctx):

@@ -14,7 +14,11 @@ echo "pytest_gpu exit $?" | tee -a $OUT/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo smoke failed; exit 1; }
 timeout -k 10 400 python bench.py --steps $STEPS --warmup 200 > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; exit 1; }
 cat $OUT/bench.json
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 bench.py --steps $STEPS --warmup 200 --no-cpu-baseline --no-extras > $OUT/prof_bench.log 2>&1 || { echo rocprof failed; exit 1; }
+# kernel trace of the C2 headline alone (no parity mode, fp64 count or extras: every
+# k_f8_count32q launch in it is a C2-size launch, so the stats average is the line's kernel)
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 bench.py --steps $STEPS --warmup 200 --no-cpu-baseline --no-extras --no-parity-mode --no-fp64-count > $OUT/prof_bench.log 2>&1 || { echo rocprof failed; exit 1; }
+# and the whole line's kernels (parity mode and its split projection included) for reference
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_all -o bench -- python3 bench.py --steps $STEPS --warmup 200 --no-cpu-baseline --no-extras > $OUT/prof_all.log 2>&1 || { echo rocprof all failed; exit 1; }
 # PMC passes on a warmed, clock-ramped run (200 warm-up launches, 50 counted), one pass per
 # counter block (MI355X_MICROARCH.md: FETCH_SIZE alone, WRITE_SIZE alone)
 B="python3 bench.py --steps 50 --warmup 200 --no-cpu-baseline --no-parity-mode --no-extras --no-fp64-count"

@@ -37,6 +37,9 @@ def main():
     os.makedirs(prof, exist_ok=True)
     shutil.copy(os.path.join(src, "prof", "bench_kernel_stats.csv"),
                 os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    if os.path.exists(os.path.join(src, "prof_all", "bench_kernel_stats.csv")):
+        shutil.copy(os.path.join(src, "prof_all", "bench_kernel_stats.csv"),
+                    os.path.join(prof, f"{tag}_kernel_stats_all.csv"))
     bench = json.load(open(os.path.join(src, "bench.json")))
     counters, launches = {}, {}
     for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sqc"):
@@ -48,6 +51,14 @@ def main():
     stats = {r["Name"].split("(")[0]: {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                                        "pct": float(r["Percentage"])}
              for r in csv.DictReader(open(os.path.join(src, "prof", "bench_kernel_stats.csv")))}
+    # the C2-only kernel trace: every k_f8_count32q launch is C2-size; the timed steps are the
+    # last `steps` launches of the trace
+    c2 = [r for r in csv.DictReader(open(os.path.join(src, "prof", "bench_kernel_trace.csv")))
+          if KERNEL in r["Kernel_Name"]]
+    dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in c2]
+    steps = int(bench["steps"])
+    c2_all_ns = sum(dur) / len(dur) if dur else None
+    c2_timed_ns = sum(dur[-steps:]) / len(dur[-steps:]) if dur else None
     fetch = counters.get("FETCH_SIZE", 0.0) * 1024
     write = counters.get("WRITE_SIZE", 0.0) * 1024
     out = {
@@ -59,6 +70,12 @@ def main():
         "hbm_bytes_per_launch": fetch + write,
         "hbm_bytes_per_launch_fetch_x2_upper": 2 * fetch + write,
         "kernel_stats_avg_ns": next((v["avg_ns"] for k, v in stats.items() if KERNEL in k), None),
+        "rocprof_c2_launches": len(dur),
+        "rocprof_c2_avg_ns": c2_all_ns,
+        "rocprof_c2_timed_avg_ns": c2_timed_ns,
+        "rocprof_c2_note": "rocprofv3 --kernel-trace of bench.py with --no-parity-mode --no-fp64-count "
+                           "--no-extras: every k_f8_count32q launch is a C2 launch (warm-up + steps); "
+                           "timed = the last `steps` launches",
         "bench_hip_event_avg_ms": bench["kernels_ms"].get("k_f8_count32q",
                                                           bench["kernels_ms"].get("k_f8_count")),
         "valu_insts_per_wave_point": (counters.get("SQ_INSTS_VALU", 0.0) /

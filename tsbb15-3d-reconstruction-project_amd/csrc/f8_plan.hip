@@ -76,6 +76,7 @@ int env_int(const char *name, int dflt) {
 struct rs_f8_plan {
   rs_ctx *ctx = nullptr;
   int64_t n = 0, max_hyp = 0, ld = 0;
+  int64_t cap_n = 0;           // points the per-point buffers hold (>= n; plan_retarget)
   double *d_p12 = nullptr;     // staging (2,n) p1 then (2,n) p2
   rsd::Pt *d_pts = nullptr;    // AoS float64 points
   float4 *d_pts32q = nullptr;  // the same, point-pair layout (k_f8_count32q)
@@ -175,6 +176,7 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
   auto *p = new rs_f8_plan();
   p->ctx = c;
   p->n = n;
+  p->cap_n = n;
   p->max_hyp = max_hyp;
   p->ld = (max_hyp + 63) / 64 * 64;
   const size_t res_bytes = sizeof(rsd::F8DevResult) + sizeof(int64_t) * static_cast<size_t>(n);
@@ -248,6 +250,44 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
     return hip_fail(e, "rs_f8_plan_create");
   }
   *out = p;
+  return RS_OK;
+}
+
+static int plan_flush(rs_f8_plan *p);
+
+// A new population for an existing plan (the drop-in's calls, one pair after another): the
+// per-point buffers are reallocated only when n exceeds what they hold; the per-hypothesis
+// buffers, events and pinned slots are kept (a fresh plan allocates ~20 buffers)
+static int plan_retarget(rs_f8_plan *p, int64_t n) {
+  if (n < 8) return fail(RS_EINVAL, "Cannot take a larger sample than population when 'replace=False'");
+  if (n > (1LL << 30)) return fail(RS_EINVAL, "plan dimensions out of range");
+  int st = plan_flush(p);  // runs in flight read the resident points and results
+  if (st) return st;
+  if (n > p->cap_n) {
+    const int64_t cap = std::max<int64_t>(n, p->cap_n + p->cap_n / 4);
+    (void)hipFree(p->d_p12);
+    (void)hipFree(p->d_pts);
+    (void)hipFree(p->d_pts32q);
+    p->d_p12 = nullptr;
+    p->d_pts = nullptr;
+    p->d_pts32q = nullptr;
+    hipError_t e = hipMalloc(&p->d_p12, sizeof(double) * 4 * cap);
+    if (e == hipSuccess) e = hipMalloc(&p->d_pts, sizeof(rsd::Pt) * cap);
+    if (e == hipSuccess) e = hipMalloc(&p->d_pts32q, sizeof(float4) * ((cap + 7) & ~7LL));
+    for (RunBufs &b : p->buf) {
+      (void)hipFree(b.d_spec);
+      (void)hipFree(b.d_res);
+      b.d_spec = nullptr;
+      b.d_res = nullptr;
+      if (e == hipSuccess) e = hipMalloc(&b.d_spec, sizeof(int) * rsd::kSelectBlocks * static_cast<size_t>(cap));
+      if (e == hipSuccess)
+        e = hipMalloc(&b.d_res, sizeof(rsd::F8DevResult) + sizeof(int64_t) * static_cast<size_t>(cap));
+    }
+    if (e != hipSuccess) return hip_fail(e, "rs_f8_plan retarget");
+    p->cap_n = cap;
+  }
+  p->n = n;
+  p->fp32_ok = false;  // set_points decides it for the new points
   return RS_OK;
 }
 
@@ -679,12 +719,14 @@ extern "C" int rs_f8_ransac_np(rs_ctx *c, const double *p1, const double *p2, in
   if (n < 8)
     return fail(RS_EINVAL, "Cannot take a larger sample than population when 'replace=False'");
   if (H < 1) return fail(RS_EINVAL, "hypothesis count must be positive");
-  if (c->np_plan && (c->np_plan->n != n || c->np_plan->max_hyp < H)) {
+  if (c->np_plan && c->np_plan->max_hyp < H) {
     rs_f8_plan_destroy(c->np_plan);
     c->np_plan = nullptr;
   }
   int st;
   if (!c->np_plan && (st = rs_f8_plan_create(c, n, H, &c->np_plan))) return st;
+  // another pair's population: the same plan, its per-point buffers grown if need be
+  if (c->np_plan->n != n && (st = plan_retarget(c->np_plan, n))) return st;
   if ((st = rs_f8_plan_set_points(c->np_plan, p1, p2))) return st;
   uint32_t key[RS_MT_N];
   int32_t pos = *mt_pos;

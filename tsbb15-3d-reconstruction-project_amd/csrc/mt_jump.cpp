@@ -8,8 +8,8 @@
 // is the XOR of y_{i+w} over the set bits i of p (only the top bit of word 0 is state; the
 // caller asks for the window one word early when it needs that word whole).
 //
-//   phi: Berlekamp-Massey on 2 x 19937 output bits of any seeded generator (once per
-//        process, ~20 ms), verified against the next 4096 bits;
+//   phi: Berlekamp-Massey on 2 x 19937 output bits of any seeded generator, embedded as a
+//        constant (mt_phi.h, tools/gen_mt_phi.cpp) and re-derived by the self-test;
 //   p:   x^(J mod 624) by shifts times cached x^(624 2^k) over the set bits of J div 624,
 //        products by carry-less multiplication with Barrett reduction (below);
 //   numpy's state (key[624], pos) is the raw block holding the next word plus the offset.
@@ -25,6 +25,12 @@
 #endif
 
 #include "common.h"
+#if RSAMD_GEN_PHI  // tools/gen_mt_phi.cpp: writes the constants below from charpoly_bm
+constexpr uint64_t kPhiWords[312] = {};
+constexpr uint64_t kMuWords[312] = {};
+#else
+#include "mt_phi.h"
+#endif
 
 namespace {
 
@@ -64,7 +70,8 @@ void xor_shifted(Poly &p, const Poly &q, int64_t s) {
   }
 }
 
-const Poly &charpoly() {
+// phi by Berlekamp-Massey (~50 ms): the generator of mt_phi.h and the self-test's check of it
+const Poly &charpoly_bm() {
   static Poly phi;
   static std::once_flag once;
   std::call_once(once, [] {
@@ -131,6 +138,16 @@ const Poly &charpoly() {
       if (getbit(C, i)) flipbit(phi, L - i);
     (void)T;
   });
+  return phi;
+}
+
+// phi from mt_phi.h (the process never pays for Berlekamp-Massey)
+const Poly &charpoly() {
+  static const Poly phi = [] {
+    Poly p(kWords, 0);
+    for (int i = 0; i < 312; ++i) p[static_cast<size_t>(i)] = kPhiWords[i];
+    return p;
+  }();
   return phi;
 }
 
@@ -211,22 +228,28 @@ struct Barrett {
   u64 phi[kR], mu[kR];
 };
 
+// mu = x^(2 kDeg) div phi by long division (the generator of mt_phi.h and the self-test)
+Poly barrett_mu_bm(const Poly &phi) {
+  Poly rem(2 * kR + 2, 0), mu(kR + 1, 0);
+  flipbit(rem, 2 * static_cast<int64_t>(kDeg));
+  for (int64_t i = 2 * static_cast<int64_t>(kDeg); i >= kDeg; --i)
+    if (getbit(rem, i)) {
+      flipbit(mu, i - kDeg);
+      xor_shifted(rem, phi, i - kDeg);
+    }
+  mu.resize(kR);
+  return mu;
+}
+
 const Barrett &barrett() {
-  static Barrett B;
-  static std::once_flag once;
-  std::call_once(once, [] {
-    const Poly &phi = charpoly();
-    for (int i = 0; i < kR; ++i) B.phi[i] = phi[i];
-    // mu = x^(2 kDeg) div phi, by long division (once per process, a few ms)
-    Poly rem(2 * kR + 2, 0), mu(kR + 1, 0);
-    flipbit(rem, 2 * static_cast<int64_t>(kDeg));
-    for (int64_t i = 2 * static_cast<int64_t>(kDeg); i >= kDeg; --i)
-      if (getbit(rem, i)) {
-        flipbit(mu, i - kDeg);
-        xor_shifted(rem, phi, i - kDeg);
-      }
-    for (int i = 0; i < kR; ++i) B.mu[i] = mu[i];
-  });
+  static const Barrett B = [] {
+    Barrett b;
+    for (int i = 0; i < kR; ++i) {
+      b.phi[i] = kPhiWords[i];
+      b.mu[i] = kMuWords[i];
+    }
+    return b;
+  }();
   return B;
 }
 
@@ -264,33 +287,35 @@ void sqrmod_fast(const u64 *a, u64 *r) {
   barrett_reduce(p, r);
 }
 
-// x^(624 * 2^k) mod phi for k < 40, built once: x^(624 JB) is the product over JB's set bits
-const std::vector<std::vector<u64>> &pow2_table() {
+// x^(624 * 2^k) mod phi for k < 40, built on demand (each a squaring of the one before):
+// x^(624 JB) is the product over JB's set bits
+constexpr int kPow2 = 40;
+std::mutex g_pow2_mu;
+const std::vector<u64> &pow2(int k) {
   static std::vector<std::vector<u64>> T;
-  static std::once_flag once;
-  std::call_once(once, [] {
-    std::vector<u64> p(kR, 0), q(kR, 0);
-    // x^624 = x^512 * x^112: times-x steps are cheap enough for this once
+  std::lock_guard<std::mutex> g(g_pow2_mu);
+  if (T.empty()) {
+    T.reserve(kPow2);  // no reallocation: references handed out stay valid
+    std::vector<u64> p(kR, 0);
     p[0] = 1;
-    for (int s = 0; s < kN; ++s) {
+    for (int s = 0; s < kN; ++s) {  // x^624 by times-x steps
       u64 carry = 0;
       for (int i = 0; i < kR; ++i) {
         const u64 v = p[i];
         p[i] = (v << 1) | carry;
         carry = v >> 63;
       }
-      if ((p[kR - 1] >> (kDeg - 64 * (kR - 1))) & 1u) {
-        const Barrett &B = barrett();
-        for (int i = 0; i < kR; ++i) p[i] ^= B.phi[i];
-      }
+      if ((p[kR - 1] >> (kDeg - 64 * (kR - 1))) & 1u)
+        for (int i = 0; i < kR; ++i) p[i] ^= kPhiWords[i];
     }
-    for (int k = 0; k < 40; ++k) {
-      T.push_back(p);
-      sqrmod_fast(p.data(), q.data());
-      p.swap(q);
-    }
-  });
-  return T;
+    T.push_back(p);
+  }
+  while (static_cast<int>(T.size()) <= k) {
+    std::vector<u64> q(kR, 0);
+    sqrmod_fast(T.back().data(), q.data());
+    T.push_back(q);
+  }
+  return T[static_cast<size_t>(k)];
 }
 
 // r = r^2 mod phi (deg r < kDeg)
@@ -341,11 +366,10 @@ void narrow(const std::vector<uint64_t> &p, u64 *r) {
 // the cached x^(624 2^k) over the set bits of J div 624 (a handful of products instead of 64
 // squarings)
 void mt_jump_poly(uint64_t J, std::vector<uint64_t> &out) {
-  if ((J / kN) >> 40) {  // beyond the cached powers (no caller comes near)
+  if ((J / kN) >> kPow2) {  // beyond the cached powers (no caller comes near)
     mt_jump_poly_slow(J, out);
     return;
   }
-  const auto &T = pow2_table();
   const Barrett &B = barrett();
   u64 r[kR] = {}, t[kR];
   r[0] = 1;
@@ -360,9 +384,9 @@ void mt_jump_poly(uint64_t J, std::vector<uint64_t> &out) {
       for (int i = 0; i < kR; ++i) r[i] ^= B.phi[i];
   }
   const uint64_t q = J / kN;
-  for (int k = 0; k < 40; ++k)
+  for (int k = 0; k < kPow2; ++k)
     if ((q >> k) & 1u) {
-      mulmod_fast(r, T[static_cast<size_t>(k)].data(), t);
+      mulmod_fast(r, pow2(k).data(), t);
       std::memcpy(r, t, sizeof(t));
     }
   out = widen(r);
@@ -477,5 +501,14 @@ extern "C" int rs_mt_poly_selftest(int64_t j1, int64_t j2) {
   std::vector<uint64_t> sq = a, sqs;
   rs::mt_poly_square(sq);
   rs::mt_jump_poly_slow(2 * static_cast<uint64_t>(j1), sqs);
-  return (r == c && a == as && b == bs && c == cs && rs_ == cs && sq == sqs) ? 1 : 0;
+  // the embedded phi and mu (mt_phi.h) against Berlekamp-Massey and long division, once
+  static const bool consts_ok = [] {
+    const Poly &bm = charpoly_bm(), &em = charpoly();
+    const Poly mu = barrett_mu_bm(bm);
+    bool ok = true;
+    for (int i = 0; i < kR; ++i) ok = ok && bm[static_cast<size_t>(i)] == em[static_cast<size_t>(i)] &&
+                                      mu[static_cast<size_t>(i)] == kMuWords[i];
+    return ok;
+  }();
+  return (consts_ok && r == c && a == as && b == bs && c == cs && rs_ == cs && sq == sqs) ? 1 : 0;
 }

@@ -24,6 +24,7 @@
 // replay (tests/test_gpu_np_sampler.py).
 #include <hip/hip_runtime.h>
 #include <array>
+#include <chrono>
 #include <memory>
 
 #include <algorithm>
@@ -584,6 +585,12 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
   if (a.resume) {  // the paused list, draw position and wrap count
     m = a.fin_m[c];
     t = a.tpos[c];
+    // (a bound on everything the resume indexes by: a paused chunk's list and position came from
+    // the first launch, a corrupt one fails the parse loudly instead of reading out of range)
+    if (m < 1 || m > n1 || t < 0 || t > T) {
+      if (tid == 0) atomicOr(a.err, 4);
+      return;
+    }
     for (int q = tid; q < m; q += kEntryThreads) {
       const uint32_t x = a.fin[static_cast<size_t>(c) * n1 + q];
       st[q] = static_cast<uint16_t>(x >> 16);
@@ -1517,6 +1524,10 @@ __device__ __forceinline__ void np_track_body(const EntryArgs &a, const uint32_t
   const int T = static_cast<int>(std::min<int64_t>(a.W, a.D - t0));
   int t = a.tpos[c];
   if (t >= T) return;
+  if (t < 0 || m < 1) {  // a corrupt hand-over: fail the parse, index nothing
+    if (threadIdx.x == 0) atomicOr(a.err, 4);
+    return;
+  }
   // (the busy wave is wave q % kTrackWaves for trajectory q; placing the trajectories by the
   // waves' hardware SIMD ids, the two chunks of a CU on opposite SIMDs: no gain, 6.46 vs 6.40 ms
   // at C2 with the SGPRs capped at 70 -- this kernel must stay within ~80 SGPRs, at 84-86 it
@@ -2277,16 +2288,19 @@ struct JumpBits {
 // With the fast arithmetic of mt_jump.cpp a new generator length costs a few ms of host time
 // (x^(624 JB) from cached powers of x^624, then the tree's products).
 constexpr size_t kJumpCache = 8;
+std::mutex g_jump_mu;
+double g_jump_host_ms = 0.0;  // host time spent building level polynomials (rs_np_host_stats)
+int64_t g_jump_builds = 0;
 void jump_bits_cached(int kind, int JB, int levels, JumpBits &out) {
-  static std::mutex mu;
   static std::vector<std::pair<std::array<int, 3>, std::shared_ptr<const JumpBits>>> cache;
-  std::lock_guard<std::mutex> g(mu);
+  std::lock_guard<std::mutex> g(g_jump_mu);
   const std::array<int, 3> key{kind, JB, levels};
   for (auto &e : cache)
     if (e.first == key) {
       out = *e.second;
       return;
     }
+  const auto t0 = std::chrono::steady_clock::now();
   auto jb = std::make_shared<JumpBits>();
   std::vector<uint64_t> p;
   rs::mt_jump_poly(static_cast<uint64_t>(kN) * static_cast<uint64_t>(JB), p);
@@ -2297,23 +2311,28 @@ void jump_bits_cached(int kind, int JB, int levels, JumpBits &out) {
       jb->add(p);
     }
   } else {
-    // radix R: level k's multipliers m = 1 .. R-1 are x^(m R^k J), index k (R-1) + m - 1
+    // radix R: level k's multipliers m = 1 .. R-1 are x^(m R^k J), index k (R-1) + m - 1;
+    // even powers by squaring (cheaper than a product): b^2m = (b^m)^2, b^(2m+1) = b^2m b
     for (int k = 0; k < levels; ++k) {
-      const std::vector<uint64_t> base = p;
-      std::vector<uint64_t> q = base, t;
-      for (int m = 1; m < kind; ++m) {
-        if (m > 1) {
-          rs::mt_poly_mulmod(q, base, t);
-          q.swap(t);
+      std::vector<std::vector<uint64_t>> pw(static_cast<size_t>(kind) + 1);
+      pw[1] = p;
+      for (int m = 2; m <= kind; ++m) {
+        if (m % 2 == 0) {
+          pw[static_cast<size_t>(m)] = pw[static_cast<size_t>(m / 2)];
+          rs::mt_poly_square(pw[static_cast<size_t>(m)]);
+        } else {
+          rs::mt_poly_mulmod(pw[static_cast<size_t>(m - 1)], pw[1], pw[static_cast<size_t>(m)]);
         }
-        jb->add(q);
       }
-      rs::mt_poly_mulmod(q, base, p);  // x^(R^(k+1) J)
+      for (int m = 1; m < kind; ++m) jb->add(pw[static_cast<size_t>(m)]);
+      p = pw[static_cast<size_t>(kind)];  // x^(R^(k+1) J)
     }
   }
   if (cache.size() >= kJumpCache) cache.erase(cache.begin());
   cache.emplace_back(key, jb);
   out = *jb;
+  g_jump_host_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  ++g_jump_builds;
 }
 
 // Radix-R tree levels (RSAMD_JRADIX, R <= 8): level k sends window g < R^k to g + m R^k
@@ -2412,10 +2431,14 @@ __global__ __launch_bounds__(256) void k_np_starts_local(const uint2 *__restrict
                                                          const int *__restrict__ vcnt,
                                                          const int *__restrict__ off,
                                                          int64_t *__restrict__ starts, int ecap,
-                                                         int W, int lead) {
+                                                         int W, int lead, int64_t scap, int *err) {
   const int c = blockIdx.x;
   const int n = vcnt[c];
   const int64_t base = lead + off[c];
+  if (base + n > scap) {  // more starts than a hypothesis per n1 draws allows: a corrupt log
+    if (threadIdx.x == 0) atomicOr(err, 8);
+    return;
+  }
   for (int i = threadIdx.x; i < n; i += 256)
     starts[base + i] = static_cast<int64_t>(c) * W + ev[static_cast<size_t>(c) * ecap + i].x;
   if (lead && c == 0 && threadIdx.x == 0) starts[0] = 0;
@@ -2593,6 +2616,11 @@ int shard_layout(rs_np_shard &w, int32_t pos, int64_t count) {
   }
   w.nwords = w.Lb * kN - (w.s_lo - w.wbase);
   w.ecap_shift = 0;
+  // host-side bounds of what the kernels index: every chunk's draws (and the straddling
+  // hypothesis's margin) inside the generated words, the first pass inside a generator
+  if (w.Cr * w.Wc + margin > w.nwords || w.Wc > std::numeric_limits<int>::max() / 2 ||
+      (w.xb > 0 && w.xb >= w.JB))
+    return rs::fail(RS_EINVAL, "np shard: segment layout exceeds the generated stream");
   return RS_OK;
 }
 
@@ -2845,7 +2873,8 @@ int shard_enqueue_starts(rs_np_shard &w, int64_t cap, int64_t *got) {
   k_np_scan<<<1, 1024, 0, s>>>(w.d_vcnt, Cr, w.d_off, cap, got);
   HIP_TRY(hipGetLastError());
   k_np_starts_local<<<Cr, 256, 0, s>>>(w.d_ev, w.d_vcnt, w.d_off, w.d_starts, w.ecap,
-                                       static_cast<int>(w.Wc), w.rank == 0 ? 1 : 0);
+                                       static_cast<int>(w.Wc), w.rank == 0 ? 1 : 0, w.cap_starts,
+                                       w.d_err);
   HIP_TRY(hipGetLastError());
   return RS_OK;
 }
@@ -3057,7 +3086,8 @@ int shard_run_local(rs_np_shard &w, uint32_t *key, int32_t *pos, int64_t count, 
     }
     break;
   }
-  if (res.err) return rs::fail(RS_EDEVICE, "np sampler: hypothesis parse mismatch");
+  if (res.err & 2) return rs::fail(RS_EDEVICE, "np sampler: hypothesis parse mismatch");
+  if (res.err) return rs::fail(RS_EDEVICE, "np sampler: corrupt chunk hand-over or start list");
   if (res.got < 1) return rs::fail(RS_EDEVICE, "np sampler: segment holds no complete hypothesis");
   // state after `used` draws: the block holding the last word drawn (rs_mt_jump's convention)
   const int64_t W = *pos + res.used;
@@ -3114,8 +3144,13 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
   }
   rs_np_shard *w = c->np_shard;
   if (w && (w->n != n || w->k != k || w->py != py)) {
-    np_shard_free(c);
-    w = nullptr;
+    // another population (the drop-in's next pair): the session keeps its device buffers,
+    // which only grow, and lays the next segment out for the new n (shard_layout)
+    w->n = n;
+    w->n1 = static_cast<int>(n - 1);
+    w->k = k;
+    w->py = py;
+    w->state = 0;
   }
   int st;
   if (!w) {
@@ -3259,5 +3294,15 @@ extern "C" int rs_np_shard_tuples(rs_np_shard *w, int64_t base, int64_t hi, int6
   if ((st = shard_tuples(*w, base, hi, next_start, final_idx, d, key_out, pos_out))) return st;
   if (cnt > 0)
     HIP_TRY(hipMemcpy(out, d, sizeof(int32_t) * static_cast<size_t>(cnt) * w->k, hipMemcpyDeviceToHost));
+  return RS_OK;
+}
+
+// Host time the parse has spent building MT jump polynomials in this process (first calls at a
+// new generator length), and how many level sets it built.
+extern "C" int rs_np_host_stats(double *jump_ms, int64_t *builds) {
+  if (!jump_ms || !builds) return rs::fail(RS_EINVAL, "rs_np_host_stats: null pointer");
+  std::lock_guard<std::mutex> g(g_jump_mu);
+  *jump_ms = g_jump_host_ms;
+  *builds = g_jump_builds;
   return RS_OK;
 }

@@ -8,7 +8,9 @@
 //                 tau A by 3x3 Jacobi SVD, lambda = 3 tau / tr S, t = lambda b.
 //   k_pnp_count   lane per hypothesis x chunk of `med` points (wave-uniform scalar loads):
 //                 e = |pi(y) - pi(R x + t)|^2 <= thresh, evaluated division-free.
-//   k_pnp_select  one workgroup: first hypothesis with the largest count (strict ">").
+//   k_pnp_select  one workgroup: first hypothesis with the largest count (strict ">"); for the
+//                 P3P branch a mirrored-depth pose only where it clearly out-counts (x2) every
+//                 front-facing one.
 //   k_pnp_inliers consensus sets of the winner on `med` and `high` (reference order).
 //
 // The cv.solvePnPRansac drop-in (rs_pnp_ransac_cv) reuses solve / count with the test in
@@ -386,7 +388,8 @@ constexpr int kP3pSlots = 8;
 __global__ __launch_bounds__(64) void k_pnp_solve_p3p(const PPt *__restrict__ pts, int m, int H,
                                                       int mode, uint64_t seed,
                                                       const int *__restrict__ tuples,
-                                                      double *__restrict__ Psoa, int64_t ld) {
+                                                      double *__restrict__ Psoa, int64_t ld,
+                                                      unsigned char *__restrict__ mirf) {
   const int h = blockIdx.x * blockDim.x + threadIdx.x;
   if (h >= H) return;
   int idx[3];
@@ -419,6 +422,7 @@ __global__ __launch_bounds__(64) void k_pnp_solve_p3p(const PPt *__restrict__ pt
     for (int q = 0; q < 9; ++q) Psoa[q * ld + base + s] = ok ? Rs[s][q] : qn;
 #pragma unroll
     for (int q = 0; q < 3; ++q) Psoa[(9 + q) * ld + base + s] = ok ? ts[s][q] : qn;
+    mirf[base + s] = ok && mir[s] ? 1 : 0;
   }
 }
 
@@ -491,54 +495,69 @@ struct PnpDevResult {
   int64_t inliers[];  // med then high
 };
 
+// (mirf, the P3P branch: each pose's mirrored-depth flag.  A mirrored pose -- all depths
+// negated: the scene behind a positive-scale camera -- reprojects like its front-facing twin,
+// so on a noisy near-planar scene the twin can out-count the true pose by a few points.  The
+// winner is then the first best front-facing pose unless the best mirrored count is more than
+// kMirrorCountWins times it: a negative-scale camera (BAdino2's) has no front-facing fit at all.)
+constexpr int kMirrorCountWins = 2;
+__device__ __forceinline__ void sel_better(int c, int i, int &bm, int &bi) {
+  if (c > bm || (c == bm && i < bi)) {
+    bm = c;
+    bi = i;
+  }
+}
 __global__ __launch_bounds__(1024) void k_pnp_select(const int *__restrict__ counts, int H,
                                                      const double *__restrict__ Psoa,
-                                                     int64_t ld, PnpDevResult *res) {
-  __shared__ int sm[16], si[16];
+                                                     int64_t ld, PnpDevResult *res,
+                                                     const unsigned char *__restrict__ mirf) {
+  __shared__ int sm[2][16], si[2][16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  int bm = 0, bi = 0x7fffffff;
+  int bm[2] = {0, 0}, bi[2] = {0x7fffffff, 0x7fffffff};  // front-facing, mirrored
   // 8 loads in flight per thread before the (order-free) max / first-index comparisons
   for (int i0 = tid; i0 < H; i0 += 8 * 1024) {
-    int c[8];
+    int c[8], f[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int i = i0 + u * 1024;
       c[u] = i < H ? counts[i] : -1;
+      f[u] = mirf && i < H ? mirf[i] : 0;
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int i = i0 + u * 1024;
-      if (c[u] > bm || (c[u] == bm && i < bi)) {
-        bm = c[u];
-        bi = i;
-      }
+      if (f[u]) sel_better(c[u], i, bm[1], bi[1]);
+      else sel_better(c[u], i, bm[0], bi[0]);
     }
   }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const int om = __shfl_xor(bm, o), oi = __shfl_xor(bi, o);
-    if (om > bm || (om == bm && oi < bi)) {
-      bm = om;
-      bi = oi;
+  for (int k = 0; k < 2; ++k) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const int om = __shfl_xor(bm[k], o), oi = __shfl_xor(bi[k], o);
+      sel_better(om, oi, bm[k], bi[k]);
     }
-  }
-  if (lane == 0) {
-    sm[w] = bm;
-    si[w] = bi;
+    if (lane == 0) {
+      sm[k][w] = bm[k];
+      si[k][w] = bi[k];
+    }
   }
   __syncthreads();
   if (tid == 0) {
-    for (int q = 1; q < 16; ++q)
-      if (sm[q] > bm || (sm[q] == bm && si[q] < bi)) {
-        bm = sm[q];
-        bi = si[q];
-      }
+    for (int k = 0; k < 2; ++k)
+      for (int q = 1; q < 16; ++q) sel_better(sm[k][q], si[k][q], bm[k], bi[k]);
+    const int cls = bm[1] > kMirrorCountWins * bm[0] ? 1 : 0;
+    int bm0 = bm[cls], bi0 = bi[cls];
+    if (!mirf) {  // one class: the first largest count over all hypotheses
+      bm0 = bm[0];
+      bi0 = bi[0];
+    }
     // strict ">" against an initial best of 0 (ransac.py:108): zero consensus never wins
-    if (bm > 0) {
-      res->best_index = bi;
-      res->best_count = bm;
-      for (int q = 0; q < 9; ++q) res->R[q] = Psoa[q * ld + bi];
-      for (int q = 0; q < 3; ++q) res->t[q] = Psoa[(9 + q) * ld + bi];
+    if (bm0 > 0) {
+      res->best_index = bi0;
+      res->best_count = bm0;
+      for (int q = 0; q < 9; ++q) res->R[q] = Psoa[q * ld + bi0];
+      for (int q = 0; q < 3; ++q) res->t[q] = Psoa[(9 + q) * ld + bi0];
     } else {
       res->best_index = -1;
       res->best_count = 0;
@@ -992,7 +1011,9 @@ extern "C" int rs_pnp_ransac(rs_ctx *c, const double *X_med, const double *y_med
   const size_t b_tup = align256(sizeof(int) * (mode == RS_SAMPLER_TUPLES ? H * k : 1));
   const size_t b_P = align256(sizeof(double) * 12 * ld), b_cnt = align256(sizeof(int) * ld);
   const size_t b_res = align256(sizeof(rsd::PnpDevResult) + sizeof(int64_t) * (m_med + m_high));
-  int st = rs::ensure_scratch(c, 2 * b_in_m + 2 * b_in_h + b_pm + b_ph + b_tup + b_P + b_cnt + b_res);
+  const size_t b_mir = align256(k == 3 ? static_cast<size_t>(Hm) : 1);
+  int st = rs::ensure_scratch(c, 2 * b_in_m + 2 * b_in_h + b_pm + b_ph + b_tup + b_P + b_cnt + b_res +
+                                     b_mir);
   if (st) return st;
   char *p = static_cast<char *>(c->scratch);
   auto take = [&p](size_t b) {
@@ -1010,6 +1031,7 @@ extern "C" int rs_pnp_ransac(rs_ctx *c, const double *X_med, const double *y_med
   double *dP = reinterpret_cast<double *>(take(b_P));
   int *dcnt = reinterpret_cast<int *>(take(b_cnt));
   auto *dres = reinterpret_cast<rsd::PnpDevResult *>(take(b_res));
+  auto *dmir = reinterpret_cast<unsigned char *>(take(b_mir));  // P3P poses' mirrored flags
   hipStream_t s = c->stream;
   HIP_TRY(hipMemcpyAsync(dXm, X_med, sizeof(double) * 3 * m_med, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(dym, y_med, sizeof(double) * 3 * m_med, hipMemcpyHostToDevice, s));
@@ -1024,7 +1046,7 @@ extern "C" int rs_pnp_ransac(rs_ctx *c, const double *X_med, const double *y_med
   HIP_TRY(hipMemsetAsync(dcnt, 0, sizeof(int) * Hm, s));
   if (k == 3)
     hipLaunchKernelGGL(rsd::k_pnp_solve_p3p, dim3((H + 63) / 64), dim3(64), 0, s, ph,
-                       static_cast<int>(m_high), static_cast<int>(H), mode, seed, dtup, dP, ld);
+                       static_cast<int>(m_high), static_cast<int>(H), mode, seed, dtup, dP, ld, dmir);
   else
     hipLaunchKernelGGL(rsd::k_pnp_solve, dim3((H + 255) / 256), dim3(256), 0, s, ph,
                        static_cast<int>(m_high), static_cast<int>(H), k, mode, seed, dtup, dP,
@@ -1040,7 +1062,7 @@ extern "C" int rs_pnp_ransac(rs_ctx *c, const double *X_med, const double *y_med
                      static_cast<int>(nch), thresh, rsd::PxMetric{1.0, 0.0, 1.0}, dcnt);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(rsd::k_pnp_select, dim3(1), dim3(1024), 0, s, dcnt, static_cast<int>(Hm), dP,
-                     ld, dres);
+                     ld, dres, k == 3 ? static_cast<const unsigned char *>(dmir) : nullptr);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(rsd::k_pnp_inliers, dim3(1), dim3(1024), 0, s, pm, static_cast<int>(m_med),
                      ph, static_cast<int>(m_high), thresh, dres);

@@ -77,6 +77,7 @@ _SIGS = {
     "rs_py_shuffle_tuples_gpu": (C.c_int, [C.c_void_p, _u32p, _i32p, C.c_int64, C.c_int32,
                                            C.c_int64, _i32p]),
     "rs_mt_jump": (C.c_int, [_u32p, C.c_int32, C.c_int64, _u32p, _i32p]),
+    "rs_np_host_stats": (C.c_int, [C.POINTER(C.c_double), _i64p]),
     "rs_mt_poly_selftest": (C.c_int, [C.c_int64, C.c_int64]),
     "rs_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "rs_ctx_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
@@ -335,6 +336,13 @@ def py_shuffle_tuples_gpu(key, pos, n, k, count, ctx=None):
     check(lib().rs_py_shuffle_tuples_gpu(ctx.handle, ptr(key, C.c_uint32), C.byref(p), int(n),
                                          int(k), int(count), ptr(out, C.c_int32)))
     return out, key, p.value
+
+
+def np_host_stats():
+    """(host ms spent building MT jump polynomials in this process, level sets built)."""
+    ms, n = C.c_double(0.0), C.c_int64(0)
+    check(lib().rs_np_host_stats(C.byref(ms), C.byref(n)))
+    return ms.value, n.value
 
 
 def mt_jump(key, pos, steps):
