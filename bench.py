@@ -227,7 +227,7 @@ def _best_of(f, reps):
     return best, out
 
 
-def extras(ctx, rank, world, dist, comm):
+def extras(ctx, rank, world, dist, comm):  # noqa: C901
     """The other BASELINE.json configs and the stages after the RANSAC loop, measured on the
     same box (not the headline): C3 PnP, C5 stress, C4 ring (sharded over all ranks, RCCL
     all-gather), the gold standard and the getFFromLabCode drop-in end to end."""
@@ -268,12 +268,39 @@ def extras(ctx, rank, world, dist, comm):
     try:
         X, _, y, _, _, _ = synth.pnp_scene(500, 0.30, seed=3)
         thr = (1.5 / 800.0) ** 2
-        run = lambda: ransac.ransac_pnp(X, y, X, y, 50_000, thr, 6, sampler="philox", seed=11)
+        run = lambda: ransac.ransac_pnp(X, y, X, y, 50_000, thr, 6, sampler="philox", seed=11,
+                                        ctx=ctx)
         run()
         el, r = _best_of(run, 5)
+        # W_P(M) = 27 M + 37 000 flop per hypothesis (the 12 x 12 DLT null
+        # space 37 000, scoring 27 per point, ransac.py:93-105); kernel times by HIP events on
+        # the context stream around the solve and the count launches, best of 5 timed calls
+        _ffi.pnp_timing(ctx, 1)
+        ks, kc = [], []
+        for _ in range(5):
+            run()
+            a, b = _ffi.pnp_timing(ctx, 1)
+            ks.append(a)
+            kc.append(b)
+        _ffi.pnp_timing(ctx, 0)
+        Hc, Mc = 50_000, 500
+        fs, fc = 37_000.0 * Hc, 27.0 * Mc * Hc
+        s_ms, c_ms3 = min(ks), min(kc)
+        dom = ("k_pnp_solve", fs, s_ms) if s_ms >= c_ms3 else ("k_pnp_count", fc, c_ms3)
+        ach = dom[1] / (dom[2] * 1e-3) / 1e12
         out["c3_pnp"] = {"metric": "PnP-DLT RANSAC hypotheses/s", "value": 50_000 / el,
                          "ms": el * 1e3, "points": 500, "hypotheses": 50_000,
-                         "consensus": int(r[5])}
+                         "consensus": int(r[5]),
+                         "roofline": {"bound": "valu (fp64)", "kernel": dom[0],
+                                      "achieved": ach, "peak": PEAK_FP64_VALU_TFLOPS,
+                                      "unit": "TFLOP/s", "frac": ach / PEAK_FP64_VALU_TFLOPS,
+                                      "kernels_ms": {"k_pnp_solve": s_ms, "k_pnp_count": c_ms3},
+                                      "flop_per_hypothesis": {"solve": 37_000, "count": 27 * Mc,
+                                                              "total": 37_000 + 27 * Mc},
+                                      "whole_call_tflops": (fs + fc) / el / 1e12,
+                                      "note": "SURVEY.md 8(d) W_P(M) = 27 M + 37 000 flop per "
+                                              "hypothesis; HIP events on the context stream, "
+                                              "best of 5 calls"}}
         import random
         runp = lambda: ransac.ransac_pnp(X, y, X, y, 50_000, thr, 6, sampler="exact",
                                          rng=random.Random(0))

@@ -266,6 +266,9 @@ int rs_pnp_dlt(rs_ctx *ctx, const double *X, const double *y, int64_t m, double 
  * (pnp.py:132-160).  k = 3: the reference's p3p branch (ransac.py:81-82, 91-111), Lambda
  * Twist P3P with every pose of a trial scored (trial-major, pose-minor first occurrence;
  * best_index is the trial).  Replaces ransac.ransac_robust's loop (ransac.py:72-111). */
+/* HIP events around rs_pnp_ransac's solve and count kernels (ransac.py:93-105's work): enable = 1
+ * records them in the following calls; returns the last timed call's milliseconds (-1: none). */
+int rs_pnp_timing(rs_ctx *ctx, int32_t enable, double *solve_ms, double *count_ms);
 int rs_pnp_ransac(rs_ctx *ctx, const double *X_med, const double *y_med, int64_t m_med,
                   const double *X_high, const double *y_high, int64_t m_high, int32_t k,
                   int64_t H, int32_t mode, uint64_t seed, const int32_t *host_tuples,

@@ -99,6 +99,8 @@ extern "C" int rs_ctx_destroy(rs_ctx *c) {
   if (c->np_plan) rs_f8_plan_destroy(c->np_plan);
   rs::np_shard_free(c);
   if (c->scratch) (void)hipFree(c->scratch);
+  for (auto &e : c->pnp_ev)
+    if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return RS_OK;

@@ -16,6 +16,10 @@ struct rs_ctx {
   void *comm = nullptr;        // ncclComm_t
   void *comm_buf = nullptr;    // device staging for collectives
   size_t comm_buf_bytes = 0;
+  // rs_pnp_timing: HIP events around the PnP-RANSAC solve and count kernels of the next calls
+  int pnp_timing = 0;
+  hipEvent_t pnp_ev[3] = {};
+  double pnp_solve_ms = -1.0, pnp_count_ms = -1.0;
 };
 
 namespace rs {

@@ -251,6 +251,11 @@ __device__ __forceinline__ void group_done_max(int *counts, int *gdone, int *sta
   if ((threadIdx.x & 63) == 0 && v > 0) atomicMax(&status[0], v);
 }
 
+#ifndef RSAMD_COUNT_LDS
+#define RSAMD_COUNT_LDS 1  // per-workgroup group sums in LDS, one count atomic per group (A/B: 0)
+#endif
+constexpr int kCountGrpSlots = 8;  // hypothesis groups a workgroup sums in LDS (more: direct)
+
 typedef float f2q __attribute__((ext_vector_type(2)));
 // v_pk_mul_f32 with a broadcast half of a VGPR pair (OPSEL / OPSELHI pick, per result lane,
 // the half of each source).
@@ -332,6 +337,22 @@ __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ p
   const int64_t total = static_cast<int64_t>((H + 63) >> 6) * npad;
   int64_t pos = w * per_wave;
   const int64_t end = min(total, pos + per_wave);
+#if RSAMD_COUNT_LDS
+  // The workgroup's slices are consecutive, so they cover a few hypothesis groups (two at C2):
+  // their partial counts are summed in LDS, and the workgroup's last wave to finish adds each
+  // group's 64 counts to HBM once and folds the group's completion (gdone, c*).  One 256-B
+  // count atomic per workgroup and group instead of one per slice segment (WRITE_SIZE per C2
+  // launch 3.99 MB for 0.4 MB of counts, profiles/r04k_pmc_k_f8_count.json); no barrier: the
+  // finished waves never wait for the slow ones.
+  __shared__ int s_cnt[kCountGrpSlots * 64];
+  __shared__ int s_len[kCountGrpSlots];
+  __shared__ int s_fin;
+  const int g0 = static_cast<int>(min(total - 1, bslot * (BT / 64) * per_wave) / npad);
+  for (int x = threadIdx.x; x < kCountGrpSlots * 64; x += BT) s_cnt[x] = 0;
+  if (threadIdx.x < kCountGrpSlots) s_len[threadIdx.x] = 0;
+  if (threadIdx.x == 0) s_fin = 0;
+  __syncthreads();
+#endif
   uint64_t *ts = g_count_ts;  // diagnostic wave timeline (RSAMD_TSTAMP), null in production
   const uint64_t t_start = ts ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const uint64_t c_start = ts ? __builtin_amdgcn_s_memtime() : 0ull;  // shader clock
@@ -382,9 +403,38 @@ __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ p
         }
       }
     }
+#if RSAMD_COUNT_LDS
+    if (grp - g0 < kCountGrpSlots) {
+      atomicAdd(&s_cnt[(grp - g0) * 64 + lane], cnt);
+      if (lane == 0) atomicAdd(&s_len[grp - g0], p1 - p0);
+      continue;
+    }
+#endif
     if (h < H) atomicAdd(&counts[h], cnt);
     if (gdone) group_done_max(counts, gdone, status, grp, p1 - p0, npad, h, H);
   }
+#if RSAMD_COUNT_LDS
+  {
+    // the last wave of the workgroup (its LDS adds, and every other wave's, are complete:
+    // workgroup-scope acquire-release on the finish counter) flushes the group sums
+    int last = 0;
+    if (lane == 0)
+      last = __hip_atomic_fetch_add(&s_fin, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) ==
+             BT / 64 - 1;
+    last = __shfl(last, 0);
+    if (last) {
+      for (int k = 0; k < kCountGrpSlots; ++k) {
+        const int len = __hip_atomic_load(&s_len[k], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (len == 0) continue;  // wave-uniform (an LDS word)
+        const int grp = g0 + k, h = grp * 64 + lane;
+        const int c = __hip_atomic_load(&s_cnt[k * 64 + lane], __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (h < H) atomicAdd(&counts[h], c);
+        if (gdone) group_done_max(counts, gdone, status, grp, len, npad, h, H);
+      }
+    }
+  }
+#endif
   if (ts && lane == 0) {
     uint64_t *o = ts + kCountTsWords * w;
     o[0] = t_start;

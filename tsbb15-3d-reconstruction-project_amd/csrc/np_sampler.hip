@@ -133,7 +133,10 @@ constexpr int kRFast = 8;                    // slots per thread of the branch-f
 // kernel's list capacity (a template argument, <= 8 per wave of its 16).  The
 // one-slot dense path costs ~N per draw and chunk, so large N hands over earlier: measured
 // (probe, C2 / N = 10 000): 64 -> 6.40 / 36.6 ms, 128 -> 6.48 / 34.2 ms.
-__host__ __device__ constexpr int hand_of(int n1) { return n1 >= 4096 ? 128 : 64; }
+#ifndef RSAMD_HAND_SMALL
+#define RSAMD_HAND_SMALL 64  // hand-over list for N - 1 < 4096 (A/B builds: 128)
+#endif
+__host__ __device__ constexpr int hand_of(int n1) { return n1 >= 4096 ? 128 : RSAMD_HAND_SMALL; }
 
 constexpr uint32_t kSentinel = 0x80000000u;  // an empty slot: never reaches 0 within kW steps
 
@@ -1215,6 +1218,9 @@ __device__ __forceinline__ uint64_t rej_fixed_point_aa1(uint32_t w, uint32_t bas
 #ifndef RSAMD_MULTI_FP
 #define RSAMD_MULTI_FP rej_fixed_point_aa  // multi-trajectory blocks (A/B: rej_fixed_point_aa1)
 #endif
+#ifndef RSAMD_SINGLE_FP
+#define RSAMD_SINGLE_FP rej_fixed_point_aa  // one-per-wave blocks (A/B: rej_fixed_point_aa1)
+#endif
 // add + popcount(r) on the vector unit: the mask comes from a vector compare, so the count never
 // takes the vector -> scalar -> vector round trip (s_bcnt1 then a VGPR operand: ~20 cycles more
 // per window, tools/ubench/lat_bench.hip).  The s_nop pair covers the SGPR read after the VALU
@@ -1363,7 +1369,7 @@ __device__ __forceinline__ uint32_t track_one(const EntryArgs &a, const uint32_t
           if (k < kf) {
             const uint32_t w = q[k];
             q[k] = sw[(d - t + 64 * (kAhead + k) + lane) & (kCheck - 1)];
-            base = vbcnt_add(rej_fixed_point_aa(w, base, M2), base - 64u);
+            base = vbcnt_add(RSAMD_SINGLE_FP(w, base, M2), base - 64u);
           }
         }
         i = uni(base);  // lane 0's base is i

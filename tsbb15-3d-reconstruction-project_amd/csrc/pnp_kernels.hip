@@ -1044,6 +1044,8 @@ extern "C" int rs_pnp_ransac(rs_ctx *c, const double *X_med, const double *y_med
   hipLaunchKernelGGL(rsd::k_pack_ppts, dim3((m_high + 255) / 256), dim3(256), 0, s, dXh, dyh,
                      static_cast<int>(m_high), ph);
   HIP_TRY(hipMemsetAsync(dcnt, 0, sizeof(int) * Hm, s));
+  const bool timed = c->pnp_timing != 0;
+  if (timed) HIP_TRY(hipEventRecord(c->pnp_ev[0], s));
   if (k == 3)
     hipLaunchKernelGGL(rsd::k_pnp_solve_p3p, dim3((H + 63) / 64), dim3(64), 0, s, ph,
                        static_cast<int>(m_high), static_cast<int>(H), mode, seed, dtup, dP, ld, dmir);
@@ -1052,6 +1054,7 @@ extern "C" int rs_pnp_ransac(rs_ctx *c, const double *X_med, const double *y_med
                        static_cast<int>(m_high), static_cast<int>(H), k, mode, seed, dtup, dP,
                        ld, 0);
   HIP_TRY(hipGetLastError());
+  if (timed) HIP_TRY(hipEventRecord(c->pnp_ev[1], s));
   const int64_t groups = (Hm + 63) / 64;
   int64_t nch = std::max<int64_t>(1, std::min<int64_t>((8192 + groups - 1) / groups, (m_med + 63) / 64));
   const int chunk = static_cast<int>((m_med + nch - 1) / nch);
@@ -1061,6 +1064,7 @@ extern "C" int rs_pnp_ransac(rs_ctx *c, const double *X_med, const double *y_med
                      static_cast<int>(m_med), static_cast<int>(Hm), dP, ld, chunk,
                      static_cast<int>(nch), thresh, rsd::PxMetric{1.0, 0.0, 1.0}, dcnt);
   HIP_TRY(hipGetLastError());
+  if (timed) HIP_TRY(hipEventRecord(c->pnp_ev[2], s));
   hipLaunchKernelGGL(rsd::k_pnp_select, dim3(1), dim3(1024), 0, s, dcnt, static_cast<int>(Hm), dP,
                      ld, dres, k == 3 ? static_cast<const unsigned char *>(dmir) : nullptr);
   HIP_TRY(hipGetLastError());
@@ -1070,6 +1074,13 @@ extern "C" int rs_pnp_ransac(rs_ctx *c, const double *X_med, const double *y_med
   std::vector<char> host(sizeof(rsd::PnpDevResult) + sizeof(int64_t) * (m_med + m_high));
   HIP_TRY(hipMemcpyAsync(host.data(), dres, host.size(), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  if (timed) {
+    float a = 0.f, b = 0.f;
+    HIP_TRY(hipEventElapsedTime(&a, c->pnp_ev[0], c->pnp_ev[1]));
+    HIP_TRY(hipEventElapsedTime(&b, c->pnp_ev[1], c->pnp_ev[2]));
+    c->pnp_solve_ms = a;
+    c->pnp_count_ms = b;
+  }
   const auto *r = reinterpret_cast<const rsd::PnpDevResult *>(host.data());
   std::memcpy(out->R, r->R, sizeof(out->R));
   std::memcpy(out->t, r->t, sizeof(out->t));
@@ -1259,5 +1270,19 @@ extern "C" int rs_pnp_refine_lm(rs_ctx *c, const double *X, const double *uv, in
   std::memcpy(R_io, io, sizeof(double) * 9);
   std::memcpy(t_io, io + 9, sizeof(double) * 3);
   if (cost_out) std::memcpy(cost_out, io + 12, sizeof(double) * 4);
+  return RS_OK;
+}
+
+// HIP events around the solve and the count kernel of rs_pnp_ransac (the bench's C3 roofline):
+// enable = 1 records them in the following calls (0 stops); returns the last call's times
+// (-1 before any timed call).  No reference counterpart (ransac.py:93-105 is the loop timed).
+extern "C" int rs_pnp_timing(rs_ctx *c, int32_t enable, double *solve_ms, double *count_ms) {
+  if (!c || !solve_ms || !count_ms) return fail(RS_EINVAL, "null pointer");
+  HIP_TRY(hipSetDevice(c->device));
+  if (enable && !c->pnp_ev[0])
+    for (auto &e : c->pnp_ev) HIP_TRY(hipEventCreate(&e));
+  c->pnp_timing = enable ? 1 : 0;
+  *solve_ms = c->pnp_solve_ms;
+  *count_ms = c->pnp_count_ms;
   return RS_OK;
 }

@@ -78,6 +78,8 @@ _SIGS = {
                                            C.c_int64, _i32p]),
     "rs_mt_jump": (C.c_int, [_u32p, C.c_int32, C.c_int64, _u32p, _i32p]),
     "rs_np_host_stats": (C.c_int, [C.POINTER(C.c_double), _i64p]),
+    "rs_pnp_timing": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_double),
+                                C.POINTER(C.c_double)]),
     "rs_mt_poly_selftest": (C.c_int, [C.c_int64, C.c_int64]),
     "rs_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "rs_ctx_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
@@ -336,6 +338,14 @@ def py_shuffle_tuples_gpu(key, pos, n, k, count, ctx=None):
     check(lib().rs_py_shuffle_tuples_gpu(ctx.handle, ptr(key, C.c_uint32), C.byref(p), int(n),
                                          int(k), int(count), ptr(out, C.c_int32)))
     return out, key, p.value
+
+
+def pnp_timing(ctx, enable):
+    """Enable / disable HIP events around rs_pnp_ransac's kernels; returns the last timed call's
+    (solve_ms, count_ms), -1 when none."""
+    a, b = C.c_double(0.0), C.c_double(0.0)
+    check(lib().rs_pnp_timing(ctx.handle, int(enable), C.byref(a), C.byref(b)))
+    return a.value, b.value
 
 
 def np_host_stats():
