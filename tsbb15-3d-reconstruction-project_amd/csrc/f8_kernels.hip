@@ -255,6 +255,13 @@ __device__ __forceinline__ void group_done_max(int *counts, int *gdone, int *sta
 #define RSAMD_COUNT_LDS 1  // per-workgroup group sums in LDS, one count atomic per group (A/B: 0)
 #endif
 constexpr int kCountGrpSlots = 8;  // hypothesis groups a workgroup sums in LDS (more: direct)
+#ifndef RSAMD_COUNT_BT
+#define RSAMD_COUNT_BT 256  // threads per counting workgroup (A/B: 512)
+#endif
+constexpr int kCountBT = RSAMD_COUNT_BT;
+#ifndef RSAMD_RETEST_LANES
+#define RSAMD_RETEST_LANES 1  // float64 re-test loads by the ambiguous lanes only (A/B: 0)
+#endif
 
 typedef float f2q __attribute__((ext_vector_type(2)));
 // v_pk_mul_f32 with a broadcast half of a VGPR pair (OPSEL / OPSELHI pick, per result lane,
@@ -395,11 +402,19 @@ __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ p
           // the opaque pointer keeps these loads (and their 18 VGPRs) inside the rare branch
           const double *fp = Fsoa + hl;
           asm volatile("" : "+v"(fp));
+#if RSAMD_RETEST_LANES
+          // only the ambiguous lanes fetch their float64 model (a 128-B line of each row holds
+          // 16 hypotheses: a re-test touches the lines of its lanes, not all 36 of the group)
+          if (((a0 | a1) >> lane) & 1ull) {
+#endif
           double fdd[9];
 #pragma unroll
           for (int k = 0; k < 9; ++k) fdd[k] = fp[k * ld];
           if ((a0 >> lane) & 1ull) cnt += test64(fdd, pts[i + 2 * j], g.thr2_px) ? 1 : 0;
           if ((a1 >> lane) & 1ull) cnt += test64(fdd, pts[i + 2 * j + 1], g.thr2_px) ? 1 : 0;
+#if RSAMD_RETEST_LANES
+          }
+#endif
         }
       }
     }
@@ -1041,7 +1056,7 @@ Count32qShape count32q_shape(int n, int H, int waves, int slices_per_wave) {
   per = (per + 7) / 8 * 8;
   W = (total + per - 1) / per;
   sh.per_wave = per;
-  sh.blocks = (W + 3) / 4;
+  sh.blocks = (W + kCountBT / 64 - 1) / (kCountBT / 64);
   return sh;
 }
 
@@ -1049,7 +1064,7 @@ hipError_t launch_f8_count32q(const float4 *ptsq, const Pt *pts, int n, int H,
                               const float *F32soa, const double *Fsoa, int64_t ld,
                               const Count32qShape &sh, const GuardW &g, int *counts,
                               hipStream_t s, int *gdone, int *status, const float4 *G4) {
-  hipLaunchKernelGGL((k_f8_count32q<256>), dim3(static_cast<unsigned>(sh.blocks)), dim3(256), 0,
+  hipLaunchKernelGGL((k_f8_count32q<kCountBT>), dim3(static_cast<unsigned>(sh.blocks)), dim3(kCountBT), 0,
                      s, ptsq, pts, n, H, F32soa, Fsoa, ld, sh.per_wave, g, counts, gdone, status,
                      G4);
   return hipGetLastError();

@@ -1205,7 +1205,7 @@ __device__ __forceinline__ uint64_t rej_fixed_point_aa(uint32_t w, uint32_t base
 }
 // The same fixed point checked after every round: fewer vector instructions per window where
 // the waves are issue-bound (the multi-trajectory phase) rather than latency-bound
-__device__ __forceinline__ uint64_t rej_fixed_point_aa1(uint32_t w, uint32_t base, uint32_t M2) {
+[[maybe_unused]] __device__ __forceinline__ uint64_t rej_fixed_point_aa1(uint32_t w, uint32_t base, uint32_t M2) {
   uint64_t r = __ballot((w & (base | M2)) > base), rn;
   for (;;) {
     const uint32_t sl = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(r >> 32),
@@ -1965,6 +1965,12 @@ __host__ __device__ constexpr int64_t tup_lds_bytes(int n1) {
 #define RSAMD_TUP_AHEAD 6
 #endif
 constexpr int kTupAhead = RSAMD_TUP_AHEAD;
+#ifndef RSAMD_TUP_BLOCK2
+#define RSAMD_TUP_BLOCK2 1  // two-window blocks with a VGPR state (A/B: 0)
+#endif
+#ifndef RSAMD_TUP_FP
+#define RSAMD_TUP_FP rej_fixed_point_aa  // (A/B: rej_fixed_point_aa1)
+#endif
 
 
 template <bool PY>
@@ -2020,6 +2026,16 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
     __builtin_amdgcn_wave_barrier();
     uint64_t bad = __ballot(st && F[fi] > sl);
     for (int r = 0; bad && r < 64; ++r) {  // each round settles at least one lane
+      if ((bad >> l) & 1ull) F[fi] = static_cast<uint16_t>(sl);
+      __builtin_amdgcn_wave_barrier();
+      bad = __ballot(st && F[fi] > sl);
+    }
+  };
+  // the read-back alone, for stores already made (rare path: a partner value twice in a window)
+  [[maybe_unused]] auto fstore_fix = [&](bool st, uint32_t fi, uint32_t sl) {
+    __builtin_amdgcn_wave_barrier();
+    uint64_t bad = __ballot(st && F[fi] > sl);
+    for (int r = 0; bad && r < 64; ++r) {
       if ((bad >> l) & 1ull) F[fi] = static_cast<uint16_t>(sl);
       __builtin_amdgcn_wave_barrier();
       bad = __ballot(st && F[fi] > sl);
@@ -2156,6 +2172,51 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
 #pragma unroll
     for (int q = 0; q < kTupAhead; ++q) {
       while (o + 64 <= filled) {
+#if RSAMD_TUP_BLOCK2 && RSAMD_TUPF && RSAMD_REJFP
+        if constexpr (!PY) {
+          // Two windows under one two-bucket test (all 128 states at least the lower bucket's
+          // lowest), the state per lane in a VGPR advanced by v_bcnt (as the tracking kernel's
+          // blocks), both windows' stores checked by one read-back: the scalar unit, not the
+          // vector unit, bounded the window-by-window form (PMC: SALU 1.97e8 per C2 launch).
+          uint32_t iv;
+          asm volatile("v_mov_b32 %0, %1" : "=v"(iv) : "s"(i));
+          const uint32_t cz = static_cast<uint32_t>(__builtin_clz(iv));
+          if (o + 128 <= filled &&
+              __ballot(static_cast<int>(iv) - 127 >= static_cast<int>(0x40000000u >> cz)) != 0ull) {
+            const uint32_t M2 = 0x7fffffffu >> cz;
+            uint32_t base = iv - static_cast<uint32_t>(l);
+            const uint32_t wd0 = ring[(o + l) & (kTupRing - 1)];
+            const uint32_t wd1 = ring[(o + 64 + l) & (kTupRing - 1)];
+            const uint64_t r0 = RSAMD_TUP_FP(wd0, base, M2);
+            const uint32_t sl0 = __builtin_amdgcn_mbcnt_hi(
+                static_cast<uint32_t>(r0 >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(r0), base));
+            const uint32_t v0 = wd0 & (sl0 | M2);
+            const bool st0 = v0 < sl0;
+            const uint32_t fi0 = st0 ? v0 : jdummy;
+            F[fi0] = static_cast<uint16_t>(sl0);
+            base = vbcnt_add(r0, base - 64u);
+            const uint64_t r1 = RSAMD_TUP_FP(wd1, base, M2);
+            const uint32_t sl1 = __builtin_amdgcn_mbcnt_hi(
+                static_cast<uint32_t>(r1 >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(r1), base));
+            const uint32_t v1 = wd1 & (sl1 | M2);
+            const bool st1 = v1 < sl1;
+            const uint32_t fi1 = st1 ? v1 : jdummy;
+            F[fi1] = static_cast<uint16_t>(sl1);
+            base = vbcnt_add(r1, base - 64u);
+            __builtin_amdgcn_wave_barrier();
+            // a later (smaller) state of window 1 may already have replaced window 0's entry: the
+            // check is F <= sl, and a fix only ever lowers an entry
+            const uint32_t c0 = F[fi0], c1 = F[fi1];
+            if (__ballot((st0 && c0 > sl0) || (st1 && c1 > sl1))) {
+              fstore_fix(st0, fi0, sl0);
+              fstore_fix(st1, fi1, sl1);
+            }
+            i = __builtin_amdgcn_readfirstlane(base);  // lane 0's base is i
+            o += 128;
+            continue;
+          }
+        }
+#endif
         if (window2()) continue;
         window();
         if (i == 0) goto parsed;
