@@ -32,7 +32,7 @@
 //   k_e5_select  c* = the largest count; among the slots with c* the smallest residual norm
 //                ||d||, d_i = max(|r1_i|, |r2_i|) over all points (the quantity the
 //                reference's F loop compares on ties, fun.py:317-325), first slot on equal norms.
-//   k_e5_inliers one workgroup: the winner's consensus set in point order.
+//                Then, in the same launch, the winner's consensus set in point order.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -262,22 +262,38 @@ __device__ __forceinline__ void e5_polys(const double (&Bm)[6][10], E5Polys &P, 
 // The solution of one root z of d (Newton-polished on the real axis): (x, y, 1) = the row cross
 // product of [k; l; m](z) with the largest third component (first on ties), E = x X + y Y +
 // z Z + W from the null basis in memory, unit norm.  False when it degenerates.
-__device__ __forceinline__ bool e5_solution(const E5Polys &P, const double (&d)[11], double z,
-                                            const double *bas, int64_t ldb, double (&E)[9]) {
-  double dp[10];  // derivative, ascending
+// (d and the rows' polynomials read from memory, pg = k_e5_polys' column of the sample with
+// stride ldp: the kernel's register peak was the 50 doubles held at once)
+template <int N>
+__device__ __forceinline__ double horner_mem(const double *p, int64_t ld, double z) {
+  double q[N];
 #pragma unroll
-  for (int i = 0; i < 10; ++i) dp[i] = (i + 1) * d[i + 1];
+  for (int i = 0; i < N; ++i) q[i] = p[i * ld];
+  return horner_asc(q, z);
+}
+__device__ __forceinline__ bool e5_solution(const double *pg, int64_t ldp, double z,
+                                            const double *bas, int64_t ldb, double (&E)[9]) {
+  double d[11];
+#pragma unroll
+  for (int i = 0; i < 11; ++i) d[i] = pg[i * ldp];
   // Newton polish on the real axis (the complex iteration may stop at its rounding floor)
   for (int it = 0; it < 3; ++it) {
-    const double f = horner_asc(d, z), fp = horner_asc(dp, z);
+    double fp = 10 * d[10];  // the derivative, ascending (i + 1) d[i + 1], by Horner
+#pragma unroll
+    for (int i = 8; i >= 0; --i) fp = fma(fp, z, (i + 1) * d[i + 1]);
+    const double f = horner_asc(d, z);
     if (!(fp != 0.0)) break;
     const double step = f / fp;
     if (!(fabs(step) <= 1e-3 * fmax(1.0, fabs(z)))) break;
     z -= step;
   }
-  const double A0[3] = {horner_asc(P.kx, z), horner_asc(P.ky, z), horner_asc(P.k1, z)};
-  const double A1[3] = {horner_asc(P.lx, z), horner_asc(P.ly, z), horner_asc(P.l1, z)};
-  const double A2[3] = {horner_asc(P.mx, z), horner_asc(P.my, z), horner_asc(P.m1, z)};
+  const double *P = pg + 11 * ldp;  // kx ky k1 lx ly l1 mx my m1: 4 4 5 4 4 5 4 4 5 doubles
+  const double A0[3] = {horner_mem<4>(P, ldp, z), horner_mem<4>(P + 4 * ldp, ldp, z),
+                        horner_mem<5>(P + 8 * ldp, ldp, z)};
+  const double A1[3] = {horner_mem<4>(P + 13 * ldp, ldp, z), horner_mem<4>(P + 17 * ldp, ldp, z),
+                        horner_mem<5>(P + 21 * ldp, ldp, z)};
+  const double A2[3] = {horner_mem<4>(P + 26 * ldp, ldp, z), horner_mem<4>(P + 30 * ldp, ldp, z),
+                        horner_mem<5>(P + 34 * ldp, ldp, z)};
   double v0 = 0.0, v1 = 0.0, v2 = 0.0, bz = -1.0;
   auto cand = [&](const double (&a)[3], const double (&b)[3]) {
     const double c0 = a[1] * b[2] - a[2] * b[1];
@@ -357,6 +373,9 @@ struct E5Args {
   // stores coalesce over its lanes): the 10 x 20 system (200 x ldw), the null basis
   // (36 x ldw), B's rows 4..9 (60 x ldw), Gauss-Jordan success (ldw)
   double *Mg, *Bas, *Bg;
+  // d(z) and the three rows' polynomials per sample (k_e5_polys; 50 x ldw: d ascending, then
+  // kx ky k1 lx ly l1 mx my m1 as in E5Polys), in Mg's space once Gauss-Jordan is done
+  double *Pg;
   int *okg;
   int64_t ldw;
   // two-phase root finding (k_e5_roots): after `split` sweeps the samples whose roots are still
@@ -478,6 +497,30 @@ __global__ __launch_bounds__(64) void k_e5_gj(E5Args a) {
   if (own && j == 0) a.okg[s] = ok ? 1 : 0;
 }
 
+// (B') lane per sample: the rows' polynomials and d(z) = det [k; l; m] once per sample (the
+// root kernel's 16 lanes of a sample computed them twice each: 32 copies, and B's 60 rows
+// were its register peak)
+static_assert(sizeof(E5Polys) == 39 * sizeof(double), "E5Polys is 39 packed doubles");
+__global__ __launch_bounds__(64) void k_e5_polys(E5Args a) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= a.S) return;
+  double Bm[6][10];
+  const double *bg = a.Bg + s;
+#pragma unroll
+  for (int rr = 0; rr < 6; ++rr)
+#pragma unroll
+    for (int q = 0; q < 10; ++q) Bm[rr][q] = bg[(10 * rr + q) * a.ldw];
+  E5Polys P;
+  double d[11];
+  e5_polys(Bm, P, d);
+  double *o = a.Pg + s;
+#pragma unroll
+  for (int i = 0; i < 11; ++i) o[i * a.ldw] = d[i];
+  const double *pp = P.kx;
+#pragma unroll
+  for (int j = 0; j < 39; ++j) o[(11 + j) * a.ldw] = pp[j];
+}
+
 // (C) 16 lanes per sample (a DPP row), lane r owns root r: the degree-10 polynomial of B's rows
 // 4..9 (every lane of the row), its roots by Aberth-Ehrlich with the Newton-polygon start points
 // of twoview_math.h aberth_roots (same start points, Horner steps and freeze tests, but every
@@ -493,6 +536,9 @@ __global__ __launch_bounds__(64) void k_e5_gj(E5Args a) {
 // phase 2, which resumes them from their saved roots packed densely (rows never interact --
 // the sweep reads only its own row, converged roots stay frozen -- so the roots, and every
 // solution, are the same as one phase's).
+#ifdef RSAMD_DIAG
+__device__ int *g_e5_stats = nullptr;  // per sample: row sweeps, wave sweeps, degree, ok, am[11]
+#endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSD_E5_ROOTS_WAVES))) void k_e5_roots(E5Args a, int phase) {
   const int r = threadIdx.x & 15;
   const int row_id = blockIdx.x * (blockDim.x >> 4) + (threadIdx.x >> 4);
@@ -506,17 +552,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSD_E5_ROOT
   }
   const int sc = live ? s : a.S - 1;
   const bool ok = live && a.okg[sc];
-  double Bm[6][10];
-  const double *bg = a.Bg + sc;
-#pragma unroll
-  for (int rr = 0; rr < 6; ++rr)
-#pragma unroll
-    for (int q = 0; q < 10; ++q) Bm[rr][q] = bg[(10 * rr + q) * a.ldw];
+  const double *pg = a.Pg + sc;  // d, then the rows' polynomials (k_e5_polys)
   double d[11];
-  {
-    E5Polys P;
-    e5_polys(Bm, P, d);
-  }
+#pragma unroll
+  for (int i = 0; i < 11; ++i) d[i] = pg[i * a.ldw];
   // monic descending coefficients padded to degree 10: zero roots (trailing zeros of the
   // ascending d) shifted out, leading zeros kept (they add exact zeros in Horner)
   double g[11];
@@ -550,13 +589,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSD_E5_ROOT
   // start point of root r: edge e of the Newton polygon (upper hull of (k, log |b_k|), b_k =
   // am[10 - k]) with m = k2 - k1 points on |z| = (|b_k1| / |b_k2|)^(1/m)
   double zr = __builtin_nan(""), zi = __builtin_nan("");
-  if (r < deg) {
-    double lg[11];
+  // log |b_k| by lane k of the row, read across the row (one log per lane instead of eleven)
+  double lgl;
+  {
+    double bk = am[0];
 #pragma unroll
-    for (int k = 0; k < 11; ++k) {
-      const double v = fabs(am[10 - k]);
-      lg[k] = v > 0.0 ? log(v) : -1.0e300;
-    }
+    for (int k = 1; k < 11; ++k) bk = r == k ? am[10 - k] : bk;
+    bk = r == 0 ? am[10] : bk;
+    const double v = fabs(bk);
+    lgl = v > 0.0 && r < 11 ? log(v) : -1.0e300;
+  }
+  double lg[11];
+#pragma unroll
+  for (int k = 0; k < 11; ++k) lg[k] = __shfl(lgl, k, 16);
+  if (r < deg) {
     int hull[11], nh = 0;
     hull[nh++] = 0;
     for (int k = 1; k <= deg; ++k) {
@@ -593,7 +639,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSD_E5_ROOT
     conv = !live || zs[2] != 0.0;
     it0 = a.split;
   }
+#ifdef RSAMD_DIAG
+  int row_done = -1, wave_it = it0;  // sweeps until this row converged / the wave stopped
+  const uint64_t rowmask = 0xffffull << (threadIdx.x & 48);
+#endif
   for (int it = it0; it < it1; ++it) {
+#ifdef RSAMD_DIAG
+    if (row_done < 0 && !(__ballot(!conv) & rowmask)) row_done = it;
+    wave_it = it + 1;
+#endif
     if (!__ballot(!conv)) break;  // wave-uniform: every row keeps sweeping while one root moves
     double sr = 0.0, si = 0.0;  // sum_{j != r} 1 / (z_r - z_j), the previous sweep's z_j
     aberth_sum<1>(zr, zi, sr, si);
@@ -646,21 +700,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RSD_E5_ROOT
       return;
     }
   }
+#ifdef RSAMD_DIAG
+  if (g_e5_stats && live && r == 0) {
+    int *o = g_e5_stats + 26 * static_cast<int64_t>(s);
+    o[0] = row_done < 0 ? wave_it : row_done;
+    o[1] = wave_it;
+    o[2] = deg;
+    o[3] = ok ? 1 : 0;
+    double *od = reinterpret_cast<double *>(o + 4);  // the monic descending coefficients
+#pragma unroll
+    for (int i = 0; i < 11; ++i) od[i] = am[i];
+  }
+#endif
   // lane r's solution: real iterated roots (|Im| <= 1e-6 max(1, |Re|)) and the zero roots
   double E[9];
   bool valid = false;
   if (ok && r < deg + trailing && (r >= deg || fabs(zi) <= 1e-6 * fmax(1.0, fabs(zr)))) {
-    // the row polynomials again, from memory (not kept live through the sweeps)
-    const double *bg2 = bg;
-    asm volatile("" : "+v"(bg2));
-#pragma unroll
-    for (int rr = 0; rr < 6; ++rr)
-#pragma unroll
-      for (int q = 0; q < 10; ++q) Bm[rr][q] = bg2[(10 * rr + q) * a.ldw];
-    E5Polys P;
-    double d2[11];
-    e5_polys(Bm, P, d2);
-    valid = e5_solution(P, d2, r < deg ? zr : 0.0, a.Bas + sc, a.ldw, E);
+    // d and the rows' polynomials from memory (not kept live through the sweeps)
+    const double *pg2 = pg;
+    asm volatile("" : "+v"(pg2));
+    valid = e5_solution(pg2, a.ldw, r < deg ? zr : 0.0, a.Bas + sc, a.ldw, E);
   }
   const uint64_t row = 0xffffull << (threadIdx.x & 48);
   const uint64_t vb = __ballot(valid) & row;
@@ -729,9 +788,11 @@ constexpr int kPackSamples = 256, kPackInline = 128;
 __global__ __launch_bounds__(kPackSamples) void k_e5_pack(const int *__restrict__ nsol, int S,
                                                           const int *__restrict__ bbase,
                                                           int *__restrict__ slot_of,
-                                                          int *__restrict__ hc) {
+                                                          int *__restrict__ hc,
+                                                          int *__restrict__ zero2) {
   __shared__ int sw[kPackSamples / 64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (zero2 && blockIdx.x == 0 && tid < 2) zero2[tid] = 0;  // c* and the candidate count
   const int b0 = blockIdx.x * kPackSamples;  // a multiple of 4: int4 loads below b0
   int pre = 0;
   if (bbase) {
@@ -770,14 +831,19 @@ __global__ __launch_bounds__(kPackSamples) void k_e5_pack(const int *__restrict_
 // The counting models of the real solutions (dense index h -> slot): the float64 F for the
 // guard re-test (Fd) and the fp32 unit-frame model with its decision constants (f32_model, as
 // the F-RANSAC solve writes them)
-__global__ __launch_bounds__(256) void k_e5_models(const int *__restrict__ slot_of, int Hc,
+__global__ __launch_bounds__(256) void k_e5_models(const int *__restrict__ slot_of,
+                                                   const int *__restrict__ hc,
                                                    const double *__restrict__ Fsoa, int64_t ld,
                                                    Frame fr, double gT, double gDe, double gDn,
                                                    double *__restrict__ Fd,
                                                    float *__restrict__ F32soa,
-                                                   float4 *__restrict__ G4) {
+                                                   float4 *__restrict__ G4,
+                                                   int *__restrict__ counts,
+                                                   int *__restrict__ gdone) {
   const int h = blockIdx.x * blockDim.x + threadIdx.x;
-  if (h >= Hc) return;
+  if (h >= *hc) return;  // (the grid covers every slot: the real-solution count is on the device)
+  counts[h] = 0;         // (the counting kernel adds into the first *hc counts only)
+  if ((h & 63) == 0) gdone[h >> 6] = 0;  // its groups' completion counters (c* on the fly)
   const int64_t slot = slot_of[h];
   double F[9];
 #pragma unroll
@@ -860,6 +926,31 @@ __global__ __launch_bounds__(256) void k_e5_cands(const int *__restrict__ counts
 // sequential one, so two candidates whose norms differ by a few ulp can rank differently
 // from a numpy restatement; the E path has no reference counterpart (SURVEY a-15), so the
 // tie-break is deterministic but unpinned at that level.
+// ||d||^2 of the model at f (stride ld) over the points, by one wave (lanes over the points,
+// a fixed butterfly)
+__device__ __forceinline__ double e5_norm_wave(const Pt *__restrict__ pts, int n,
+                                               const double *__restrict__ fp, int64_t ld) {
+  const int lane = threadIdx.x & 63;
+  double f[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) f[q] = fp[q * ld];
+  double ss = 0.0;
+  for (int i = lane; i < n; i += 64) {
+    const Pt p = pts[i];
+    const double l10 = fma(f[0], p.x2, fma(f[1], p.y2, f[2]));
+    const double l11 = fma(f[3], p.x2, fma(f[4], p.y2, f[5]));
+    const double l12 = fma(f[6], p.x2, fma(f[7], p.y2, f[8]));
+    const double l20 = fma(f[0], p.x1, fma(f[3], p.y1, f[6]));
+    const double l21 = fma(f[1], p.x1, fma(f[4], p.y1, f[7]));
+    const double e = fabs(fma(l10, p.x1, fma(l11, p.y1, l12)));
+    const double d = fmax(e / sqrt(fma(l10, l10, l11 * l11)), e / sqrt(fma(l20, l20, l21 * l21)));
+    ss = fma(d, d, ss);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+  return ss;
+}
+
 __global__ __launch_bounds__(256) void k_e5_norms(const Pt *__restrict__ pts, int n,
                                                   const int *__restrict__ cand,
                                                   const int *__restrict__ ncand,
@@ -870,29 +961,50 @@ __global__ __launch_bounds__(256) void k_e5_norms(const Pt *__restrict__ pts, in
   const int nw = static_cast<int>(gridDim.x) * (blockDim.x >> 6);
   const int nc = *ncand;
   for (int k = static_cast<int>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6); k < nc; k += nw) {
-    const int64_t h = slot_of[cand[k]];  // dense index -> slot
-    double f[9];
-#pragma unroll
-    for (int q = 0; q < 9; ++q) f[q] = Fsoa[q * ld + h];
-    double ss = 0.0;
-    for (int i = lane; i < n; i += 64) {
-      const Pt p = pts[i];
-      const double l10 = fma(f[0], p.x2, fma(f[1], p.y2, f[2]));
-      const double l11 = fma(f[3], p.x2, fma(f[4], p.y2, f[5]));
-      const double l12 = fma(f[6], p.x2, fma(f[7], p.y2, f[8]));
-      const double l20 = fma(f[0], p.x1, fma(f[3], p.y1, f[6]));
-      const double l21 = fma(f[1], p.x1, fma(f[4], p.y1, f[7]));
-      const double e = fabs(fma(l10, p.x1, fma(l11, p.y1, l12)));
-      const double d = fmax(e / sqrt(fma(l10, l10, l11 * l11)), e / sqrt(fma(l20, l20, l21 * l21)));
-      ss = fma(d, d, ss);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+    const double ss = e5_norm_wave(pts, n, Fsoa + slot_of[cand[k]], ld);  // dense index -> slot
     if (lane == 0) norms[k] = ss == ss ? ss : __builtin_inf();
   }
 }
 
-// the winner among the candidates: the smallest norm, the smallest slot on equal norms
+// k_e5_cands and k_e5_norms in one launch (c* from the counting kernel's group completion):
+// a wave per 64 counts, and for each count equal to c* its slot appended and its norm by the
+// same wave
+__global__ __launch_bounds__(256) void k_e5_cand_norms(const int *__restrict__ counts, int64_t H,
+                                                       const int *__restrict__ hc,
+                                                       const int *__restrict__ cmax,
+                                                       int *__restrict__ cand,
+                                                       int *__restrict__ ncand,
+                                                       const Pt *__restrict__ pts, int n,
+                                                       const int *__restrict__ slot_of,
+                                                       const double *__restrict__ Fsoa, int64_t ld,
+                                                       double *__restrict__ norms) {
+  const int c = *cmax;
+  if (c <= 0) return;
+  H = hc ? min<int64_t>(H, *hc) : H;
+  const int lane = threadIdx.x & 63;
+  const int64_t nwv = static_cast<int64_t>(gridDim.x) * (blockDim.x >> 6);
+  for (int64_t b = (static_cast<int64_t>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64;
+       b < H; b += nwv * 64) {
+    const int64_t h = b + lane;
+    uint64_t bal = __ballot(h < H && counts[h] == c);
+    while (bal) {
+      const int f = __ffsll(static_cast<long long>(bal)) - 1;
+      bal &= bal - 1ull;
+      int k = 0;
+      if (lane == 0) k = atomicAdd(ncand, 1);
+      k = __shfl(k, 0);
+      if (lane == 0) cand[k] = static_cast<int>(b + f);
+      const double ss = e5_norm_wave(pts, n, Fsoa + slot_of[b + f], ld);
+      if (lane == 0) norms[k] = ss == ss ? ss : __builtin_inf();
+    }
+  }
+}
+
+__device__ __forceinline__ void e5_inliers_body(const Pt *__restrict__ pts, int n, double thr2,
+                                                E5DevResult *res);
+
+// the winner among the candidates: the smallest norm, the smallest slot on equal norms; then
+// its inlier list (e5_inliers_body)
 __global__ __launch_bounds__(1024) void k_e5_select(const double *__restrict__ norms,
                                                     const int *__restrict__ cand,
                                                     const int *__restrict__ ncand,
@@ -900,7 +1012,8 @@ __global__ __launch_bounds__(1024) void k_e5_select(const double *__restrict__ n
                                                     const int *__restrict__ slot_of,
                                                     const double *__restrict__ Esoa,
                                                     const double *__restrict__ Fsoa, int64_t ld,
-                                                    E5DevResult *res) {
+                                                    E5DevResult *res, const Pt *__restrict__ pts,
+                                                    int n, double thr2) {
   __shared__ double sv[16];
   __shared__ int64_t si[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -945,10 +1058,13 @@ __global__ __launch_bounds__(1024) void k_e5_select(const double *__restrict__ n
       res->F[q] = ok ? Fsoa[q * ld + slot] : 0.0;
     }
   }
+  // the winner's inlier list in the same launch (thread 0's record is visible after the barrier)
+  __syncthreads();
+  e5_inliers_body(pts, n, thr2, res);
 }
 
-__global__ __launch_bounds__(1024) void k_e5_inliers(const Pt *__restrict__ pts, int n,
-                                                     double thr2, E5DevResult *res) {
+__device__ __forceinline__ void e5_inliers_body(const Pt *__restrict__ pts, int n, double thr2,
+                                                E5DevResult *res) {
   __shared__ int woff[16];
   __shared__ int base_s;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1048,6 +1164,9 @@ static int launch_e5_solve(rsd::E5Args &a, char *work, hipStream_t s) {
   hipLaunchKernelGGL(rsd::k_e5_build, dim3((S + 63) / 64), dim3(64), 0, s, a);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(rsd::k_e5_gj, dim3((S + 1) / 2), dim3(64), 0, s, a);
+  HIP_TRY(hipGetLastError());
+  a.Pg = a.Mg;  // the 10 x 20 systems are dead after Gauss-Jordan (200 >= 50 doubles per sample)
+  hipLaunchKernelGGL(rsd::k_e5_polys, dim3((S + 63) / 64), dim3(64), 0, s, a);
   HIP_TRY(hipGetLastError());
   if (a.split > 0) {
     HIP_TRY(hipMemsetAsync(a.defer_n, 0, sizeof(int), s));
@@ -1152,7 +1271,7 @@ extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64
   const size_t bF32 = e5_align(sizeof(float) * 9 * ld), bG4 = e5_align(sizeof(float4) * ld);
   int st = rs::ensure_scratch(c, 2 * bin + bp + 3 * bE + bc + br + bnorm + 256 + bpq + bF32 + bG4 +
                                      2 * e5_align(sizeof(int) * ld) + 2 * e5_align(sizeof(int) * S) +
-                                     e5_work_bytes(S));
+                                     e5_align(sizeof(int) * (ld / 64 + 1)) + e5_work_bytes(S));
   if (st) return st;
   char *ptr = static_cast<char *>(c->scratch);
   auto take = [&ptr](size_t b) {
@@ -1173,6 +1292,7 @@ extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64
   int *dnsol = reinterpret_cast<int *>(take(e5_align(sizeof(int) * S)));
   int *dslot = reinterpret_cast<int *>(take(e5_align(sizeof(int) * ld)));
   int *doff = reinterpret_cast<int *>(take(e5_align(sizeof(int) * S)));  // workgroup bases
+  int *dgdone = reinterpret_cast<int *>(take(e5_align(sizeof(int) * (ld / 64 + 1))));  // per group
   // fp32 counting: point-pair layout, dense float64 / fp32 models, decision constants
   auto *dpq = reinterpret_cast<float4 *>(take(bpq));
   double *dFd = reinterpret_cast<double *>(take(bE));
@@ -1182,14 +1302,13 @@ extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64
   hipStream_t s = c->stream;
   HIP_TRY(hipMemcpyAsync(d1, p1, sizeof(double) * 2 * n, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(d2, p2, sizeof(double) * 2 * n, hipMemcpyHostToDevice, s));
-  HIP_TRY(rsd::launch_pack_points(d1, d2, static_cast<int>(n), dp, s));
   // counting in fp32 with the float64 guard band (k_f8_count32q, the F-RANSAC product kernel:
   // counts identical to the float64 test's) unless the points give no unit frame
   rsd::Frame fr{};
   // (RSAMD_E5_FP64=1, a test hook: the plain float64 kernel, for the equal-counts test)
   const char *f64 = std::getenv("RSAMD_E5_FP64");
   const bool fp32 = rsd::unit_frame(p1, p2, n, fr) && !(f64 && f64[0] == '1');
-  if (fp32) HIP_TRY(rsd::launch_pack_points32q(dp, static_cast<int>(n), fr, dpq, s));
+  HIP_TRY(rsd::launch_pack_points_both(d1, d2, static_cast<int>(n), dp, fp32 ? &fr : nullptr, dpq, s));
   a.pts = dp;
   a.n = static_cast<int>(n);
   a.S = static_cast<int>(S);
@@ -1200,6 +1319,24 @@ extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64
   a.nsol = dnsol;
   a.ld = ld;
   if ((st = launch_e5_solve(a, work, s))) return st;
+#ifdef RSAMD_DIAG
+  if (const char *path = std::getenv("RSAMD_E5_STATS")) {  // diagnostic builds: sweep counts
+    int *dst = nullptr;
+    HIP_TRY(hipMalloc(&dst, sizeof(int) * 26 * S));
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(rsd::g_e5_stats), &dst, sizeof(dst)));
+    if ((st = launch_e5_solve(a, work, s))) return st;
+    std::vector<int> h(static_cast<size_t>(26 * S));
+    HIP_TRY(hipMemcpyAsync(h.data(), dst, sizeof(int) * h.size(), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    int *np = nullptr;
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(rsd::g_e5_stats), &np, sizeof(np)));
+    HIP_TRY(hipFree(dst));
+    if (FILE *f = std::fopen(path, "wb")) {
+      std::fwrite(h.data(), sizeof(int), h.size(), f);
+      std::fclose(f);
+    }
+  }
+#endif
   // only the real solutions are counted: the map dslot (dense index -> slot, *hc entries)
   const int npack = static_cast<int>((S + rsd::kPackSamples - 1) / rsd::kPackSamples);
   int *dbsum = nullptr;
@@ -1210,21 +1347,22 @@ extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64
     hipLaunchKernelGGL(rsd::k_e5_bscan, dim3(1), dim3(1024), 0, s, dbsum, npack);
   }
   hipLaunchKernelGGL(rsd::k_e5_pack, dim3(npack), dim3(rsd::kPackSamples), 0, s, dnsol,
-                     static_cast<int>(S), dbsum, dslot, dcmax + 2);
+                     static_cast<int>(S), dbsum, dslot, dcmax + 2, dcmax);
   if (fp32) {
-    // the launch shape of k_f8_count32q needs the number of real solutions on the host
-    int Hc = 0;
-    HIP_TRY(hipMemcpyAsync(&Hc, dcmax + 2, sizeof(int), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    if (Hc > 0) {
-      const rsd::Bounds gb = rsd::fp32_bounds(fr, thresh);
-      hipLaunchKernelGGL(rsd::k_e5_models, dim3((Hc + 255) / 256), dim3(256), 0, s, dslot, Hc, dF,
-                         ld, fr, gb.thr2, gb.De, gb.Dn, dFd, dF32, dG4);
-      HIP_TRY(hipMemsetAsync(dc, 0, sizeof(int) * Hc, s));
-      const rsd::Count32qShape sh = rsd::count32q_shape(static_cast<int>(n), Hc, kE5CountWaves);
-      HIP_TRY(rsd::launch_f8_count32q(dpq, dp, static_cast<int>(n), Hc, dF32, dFd, ld, sh,
-                                      rsd::GuardW{thresh * thresh}, dc, s, nullptr, nullptr, dG4));
-    }
+    // the real solutions' count stays on the device: the models kernel and the counting kernel
+    // are sized for every slot and read it (no host round trip between the solve and the count)
+    const rsd::Bounds gb = rsd::fp32_bounds(fr, thresh);
+    hipLaunchKernelGGL(rsd::k_e5_models, dim3(static_cast<unsigned>((H + 255) / 256)), dim3(256), 0, s,
+                       dslot, dcmax + 2, dF, ld, fr, gb.thr2, gb.De, gb.Dn, dFd, dF32, dG4, dc, dgdone);
+    static const int slices = [] {  // RSAMD_E5_SLICES: slices per resident wave (A/B)
+      const char *e = std::getenv("RSAMD_E5_SLICES");
+      return e ? std::atoi(e) : 0;
+    }();
+    const rsd::Count32qShape sh =
+        rsd::count32q_shape(static_cast<int>(n), static_cast<int>(H), kE5CountWaves, slices);
+    HIP_TRY(rsd::launch_f8_count32q(dpq, dp, static_cast<int>(n), static_cast<int>(H), dF32, dFd, ld, sh,
+                                    rsd::GuardW{thresh * thresh}, dc, s, dgdone, dcmax, dG4,
+                                    dcmax + 2));  // (c* into dcmax[0] as groups complete)
   } else {
     HIP_TRY(hipMemsetAsync(dc, 0, sizeof(int) * H, s));
     // chunking of k_f8_count: >= 8 units of work per SIMD, chunks of >= 64 points (sized for
@@ -1235,18 +1373,20 @@ extern "C" int rs_e5_ransac(rs_ctx *c, const double *p1, const double *p2, int64
     HIP_TRY(rsd::launch_f8_count(dp, static_cast<int>(n), static_cast<int>(H), dF, ld, chunk,
                                  thresh * thresh, dc, s, dcmax + 2, dslot));
   }
-  HIP_TRY(hipMemsetAsync(dcmax, 0, 2 * sizeof(int), s));
-  hipLaunchKernelGGL(rsd::k_e5_max, dim3(static_cast<unsigned>(std::min<int64_t>((H + 255) / 256, 64))),
-                     dim3(256), 0, s, dc, H, dcmax + 2, dcmax);
-  hipLaunchKernelGGL(rsd::k_e5_cands, dim3(static_cast<unsigned>(std::min<int64_t>((H + 255) / 256, 1024))),
-                     dim3(256), 0, s, dc, H, dcmax + 2, dcmax, dcand, dcmax + 1);
-  hipLaunchKernelGGL(rsd::k_e5_norms, dim3(256), dim3(256), 0, s, dp, static_cast<int>(n), dcand,
-                     dcmax + 1, dslot, dF, ld, dnorm);
+  if (fp32) {  // c* is in dcmax[0] already
+    hipLaunchKernelGGL(rsd::k_e5_cand_norms, dim3(256), dim3(256), 0, s, dc, H, dcmax + 2, dcmax, dcand,
+                       dcmax + 1, dp, static_cast<int>(n), dslot, dF, ld, dnorm);
+  } else {
+    hipLaunchKernelGGL(rsd::k_e5_max, dim3(static_cast<unsigned>(std::min<int64_t>((H + 255) / 256, 64))),
+                       dim3(256), 0, s, dc, H, dcmax + 2, dcmax);
+    hipLaunchKernelGGL(rsd::k_e5_cands, dim3(static_cast<unsigned>(std::min<int64_t>((H + 255) / 256, 1024))),
+                       dim3(256), 0, s, dc, H, dcmax + 2, dcmax, dcand, dcmax + 1);
+    hipLaunchKernelGGL(rsd::k_e5_norms, dim3(256), dim3(256), 0, s, dp, static_cast<int>(n), dcand,
+                       dcmax + 1, dslot, dF, ld, dnorm);
+  }
+  // (the selection and the winner's inlier list: one single-workgroup launch)
   hipLaunchKernelGGL(rsd::k_e5_select, dim3(1), dim3(1024), 0, s, dnorm, dcand, dcmax + 1, dcmax,
-                     dslot, dE, dF, ld, dr);
-  HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(rsd::k_e5_inliers, dim3(1), dim3(1024), 0, s, dp, static_cast<int>(n),
-                     thresh * thresh, dr);
+                     dslot, dE, dF, ld, dr, dp, static_cast<int>(n), thresh * thresh);
   HIP_TRY(hipGetLastError());
   std::vector<char> host(sizeof(rsd::E5DevResult) + sizeof(int64_t) * n);
   HIP_TRY(hipMemcpyAsync(host.data(), dr, host.size(), hipMemcpyDeviceToHost, s));

@@ -96,10 +96,14 @@ struct Bounds {
 Bounds fp32_bounds(const Frame &fr, double thresh);
 bool unit_frame(const double *p1, const double *p2, int64_t n, Frame &fr);
 Count32qShape count32q_shape(int n, int H, int waves, int slices_per_wave = 0);
+// pts (and with fr the point-pair layout ptsq) from the (2, n) arrays in one launch
+hipError_t launch_pack_points_both(const double *p1, const double *p2, int n, Pt *pts,
+                                   const Frame *fr, float4 *ptsq, hipStream_t s);
 hipError_t launch_f8_count32q(const float4 *ptsq, const Pt *pts, int n, int H,
                               const float *F32soa, const double *Fsoa, int64_t ld,
                               const Count32qShape &sh, const GuardW &g, int *counts,
-                              hipStream_t s, int *gdone, int *status, const float4 *G4);
+                              hipStream_t s, int *gdone, int *status, const float4 *G4,
+                              const int *Hdev = nullptr);
 hipError_t launch_f8_count(const Pt *pts, int n, int H, const double *Fsoa, int64_t ld,
                            int chunk, double thr2, int *counts, hipStream_t s,
                            const int *Hdev = nullptr, const int *Hmap = nullptr);

@@ -328,7 +328,8 @@ __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ p
                                                      int *__restrict__ counts,
                                                      int *__restrict__ gdone,
                                                      int *__restrict__ status,
-                                                     const float4 *__restrict__ G4) {
+                                                     const float4 *__restrict__ G4,
+                                                     const int *__restrict__ Hdev) {
 #pragma clang fp contract(off)
   typedef float f2 __attribute__((ext_vector_type(2)));
   const int lane = threadIdx.x & 63;
@@ -341,6 +342,15 @@ __global__ __launch_bounds__(BT) void k_f8_count32q(const float4 *__restrict__ p
   const int bslot = xc * xq + min(xc, xr) + (bx >> 3);
   const int64_t w = wave_uniform(bslot * (BT / 64) + (threadIdx.x >> 6));
   const int npad = (n + 7) / 8 * 8;
+  if (Hdev) {
+    // the hypothesis count on the device (at most H, the bound the grid was sized for): the
+    // slice length from it as count32q_shape would, so no host round trip before the launch
+    H = min(H, *Hdev);
+    const int64_t tot = static_cast<int64_t>((H + 63) >> 6) * npad;
+    if (tot == 0) return;  // uniform over the grid, before any barrier
+    const int64_t Wd = max<int64_t>(1, min<int64_t>(static_cast<int64_t>(nb) * (BT / 64), tot / 64));
+    per_wave = ((tot + Wd - 1) / Wd + 7) / 8 * 8;
+  }
   const int64_t total = static_cast<int64_t>((H + 63) >> 6) * npad;
   int64_t pos = w * per_wave;
   const int64_t end = min(total, pos + per_wave);
@@ -937,6 +947,37 @@ __global__ __launch_bounds__(256) void k_pack_points(const double *__restrict__ 
   pts[i] = p;
 }
 
+// both layouts in one launch (the E-RANSAC path: a launch fewer): pts as k_pack_points, and
+// when fr is given the point-pair layout as k_pack_points32q, from the same doubles
+__global__ __launch_bounds__(256) void k_pack_points_both(const double *__restrict__ p1,
+                                                          const double *__restrict__ p2, int n,
+                                                          Pt *__restrict__ pts, bool q, Frame fr,
+                                                          float *__restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ((n + 7) & ~7)) return;
+  float *o = out + 32 * (i >> 3) + (i & 7);
+  if (i >= n) {
+    if (q) {
+      const float qn = __builtin_nanf("");
+      o[0] = o[8] = o[16] = o[24] = qn;
+    }
+    return;
+  }
+  Pt p;
+  p.x1 = p1[i];
+  p.y1 = p1[n + i];
+  p.x2 = p2[i];
+  p.y2 = p2[n + i];
+  pts[i] = p;
+  if (q) {
+    const double is = 1.0 / fr.s;
+    o[0] = static_cast<float>((p.x2 - fr.cx2) * is);
+    o[8] = static_cast<float>((p.y2 - fr.cy2) * is);
+    o[16] = static_cast<float>((p.x1 - fr.cx1) * is);
+    o[24] = static_cast<float>((p.y1 - fr.cy1) * is);
+  }
+}
+
 }  // namespace rsd
 
 // ------------------------------------------------------------------------------------------
@@ -985,6 +1026,13 @@ hipError_t launch_f8_count(const Pt *pts, int n, int H, const double *Fsoa, int6
 
 hipError_t set_count_timeline(uint64_t *buf) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_count_ts), &buf, sizeof(buf));
+}
+
+hipError_t launch_pack_points_both(const double *p1, const double *p2, int n, Pt *pts,
+                                   const Frame *fr, float4 *ptsq, hipStream_t s) {
+  hipLaunchKernelGGL(k_pack_points_both, dim3((n + 7 + 255) / 256), dim3(256), 0, s, p1, p2, n, pts,
+                     fr != nullptr, fr ? *fr : Frame{}, reinterpret_cast<float *>(ptsq));
+  return hipGetLastError();
 }
 
 hipError_t launch_pack_points32q(const Pt *pts, int n, const Frame &fr, float4 *ptsq,
@@ -1063,10 +1111,11 @@ Count32qShape count32q_shape(int n, int H, int waves, int slices_per_wave) {
 hipError_t launch_f8_count32q(const float4 *ptsq, const Pt *pts, int n, int H,
                               const float *F32soa, const double *Fsoa, int64_t ld,
                               const Count32qShape &sh, const GuardW &g, int *counts,
-                              hipStream_t s, int *gdone, int *status, const float4 *G4) {
+                              hipStream_t s, int *gdone, int *status, const float4 *G4,
+                              const int *Hdev) {
   hipLaunchKernelGGL((k_f8_count32q<kCountBT>), dim3(static_cast<unsigned>(sh.blocks)), dim3(kCountBT), 0,
                      s, ptsq, pts, n, H, F32soa, Fsoa, ld, sh.per_wave, g, counts, gdone, status,
-                     G4);
+                     G4, Hdev);
   return hipGetLastError();
 }
 
