@@ -171,3 +171,28 @@ def test_dino_ring_pipeline_poses(ctx):
         worst_t = max(worst_t, np.abs(tab["t"][k] + tt / np.linalg.norm(tt)).max())
         assert tab["gs_cost"][k] < 1e-12
     assert worst_R < 1e-6 and worst_t < 1e-6, (worst_R, worst_t)
+
+
+def test_dino_ring_array_path_matches_object_path(ctx):
+    """run_pairs' array path (many_arrays / arrays: concatenated points, column-wise records)
+    gives the same table as the per-pair object path (many / __call__), field for field."""
+    z = golden("dino_pnp_kat.npz")
+    pairs = _dino_pairs()
+    solver = parallel.GpuPairBatchSolver(ctx, 1000)
+    refiner = parallel.GpuPairRefiner(ctx, z["K_last"])
+
+    class ObjSolver:  # the object path only
+        def __init__(self, inner):
+            self.many = inner.many
+
+    class ObjRefiner:
+        def __init__(self, inner):
+            self.inner = inner
+
+        def __call__(self, items):
+            return self.inner(items)
+
+    fast = parallel.run_pairs(_Solo(), pairs, 1000, solver, refine=refiner)
+    slow = parallel.run_pairs(_Solo(), pairs, 1000, ObjSolver(solver), refine=ObjRefiner(refiner))
+    for f in parallel.PAIR_DTYPE.names:
+        assert np.array_equal(fast[f], slow[f], equal_nan=fast[f].dtype.kind == "f"), f

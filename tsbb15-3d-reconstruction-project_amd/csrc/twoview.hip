@@ -237,31 +237,80 @@ __global__ __launch_bounds__(128) void k_fmatrix_from_cameras(const double *__re
 // ----------------------------------------------------------------------------------------
 // Gold standard (fun.py:336-369), one workgroup per pair.
 // ----------------------------------------------------------------------------------------
-constexpr int kGsT = 256;
-constexpr int kGsW = kGsT / 64;
+#ifndef RSAMD_GS_T
+#define RSAMD_GS_T 256  // threads per pair (A/B: 64; r05c4a: 463 vs 561 us per C4 launch)
+#endif
+constexpr int kGsT = RSAMD_GS_T;
 constexpr int kPerPt = 45;  // W (12x3), V (3x3 upper: 6), gx (3)
 
 // Index of (r, c), r <= c, in a packed upper-triangular 12x12.
 __device__ __forceinline__ int up12(int r, int c) { return r * 12 - (r * (r - 1)) / 2 + (c - r); }
 
-template <int K>
+// One halving step of a wave's reduce-scatter: lanes with bit o set keep the upper half of x
+// and send the lower half to lane ^ o (the others the reverse), each adding what it receives.
+template <int N>
+__device__ __forceinline__ void rs_halve(const double (&x)[N], double (&y)[N / 2], int o) {
+  const bool up = (threadIdx.x & o) != 0;
+#pragma unroll
+  for (int i = 0; i < N / 2; ++i) {
+    const double send = up ? x[i] : x[i + N / 2];
+    const double keep = up ? x[i + N / 2] : x[i];
+    y[i] = keep + __shfl_xor(send, o);
+  }
+}
+
+// Sum over the workgroup's T threads of K values per thread into out[0..K) (LDS).  Large K: a
+// reduce-scatter inside each wave (six halving exchanges of the values padded to 128: 126
+// exchanges instead of a 6-step butterfly per value, 6 K), lane l ending with the wave's sums
+// of values 2 l and 2 l + 1; then the waves' partial sums added in wave order.
+template <int K, int T>
 __device__ __forceinline__ void block_reduce(double (&v)[K], double *scratch, double *out) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if constexpr (K > 16) {
+    static_assert(K <= 128, "reduce-scatter holds 128 values");
+    double x[128], a[64], b[32], c[16], d[8], e[4], f[2];
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    double x = v[k];
+    for (int k = 0; k < 128; ++k) x[k] = k < K ? v[k] : 0.0;
+    rs_halve<128>(x, a, 32);
+    rs_halve<64>(a, b, 16);
+    rs_halve<32>(b, c, 8);
+    rs_halve<16>(c, d, 4);
+    rs_halve<8>(d, e, 2);
+    rs_halve<4>(e, f, 1);
+    if constexpr (T == 64) {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-    if (lane == 0) scratch[w * K + k] = x;
+      for (int i = 0; i < 2; ++i)
+        if (2 * lane + i < K) out[2 * lane + i] = f[i];
+      __syncthreads();
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) scratch[w * 128 + 2 * lane + i] = f[i];
+      __syncthreads();
+      for (int k = threadIdx.x; k < K; k += T) {
+        double s = 0.0;
+#pragma unroll
+        for (int q = 0; q < T / 64; ++q) s += scratch[q * 128 + k];
+        out[k] = s;
+      }
+      __syncthreads();
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      double x = v[k];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+      if (lane == 0) scratch[w * K + k] = x;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < K; k += T) {
+      double s = 0.0;
+#pragma unroll
+      for (int q = 0; q < T / 64; ++q) s += scratch[q * K + k];
+      out[k] = s;
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  for (int k = threadIdx.x; k < K; k += kGsT) {
-    double s = 0.0;
-#pragma unroll
-    for (int q = 0; q < kGsW; ++q) s += scratch[q * K + k];
-    out[k] = s;
-  }
-  __syncthreads();
 }
 
 // Residuals of lab3.fmatrix_residuals_gs for one point and their Jacobians:
@@ -413,12 +462,13 @@ __global__ __launch_bounds__(128) void k_gs_fd(const double *__restrict__ x,
   }
 }
 
-__global__ __launch_bounds__(kGsT) void k_gold_standard(
+template <int T>
+__global__ __launch_bounds__(T) void k_gold_standard(
     const double *__restrict__ Fin, const double *__restrict__ pl, const double *__restrict__ pr,
     int64_t total, const int64_t *__restrict__ off, int max_iter, double *__restrict__ Xb,
     double *__restrict__ Xc, double *__restrict__ Wb, double *__restrict__ Fout,
     double *__restrict__ C1out, GsInfo *__restrict__ info) {
-  __shared__ double red[kGsW * 94];
+  __shared__ double red[(T / 64) * 128];
   __shared__ double sU[78], sgc[12], sres[94], sC[12], sdc[12];
   __shared__ double s_lam, s_nu, s_cost, s_cost0;
   __shared__ int s_state, s_it, s_acc, s_status;
@@ -445,7 +495,7 @@ __global__ __launch_bounds__(kGsT) void k_gold_standard(
   double C[12];
 #pragma unroll
   for (int q = 0; q < 12; ++q) C[q] = sC[q];
-  for (int j = tid; j < n; j += kGsT)
+  for (int j = tid; j < n; j += T)
     triangulate_optimal(C, I34, plx[j], ply[j], prx[j], pry[j], X + 3 * j);
   __syncthreads();
 
@@ -456,7 +506,7 @@ __global__ __launch_bounds__(kGsT) void k_gold_standard(
       double acc[91];
 #pragma unroll
       for (int k = 0; k < 91; ++k) acc[k] = 0.0;
-      for (int j = tid; j < n; j += kGsT) {
+      for (int j = tid; j < n; j += T) {
         double r[4], a0[12], a1[12], Bj[12];
         gs_point(C, X + 3 * j, plx[j], ply[j], prx[j], pry[j], r, a0, a1, Bj);
 #pragma unroll
@@ -482,7 +532,7 @@ __global__ __launch_bounds__(kGsT) void k_gold_standard(
         for (int k = 0; k < 3; ++k)
           w[42 + k] = Bj[k] * r[0] + Bj[3 + k] * r[1] + Bj[6 + k] * r[2] + Bj[9 + k] * r[3];
       }
-      block_reduce<91>(acc, red, sres);
+      block_reduce<91, T>(acc, red, sres);
       if (tid == 0) {
         for (int k = 0; k < 78; ++k) sU[k] = sres[k];
         for (int k = 0; k < 12; ++k) sgc[k] = sres[78 + k];
@@ -499,7 +549,7 @@ __global__ __launch_bounds__(kGsT) void k_gold_standard(
       double acc[90];
 #pragma unroll
       for (int k = 0; k < 90; ++k) acc[k] = 0.0;
-      for (int j = tid; j < n; j += kGsT) {
+      for (int j = tid; j < n; j += T) {
         const double *w = W + kPerPt * j;
         double Vi[6];
         inv_sym3(w + 36, lam, Vi);
@@ -514,7 +564,7 @@ __global__ __launch_bounds__(kGsT) void k_gold_standard(
           acc[78 + p] += wv[p][0] * w[42] + wv[p][1] * w[43] + wv[p][2] * w[44];
         }
       }
-      block_reduce<90>(acc, red, sres);
+      block_reduce<90, T>(acc, red, sres);
     }
     if (tid == 0) {
       // S = U + lam diag(U) - sum W Vi W^T;  rhs = -gc + sum W Vi gx;  Cholesky.  Fully
@@ -579,7 +629,7 @@ __global__ __launch_bounds__(kGsT) void k_gold_standard(
         Cn[p] = C[p] + dc[p];
       }
       double acc[4] = {0.0, 0.0, 0.0, 0.0};  // cost_n*2, x-part of pred*2, |dx|^2, |X|^2
-      for (int j = tid; j < n; j += kGsT) {
+      for (int j = tid; j < n; j += T) {
         const double *w = W + kPerPt * j;
         double Vi[6];
         inv_sym3(w + 36, lam, Vi);
@@ -605,7 +655,7 @@ __global__ __launch_bounds__(kGsT) void k_gold_standard(
         acc[2] += dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2];
         acc[3] += x[0] * x[0] + x[1] * x[1] + x[2] * x[2];
       }
-      block_reduce<4>(acc, red, sres);
+      block_reduce<4, T>(acc, red, sres);
       if (tid == 0) {
         double pc = 0.0, dn = 0.0, cn = 0.0;
         for (int p = 0; p < 12; ++p) {
@@ -643,7 +693,7 @@ __global__ __launch_bounds__(kGsT) void k_gold_standard(
       stop = s_state == 3;
 #pragma unroll
       for (int p = 0; p < 12; ++p) C[p] += sdc[p];
-      for (int j = tid; j < n; j += kGsT) {
+      for (int j = tid; j < n; j += T) {
         X[3 * j + 0] = XN[3 * j + 0];
         X[3 * j + 1] = XN[3 * j + 1];
         X[3 * j + 2] = XN[3 * j + 2];
@@ -881,7 +931,7 @@ extern "C" int rs_gold_standard(rs_ctx *c, const double *F, const double *pl, co
     HIP_TRY(hipMemcpyAsync(b[2], pr, sizeof(double) * 2 * total, hipMemcpyHostToDevice, c->stream));
   }
   HIP_TRY(hipMemcpyAsync(b[3], off, sizeof(int64_t) * (B + 1), hipMemcpyHostToDevice, c->stream));
-  hipLaunchKernelGGL(rsd::k_gold_standard, dim3(static_cast<unsigned>(B)), dim3(rsd::kGsT), 0,
+  hipLaunchKernelGGL(rsd::k_gold_standard<rsd::kGsT>, dim3(static_cast<unsigned>(B)), dim3(rsd::kGsT), 0,
                      c->stream, reinterpret_cast<double *>(b[0]),
                      reinterpret_cast<double *>(b[1]), reinterpret_cast<double *>(b[2]), tp,
                      reinterpret_cast<int64_t *>(b[3]), max_iter, reinterpret_cast<double *>(b[4]),

@@ -83,6 +83,37 @@ def ransac_pairs(pairs, H, seed_base=1000, thresh=1.5, tuples=None, ids=None, ct
     return out
 
 
+# numpy view of _ffi.PairResult (112 packed bytes)
+PAIR_RESULT_DTYPE = np.dtype([("F", "<f8", (9,)), ("best_index", "<i8"), ("best_count", "<i8"),
+                              ("best_std", "<f8"), ("best_norm", "<f8"), ("n_candidates", "<i8")])
+
+
+def ransac_pairs_raw(p1, p2, off, H, seed_base=1000, thresh=1.5, ids=None, ctx=None):
+    """ransac_pairs on pre-concatenated points (p1, p2 (2, total), off (B + 1) column offsets),
+    Philox mode: (results as a PAIR_RESULT_DTYPE array, inlier buffer) -- pair b's inliers are
+    inl[off[b]:off[b] + best_count[b]] when best_index[b] >= 0 -- without a Python object per
+    pair."""
+    p1, p2 = _ffi.f64c(p1), _ffi.f64c(p2)
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    B = len(off) - 1
+    if p1.shape != p2.shape or p1.ndim != 2 or p1.shape[0] != 2 or p1.shape[1] != int(off[-1]):
+        raise ValueError('p1, p2 must be (2, off[-1])')
+    ip = None
+    if ids is not None:
+        ids = np.ascontiguousarray(ids, dtype=np.int64)
+        if ids.shape != (B,):
+            raise ValueError('ids must be (B,)')
+        ip = _ffi.ptr(ids, _ffi.C.c_int64)
+    res = (_ffi.PairResult * B)()
+    inl = np.empty(max(int(off[-1]), 1), dtype=np.int32)
+    _ffi.check(_ffi.lib().rs_pairs_f8_ransac(
+        (ctx or _ffi.default_context()).handle, _ffi.ptr(p1, _ffi.C.c_double),
+        _ffi.ptr(p2, _ffi.C.c_double), _ffi.ptr(off, _ffi.C.c_int64), B, int(H),
+        _ffi.SAMPLER_PHILOX, int(seed_base) & (2**64 - 1), ip, None, float(thresh), res,
+        _ffi.ptr(inl, _ffi.C.c_int32)))
+    return np.frombuffer(res, dtype=PAIR_RESULT_DTYPE).copy(), inl
+
+
 @dataclass
 class PairGeometry:
     ransac: PairRansac

@@ -262,6 +262,8 @@ def lpt_assign(costs, world):
     cost go to the lower index, ties in load to the lower rank)."""
     import heapq
     costs = np.asarray(costs, dtype=np.float64)
+    if world == 1:
+        return [list(range(len(costs)))]
     order = np.lexsort((np.arange(len(costs)), -costs))
     heap = [(0.0, q) for q in range(world)]
     out = [[] for _ in range(world)]
@@ -701,6 +703,12 @@ class GpuPairBatchSolver:
     def __init__(self, ctx, H, seed_base=1000, thresh=1.5):
         self.ctx, self.H, self.seed_base, self.thresh = ctx, int(H), seed_base, thresh
 
+    def many_arrays(self, ids, p1, p2, off):
+        """The same on pre-concatenated points: (PAIR_RESULT_DTYPE array, inlier buffer)."""
+        from . import pairs as pairs_mod
+        return pairs_mod.ransac_pairs_raw(p1, p2, off, self.H, self.seed_base, self.thresh,
+                                          ids=ids, ctx=self.ctx)
+
     def many(self, ids, pairs):
         from . import pairs as pairs_mod
         if not ids:
@@ -720,6 +728,23 @@ class GpuPairRefiner:
     def __init__(self, ctx, K=None):
         self.ctx = ctx
         self.K = None if K is None else np.ascontiguousarray(K, dtype=np.float64)
+
+    def arrays(self, F, pl, pr, off, first1, first2):
+        """The same on arrays: F (B,9) F_RANSAC, the inlier points concatenated (pl, pr
+        (2, total), off (B + 1)), each pair's first correspondence first1, first2 (B,2).
+        Returns (F_gold (B,9), gs_cost (B,), pose found (B,), R (B,9), t (B,3))."""
+        from . import twoview
+        B = len(off) - 1
+        Fg, _, _, info = twoview.gold_standard_arrays(np.asarray(F).reshape(B, 3, 3), pl, pr, off,
+                                                      ctx=self.ctx)
+        if self.K is None:
+            return (Fg.reshape(B, 9), info["cost"], np.zeros(B, dtype=np.int64),
+                    np.full((B, 9), np.nan), np.full((B, 3), np.nan))
+        E = twoview.essential_batch(self.K, Fg, ctx=self.ctx)
+        y1 = twoview.MakeHomogenous(self.K, first1)[:, :2]
+        y2 = twoview.MakeHomogenous(self.K, first2)[:, :2]
+        R, t, found = twoview.relative_camera_pose_batch(E, y1, y2, ctx=self.ctx)
+        return Fg.reshape(B, 9), info["cost"], found, R.reshape(B, 9), t
 
     def __call__(self, items):
         from . import twoview
@@ -750,7 +775,8 @@ def run_pairs(comm, pairs, H, solve, refine=None):
     all-gather in which each rank sends only the records of the pairs it owns (padded to the
     largest owner list, as an all-gather needs equal sizes; every rank derives the same
     owner lists from the costs)."""
-    costs = [p1.shape[1] * H if p1.shape[1] >= 8 else 0 for p1, _ in pairs]
+    ns_all = np.fromiter((p1.shape[1] for p1, _ in pairs), dtype=np.int64, count=len(pairs))
+    costs = np.where(ns_all >= 8, ns_all * H, 0)
     owners = lpt_assign(costs, comm.world)
     recs = np.zeros(len(pairs), dtype=PAIR_DTYPE)
     recs["pair"] = np.arange(len(pairs))
@@ -758,7 +784,12 @@ def run_pairs(comm, pairs, H, solve, refine=None):
     for f in ("F_gold", "gs_cost", "R", "t"):
         recs[f] = np.nan
     items = []
-    mine = [i for i in owners[comm.rank] if pairs[i][0].shape[1] >= 8]
+    own = np.asarray(owners[comm.rank], dtype=np.int64)
+    mine = own[ns_all[own] >= 8].tolist()
+    if hasattr(solve, "many_arrays") and (refine is None or hasattr(refine, "arrays")):
+        if mine:
+            _pairs_arrays(pairs, H, mine, ns_all, solve, refine, recs)
+        return _pairs_gather(comm, pairs, owners, recs)
     if hasattr(solve, "many"):
         outs = solve.many(mine, [pairs[i] for i in mine])
     else:
@@ -784,6 +815,47 @@ def run_pairs(comm, pairs, H, solve, refine=None):
         recs["pose"][idx] = [r[2] for r in ref]
         recs["R"][idx] = np.stack([np.asarray(r[3], dtype=np.float64).ravel() for r in ref])
         recs["t"][idx] = np.stack([np.asarray(r[4], dtype=np.float64).ravel() for r in ref])
+    return _pairs_gather(comm, pairs, owners, recs)
+
+
+def _pairs_arrays(pairs, H, mine, ns_all, solve, refine, recs):
+    """run_pairs' stages on concatenated arrays (a solver with many_arrays, a refiner with
+    arrays): one concatenation of the rank's pairs, the inlier columns gathered by one fancy
+    index, the records filled column-wise -- no Python object per pair."""
+    idx = np.asarray(mine, dtype=np.int64)
+    off = np.zeros(len(mine) + 1, dtype=np.int64)
+    np.cumsum(ns_all[idx], out=off[1:])
+    p1 = np.hstack([pairs[i][0] for i in mine]).astype(np.float64, copy=False)
+    p2 = np.hstack([pairs[i][1] for i in mine]).astype(np.float64, copy=False)
+    res, inl = solve.many_arrays(idx, p1, p2, off)
+    valid = res["best_index"] >= 0
+    cnt = np.where(valid, res["best_count"], 0)
+    recs["valid"][idx] = valid
+    recs["best_index"][idx] = res["best_index"]
+    recs["count"][idx] = cnt
+    recs["std"][idx] = res["best_std"]
+    recs["F"][idx] = res["F"]
+    sel = np.flatnonzero(valid & (cnt > 0))
+    if refine is None or len(sel) == 0:
+        return
+    k = cnt[sel]
+    goff = np.zeros(len(sel) + 1, dtype=np.int64)
+    np.cumsum(k, out=goff[1:])
+    base = np.repeat(off[sel], k)  # pair b's inlier j: column off[b] + inl[off[b] + j]
+    cols = base + inl[base + (np.arange(int(goff[-1])) - np.repeat(goff[:-1], k))]
+    Fg, cost, found, R, t = refine.arrays(res["F"][sel], p1[:, cols], p2[:, cols], goff,
+                                          p1[:, off[sel]].T, p2[:, off[sel]].T)
+    ri = idx[sel]
+    recs["refined"][ri] = 1
+    recs["F_gold"][ri] = Fg
+    recs["gs_cost"][ri] = cost
+    recs["pose"][ri] = found
+    recs["R"][ri] = R
+    recs["t"][ri] = t
+
+
+def _pairs_gather(comm, pairs, owners, recs):
+    """run_pairs' exchange: each rank's own records, one all-gather, the full table."""
     width = max(len(o) for o in owners)
     send = np.zeros(width, dtype=PAIR_DTYPE)
     own = np.asarray(owners[comm.rank], dtype=np.int64)

@@ -219,6 +219,31 @@ def gold_standard_batch(Fs, pls, prs, max_iter=MAX_ITER, ctx=None):
                          info[b].cost, info[b].iterations, info[b].status) for b in range(B)]
 
 
+GS_INFO_DTYPE = np.dtype([("cost_init", "<f8"), ("cost", "<f8"), ("iterations", "<i4"),
+                          ("accepted", "<i4"), ("status", "<i4"), ("n", "<i4")])
+
+
+def gold_standard_arrays(Fs, pl, pr, off, max_iter=MAX_ITER, ctx=None):
+    """gold_standard_batch on pre-concatenated inlier points (pl, pr (2, total), off (B + 1)):
+    (F_gold (B,3,3), C1 (B,3,4), X (total,3), info as a GS_INFO_DTYPE array), no Python object
+    per pair."""
+    Fs = _ffi.f64c(Fs).reshape(-1, 3, 3)
+    B = Fs.shape[0]
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    pl, pr = _ffi.f64c(pl), _ffi.f64c(pr)
+    if off.shape != (B + 1,) or pl.shape != pr.shape or pl.shape != (2, int(off[-1])):
+        raise ValueError('pl, pr must be (2, off[-1]) with one offset per F')
+    Fg = np.empty((B, 3, 3))
+    C1 = np.empty((B, 3, 4))
+    X = np.empty((max(int(off[-1]), 1), 3))
+    info = (_ffi.GsInfo * B)()
+    _ffi.check(_ffi.lib().rs_gold_standard(
+        _ctx(ctx), _ffi.ptr(Fs, _d), _ffi.ptr(pl, _d), _ffi.ptr(pr, _d),
+        _ffi.ptr(off, _ffi.C.c_int64), B, int(max_iter), _ffi.ptr(Fg, _d), _ffi.ptr(C1, _d),
+        _ffi.ptr(X, _d), info))
+    return Fg, C1, X, np.frombuffer(info, dtype=GS_INFO_DTYPE).copy()
+
+
 def gold_standard(F, pl, pr, max_iter=MAX_ITER, ctx=None):
     """F_gold of fun.py:336-369 from F_RANSAC and the inlier points pl, pr (2, n)."""
     return gold_standard_batch(np.asarray(F).reshape(1, 3, 3), [pl], [pr], max_iter, ctx)[0].F
