@@ -77,26 +77,55 @@ __global__ __launch_bounds__(256) void k_pairs_solve(const Pt *__restrict__ pts,
   for (int k = 0; k < 9; ++k) Fsoa[k * ld + g] = F[k];
 }
 
+// (and np.linalg.norm(d) of every hypothesis, for the selection's ties: the sum a wave per
+// hypothesis forms -- 64 lane sums over the points i = l, l + 64, ..., combined by the xor
+// butterfly (wsum) -- is the balanced pairwise sum of the lane sums in bit-reversed lane
+// order.  A wave takes one of kCountChunks runs of those leaves, a complete subtree: its sum
+// goes to nrmp[hypothesis][chunk] and k_pairs_select adds the chunks' subtrees in tree order
+// (same bits).  Counts are added atomically (order-free).  Chunks: the largest pairs' point
+// loops were the kernel's serial chains.)
+constexpr int kCountChunks = 8;  // leaves per chunk: 64 / kCountChunks = 8 (a subtree)
 __global__ __launch_bounds__(256) void k_pairs_count(const Pt *__restrict__ pts,
                                                      const int64_t *__restrict__ off, int B,
                                                      int H, const double *__restrict__ Fsoa,
                                                      int64_t ld, double thresh,
-                                                     int *__restrict__ counts) {
+                                                     int *__restrict__ counts,
+                                                     double *__restrict__ nrmp) {
   const int groups = (H + 63) >> 6;
   const int u = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-  if (u >= B * groups) return;
-  const int b = u / groups, grp = u - b * groups;
+  if (u >= B * groups * kCountChunks) return;
+  const int ch = u % kCountChunks, ug = u / kCountChunks;
+  const int b = ug / groups, grp = ug - b * groups;
   const int h = grp * 64 + (threadIdx.x & 63);
   const int64_t o = off[b];
   const int n = static_cast<int>(off[b + 1] - o);
+  if (n < 8) return;  // no candidates: the counts stay 0
   const int64_t g = static_cast<int64_t>(b) * H + (h < H ? h : H - 1);
   double f[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) f[k] = Fsoa[k * ld + g];
+  constexpr int kLeaves = 64 / kCountChunks, kLev = 3;  // log2(kLeaves)
   int cnt = 0;
-  if (n >= 8)
-    for (int i = 0; i < n; ++i) cnt += dist_ref(f, pts[o + i]) < thresh ? 1 : 0;
-  if (h < H) counts[static_cast<int64_t>(b) * H + h] = cnt;
+  double acc[kLev], tot = 0.0;
+  for (int q = 0; q < kLeaves; ++q) {
+    const int k = ch * kLeaves + q;
+    const int l = static_cast<int>(__builtin_bitreverse32(static_cast<uint32_t>(k)) >> 26);
+    double s2 = 0.0;
+    for (int i = l; i < n; i += 64) {
+      const double d = dist_ref(f, pts[o + i]);
+      cnt += d < thresh ? 1 : 0;
+      s2 += d * d;
+    }
+    double carry = s2;  // leaf q closes the subtrees of its trailing one bits
+    int lev = 0;
+    for (; lev < kLev && ((q >> lev) & 1); ++lev) carry = acc[lev] + carry;
+    if (lev < kLev) acc[lev] = carry;
+    else tot = carry;
+  }
+  if (h < H) {
+    if (cnt) atomicAdd(&counts[static_cast<int64_t>(b) * H + h], cnt);
+    nrmp[(static_cast<int64_t>(b) * H + h) * kCountChunks + ch] = tot;
+  }
 }
 
 __device__ __forceinline__ double wsum(double v) {
@@ -108,7 +137,7 @@ __device__ __forceinline__ double wsum(double v) {
 __global__ __launch_bounds__(kPairSelT) void k_pairs_select(
     const Pt *__restrict__ pts, const int64_t *__restrict__ off, int H,
     const double *__restrict__ Fsoa, int64_t ld, const int *__restrict__ counts, double thresh,
-    int *__restrict__ cand, double *__restrict__ cstd, double *__restrict__ cnorm,
+    int *__restrict__ cand, const double *__restrict__ nrmp, double *__restrict__ cnorm,
     PairDevResult *__restrict__ res, int32_t *__restrict__ inl) {
   __shared__ int sh_i[kPairSelW];
   __shared__ int s_cstar, s_best;
@@ -118,7 +147,7 @@ __global__ __launch_bounds__(kPairSelT) void k_pairs_select(
   const int n = static_cast<int>(off[b + 1] - o);
   const int *cnt = counts + static_cast<int64_t>(b) * H;
   int *cb = cand + static_cast<int64_t>(b) * H;
-  double *nb = cnorm + static_cast<int64_t>(b) * H;  // cstd: kept for the launch layout
+  double *nb = cnorm + static_cast<int64_t>(b) * H;  // the candidates' norms, in list order
   // ---- c* ----
   int m = 0;
   for (int i = tid; i < H; i += kPairSelT) m = max(m, cnt[i]);
@@ -152,19 +181,13 @@ __global__ __launch_bounds__(kPairSelT) void k_pairs_select(
       __syncthreads();
     }
   }
-  // ---- np.linalg.norm(d) of every candidate (wave per candidate, one pass) ----
-  for (int j = w; j < nloc; j += kPairSelW) {
-    const int64_t g = static_cast<int64_t>(b) * H + cb[j];
-    double f[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) f[k] = Fsoa[k * ld + g];
-    double s2 = 0.0;
-    for (int i = lane; i < n; i += 64) {
-      const double d = dist_ref(f, pts[o + i]);
-      s2 += d * d;
-    }
-    s2 = wsum(s2);
-    if (lane == 0) nb[j] = sqrt(s2);
+  // ---- np.linalg.norm(d) of every candidate: k_pairs_count's (same bits as a wave per
+  // candidate; C4's ~1 000 tied candidates per pair took one wave pass each here) ----
+  __syncthreads();  // (cb complete)
+  for (int j = tid; j < nloc; j += kPairSelT) {  // the chunks' subtrees, in tree order
+    const double *t = nrmp + (static_cast<int64_t>(b) * H + cb[j]) * kCountChunks;
+    static_assert(kCountChunks == 8, "three levels above the chunks");
+    nb[j] = sqrt(((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7])));
   }
   __syncthreads();
   // ---- fun.py:320-328 replay over the c* candidates (wave 0).  The first one is always
@@ -300,7 +323,7 @@ extern "C" int rs_pairs_f8_ransac(rs_ctx *c, const double *p1, const double *p2,
   auto al = [](size_t x) { return (x + 255) / 256 * 256; };
   const size_t sizes[] = {sizeof(rsd::Pt) * tp,         sizeof(int64_t) * (B + 1),
                           sizeof(double) * 9 * ld,      sizeof(int) * ld,
-                          sizeof(int) * ld,             sizeof(double) * ld,
+                          sizeof(int) * ld,             sizeof(double) * rsd::kCountChunks * ld,
                           sizeof(double) * ld,          sizeof(rsd::PairDevResult) * B,
                           sizeof(int32_t) * tp,
                           mode == RS_SAMPLER_TUPLES ? sizeof(int32_t) * 8 * ld : 0,
@@ -320,7 +343,7 @@ extern "C" int rs_pairs_f8_ransac(rs_ctx *c, const double *p1, const double *p2,
   auto *d_F = reinterpret_cast<double *>(buf[2]);
   auto *d_counts = reinterpret_cast<int *>(buf[3]);
   auto *d_cand = reinterpret_cast<int *>(buf[4]);
-  auto *d_cstd = reinterpret_cast<double *>(buf[5]);
+  auto *d_nrm = reinterpret_cast<double *>(buf[5]);
   auto *d_cnorm = reinterpret_cast<double *>(buf[6]);
   auto *d_res = reinterpret_cast<rsd::PairDevResult *>(buf[7]);
   auto *d_inl = reinterpret_cast<int32_t *>(buf[8]);
@@ -343,14 +366,15 @@ extern "C" int rs_pairs_f8_ransac(rs_ctx *c, const double *p1, const double *p2,
                      0, c->stream, d_pts, d_off, static_cast<int>(B), static_cast<int>(H), mode,
                      seed_base, d_ids, d_tup, d_F, ld);
   HIP_TRY(hipGetLastError());
-  const int64_t units = B * ((H + 63) / 64);
+  const int64_t units = B * ((H + 63) / 64) * rsd::kCountChunks;
+  HIP_TRY(hipMemsetAsync(d_counts, 0, sizeof(int) * ld, c->stream));
   hipLaunchKernelGGL(rsd::k_pairs_count, dim3(static_cast<unsigned>((units + 3) / 4)), dim3(256),
                      0, c->stream, d_pts, d_off, static_cast<int>(B), static_cast<int>(H), d_F,
-                     ld, thresh, d_counts);
+                     ld, thresh, d_counts, d_nrm);  // (every hypothesis's norm subtrees)
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(rsd::k_pairs_select, dim3(static_cast<unsigned>(B)), dim3(rsd::kPairSelT), 0,
                      c->stream, d_pts, d_off, static_cast<int>(H), d_F, ld, d_counts, thresh,
-                     d_cand, d_cstd, d_cnorm, d_res, d_inl);
+                     d_cand, d_nrm, d_cnorm, d_res, d_inl);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(out, d_res, sizeof(rs_pair_result) * B, hipMemcpyDeviceToHost, c->stream));
   if (total > 0)

@@ -736,7 +736,7 @@ class GpuPairRefiner:
         from . import twoview
         B = len(off) - 1
         Fg, _, _, info = twoview.gold_standard_arrays(np.asarray(F).reshape(B, 3, 3), pl, pr, off,
-                                                      ctx=self.ctx)
+                                                      ctx=self.ctx, want_points=False)
         if self.K is None:
             return (Fg.reshape(B, 9), info["cost"], np.zeros(B, dtype=np.int64),
                     np.full((B, 9), np.nan), np.full((B, 3), np.nan))

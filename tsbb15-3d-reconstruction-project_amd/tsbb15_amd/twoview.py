@@ -223,10 +223,10 @@ GS_INFO_DTYPE = np.dtype([("cost_init", "<f8"), ("cost", "<f8"), ("iterations", 
                           ("accepted", "<i4"), ("status", "<i4"), ("n", "<i4")])
 
 
-def gold_standard_arrays(Fs, pl, pr, off, max_iter=MAX_ITER, ctx=None):
+def gold_standard_arrays(Fs, pl, pr, off, max_iter=MAX_ITER, ctx=None, want_points=True):
     """gold_standard_batch on pre-concatenated inlier points (pl, pr (2, total), off (B + 1)):
     (F_gold (B,3,3), C1 (B,3,4), X (total,3), info as a GS_INFO_DTYPE array), no Python object
-    per pair."""
+    per pair.  want_points=False: C1 and X are not copied back (None)."""
     Fs = _ffi.f64c(Fs).reshape(-1, 3, 3)
     B = Fs.shape[0]
     off = np.ascontiguousarray(off, dtype=np.int64)
@@ -234,13 +234,13 @@ def gold_standard_arrays(Fs, pl, pr, off, max_iter=MAX_ITER, ctx=None):
     if off.shape != (B + 1,) or pl.shape != pr.shape or pl.shape != (2, int(off[-1])):
         raise ValueError('pl, pr must be (2, off[-1]) with one offset per F')
     Fg = np.empty((B, 3, 3))
-    C1 = np.empty((B, 3, 4))
-    X = np.empty((max(int(off[-1]), 1), 3))
+    C1 = np.empty((B, 3, 4)) if want_points else None
+    X = np.empty((max(int(off[-1]), 1), 3)) if want_points else None
     info = (_ffi.GsInfo * B)()
     _ffi.check(_ffi.lib().rs_gold_standard(
         _ctx(ctx), _ffi.ptr(Fs, _d), _ffi.ptr(pl, _d), _ffi.ptr(pr, _d),
-        _ffi.ptr(off, _ffi.C.c_int64), B, int(max_iter), _ffi.ptr(Fg, _d), _ffi.ptr(C1, _d),
-        _ffi.ptr(X, _d), info))
+        _ffi.ptr(off, _ffi.C.c_int64), B, int(max_iter), _ffi.ptr(Fg, _d),
+        _ffi.ptr(C1, _d) if want_points else None, _ffi.ptr(X, _d) if want_points else None, info))
     return Fg, C1, X, np.frombuffer(info, dtype=GS_INFO_DTYPE).copy()
 
 
