@@ -396,7 +396,8 @@ def extras(ctx, rank, world, dist, comm):  # noqa: C901
         p1, p2, _ = synth.two_view(N_CORR, OUTLIERS, seed=1)
         S = 20_000
         essential.ransac_e(p1, p2, synth.K_SYNTH, samples=S, seed=1)
-        el, r = _best_of(lambda: essential.ransac_e(p1, p2, synth.K_SYNTH, samples=S, seed=1), 3)
+        # (best of 10: a 0.4 ms call whose spread box to box and call to call is ~5 %)
+        el, r = _best_of(lambda: essential.ransac_e(p1, p2, synth.K_SYNTH, samples=S, seed=1), 10)
         out["e5_ransac_c2"] = {"metric": "five-point E-RANSAC minimal samples/s", "value": S / el,
                                "ms": el * 1e3, "samples": S, "hypotheses": 10 * S,
                                "consensus": r.count,
