@@ -88,6 +88,20 @@ extern "C" int rs_ctx_create(int device, rs_ctx **out) {
     delete c;
     return hip_fail(e, "hipStreamCreate");
   }
+  // the F-RANSAC and parity sampler code objects are loaded here rather than by the first
+  // RANSAC call (HIP loads a module at the first use of one of its kernels; a no-op once the
+  // process has them on this device)
+  e = rsd::preload_f8();
+  if (e != hipSuccess) {
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return hip_fail(e, "code object load");
+  }
+  if (int st = rs::np_preload()) {
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return st;
+  }
   *out = c;
   return RS_OK;
 }

@@ -26,6 +26,7 @@ namespace rs {
 int hip_fail(hipError_t e, const char *what);
 int ensure_scratch(rs_ctx *c, size_t bytes);
 void np_shard_free(rs_ctx *c);
+int np_preload();  // the parse kernels' code object onto the current device (rs_ctx_create)
 bool np_gpu_supported(int64_t n, int32_t k);  // within the GPU parse's population range
 // The numpy (py: CPython) stream's next `count` choice(n, k) tuples; rows [skip, skip + take)
 // (take < 0: to the end) are written to d_out (take * k int32); (key, pos) advance past all

@@ -96,6 +96,7 @@ struct Bounds {
 Bounds fp32_bounds(const Frame &fr, double thresh);
 bool unit_frame(const double *p1, const double *p2, int64_t n, Frame &fr);
 Count32qShape count32q_shape(int n, int H, int waves, int slices_per_wave = 0);
+hipError_t preload_f8();  // the F-RANSAC kernels' code object onto the current device
 // pts (and with fr the point-pair layout ptsq) from the (2, n) arrays in one launch
 hipError_t launch_pack_points_both(const double *p1, const double *p2, int n, Pt *pts,
                                    const Frame *fr, float4 *ptsq, hipStream_t s);

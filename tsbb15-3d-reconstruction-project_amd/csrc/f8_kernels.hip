@@ -985,6 +985,12 @@ __global__ __launch_bounds__(256) void k_pack_points_both(const double *__restri
 // ------------------------------------------------------------------------------------------
 namespace rsd {
 
+// this file's code object onto the current device (rs_ctx_create: not at the first RANSAC)
+hipError_t preload_f8() {
+  hipFuncAttributes fa{};
+  return hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(k_pack_points));
+}
+
 hipError_t launch_pack_points(const double *p1, const double *p2, int n, Pt *pts,
                               hipStream_t s) {
   hipLaunchKernelGGL(k_pack_points, dim3((n + 255) / 256), dim3(256), 0, s, p1, p2, n, pts);
