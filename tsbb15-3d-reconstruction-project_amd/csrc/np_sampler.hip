@@ -1972,6 +1972,9 @@ constexpr int kTupAhead = RSAMD_TUP_AHEAD;
 #ifndef RSAMD_TUP_FP
 #define RSAMD_TUP_FP rej_fixed_point_aa  // (A/B: rej_fixed_point_aa1)
 #endif
+#ifndef RSAMD_TUP_VWIN
+#define RSAMD_TUP_VWIN 1  // general windows with a mask per lane (A/B: 0)
+#endif
 
 
 template <bool PY>
@@ -2164,6 +2167,33 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
     i -= static_cast<uint32_t>(__popcll(acc));
     o += W;
   };
+#if RSAMD_TUPF
+  // The general window with a mask per lane (numpy rule): 64 draws whatever buckets they span,
+  // the hypothesis end inside -- lane l's state s_l = i - rank_l(acc), its draw w_l & mask(s_l)
+  // accepted iff <= s_l, lanes past the end (s_l < 1) never; the fixed point from "all
+  // accept" is the sequential answer (lane 0 is right, and lane l is once lanes < l are).  The
+  // single-mask window above stops at every bucket edge, so below the two-bucket range a
+  // hypothesis took ~30 windows of a few draws each; this takes two or three.
+  [[maybe_unused]] auto window_v = [&]() {
+    const uint32_t wd = ring[(o + l) & (kTupRing - 1)];
+    uint32_t iv;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(iv) : "s"(i));
+    uint64_t acc = ~0ull, prev;
+    uint32_t sl, u;
+    do {
+      prev = acc;
+      sl = iv - lane_rank(prev);
+      u = wd & (0xffffffffu >> __builtin_clz(sl | 1u));
+      acc = __ballot(static_cast<int>(sl) >= 1 && u <= sl);
+    } while (acc != prev);
+    const bool ap = (acc >> l) & 1ull;
+    if (ap && sl <= 7u) J7[sl - 1u] = static_cast<uint16_t>(u);
+    fstore(ap && sl >= 8u && u < sl, u, sl);
+    const uint64_t endb = __ballot(ap && sl == 1u);  // state 1 always accepts: the end
+    i -= static_cast<uint32_t>(__popcll(acc));
+    o += endb ? __ffsll(static_cast<long long>(endb)) : 64;
+  };
+#endif
   // The register queue rotates by unrolling (slot q is refilled in turn), never by moving a
   // register: a move of a load's destination would wait for that load.
   // (a two-bucket window never ends the hypothesis: only the general one is followed by the
@@ -2219,7 +2249,12 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
         }
 #endif
         if (window2()) continue;
+#if RSAMD_TUPF && RSAMD_TUP_VWIN
+        if constexpr (!PY) window_v();
+        else window();
+#else
         window();
+#endif
         if (i == 0) goto parsed;
       }
       // the oldest block in flight lands in the ring; its slot loads the next
