@@ -28,6 +28,8 @@
 #if RSAMD_GEN_PHI  // tools/gen_mt_phi.cpp: writes the constants below from charpoly_bm
 constexpr uint64_t kPhiWords[312] = {};
 constexpr uint64_t kMuWords[312] = {};
+constexpr int kPow2Embed = 0;
+constexpr uint64_t kPow2Words[1][312] = {};
 #else
 #include "mt_phi.h"
 #endif
@@ -287,15 +289,35 @@ void sqrmod_fast(const u64 *a, u64 *r) {
   barrett_reduce(p, r);
 }
 
-// x^(624 * 2^k) mod phi for k < 40, built on demand (each a squaring of the one before):
-// x^(624 JB) is the product over JB's set bits
+// x^(624 * 2^k) mod phi for k < 40: the first kPow2Embed from mt_phi.h (checked by the
+// self-test), the rest built on demand (each a squaring of the one before): x^(624 JB) is the
+// product over JB's set bits
 constexpr int kPow2 = 40;
 std::mutex g_pow2_mu;
+// x^624 mod phi by times-x steps
+std::vector<u64> x624() {
+  std::vector<u64> p(kR, 0);
+  p[0] = 1;
+  for (int s = 0; s < kN; ++s) {
+    u64 carry = 0;
+    for (int i = 0; i < kR; ++i) {
+      const u64 v = p[i];
+      p[i] = (v << 1) | carry;
+      carry = v >> 63;
+    }
+    if ((p[kR - 1] >> (kDeg - 64 * (kR - 1))) & 1u)
+      for (int i = 0; i < kR; ++i) p[i] ^= kPhiWords[i];
+  }
+  return p;
+}
 const std::vector<u64> &pow2(int k) {
   static std::vector<std::vector<u64>> T;
   std::lock_guard<std::mutex> g(g_pow2_mu);
   if (T.empty()) {
     T.reserve(kPow2);  // no reallocation: references handed out stay valid
+    for (int e = 0; e < kPow2Embed && e < kPow2; ++e) T.emplace_back(kPow2Words[e], kPow2Words[e] + kR);
+  }
+  if (T.empty()) {
     std::vector<u64> p(kR, 0);
     p[0] = 1;
     for (int s = 0; s < kN; ++s) {  // x^624 by times-x steps
@@ -510,5 +532,18 @@ extern "C" int rs_mt_poly_selftest(int64_t j1, int64_t j2) {
                                       mu[static_cast<size_t>(i)] == kMuWords[i];
     return ok;
   }();
-  return (consts_ok && r == c && a == as && b == bs && c == cs && rs_ == cs && sq == sqs) ? 1 : 0;
+  // the embedded x^(624 2^k) (mt_phi.h): x^624 by times-x steps, then squarings
+  static const bool pow2_ok = [] {
+    std::vector<u64> p = x624(), q(kR, 0);
+    bool ok = true;
+    for (int k = 0; k < kPow2Embed; ++k) {
+      if (k) {
+        sqrmod_fast(p.data(), q.data());
+        p.swap(q);
+      }
+      ok = ok && std::equal(p.begin(), p.end(), kPow2Words[k]);
+    }
+    return ok;
+  }();
+  return (consts_ok && pow2_ok && r == c && a == as && b == bs && c == cs && rs_ == cs && sq == sqs) ? 1 : 0;
 }

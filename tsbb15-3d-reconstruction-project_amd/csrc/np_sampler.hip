@@ -2423,14 +2423,32 @@ void jump_bits_cached(int kind, int JB, int levels, JumpBits &out) {
     auto powers = [kind](const std::vector<uint64_t> &b, std::vector<std::vector<uint64_t>> &pw) {
       pw.assign(static_cast<size_t>(kind) + 1, {});
       pw[1] = b;
-      for (int m = 2; m < kind; ++m) {
+      auto step = [&pw](int m) {
         if (m % 2 == 0) {
           pw[static_cast<size_t>(m)] = pw[static_cast<size_t>(m / 2)];
           rs::mt_poly_square(pw[static_cast<size_t>(m)]);
         } else {
           rs::mt_poly_mulmod(pw[static_cast<size_t>(m - 1)], pw[1], pw[static_cast<size_t>(m)]);
         }
+      };
+      if (kind != 8) {
+        for (int m = 2; m < kind; ++m) step(m);
+        return;
       }
+      // radix 8: after b^2, the chains b^4, b^5 and b^3, b^6, b^7 are independent (the second
+      // on a helper thread: 1.6 -> 1.0 ms per level)
+      step(2);
+      std::thread t;
+      try {
+        t = std::thread([&step] { step(3); step(6); step(7); });
+      } catch (...) {
+        step(3);
+        step(6);
+        step(7);
+      }
+      step(4);
+      step(5);
+      if (t.joinable()) t.join();
     };
     const bool pow2 = (kind & (kind - 1)) == 0;
     std::vector<std::thread> th;
@@ -2639,7 +2657,7 @@ void shard_free(rs_np_shard *w) {
   if (w->d_io) (void)hipFree(w->d_io);
   if (w->ev_a) (void)hipEventDestroy(w->ev_a);
   if (w->ev_b) (void)hipEventDestroy(w->ev_b);
-  if (w->s2) (void)hipStreamDestroy(w->s2);
+  // (w->s2 belongs to the process-wide pool: np_aux_stream)
 }
 
 // kernel attributes for populations up to n1 (dynamic LDS of the entry and tuple kernels)
@@ -2677,12 +2695,19 @@ int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 }  // namespace
 
+namespace {
+int np_aux_stream(int device, hipStream_t *out);
+}  // namespace
+
 // Loads this file's code object on the current device (HIP loads a module at the first use of
 // any of its kernels: ~10 ms for the parse kernels, paid by the first parity call otherwise).
 int rs::np_preload() {
   hipFuncAttributes fa{};
   HIP_TRY(hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(k_np_track<false, false>)));
-  return RS_OK;
+  int device = 0;
+  HIP_TRY(hipGetDevice(&device));
+  hipStream_t s2 = nullptr;  // the parse's second stream, created once per device (np_aux_stream)
+  return np_aux_stream(device, &s2);
 }
 
 namespace {
@@ -2866,6 +2891,22 @@ int shard_windows(rs_np_shard &w, const uint32_t *key, hipStream_t s) {
   return RS_OK;
 }
 
+// The second stream of the parse (stream pass 2 beside the entry kernel), one per device for
+// the whole process: creating a HIP stream costs 15-30 ms here (it was most of a new context's
+// first parity call, tools/probe_first_call2.py).  Sessions of several contexts on one device
+// share it; each orders its work on it by its own events.
+int np_aux_stream(int device, hipStream_t *out) {
+  static std::mutex mu;
+  static std::vector<hipStream_t> pool;
+  std::lock_guard<std::mutex> g(mu);
+  if (device < 0) return rs::fail(RS_EINVAL, "np: bad device");
+  if (static_cast<size_t>(device) >= pool.size()) pool.resize(static_cast<size_t>(device) + 1, nullptr);
+  if (!pool[static_cast<size_t>(device)])
+    HIP_TRY(hipStreamCreateWithFlags(&pool[static_cast<size_t>(device)], hipStreamNonBlocking));
+  *out = pool[static_cast<size_t>(device)];
+  return RS_OK;
+}
+
 // device set-up shared by both drivers: kernel attributes, the jump polynomials, counters
 int shard_init(rs_np_shard &w) {
   HIP_TRY(hipSetDevice(w.ctx->device));
@@ -2875,7 +2916,7 @@ int shard_init(rs_np_shard &w) {
     int64_t c1 = 0, c2 = 0, c3 = 0;
     if ((st = sgrow(w.d_err, c1, 1)) || (st = sgrow(w.d_got, c2, 1)) || (st = sgrow(w.d_res, c3, 1)))
       return st;
-    HIP_TRY(hipStreamCreateWithFlags(&w.s2, hipStreamNonBlocking));
+    if ((st = np_aux_stream(w.ctx->device, &w.s2))) return st;
     HIP_TRY(hipEventCreateWithFlags(&w.ev_a, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&w.ev_b, hipEventDisableTiming));
   }
