@@ -437,6 +437,22 @@ int rs_gold_standard(rs_ctx *ctx, const double *F, const double *pl, const doubl
                      const int64_t *off, int64_t B, int32_t max_iter, double *F_gold,
                      double *C1_out, double *X_out, rs_gs_info *info);
 
+/* Config C4 end to end (run_pairs with a refiner: fun.py:298-328, 336-369 and main.py:50-63 per
+ * pair) in one call: rs_pairs_f8_ransac's stages, then for every pair with a consensus
+ * (best_index >= 0 and best_count > 0) rs_gold_standard (max_iter) on its S_RANSAC points,
+ * and -- when K (3, 3) is given -- E = K^T F_gold K and rs_relative_camera_pose on y1[b], y2[b]
+ * (B, 2), the caller's C-normalised first correspondence of each pair.  Everything between the
+ * stages stays on the device (the inlier points are gathered there): one upload, one download.
+ * Outputs as the three calls': out (B), inliers (total), F_gold (B, 3, 3), info (B), R (B, 3, 3),
+ * t (B, 3), found (B).  Pairs without a consensus: F_gold, R, t NaN, info zero, found 0; K NULL:
+ * R, t NaN and found 0 for every pair. */
+int rs_pairs_two_view(rs_ctx *ctx, const double *p1, const double *p2, const int64_t *off,
+                      int64_t B, int64_t H, int32_t mode, uint64_t seed_base,
+                      const int64_t *seed_ids, const int32_t *host_tuples, double thresh,
+                      int32_t max_iter, const double *K, const double *y1, const double *y2,
+                      rs_pair_result *out, int32_t *inliers, double *F_gold, rs_gs_info *info,
+                      double *R, double *t, int32_t *found);
+
 /* ------------------------------------------------------------------------------------------
  * Per-view SfM steps around PnP (tables.py, fun.py:12-21)
  * ---------------------------------------------------------------------------------------- */

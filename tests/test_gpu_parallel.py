@@ -196,3 +196,57 @@ def test_dino_ring_array_path_matches_object_path(ctx):
     slow = parallel.run_pairs(_Solo(), pairs, 1000, ObjSolver(solver), refine=ObjRefiner(refiner))
     for f in parallel.PAIR_DTYPE.names:
         assert np.array_equal(fast[f], slow[f], equal_nan=fast[f].dtype.kind == "f"), f
+    assert int(fast["refined"].sum()) > 100 and int((fast["pose"] > 0).sum()) > 100
+
+
+@pytest.mark.parametrize("with_k", [True, False])
+def test_dino_ring_fused_call_matches_separate_calls(ctx, with_k):
+    """rs_pairs_two_view (RANSAC, gold standard, E and pose in one device call) gives the
+    table of the separate calls (rs_pairs_f8_ransac, host gather, rs_gold_standard,
+    rs_essential_from_f, rs_relative_camera_pose), field for field; without K no pose."""
+    z = golden("dino_pnp_kat.npz")
+    pairs = _dino_pairs()
+    K = z["K_last"] if with_k else None
+    solver = parallel.GpuPairBatchSolver(ctx, 1000)
+    fused = parallel.run_pairs(_Solo(), pairs, 1000, solver,
+                               refine=parallel.GpuPairRefiner(ctx, K))
+    sep = parallel.run_pairs(_Solo(), pairs, 1000, solver,
+                             refine=parallel.GpuPairRefiner(ctx, K, fused=False))
+    for f in parallel.PAIR_DTYPE.names:
+        assert np.array_equal(fused[f], sep[f], equal_nan=fused[f].dtype.kind == "f"), f
+    if not with_k:
+        assert int((fused["pose"] > 0).sum()) == 0
+
+
+def test_two_view_pairs_raw_edges(ctx):
+    """Pairs without a consensus (N < 8, empty) inside a fused call: NaN F_gold / pose, found
+    0, zero gold-standard info; the other pairs as in a call without them."""
+    from tsbb15_amd import pairs as pairs_mod
+    z = golden("dino_pnp_kat.npz")
+    allp = _dino_pairs()
+    big = [p for p in allp if p[0].shape[1] >= 20]
+    dp = [big[0], big[1], big[2]]
+    chosen = [dp[0], (dp[1][0][:, :5], dp[1][1][:, :5]), (np.zeros((2, 0)), np.zeros((2, 0))),
+              dp[2]]
+    off = np.zeros(len(chosen) + 1, dtype=np.int64)
+    np.cumsum([p[0].shape[1] for p in chosen], out=off[1:])
+    p1 = np.hstack([p[0] for p in chosen])
+    p2 = np.hstack([p[1] for p in chosen])
+    res, _, Fg, info, R, t, found = pairs_mod.two_view_pairs_raw(p1, p2, off, 1000, z["K_last"],
+                                                                 ctx=ctx)
+    for b in (1, 2):
+        assert res["best_index"][b] == -1
+        assert np.isnan(Fg[b]).all() and np.isnan(R[b]).all() and np.isnan(t[b]).all()
+        assert found[b] == 0 and info["n"][b] == 0 and info["iterations"][b] == 0
+    keep = [0, 3]
+    off2 = np.array([0, dp[0][0].shape[1], dp[0][0].shape[1] + dp[2][0].shape[1]])
+    r2 = pairs_mod.two_view_pairs_raw(np.hstack([dp[0][0], dp[2][0]]),
+                                      np.hstack([dp[0][1], dp[2][1]]), off2, 1000, z["K_last"],
+                                      ids=np.array(keep), ctx=ctx)
+    for a, b in zip((res, Fg, info, R, t, found), (r2[0], r2[2], r2[3], r2[4], r2[5], r2[6])):
+        a2 = a[keep]
+        if a2.dtype.names:
+            for f in a2.dtype.names:
+                assert np.array_equal(a2[f], b[f], equal_nan=True), f
+        else:
+            assert np.array_equal(a2, b, equal_nan=True)

@@ -29,7 +29,8 @@ def main():
         pairs.append((np.ascontiguousarray(Q[i][:, vis]), np.ascontiguousarray(Q[j][:, vis])))
     ctx = _ffi.Context(0)
     solver = parallel.GpuPairBatchSolver(ctx, 1000)
-    refiner = None if os.environ.get("PROBE_NOREFINE") else parallel.GpuPairRefiner(ctx, z["K_last"])
+    refiner = None if os.environ.get("PROBE_NOREFINE") else parallel.GpuPairRefiner(
+        ctx, z["K_last"], fused=not os.environ.get("PROBE_UNFUSED"))
     ts = []
     for _ in range(int(os.environ.get("PROBE_RUNS", 10))):
         t = time.perf_counter()

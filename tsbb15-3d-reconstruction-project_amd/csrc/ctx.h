@@ -37,5 +37,18 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
 // Step 4 of a sharded parse (np_sampler.hip, rs_np_shard_*) into device memory.
 int np_shard_tuples_device(rs_np_shard *w, int64_t base, int64_t hi, int64_t next_start,
                            int64_t final_idx, int32_t *d_out, uint32_t *key_out, int32_t *pos_out);
+// The batched pair RANSAC (pairs.hip) enqueued without its download; the records (rs_pair_result
+// layout), inlier lists and points stay on the device for the stages after it.
+struct PairsDev {
+  const void *pts;       // rsd::Pt per point (x1, y1, x2, y2), pair b at off[b]
+  const int64_t *off;    // B + 1 offsets
+  void *res;             // B records (rs_pair_result)
+  int32_t *inl;          // S_RANSAC of pair b at inl[off[b] ..]
+  int64_t total;         // off[B]
+  char *extra;           // the caller's `extra` bytes of scratch (256-aligned)
+};
+int pairs_enqueue(rs_ctx *c, const double *p1, const double *p2, const int64_t *off, int64_t B,
+                  int64_t H, int32_t mode, uint64_t seed_base, const int64_t *seed_ids,
+                  const int32_t *host_tuples, double thresh, size_t extra, PairsDev *d);
 int fmatrix_stls_lsq(rs_ctx *c, const double *pl, const double *pr, int64_t n, double *F_out);
 }  // namespace rs

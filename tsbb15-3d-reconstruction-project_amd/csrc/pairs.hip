@@ -293,12 +293,14 @@ using rs::hip_fail;
 
 static_assert(sizeof(rsd::PairDevResult) == sizeof(rs_pair_result), "rs_pair_result layout");
 
-extern "C" int rs_pairs_f8_ransac(rs_ctx *c, const double *p1, const double *p2,
-                                  const int64_t *off, int64_t B, int64_t H, int32_t mode,
-                                  uint64_t seed_base, const int64_t *seed_ids,
-                                  const int32_t *host_tuples, double thresh,
-                                  rs_pair_result *out, int32_t *inliers) {
-  if (!c || !off || !out || !inliers) return fail(RS_EINVAL, "null pointer");
+namespace rs {
+// rs_pairs_f8_ransac's validation, upload and kernels, enqueued on the context stream without
+// the download: the pair records and inlier lists stay in device memory (PairsDev), with
+// `extra` bytes of scratch after them for the caller's next stages (rs_pairs_two_view).
+int pairs_enqueue(rs_ctx *c, const double *p1, const double *p2, const int64_t *off, int64_t B,
+                  int64_t H, int32_t mode, uint64_t seed_base, const int64_t *seed_ids,
+                  const int32_t *host_tuples, double thresh, size_t extra, PairsDev *d) {
+  if (!c || !off || !d) return fail(RS_EINVAL, "null pointer");
   if (B < 1 || B > (1 << 20)) return fail(RS_EINVAL, "bad pair count");
   if (H < 1 || H > (1 << 24) || B * H > (1LL << 31) - 64)
     return fail(RS_EINVAL, "bad hypothesis count");
@@ -327,7 +329,7 @@ extern "C" int rs_pairs_f8_ransac(rs_ctx *c, const double *p1, const double *p2,
                           sizeof(double) * ld,          sizeof(rsd::PairDevResult) * B,
                           sizeof(int32_t) * tp,
                           mode == RS_SAMPLER_TUPLES ? sizeof(int32_t) * 8 * ld : 0,
-                          seed_ids ? sizeof(int64_t) * B : 0};
+                          seed_ids ? sizeof(int64_t) * B : 0, extra};
   size_t tot = 0;
   for (size_t s : sizes) tot += al(s);
   int st = rs::ensure_scratch(c, tot + 256);
@@ -376,9 +378,29 @@ extern "C" int rs_pairs_f8_ransac(rs_ctx *c, const double *p1, const double *p2,
                      c->stream, d_pts, d_off, static_cast<int>(H), d_F, ld, d_counts, thresh,
                      d_cand, d_nrm, d_cnorm, d_res, d_inl);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(out, d_res, sizeof(rs_pair_result) * B, hipMemcpyDeviceToHost, c->stream));
-  if (total > 0)
-    HIP_TRY(hipMemcpyAsync(inliers, d_inl, sizeof(int32_t) * total, hipMemcpyDeviceToHost,
+  d->pts = d_pts;
+  d->off = d_off;
+  d->res = d_res;
+  d->inl = d_inl;
+  d->total = total;
+  d->extra = buf[11];
+  return RS_OK;
+}
+}  // namespace rs
+
+extern "C" int rs_pairs_f8_ransac(rs_ctx *c, const double *p1, const double *p2,
+                                  const int64_t *off, int64_t B, int64_t H, int32_t mode,
+                                  uint64_t seed_base, const int64_t *seed_ids,
+                                  const int32_t *host_tuples, double thresh,
+                                  rs_pair_result *out, int32_t *inliers) {
+  if (!out || !inliers) return fail(RS_EINVAL, "null pointer");
+  rs::PairsDev d{};
+  const int st = rs::pairs_enqueue(c, p1, p2, off, B, H, mode, seed_base, seed_ids, host_tuples,
+                                   thresh, 0, &d);
+  if (st) return st;
+  HIP_TRY(hipMemcpyAsync(out, d.res, sizeof(rs_pair_result) * B, hipMemcpyDeviceToHost, c->stream));
+  if (d.total > 0)
+    HIP_TRY(hipMemcpyAsync(inliers, d.inl, sizeof(int32_t) * d.total, hipMemcpyDeviceToHost,
                            c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return RS_OK;

@@ -128,15 +128,19 @@ __global__ __launch_bounds__(128) void k_essential(const double *__restrict__ K,
 __global__ __launch_bounds__(128) void k_relative_pose(const double *__restrict__ Es, const double *__restrict__ y1,
                                 const double *__restrict__ y2, int64_t Bn,
                                 double *__restrict__ Rout, double *__restrict__ tout,
-                                int32_t *__restrict__ found) {
+                                int32_t *__restrict__ found,
+                                const int32_t *__restrict__ act = nullptr) {
   const int64_t gt = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const int64_t i0 = gt >> 2;
   const int k = static_cast<int>(gt & 3);
   const bool live = i0 < Bn;
   const int64_t i = live ? i0 : Bn - 1;  // padding quads recompute the last pair, store nothing
+  // (act: pairs with act[i] == 0 have no E -- rs_pairs_two_view's pairs without a consensus:
+  // a stand-in E, no candidate passes, NaN pose and found 0)
+  const bool skip = act && !act[i];
   double B[9], V[9];
 #pragma unroll
-  for (int q = 0; q < 9; ++q) B[q] = Es[9 * i + q];
+  for (int q = 0; q < 9; ++q) B[q] = skip ? (q == 0 || q == 4 ? 1.0 : 0.0) : Es[9 * i + q];
   svd3_jacobi(B, V);
   double s[3];
 #pragma unroll
@@ -186,7 +190,7 @@ __global__ __launch_bounds__(128) void k_relative_pose(const double *__restrict_
   double X[3];
   triangulate_optimal(I34, C2, y1[2 * i], y1[2 * i + 1], y2[2 * i], y2[2 * i + 1], X);
   const double z2 = Rk[6] * X[0] + Rk[7] * X[1] + Rk[8] * X[2] + sg * v3[2];
-  const bool pass = X[2] > 0.0 && z2 > 0.0;
+  const bool pass = !skip && X[2] > 0.0 && z2 > 0.0;
   // quad lanes 4j..4j+3 hold k = 0..3 of one pair (the grid is a multiple of 4 lanes)
   const unsigned long long bal = __ballot(pass);
   const int q0 = (threadIdx.x & 63) & ~3;
@@ -467,7 +471,7 @@ __global__ __launch_bounds__(T) void k_gold_standard(
     const double *__restrict__ Fin, const double *__restrict__ pl, const double *__restrict__ pr,
     int64_t total, const int64_t *__restrict__ off, int max_iter, double *__restrict__ Xb,
     double *__restrict__ Xc, double *__restrict__ Wb, double *__restrict__ Fout,
-    double *__restrict__ C1out, GsInfo *__restrict__ info) {
+    double *__restrict__ C1out, GsInfo *__restrict__ info, const int32_t *__restrict__ act) {
   __shared__ double red[(T / 64) * 128];
   __shared__ double sU[78], sgc[12], sres[94], sC[12], sdc[12];
   __shared__ double s_lam, s_nu, s_cost, s_cost0;
@@ -479,6 +483,11 @@ __global__ __launch_bounds__(T) void k_gold_standard(
   const double *prx = pr + j0, *pry = pr + total + j0;
   double *X = Xb + 3 * j0, *XN = Xc + 3 * j0, *W = Wb + kPerPt * j0;
   const double I34[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+  if (act && !act[blockIdx.x]) {  // (rs_pairs_two_view: a pair without a consensus)
+    if (tid < 9) Fout[9 * blockIdx.x + tid] = __builtin_nan("");
+    if (tid == 0) info[blockIdx.x] = GsInfo{0.0, 0.0, 0, 0, 0, 0};
+    return;
+  }
 
   if (tid == 0) {
     double f[9], c[12];
@@ -729,6 +738,81 @@ __global__ __launch_bounds__(T) void k_gold_standard(
   }
 }
 
+// ---- rs_pairs_two_view: the pair records -> the gold standard, on the device ----------------
+// (parallel._pairs_arrays' host steps between rs_pairs_f8_ransac and rs_gold_standard)
+struct PairRec {  // == rs_pair_result
+  double F[9];
+  int64_t best_index, best_count;
+  double best_std, best_norm;
+  int64_t n_candidates;
+};
+
+// Which pairs refine (a consensus: best_index >= 0 and best_count > 0), where their inliers go
+// in the gathered arrays (goff: exclusive scan of the counts in pair order, goff[B] = total)
+// and F_RANSAC in the gold standard's (B, 9) layout.  One workgroup, 1 024 pairs a round.
+__global__ __launch_bounds__(1024) void k_twoview_prep(const PairRec *__restrict__ res, int64_t B,
+                                                       int64_t *__restrict__ goff,
+                                                       int32_t *__restrict__ act,
+                                                       double *__restrict__ Fin) {
+  __shared__ long long sw[16];
+  __shared__ long long s_carry;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid == 0) s_carry = 0;
+  __syncthreads();
+  for (int64_t b0 = 0; b0 < B; b0 += 1024) {
+    const int64_t b = b0 + tid;
+    long long v = 0;
+    if (b < B) {
+      const PairRec &r = res[b];
+      const bool a = r.best_index >= 0 && r.best_count > 0;
+      act[b] = a ? 1 : 0;
+      v = a ? r.best_count : 0;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) Fin[9 * b + q] = r.F[q];
+    }
+    long long x = v;  // inclusive wave scan
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const long long y = __shfl_up(x, d);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) sw[w] = x;
+    __syncthreads();
+    long long pre = s_carry, tot = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      pre += q < w ? sw[q] : 0;
+      tot += sw[q];
+    }
+    if (b < B) goff[b] = pre + x - v;
+    __syncthreads();
+    if (tid == 0) s_carry += tot;
+    __syncthreads();
+  }
+  if (tid == 0) goff[B] = s_carry;
+}
+
+// The refining pairs' inlier points, gathered in S_RANSAC order into the gold standard's
+// (2, tp) arrays (row stride tp >= goff[B]): a wave per pair.
+__global__ __launch_bounds__(64) void k_twoview_gather(const Pt *__restrict__ pts,
+                                                       const int64_t *__restrict__ off,
+                                                       const int32_t *__restrict__ inl,
+                                                       const int64_t *__restrict__ goff,
+                                                       const int32_t *__restrict__ act, int64_t tp,
+                                                       double *__restrict__ pl,
+                                                       double *__restrict__ pr) {
+  const int64_t b = blockIdx.x;
+  if (!act[b]) return;
+  const int64_t o = off[b], g = goff[b], k = goff[b + 1] - g;
+  for (int64_t j = threadIdx.x; j < k; j += 64) {
+    const Pt P = pts[o + inl[o + j]];
+    pl[g + j] = P.x1;
+    pl[tp + g + j] = P.y1;
+    pr[g + j] = P.x2;
+    pr[tp + g + j] = P.y2;
+  }
+}
+
 }  // namespace rsd
 
 // ------------------------------------------------------------------------------------------
@@ -937,7 +1021,7 @@ extern "C" int rs_gold_standard(rs_ctx *c, const double *F, const double *pl, co
                      reinterpret_cast<int64_t *>(b[3]), max_iter, reinterpret_cast<double *>(b[4]),
                      reinterpret_cast<double *>(b[5]), reinterpret_cast<double *>(b[6]),
                      reinterpret_cast<double *>(b[7]), reinterpret_cast<double *>(b[8]),
-                     reinterpret_cast<rsd::GsInfo *>(b[9]));
+                     reinterpret_cast<rsd::GsInfo *>(b[9]), nullptr);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(F_gold, b[7], sizeof(double) * 9 * B, hipMemcpyDeviceToHost, c->stream));
   if (C1_out)
@@ -979,5 +1063,98 @@ extern "C" int rs_gs_residuals_fd(rs_ctx *c, const double *x, const double *xp, 
   HIP_TRY(hipMemcpyAsync(f, b[5], sizeof(double) * nr, hipMemcpyDeviceToHost, c->stream));
   if (J) HIP_TRY(hipMemcpyAsync(J, b[6], jb, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  return RS_OK;
+}
+
+static_assert(sizeof(rsd::PairRec) == sizeof(rs_pair_result), "rs_pair_result layout");
+
+extern "C" int rs_pairs_two_view(rs_ctx *c, const double *p1, const double *p2, const int64_t *off,
+                                 int64_t B, int64_t H, int32_t mode, uint64_t seed_base,
+                                 const int64_t *seed_ids, const int32_t *host_tuples,
+                                 double thresh, int32_t max_iter, const double *K,
+                                 const double *y1, const double *y2, rs_pair_result *out,
+                                 int32_t *inliers, double *F_gold, rs_gs_info *info, double *R,
+                                 double *t, int32_t *found) {
+  if (!out || !inliers || !F_gold || !info || !R || !t || !found)
+    return fail(RS_EINVAL, "null pointer");
+  if (K && (!y1 || !y2)) return fail(RS_EINVAL, "K needs y1 and y2");
+  if (max_iter < 1 || max_iter > 100000) return fail(RS_EINVAL, "max_iter must be in [1, 1e5]");
+  if (!off || B < 1 || B > (1 << 20)) return fail(RS_EINVAL, "bad pair count");
+  const int64_t tp = off[B] > 0 ? off[B] : 1;
+  // the stages' buffers after the pair RANSAC's, then the output block (one download)
+  const size_t sz[] = {sizeof(int64_t) * (B + 1), sizeof(int32_t) * B, sizeof(double) * 9 * B,
+                       sizeof(double) * 2 * tp,   sizeof(double) * 2 * tp,
+                       sizeof(double) * 3 * tp,   sizeof(double) * 3 * tp,
+                       sizeof(double) * rsd::kPerPt * tp, sizeof(double) * 9,
+                       sizeof(double) * 2 * B,    sizeof(double) * 2 * B, sizeof(double) * 9 * B};
+  const size_t osz[] = {sizeof(double) * 9 * B, sizeof(rs_gs_info) * B, sizeof(double) * 9 * B,
+                        sizeof(double) * 3 * B, sizeof(int32_t) * B};
+  size_t extra = 0, oblk = 0;
+  for (size_t x : sz) extra += al(x);
+  for (size_t x : osz) oblk += al(x);
+  rs::PairsDev d{};
+  int st = rs::pairs_enqueue(c, p1, p2, off, B, H, mode, seed_base, seed_ids, host_tuples,
+                             thresh, extra + oblk, &d);
+  if (st) return st;
+  std::vector<char *> b;
+  char *p = d.extra;
+  for (size_t x : sz) {
+    b.push_back(p);
+    p += al(x);
+  }
+  char *ob = p;
+  std::vector<char *> o;
+  for (size_t x : osz) {
+    o.push_back(p);
+    p += al(x);
+  }
+  auto *goff = reinterpret_cast<int64_t *>(b[0]);
+  auto *act = reinterpret_cast<int32_t *>(b[1]);
+  auto *Fin = reinterpret_cast<double *>(b[2]);
+  auto *pl = reinterpret_cast<double *>(b[3]), *pr = reinterpret_cast<double *>(b[4]);
+  auto *dK = reinterpret_cast<double *>(b[8]);
+  auto *dy1 = reinterpret_cast<double *>(b[9]), *dy2 = reinterpret_cast<double *>(b[10]);
+  auto *dE = reinterpret_cast<double *>(b[11]);
+  auto *dFg = reinterpret_cast<double *>(o[0]);
+  auto *dinfo = reinterpret_cast<rsd::GsInfo *>(o[1]);
+  auto *dR = reinterpret_cast<double *>(o[2]), *dt = reinterpret_cast<double *>(o[3]);
+  auto *dfound = reinterpret_cast<int32_t *>(o[4]);
+  hipStream_t s = c->stream;
+  if (K) {
+    HIP_TRY(hipMemcpyAsync(dK, K, sizeof(double) * 9, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(dy1, y1, sizeof(double) * 2 * B, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(dy2, y2, sizeof(double) * 2 * B, hipMemcpyHostToDevice, s));
+  }
+  hipLaunchKernelGGL(rsd::k_twoview_prep, dim3(1), dim3(1024), 0, s,
+                     static_cast<const rsd::PairRec *>(d.res), B, goff, act, Fin);
+  hipLaunchKernelGGL(rsd::k_twoview_gather, dim3(static_cast<unsigned>(B)), dim3(64), 0, s,
+                     static_cast<const rsd::Pt *>(d.pts), d.off, d.inl, goff, act, tp, pl, pr);
+  hipLaunchKernelGGL(rsd::k_gold_standard<rsd::kGsT>, dim3(static_cast<unsigned>(B)), dim3(rsd::kGsT),
+                     0, s, Fin, pl, pr, tp, goff, max_iter, reinterpret_cast<double *>(b[5]),
+                     reinterpret_cast<double *>(b[6]), reinterpret_cast<double *>(b[7]), dFg,
+                     nullptr, dinfo, act);
+  if (K) {
+    hipLaunchKernelGGL(rsd::k_essential, dim3(grid(B)), dim3(128), 0, s, dK, 0, dFg, B, dE);
+    hipLaunchKernelGGL(rsd::k_relative_pose, dim3(grid(4 * B)), dim3(128), 0, s, dE, dy1, dy2, B,
+                       dR, dt, dfound, act);
+  }
+  HIP_TRY(hipGetLastError());
+  std::vector<char> host(static_cast<size_t>(p - ob));
+  HIP_TRY(hipMemcpyAsync(out, d.res, sizeof(rs_pair_result) * B, hipMemcpyDeviceToHost, s));
+  if (d.total > 0)
+    HIP_TRY(hipMemcpyAsync(inliers, d.inl, sizeof(int32_t) * d.total, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(host.data(), ob, host.size(), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  std::memcpy(F_gold, host.data() + (o[0] - ob), osz[0]);
+  std::memcpy(info, host.data() + (o[1] - ob), osz[1]);
+  if (K) {
+    std::memcpy(R, host.data() + (o[2] - ob), osz[2]);
+    std::memcpy(t, host.data() + (o[3] - ob), osz[3]);
+    std::memcpy(found, host.data() + (o[4] - ob), osz[4]);
+  } else {
+    for (int64_t i = 0; i < 9 * B; ++i) R[i] = __builtin_nan("");
+    for (int64_t i = 0; i < 3 * B; ++i) t[i] = __builtin_nan("");
+    std::memset(found, 0, sizeof(int32_t) * B);
+  }
   return RS_OK;
 }

@@ -121,6 +121,10 @@ _SIGS = {
     "rs_pairs_f8_ransac": (C.c_int, [C.c_void_p, _dp, _dp, _i64p, C.c_int64, C.c_int64,
                                      C.c_int32, C.c_uint64, _i64p, _i32p, C.c_double,
                                      C.POINTER(PairResult), _i32p]),
+    "rs_pairs_two_view": (C.c_int, [C.c_void_p, _dp, _dp, _i64p, C.c_int64, C.c_int64,
+                                    C.c_int32, C.c_uint64, _i64p, _i32p, C.c_double, C.c_int32,
+                                    _dp, _dp, _dp, C.POINTER(PairResult), _i32p, _dp,
+                                    C.POINTER(GsInfo), _dp, _dp, _i32p]),
     "rs_triangulate_optimal": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, _dp, _i32p,
                                          C.c_int64, _dp]),
     "rs_camera_resectioning": (C.c_int, [C.c_void_p, _dp, C.c_int64, _dp, _dp, _dp]),

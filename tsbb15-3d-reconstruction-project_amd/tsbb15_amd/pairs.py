@@ -114,6 +114,55 @@ def ransac_pairs_raw(p1, p2, off, H, seed_base=1000, thresh=1.5, ids=None, ctx=N
     return np.frombuffer(res, dtype=PAIR_RESULT_DTYPE).copy(), inl
 
 
+def two_view_pairs_raw(p1, p2, off, H, K=None, seed_base=1000, thresh=1.5, ids=None,
+                       max_iter=None, ctx=None):
+    """ransac_pairs_raw, then -- on the device, in the same call (rs_pairs_two_view) -- the
+    gold standard of every pair with a consensus and, given K, E = K^T F_gold K and the
+    relative pose from the pair's first correspondence (main.py:50-63).  Returns (results
+    PAIR_RESULT_DTYPE, inliers, F_gold (B, 9), info GS_INFO_DTYPE, R (B, 9), t (B, 3), found
+    (B,)); F_gold / R / t are NaN and found 0 where there is no consensus."""
+    p1, p2 = _ffi.f64c(p1), _ffi.f64c(p2)
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    B = len(off) - 1
+    if p1.shape != p2.shape or p1.ndim != 2 or p1.shape[0] != 2 or p1.shape[1] != int(off[-1]):
+        raise ValueError('p1, p2 must be (2, off[-1])')
+    ip = None
+    if ids is not None:
+        ids = np.ascontiguousarray(ids, dtype=np.int64)
+        if ids.shape != (B,):
+            raise ValueError('ids must be (B,)')
+        ip = _ffi.ptr(ids, _ffi.C.c_int64)
+    Kp = y1p = y2p = None
+    if K is not None:
+        K = _ffi.f64c(K).reshape(3, 3)
+        # each pair's first correspondence, C-normalised on the host point by point
+        # (twoview.normalise_each): the same bits as GpuPairRefiner's three-call path
+        n = np.diff(off)
+        first = np.where(n > 0, off[:-1], 0)
+        y1 = np.zeros((B, 2))
+        y2 = np.zeros((B, 2))
+        if int(off[-1]) > 0:
+            y1 = np.ascontiguousarray(twoview.normalise_each(K, p1[:, first].T)[:, :2])
+            y2 = np.ascontiguousarray(twoview.normalise_each(K, p2[:, first].T)[:, :2])
+        Kp, y1p, y2p = _ffi.ptr(K, _ffi.C.c_double), _ffi.ptr(y1, _ffi.C.c_double), \
+            _ffi.ptr(y2, _ffi.C.c_double)
+    res = (_ffi.PairResult * B)()
+    info = (_ffi.GsInfo * B)()
+    inl = np.empty(max(int(off[-1]), 1), dtype=np.int32)
+    Fg, R, t = np.empty((B, 9)), np.empty((B, 9)), np.empty((B, 3))
+    found = np.empty(B, dtype=np.int32)
+    d = _ffi.C.c_double
+    _ffi.check(_ffi.lib().rs_pairs_two_view(
+        (ctx or _ffi.default_context()).handle, _ffi.ptr(p1, d), _ffi.ptr(p2, d),
+        _ffi.ptr(off, _ffi.C.c_int64), B, int(H), _ffi.SAMPLER_PHILOX,
+        int(seed_base) & (2**64 - 1), ip, None, float(thresh),
+        int(twoview.MAX_ITER if max_iter is None else max_iter), Kp, y1p, y2p, res,
+        _ffi.ptr(inl, _ffi.C.c_int32), _ffi.ptr(Fg, d), info, _ffi.ptr(R, d), _ffi.ptr(t, d),
+        _ffi.ptr(found, _ffi.C.c_int32)))
+    return (np.frombuffer(res, dtype=PAIR_RESULT_DTYPE).copy(), inl, Fg,
+            np.frombuffer(info, dtype=twoview.GS_INFO_DTYPE).copy(), R, t, found)
+
+
 @dataclass
 class PairGeometry:
     ransac: PairRansac
@@ -141,8 +190,8 @@ def two_view_pairs(pairs, H, K=None, seed_base=1000, thresh=1.5, tuples=None, id
     if K is not None:
         K = np.asarray(K, dtype=np.float64)
         E = twoview.essential_batch(K, np.stack([g.F for g in gs]), ctx=ctx)
-        y1 = twoview.MakeHomogenous(K, np.stack([np.asarray(pairs[b][0])[:, 0] for b in ok]))
-        y2 = twoview.MakeHomogenous(K, np.stack([np.asarray(pairs[b][1])[:, 0] for b in ok]))
+        y1 = twoview.normalise_each(K, np.stack([np.asarray(pairs[b][0])[:, 0] for b in ok]))
+        y2 = twoview.normalise_each(K, np.stack([np.asarray(pairs[b][1])[:, 0] for b in ok]))
         R, t, found = twoview.relative_camera_pose_batch(E, y1[:, :2], y2[:, :2], ctx=ctx)
         for k, b in enumerate(ok):
             if found[k]:

@@ -709,6 +709,13 @@ class GpuPairBatchSolver:
         return pairs_mod.ransac_pairs_raw(p1, p2, off, self.H, self.seed_base, self.thresh,
                                           ids=ids, ctx=self.ctx)
 
+    def many_two_view(self, ids, p1, p2, off, K):
+        """many_arrays and a GpuPairRefiner's stages in one device call (rs_pairs_two_view):
+        (results, inliers, F_gold (B,9), gs info, R (B,9), t (B,3), found (B,))."""
+        from . import pairs as pairs_mod
+        return pairs_mod.two_view_pairs_raw(p1, p2, off, self.H, K, self.seed_base, self.thresh,
+                                            ids=ids, ctx=self.ctx)
+
     def many(self, ids, pairs):
         from . import pairs as pairs_mod
         if not ids:
@@ -725,9 +732,12 @@ class GpuPairRefiner:
     the relative pose from the pair's first correspondence (fun.py:91-102, 209-258, as
     main.py:50-63 does for the initial pair)."""
 
-    def __init__(self, ctx, K=None):
+    def __init__(self, ctx, K=None, fused=True):
         self.ctx = ctx
         self.K = None if K is None else np.ascontiguousarray(K, dtype=np.float64)
+        # run_pairs with a GpuPairBatchSolver on the same context: RANSAC and these stages in
+        # one device call (the inlier points never leave the GPU); False: separate calls
+        self.fused = fused
 
     def arrays(self, F, pl, pr, off, first1, first2):
         """The same on arrays: F (B,9) F_RANSAC, the inlier points concatenated (pl, pr
@@ -741,8 +751,8 @@ class GpuPairRefiner:
             return (Fg.reshape(B, 9), info["cost"], np.zeros(B, dtype=np.int64),
                     np.full((B, 9), np.nan), np.full((B, 3), np.nan))
         E = twoview.essential_batch(self.K, Fg, ctx=self.ctx)
-        y1 = twoview.MakeHomogenous(self.K, first1)[:, :2]
-        y2 = twoview.MakeHomogenous(self.K, first2)[:, :2]
+        y1 = twoview.normalise_each(self.K, first1)[:, :2]
+        y2 = twoview.normalise_each(self.K, first2)[:, :2]
         R, t, found = twoview.relative_camera_pose_batch(E, y1, y2, ctx=self.ctx)
         return Fg.reshape(B, 9), info["cost"], found, R.reshape(B, 9), t
 
@@ -758,8 +768,8 @@ class GpuPairRefiner:
         if self.K is None:
             return [(g.F.ravel(), g.cost, 0, nan9, nan3) for g in gs]
         E = twoview.essential_batch(self.K, Fg, ctx=self.ctx)
-        y1 = twoview.MakeHomogenous(self.K, np.stack([it[4] for it in items]))[:, :2]
-        y2 = twoview.MakeHomogenous(self.K, np.stack([it[5] for it in items]))[:, :2]
+        y1 = twoview.normalise_each(self.K, np.stack([it[4] for it in items]))[:, :2]
+        y2 = twoview.normalise_each(self.K, np.stack([it[5] for it in items]))[:, :2]
         R, t, found = twoview.relative_camera_pose_batch(E, y1, y2, ctx=self.ctx)
         return [(g.F.ravel(), g.cost, int(f), R[k].ravel(), t[k])
                 for k, (g, f) in enumerate(zip(gs, found))]
@@ -827,14 +837,21 @@ def _pairs_arrays(pairs, H, mine, ns_all, solve, refine, recs):
     np.cumsum(ns_all[idx], out=off[1:])
     p1 = np.hstack([pairs[i][0] for i in mine]).astype(np.float64, copy=False)
     p2 = np.hstack([pairs[i][1] for i in mine]).astype(np.float64, copy=False)
+    if (refine is not None and getattr(refine, "fused", False) and hasattr(solve, "many_two_view")
+            and getattr(refine, "ctx", None) is getattr(solve, "ctx", None)):
+        res, _, Fg, info, R, t, found = solve.many_two_view(idx, p1, p2, off, refine.K)
+        _fill_ransac(recs, idx, res)
+        sel = np.flatnonzero((res["best_index"] >= 0) & (res["best_count"] > 0))
+        ri = idx[sel]
+        recs["refined"][ri] = 1
+        recs["F_gold"][ri] = Fg[sel]
+        recs["gs_cost"][ri] = info["cost"][sel]
+        recs["pose"][ri] = found[sel]
+        recs["R"][ri] = R[sel]
+        recs["t"][ri] = t[sel]
+        return
     res, inl = solve.many_arrays(idx, p1, p2, off)
-    valid = res["best_index"] >= 0
-    cnt = np.where(valid, res["best_count"], 0)
-    recs["valid"][idx] = valid
-    recs["best_index"][idx] = res["best_index"]
-    recs["count"][idx] = cnt
-    recs["std"][idx] = res["best_std"]
-    recs["F"][idx] = res["F"]
+    valid, cnt = _fill_ransac(recs, idx, res)
     sel = np.flatnonzero(valid & (cnt > 0))
     if refine is None or len(sel) == 0:
         return
@@ -852,6 +869,18 @@ def _pairs_arrays(pairs, H, mine, ns_all, solve, refine, recs):
     recs["pose"][ri] = found
     recs["R"][ri] = R
     recs["t"][ri] = t
+
+
+def _fill_ransac(recs, idx, res):
+    """The RANSAC columns of the rank's records from a PAIR_RESULT_DTYPE array."""
+    valid = res["best_index"] >= 0
+    cnt = np.where(valid, res["best_count"], 0)
+    recs["valid"][idx] = valid
+    recs["best_index"][idx] = res["best_index"]
+    recs["count"][idx] = cnt
+    recs["std"][idx] = res["best_std"]
+    recs["F"][idx] = res["F"]
+    return valid, cnt
 
 
 def _pairs_gather(comm, pairs, owners, recs):

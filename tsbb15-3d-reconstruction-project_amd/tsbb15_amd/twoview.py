@@ -142,6 +142,17 @@ def MakeHomogenous(K, coord):
     return np.linalg.solve(np.asarray(K, dtype=np.float64), h).T
 
 
+def normalise_each(K, coord):
+    """MakeHomogenous(K, [p])[0] for each row p of coord (n, 2) -- the C-normalised first
+    correspondence main.py:59-63 passes to relative_camera_pose -- as a one-right-hand-side
+    solve per point, so a point's bits do not depend on how many are normalised together
+    (LAPACK's multi-RHS kernels may round differently: the batched pair paths must agree)."""
+    coord = np.asarray(coord, dtype=np.float64).reshape(-1, 2)
+    h = np.concatenate([coord, np.ones((coord.shape[0], 1))], axis=1)[..., None]
+    K = np.asarray(K, dtype=np.float64)
+    return np.linalg.solve(np.broadcast_to(K, (coord.shape[0], 3, 3)), h)[..., 0]
+
+
 def relative_camera_pose_batch(E, y1, y2, ctx=None):
     """fun.relative_camera_pose over pairs: E (B,3,3), y1, y2 (B,2).  Returns R (B,3,3),
     t (B,3), found (B,) int32 (0 where the reference returns None)."""
