@@ -30,7 +30,7 @@ def spy(Fs, pl, pr, off, **kw):
 
 twoview.gold_standard_arrays = spy
 parallel.run_pairs(probe_c4._Solo(), pairs, 1000, parallel.GpuPairBatchSolver(ctx, 1000),
-                   refine=parallel.GpuPairRefiner(ctx, z["K_last"]))
+                   refine=parallel.GpuPairRefiner(ctx, z["K_last"], fused=False))
 n = np.diff(captured["off"])
 it = captured["info"]["iterations"]
 print("pairs", len(n), "n: max", n.max(), "mean %.1f" % n.mean(), ">64:", int((n > 64).sum()), ">256:", int((n > 256).sum()))

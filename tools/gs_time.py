@@ -30,7 +30,7 @@ def spy(Fs, pl, pr, off, **kw):
 
 twoview.gold_standard_arrays = spy
 parallel.run_pairs(probe_c4._Solo(), pairs, 1000, parallel.GpuPairBatchSolver(ctx, 1000),
-                   refine=parallel.GpuPairRefiner(ctx, z["K_last"]))
+                   refine=parallel.GpuPairRefiner(ctx, z["K_last"], fused=False))
 twoview.gold_standard_arrays = orig
 for mi in (1, 2, 3, 5, 10, 500):
     ts = []

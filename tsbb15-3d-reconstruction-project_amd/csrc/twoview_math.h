@@ -236,6 +236,9 @@ __device__ __forceinline__ void triangulate_linear(const double *C1, const doubl
 // Generic degree-N form: g descending (g[0] the z^N coefficient).  Leading zeros lower the
 // degree, trailing zeros are roots at 0 (not iterated): returns the iterated degree `deg`,
 // with the roots in zr / zi[0 .. deg), and the number of zero roots in `trailing`.
+#ifndef RSAMD_ABERTH_MAX
+#define RSAMD_ABERTH_MAX 100  // sweep cap (A/B builds may lower it to time the tail)
+#endif
 template <int N>
 __device__ __forceinline__ int aberth_roots(const double (&g)[N + 1], double (&zr)[N],
                                             double (&zi)[N], int &trailing) {
@@ -280,7 +283,7 @@ __device__ __forceinline__ int aberth_roots(const double (&g)[N + 1], double (&z
       }
     }
     unsigned conv = 0, all = (1u << deg) - 1u;
-    for (int it = 0; it < 100 && conv != all; ++it) {
+    for (int it = 0; it < RSAMD_ABERTH_MAX && conv != all; ++it) {
       for (int k = 0; k < deg; ++k) {
         if (conv & (1u << k)) continue;
         const double xr = zr[k], xi = zi[k];
