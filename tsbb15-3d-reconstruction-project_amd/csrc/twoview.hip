@@ -188,7 +188,7 @@ __global__ __launch_bounds__(128) void k_relative_pose(const double *__restrict_
     C2[4 * r + 3] = sg * v3[r];
   }
   double X[3];
-  triangulate_optimal(I34, C2, y1[2 * i], y1[2 * i + 1], y2[2 * i], y2[2 * i + 1], X);
+  triangulate_optimal<true>(I34, C2, y1[2 * i], y1[2 * i + 1], y2[2 * i], y2[2 * i + 1], X);
   const double z2 = Rk[6] * X[0] + Rk[7] * X[1] + Rk[8] * X[2] + sg * v3[2];
   const bool pass = !skip && X[2] > 0.0 && z2 > 0.0;
   // quad lanes 4j..4j+3 hold k = 0..3 of one pair (the grid is a multiple of 4 lanes)
@@ -245,6 +245,9 @@ __global__ __launch_bounds__(128) void k_fmatrix_from_cameras(const double *__re
 #define RSAMD_GS_T 256  // threads per pair (A/B: 64; r05c4a: 463 vs 561 us per C4 launch)
 #endif
 constexpr int kGsT = RSAMD_GS_T;
+#ifndef RSAMD_GS_WAVE
+#define RSAMD_GS_WAVE 1  // pairs of <= 64 inliers on one wave (A/B: 0)
+#endif
 constexpr int kPerPt = 45;  // W (12x3), V (3x3 upper: 6), gx (3)
 
 // Index of (r, c), r <= c, in a packed upper-triangular 12x12.
@@ -260,6 +263,20 @@ __device__ __forceinline__ void rs_halve(const double (&x)[N], double (&y)[N / 2
     const double send = up ? x[i] : x[i + N / 2];
     const double keep = up ? x[i + N / 2] : x[i];
     y[i] = keep + __shfl_xor(send, o);
+  }
+}
+
+// The gold standard's barrier: a workgroup barrier, or for a one-wave pair (T == 64: the
+// workgroup's other waves have left) a wave-level LDS fence -- no s_barrier across waves that
+// have exited.  Points are owned by one thread in every phase, so only LDS is shared.
+template <int T>
+__device__ __forceinline__ void gs_sync() {
+  if constexpr (T == 64) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    __syncthreads();
   }
 }
 
@@ -285,18 +302,18 @@ __device__ __forceinline__ void block_reduce(double (&v)[K], double *scratch, do
 #pragma unroll
       for (int i = 0; i < 2; ++i)
         if (2 * lane + i < K) out[2 * lane + i] = f[i];
-      __syncthreads();
+      gs_sync<T>();
     } else {
 #pragma unroll
       for (int i = 0; i < 2; ++i) scratch[w * 128 + 2 * lane + i] = f[i];
-      __syncthreads();
+      gs_sync<T>();
       for (int k = threadIdx.x; k < K; k += T) {
         double s = 0.0;
 #pragma unroll
         for (int q = 0; q < T / 64; ++q) s += scratch[q * 128 + k];
         out[k] = s;
       }
-      __syncthreads();
+      gs_sync<T>();
     }
   } else {
 #pragma unroll
@@ -306,14 +323,14 @@ __device__ __forceinline__ void block_reduce(double (&v)[K], double *scratch, do
       for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
       if (lane == 0) scratch[w * K + k] = x;
     }
-    __syncthreads();
+    gs_sync<T>();
     for (int k = threadIdx.x; k < K; k += T) {
       double s = 0.0;
 #pragma unroll
       for (int q = 0; q < T / 64; ++q) s += scratch[q * K + k];
       out[k] = s;
     }
-    __syncthreads();
+    gs_sync<T>();
   }
 }
 
@@ -466,12 +483,13 @@ __global__ __launch_bounds__(128) void k_gs_fd(const double *__restrict__ x,
   }
 }
 
+// One pair's gold standard by the workgroup's first T threads (T = 64: one wave)
 template <int T>
-__global__ __launch_bounds__(T) void k_gold_standard(
+__device__ __forceinline__ void gs_pair(
     const double *__restrict__ Fin, const double *__restrict__ pl, const double *__restrict__ pr,
     int64_t total, const int64_t *__restrict__ off, int max_iter, double *__restrict__ Xb,
     double *__restrict__ Xc, double *__restrict__ Wb, double *__restrict__ Fout,
-    double *__restrict__ C1out, GsInfo *__restrict__ info, const int32_t *__restrict__ act) {
+    double *__restrict__ C1out, GsInfo *__restrict__ info) {
   __shared__ double red[(T / 64) * 128];
   __shared__ double sU[78], sgc[12], sres[94], sC[12], sdc[12];
   __shared__ double s_lam, s_nu, s_cost, s_cost0;
@@ -483,11 +501,6 @@ __global__ __launch_bounds__(T) void k_gold_standard(
   const double *prx = pr + j0, *pry = pr + total + j0;
   double *X = Xb + 3 * j0, *XN = Xc + 3 * j0, *W = Wb + kPerPt * j0;
   const double I34[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
-  if (act && !act[blockIdx.x]) {  // (rs_pairs_two_view: a pair without a consensus)
-    if (tid < 9) Fout[9 * blockIdx.x + tid] = __builtin_nan("");
-    if (tid == 0) info[blockIdx.x] = GsInfo{0.0, 0.0, 0, 0, 0, 0};
-    return;
-  }
 
   if (tid == 0) {
     double f[9], c[12];
@@ -500,13 +513,13 @@ __global__ __launch_bounds__(T) void k_gold_standard(
     s_acc = 0;
     s_status = 0;
   }
-  __syncthreads();
+  gs_sync<T>();
   double C[12];
 #pragma unroll
   for (int q = 0; q < 12; ++q) C[q] = sC[q];
   for (int j = tid; j < n; j += T)
-    triangulate_optimal(C, I34, plx[j], ply[j], prx[j], pry[j], X + 3 * j);
-  __syncthreads();
+    triangulate_optimal<true>(C, I34, plx[j], ply[j], prx[j], pry[j], X + 3 * j);
+  gs_sync<T>();
 
   bool relinearize = true;
   for (;;) {
@@ -549,7 +562,7 @@ __global__ __launch_bounds__(T) void k_gold_standard(
         if (s_it == 0) s_cost0 = s_cost;
         s_it += 1;
       }
-      __syncthreads();
+      gs_sync<T>();
       relinearize = false;
     }
     const double lam = s_lam;
@@ -627,7 +640,7 @@ __global__ __launch_bounds__(T) void k_gold_standard(
       for (int p = 0; p < 12; ++p) sdc[p] = ok ? y[p] : 0.0;
       s_state = ok ? 0 : 1;
     }
-    __syncthreads();
+    gs_sync<T>();
     bool accepted = false, stop = false;
     if (s_state == 0) {
       // ---- point steps, candidate cost, predicted reduction, step / parameter norms ----
@@ -695,7 +708,7 @@ __global__ __launch_bounds__(T) void k_gold_standard(
           if (pred >= 0.0 && pred <= 1e-15 * cost) s_status = 2;
         }
       }
-      __syncthreads();
+      gs_sync<T>();
     }
     if (s_state >= 2) {
       accepted = true;
@@ -714,7 +727,7 @@ __global__ __launch_bounds__(T) void k_gold_standard(
         if (s_lam > 1e32) s_status = 2;
       }
     }
-    __syncthreads();
+    gs_sync<T>();
     if (stop || s_status == 2) break;
     if (accepted) {
       if (s_it >= max_iter) break;
@@ -736,6 +749,32 @@ __global__ __launch_bounds__(T) void k_gold_standard(
     g.n = n;
     info[blockIdx.x] = g;
   }
+}
+
+// Workgroup (T threads) per pair; a pair of at most 64 inliers runs on the first wave alone
+// (wave-level reductions and fences, the other waves leave at once): the C4 pairs that bound
+// the launch are small ones with many LM iterations, where the workgroup barriers and the
+// cross-wave sums were most of an iteration
+template <int T>
+__global__ __launch_bounds__(T) void k_gold_standard(
+    const double *__restrict__ Fin, const double *__restrict__ pl, const double *__restrict__ pr,
+    int64_t total, const int64_t *__restrict__ off, int max_iter, double *__restrict__ Xb,
+    double *__restrict__ Xc, double *__restrict__ Wb, double *__restrict__ Fout,
+    double *__restrict__ C1out, GsInfo *__restrict__ info, const int32_t *__restrict__ act) {
+  const int tid = threadIdx.x;
+  if (act && !act[blockIdx.x]) {  // (rs_pairs_two_view: a pair without a consensus)
+    if (tid < 9) Fout[9 * blockIdx.x + tid] = __builtin_nan("");
+    if (tid == 0) info[blockIdx.x] = GsInfo{0.0, 0.0, 0, 0, 0, 0};
+    return;
+  }
+  if constexpr (T > 64 && RSAMD_GS_WAVE) {
+    if (off[blockIdx.x + 1] - off[blockIdx.x] <= 64) {
+      if (tid >= 64) return;
+      gs_pair<64>(Fin, pl, pr, total, off, max_iter, Xb, Xc, Wb, Fout, C1out, info);
+      return;
+    }
+  }
+  gs_pair<T>(Fin, pl, pr, total, off, max_iter, Xb, Xc, Wb, Fout, C1out, info);
 }
 
 // ---- rs_pairs_two_view: the pair records -> the gold standard, on the device ----------------

@@ -142,10 +142,14 @@ __device__ __forceinline__ void fmatrix_cameras(const double *F, double *C1) {
   }
 }
 
+#ifndef RSAMD_TRI_JTOL
+#define RSAMD_TRI_JTOL 4e-16  // triangulate_linear's Jacobi rotation threshold (A/B: 1e-16)
+#endif
 // ----------------------------------------------------------------------------------------
 // lab3.triangulate_linear (lab3.py:477-503): X = null vector of the 6x4 matrix
 // [[x1]_x C1; [x2]_x C2] (numpy svd V[-1]) by one-sided Jacobi on its columns.
 // ----------------------------------------------------------------------------------------
+template <bool FAST>
 __device__ __forceinline__ void triangulate_linear(const double *C1, const double *C2,
                                                    const double *x1, const double *x2,
                                                    double *X) {
@@ -180,7 +184,10 @@ __device__ __forceinline__ void triangulate_linear(const double *C1, const doubl
           b += B[r][q] * B[r][q];
           g += B[r][p] * B[r][q];
         }
-        if (fabs(g) > 1e-16 * sqrt(a * b) && g != 0.0) {
+        // (FAST: rotate while the columns' cosine is above ~2 eps.  At 1e-16, below the rounding
+        // level of g, a converged matrix keeps rotating by rounding noise to the 20-sweep cap
+        // in ~1 % of points, and a wave waits for its slowest lane; FAST takes 5-6 sweeps)
+        if (fabs(g) > (FAST ? RSAMD_TRI_JTOL : 1e-16) * sqrt(a * b) && g != 0.0) {
           rotated = true;
           const double zeta = (b - a) / (2.0 * g);
           const double t = copysign(1.0, zeta) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
@@ -239,8 +246,11 @@ __device__ __forceinline__ void triangulate_linear(const double *C1, const doubl
 #ifndef RSAMD_ABERTH_MAX
 #define RSAMD_ABERTH_MAX 100  // sweep cap (A/B builds may lower it to time the tail)
 #endif
+// The same iteration with the roots in a run-time-indexed array (scratch memory): the form
+// k_triangulate_optimal keeps, because the reference-faithful gold standard (scipy TRF from
+// rs_triangulate_optimal's start) is chaotic in the last bits of that start
 template <int N>
-__device__ __forceinline__ int aberth_roots(const double (&g)[N + 1], double (&zr)[N],
+__device__ __forceinline__ int aberth_roots_serial(const double (&g)[N + 1], double (&zr)[N],
                                             double (&zi)[N], int &trailing) {
   trailing = 0;
   int lo = 0;
@@ -283,7 +293,7 @@ __device__ __forceinline__ int aberth_roots(const double (&g)[N + 1], double (&z
       }
     }
     unsigned conv = 0, all = (1u << deg) - 1u;
-    for (int it = 0; it < RSAMD_ABERTH_MAX && conv != all; ++it) {
+    for (int it = 0; it < 100 && conv != all; ++it) {
       for (int k = 0; k < deg; ++k) {
         if (conv & (1u << k)) continue;
         const double xr = zr[k], xi = zi[k];
@@ -338,13 +348,170 @@ __device__ __forceinline__ int aberth_roots(const double (&g)[N + 1], double (&z
   return deg;
 }
 
+// v[i] for a run-time i < M by a select chain: the array stays in registers (an array indexed
+// by a run-time value anywhere lives in scratch memory, and every Aberth sweep then waits on
+// memory: k_relative_pose 100 us and the gold standard's triangulation at C4)
+template <int M>
+__device__ __forceinline__ double pick(const double (&v)[M], int i) {
+  double r = v[0];
+#pragma unroll
+  for (int m = 1; m < M; ++m) r = i == m ? v[m] : r;
+  return r;
+}
+
+template <int N>
+__device__ __forceinline__ int aberth_roots(const double (&g)[N + 1], double (&zr)[N],
+                                            double (&zi)[N], int &trailing) {
+  trailing = 0;
+  int lo = N + 1, hi = 0;
+#pragma unroll
+  for (int k = N; k >= 0; --k)
+    if (g[k] != 0.0) lo = k;  // first non-zero coefficient
+  if (lo == N + 1) return 0;
+#pragma unroll
+  for (int k = 0; k <= N; ++k)
+    if (g[k] != 0.0) hi = k;  // last non-zero coefficient
+  trailing = N - hi;
+  const int deg = hi - lo;
+  double a[N + 1];  // monic, descending: z^deg + a[1] z^(deg-1) + ... + a[deg]
+  {
+    const double g0 = pick(g, lo);
+#pragma unroll
+    for (int k = 0; k <= N; ++k) a[k] = k <= deg ? pick(g, lo + k) / g0 : 0.0;
+  }
+  if (deg > 0) {
+    double lg[N + 1];  // log |b_k|, b_k = a[deg - k] (ascending)
+#pragma unroll
+    for (int k = 0; k <= N; ++k) {
+      const double v = k <= deg ? fabs(pick(a, deg - k)) : 0.0;
+      lg[k] = v > 0.0 ? log(v) : -1.0e300;
+    }
+    // upper convex hull of (k, lg[k]) as a bit set of its vertices (k = 0 .. deg)
+    unsigned hull = 1u;
+#pragma unroll
+    for (int k = 1; k <= N; ++k) {
+      if (k > deg || lg[k] == -1.0e300) continue;
+      // pop while the last two vertices and k turn the wrong way
+      for (;;) {
+        const int k2 = 31 - __builtin_clz(hull);
+        if (k2 == 0) break;
+        const unsigned rest = hull & ~(1u << k2);
+        const int k1 = 31 - __builtin_clz(rest);
+        const double l1 = pick(lg, k1), l2 = pick(lg, k2);
+        if ((l2 - l1) * (k - k1) <= (lg[k] - l1) * (k2 - k1))
+          hull = rest;
+        else
+          break;
+      }
+      hull |= 1u << k;
+    }
+    // m = k2 - k1 start points per hull edge on |z| = (|b_k1| / |b_k2|)^(1/m); root q of the
+    // edge e (0-based) at angle 2 pi u / m + 2 pi e / deg + 0.4, in edge order
+    {
+      int e = 0, k1 = 0;
+      unsigned rest = hull & ~1u;
+      double rad = 0.0;
+      int m = 1, u = 0;
+#pragma unroll
+      for (int q = 0; q < N; ++q) {
+        if (q < deg) {
+          if (q == 0 || u == m) {  // next edge
+            if (q > 0) {
+              ++e;
+              k1 += m;
+            }
+            const int k2 = __builtin_ctz(rest);
+            rest &= rest - 1u;
+            m = k2 - k1;
+            rad = exp((pick(lg, k1) - pick(lg, k2)) / m);
+            u = 0;
+          }
+          const double ang = 6.283185307179586 * u / m + 6.283185307179586 * e / deg + 0.4;
+          zr[q] = rad * cos(ang);
+          zi[q] = rad * sin(ang);
+          ++u;
+        } else {
+          zr[q] = 0.0;
+          zi[q] = 0.0;
+        }
+      }
+    }
+    unsigned conv = 0, all = (1u << deg) - 1u;
+    for (int it = 0; it < RSAMD_ABERTH_MAX && conv != all; ++it) {
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        if (k >= deg || (conv & (1u << k))) continue;
+        const double xr = zr[k], xi = zi[k];
+        const double az = sqrt(xr * xr + xi * xi);
+        double pr = 1.0, pi = 0.0, dr = 0.0, di = 0.0, S = 1.0;
+#pragma unroll
+        for (int j = 1; j <= N; ++j) {
+          if (j > deg) break;
+          const double ndr = dr * xr - di * xi + pr, ndi = dr * xi + di * xr + pi;
+          dr = ndr;
+          di = ndi;
+          const double npr = pr * xr - pi * xi + a[j], npi = pr * xi + pi * xr;
+          pr = npr;
+          pi = npi;
+          S = S * az + fabs(a[j]);
+        }
+        if (sqrt(pr * pr + pi * pi) <= 8.0 * 2.220446049250313e-16 * S) {
+          conv |= 1u << k;
+          continue;
+        }
+        double rr, ri;  // p / p'
+        const double den = dr * dr + di * di;
+        if (den == 0.0) {
+          rr = pr;
+          ri = pi;
+        } else {
+          rr = (pr * dr + pi * di) / den;
+          ri = (pi * dr - pr * di) / den;
+        }
+        double sr = 0.0, si = 0.0;  // sum_{j != k} 1 / (z_k - z_j)
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          if (j == k || j >= deg) continue;
+          const double ur = xr - zr[j], ui = xi - zi[j];
+          const double dd = ur * ur + ui * ui;
+          if (dd > 0.0) {
+            sr += ur / dd;
+            si -= ui / dd;
+          }
+        }
+        const double qr = 1.0 - (rr * sr - ri * si), qi = -(rr * si + ri * sr);
+        const double qd = qr * qr + qi * qi;
+        double wr = rr, wi = ri;
+        if (qd != 0.0) {
+          wr = (rr * qr + ri * qi) / qd;
+          wi = (ri * qr - rr * qi) / qd;
+        }
+        zr[k] = xr - wr;
+        zi[k] = xi - wi;
+        if (fabs(wr) + fabs(wi) <= 2.0 * 2.220446049250313e-16 * (fabs(zr[k]) + fabs(zi[k])))
+          conv |= 1u << k;
+      }
+    }
+  }
+  return deg;
+}
+
+template <bool FAST>
 __device__ __forceinline__ int roots_real_parts(const double (&g)[7], double (&out)[6]) {
   double zr[6], zi[6];
   int trailing = 0;
-  const int deg = aberth_roots<6>(g, zr, zi, trailing);
-  for (int k = 0; k < deg; ++k) out[k] = zr[k];
-  for (int k = 0; k < trailing; ++k) out[deg + k] = 0.0;
-  return deg + trailing;
+  if constexpr (FAST) {
+    const int deg = aberth_roots<6>(g, zr, zi, trailing);
+    // the iterated roots, then `trailing` zero roots (zr is 0 beyond deg)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) out[k] = k < deg ? zr[k] : 0.0;
+    return deg + trailing;
+  } else {
+    const int deg = aberth_roots_serial<6>(g, zr, zi, trailing);
+    for (int k = 0; k < deg; ++k) out[k] = zr[k];
+    for (int k = 0; k < trailing; ++k) out[deg + k] = 0.0;
+    return deg + trailing;
+  }
 }
 
 // ----------------------------------------------------------------------------------------
@@ -353,6 +520,9 @@ __device__ __forceinline__ int roots_real_parts(const double (&g)[7], double (&o
 // the real part of every root and at t = inf, the argmin (first NaN wins, as np.argmin), the
 // closest points on the two lines, back-transfer, linear triangulation.
 // ----------------------------------------------------------------------------------------
+// FAST (k_relative_pose, which reads only the depth signs): register-resident roots and the
+// 2-eps Jacobi stop; else the arithmetic rs_triangulate_optimal and the gold standard keep.
+template <bool FAST = false>
 __device__ __forceinline__ void triangulate_optimal(const double *C1, const double *C2,
                                                     double x1, double y1, double x2, double y2,
                                                     double *X) {
@@ -397,11 +567,13 @@ __device__ __forceinline__ void triangulate_optimal(const double *C1, const doub
   g[5] = b * b * b * b - a * a * d * d + d * d * d * d + b * b * (c * c + 2 * d * d);
   g[6] = b * d * k1;
   double r[6];
-  const int nr = roots_real_parts(g, r);
+  const int nr = roots_real_parts<FAST>(g, r);
   int best = -1;
   double bs = 0.0;
   bool nan_seen = false;
-  for (int i = 0; i <= nr; ++i) {
+#pragma unroll
+  for (int i = 0; i <= 6; ++i) {
+    if (i > nr) break;
     double s;
     if (i < nr) {
       const double t = r[i];
@@ -421,7 +593,7 @@ __device__ __forceinline__ void triangulate_optimal(const double *C1, const doub
   }
   double l1[3], l2[3];
   if (best < nr) {
-    const double tm = r[best];
+    const double tm = pick(r, best);
     l1[0] = -(c * tm + d);
     l1[1] = a * tm + b;
     l1[2] = c * tm + d;
@@ -450,7 +622,7 @@ __device__ __forceinline__ void triangulate_optimal(const double *C1, const doub
   p2[2] = q2[2];
   p2[0] += x2 * p2[2];
   p2[1] += y2 * p2[2];
-  triangulate_linear(C1, C2, p1, p2, X);
+  triangulate_linear<FAST>(C1, C2, p1, p2, X);
 }
 
 }  // namespace rsd
