@@ -835,8 +835,8 @@ def _pairs_arrays(pairs, H, mine, ns_all, solve, refine, recs):
     idx = np.asarray(mine, dtype=np.int64)
     off = np.zeros(len(mine) + 1, dtype=np.int64)
     np.cumsum(ns_all[idx], out=off[1:])
-    p1 = np.hstack([pairs[i][0] for i in mine]).astype(np.float64, copy=False)
-    p2 = np.hstack([pairs[i][1] for i in mine]).astype(np.float64, copy=False)
+    p1 = np.concatenate([pairs[i][0] for i in mine], axis=1).astype(np.float64, copy=False)
+    p2 = np.concatenate([pairs[i][1] for i in mine], axis=1).astype(np.float64, copy=False)
     if (refine is not None and getattr(refine, "fused", False) and hasattr(solve, "many_two_view")
             and getattr(refine, "ctx", None) is getattr(solve, "ctx", None)):
         res, _, Fg, info, R, t, found = solve.many_two_view(idx, p1, p2, off, refine.K)
@@ -885,6 +885,11 @@ def _fill_ransac(recs, idx, res):
 
 def _pairs_gather(comm, pairs, owners, recs):
     """run_pairs' exchange: each rank's own records, one all-gather, the full table."""
+    if comm.world == 1:  # every record is this rank's already
+        table = recs.copy()
+        table["pair"] = np.arange(len(pairs))
+        table["best_index"][table["valid"] == 0] = -1
+        return table
     width = max(len(o) for o in owners)
     send = np.zeros(width, dtype=PAIR_DTYPE)
     own = np.asarray(owners[comm.rank], dtype=np.int64)

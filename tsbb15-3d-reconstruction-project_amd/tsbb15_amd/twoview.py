@@ -143,14 +143,18 @@ def MakeHomogenous(K, coord):
 
 
 def normalise_each(K, coord):
-    """MakeHomogenous(K, [p])[0] for each row p of coord (n, 2) -- the C-normalised first
-    correspondence main.py:59-63 passes to relative_camera_pose -- as a one-right-hand-side
-    solve per point, so a point's bits do not depend on how many are normalised together
-    (LAPACK's multi-RHS kernels may round differently: the batched pair paths must agree)."""
+    """K^-1 [u, v, 1] for each row (u, v) of coord (n, 2) -- the C-normalised first
+    correspondence main.py:59-63 passes to relative_camera_pose, as fun.MakeHomogenous forms it
+    (scipy.linalg.inv(K) @ coord_hom, fun.py:48-55) -- with elementwise products and sums, so
+    a point's bits do not depend on how many are normalised together (a BLAS product may
+    round differently per batch size: the batched pair paths must agree field for field)."""
     coord = np.asarray(coord, dtype=np.float64).reshape(-1, 2)
-    h = np.concatenate([coord, np.ones((coord.shape[0], 1))], axis=1)[..., None]
-    K = np.asarray(K, dtype=np.float64)
-    return np.linalg.solve(np.broadcast_to(K, (coord.shape[0], 3, 3)), h)[..., 0]
+    Ki = np.linalg.inv(np.asarray(K, dtype=np.float64))
+    u, v = coord[:, 0], coord[:, 1]
+    out = np.empty((coord.shape[0], 3))
+    for r in range(3):
+        out[:, r] = (Ki[r, 0] * u + Ki[r, 1] * v) + Ki[r, 2]
+    return out
 
 
 def relative_camera_pose_batch(E, y1, y2, ctx=None):
