@@ -246,7 +246,10 @@ __global__ __launch_bounds__(128) void k_fmatrix_from_cameras(const double *__re
 #endif
 constexpr int kGsT = RSAMD_GS_T;
 #ifndef RSAMD_GS_WAVE
-#define RSAMD_GS_WAVE 1  // pairs of <= 64 inliers on one wave (A/B: 0)
+#define RSAMD_GS_WAVE 1  // pairs of <= RSAMD_GS_WAVE_MAX inliers on one wave (A/B: 0)
+#endif
+#ifndef RSAMD_GS_WAVE_MAX
+#define RSAMD_GS_WAVE_MAX 64
 #endif
 constexpr int kPerPt = 45;  // W (12x3), V (3x3 upper: 6), gx (3)
 
@@ -332,6 +335,39 @@ __device__ __forceinline__ void block_reduce(double (&v)[K], double *scratch, do
     }
     gs_sync<T>();
   }
+}
+
+// The gold standard's sums on a one-wave pair (n <= 64 points, lane j = point j): the lanes'
+// K values transposed through LDS (tr: n rows of K) and column k summed over the rows, in
+// point order, by lane k -- n adds instead of block_reduce's reduce-scatter, whose 128 padded
+// values spill to AGPRs at this kernel's register pressure (gold standard at C4: 437 -> 353
+// us).  (The same for the 256-thread pairs up to 160 points, rows summed in two halves by two
+// thread groups: 361 us, not kept -- a 116 KB row buffer for no gain.)
+#ifndef RSAMD_GS_TR
+#define RSAMD_GS_TR 1
+#endif
+template <int K>
+__device__ __forceinline__ void wave_reduce_tr(double (&v)[K], double *tr, double *out, int n) {
+  const int lane = threadIdx.x & 63;
+  n = min(n, 64);  // rows: the lanes holding points (lane l sums points l, l + 64, ...)
+  if (lane < n) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) tr[lane * K + k] = v[k];
+  }
+  gs_sync<64>();
+  for (int k = lane; k < K; k += 64) {
+    double s = 0.0;
+    for (int j = 0; j < n; ++j) s += tr[j * K + k];
+    out[k] = s;
+  }
+  gs_sync<64>();
+}
+
+template <int K, int T>
+__device__ __forceinline__ void gs_reduce(double (&v)[K], double *red, double *tr, double *out,
+                                          int n) {
+  if constexpr (T == 64 && RSAMD_GS_TR) wave_reduce_tr<K>(v, tr, out, n);
+  else block_reduce<K, T>(v, red, out);
 }
 
 // Residuals of lab3.fmatrix_residuals_gs for one point and their Jacobians:
@@ -489,7 +525,7 @@ __device__ __forceinline__ void gs_pair(
     const double *__restrict__ Fin, const double *__restrict__ pl, const double *__restrict__ pr,
     int64_t total, const int64_t *__restrict__ off, int max_iter, double *__restrict__ Xb,
     double *__restrict__ Xc, double *__restrict__ Wb, double *__restrict__ Fout,
-    double *__restrict__ C1out, GsInfo *__restrict__ info) {
+    double *__restrict__ C1out, GsInfo *__restrict__ info, double *tr) {
   __shared__ double red[(T / 64) * 128];
   __shared__ double sU[78], sgc[12], sres[94], sC[12], sdc[12];
   __shared__ double s_lam, s_nu, s_cost, s_cost0;
@@ -554,7 +590,7 @@ __device__ __forceinline__ void gs_pair(
         for (int k = 0; k < 3; ++k)
           w[42 + k] = Bj[k] * r[0] + Bj[3 + k] * r[1] + Bj[6 + k] * r[2] + Bj[9 + k] * r[3];
       }
-      block_reduce<91, T>(acc, red, sres);
+      gs_reduce<91, T>(acc, red, tr, sres, n);
       if (tid == 0) {
         for (int k = 0; k < 78; ++k) sU[k] = sres[k];
         for (int k = 0; k < 12; ++k) sgc[k] = sres[78 + k];
@@ -586,7 +622,7 @@ __device__ __forceinline__ void gs_pair(
           acc[78 + p] += wv[p][0] * w[42] + wv[p][1] * w[43] + wv[p][2] * w[44];
         }
       }
-      block_reduce<90, T>(acc, red, sres);
+      gs_reduce<90, T>(acc, red, tr, sres, n);
     }
     if (tid == 0) {
       // S = U + lam diag(U) - sum W Vi W^T;  rhs = -gc + sum W Vi gx;  Cholesky.  Fully
@@ -677,7 +713,7 @@ __device__ __forceinline__ void gs_pair(
         acc[2] += dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2];
         acc[3] += x[0] * x[0] + x[1] * x[1] + x[2] * x[2];
       }
-      block_reduce<4, T>(acc, red, sres);
+      gs_reduce<4, T>(acc, red, tr, sres, n);
       if (tid == 0) {
         double pc = 0.0, dn = 0.0, cn = 0.0;
         for (int p = 0; p < 12; ++p) {
@@ -761,6 +797,7 @@ __global__ __launch_bounds__(T) void k_gold_standard(
     int64_t total, const int64_t *__restrict__ off, int max_iter, double *__restrict__ Xb,
     double *__restrict__ Xc, double *__restrict__ Wb, double *__restrict__ Fout,
     double *__restrict__ C1out, GsInfo *__restrict__ info, const int32_t *__restrict__ act) {
+  __shared__ double trbuf[RSAMD_GS_TR ? 64 * 91 : 1];  // wave_reduce_tr's rows
   const int tid = threadIdx.x;
   if (act && !act[blockIdx.x]) {  // (rs_pairs_two_view: a pair without a consensus)
     if (tid < 9) Fout[9 * blockIdx.x + tid] = __builtin_nan("");
@@ -768,13 +805,13 @@ __global__ __launch_bounds__(T) void k_gold_standard(
     return;
   }
   if constexpr (T > 64 && RSAMD_GS_WAVE) {
-    if (off[blockIdx.x + 1] - off[blockIdx.x] <= 64) {
+    if (off[blockIdx.x + 1] - off[blockIdx.x] <= RSAMD_GS_WAVE_MAX) {
       if (tid >= 64) return;
-      gs_pair<64>(Fin, pl, pr, total, off, max_iter, Xb, Xc, Wb, Fout, C1out, info);
+      gs_pair<64>(Fin, pl, pr, total, off, max_iter, Xb, Xc, Wb, Fout, C1out, info, trbuf);
       return;
     }
   }
-  gs_pair<T>(Fin, pl, pr, total, off, max_iter, Xb, Xc, Wb, Fout, C1out, info);
+  gs_pair<T>(Fin, pl, pr, total, off, max_iter, Xb, Xc, Wb, Fout, C1out, info, trbuf);
 }
 
 // ---- rs_pairs_two_view: the pair records -> the gold standard, on the device ----------------
