@@ -18,5 +18,5 @@ unset RSAMD_LIB
 for v in prod "$@"; do
   if [ $v = prod ]; then unset RSAMD_LIB; else export RSAMD_LIB=$R/tsbb15-3d-reconstruction-project_amd/lib_ab/$v/librsamd.so; fi
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$v -o c4 -- python3 $R/tools/probe_c4.py > $OUT/prof_$v.log 2>&1 || { echo "rocprof failed"; exit 1; }
-  echo "== $v"; python3 $R/tools/kstats.py $(find $OUT/prof_$v -name "*kernel_stats.csv") | head -8
+  echo "== $v"; python3 $R/tools/kstats.py $(find $OUT/prof_$v -name "*kernel_stats.csv") > $OUT/kstats_$v.txt; sed -n 1,9p $OUT/kstats_$v.txt
 done

@@ -13,4 +13,4 @@ for pass in 1 2 3; do
   echo "separate pass $pass $(PROBE_UNFUSED=1 timeout -k 10 100 python3 $R/tools/probe_c4.py)" || exit 1
 done
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_fused -o c4 -- python3 $R/tools/probe_c4.py > $OUT/prof_fused.log 2>&1 || { echo "rocprof failed"; exit 1; }
-echo "== fused"; python3 $R/tools/kstats.py $(find $OUT/prof_fused -name "*kernel_stats.csv") | head -12
+echo "== fused"; python3 $R/tools/kstats.py $(find $OUT/prof_fused -name "*kernel_stats.csv") > $OUT/kstats_fused.txt; sed -n 1,13p $OUT/kstats_fused.txt
