@@ -7,6 +7,8 @@
 
 #include <cmath>
 
+#include "device_math.h"
+
 namespace rsd {
 
 // ----------------------------------------------------------------------------------------
@@ -189,9 +191,20 @@ __device__ __forceinline__ void triangulate_linear(const double *C1, const doubl
         // in ~1 % of points, and a wave waits for its slowest lane; FAST takes 5-6 sweeps)
         if (fabs(g) > (FAST ? RSAMD_TRI_JTOL : 1e-16) * sqrt(a * b) && g != 0.0) {
           rotated = true;
-          const double zeta = (b - a) / (2.0 * g);
-          const double t = copysign(1.0, zeta) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-          const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+          double c, s;
+          if constexpr (FAST) {  // (fast reciprocals / square roots, as jacobi_rot)
+            const double zeta = (b - a) * (0.5 * rcp_fast(g));
+            const double az = fabs(zeta), z2 = fma(zeta, zeta, 1.0);
+            const double t = az < 1e150 ? copysign(rcp_fast(az + z2 * rsqrt_fast(z2)), zeta)
+                                        : 0.5 * rcp_fast(zeta);
+            c = rsqrt_fast(fma(t, t, 1.0));
+            s = c * t;
+          } else {
+            const double zeta = (b - a) / (2.0 * g);
+            const double t = copysign(1.0, zeta) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+            c = 1.0 / sqrt(1.0 + t * t);
+            s = c * t;
+          }
 #pragma unroll
           for (int r = 0; r < 6; ++r) {
             const double bp = B[r][p], bq = B[r][q];
@@ -464,9 +477,10 @@ __device__ __forceinline__ int aberth_roots(const double (&g)[N + 1], double (&z
         if (den == 0.0) {
           rr = pr;
           ri = pi;
-        } else {
-          rr = (pr * dr + pi * di) / den;
-          ri = (pi * dr - pr * di) / den;
+        } else {  // (one reciprocal, a few ulp: rcp_fast)
+          const double iden = rcp_fast(den);
+          rr = (pr * dr + pi * di) * iden;
+          ri = (pi * dr - pr * di) * iden;
         }
         double sr = 0.0, si = 0.0;  // sum_{j != k} 1 / (z_k - z_j)
 #pragma unroll
@@ -475,16 +489,18 @@ __device__ __forceinline__ int aberth_roots(const double (&g)[N + 1], double (&z
           const double ur = xr - zr[j], ui = xi - zi[j];
           const double dd = ur * ur + ui * ui;
           if (dd > 0.0) {
-            sr += ur / dd;
-            si -= ui / dd;
+            const double idd = rcp_fast(dd);
+            sr += ur * idd;
+            si -= ui * idd;
           }
         }
         const double qr = 1.0 - (rr * sr - ri * si), qi = -(rr * si + ri * sr);
         const double qd = qr * qr + qi * qi;
         double wr = rr, wi = ri;
         if (qd != 0.0) {
-          wr = (rr * qr + ri * qi) / qd;
-          wi = (ri * qr - rr * qi) / qd;
+          const double iqd = rcp_fast(qd);
+          wr = (rr * qr + ri * qi) * iqd;
+          wi = (ri * qr - rr * qi) * iqd;
         }
         zr[k] = xr - wr;
         zi[k] = xi - wi;
