@@ -527,7 +527,9 @@ __device__ __forceinline__ void gs_pair(
     double *__restrict__ Xc, double *__restrict__ Wb, double *__restrict__ Fout,
     double *__restrict__ C1out, GsInfo *__restrict__ info, double *tr) {
   __shared__ double red[(T / 64) * 128];
-  __shared__ double sU[78], sgc[12], sres[94], sC[12], sdc[12];
+  // the linearisation's sums land in sLin (U: 78, gc: 12, |r|^2): no copy out of sres
+  __shared__ double sLin[91], sres[94], sC[12], sdc[12];
+  double *const sU = sLin, *const sgc = sLin + 78;
   __shared__ double s_lam, s_nu, s_cost, s_cost0;
   __shared__ int s_state, s_it, s_acc, s_status;
   const int tid = threadIdx.x;
@@ -590,11 +592,9 @@ __device__ __forceinline__ void gs_pair(
         for (int k = 0; k < 3; ++k)
           w[42 + k] = Bj[k] * r[0] + Bj[3 + k] * r[1] + Bj[6 + k] * r[2] + Bj[9 + k] * r[3];
       }
-      gs_reduce<91, T>(acc, red, tr, sres, n);
+      gs_reduce<91, T>(acc, red, tr, sLin, n);
       if (tid == 0) {
-        for (int k = 0; k < 78; ++k) sU[k] = sres[k];
-        for (int k = 0; k < 12; ++k) sgc[k] = sres[78 + k];
-        s_cost = 0.5 * sres[90];
+        s_cost = 0.5 * sLin[90];
         if (s_it == 0) s_cost0 = s_cost;
         s_it += 1;
       }
