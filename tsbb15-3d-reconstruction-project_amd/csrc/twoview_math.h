@@ -440,8 +440,10 @@ __device__ __forceinline__ int aberth_roots(const double (&g)[N + 1], double (&z
             u = 0;
           }
           const double ang = 6.283185307179586 * u / m + 6.283185307179586 * e / deg + 0.4;
-          zr[q] = rad * cos(ang);
-          zi[q] = rad * sin(ang);
+          double sa, ca;
+          sincos(ang, &sa, &ca);  // (one range reduction for both)
+          zr[q] = rad * ca;
+          zi[q] = rad * sa;
           ++u;
         } else {
           zr[q] = 0.0;
