@@ -53,3 +53,20 @@ def test_gen_rnd_indices_drop_in_equal_reference():
         random.seed(seed)
         got = [list(ransac.gen_rnd_indices(L, n)) for _ in range(len(misc[key]))]
         assert got == [list(x) for x in misc[key]]
+
+
+def test_normalise_each_is_batch_independent():
+    """twoview.normalise_each (the C-normalised first correspondences of the C4 paths): a
+    point's bits do not depend on which other points are normalised with it, so the fused
+    device call and the separate calls agree field for field; the values are fun.MakeHomogenous's
+    K^-1 [u, v, 1] (fun.py:48-55) to rounding."""
+    from conftest import golden
+    from tsbb15_amd import twoview
+    K = golden("dino_pnp_kat.npz")["K_last"]
+    rng = np.random.default_rng(3)
+    P = rng.uniform(0.0, 720.0, (257, 2))
+    full = twoview.normalise_each(K, P)
+    for sub in (np.arange(1), np.arange(5, 9), rng.choice(257, 100, replace=False), np.arange(257)):
+        assert np.array_equal(twoview.normalise_each(K, P[sub]), full[sub])
+    ref = (np.linalg.inv(K) @ np.vstack([P.T, np.ones((1, len(P)))])).T
+    np.testing.assert_allclose(full, ref, rtol=1e-14, atol=1e-15)
