@@ -250,3 +250,29 @@ def test_two_view_pairs_raw_edges(ctx):
                 assert np.array_equal(a2[f], b[f], equal_nan=True), f
         else:
             assert np.array_equal(a2, b, equal_nan=True)
+
+
+def test_two_view_pairs_raw_rejects_bad_arguments(ctx):
+    """rs_pairs_two_view's argument errors fail loudly (ValueError from RS_EINVAL) before any
+    launch: max_iter outside [1, 1e5], K without the first correspondences, bad offsets."""
+    from tsbb15_amd import pairs as pairs_mod
+    z = golden("dino_pnp_kat.npz")
+    p = [q for q in _dino_pairs() if q[0].shape[1] >= 20][0]
+    off = np.array([0, p[0].shape[1]])
+    with pytest.raises(ValueError, match="max_iter"):
+        pairs_mod.two_view_pairs_raw(p[0], p[1], off, 100, z["K_last"], max_iter=0, ctx=ctx)
+    with pytest.raises(ValueError):
+        pairs_mod.two_view_pairs_raw(p[0], p[1], np.array([0, p[0].shape[1] + 1]), 100, ctx=ctx)
+    d = _ffi.C.c_double
+    res = (_ffi.PairResult * 1)()
+    info = (_ffi.GsInfo * 1)()
+    buf = np.zeros(64)
+    K = np.ascontiguousarray(z["K_last"], dtype=np.float64)
+    st = _ffi.lib().rs_pairs_two_view(
+        ctx.handle, _ffi.ptr(np.ascontiguousarray(p[0], dtype=np.float64), d),
+        _ffi.ptr(np.ascontiguousarray(p[1], dtype=np.float64), d),
+        _ffi.ptr(np.ascontiguousarray(off, dtype=np.int64), _ffi.C.c_int64), 1, 100,
+        _ffi.SAMPLER_PHILOX, 0, None, None, 1.5, 50, _ffi.ptr(K, d), None, None, res,
+        _ffi.ptr(np.zeros(p[0].shape[1], dtype=np.int32), _ffi.C.c_int32), _ffi.ptr(buf, d), info,
+        _ffi.ptr(buf, d), _ffi.ptr(buf, d), _ffi.ptr(np.zeros(1, dtype=np.int32), _ffi.C.c_int32))
+    assert st == _ffi.RS_EINVAL
