@@ -130,6 +130,19 @@ int rs_py_shuffle_tuples_gpu(rs_ctx *ctx, uint32_t *mt_key, int32_t *mt_pos, int
  * No reference counterpart: it accounts for the first-call cost of getFFromLabCode (fun.py:291). */
 int rs_np_host_stats(double *jump_ms, int64_t *builds);
 
+/* Step split of the GPU parse of the numpy stream (the sampling of fun.py:305-306): enable = 1
+ * records HIP events between the steps of the following world-1 parses on this context (each
+ * event is a marker between two kernels: a few microseconds each, so not in timed headline
+ * runs).  Returns the last parse call's milliseconds summed over its segments, ms_out[10]:
+ * 0 jump (MT windows), 1 first stream pass, 2 entry parse (with its resume launch, which waits
+ * for the second pass), 3 tracking, 4 compose, 5 filter / scan / starts, 6 tuples, 7 result
+ * copy, 8 the second stream pass (on the second stream, beside the entry parse), 9 the parse
+ * from first to last mark; bytes_out[3]: algorithmic HBM bytes -- stream words written, chunk
+ * draws read by the parse, hypothesis draws read by the tuple kernel; *segments. */
+#define RS_NP_TIMING_SLOTS 10
+int rs_np_timing(rs_ctx *ctx, int32_t enable, double *ms_out, double *bytes_out,
+                 int64_t *segments);
+
 typedef struct rs_np_shard rs_np_shard;
 int rs_np_shard_create(rs_ctx *ctx, int64_t n, int32_t k, int32_t world, int32_t rank, int32_t py,
                        rs_np_shard **out);
@@ -264,8 +277,13 @@ int rs_pnp_dlt(rs_ctx *ctx, const double *X, const double *y, int64_t m, double 
  * consensus e = |pi(y) - pi(R x + t)|^2 <= thresh is counted on the `med` set.  mode as for
  * F; in tuple mode host_tuples come from rs_py_shuffle_tuples.  k in [6, 16]: the DLT
  * (pnp.py:132-160).  k = 3: the reference's p3p branch (ransac.py:81-82, 91-111), Lambda
- * Twist P3P with every pose of a trial scored (trial-major, pose-minor first occurrence;
- * best_index is the trial).  Replaces ransac.ransac_robust's loop (ransac.py:72-111). */
+ * Twist P3P with every pose of a trial scored (best_index is the trial).  The k = 3 winner is
+ * chosen in two classes: the first (trial-major, pose-minor) front-facing pose with the largest
+ * count, unless the best mirrored-depth pose counts more than twice as many (kMirrorCountWins =
+ * 2; then the first such mirrored pose) -- so a mirrored pose with a higher count can lose.
+ * Counts are exact in the reference's arithmetic (rs_pnp_count_poses), and the call fails with
+ * RS_EDEVICE if the winner's count differs from its D_med consensus size.  Replaces
+ * ransac.ransac_robust's loop (ransac.py:72-111). */
 /* HIP events around rs_pnp_ransac's solve and count kernels (ransac.py:93-105's work): enable = 1
  * records them in the following calls; returns the last timed call's milliseconds (-1: none). */
 int rs_pnp_timing(rs_ctx *ctx, int32_t enable, double *solve_ms, double *count_ms);
@@ -274,6 +292,14 @@ int rs_pnp_ransac(rs_ctx *ctx, const double *X_med, const double *y_med, int64_t
                   int64_t H, int32_t mode, uint64_t seed, const int32_t *host_tuples,
                   double thresh, rs_pnp_result *out, int64_t *inl_med, int64_t *n_inl_med,
                   int64_t *inl_high, int64_t *n_inl_high);
+
+/* Consensus counts of H given poses (H x 12: R row-major, then t) on m correspondences X (m,3),
+ * y (m,3): the scoring of ransac.py:96-105 (`thresh >= dpp_squared(y, R x + t)`) with the same
+ * kernel rs_pnp_ransac counts with -- division-free, pairs within a rigorous error band of the
+ * threshold re-tested in the reference's arithmetic, so every count equals the reference-order
+ * count.  counts_out: H int32. */
+int rs_pnp_count_poses(rs_ctx *ctx, const double *X, const double *y, int64_t m,
+                       const double *poses, int64_t H, double thresh, int32_t *counts_out);
 
 /* Minimal solvers of the OpenCV drop-ins: RS_PNP_DLT6 the reference's DLT (pnp.py:132-160) on
  * 6-point samples, RS_PNP_EPNP5 EPnP on 5-point samples (OpenCV's solvePnPRansac kernel),

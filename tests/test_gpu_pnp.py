@@ -470,3 +470,56 @@ def _ffi_refine_short(X, uv, K):
                                            2, _ffi.ptr(np.ascontiguousarray(K), _ffi.C.c_double),
                                            _ffi.ptr(R, _ffi.C.c_double), _ffi.ptr(t, _ffi.C.c_double),
                                            20, _ffi.ptr(c, _ffi.C.c_double)))
+
+
+def test_consensus_counts_exact_at_the_threshold(ctx):
+    """ransac.py:104-105 keeps a point when thresh >= e.  Points whose e lies within a few
+    hundred ulps of thresh (copies of one point nudged by 1..12 ulps of its world coordinates)
+    are decided by the last bits of the reference's arithmetic; the counting kernel must agree
+    with it exactly (division-free test + exact guard band + reference-order re-test), for the
+    pose that placed the threshold and for nearby poses."""
+    import pnp_exact
+    X, _, y, R, t, _ = synth.pnp_scene(64, 0.0, seed=21)
+    P0 = np.concatenate([R.ravel(), t])
+    picks = [3, 17, 40]
+    Xb, yb = pnp_exact.boundary_cloud(X, y, P0, picks, spread=12, seed=1)
+    Xa, ya = np.vstack([X, Xb]), np.vstack([y, yb])
+    rs = np.random.RandomState(2)
+    poses = np.array([P0] + [P0 * (1.0 + rs.normal(0, s, 12)) for s in [1e-15] * 7 + [1e-13] * 8])
+    e_all = [pnp_exact.errors_exact(P, Xa, ya) for P in poses]
+    straddled = 0
+    for q, j in enumerate(picks):
+        centre = len(X) + q * 25 + 12
+        thresh = e_all[0][centre]
+        ref = np.array([np.count_nonzero(thresh >= e) for e in e_all], np.int32)
+        got = ransac.consensus_counts(Xa, ya, poses, thresh, ctx=ctx)
+        np.testing.assert_array_equal(got, ref)
+        block = e_all[0][len(X) + q * 25: len(X) + (q + 1) * 25]
+        straddled += int(0 < np.count_nonzero(thresh >= block) < 25)
+    assert straddled == len(picks)   # the threshold really cuts each cloud
+
+
+def test_consensus_counts_threshold_sweep_equals_reference_order(ctx):
+    """Every point's own e as the threshold (inclusive test), C3-like noisy scene, 16 poses."""
+    import pnp_exact
+    X, _, y, R, t, _ = synth.pnp_scene(48, 0.3, seed=8)
+    rs = np.random.RandomState(4)
+    P0 = np.concatenate([R.ravel(), t])
+    poses = np.array([P0 * (1.0 + rs.normal(0, 1e-6, 12)) for _ in range(16)])
+    e_all = [pnp_exact.errors_exact(P, X, y) for P in poses]
+    for j in range(0, 48, 3):
+        thresh = e_all[j % 16][j]
+        ref = np.array([np.count_nonzero(thresh >= e) for e in e_all], np.int32)
+        np.testing.assert_array_equal(ransac.consensus_counts(X, y, poses, thresh, ctx=ctx), ref)
+
+
+def test_ransac_pnp_best_count_is_the_consensus_size(ctx):
+    """The winner's count equals its D_med consensus set (the library fails otherwise)."""
+    X, _, y, _, _, _ = synth.pnp_scene(300, 0.3, seed=12)
+    thr = (1.5 / 800.0) ** 2
+    for n, sampler in ((6, "philox"), (3, "philox"), (6, "exact")):
+        R, t, im, ih, best, cnt = ransac.ransac_pnp(X, y, X, y, 2000, thr, n, sampler=sampler,
+                                                    seed=5, rng=random.Random(3), ctx=ctx)
+        assert best >= 0 and cnt == len(im)
+        assert cnt == int(ransac.consensus_counts(X, y, np.concatenate([R.ravel(), t])[None],
+                                                  thr, ctx=ctx)[0])

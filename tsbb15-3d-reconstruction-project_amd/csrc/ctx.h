@@ -20,6 +20,12 @@ struct rs_ctx {
   int pnp_timing = 0;
   hipEvent_t pnp_ev[3] = {};
   double pnp_solve_ms = -1.0, pnp_count_ms = -1.0;
+  // rs_np_timing: HIP events between the parity-stream parse's steps (np_sampler.hip), the
+  // last np_choice_device call's sums over its segments (RS_NP_TIMING_SLOTS ms, 3 byte counts)
+  int np_timing = 0;
+  double np_ms[RS_NP_TIMING_SLOTS] = {};
+  double np_bytes[3] = {};
+  int64_t np_segments = 0;
 };
 
 namespace rs {

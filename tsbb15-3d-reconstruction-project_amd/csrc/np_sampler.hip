@@ -2606,6 +2606,12 @@ int sgrow(T *&p, int64_t &cap, int64_t need) {
 
 }  // namespace
 
+// rs_np_timing marks: 0 start, 1 windows (jump) done, 2 first stream pass done, 3 entry done
+// (with its resume launch, which waits for the second pass), 4 track done, 5 compose done,
+// 6 starts done, 7 tuples done, 8 result copied.  Slots kNpMarks, kNpMarks + 1: the second
+// stream pass on s2.
+constexpr int kNpMarks = 9;
+
 struct rs_np_shard {
   rs_ctx *ctx = nullptr;
   int world = 1, rank = 0, n1 = 0, cus = 256;
@@ -2639,6 +2645,10 @@ struct rs_np_shard {
   int64_t *d_row_off = nullptr, *d_starts = nullptr, *d_got = nullptr;
   uint2 *d_ev = nullptr;
   NpResult *d_res = nullptr;  // world 1 (np_choice_device): the segment's outcome in one copy
+  // rs_np_timing: HIP events between the steps of a world-1 segment (kNpMarks on the context
+  // stream, two around the second stream pass on s2); null unless timing was ever enabled
+  bool timed = false;
+  hipEvent_t tev[kNpMarks + 2] = {};
   int64_t cap_win = 0, cap_chain = 0, cap_stream = 0, cap_fin = 0, cap_fin_all = 0, cap_fm = 0,
           cap_fm_all = 0, cap_ev = 0, cap_evn = 0, cap_ent = 0, cap_vcnt = 0, cap_off = 0,
           cap_tpos = 0, cap_row = 0, cap_starts = 0, cap_pause = 0, cap_io = 0;
@@ -2657,6 +2667,8 @@ void shard_free(rs_np_shard *w) {
   if (w->d_io) (void)hipFree(w->d_io);
   if (w->ev_a) (void)hipEventDestroy(w->ev_a);
   if (w->ev_b) (void)hipEventDestroy(w->ev_b);
+  for (hipEvent_t e : w->tev)
+    if (e) (void)hipEventDestroy(e);
   // (w->s2 belongs to the process-wide pool: np_aux_stream)
 }
 
@@ -2692,6 +2704,12 @@ int shard_kernel_attrs(int n1) {
 }
 
 int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// a timing mark of rs_np_timing (no-op unless the segment is timed)
+int tmark(rs_np_shard &w, int slot, hipStream_t s) {
+  if (w.timed) HIP_TRY(hipEventRecord(w.tev[slot], s));
+  return RS_OK;
+}
 
 }  // namespace
 
@@ -2928,23 +2946,28 @@ int shard_stream(rs_np_shard &w, const uint32_t *key) {
   hipStream_t s = w.ctx->stream;
   int st;
   if ((st = sgrow(w.d_stream, w.cap_stream, w.Lb * kN))) return st;
-  if ((st = shard_windows(w, key, s))) return st;
+  if ((st = shard_windows(w, key, s)) || (st = tmark(w, 1, s))) return st;
   const int G = static_cast<int>(w.G), JB = w.JB;
   if (w.xb > 0) {  // blocks 1..xb here, the rest on s2 beside the entry kernel (event ev_b)
     if ((st = sgrow(w.d_io, w.cap_io, w.G * kN))) return st;
     k_mt_stream<<<static_cast<unsigned>(G), 256, 0, s>>>(w.d_win, w.d_stream, w.Lb, JB, G, w.gext, 0,
                                                          w.xb, w.d_io);
     HIP_TRY(hipGetLastError());
+    if ((st = tmark(w, 2, s))) return st;
     HIP_TRY(hipEventRecord(w.ev_a, s));
     HIP_TRY(hipStreamWaitEvent(w.s2, w.ev_a, 0));
+    if ((st = tmark(w, kNpMarks, w.s2))) return st;
     k_mt_stream<<<static_cast<unsigned>(G), 256, 0, w.s2>>>(w.d_win, w.d_stream, w.Lb, JB, G, w.gext,
                                                             w.xb, std::numeric_limits<int>::max(), w.d_io);
     HIP_TRY(hipGetLastError());
+    if ((st = tmark(w, kNpMarks + 1, w.s2))) return st;
     HIP_TRY(hipEventRecord(w.ev_b, w.s2));
   } else {
     k_mt_stream<<<static_cast<unsigned>(G), 256, 0, s>>>(w.d_win, w.d_stream, w.Lb, JB, G, w.gext, 0,
                                                          std::numeric_limits<int>::max(), nullptr);
     HIP_TRY(hipGetLastError());
+    if ((st = tmark(w, 2, s)) || (st = tmark(w, kNpMarks, s)) || (st = tmark(w, kNpMarks + 1, s)))
+      return st;
   }
   if ((st = sgrow(w.d_fin, w.cap_fin, w.Cr * w.n1)) || (st = sgrow(w.d_fin_m, w.cap_fm, w.Cr)) ||
       (st = sgrow(w.d_ev_n, w.cap_evn, w.Cr)) || (st = sgrow(w.d_tpos, w.cap_tpos, w.Cr)) ||
@@ -3006,7 +3029,7 @@ int shard_enqueue_parse(rs_np_shard &w) {
     }
     return RS_OK;
   };
-  if ((st = entry(w.py))) return st;
+  if ((st = entry(w.py)) || (st = tmark(w, 3, s))) return st;
   if (w.py) {
     (small ? k_np_track<true, true>
            : (hand_of(w.n1) > 64 ? k_np_track128<true> : k_np_track<true, false>))<<<Cr, 64 * kTrackWaves, 0, s>>>(ea, ea.draws);
@@ -3015,6 +3038,7 @@ int shard_enqueue_parse(rs_np_shard &w) {
            : (hand_of(w.n1) > 64 ? k_np_track128<false> : k_np_track<false, false>))<<<Cr, 64 * kTrackWaves, 0, s>>>(ea, ea.draws);
   }
   HIP_TRY(hipGetLastError());
+  if ((st = tmark(w, 4, s))) return st;
   if (ts_path) {
     // header: n1, chunks, chunk length, draws, rank, world, then kTs words per chunk
     std::vector<unsigned long long> h(static_cast<size_t>(w.Cr) * kTs + 8, 0ull);
@@ -3243,25 +3267,50 @@ int shard_tuples(rs_np_shard &w, int64_t base, int64_t hi, int64_t next_start, i
 int shard_run_local(rs_np_shard &w, uint32_t *key, int32_t *pos, int64_t count, int64_t lo,
                     int64_t hi, int32_t *d_out, int64_t *got_out) {
   int st;
-  if ((st = shard_init(w)) || (st = shard_layout(w, *pos, count)) || (st = shard_stream(w, key)))
-    return st;
   hipStream_t s = w.ctx->stream;
+  if ((st = shard_init(w))) return st;
+  w.timed = w.ctx->np_timing != 0;
+  if (w.timed && !w.tev[0])
+    for (auto &e : w.tev) HIP_TRY(hipEventCreate(&e));
+  if ((st = tmark(w, 0, s)) || (st = shard_layout(w, *pos, count)) || (st = shard_stream(w, key)))
+    return st;
   NpResult res;
   for (;;) {
     if ((st = shard_enqueue_parse(w))) return st;
     k_np_compose<<<1, 1024, 0, s>>>(w.d_fin, w.d_fin_m, w.n1, static_cast<int>(w.Cr), w.d_ent,
                                     nullptr);
     HIP_TRY(hipGetLastError());
-    if ((st = shard_enqueue_starts(w, w.count, &w.d_res->got))) return st;
+    if ((st = tmark(w, 5, s))) return st;
+    if ((st = shard_enqueue_starts(w, w.count, &w.d_res->got)) || (st = tmark(w, 6, s))) return st;
     if (hi > lo) {  // waves beyond the delivered count exit
       shard_launch_tuples(w, lo, hi, &w.d_res->got, d_out);
       HIP_TRY(hipGetLastError());
     }
+    if ((st = tmark(w, 7, s))) return st;
     // delivered count, draws used, errors and the stream block holding the next word
     k_np_result<<<1, 64, 0, s>>>(w.d_stream, w.d_starts, *pos, w.d_err, w.d_res);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(&res, w.d_res, sizeof(res), hipMemcpyDeviceToHost, s));
+    if ((st = tmark(w, 8, s))) return st;
     HIP_TRY(hipStreamSynchronize(s));
+    if (w.timed) {  // this segment's steps, summed over the call's segments (rs_np_timing)
+      float ms = 0.f;
+      for (int k = 0; k + 1 < kNpMarks; ++k) {
+        HIP_TRY(hipEventElapsedTime(&ms, w.tev[k], w.tev[k + 1]));
+        w.ctx->np_ms[k] += ms;
+      }
+      HIP_TRY(hipEventElapsedTime(&ms, w.tev[kNpMarks], w.tev[kNpMarks + 1]));
+      w.ctx->np_ms[kNpMarks - 1] += ms;
+      HIP_TRY(hipEventElapsedTime(&ms, w.tev[0], w.tev[kNpMarks - 1]));
+      w.ctx->np_ms[kNpMarks] += ms;
+      // algorithmic HBM bytes of the segment: stream words written once, every parsed draw
+      // read once by the chunk parse (entry + track), every hypothesis's draws read once by
+      // the tuple kernel (words up to the last start)
+      w.ctx->np_bytes[0] += 4.0 * static_cast<double>(w.Lb) * kN;
+      w.ctx->np_bytes[1] += 4.0 * static_cast<double>(w.Cr * w.Wc);
+      w.ctx->np_bytes[2] += 4.0 * static_cast<double>(res.used);
+      w.ctx->np_segments += 1;
+    }
     if (res.err & 1) {  // wrap log overflow: a larger log, the same chunks again
       if (w.ecap >= w.Wc + 2 * w.n1) return rs::fail(RS_EDEVICE, "np sampler: wrap log overflow");
       ++w.ecap_shift;
@@ -3324,6 +3373,11 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
     HIP_TRY(hipMemsetAsync(d_out, 0, sizeof(int32_t) * static_cast<size_t>(take) * k, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return RS_OK;
+  }
+  if (c->np_timing) {  // rs_np_timing reports this call's steps
+    for (double &v : c->np_ms) v = 0.0;
+    for (double &v : c->np_bytes) v = 0.0;
+    c->np_segments = 0;
   }
   rs_np_shard *w = c->np_shard;
   if (w && (w->n != n || w->k != k || w->py != py)) {
@@ -3482,6 +3536,17 @@ extern "C" int rs_np_shard_tuples(rs_np_shard *w, int64_t base, int64_t hi, int6
 
 // Host time the parse has spent building MT jump polynomials in this process (first calls at a
 // new generator length), and how many level sets it built.
+extern "C" int rs_np_timing(rs_ctx *c, int32_t enable, double *ms_out, double *bytes_out,
+                            int64_t *segments) {
+  if (!c) return rs::fail(RS_EINVAL, "null pointer");
+  static_assert(kNpMarks + 1 == RS_NP_TIMING_SLOTS, "rs_np_timing slots");
+  c->np_timing = enable ? 1 : 0;
+  if (ms_out) std::memcpy(ms_out, c->np_ms, sizeof(c->np_ms));
+  if (bytes_out) std::memcpy(bytes_out, c->np_bytes, sizeof(c->np_bytes));
+  if (segments) *segments = c->np_segments;
+  return RS_OK;
+}
+
 extern "C" int rs_np_host_stats(double *jump_ms, int64_t *builds) {
   if (!jump_ms || !builds) return rs::fail(RS_EINVAL, "rs_np_host_stats: null pointer");
   std::lock_guard<std::mutex> g(g_jump_mu);

@@ -7,7 +7,8 @@
 //                 inverse iteration on R^T R, C0 = (A|b), tau = sign det A, polar factor of
 //                 tau A by 3x3 Jacobi SVD, lambda = 3 tau / tr S, t = lambda b.
 //   k_pnp_count   lane per hypothesis x chunk of `med` points (wave-uniform scalar loads):
-//                 e = |pi(y) - pi(R x + t)|^2 <= thresh, evaluated division-free.
+//                 e = |pi(y) - pi(R x + t)|^2 <= thresh, evaluated division-free; pairs within
+//                 a rigorous error band of the threshold re-tested in the reference's order.
 //   k_pnp_select  one workgroup: first hypothesis with the largest count (strict ">"); for the
 //                 P3P branch a mirrored-depth pose only where it clearly out-counts (x2) every
 //                 front-facing one.
@@ -457,6 +458,45 @@ __global__ __launch_bounds__(64) void k_pnp_dlt_all(const PPt *__restrict__ pts,
   for (int q = 0; q < 3; ++q) out[9 + q] = t[q];
 }
 
+// e = dpp_squared(y, R x + t) in the reference's arithmetic (ransac.py:21-35; calc_y_prim
+// ransac.py:34-35): R x by numpy's matmul, which on the build container's OpenBLAS dgemm is the
+// FMA chain fma(R_i2, z, fma(R_i1, y, R_i0 x)) (checked bit for bit against oracle/pnp_ref's
+// pose_errors, tests/test_oracle_p3p.py), then + t, pi, diff, and the dot in order.
+// P: R row-major (9), then t (3).
+__device__ __forceinline__ bool pnp_inlier_ref(const double *P, const PPt &p, double thresh) {
+#pragma clang fp contract(off)
+  const double q0 = fma(P[2], p.Z, fma(P[1], p.Y, P[0] * p.X)) + P[9];
+  const double q1 = fma(P[5], p.Z, fma(P[4], p.Y, P[3] * p.X)) + P[10];
+  const double q2 = fma(P[8], p.Z, fma(P[7], p.Y, P[6] * p.X)) + P[11];
+  const double a0 = p.u - q0 / q2, a1 = p.v - q1 / q2;
+  const double a2 = p.y2 / p.y2 - q2 / q2;
+  const double e = (a0 * a0 + a1 * a1) + a2 * a2;
+  return thresh >= e;
+}
+
+// Consensus counts of ransac.py:96-105 (`thresh >= dpp_squared(y, R x + t)`, counted on D_med).
+//
+// The division-free test |M (u q2 - q0, v q2 - q1)|^2 <= thr q2^2 decides almost every
+// (hypothesis, point); with Exact (the reference-mode metric, M = I) it is exact: a pair whose
+// margin |D - thr q2^2| is within the rigorous error band below is re-tested in the reference's
+// own arithmetic (pnp_inlier_ref: three divisions, numpy's order), so every count equals the
+// reference-order count -- and so the winner's count equals its consensus set (k_pnp_inliers,
+// the same arithmetic; the host checks best_count == n_med).
+//
+// The band (u = 2^-53, first-order error analysis, then x2 for the second-order terms).  With
+// S_i = sum_j |R_ij x_j| + |t_i| <= L = rmax |x|_1 + tmax (rmax the largest row 2-norm of R,
+// Cauchy-Schwarz), Q = |q2|, U = max(|u|, |v|), d = (du, dv), D = |d|^2, a = |du| + |dv|:
+//   * each q_i (either fma chain, the reference's with + t apart) is within 4u S_i of exact;
+//   * fast: |d_i - A_i| <= 3u (U S_2 + S_i) + u |d_i|, A_i = u_i q2* - q_i* the exact residual;
+//     and e* q2^2 differs from |A|^2 by the relative 2 (3u S_2 / Q) of q2's error;
+//   * reference: |a_i - a_i*| Q <= 4u (S_i + |q_i| / Q S_2) + u |q_i| + u |A_i| (the quotient's
+//     and the difference's roundings), and the dot product adds 2u D;
+//   * thr q2^2 is rounded twice (2u).
+// Collected with g = 4.01u L (3 + U + L / Q):  band = 2 (2 g a + 4 g^2 + u (D (8.1 + 6.1 L / Q)
+// + 2.01 thr q2^2)).  If D - thr q2^2 > band the exact e exceeds thr by more than the
+// reference's own error (outlier in both); below -band it is an inlier in both.  Q = 0, a NaN or
+// an infinity makes the band non-finite, and the pair takes the reference test.
+template <bool Exact>
 __global__ __launch_bounds__(256) void k_pnp_count(const PPt *__restrict__ pts, int m, int H,
                                                    const double *__restrict__ Psoa, int64_t ld,
                                                    int chunk, int nchunks, double thresh,
@@ -472,6 +512,17 @@ __global__ __launch_bounds__(256) void k_pnp_count(const PPt *__restrict__ pts, 
   double P[12];
 #pragma unroll
   for (int q = 0; q < 12; ++q) P[q] = Psoa[q * ld + hl];
+  constexpr double kU = 0x1p-53;
+  double rmax = 0.0, tmax = 0.0;
+  if (Exact) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      rmax = fmax(rmax, fma(P[3 * r], P[3 * r], fma(P[3 * r + 1], P[3 * r + 1], P[3 * r + 2] * P[3 * r + 2])));
+      tmax = fmax(tmax, fabs(P[9 + r]));
+    }
+    // (a NaN pose makes D NaN, so its band is NaN and the reference test decides: false)
+    rmax = sqrt(rmax) * (1.0 + 8.0 * kU);
+  }
   int cnt = 0;
   for (int i = p0; i < p1; ++i) {
     const PPt p = pts[i];
@@ -483,7 +534,18 @@ __global__ __launch_bounds__(256) void k_pnp_count(const PPt *__restrict__ pts, 
     const double du0 = fma(p.u, q2, -q0), dv = fma(p.v, q2, -q1);
     const double du = fma(mt.a, du0, mt.b * dv), dvm = mt.c * dv;
     const double lhs = fma(du, du, dvm * dvm);
-    cnt += (q2 != 0.0 && lhs <= thresh * (q2 * q2)) ? 1 : 0;
+    const double rhs = thresh * (q2 * q2);
+    bool in = q2 != 0.0 && lhs <= rhs;
+    if (Exact) {
+      const double L = fma(fabs(p.X) + fabs(p.Y) + fabs(p.Z), rmax, tmax);
+      const double Lr = L * __builtin_amdgcn_rcp(fabs(q2));
+      const double gg = (4.01 * kU) * L * (3.0 + fmax(fabs(p.u), fabs(p.v)) + Lr);
+      const double a = fabs(du) + fabs(dv);
+      const double band = 2.0 * fma(2.0 * gg, a + 2.0 * gg,
+                                    kU * fma(lhs, fma(6.1, Lr, 8.1), 2.01 * rhs));
+      if (!(fabs(lhs - rhs) > band)) in = pnp_inlier_ref(P, p, thresh);
+    }
+    cnt += in ? 1 : 0;
   }
   if (h < H) atomicAdd(&counts[h], cnt);
 }
@@ -567,19 +629,6 @@ __global__ __launch_bounds__(1024) void k_pnp_select(const int *__restrict__ cou
   }
 }
 
-// e = dpp_squared(y, R x + t) in the reference's order (ransac.py:21-35): pi, diff, dot.
-__device__ __forceinline__ bool pnp_inlier_ref(const double (&Rm)[9], const double (&t)[3],
-                                               const PPt &p, double thresh) {
-#pragma clang fp contract(off)
-  const double q0 = ((Rm[0] * p.X + Rm[1] * p.Y) + Rm[2] * p.Z) + t[0];
-  const double q1 = ((Rm[3] * p.X + Rm[4] * p.Y) + Rm[5] * p.Z) + t[1];
-  const double q2 = ((Rm[6] * p.X + Rm[7] * p.Y) + Rm[8] * p.Z) + t[2];
-  const double a0 = p.u - q0 / q2, a1 = p.v - q1 / q2;
-  const double a2 = p.y2 / p.y2 - q2 / q2;
-  const double e = (a0 * a0 + a1 * a1) + a2 * a2;
-  return thresh >= e;
-}
-
 // cv.solvePnPRansac's inlier test (OpenCV: projectPoints, dx^2 + dy^2 <= err^2) in pixels.
 __device__ __forceinline__ bool pnp_inlier_px(const double (&Rm)[9], const double (&t)[3],
                                               const PPt &p, double thresh, const PxMetric &mt) {
@@ -627,16 +676,16 @@ __global__ __launch_bounds__(1024) void k_pnp_inliers(const PPt *__restrict__ me
   __shared__ int woff[16];
   __shared__ int base_s;
   const bool have = res->best_index >= 0;
-  double Rm[9], t[3];
+  double P[12];
 #pragma unroll
-  for (int q = 0; q < 9; ++q) Rm[q] = res->R[q];
+  for (int q = 0; q < 9; ++q) P[q] = res->R[q];
 #pragma unroll
-  for (int q = 0; q < 3; ++q) t[q] = res->t[q];
+  for (int q = 0; q < 3; ++q) P[9 + q] = res->t[q];
   ordered_compact(
-      m_med, [&](int i) { return pnp_inlier_ref(Rm, t, med[i], thresh); }, have, res->inliers,
+      m_med, [&](int i) { return pnp_inlier_ref(P, med[i], thresh); }, have, res->inliers,
       &res->n_med, woff, &base_s);
   ordered_compact(
-      m_high, [&](int i) { return pnp_inlier_ref(Rm, t, high[i], thresh); }, have,
+      m_high, [&](int i) { return pnp_inlier_ref(P, high[i], thresh); }, have,
       res->inliers + m_med, &res->n_high, woff, &base_s);
 }
 
@@ -1060,7 +1109,7 @@ extern "C" int rs_pnp_ransac(rs_ctx *c, const double *X_med, const double *y_med
   const int chunk = static_cast<int>((m_med + nch - 1) / nch);
   nch = (m_med + chunk - 1) / chunk;
   const int64_t units = groups * nch;
-  hipLaunchKernelGGL(rsd::k_pnp_count, dim3((units + 3) / 4), dim3(256), 0, s, pm,
+  hipLaunchKernelGGL(rsd::k_pnp_count<true>, dim3((units + 3) / 4), dim3(256), 0, s, pm,
                      static_cast<int>(m_med), static_cast<int>(Hm), dP, ld, chunk,
                      static_cast<int>(nch), thresh, rsd::PxMetric{1.0, 0.0, 1.0}, dcnt);
   HIP_TRY(hipGetLastError());
@@ -1086,11 +1135,59 @@ extern "C" int rs_pnp_ransac(rs_ctx *c, const double *X_med, const double *y_med
   std::memcpy(out->t, r->t, sizeof(out->t));
   // n = 3: the trial of the winning pose (its slot: best_index % kP3pSlots on the device)
   out->best_index = k == 3 && r->best_index >= 0 ? r->best_index / rsd::kP3pSlots : r->best_index;
+  // the counts are exact in the reference's arithmetic (k_pnp_count<true>), so the winner's
+  // count IS the size of its consensus set on D_med (ransac.py:104,108)
+  if (r->best_index >= 0 && r->n_med != r->best_count)
+    return fail(RS_EDEVICE, "PnP consensus recount mismatch (best_count != |C_med|)");
   out->best_count = r->best_count;
   if (n_inl_med) *n_inl_med = r->n_med;
   if (n_inl_high) *n_inl_high = r->n_high;
   if (inl_med) std::memcpy(inl_med, r->inliers, sizeof(int64_t) * r->n_med);
   if (inl_high) std::memcpy(inl_high, r->inliers + m_med, sizeof(int64_t) * r->n_high);
+  return RS_OK;
+}
+
+// Consensus counts of given poses (the scoring of ransac.py:96-105 without the sampling): the
+// product counting kernel k_pnp_count<true>, so a count here is what rs_pnp_ransac would count
+// for that pose.  poses: H x 12 (R row-major, then t).
+extern "C" int rs_pnp_count_poses(rs_ctx *c, const double *X, const double *y, int64_t m,
+                                  const double *poses, int64_t H, double thresh,
+                                  int32_t *counts_out) {
+  if (!c || !X || !y || !poses || !counts_out) return fail(RS_EINVAL, "null pointer");
+  if (m < 1 || H < 1 || m > (1 << 26) || H > (1LL << 26)) return fail(RS_EINVAL, "bad dimensions");
+  HIP_TRY(hipSetDevice(c->device));
+  const int64_t ld = (H + 63) / 64 * 64;
+  const size_t b_in = align256(sizeof(double) * 3 * m), b_p = align256(sizeof(rsd::PPt) * m);
+  const size_t b_P = align256(sizeof(double) * 12 * ld), b_cnt = align256(sizeof(int) * ld);
+  int st = rs::ensure_scratch(c, 2 * b_in + b_p + b_P + b_cnt);
+  if (st) return st;
+  char *p = static_cast<char *>(c->scratch);
+  double *dX = reinterpret_cast<double *>(p);
+  double *dy = reinterpret_cast<double *>(p + b_in);
+  auto *pts = reinterpret_cast<rsd::PPt *>(p + 2 * b_in);
+  double *dP = reinterpret_cast<double *>(p + 2 * b_in + b_p);
+  int *dcnt = reinterpret_cast<int *>(p + 2 * b_in + b_p + b_P);
+  std::vector<double> soa(static_cast<size_t>(12 * ld), 0.0);
+  for (int64_t h = 0; h < H; ++h)
+    for (int q = 0; q < 12; ++q) soa[static_cast<size_t>(q * ld + h)] = poses[12 * h + q];
+  hipStream_t s = c->stream;
+  HIP_TRY(hipMemcpyAsync(dX, X, sizeof(double) * 3 * m, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(dy, y, sizeof(double) * 3 * m, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(dP, soa.data(), sizeof(double) * soa.size(), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(rsd::k_pack_ppts, dim3((m + 255) / 256), dim3(256), 0, s, dX, dy,
+                     static_cast<int>(m), pts);
+  HIP_TRY(hipMemsetAsync(dcnt, 0, sizeof(int) * H, s));
+  const int64_t groups = (H + 63) / 64;
+  int64_t nch = std::max<int64_t>(1, std::min<int64_t>((8192 + groups - 1) / groups, (m + 63) / 64));
+  const int chunk = static_cast<int>((m + nch - 1) / nch);
+  nch = (m + chunk - 1) / chunk;
+  const int64_t units = groups * nch;
+  hipLaunchKernelGGL(rsd::k_pnp_count<true>, dim3((units + 3) / 4), dim3(256), 0, s, pts,
+                     static_cast<int>(m), static_cast<int>(H), dP, ld, chunk,
+                     static_cast<int>(nch), thresh, rsd::PxMetric{1.0, 0.0, 1.0}, dcnt);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(counts_out, dcnt, sizeof(int) * H, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
   return RS_OK;
 }
 
@@ -1194,7 +1291,7 @@ extern "C" int rs_pnp_ransac_cv(rs_ctx *c, const double *X, const double *uv, in
   const int chunk = static_cast<int>((m + nch - 1) / nch);
   nch = (m + chunk - 1) / chunk;
   const int64_t units = groups * nch;
-  hipLaunchKernelGGL(rsd::k_pnp_count, dim3((units + 3) / 4), dim3(256), 0, s, pts,
+  hipLaunchKernelGGL(rsd::k_pnp_count<false>, dim3((units + 3) / 4), dim3(256), 0, s, pts,
                      static_cast<int>(m), static_cast<int>(H), dP, ld, chunk,
                      static_cast<int>(nch), thresh, mt, dcnt);
   HIP_TRY(hipGetLastError());

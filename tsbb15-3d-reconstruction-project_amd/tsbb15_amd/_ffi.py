@@ -78,6 +78,7 @@ _SIGS = {
                                            C.c_int64, _i32p]),
     "rs_mt_jump": (C.c_int, [_u32p, C.c_int32, C.c_int64, _u32p, _i32p]),
     "rs_np_host_stats": (C.c_int, [C.POINTER(C.c_double), _i64p]),
+    "rs_np_timing": (C.c_int, [C.c_void_p, C.c_int32, _dp, _dp, _i64p]),
     "rs_pnp_timing": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_double),
                                 C.POINTER(C.c_double)]),
     "rs_mt_poly_selftest": (C.c_int, [C.c_int64, C.c_int64]),
@@ -110,6 +111,8 @@ _SIGS = {
     "rs_pnp_ransac": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, _dp, C.c_int64, C.c_int32,
                                 C.c_int64, C.c_int32, C.c_uint64, _i32p, C.c_double,
                                 C.POINTER(PnpResult), _i64p, _i64p, _i64p, _i64p]),
+    "rs_pnp_count_poses": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, C.c_int64, C.c_double,
+                                     _i32p]),
     "rs_pnp_ransac_cv": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, C.c_int64, C.c_uint64,
                                    C.c_double, C.c_double, C.c_int32, _dp, C.POINTER(PnpResult),
                                    _i64p, _i64p, _i64p]),
@@ -350,6 +353,20 @@ def pnp_timing(ctx, enable):
     a, b = C.c_double(0.0), C.c_double(0.0)
     check(lib().rs_pnp_timing(ctx.handle, int(enable), C.byref(a), C.byref(b)))
     return a.value, b.value
+
+
+NP_STEPS = ("jump", "stream_pass1", "entry", "track", "compose", "starts", "tuples", "result",
+            "stream_pass2", "parse_total")
+
+
+def np_timing(ctx, enable):
+    """Enable / disable the parse's step events (rs_np_timing); returns the last parse call's
+    ({step: ms}, {stream_written, parse_read, tuples_read: bytes}, segments)."""
+    ms, by, seg = np.zeros(len(NP_STEPS)), np.zeros(3), C.c_int64(0)
+    check(lib().rs_np_timing(ctx.handle, int(enable), ptr(ms, C.c_double), ptr(by, C.c_double),
+                             C.byref(seg)))
+    return (dict(zip(NP_STEPS, ms.tolist())),
+            dict(zip(("stream_written", "parse_read", "tuples_read"), by.tolist())), seg.value)
 
 
 def np_host_stats():

@@ -157,6 +157,25 @@ def ransac_pnp(X_med, y_med, X_high, y_high, r, thresh, n=6, rng=None, sampler="
             ih[:kh.value].copy(), int(res.best_index), int(res.best_count))
 
 
+def consensus_counts(X, y, poses, thresh, ctx=None):
+    """Consensus sizes ``sum(thresh >= dpp_squared(y, R x + t))`` of given poses (the scoring of
+    ransac.py:96-105), counted by the kernel ransac_pnp uses (exact in the reference's
+    arithmetic).  ``poses``: (H, 3, 4) [R | t] or (H, 12).  Returns int32 (H,)."""
+    X, y = _ffi.f64c(X), _ffi.f64c(y)
+    if X.ndim != 2 or X.shape[1] != 3 or y.shape != X.shape:
+        raise ValueError("X must be (m, 3) and y (m, 3)")
+    P = np.asarray(poses, dtype=np.float64)
+    if P.ndim == 3 and P.shape[1:] == (3, 4):
+        P = np.concatenate([P[:, :, :3].reshape(-1, 9), P[:, :, 3]], axis=1)
+    P = np.ascontiguousarray(P.reshape(-1, 12))
+    out = np.zeros(len(P), np.int32)
+    ctx = ctx or _ffi.default_context()
+    _ffi.check(_ffi.lib().rs_pnp_count_poses(
+        ctx.handle, _ffi.ptr(X, _ffi.C.c_double), _ffi.ptr(y, _ffi.C.c_double), len(X),
+        _ffi.ptr(P, _ffi.C.c_double), len(P), float(thresh), _ffi.ptr(out, _ffi.C.c_int32)))
+    return out
+
+
 def ransac_robust(D_med, D_high, r, thresh, n):
     """Returns (R_est, t_est, C_est) lists as ransac.py:109-113 builds them."""
     if n == 4:
