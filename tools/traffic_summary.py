@@ -28,6 +28,8 @@ def base(name):
     n = name.strip()
     if n.startswith("void "):
         n = n[5:]
+    for ns in ("rsd::", "(anonymous namespace)::"):
+        n = n.replace(ns, "")
     return n.split("(")[0].strip()
 
 
