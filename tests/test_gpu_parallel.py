@@ -218,6 +218,22 @@ def test_dino_ring_fused_call_matches_separate_calls(ctx, with_k):
         assert int((fused["pose"] > 0).sum()) == 0
 
 
+def test_fused_call_over_1024_pairs_matches_separate_calls(ctx):
+    """More than 1024 pairs in one rs_pairs_two_view call (the gather's multi-round scan in
+    k_twoview_prep): the Dino ring's 630 pairs twice, fused against the separate calls."""
+    z = golden("dino_pnp_kat.npz")
+    pairs = _dino_pairs() * 2
+    assert len(pairs) > 1024
+    solver = parallel.GpuPairBatchSolver(ctx, 200)
+    fused = parallel.run_pairs(_Solo(), pairs, 200, solver,
+                               refine=parallel.GpuPairRefiner(ctx, z["K_last"]))
+    sep = parallel.run_pairs(_Solo(), pairs, 200, solver,
+                             refine=parallel.GpuPairRefiner(ctx, z["K_last"], fused=False))
+    for f in parallel.PAIR_DTYPE.names:
+        assert np.array_equal(fused[f], sep[f], equal_nan=fused[f].dtype.kind == "f"), f
+    assert int((fused["valid"] == 1).sum()) > 300
+
+
 def test_two_view_pairs_raw_edges(ctx):
     """Pairs without a consensus (N < 8, empty) inside a fused call: NaN F_gold / pose, found
     0, zero gold-standard info; the other pairs as in a call without them."""
@@ -276,3 +292,18 @@ def test_two_view_pairs_raw_rejects_bad_arguments(ctx):
         _ffi.ptr(np.zeros(p[0].shape[1], dtype=np.int32), _ffi.C.c_int32), _ffi.ptr(buf, d), info,
         _ffi.ptr(buf, d), _ffi.ptr(buf, d), _ffi.ptr(np.zeros(1, dtype=np.int32), _ffi.C.c_int32))
     assert st == _ffi.RS_EINVAL
+    # decreasing offsets straight through the C ABI (the Python wrapper rejects them first):
+    # the library's own check, before the offsets size any buffer
+    n = p[0].shape[1]
+    bad = np.array([0, n, n // 2], dtype=np.int64)
+    res2 = (_ffi.PairResult * 2)()
+    info2 = (_ffi.GsInfo * 2)()
+    big = np.zeros(64)
+    st = _ffi.lib().rs_pairs_two_view(
+        ctx.handle, _ffi.ptr(np.ascontiguousarray(p[0], dtype=np.float64), d),
+        _ffi.ptr(np.ascontiguousarray(p[1], dtype=np.float64), d), _ffi.ptr(bad, _ffi.C.c_int64),
+        2, 100, _ffi.SAMPLER_PHILOX, 0, None, None, 1.5, 50, None, None, None, res2,
+        _ffi.ptr(np.zeros(n, dtype=np.int32), _ffi.C.c_int32), _ffi.ptr(big, d), info2,
+        _ffi.ptr(big, d), _ffi.ptr(big, d), _ffi.ptr(np.zeros(2, dtype=np.int32), _ffi.C.c_int32))
+    assert st == _ffi.RS_EINVAL
+    assert b"non-decreasing" in _ffi.lib().rs_last_error()

@@ -84,7 +84,9 @@ extern "C" int rs_ctx_create(int device, rs_ctx **out) {
   rs_ctx *c = new rs_ctx();
   c->device = device;
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return hip_fail(e, "hipStreamCreate");
   }
@@ -93,11 +95,13 @@ extern "C" int rs_ctx_create(int device, rs_ctx **out) {
   // process has them on this device)
   e = rsd::preload_f8();
   if (e != hipSuccess) {
+    (void)hipStreamDestroy(c->aux_stream);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return hip_fail(e, "code object load");
   }
   if (int st = rs::np_preload()) {
+    (void)hipStreamDestroy(c->aux_stream);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return st;
@@ -115,6 +119,7 @@ extern "C" int rs_ctx_destroy(rs_ctx *c) {
   if (c->scratch) (void)hipFree(c->scratch);
   for (auto &e : c->pnp_ev)
     if (e) (void)hipEventDestroy(e);
+  if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return RS_OK;

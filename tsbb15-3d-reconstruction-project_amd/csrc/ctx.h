@@ -9,6 +9,9 @@
 struct rs_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  // the parity parse's second stream (the second MT stream pass beside the entry kernel), one per
+  // context, created with it: independent contexts never wait for each other's parse work
+  hipStream_t aux_stream = nullptr;
   void *scratch = nullptr;     // grow-only device scratch for single-shot ops
   size_t scratch_bytes = 0;
   rs_f8_plan *np_plan = nullptr;  // cached plan of rs_f8_ransac_np

@@ -283,7 +283,13 @@ static int plan_retarget(rs_f8_plan *p, int64_t n) {
       if (e == hipSuccess)
         e = hipMalloc(&b.d_res, sizeof(rsd::F8DevResult) + sizeof(int64_t) * static_cast<size_t>(cap));
     }
-    if (e != hipSuccess) return hip_fail(e, "rs_f8_plan retarget");
+    if (e != hipSuccess) {
+      // the old buffers are gone: mark the plan empty (a later retarget reallocates) and let
+      // the caller drop it (rs_f8_ransac_np destroys its cached plan)
+      p->cap_n = 0;
+      p->n = 0;
+      return hip_fail(e, "rs_f8_plan retarget");
+    }
     p->cap_n = cap;
   }
   p->n = n;
@@ -726,7 +732,13 @@ extern "C" int rs_f8_ransac_np(rs_ctx *c, const double *p1, const double *p2, in
   int st;
   if (!c->np_plan && (st = rs_f8_plan_create(c, n, H, &c->np_plan))) return st;
   // another pair's population: the same plan, its per-point buffers grown if need be
-  if (c->np_plan->n != n && (st = plan_retarget(c->np_plan, n))) return st;
+  if (c->np_plan->n != n && (st = plan_retarget(c->np_plan, n))) {
+    // a failed reallocation leaves the per-point buffers freed: drop the plan, so that the next
+    // call builds a fresh one instead of running on null buffers
+    rs_f8_plan_destroy(c->np_plan);
+    c->np_plan = nullptr;
+    return st;
+  }
   if ((st = rs_f8_plan_set_points(c->np_plan, p1, p2))) return st;
   uint32_t key[RS_MT_N];
   int32_t pos = *mt_pos;

@@ -1994,8 +1994,11 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
   const int64_t a = starts[h], b = starts[h + 1];
   const uint32_t *__restrict__ src = draws + a;
   // read-ahead never leaves the stream allocation (nwords words from draws[0]), nor the
-  // hypothesis by more than the queue
-  const int64_t lim = nwords - 1 - a;
+  // hypothesis by more than one window: the queue's look-ahead past the hypothesis's last word
+  // (up to kTupAhead blocks, ~25 % of a C2 hypothesis) would fetch the next hypothesis's words
+  // from HBM a second time (calibrated PMC, profiles/r06a_traffic.json: 1.46 GB per C2 run
+  // against 1.11 GB of hypothesis words); clamped loads all read one word (one cache line)
+  const int64_t lim = min(nwords - 1 - a, b - a + 63);
   auto ld = [&](int64_t x) { return src[x < lim ? x : lim]; };
   constexpr int kPerLane = kTupBlk / 64;
   uint32_t nb[kTupAhead][kPerLane];  // blocks 1 .. kTupAhead after the ring's newest
@@ -2669,7 +2672,7 @@ void shard_free(rs_np_shard *w) {
   if (w->ev_b) (void)hipEventDestroy(w->ev_b);
   for (hipEvent_t e : w->tev)
     if (e) (void)hipEventDestroy(e);
-  // (w->s2 belongs to the process-wide pool: np_aux_stream)
+  // (w->s2 is the context's aux_stream: rs_ctx_destroy destroys it)
 }
 
 // kernel attributes for populations up to n1 (dynamic LDS of the entry and tuple kernels)
@@ -2713,19 +2716,12 @@ int tmark(rs_np_shard &w, int slot, hipStream_t s) {
 
 }  // namespace
 
-namespace {
-int np_aux_stream(int device, hipStream_t *out);
-}  // namespace
-
 // Loads this file's code object on the current device (HIP loads a module at the first use of
 // any of its kernels: ~10 ms for the parse kernels, paid by the first parity call otherwise).
 int rs::np_preload() {
   hipFuncAttributes fa{};
   HIP_TRY(hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(k_np_track<false, false>)));
-  int device = 0;
-  HIP_TRY(hipGetDevice(&device));
-  hipStream_t s2 = nullptr;  // the parse's second stream, created once per device (np_aux_stream)
-  return np_aux_stream(device, &s2);
+  return RS_OK;
 }
 
 namespace {
@@ -2909,22 +2905,6 @@ int shard_windows(rs_np_shard &w, const uint32_t *key, hipStream_t s) {
   return RS_OK;
 }
 
-// The second stream of the parse (stream pass 2 beside the entry kernel), one per device for
-// the whole process: creating a HIP stream costs 15-30 ms here (it was most of a new context's
-// first parity call, tools/probe_first_call2.py).  Sessions of several contexts on one device
-// share it; each orders its work on it by its own events.
-int np_aux_stream(int device, hipStream_t *out) {
-  static std::mutex mu;
-  static std::vector<hipStream_t> pool;
-  std::lock_guard<std::mutex> g(mu);
-  if (device < 0) return rs::fail(RS_EINVAL, "np: bad device");
-  if (static_cast<size_t>(device) >= pool.size()) pool.resize(static_cast<size_t>(device) + 1, nullptr);
-  if (!pool[static_cast<size_t>(device)])
-    HIP_TRY(hipStreamCreateWithFlags(&pool[static_cast<size_t>(device)], hipStreamNonBlocking));
-  *out = pool[static_cast<size_t>(device)];
-  return RS_OK;
-}
-
 // device set-up shared by both drivers: kernel attributes, the jump polynomials, counters
 int shard_init(rs_np_shard &w) {
   HIP_TRY(hipSetDevice(w.ctx->device));
@@ -2934,7 +2914,7 @@ int shard_init(rs_np_shard &w) {
     int64_t c1 = 0, c2 = 0, c3 = 0;
     if ((st = sgrow(w.d_err, c1, 1)) || (st = sgrow(w.d_got, c2, 1)) || (st = sgrow(w.d_res, c3, 1)))
       return st;
-    if ((st = np_aux_stream(w.ctx->device, &w.s2))) return st;
+    w.s2 = w.ctx->aux_stream;  // the context's own (rs_ctx_create)
     HIP_TRY(hipEventCreateWithFlags(&w.ev_a, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&w.ev_b, hipEventDisableTiming));
   }

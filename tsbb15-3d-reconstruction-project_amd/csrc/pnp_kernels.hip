@@ -221,6 +221,81 @@ __device__ __forceinline__ void smallest_right_sv(const double (&R)[78], double 
   for (int j = 0; j < 12; ++j) x[j] *= in;
 }
 
+// Three-vector variant (blk_smallest_right_sv3 below, on the block factor): a block of THREE
+// vectors and a 3x3 Rayleigh-Ritz step per sweep: the Ritz
+// vector converges at (s12 / s9)^2 per sweep.  The kernel's time is its slowest wave's, and a
+// wave runs until its slowest lane converges: C3 samples (host prototype, 20 000 DLT samples of
+// the C3 scene) need at most 46 sweeps of the two-vector block (mean 6.5, a wave's slowest 17
+// on average) but 15 of the three-vector block (mean 4.8, a wave's slowest 8.9), at ~1.35x the
+// work per sweep.  The basis is rotated onto the Ritz vectors every sweep (smallest first), so
+// the 3x3 Gram matrix arrives nearly diagonal and its Jacobi eigen-solve ends after a sweep or
+// two.  Stops when the Ritz vector moves <= 1e-15, or stagnates at the rounding floor.
+__device__ __forceinline__ void jacobi_sym3(double (&G)[6], double (&Z)[9], int p, int q,
+                                            bool &rotated) {
+  // G packed (00, 11, 22, 01, 02, 12); rotate rows / columns p < q, accumulate Z's columns
+  const int ipq = p == 0 ? (q == 1 ? 3 : 4) : 5;
+  const int r = 3 - p - q;
+  const int ipr = (p == 0 ? (r == 1 ? 3 : 4) : (r == 0 ? (p == 1 ? 3 : 4) : 5));
+  const int iqr = (q == 1 ? (r == 0 ? 3 : 5) : (r == 0 ? 4 : 5));
+  const double gpq = G[ipq], gpp = G[p], gqq = G[q];
+  if (gpq * gpq > 1e-32 * fabs(gpp * gqq) && gpq != 0.0) {
+    rotated = true;
+    const double zeta = (gqq - gpp) * (0.5 * rcp_fast(gpq));
+    const double az = fabs(zeta), z2 = fma(zeta, zeta, 1.0);
+    const double t = az < 1e150 ? copysign(rcp_fast(az + z2 * rsqrt_fast(z2)), zeta)
+                                : 0.5 * rcp_fast(zeta);
+    const double c = rsqrt_fast(fma(t, t, 1.0)), s = c * t;
+    G[p] = fma(-t, gpq, gpp);
+    G[q] = fma(t, gpq, gqq);
+    G[ipq] = 0.0;
+    const double grp = G[ipr], grq = G[iqr];
+    G[ipr] = c * grp - s * grq;
+    G[iqr] = s * grp + c * grq;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const double zp = Z[3 * k + p], zq = Z[3 * k + q];
+      Z[3 * k + p] = c * zp - s * zq;
+      Z[3 * k + q] = s * zp + c * zq;
+    }
+  }
+}
+
+// Gram-Schmidt with one re-orthogonalisation ("twice is enough"): the inverse iterates are
+// nearly parallel (on exact data they differ by ~1e16 along the null direction), and one
+// classical pass leaves the remainder's rounding noise along u, which corrupts the 3x3 Ritz step.
+__device__ __forceinline__ void orthonormalize3(double (&u)[12], double (&v)[12],
+                                                double (&w)[12]) {
+  const double iu = rsqrt_fast(dot12(u, u));
+#pragma unroll
+  for (int j = 0; j < 12; ++j) u[j] *= iu;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const double p = dot12(u, v);
+#pragma unroll
+    for (int j = 0; j < 12; ++j) v[j] = fma(-p, u[j], v[j]);
+  }
+  const double iv = rsqrt_fast(dot12(v, v));
+#pragma unroll
+  for (int j = 0; j < 12; ++j) v[j] *= iv;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const double pu = dot12(u, w), pv = dot12(v, w);
+#pragma unroll
+    for (int j = 0; j < 12; ++j) w[j] = fma(-pv, v[j], fma(-pu, u[j], w[j]));
+  }
+  const double iw = rsqrt_fast(dot12(w, w));
+#pragma unroll
+  for (int j = 0; j < 12; ++j) w[j] *= iw;
+}
+
+#ifndef RSAMD_PNP_MAXIT
+#define RSAMD_PNP_MAXIT 200  // (A/B builds time the rest of the solve with 1)
+#endif
+// 3: block-structured factor + three-vector block (below); 2: the dense factor and the
+// two-vector block (A/B builds)
+#ifndef RSAMD_PNP_BLOCK
+#define RSAMD_PNP_BLOCK 3
+#endif
 // Constraint enforcement (pnp.py:141-145): C0 = (A | b) -> (R, t).
 __device__ __forceinline__ void enforce_pose(const double (&c0)[12], double (&Rm)[9],
                                              double (&t)[3]) {
@@ -252,6 +327,269 @@ __device__ __forceinline__ void enforce_pose(const double (&c0)[12], double (&Rm
   t[2] = lam * c0[11];
 }
 
+// ---- The DLT system's block structure ----------------------------------------------------
+// The two rows of a correspondence are [y]_x rows 0 and 1 times x~ = (X, Y, Z, 1) (pnp.py:
+// 132-160, dlt_rows): a0 = (0, -y2 x~, y1 x~), a1 = (y2 x~, 0, -y0 x~) in column blocks of four
+// (P's rows 1, 2, 3).  With the a1 rows first the matrix is [[P, 0, Q], [0, S, T]], so A^T A has a
+// zero block (0:4, 4:8) and so has its Cholesky factor R:
+//   R = [[R1, 0, X1], [0, R2, X2], [0, 0, R3]]   (R1, R2, R3 4x4 upper triangular)
+// An a1 row (p, 0, q) rotates into [R1 | X1] and leaves (0, 0, q') for R3; an a0 row (0, s, t)
+// into [R2 | X2], leaving t'.  Givens streaming then costs 168 instead of 348 operations a row,
+// R takes 62 doubles instead of 78, and R1 / R2 solve independently (R^T R is the same matrix
+// as for the dense factor: the same singular vectors).
+struct BlkR {
+  double R1[10], X1[16], R2[10], X2[16], R3[10];
+};
+constexpr int t4(int j, int l) { return j * 4 - (j * (j - 1)) / 2 + (l - j); }
+
+// one Givens pivot of the row's entry a (the pivot column's) against the diagonal r; returns
+// (c, s) and the new diagonal (givens_row's arithmetic)
+__device__ __forceinline__ void givens_cs(double &r, double aj, double &c, double &s) {
+  const double q = fma(r, r, aj * aj);
+  const bool live = q > 0.0;
+  const double inv = live ? rsqrt_fast(live ? q : 1.0) : 0.0;
+  c = live ? r * inv : 1.0;
+  s = aj * inv;
+  r = live ? q * inv : 0.0;
+}
+
+// row (p | q) into [Rk | Xk] (4x4 upper, 4x4), q' left in q
+__device__ __forceinline__ void givens_blk(double (&Rk)[10], double (&Xk)[16], double (&p)[4],
+                                           double (&q)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double c, s;
+    givens_cs(Rk[t4(j, j)], p[j], c, s);
+#pragma unroll
+    for (int l = j + 1; l < 4; ++l) {
+      const double rl = Rk[t4(j, l)];
+      Rk[t4(j, l)] = fma(c, rl, s * p[l]);
+      p[l] = fma(c, p[l], -s * rl);
+    }
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      const double xl = Xk[4 * j + l];
+      Xk[4 * j + l] = fma(c, xl, s * q[l]);
+      q[l] = fma(c, q[l], -s * xl);
+    }
+  }
+}
+
+__device__ __forceinline__ void givens_tri(double (&Rk)[10], double (&p)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double c, s;
+    givens_cs(Rk[t4(j, j)], p[j], c, s);
+#pragma unroll
+    for (int l = j + 1; l < 4; ++l) {
+      const double rl = Rk[t4(j, l)];
+      Rk[t4(j, l)] = fma(c, rl, s * p[l]);
+      p[l] = fma(c, p[l], -s * rl);
+    }
+  }
+}
+
+// the two DLT rows of one correspondence into R
+__device__ __forceinline__ void blk_add_point(BlkR &B, const PPt &p) {
+  const double xh[4] = {p.X, p.Y, p.Z, 1.0};
+  double a[4], b[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {  // a1 = (y2 x~, 0, -y0 x~)
+    a[j] = p.y2 * xh[j];
+    b[j] = -p.y0 * xh[j];
+  }
+  givens_blk(B.R1, B.X1, a, b);
+  givens_tri(B.R3, b);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {  // a0 = (0, -y2 x~, y1 x~)
+    a[j] = -p.y2 * xh[j];
+    b[j] = p.y1 * xh[j];
+  }
+  givens_blk(B.R2, B.X2, a, b);
+  givens_tri(B.R3, b);
+}
+
+// R^T z = v for one 4x4 block (forward), R w = z (backward); di = 1 / diag
+__device__ __forceinline__ void tri4_t(const double (&Rk)[10], const double *di, double *v) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double acc = v[j];
+#pragma unroll
+    for (int i = 0; i < j; ++i) acc = fma(-Rk[t4(i, j)], v[i], acc);
+    v[j] = acc * di[j];
+  }
+}
+__device__ __forceinline__ void tri4(const double (&Rk)[10], const double *di, double *v) {
+#pragma unroll
+  for (int j = 3; j >= 0; --j) {
+    double acc = v[j];
+#pragma unroll
+    for (int l = j + 1; l < 4; ++l) acc = fma(-Rk[t4(j, l)], v[l], acc);
+    v[j] = acc * di[j];
+  }
+}
+
+// v <- (R^T R)^-1 v with the block factor
+__device__ __forceinline__ void blk_solve(const BlkR &B, const double (&di)[12], double (&v)[12]) {
+  tri4_t(B.R1, di, v);
+  tri4_t(B.R2, di + 4, v + 4);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    double acc = v[8 + c];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc = fma(-B.X1[4 * j + c], v[j], fma(-B.X2[4 * j + c], v[4 + j], acc));
+    v[8 + c] = acc;
+  }
+  tri4_t(B.R3, di + 8, v + 8);
+  tri4(B.R3, di + 8, v + 8);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double a0 = v[j], a1 = v[4 + j];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      a0 = fma(-B.X1[4 * j + c], v[8 + c], a0);
+      a1 = fma(-B.X2[4 * j + c], v[8 + c], a1);
+    }
+    v[j] = a0;
+    v[4 + j] = a1;
+  }
+  tri4(B.R1, di, v);
+  tri4(B.R2, di + 4, v + 4);
+}
+
+// r = R v
+__device__ __forceinline__ void blk_mul(const BlkR &B, const double (&v)[12], double (&r)[12]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+#pragma unroll
+    for (int l = j; l < 4; ++l) {
+      a0 = fma(B.R1[t4(j, l)], v[l], a0);
+      a1 = fma(B.R2[t4(j, l)], v[4 + l], a1);
+      a2 = fma(B.R3[t4(j, l)], v[8 + l], a2);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      a0 = fma(B.X1[4 * j + c], v[8 + c], a0);
+      a1 = fma(B.X2[4 * j + c], v[8 + c], a1);
+    }
+    r[j] = a0;
+    r[4 + j] = a1;
+    r[8 + j] = a2;
+  }
+}
+
+// smallest_right_sv3 on the block factor: the start span(R^-1 e_11, e_10, e_9), then the same
+// three-vector block inverse iteration with the 3x3 Rayleigh-Ritz step
+__device__ __forceinline__ void blk_smallest_right_sv3(const BlkR &B, double (&x)[12]) {
+  double di[12];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    di[j] = 1.0 / B.R1[t4(j, j)];
+    di[4 + j] = 1.0 / B.R2[t4(j, j)];
+    di[8 + j] = 1.0 / B.R3[t4(j, j)];
+  }
+  double u[12], v[12], w[12];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    u[j] = j == 11 ? 1.0 : 0.0;
+    v[j] = j == 10 ? 1.0 : 0.0;
+    w[j] = j == 9 ? 1.0 : 0.0;
+  }
+  // R^-1 e_k: R3 back-substitution, then blocks 1, 2 from the X coupling
+  auto rinv = [&](double (&a)[12]) {
+    tri4(B.R3, di + 8, a + 8);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        a0 = fma(-B.X1[4 * j + c], a[8 + c], a0);
+        a1 = fma(-B.X2[4 * j + c], a[8 + c], a1);
+      }
+      a[j] = a0;
+      a[4 + j] = a1;
+    }
+    tri4(B.R1, di, a);
+    tri4(B.R2, di + 4, a + 4);
+  };
+  rinv(u);
+  rinv(v);
+  rinv(w);
+  orthonormalize3(u, v, w);
+#pragma unroll
+  for (int j = 0; j < 12; ++j) x[j] = u[j];
+  double prev_delta = 1.0;
+  for (int it = 0; it < RSAMD_PNP_MAXIT; ++it) {
+    blk_solve(B, di, u);
+    blk_solve(B, di, v);
+    blk_solve(B, di, w);
+    orthonormalize3(u, v, w);
+    double G[6];
+    {
+      double ru[12], rv[12], rw[12];
+      blk_mul(B, u, ru);
+      blk_mul(B, v, rv);
+      blk_mul(B, w, rw);
+      G[0] = dot12(ru, ru);
+      G[1] = dot12(rv, rv);
+      G[2] = dot12(rw, rw);
+      G[3] = dot12(ru, rv);
+      G[4] = dot12(ru, rw);
+      G[5] = dot12(rv, rw);
+    }
+    double Z[9] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0};
+    for (int sw = 0; sw < 8; ++sw) {
+      bool rotated = false;
+      jacobi_sym3(G, Z, 0, 1, rotated);
+      jacobi_sym3(G, Z, 0, 2, rotated);
+      jacobi_sym3(G, Z, 1, 2, rotated);
+      if (!rotated) break;
+    }
+    const int m0 = (G[0] <= G[1] && G[0] <= G[2]) ? 0 : (G[1] <= G[2] ? 1 : 2);
+    const int m1 = m0 == 0 ? 1 : 0, m2 = m0 == 2 ? 1 : 2;
+    double z0[3], z1[3], z2[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      z0[k] = m0 == 0 ? Z[3 * k] : (m0 == 1 ? Z[3 * k + 1] : Z[3 * k + 2]);
+      z1[k] = m1 == 0 ? Z[3 * k] : Z[3 * k + 1];
+      z2[k] = m2 == 1 ? Z[3 * k + 1] : Z[3 * k + 2];
+    }
+    double sgn = 0.0;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      const double a = fma(z0[0], u[j], fma(z0[1], v[j], z0[2] * w[j]));
+      const double b = fma(z1[0], u[j], fma(z1[1], v[j], z1[2] * w[j]));
+      const double c = fma(z2[0], u[j], fma(z2[1], v[j], z2[2] * w[j]));
+      sgn = fma(a, x[j], sgn);
+      u[j] = a;
+      v[j] = b;
+      w[j] = c;
+    }
+    sgn = sgn < 0.0 ? -1.0 : 1.0;
+    double delta = 0.0;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      const double nv = sgn * u[j];
+      delta = fmax(delta, fabs(nv - x[j]));
+      x[j] = nv;
+    }
+    if (it > 0 && !(delta > 1e-15)) break;
+    if (it > 1 && delta < 1e-13 && delta > 0.5 * prev_delta) break;
+    prev_delta = delta;
+  }
+  const double in = 1.0 / sqrt(dot12(x, x));
+#pragma unroll
+  for (int j = 0; j < 12; ++j) x[j] *= in;
+}
+
+__device__ __forceinline__ void blk_zero(BlkR &B) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) B.R1[i] = B.R2[i] = B.R3[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) B.X1[i] = B.X2[i] = 0.0;
+}
+
 // cond = false: the reference DLT on the raw world points (pnp.py:132-160).
 // cond = true (the cv.solvePnPRansac drop-in): the sample's world points are first centred on
 // their centroid c and scaled to unit RMS distance s (Hartley conditioning), the DLT solves for
@@ -261,9 +599,14 @@ __device__ __forceinline__ void enforce_pose(const double (&c0)[12], double (&Rm
 template <bool Cond, class IndexAt>
 __device__ __forceinline__ void pnp_solve_points(const PPt *pts, int k, IndexAt index_at,
                                                  double (&Rm)[9], double (&t)[3]) {
+#if RSAMD_PNP_BLOCK == 3
+  BlkR R;
+  blk_zero(R);
+#else
   double R[78];
 #pragma unroll
   for (int i = 0; i < 78; ++i) R[i] = 0.0;
+#endif
   double cx = 0.0, cy = 0.0, cz = 0.0, sc = 1.0;
   if (Cond) {
     for (int q = 0; q < k; ++q) {
@@ -291,13 +634,21 @@ __device__ __forceinline__ void pnp_solve_points(const PPt *pts, int k, IndexAt 
       p.Y = (p.Y - cy) * isc;
       p.Z = (p.Z - cz) * isc;
     }
+#if RSAMD_PNP_BLOCK == 3
+    blk_add_point(R, p);
+#else
     double a0[12], a1[12];
     dlt_rows(p, a0, a1);
     givens_row(R, a0);
     givens_row(R, a1);
+#endif
   }
   double c0[12];
+#if RSAMD_PNP_BLOCK == 3
+  blk_smallest_right_sv3(R, c0);
+#else
   smallest_right_sv(R, c0);
+#endif
   enforce_pose(c0, Rm, t);
   if (Cond) {
     t[0] = sc * t[0] - (Rm[0] * cx + Rm[1] * cy + Rm[2] * cz);
@@ -443,16 +794,11 @@ __global__ __launch_bounds__(64) void k_pnp_minimal_all(const PPt *__restrict__ 
 __global__ __launch_bounds__(64) void k_pnp_dlt_all(const PPt *__restrict__ pts, int m,
                                                     double *__restrict__ out) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  double R[78];
-  for (int i = 0; i < 78; ++i) R[i] = 0.0;
-  for (int q = 0; q < m; ++q) {
-    double a0[12], a1[12];
-    dlt_rows(pts[q], a0, a1);
-    givens_row(R, a0);
-    givens_row(R, a1);
-  }
+  BlkR R;
+  blk_zero(R);
+  for (int q = 0; q < m; ++q) blk_add_point(R, pts[q]);
   double c0[12], Rm[9], t[3];
-  smallest_right_sv(R, c0);
+  blk_smallest_right_sv3(R, c0);
   enforce_pose(c0, Rm, t);
   for (int q = 0; q < 9; ++q) out[q] = Rm[q];
   for (int q = 0; q < 3; ++q) out[9 + q] = t[q];
@@ -484,23 +830,26 @@ __device__ __forceinline__ bool pnp_inlier_ref(const double *P, const PPt &p, do
 // the same arithmetic; the host checks best_count == n_med).
 //
 // The band (u = 2^-53, first-order error analysis, then x2 for the second-order terms).  With
-// S_i = sum_j |R_ij x_j| + |t_i| <= L = rmax |x|_1 + tmax (rmax the largest row 2-norm of R,
-// Cauchy-Schwarz), Q = |q2|, U = max(|u|, |v|), d = (du, dv), D = |d|^2, a = |du| + |dv|:
+// S_i = sum_j |R_ij x_j| + |t_i| <= L = rmax xmax + tmax (rmax the largest row 2-norm of R,
+// Cauchy-Schwarz; xmax >= |x|_1 and umax >= max(|u|, |v|) over the call's points, from the host),
+// Q = |q2|, d = (du, dv), D = |d|^2, a = |du| + |dv|:
 //   * each q_i (either fma chain, the reference's with + t apart) is within 4u S_i of exact;
-//   * fast: |d_i - A_i| <= 3u (U S_2 + S_i) + u |d_i|, A_i = u_i q2* - q_i* the exact residual;
-//     and e* q2^2 differs from |A|^2 by the relative 2 (3u S_2 / Q) of q2's error;
+//   * fast: |d_i - A_i| <= 3u (umax S_2 + S_i) + u |d_i|, A_i = u_i q2* - q_i* the exact
+//     residual; and e* q2^2 differs from |A|^2 by the relative 2 (3u S_2 / Q) of q2's error;
 //   * reference: |a_i - a_i*| Q <= 4u (S_i + |q_i| / Q S_2) + u |q_i| + u |A_i| (the quotient's
 //     and the difference's roundings), and the dot product adds 2u D;
 //   * thr q2^2 is rounded twice (2u).
-// Collected with g = 4.01u L (3 + U + L / Q):  band = 2 (2 g a + 4 g^2 + u (D (8.1 + 6.1 L / Q)
+// Collected with g = 4.01u L (3 + umax + L / Q):  band = 2 (2 g a + 4 g^2 + u (D (8.1 + 6.1 L / Q)
 // + 2.01 thr q2^2)).  If D - thr q2^2 > band the exact e exceeds thr by more than the
 // reference's own error (outlier in both); below -band it is an inlier in both.  Q = 0, a NaN or
-// an infinity makes the band non-finite, and the pair takes the reference test.
+// an infinity makes the band non-finite, and the pair takes the reference test.  Per point the
+// band costs a reciprocal estimate and ~8 FMAs (the per-hypothesis L and constants hoisted).
 template <bool Exact>
 __global__ __launch_bounds__(256) void k_pnp_count(const PPt *__restrict__ pts, int m, int H,
                                                    const double *__restrict__ Psoa, int64_t ld,
                                                    int chunk, int nchunks, double thresh,
-                                                   PxMetric mt, int *__restrict__ counts) {
+                                                   PxMetric mt, double xmax, double umax,
+                                                   int *__restrict__ counts) {
   const int lane = threadIdx.x & 63;
   const int u = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   const int ngroups = (H + 63) >> 6;
@@ -513,15 +862,18 @@ __global__ __launch_bounds__(256) void k_pnp_count(const PPt *__restrict__ pts, 
 #pragma unroll
   for (int q = 0; q < 12; ++q) P[q] = Psoa[q * ld + hl];
   constexpr double kU = 0x1p-53;
-  double rmax = 0.0, tmax = 0.0;
+  double L = 0.0, g0 = 0.0, g1 = 0.0;
   if (Exact) {
+    double rmax = 0.0, tmax = 0.0;
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
       rmax = fmax(rmax, fma(P[3 * r], P[3 * r], fma(P[3 * r + 1], P[3 * r + 1], P[3 * r + 2] * P[3 * r + 2])));
       tmax = fmax(tmax, fabs(P[9 + r]));
     }
     // (a NaN pose makes D NaN, so its band is NaN and the reference test decides: false)
-    rmax = sqrt(rmax) * (1.0 + 8.0 * kU);
+    L = fma(sqrt(rmax) * (1.0 + 8.0 * kU), xmax, tmax) * (1.0 + 4.0 * kU);
+    g0 = 2.0 * (4.01 * kU) * L * (3.0 + umax);  // 2 g = g0 + g1 L / Q
+    g1 = 2.0 * (4.01 * kU) * L;
   }
   int cnt = 0;
   for (int i = p0; i < p1; ++i) {
@@ -530,19 +882,18 @@ __global__ __launch_bounds__(256) void k_pnp_count(const PPt *__restrict__ pts, 
     const double q1 = fma(P[3], p.X, fma(P[4], p.Y, fma(P[5], p.Z, P[10])));
     const double q2 = fma(P[6], p.X, fma(P[7], p.Y, fma(P[8], p.Z, P[11])));
     // |M (pi(y) - pi(q))|^2 <= thr  <=>  |M (u q2 - q0, v q2 - q1)|^2 <= thr q2^2, q2 != 0
-    // (identity M: a du + 0 dv == du and 1 dv == dv exactly, the reference-mode test)
+    // (identity M in reference mode: the plain residual)
     const double du0 = fma(p.u, q2, -q0), dv = fma(p.v, q2, -q1);
-    const double du = fma(mt.a, du0, mt.b * dv), dvm = mt.c * dv;
+    const double du = Exact ? du0 : fma(mt.a, du0, mt.b * dv), dvm = Exact ? dv : mt.c * dv;
     const double lhs = fma(du, du, dvm * dvm);
     const double rhs = thresh * (q2 * q2);
     bool in = q2 != 0.0 && lhs <= rhs;
     if (Exact) {
-      const double L = fma(fabs(p.X) + fabs(p.Y) + fabs(p.Z), rmax, tmax);
       const double Lr = L * __builtin_amdgcn_rcp(fabs(q2));
-      const double gg = (4.01 * kU) * L * (3.0 + fmax(fabs(p.u), fabs(p.v)) + Lr);
+      const double g2 = fma(g1, Lr, g0);                          // 2 g
       const double a = fabs(du) + fabs(dv);
-      const double band = 2.0 * fma(2.0 * gg, a + 2.0 * gg,
-                                    kU * fma(lhs, fma(6.1, Lr, 8.1), 2.01 * rhs));
+      const double band = fma(2.0 * g2, a + g2,                     // 2 (2 g a + 4 g^2 ...
+                              (2.0 * kU) * fma(lhs, fma(6.1, Lr, 8.1), 2.01 * rhs));
       if (!(fabs(lhs - rhs) > band)) in = pnp_inlier_ref(P, p, thresh);
     }
     cnt += in ? 1 : 0;
@@ -965,6 +1316,25 @@ using rs::hip_fail;
 
 static size_t align256(size_t b) { return (b + 255) / 256 * 256; }
 
+// Bounds of the call's points for k_pnp_count<true>'s guard band: xmax >= |x|_1 and umax >=
+// max(|y0 / y2|, |y1 / y2|) over all points (a non-finite point makes both infinite: every pair
+// then takes the reference-order test).
+static void pnp_band_bounds(const double *X, const double *y, int64_t m, double *xmax,
+                            double *umax) {
+  double a = 0.0, b = 0.0;
+  bool bad = false;
+  for (int64_t i = 0; i < m; ++i) {
+    const double sx = std::fabs(X[3 * i]) + std::fabs(X[3 * i + 1]) + std::fabs(X[3 * i + 2]);
+    const double u = y[3 * i] / y[3 * i + 2], v = y[3 * i + 1] / y[3 * i + 2];
+    bad = bad || !std::isfinite(sx) || !std::isfinite(u) || !std::isfinite(v);
+    a = std::max(a, sx);
+    b = std::max(b, std::max(std::fabs(u), std::fabs(v)));
+  }
+  const double inf = std::numeric_limits<double>::infinity();
+  *xmax = bad ? inf : a * (1.0 + 1e-15);
+  *umax = bad ? inf : b * (1.0 + 1e-15);
+}
+
 extern "C" int rs_pnp_dlt(rs_ctx *c, const double *X, const double *y, int64_t m, double *R_out,
                           double *t_out) {
   if (!c || !X || !y || !R_out || !t_out) return fail(RS_EINVAL, "null pointer");
@@ -1109,9 +1479,12 @@ extern "C" int rs_pnp_ransac(rs_ctx *c, const double *X_med, const double *y_med
   const int chunk = static_cast<int>((m_med + nch - 1) / nch);
   nch = (m_med + chunk - 1) / chunk;
   const int64_t units = groups * nch;
+  double xmax = 0.0, umax = 0.0;
+  pnp_band_bounds(X_med, y_med, m_med, &xmax, &umax);
   hipLaunchKernelGGL(rsd::k_pnp_count<true>, dim3((units + 3) / 4), dim3(256), 0, s, pm,
                      static_cast<int>(m_med), static_cast<int>(Hm), dP, ld, chunk,
-                     static_cast<int>(nch), thresh, rsd::PxMetric{1.0, 0.0, 1.0}, dcnt);
+                     static_cast<int>(nch), thresh, rsd::PxMetric{1.0, 0.0, 1.0}, xmax, umax,
+                     dcnt);
   HIP_TRY(hipGetLastError());
   if (timed) HIP_TRY(hipEventRecord(c->pnp_ev[2], s));
   hipLaunchKernelGGL(rsd::k_pnp_select, dim3(1), dim3(1024), 0, s, dcnt, static_cast<int>(Hm), dP,
@@ -1182,9 +1555,12 @@ extern "C" int rs_pnp_count_poses(rs_ctx *c, const double *X, const double *y, i
   const int chunk = static_cast<int>((m + nch - 1) / nch);
   nch = (m + chunk - 1) / chunk;
   const int64_t units = groups * nch;
+  double xmax = 0.0, umax = 0.0;
+  pnp_band_bounds(X, y, m, &xmax, &umax);
   hipLaunchKernelGGL(rsd::k_pnp_count<true>, dim3((units + 3) / 4), dim3(256), 0, s, pts,
                      static_cast<int>(m), static_cast<int>(H), dP, ld, chunk,
-                     static_cast<int>(nch), thresh, rsd::PxMetric{1.0, 0.0, 1.0}, dcnt);
+                     static_cast<int>(nch), thresh, rsd::PxMetric{1.0, 0.0, 1.0}, xmax, umax,
+                     dcnt);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(counts_out, dcnt, sizeof(int) * H, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
@@ -1293,7 +1669,7 @@ extern "C" int rs_pnp_ransac_cv(rs_ctx *c, const double *X, const double *uv, in
   const int64_t units = groups * nch;
   hipLaunchKernelGGL(rsd::k_pnp_count<false>, dim3((units + 3) / 4), dim3(256), 0, s, pts,
                      static_cast<int>(m), static_cast<int>(H), dP, ld, chunk,
-                     static_cast<int>(nch), thresh, mt, dcnt);
+                     static_cast<int>(nch), thresh, mt, 0.0, 0.0, dcnt);
   HIP_TRY(hipGetLastError());
   std::vector<int> cnt(H);
   HIP_TRY(hipMemcpyAsync(cnt.data(), dcnt, sizeof(int) * H, hipMemcpyDeviceToHost, s));

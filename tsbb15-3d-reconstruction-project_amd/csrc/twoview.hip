@@ -1156,6 +1156,12 @@ extern "C" int rs_pairs_two_view(rs_ctx *c, const double *p1, const double *p2, 
   if (K && (!y1 || !y2)) return fail(RS_EINVAL, "K needs y1 and y2");
   if (max_iter < 1 || max_iter > 100000) return fail(RS_EINVAL, "max_iter must be in [1, 1e5]");
   if (!off || B < 1 || B > (1 << 20)) return fail(RS_EINVAL, "bad pair count");
+  // the offsets size this call's buffers (tp): validated before use (pairs_enqueue checks them
+  // again for its own callers)
+  if (off[0] != 0) return fail(RS_EINVAL, "offsets must start at 0");
+  for (int64_t b = 0; b < B; ++b)
+    if (off[b + 1] < off[b] || off[b + 1] - off[b] > (1 << 24))
+      return fail(RS_EINVAL, "offsets must be non-decreasing");
   const int64_t tp = off[B] > 0 ? off[B] : 1;
   // the stages' buffers after the pair RANSAC's, then the output block (one download)
   const size_t sz[] = {sizeof(int64_t) * (B + 1), sizeof(int32_t) * B, sizeof(double) * 9 * B,

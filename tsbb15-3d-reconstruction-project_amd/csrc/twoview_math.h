@@ -538,8 +538,12 @@ __device__ __forceinline__ int roots_real_parts(const double (&g)[7], double (&o
 // the real part of every root and at t = inf, the argmin (first NaN wins, as np.argmin), the
 // closest points on the two lines, back-transfer, linear triangulation.
 // ----------------------------------------------------------------------------------------
-// FAST (k_relative_pose, which reads only the depth signs): register-resident roots and the
-// 2-eps Jacobi stop; else the arithmetic rs_triangulate_optimal and the gold standard keep.
+// FAST (k_relative_pose, which reads only the depth signs, and the LM gold standard
+// k_gold_standard, whose start it is): register-resident roots, fast reciprocals and the 2-eps
+// Jacobi stop -- the same points to rounding (the LM start's cost equals the reference start's to
+// 1e-9, test_gpu_twoview.py), not bit for bit; else the arithmetic of rs_triangulate_optimal
+// (the reference-faithful TRF path's start, bit-reproducible against lab3.triangulate_optimal's
+// order).
 template <bool FAST = false>
 __device__ __forceinline__ void triangulate_optimal(const double *C1, const double *C2,
                                                     double x1, double y1, double x2, double y2,
