@@ -1955,9 +1955,29 @@ constexpr int kTupRing = 2 * kTupBlk;       // words staged per wave
 // (entries 0..n1: the trace reads F at every state it reaches, n1 included)
 __host__ __device__ constexpr int tup_jpad(int n1) { return (n1 + 2) & ~1; }
 __host__ __device__ constexpr int tup_table(int n1) { return tup_jpad(n1) + 64 + (RSAMD_TUPF ? 8 : 0); }
-__host__ __device__ constexpr int64_t tup_lds_bytes(int n1) {
-  return (static_cast<int64_t>(sizeof(uint32_t)) * kTupRing +
-          static_cast<int64_t>(sizeof(uint16_t)) * tup_table(n1)) * kTupWaves;
+__host__ __device__ constexpr int64_t tup_wave_bytes(int n1) {
+  return static_cast<int64_t>(sizeof(uint32_t)) * kTupRing +
+         static_cast<int64_t>(sizeof(uint16_t)) * tup_table(n1);
+}
+__host__ __device__ constexpr int64_t tup_lds_bytes(int n1) { return tup_wave_bytes(n1) * kTupWaves; }
+// Waves per tuple workgroup for population n1: kTupWaves unless a smaller workgroup keeps at
+// least a quarter more waves resident in a CU's 160 KB of LDS.  (C5, N = 10 000: 21 KB per
+// wave, so 4-wave workgroups left ONE workgroup -- four waves, one per SIMD -- on a CU; 1-wave
+// workgroups keep 7.  C2 keeps 4: 28 waves against at most 31.)
+inline int tup_waves_for(int n1) {
+  constexpr int64_t kLdsCu = 160 * 1024;
+  const int64_t pw = tup_wave_bytes(n1);
+  const int64_t base = (kLdsCu / (kTupWaves * pw)) * kTupWaves;
+  int best = kTupWaves;
+  int64_t bw = base;
+  for (int t = kTupWaves - 1; t >= 1; --t) {
+    const int64_t waves = (kLdsCu / (t * pw)) * t;
+    if (waves > bw) {
+      bw = waves;
+      best = t;
+    }
+  }
+  return 4 * bw >= 5 * base ? best : kTupWaves;
 }
 // ring blocks held in registers ahead of the one being parsed: the stream comes from HBM (far
 // larger than the caches), and at large N the LDS table leaves one wave per SIMD, so one block
@@ -1987,7 +2007,7 @@ __global__ __launch_bounds__(64 * kTupWaves) void k_np_tuples_wave(
   extern __shared__ uint32_t tup_lds[];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
   // hypotheses [lo, hi) of the segment (those the caller asked for), out row h - lo
-  const int64_t h = lo + static_cast<int64_t>(blockIdx.x) * kTupWaves + wv;
+  const int64_t h = lo + static_cast<int64_t>(blockIdx.x) * (blockDim.x >> 6) + wv;
   if (h >= hi || h >= *got) return;  // wave-uniform; the kernel has no workgroup barrier
   uint32_t *ring = tup_lds + static_cast<size_t>(wv) * (kTupRing + tup_table(n1) / 2);
   uint16_t *J = reinterpret_cast<uint16_t *>(ring + kTupRing);
@@ -2745,7 +2765,11 @@ int shard_layout(rs_np_shard &w, int32_t pos, int64_t count) {
   // their time in the dense all-entry phase (~N draws per surviving trajectory), so the count
   // drops before the length does (C2 over 8 ranks, per-rank parse: 512 chunks of 73 728
   // draws 3.1 ms, 256 of 141 312 2.7 ms, 128 2.9 ms, 64 4.0 ms).
-  const int64_t Cdef = static_cast<int64_t>(w.cus) * (w.n1 < 4096 ? 2 : 1);
+  // (N - 1 >= 4096 too: the entry kernel's 8 (N - 1) bytes of LDS still fit two workgroups per
+  // CU at N = 10 000, so 2 x CUs chunks parse in one round, and the tracking kernel's serial
+  // chains are shorter -- C5 per 1e6 hypotheses: 1 x CUs (chunks capped at 2^24 draws: 435 per
+  // segment) 237.7 ms, 2 x CUs 226.9 ms, 3 x CUs 265.7 ms (entry in two rounds), gpurun_out r06g)
+  const int64_t Cdef = static_cast<int64_t>(w.cus) * 2;
   const int64_t C0 = knob_cpr() ? knob_cpr()
                                 : std::max<int64_t>(1, std::min<int64_t>(
                                                            Cdef, Dr / std::max<int64_t>(kWmin, 64 * w.n1)));
@@ -3069,9 +3093,10 @@ int shard_enqueue_starts(rs_np_shard &w, int64_t cap, int64_t *got) {
 // 4: the tuples of hypotheses [lo, hi) (rank-local start indices; waves at or beyond *got exit)
 void shard_launch_tuples(rs_np_shard &w, int64_t lo, int64_t hi, const int64_t *got,
                          int32_t *d_out) {
-  (w.py ? k_np_tuples_wave<true> : k_np_tuples_wave<false>)<<<static_cast<unsigned>(cdiv(hi - lo, kTupWaves)),
-                                                               64 * kTupWaves,
-                                                               static_cast<size_t>(tup_lds_bytes(w.n1)),
+  const int tw = tup_waves_for(w.n1);
+  (w.py ? k_np_tuples_wave<true> : k_np_tuples_wave<false>)<<<static_cast<unsigned>(cdiv(hi - lo, tw)),
+                                                               64 * tw,
+                                                               static_cast<size_t>(tup_wave_bytes(w.n1) * tw),
                                                                w.ctx->stream>>>(
       w.d_stream + (w.s_lo - w.wbase), w.d_starts, got, lo, hi, w.n1, w.k, d_out, w.d_err,
       w.nwords);
