@@ -1964,7 +1964,10 @@ __host__ __device__ constexpr int64_t tup_lds_bytes(int n1) { return tup_wave_by
 // least a quarter more waves resident in a CU's 160 KB of LDS.  (C5, N = 10 000: 21 KB per
 // wave, so 4-wave workgroups left ONE workgroup -- four waves, one per SIMD -- on a CU; 1-wave
 // workgroups keep 7.  C2 keeps 4: 28 waves against at most 31.)
+int64_t env_i64(const char *name);
 inline int tup_waves_for(int n1) {
+  static const int forced = static_cast<int>(env_i64("RSAMD_TUP_TW"));  // A/B: 1 .. kTupWaves
+  if (forced >= 1 && forced <= kTupWaves) return forced;
   constexpr int64_t kLdsCu = 160 * 1024;
   const int64_t pw = tup_wave_bytes(n1);
   const int64_t base = (kLdsCu / (kTupWaves * pw)) * kTupWaves;
