@@ -53,6 +53,7 @@ namespace rsd {
 
 constexpr int ridx(int j, int l) { return j * 12 - (j * (j - 1)) / 2 + (l - j); }
 
+
 __device__ __forceinline__ void givens_row(double (&R)[78], double (&a)[12]) {
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
@@ -479,6 +480,47 @@ __device__ __forceinline__ void blk_mul(const BlkR &B, const double (&v)[12], do
   }
 }
 
+// G = (R [u v w])^T (R [u v w]) accumulated a row of R at a time (no 12-vector temporaries:
+// the kernel is at the register limit)
+__device__ __forceinline__ void blk_gram3(const BlkR &B, const double (&u)[12],
+                                          const double (&v)[12], const double (&w)[12],
+                                          double (&G)[6]) {
+#pragma unroll
+  for (int i = 0; i < 6; ++i) G[i] = 0.0;
+  auto acc = [&](double a, double b, double c) {
+    G[0] = fma(a, a, G[0]);
+    G[1] = fma(b, b, G[1]);
+    G[2] = fma(c, c, G[2]);
+    G[3] = fma(a, b, G[3]);
+    G[4] = fma(a, c, G[4]);
+    G[5] = fma(b, c, G[5]);
+  };
+#pragma unroll
+  for (int blk = 0; blk < 3; ++blk) {
+    const double *Rk = blk == 0 ? B.R1 : (blk == 1 ? B.R2 : B.R3);
+    const double *Xk = blk == 0 ? B.X1 : B.X2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      double a = 0.0, b = 0.0, c = 0.0;
+#pragma unroll
+      for (int l = j; l < 4; ++l) {
+        a = fma(Rk[t4(j, l)], u[4 * blk + l], a);
+        b = fma(Rk[t4(j, l)], v[4 * blk + l], b);
+        c = fma(Rk[t4(j, l)], w[4 * blk + l], c);
+      }
+      if (blk < 2) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          a = fma(Xk[4 * j + q], u[8 + q], a);
+          b = fma(Xk[4 * j + q], v[8 + q], b);
+          c = fma(Xk[4 * j + q], w[8 + q], c);
+        }
+      }
+      acc(a, b, c);
+    }
+  }
+}
+
 // smallest_right_sv3 on the block factor: the start span(R^-1 e_11, e_10, e_9), then the same
 // three-vector block inverse iteration with the 3x3 Rayleigh-Ritz step
 __device__ __forceinline__ void blk_smallest_right_sv3(const BlkR &B, double (&x)[12]) {
@@ -526,18 +568,7 @@ __device__ __forceinline__ void blk_smallest_right_sv3(const BlkR &B, double (&x
     blk_solve(B, di, w);
     orthonormalize3(u, v, w);
     double G[6];
-    {
-      double ru[12], rv[12], rw[12];
-      blk_mul(B, u, ru);
-      blk_mul(B, v, rv);
-      blk_mul(B, w, rw);
-      G[0] = dot12(ru, ru);
-      G[1] = dot12(rv, rv);
-      G[2] = dot12(rw, rw);
-      G[3] = dot12(ru, rv);
-      G[4] = dot12(ru, rw);
-      G[5] = dot12(rv, rw);
-    }
+    blk_gram3(B, u, v, w, G);
     double Z[9] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0};
     for (int sw = 0; sw < 8; ++sw) {
       bool rotated = false;
@@ -555,18 +586,16 @@ __device__ __forceinline__ void blk_smallest_right_sv3(const BlkR &B, double (&x
       z1[k] = m1 == 0 ? Z[3 * k] : Z[3 * k + 1];
       z2[k] = m2 == 1 ? Z[3 * k + 1] : Z[3 * k + 2];
     }
-    double sgn = 0.0;
 #pragma unroll
     for (int j = 0; j < 12; ++j) {
       const double a = fma(z0[0], u[j], fma(z0[1], v[j], z0[2] * w[j]));
       const double b = fma(z1[0], u[j], fma(z1[1], v[j], z1[2] * w[j]));
       const double c = fma(z2[0], u[j], fma(z2[1], v[j], z2[2] * w[j]));
-      sgn = fma(a, x[j], sgn);
       u[j] = a;
       v[j] = b;
       w[j] = c;
     }
-    sgn = sgn < 0.0 ? -1.0 : 1.0;
+    const double sgn = dot12(u, x) < 0.0 ? -1.0 : 1.0;
     double delta = 0.0;
 #pragma unroll
     for (int j = 0; j < 12; ++j) {
