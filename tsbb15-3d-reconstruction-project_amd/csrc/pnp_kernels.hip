@@ -297,6 +297,18 @@ __device__ __forceinline__ void orthonormalize3(double (&u)[12], double (&v)[12]
 #ifndef RSAMD_PNP_BLOCK
 #define RSAMD_PNP_BLOCK 3
 #endif
+// The block iteration stops when the Ritz vector moves <= RSAMD_PNP_TOL (or stagnates at the
+// rounding floor).  The samples' own conditioning sets how closely any two SVDs agree: over 400
+// noisy C3 samples the GPU pose equals numpy's (oracle/pnp_ref.pnp_dlt) to max |dR| 4.6e-13
+// (p99 8.9e-14) at 1e-15, 1e-13 and 1e-12 alike (test_dlt_minimal_samples_accuracy_against_
+// numpy_svd), while the slowest trial's sweeps -- the kernel's time -- fall: C3 k_pnp_solve
+// 0.075 / 0.068 / 0.065 ms (tools/pnp_tol_ab.sh).
+#ifndef RSAMD_PNP_TOL
+#define RSAMD_PNP_TOL 1e-12
+#endif
+#ifndef RSAMD_PNP_HOUSE6
+#define RSAMD_PNP_HOUSE6 1  // six-point samples by Householder (blk_house6)
+#endif
 // Constraint enforcement (pnp.py:141-145): C0 = (A | b) -> (R, t).
 __device__ __forceinline__ void enforce_pose(const double (&c0)[12], double (&Rm)[9],
                                              double (&t)[3]) {
@@ -603,13 +615,100 @@ __device__ __forceinline__ void blk_smallest_right_sv3(const BlkR &B, double (&x
       delta = fmax(delta, fabs(nv - x[j]));
       x[j] = nv;
     }
-    if (it > 0 && !(delta > 1e-15)) break;
+    if (it > 0 && !(delta > RSAMD_PNP_TOL)) break;
     if (it > 1 && delta < 1e-13 && delta > 0.5 * prev_delta) break;
     prev_delta = delta;
   }
   const double in = 1.0 / sqrt(dot12(x, x));
 #pragma unroll
   for (int j = 0; j < 12; ++j) x[j] *= in;
+}
+
+// Six correspondences (the minimal DLT sample) by Householder instead of row streaming.  Block 1
+// is [P | Q] with rows y2 x~ | -y0 x~, block 2 is [S | T] with rows -y2 x~ | y1 x~, and S = -P:
+// with P = H [R1; 0] (four reflections, applied to Q and T as well),
+//   H^T [P | 0 | Q] = [[R1, 0, X1 = (H^T Q)_top], [0, 0, (H^T Q)_bot]],
+//   H^T [0 | S | T] = [[0, -R1, (H^T T)_top], [0, 0, (H^T T)_bot]],
+// so R2 = R1 and X2 = -(H^T T)_top (the second block's rows negated), and R3 is the QR of the four
+// leftover rows.  ~700 operations for the sample instead of twelve streamed rows' ~3 300, and R1
+// is shared (RSAMD_PNP_HOUSE6 = 0: the streaming form for k = 6 as well).
+__device__ __forceinline__ void blk_house6(const PPt (&p)[6], BlkR &B) {
+  double P[6][4], Q[6][4], T[6][4];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const double xh[4] = {p[i].X, p[i].Y, p[i].Z, 1.0};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      P[i][c] = p[i].y2 * xh[c];
+      Q[i][c] = -p[i].y0 * xh[c];
+      T[i][c] = p[i].y1 * xh[c];
+    }
+  }
+  double diag[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    // reflection of column k, rows k..5: v = (1, x_{k+1..} / (alpha - beta)), tau = 2 / v^T v
+    const double alpha = P[k][k];
+    double sig = 0.0;
+#pragma unroll
+    for (int i = k + 1; i < 6; ++i) sig = fma(P[i][k], P[i][k], sig);
+    const double nrm = sqrt(fma(alpha, alpha, sig));
+    const bool refl = sig > 0.0;
+    const double beta = refl ? (alpha >= 0.0 ? -nrm : nrm) : alpha;
+    const double sc = refl ? 1.0 / (alpha - beta) : 0.0;
+    double v[6];
+#pragma unroll
+    for (int i = k + 1; i < 6; ++i) v[i] = P[i][k] * sc;
+    double vv = 1.0;
+#pragma unroll
+    for (int i = k + 1; i < 6; ++i) vv = fma(v[i], v[i], vv);
+    const double tau = refl ? 2.0 / vv : 0.0;
+    diag[k] = beta;
+    // apply I - tau v v^T to the remaining columns of P and to Q, T
+    auto apply = [&](double (&M)[6][4], int c) {
+      double w = M[k][c];
+#pragma unroll
+      for (int i = k + 1; i < 6; ++i) w = fma(v[i], M[i][c], w);
+      w *= tau;
+      M[k][c] -= w;
+#pragma unroll
+      for (int i = k + 1; i < 6; ++i) M[i][c] = fma(-w, v[i], M[i][c]);
+    };
+#pragma unroll
+    for (int c = k + 1; c < 4; ++c) apply(P, c);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      apply(Q, c);
+      apply(T, c);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+#pragma unroll
+    for (int l = j; l < 4; ++l) {
+      const double r = l == j ? diag[j] : P[j][l];
+      B.R1[t4(j, l)] = r;
+      B.R2[t4(j, l)] = r;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      B.X1[4 * j + c] = Q[j][c];
+      B.X2[4 * j + c] = -T[j][c];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 10; ++i) B.R3[i] = 0.0;
+#pragma unroll
+  for (int i = 4; i < 6; ++i) {
+    double a[4], b[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      a[c] = Q[i][c];
+      b[c] = T[i][c];
+    }
+    givens_tri(B.R3, a);
+    givens_tri(B.R3, b);
+  }
 }
 
 __device__ __forceinline__ void blk_zero(BlkR &B) {
@@ -656,6 +755,22 @@ __device__ __forceinline__ void pnp_solve_points(const PPt *pts, int k, IndexAt 
     if (!(sc > 0.0)) sc = 1.0;
   }
   const double isc = 1.0 / sc;
+#if RSAMD_PNP_BLOCK == 3 && RSAMD_PNP_HOUSE6
+  if (k == 6) {
+    PPt p6[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      p6[q] = pts[index_at(q)];
+      if (Cond) {
+        p6[q].X = (p6[q].X - cx) * isc;
+        p6[q].Y = (p6[q].Y - cy) * isc;
+        p6[q].Z = (p6[q].Z - cz) * isc;
+      }
+    }
+    blk_house6(p6, R);
+    k = 0;  // (the streaming loop below is skipped)
+  }
+#endif
   for (int q = 0; q < k; ++q) {
     PPt p = pts[index_at(q)];
     if (Cond) {
