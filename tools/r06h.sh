@@ -10,7 +10,11 @@ for v in default RSAMD_TUP_TW=1 RSAMD_TUP_TW=2 default; do
   if [ "$v" = default ]; then e=""; else e="$v"; fi
   echo "== $v"; env $e timeout -k 10 120 python3 tools/probe_np_c2.py --reps 8 --split | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(min(d['wall_ms']), d['split_ms']['tuples'], d['split_ms']['parse_total'])" || exit 1
 done
-bash tools/pnp_ab.sh dotseq > $OUT/pnp_ab.txt 2>&1 || { echo pnp ab failed; exit 1; }
-grep -o '"lib[^R]*' $OUT/pnp_ab.txt
+if [ -n "$2" ]; then  # E5 A/B: the product against lib_ab/$2
+  for p in 1 2; do
+    echo -n "product "; timeout -k 10 120 python3 tools/probe_e5.py || exit 1
+    echo -n "$2 "; RSAMD_LIB=$(pwd)/tsbb15-3d-reconstruction-project_amd/lib_ab/$2/librsamd.so timeout -k 10 120 python3 tools/probe_e5.py || exit 1
+  done
+fi
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; tail $OUT/bench.err; exit 1; }
 echo bench ok
