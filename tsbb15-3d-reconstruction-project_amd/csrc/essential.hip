@@ -437,31 +437,14 @@ __global__ __launch_bounds__(64) void k_e5_build(E5Args a) {
   });
 }
 
-// (B) Gauss-Jordan on the first ten columns with partial pivoting.  RSAMD_E5_GJ_WAVE = 1 (the
-// default): one sample per wave, lane j (< 20) holds column j; the pivot column's lane finds the
-// pivot (the first largest |M[r][c]|, r >= c), and its column (the multipliers), the pivot row
-// and 1 / pivot reach the other lanes by v_readlane (wave-uniform SGPR operands: no LDS round
-// trip).  0: two samples per wave (32-lane halves), the same values by ds_bpermute shuffles.
-// Every element sees the same operations as a one-lane elimination: M[c][j] *= 1 / M[c][c],
-// M[r][j] = fma(-M[r][c], M[c][j], M[r][j]).
-#ifndef RSAMD_E5_GJ_WAVE
-#define RSAMD_E5_GJ_WAVE 1
-#endif
-constexpr int kGjPerWave = RSAMD_E5_GJ_WAVE ? 1 : 2;
-__device__ __forceinline__ double gj_bcast(double v, int src) {
-#if RSAMD_E5_GJ_WAVE
-  const uint64_t b = __builtin_bit_cast(uint64_t, v);
-  const uint32_t lo = __builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(b)), src);
-  const uint32_t hi = __builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(b >> 32)), src);
-  return __builtin_bit_cast(double, (static_cast<uint64_t>(hi) << 32) | lo);
-#else
-  return __shfl(v, src);
-#endif
-}
+// (B) Gauss-Jordan on the first ten columns with partial pivoting, two samples per wave: lane j
+// (< 20) of a 32-lane half holds column j of its sample's system; the pivot column's lane finds
+// the pivot (the first largest |M[r][c]|, r >= c), and its column (the multipliers) and 1 /
+// pivot are broadcast by shuffles.  Every element sees the same operations as a one-lane
+// elimination: M[c][j] *= 1 / M[c][c], M[r][j] = fma(-M[r][c], M[c][j], M[r][j]).
 __global__ __launch_bounds__(64) void k_e5_gj(E5Args a) {
-  const int lane = threadIdx.x & 63, g = RSAMD_E5_GJ_WAVE ? 0 : lane >> 5,
-            j = RSAMD_E5_GJ_WAVE ? lane : lane & 31;
-  const int s = blockIdx.x * kGjPerWave + g;
+  const int lane = threadIdx.x & 63, g = lane >> 5, j = lane & 31;
+  const int s = blockIdx.x * 2 + g;
   const bool own = s < a.S && j < 20;
   const int64_t ldw = a.ldw;
   double col[10];
@@ -481,12 +464,8 @@ __global__ __launch_bounds__(64) void k_e5_gj(E5Args a) {
         piv = r;
       }
     }
-#if RSAMD_E5_GJ_WAVE
-    piv = __builtin_amdgcn_readlane(piv, src);
-#else
     piv = __shfl(piv, src);
-#endif
-    best = gj_bcast(best, src);
+    best = __shfl(best, src);
     ok = ok && best > 0.0;
     // swap rows c and piv (a no-op on the reduced columns j < c, zero in both rows)
     double pc = col[c];
@@ -498,10 +477,10 @@ __global__ __launch_bounds__(64) void k_e5_gj(E5Args a) {
       pc = sw ? x : pc;
     }
     col[c] = pc;
-    const double inv = gj_bcast(1.0 / col[c], src);
+    const double inv = __shfl(1.0 / col[c], src);
     double f[10];
 #pragma unroll
-    for (int r = 0; r < 10; ++r) f[r] = gj_bcast(col[r], src);
+    for (int r = 0; r < 10; ++r) f[r] = __shfl(col[r], src);
     if (j > c) {
       col[c] *= inv;
 #pragma unroll
@@ -1184,7 +1163,7 @@ static int launch_e5_solve(rsd::E5Args &a, char *work, hipStream_t s) {
   a.split = e5_split();
   hipLaunchKernelGGL(rsd::k_e5_build, dim3((S + 63) / 64), dim3(64), 0, s, a);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(rsd::k_e5_gj, dim3((S + rsd::kGjPerWave - 1) / rsd::kGjPerWave), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(rsd::k_e5_gj, dim3((S + 1) / 2), dim3(64), 0, s, a);
   HIP_TRY(hipGetLastError());
   a.Pg = a.Mg;  // the 10 x 20 systems are dead after Gauss-Jordan (200 >= 50 doubles per sample)
   hipLaunchKernelGGL(rsd::k_e5_polys, dim3((S + 63) / 64), dim3(64), 0, s, a);
