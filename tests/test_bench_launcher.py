@@ -87,3 +87,26 @@ def test_cpu_baseline_is_reported_at_world_two():
     assert p.returncode == 0, p.stderr
     cb = json.loads(p.stdout.strip())["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] == 2 and cb["value"] > 0
+
+
+def test_under_torch_distributed_run_as_the_driver_launches_it():
+    """The driver's multi-GPU invocation: python -m torch.distributed.run --nnodes=1
+    --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N; every rank
+    prints nothing but rank 0's single line, and the world is the launcher's."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                        str(port), BENCH, "--gpus", "2", "--harness-only", "--no-cpu-baseline"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [x for x in p.stdout.splitlines() if x.strip().startswith("{")]
+    assert len(lines) == 1, p.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and [r["rank"] for r in rec["ranks"]] == [0, 1]
+    assert not any(r["launched"] for r in rec["ranks"])   # the external launcher's processes
