@@ -45,6 +45,18 @@ int ensure_scratch(rs_ctx *c, size_t bytes) {
   return RS_OK;
 }
 
+int ensure_pinned(rs_ctx *c, size_t bytes) {
+  if (c->pinned_bytes >= bytes) return RS_OK;
+  if (c->pinned) (void)hipHostFree(c->pinned);
+  c->pinned = nullptr;
+  c->pinned_bytes = 0;
+  size_t want = std::max<size_t>(bytes, 1 << 16);
+  hipError_t e = hipHostMalloc(&c->pinned, want);
+  if (e != hipSuccess) return hip_fail(e, "hipHostMalloc(staging)");
+  c->pinned_bytes = want;
+  return RS_OK;
+}
+
 }  // namespace rs
 
 using rs::fail;
@@ -117,6 +129,7 @@ extern "C" int rs_ctx_destroy(rs_ctx *c) {
   if (c->np_plan) rs_f8_plan_destroy(c->np_plan);
   rs::np_shard_free(c);
   if (c->scratch) (void)hipFree(c->scratch);
+  if (c->pinned) (void)hipHostFree(c->pinned);
   for (auto &e : c->pnp_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);

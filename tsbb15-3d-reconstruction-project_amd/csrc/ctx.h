@@ -14,6 +14,8 @@ struct rs_ctx {
   hipStream_t aux_stream = nullptr;
   void *scratch = nullptr;     // grow-only device scratch for single-shot ops
   size_t scratch_bytes = 0;
+  void *pinned = nullptr;      // grow-only pinned host staging of single-shot inputs (one DMA
+  size_t pinned_bytes = 0;     // copy instead of several pageable ones; the ops synchronise)
   rs_f8_plan *np_plan = nullptr;  // cached plan of rs_f8_ransac_np
   rs_np_shard *np_shard = nullptr;  // world-1 parity-stream session (np_choice_device)
   void *comm = nullptr;        // ncclComm_t
@@ -34,6 +36,7 @@ struct rs_ctx {
 namespace rs {
 int hip_fail(hipError_t e, const char *what);
 int ensure_scratch(rs_ctx *c, size_t bytes);
+int ensure_pinned(rs_ctx *c, size_t bytes);
 void np_shard_free(rs_ctx *c);
 int np_preload();  // the parse kernels' code object onto the current device (rs_ctx_create)
 bool np_gpu_supported(int64_t n, int32_t k);  // within the GPU parse's population range

@@ -1064,10 +1064,9 @@ __device__ __forceinline__ void sel_better(int c, int i, int &bm, int &bi) {
     bi = i;
   }
 }
-__global__ __launch_bounds__(1024) void k_pnp_select(const int *__restrict__ counts, int H,
-                                                     const double *__restrict__ Psoa,
-                                                     int64_t ld, PnpDevResult *res,
-                                                     const unsigned char *__restrict__ mirf) {
+__device__ void pnp_select_block(const int *__restrict__ counts, int H,
+                                 const double *__restrict__ Psoa, int64_t ld, PnpDevResult *res,
+                                 const unsigned char *__restrict__ mirf) {
   __shared__ int sm[2][16], si[2][16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   int bm[2] = {0, 0}, bi[2] = {0x7fffffff, 0x7fffffff};  // front-facing, mirrored
@@ -1165,9 +1164,9 @@ __device__ void ordered_compact(int m, Pred pred, bool have, int64_t *out, int64
   __syncthreads();
 }
 
-__global__ __launch_bounds__(1024) void k_pnp_inliers(const PPt *__restrict__ med, int m_med,
-                                                      const PPt *__restrict__ high, int m_high,
-                                                      double thresh, PnpDevResult *res) {
+__device__ void pnp_inliers_block(const PPt *__restrict__ med, int m_med,
+                                  const PPt *__restrict__ high, int m_high, double thresh,
+                                  PnpDevResult *res) {
   __shared__ int woff[16];
   __shared__ int base_s;
   const bool have = res->best_index >= 0;
@@ -1182,6 +1181,17 @@ __global__ __launch_bounds__(1024) void k_pnp_inliers(const PPt *__restrict__ me
   ordered_compact(
       m_high, [&](int i) { return pnp_inlier_ref(P, high[i], thresh); }, have,
       res->inliers + m_med, &res->n_high, woff, &base_s);
+}
+
+// The winner and its consensus sets in one launch (one workgroup): k_pnp_select's choice, then
+// the reference-order sets of pnp_inliers_block (one launch gap less per call).
+__global__ __launch_bounds__(1024) void k_pnp_select_inliers(
+    const int *__restrict__ counts, int H, const double *__restrict__ Psoa, int64_t ld,
+    PnpDevResult *res, const unsigned char *__restrict__ mirf, const PPt *__restrict__ med,
+    int m_med, const PPt *__restrict__ high, int m_high, double thresh) {
+  pnp_select_block(counts, H, Psoa, ld, res, mirf);
+  __syncthreads();  // the winner's record (thread 0's writes) before every thread reads it
+  pnp_inliers_block(med, m_med, high, m_high, thresh, res);
 }
 
 // rs_pnp_ransac_cv: the pose of hypothesis `best` (chosen on the host by the adaptive
@@ -1596,16 +1606,35 @@ extern "C" int rs_pnp_ransac(rs_ctx *c, const double *X_med, const double *y_med
   auto *dres = reinterpret_cast<rsd::PnpDevResult *>(take(b_res));
   auto *dmir = reinterpret_cast<unsigned char *>(take(b_mir));  // P3P poses' mirrored flags
   hipStream_t s = c->stream;
-  HIP_TRY(hipMemcpyAsync(dXm, X_med, sizeof(double) * 3 * m_med, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(dym, y_med, sizeof(double) * 3 * m_med, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(dXh, X_high, sizeof(double) * 3 * m_high, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(dyh, y_high, sizeof(double) * 3 * m_high, hipMemcpyHostToDevice, s));
-  if (mode == RS_SAMPLER_TUPLES)
-    HIP_TRY(hipMemcpyAsync(dtup, host_tuples, sizeof(int) * H * k, hipMemcpyHostToDevice, s));
+  // the inputs staged contiguously in pinned memory (the layout of the scratch buffers up to the
+  // tuples) and sent with one DMA copy; the call synchronises before returning, so the staging
+  // is free again for the next call.  The same set as med and high (ransac.py's usual call,
+  // D_med = D_high) is sent and packed once.
+  const bool same = X_med == X_high && y_med == y_high && m_med == m_high;
+  const size_t n_stage = 2 * b_in_m + 2 * b_in_h + b_pm + b_ph + b_tup;
+  if ((st = rs::ensure_pinned(c, n_stage))) return st;
+  char *hp = static_cast<char *>(c->pinned);
+  std::memcpy(hp, X_med, sizeof(double) * 3 * m_med);
+  std::memcpy(hp + b_in_m, y_med, sizeof(double) * 3 * m_med);
+  size_t up = 2 * b_in_m;
+  if (!same) {
+    std::memcpy(hp + 2 * b_in_m, X_high, sizeof(double) * 3 * m_high);
+    std::memcpy(hp + 2 * b_in_m + b_in_h, y_high, sizeof(double) * 3 * m_high);
+    up = 2 * b_in_m + 2 * b_in_h;
+  }
+  HIP_TRY(hipMemcpyAsync(dXm, hp, up, hipMemcpyHostToDevice, s));
+  if (mode == RS_SAMPLER_TUPLES) {
+    const size_t to = 2 * b_in_m + 2 * b_in_h + b_pm + b_ph;  // dtup's offset, as in scratch
+    std::memcpy(hp + to, host_tuples, sizeof(int) * H * k);
+    HIP_TRY(hipMemcpyAsync(dtup, hp + to, sizeof(int) * H * k, hipMemcpyHostToDevice, s));
+  }
   hipLaunchKernelGGL(rsd::k_pack_ppts, dim3((m_med + 255) / 256), dim3(256), 0, s, dXm, dym,
                      static_cast<int>(m_med), pm);
-  hipLaunchKernelGGL(rsd::k_pack_ppts, dim3((m_high + 255) / 256), dim3(256), 0, s, dXh, dyh,
-                     static_cast<int>(m_high), ph);
+  if (same)
+    ph = pm;
+  else
+    hipLaunchKernelGGL(rsd::k_pack_ppts, dim3((m_high + 255) / 256), dim3(256), 0, s, dXh, dyh,
+                       static_cast<int>(m_high), ph);
   HIP_TRY(hipMemsetAsync(dcnt, 0, sizeof(int) * Hm, s));
   const bool timed = c->pnp_timing != 0;
   if (timed) HIP_TRY(hipEventRecord(c->pnp_ev[0], s));
@@ -1631,11 +1660,10 @@ extern "C" int rs_pnp_ransac(rs_ctx *c, const double *X_med, const double *y_med
                      dcnt);
   HIP_TRY(hipGetLastError());
   if (timed) HIP_TRY(hipEventRecord(c->pnp_ev[2], s));
-  hipLaunchKernelGGL(rsd::k_pnp_select, dim3(1), dim3(1024), 0, s, dcnt, static_cast<int>(Hm), dP,
-                     ld, dres, k == 3 ? static_cast<const unsigned char *>(dmir) : nullptr);
-  HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(rsd::k_pnp_inliers, dim3(1), dim3(1024), 0, s, pm, static_cast<int>(m_med),
-                     ph, static_cast<int>(m_high), thresh, dres);
+  hipLaunchKernelGGL(rsd::k_pnp_select_inliers, dim3(1), dim3(1024), 0, s, dcnt,
+                     static_cast<int>(Hm), dP, ld, dres,
+                     k == 3 ? static_cast<const unsigned char *>(dmir) : nullptr, pm,
+                     static_cast<int>(m_med), ph, static_cast<int>(m_high), thresh);
   HIP_TRY(hipGetLastError());
   std::vector<char> host(sizeof(rsd::PnpDevResult) + sizeof(int64_t) * (m_med + m_high));
   HIP_TRY(hipMemcpyAsync(host.data(), dres, host.size(), hipMemcpyDeviceToHost, s));
