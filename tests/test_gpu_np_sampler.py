@@ -110,12 +110,17 @@ def test_gpu_stream_many_segments(knobs):
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
 
 
+@pytest.mark.parametrize("knob", [None, "RSAMD_NP_SYNC", "RSAMD_NP_RERUN_TEST"])
 @pytest.mark.parametrize("n,H,seed,out", [(2000, 100000, 0, 0.3), (257, 10000, 3, 0.3),
                                           (10240, 2000, 7, 0.3), (10000, 100000, 5, 0.6)])
-def test_plan_run_np_equals_host_tuple_run(ctx, n, H, seed, out):
+def test_plan_run_np_equals_host_tuple_run(ctx, monkeypatch, n, H, seed, out, knob):
     """rs_f8_plan_run_np (tuples parsed on the GPU into the run's buffer) = the same plan fed the
     host replay's tuples: winner, S_RANSAC, F bits and the advanced stream state.  C2 at full
-    size, and C5's pair (N = 10 000, 60 % outliers) with 1e5 of its 1e6 hypotheses."""
+    size, and C5's pair (N = 10 000, 60 % outliers) with 1e5 of its 1e6 hypotheses.  Default:
+    the run queued behind the parse before its outcome is read; RSAMD_NP_SYNC: the parse waited
+    for first; RSAMD_NP_RERUN_TEST: the queued run superseded as after a wrap-log overflow."""
+    if knob:
+        monkeypatch.setenv(knob, "1")
     from tsbb15_amd import synth
     p1, p2, _ = synth.two_view(n, out, seed=seed + 1)
     key, pos = _state(seed)

@@ -43,6 +43,9 @@ bool np_gpu_supported(int64_t n, int32_t k);  // within the GPU parse's populati
 // The numpy (py: CPython) stream's next `count` choice(n, k) tuples; rows [skip, skip + take)
 // (take < 0: to the end) are written to d_out (take * k int32); (key, pos) advance past all
 // `count`.  Synchronous on the context stream.
+int np_choice_enqueue(rs_ctx *c, const uint32_t *key, int32_t pos, int64_t n, int32_t k,
+                      int64_t count, int32_t *d_out, bool *queued);
+int np_choice_finish(rs_ctx *c, uint32_t *key, int32_t *pos, bool *rerun);
 int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t k,
                      int64_t count, int32_t *d_out, bool py = false, int64_t skip = 0,
                      int64_t take = -1);

@@ -70,8 +70,14 @@ __device__ __forceinline__ void solve_one(const SolveArgs &a, int h) {
   if (mode == RSD_SAMPLER_PHILOX) {
     floyd_sample<8>(seed, hyp_offset + static_cast<uint64_t>(h), n, idx);
   } else {
+    // parity mode may queue this solve behind a parse it has not yet checked
+    // (rs_f8_plan_run_np_slice): an index outside [0, n) reads point 0, never past the points;
+    // such a run is discarded and run again
 #pragma unroll
-    for (int k = 0; k < 8; ++k) idx[k] = tuples[static_cast<int64_t>(h) * 8 + k];
+    for (int k = 0; k < 8; ++k) {
+      const int t = tuples[static_cast<int64_t>(h) * 8 + k];
+      idx[k] = static_cast<unsigned>(t) < static_cast<unsigned>(n) ? t : 0;
+    }
   }
   double xl[8], yl[8], xr[8], yr[8];
 #pragma unroll

@@ -99,6 +99,7 @@ struct rs_f8_plan {
   bool overlap = kOverlapDefault != 0;
   hipStream_t ss = nullptr, ts = nullptr;
   hipEvent_t ev_solve[kBufs] = {}, ev_count[kBufs] = {}, ev_tail[kBufs] = {};
+  hipEvent_t ev_np = nullptr;  // parity mode: the parse queued before the solve (overlap)
   rsd::TailArgs tail{};              // ... its arguments
   // counting kernel: fp32 point-pair kernel with the float64 guard re-test (default), or the
   // plain float64 kernel (rs_f8_plan_set_count_precision; both give identical counts)
@@ -157,6 +158,7 @@ static void plan_free(rs_f8_plan *p) {
     if (p->ev_count[k]) (void)hipEventDestroy(p->ev_count[k]);
     if (p->ev_tail[k]) (void)hipEventDestroy(p->ev_tail[k]);
   }
+  if (p->ev_np) (void)hipEventDestroy(p->ev_np);
   if (p->ss) (void)hipStreamDestroy(p->ss);
   if (p->ts) (void)hipStreamDestroy(p->ts);
   for (auto &h : p->h_slot)
@@ -505,8 +507,29 @@ extern "C" int rs_f8_plan_run_np_slice(rs_f8_plan *p, int64_t H, int64_t start, 
   if (count > p->max_hyp) return fail(RS_EINVAL, "hypothesis count out of plan range");
   int st;
   if (rs::np_gpu_supported(p->n, 8) && std::getenv("RSAMD_NP_HOST") == nullptr) {
-    RunBufs &b = p->buf[p->runs % rs_f8_plan::kBufs];
     if (p->overlap) HIP_TRY(hipEventSynchronize(p->ev_solve[p->runs % rs_f8_plan::kBufs]));
+    if (start == 0 && count == H && std::getenv("RSAMD_NP_SYNC") == nullptr) {
+      // the whole draw in one segment: the run is queued behind the parse before the host
+      // waits for the parse's outcome (no host gap between them); should the parse ask to be
+      // drawn again (a wrap-log overflow), that run is superseded by the synchronous path below
+      bool queued = false;
+      RunBufs &b = p->buf[p->runs % rs_f8_plan::kBufs];
+      if ((st = rs::np_choice_enqueue(p->ctx, key, *pos, p->n, 8, H, b.d_tuples, &queued)))
+        return st;
+      if (queued) {
+        if (p->overlap) {  // the solve's stream reads the tuples after the parse
+          if (!p->ev_np) HIP_TRY(hipEventCreateWithFlags(&p->ev_np, hipEventDisableTiming));
+          HIP_TRY(hipEventRecord(p->ev_np, p->ctx->stream));
+          HIP_TRY(hipStreamWaitEvent(p->ss, p->ev_np, 0));
+        }
+        const int run_st = plan_run(p, count, RS_SAMPLER_TUPLES, 0, 0, nullptr, thresh, true);
+        bool rerun = false;
+        if ((st = rs::np_choice_finish(p->ctx, key, pos, &rerun))) return st;
+        if (run_st || !rerun) return run_st;
+        if (p->overlap) HIP_TRY(hipEventSynchronize(p->ev_solve[p->runs % rs_f8_plan::kBufs]));
+      }
+    }
+    RunBufs &b = p->buf[p->runs % rs_f8_plan::kBufs];
     if ((st = rs::np_choice_device(p->ctx, key, pos, p->n, 8, H, b.d_tuples, false, start, count)))
       return st;
     return plan_run(p, count, RS_SAMPLER_TUPLES, 0, static_cast<uint64_t>(start), nullptr, thresh,

@@ -2675,6 +2675,11 @@ struct rs_np_shard {
   // stream, two around the second stream pass on s2); null unless timing was ever enabled
   bool timed = false;
   hipEvent_t tev[kNpMarks + 2] = {};
+  // world 1: the segment's outcome copied to pinned memory behind ev_res, so the caller can
+  // queue the evaluation before waiting for it (np_choice_enqueue / np_choice_finish)
+  NpResult *h_res = nullptr;
+  hipEvent_t ev_res = nullptr;
+  int64_t pending = 0;  // hypotheses of an enqueued, not yet finished segment
   int64_t cap_win = 0, cap_chain = 0, cap_stream = 0, cap_fin = 0, cap_fin_all = 0, cap_fm = 0,
           cap_fm_all = 0, cap_ev = 0, cap_evn = 0, cap_ent = 0, cap_vcnt = 0, cap_off = 0,
           cap_tpos = 0, cap_row = 0, cap_starts = 0, cap_pause = 0, cap_io = 0;
@@ -2695,6 +2700,8 @@ void shard_free(rs_np_shard *w) {
   if (w->ev_b) (void)hipEventDestroy(w->ev_b);
   for (hipEvent_t e : w->tev)
     if (e) (void)hipEventDestroy(e);
+  if (w->ev_res) (void)hipEventDestroy(w->ev_res);
+  if (w->h_res) (void)hipHostFree(w->h_res);
   // (w->s2 is the context's aux_stream: rs_ctx_destroy destroys it)
 }
 
@@ -2944,6 +2951,8 @@ int shard_init(rs_np_shard &w) {
     w.s2 = w.ctx->aux_stream;  // the context's own (rs_ctx_create)
     HIP_TRY(hipEventCreateWithFlags(&w.ev_a, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&w.ev_b, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&w.ev_res, hipEventDisableTiming));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&w.h_res), sizeof(NpResult)));
   }
   return RS_OK;
 }
@@ -3268,64 +3277,62 @@ int shard_tuples(rs_np_shard &w, int64_t base, int64_t hi, int64_t next_start, i
   return RS_OK;
 }
 
-// World 1, all on the device (np_choice_device): one segment of at most `count` hypotheses
-// from (key, pos) -- the same steps with the compose read straight from the device maps and
-// one host synchronisation; its hypotheses [lo, hi) go to d_out as k-tuples; *got and
-// (key, pos) advance.
-int shard_run_local(rs_np_shard &w, uint32_t *key, int32_t *pos, int64_t count, int64_t lo,
-                    int64_t hi, int32_t *d_out, int64_t *got_out) {
-  int st;
+// One world-1 segment after its stream: parse, compose, starts, tuples [lo, hi), the outcome
+// (delivered count, draws used, errors, the stream block holding the next word) copied to the
+// pinned w.h_res behind w.ev_res.  Nothing is waited for.
+int shard_local_enqueue(rs_np_shard &w, int32_t pos, int64_t lo, int64_t hi, int32_t *d_out) {
   hipStream_t s = w.ctx->stream;
-  if ((st = shard_init(w))) return st;
-  w.timed = w.ctx->np_timing != 0;
-  if (w.timed && !w.tev[0])
-    for (auto &e : w.tev) HIP_TRY(hipEventCreate(&e));
-  if ((st = tmark(w, 0, s)) || (st = shard_layout(w, *pos, count)) || (st = shard_stream(w, key)))
-    return st;
-  NpResult res;
-  for (;;) {
-    if ((st = shard_enqueue_parse(w))) return st;
-    k_np_compose<<<1, 1024, 0, s>>>(w.d_fin, w.d_fin_m, w.n1, static_cast<int>(w.Cr), w.d_ent,
-                                    nullptr);
+  int st;
+  if ((st = shard_enqueue_parse(w))) return st;
+  k_np_compose<<<1, 1024, 0, s>>>(w.d_fin, w.d_fin_m, w.n1, static_cast<int>(w.Cr), w.d_ent,
+                                  nullptr);
+  HIP_TRY(hipGetLastError());
+  if ((st = tmark(w, 5, s))) return st;
+  if ((st = shard_enqueue_starts(w, w.count, &w.d_res->got)) || (st = tmark(w, 6, s))) return st;
+  if (hi > lo) {  // waves beyond the delivered count exit
+    shard_launch_tuples(w, lo, hi, &w.d_res->got, d_out);
     HIP_TRY(hipGetLastError());
-    if ((st = tmark(w, 5, s))) return st;
-    if ((st = shard_enqueue_starts(w, w.count, &w.d_res->got)) || (st = tmark(w, 6, s))) return st;
-    if (hi > lo) {  // waves beyond the delivered count exit
-      shard_launch_tuples(w, lo, hi, &w.d_res->got, d_out);
-      HIP_TRY(hipGetLastError());
-    }
-    if ((st = tmark(w, 7, s))) return st;
-    // delivered count, draws used, errors and the stream block holding the next word
-    k_np_result<<<1, 64, 0, s>>>(w.d_stream, w.d_starts, *pos, w.d_err, w.d_res);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(&res, w.d_res, sizeof(res), hipMemcpyDeviceToHost, s));
-    if ((st = tmark(w, 8, s))) return st;
-    HIP_TRY(hipStreamSynchronize(s));
-    if (w.timed) {  // this segment's steps, summed over the call's segments (rs_np_timing)
-      float ms = 0.f;
-      for (int k = 0; k + 1 < kNpMarks; ++k) {
-        HIP_TRY(hipEventElapsedTime(&ms, w.tev[k], w.tev[k + 1]));
-        w.ctx->np_ms[k] += ms;
-      }
-      HIP_TRY(hipEventElapsedTime(&ms, w.tev[kNpMarks], w.tev[kNpMarks + 1]));
-      w.ctx->np_ms[kNpMarks - 1] += ms;
-      HIP_TRY(hipEventElapsedTime(&ms, w.tev[0], w.tev[kNpMarks - 1]));
-      w.ctx->np_ms[kNpMarks] += ms;
-      // algorithmic HBM bytes of the segment: stream words written once, every parsed draw
-      // read once by the chunk parse (entry + track), every hypothesis's draws read once by
-      // the tuple kernel (words up to the last start)
-      w.ctx->np_bytes[0] += 4.0 * static_cast<double>(w.Lb) * kN;
-      w.ctx->np_bytes[1] += 4.0 * static_cast<double>(w.Cr * w.Wc);
-      w.ctx->np_bytes[2] += 4.0 * static_cast<double>(res.used);
-      w.ctx->np_segments += 1;
-    }
-    if (res.err & 1) {  // wrap log overflow: a larger log, the same chunks again
-      if (w.ecap >= w.Wc + 2 * w.n1) return rs::fail(RS_EDEVICE, "np sampler: wrap log overflow");
-      ++w.ecap_shift;
-      continue;
-    }
-    break;
   }
+  if ((st = tmark(w, 7, s))) return st;
+  k_np_result<<<1, 64, 0, s>>>(w.d_stream, w.d_starts, pos, w.d_err, w.d_res);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(w.h_res, w.d_res, sizeof(NpResult), hipMemcpyDeviceToHost, s));
+  if ((st = tmark(w, 8, s))) return st;
+  HIP_TRY(hipEventRecord(w.ev_res, s));
+  return RS_OK;
+}
+
+// Wait for the enqueued segment's outcome; its step times (rs_np_timing); *overflow: the wrap
+// log overflowed (the same chunks must be parsed again with a larger log).
+int shard_local_wait(rs_np_shard &w, bool *overflow) {
+  HIP_TRY(hipEventSynchronize(w.ev_res));
+  const NpResult &res = *w.h_res;
+  if (w.timed) {  // this segment's steps, summed over the call's segments (rs_np_timing)
+    float ms = 0.f;
+    for (int k = 0; k + 1 < kNpMarks; ++k) {
+      HIP_TRY(hipEventElapsedTime(&ms, w.tev[k], w.tev[k + 1]));
+      w.ctx->np_ms[k] += ms;
+    }
+    HIP_TRY(hipEventElapsedTime(&ms, w.tev[kNpMarks], w.tev[kNpMarks + 1]));
+    w.ctx->np_ms[kNpMarks - 1] += ms;
+    HIP_TRY(hipEventElapsedTime(&ms, w.tev[0], w.tev[kNpMarks - 1]));
+    w.ctx->np_ms[kNpMarks] += ms;
+    // algorithmic HBM bytes of the segment: stream words written once, every parsed draw
+    // read once by the chunk parse (entry + track), every hypothesis's draws read once by
+    // the tuple kernel (words up to the last start)
+    w.ctx->np_bytes[0] += 4.0 * static_cast<double>(w.Lb) * kN;
+    w.ctx->np_bytes[1] += 4.0 * static_cast<double>(w.Cr * w.Wc);
+    w.ctx->np_bytes[2] += 4.0 * static_cast<double>(res.used);
+    w.ctx->np_segments += 1;
+  }
+  *overflow = (res.err & 1) != 0;
+  if (*overflow && w.ecap >= w.Wc + 2 * w.n1) return rs::fail(RS_EDEVICE, "np sampler: wrap log overflow");
+  return RS_OK;
+}
+
+// The finished segment's outcome: errors, delivered count, the advanced (key, pos).
+int shard_local_outcome(rs_np_shard &w, uint32_t *key, int32_t *pos, int64_t *got_out) {
+  const NpResult &res = *w.h_res;
   if (res.err & 2) return rs::fail(RS_EDEVICE, "np sampler: hypothesis parse mismatch");
   if (res.err) return rs::fail(RS_EDEVICE, "np sampler: corrupt chunk hand-over or start list");
   if (res.got < 1) return rs::fail(RS_EDEVICE, "np sampler: segment holds no complete hypothesis");
@@ -3339,6 +3346,64 @@ int shard_run_local(rs_np_shard &w, uint32_t *key, int32_t *pos, int64_t count, 
     *pos = static_cast<int32_t>(W);
   }
   *got_out = res.got;
+  return RS_OK;
+}
+
+// the segment's set-up through its stream (timing marks, layout, jump + stream launches)
+int shard_local_begin(rs_np_shard &w, const uint32_t *key, int32_t pos, int64_t count) {
+  int st;
+  if ((st = shard_init(w))) return st;
+  w.timed = w.ctx->np_timing != 0;
+  if (w.timed && !w.tev[0])
+    for (auto &e : w.tev) HIP_TRY(hipEventCreate(&e));
+  if ((st = tmark(w, 0, w.ctx->stream)) || (st = shard_layout(w, pos, count)) ||
+      (st = shard_stream(w, key)))
+    return st;
+  return RS_OK;
+}
+
+// World 1, all on the device (np_choice_device): one segment of at most `count` hypotheses
+// from (key, pos) -- the same steps with the compose read straight from the device maps and
+// one host synchronisation; its hypotheses [lo, hi) go to d_out as k-tuples; *got and
+// (key, pos) advance.
+int shard_run_local(rs_np_shard &w, uint32_t *key, int32_t *pos, int64_t count, int64_t lo,
+                    int64_t hi, int32_t *d_out, int64_t *got_out) {
+  int st;
+  if ((st = shard_local_begin(w, key, *pos, count))) return st;
+  for (;;) {
+    bool overflow = false;
+    if ((st = shard_local_enqueue(w, *pos, lo, hi, d_out)) || (st = shard_local_wait(w, &overflow)))
+      return st;
+    if (!overflow) break;
+    ++w.ecap_shift;  // wrap log overflow: a larger log, the same chunks again
+  }
+  return shard_local_outcome(w, key, pos, got_out);
+}
+
+// The context's world-1 session for (n, k, py), created on first use.
+int local_session(rs_ctx *c, int64_t n, int32_t k, bool py, rs_np_shard **out) {
+  if (c->np_timing) {  // rs_np_timing reports this call's steps
+    for (double &v : c->np_ms) v = 0.0;
+    for (double &v : c->np_bytes) v = 0.0;
+    c->np_segments = 0;
+  }
+  rs_np_shard *w = c->np_shard;
+  if (w && (w->n != n || w->k != k || w->py != py)) {
+    // another population (the drop-in's next pair): the session keeps its device buffers,
+    // which only grow, and lays the next segment out for the new n (shard_layout)
+    w->n = n;
+    w->n1 = static_cast<int>(n - 1);
+    w->k = k;
+    w->py = py;
+    w->state = 0;
+  }
+  if (!w) {
+    int st;
+    if ((st = rs_np_shard_create(c, n, k, 1, 0, py ? 1 : 0, &w))) return st;
+    c->np_shard = w;
+  }
+  w->pending = 0;
+  *out = w;
   return RS_OK;
 }
 
@@ -3382,26 +3447,9 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
     HIP_TRY(hipStreamSynchronize(c->stream));
     return RS_OK;
   }
-  if (c->np_timing) {  // rs_np_timing reports this call's steps
-    for (double &v : c->np_ms) v = 0.0;
-    for (double &v : c->np_bytes) v = 0.0;
-    c->np_segments = 0;
-  }
-  rs_np_shard *w = c->np_shard;
-  if (w && (w->n != n || w->k != k || w->py != py)) {
-    // another population (the drop-in's next pair): the session keeps its device buffers,
-    // which only grow, and lays the next segment out for the new n (shard_layout)
-    w->n = n;
-    w->n1 = static_cast<int>(n - 1);
-    w->k = k;
-    w->py = py;
-    w->state = 0;
-  }
+  rs_np_shard *w = nullptr;
   int st;
-  if (!w) {
-    if ((st = rs_np_shard_create(c, n, k, 1, 0, py ? 1 : 0, &w))) return st;
-    c->np_shard = w;
-  }
+  if ((st = local_session(c, n, k, py, &w))) return st;
   int64_t done = 0;
   while (done < count) {
     // this segment's hypotheses [done, done + got) against the slice [skip, skip + take)
@@ -3413,6 +3461,61 @@ int np_choice_device(rs_ctx *c, uint32_t *key, int32_t *pos, int64_t n, int32_t 
       return st;
     done += got;
   }
+  return RS_OK;
+}
+
+// np_choice_device's one-segment case split in two, so that the caller can queue work that
+// reads d_out before waiting: np_choice_enqueue queues all of one segment's steps when the
+// whole `count` fits one segment (*queued; otherwise nothing is queued and the caller takes
+// np_choice_device); np_choice_finish waits and advances (key, pos).  *rerun: the segment
+// must be drawn again (a wrap-log overflow, or fewer hypotheses than asked) -- (key, pos)
+// are unchanged and the caller repeats the call with np_choice_device, which handles both.
+int np_choice_enqueue(rs_ctx *c, const uint32_t *key, int32_t pos, int64_t n, int32_t k,
+                      int64_t count, int32_t *d_out, bool *queued) {
+  *queued = false;
+  if (!np_gpu_supported(n, k) || n <= 1 || count < 1 || pos < 0 || pos > kN) return RS_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  rs_np_shard *w = nullptr;
+  int st;
+  if ((st = local_session(c, n, k, false, &w))) return st;
+  if ((st = shard_init(*w))) return st;
+  w->timed = c->np_timing != 0;
+  if (w->timed && !w->tev[0])
+    for (auto &e : w->tev) HIP_TRY(hipEventCreate(&e));
+  if ((st = tmark(*w, 0, c->stream)) || (st = shard_layout(*w, pos, count))) return st;
+  if (w->count < count) return RS_OK;  // more than one segment: nothing queued yet
+  if ((st = shard_stream(*w, key)) || (st = shard_local_enqueue(*w, pos, 0, count, d_out)))
+    return st;
+  w->pending = count;
+  *queued = true;
+  return RS_OK;
+}
+
+int np_choice_finish(rs_ctx *c, uint32_t *key, int32_t *pos, bool *rerun) {
+  *rerun = false;
+  rs_np_shard *w = c->np_shard;
+  if (!w || w->pending < 1) return fail(RS_EINVAL, "np sampler: no segment enqueued");
+  const int64_t want = w->pending;
+  w->pending = 0;
+  bool overflow = false;
+  int st;
+  if ((st = shard_local_wait(*w, &overflow))) return st;
+  if (overflow) {
+    ++w->ecap_shift;  // the repeat gets the larger log
+    *rerun = true;
+    return RS_OK;
+  }
+  uint32_t k2[kN];
+  int32_t p2 = *pos;
+  std::memcpy(k2, key, sizeof(k2));
+  int64_t got = 0;
+  if ((st = shard_local_outcome(*w, k2, &p2, &got))) return st;
+  if (got != want || std::getenv("RSAMD_NP_RERUN_TEST")) {  // the test hook takes this branch
+    *rerun = true;
+    return RS_OK;
+  }
+  std::memcpy(key, k2, sizeof(k2));
+  *pos = p2;
   return RS_OK;
 }
 }  // namespace rs
