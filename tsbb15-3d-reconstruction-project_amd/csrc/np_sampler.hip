@@ -65,6 +65,7 @@ constexpr uint32_t kMatA = 0x9908b0dfu;
 constexpr int kDeg = 19937;
 constexpr int kPrefix = kDeg + kN - 1;       // words of a window's sequence a jump reads
 constexpr int kPrefixAlloc = kN * ((kPrefix + kN - 1) / kN);  // generated in whole blocks
+constexpr int kPhases = (kDeg + kN - 1) / kN;  // blocks holding a jump polynomial's bits (32)
 constexpr int kJB = 1024;                    // stream blocks per generator (unless chunk-aligned)
 constexpr int kLevels = 16;                  // jump levels: windows up to 2^16 generators apart
 constexpr int kW = 1 << 24;                  // longest automatic parse chunk (draws)
@@ -210,8 +211,8 @@ __global__ __launch_bounds__(kJumpThreads) void k_mt_jump(uint32_t *__restrict__
   const int q0 = ne + static_cast<int>(static_cast<int64_t>(no) * q / S);
   const int q1 = ne + static_cast<int>(static_cast<int64_t>(no) * (q + 1) / S);
   if (e0 >= e1 && q0 >= q1) return;
-  // words y_0 .. y_{hi-1} are read
-  const int hi = max(e1 > e0 ? bits[e1 - 1] : 0, q1 > q0 ? bits[q1 - 1] : 0) + kN;
+  // words y_0 .. y_{hi-1} are read (a bit i is stored as 8 (i >> 1), its pair's byte offset)
+  const int hi = 2 * (max(e1 > e0 ? bits[e1 - 1] : 0, q1 > q0 ? bits[q1 - 1] : 0) >> 3) + 2 + kN;
   const int tid = threadIdx.x;
   const int grp = __builtin_amdgcn_readfirstlane(tid / kJumpGroupThreads), lt = tid - grp * kJumpGroupThreads;
   for (int t = tid; t < kN; t += kJumpThreads) y[t] = win[static_cast<size_t>(g) * kN + t];
@@ -237,25 +238,43 @@ __global__ __launch_bounds__(kJumpThreads) void k_mt_jump(uint32_t *__restrict__
   // bit reads y_{i+624}, y_{i+625}: words of the last generated block)
   const bool act = lt <= kN / 2;
   uint32_t a0 = 0, a1 = 0, c0 = 0, c1 = 0;  // even bits: words 2l, 2l+1; odd: 2l-1, 2l
-  const uint2 *y2 = reinterpret_cast<const uint2 *>(y);
-  // the group's share of a sorted run of bits of one parity, 16 indices per scalar load batch
+  const char *yl = reinterpret_cast<const char *>(y) + 8 * lt;
+  // the group's share of a sorted run of bits of one parity, 16 byte offsets per scalar load
+  // batch, the next batch's load issued before this batch's LDS reads (its latency was exposed
+  // once per batch), the offsets stored ready to add (no scalar shift / mask per bit)
   auto run = [&](int r0, int r1, uint32_t &x0, uint32_t &x1) {
     const int per = (r1 - r0 + kJumpGroups - 1) / kJumpGroups;
     const int b0 = r0 + grp * per, b1 = min(r1, b0 + per);
     int b = b0;
-    for (; b + 16 <= b1; b += 16) {
+    if (b + 16 <= b1) {
       int ix[16];
 #pragma unroll
       for (int k = 0; k < 16; ++k) ix[k] = bits[b + k];
+      // the first batch waited for here, so that inside the loop only the prefetch is pending
+      // when the addresses are formed (scalar loads return out of order: the wait before the
+      // XORs then covers the prefetch and the LDS reads together)
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+      for (; b + 16 <= b1; b += 16) {
+        int nx[16];
+        const bool more = b + 32 <= b1;
+        if (more) {
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const uint2 v = y2[(ix[k] >> 1) + lt];  // pair at i - (i & 1) + 2l
-        x0 ^= v.x;
-        x1 ^= v.y;
+          for (int k = 0; k < 16; ++k) nx[k] = bits[b + 16 + k];
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const uint2 v = *reinterpret_cast<const uint2 *>(yl + ix[k]);  // pair at i - (i & 1) + 2l
+          x0 ^= v.x;
+          x1 ^= v.y;
+        }
+        if (more) {
+#pragma unroll
+          for (int k = 0; k < 16; ++k) ix[k] = nx[k];
+        }
       }
     }
     for (; b < b1; ++b) {
-      const uint2 v = y2[(bits[b] >> 1) + lt];
+      const uint2 v = *reinterpret_cast<const uint2 *>(yl + bits[b]);
       x0 ^= v.x;
       x1 ^= v.y;
     }
@@ -272,6 +291,127 @@ __global__ __launch_bounds__(kJumpThreads) void k_mt_jump(uint32_t *__restrict__
   }
   __syncthreads();
   // combine: word t = XOR over groups of pe[.][t] ^ po[.][t] (po[.][t] for odd t only)
+  uint32_t *out = win + static_cast<size_t>(dst) * kN;
+  for (int t = tid; t < kN; t += kJumpThreads) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < kJumpGroups; ++k) v ^= pe[k][t] ^ ((t & 1) ? po[k][t] : 0u);
+    if (S == 1) out[t] = v;
+    else atomicXor(out + t, v);
+  }
+}
+
+// The same jump with the window's sequence in a ring of four blocks instead of a 20 561-word
+// prefix (RSAMD_JUMP_PREFIX=1 selects the prefix form): phase p generates block p + 3 and XORs
+// the bits in block p (their reads span blocks p .. p + 2), one barrier per phase as before.
+// 27.5 KB of LDS instead of 97 KB, so two workgroups share a CU.  Reads run linearly past the
+// ring's end into a mirror of slot 0 (and slot 1's first two words): block b sits at slot b % 4,
+// and the bits of phase p read at byte offset - (p / 4) 4 kN 4.
+#ifndef RSAMD_JUMP_XOR3
+#define RSAMD_JUMP_XOR3 1  // the ring form's XORs in pairs by v_bitop3 (A/B builds: 0; C5 jump 6.5 -> 6.1 ms)
+#endif
+constexpr int kRing = 4 * kN;
+constexpr int kMirror = kN + 2;
+struct JumpIdx16 {
+  int v[16];
+};
+constexpr int kZeroPad = kN + 2;  // zeros the padding entries read (words 2 l, 2 l + 1 <= kN + 1)
+__device__ __forceinline__ void jump_gen_block(uint32_t *y, int b, int tid) {
+  // block b + 1 from block b (the three dependent runs on one thread, as in the prefix form)
+  if (tid < 227) {
+    const uint32_t *o = y + kN * (b & 3);
+    const int sn = (b + 1) & 3;
+    uint32_t *n = y + kN * sn;
+    const uint32_t n0 = o[tid + kM] ^ twist(o[tid], o[tid + 1]);
+    const uint32_t n1 = n0 ^ twist(o[tid + 227], o[tid + 228]);
+    uint32_t n2 = 0;
+    if (tid < 170) {
+      const uint32_t nx = tid + 455 < kN ? o[tid + 455] : (o[kM] ^ twist(o[0], o[1]));
+      n2 = n1 ^ twist(o[tid + 454], nx);
+    }
+    n[tid] = n0;
+    n[tid + 227] = n1;
+    if (tid < 170) n[tid + 454] = n2;
+    if (sn == 0) {  // the mirror of slot 0
+      y[kRing + tid] = n0;
+      y[kRing + tid + 227] = n1;
+      if (tid < 170) y[kRing + tid + 454] = n2;
+    } else if (sn == 1 && tid < 2) {
+      y[kRing + kN + tid] = n0;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kJumpThreads, 8) void k_mt_jump_slide(uint32_t *__restrict__ win,
+                                                                  int half, int G,
+                                                                  const int32_t *__restrict__ bits_base,
+                                                                  JumpSet js, int S) {
+  // the ring, its mirror, then zeros (the padding entries of a run read them)
+  __shared__ __attribute__((aligned(16))) uint32_t y[kRing + kMirror + kZeroPad];
+  __shared__ uint32_t pe[kJumpGroups][kN], po[kJumpGroups][kN];
+  const int per_m = half * S, mi = static_cast<int>(blockIdx.x) / per_m;
+  const int rem = static_cast<int>(blockIdx.x) - mi * per_m;
+  const int g = rem / S, q = rem % S, dst = g + (mi + 1) * half;
+  if (mi >= js.nm || dst >= G) return;
+  const int32_t *__restrict__ bits = bits_base + js.off[mi];
+  const int nbits = js.nb[mi];
+  const int32_t *__restrict__ tab = bits + nbits;     // run starts by (phase, parity)
+  const int32_t *__restrict__ pad = tab + 2 * kPhases + 1;  // the padded runs
+  // part q of S: phases [ph0, ph1) (every phase of a degree-19937 polynomial holds bits)
+  const int ph0 = kPhases * q / S, ph1 = kPhases * (q + 1) / S;
+  if (ph0 >= ph1) return;
+  const int tid = threadIdx.x;
+  const int grp = __builtin_amdgcn_readfirstlane(tid / kJumpGroupThreads), lt = tid - grp * kJumpGroupThreads;
+  for (int t = tid; t < kN; t += kJumpThreads) {
+    const uint32_t v = win[static_cast<size_t>(g) * kN + t];
+    y[t] = v;
+    y[kRing + t] = v;
+  }
+  for (int t = tid; t < kZeroPad; t += kJumpThreads) y[kRing + kMirror + t] = 0u;
+  __syncthreads();
+  jump_gen_block(y, 0, tid);
+  __syncthreads();
+  jump_gen_block(y, 1, tid);
+  __syncthreads();
+  const bool act = lt <= kN / 2;
+  uint32_t a0 = 0, a1 = 0, c0 = 0, c1 = 0;  // even bits: words 2l, 2l+1; odd: 2l-1, 2l
+  // a padded run in full batches of 16 (batch j to group j % 3), one 64-byte scalar load each,
+  // the XORs in pairs
+  auto run = [&](int r0, int r1, const char *yl, uint32_t &x0, uint32_t &x1) {
+#pragma clang loop vectorize(disable) interleave(disable)
+    for (int b = r0 + 16 * grp; b < r1; b += 16 * kJumpGroups) {
+      const JumpIdx16 t = *reinterpret_cast<const JumpIdx16 *>(pad + b);
+#pragma unroll
+      for (int k = 0; k < 16; k += 2) {
+        const uint2 u = *reinterpret_cast<const uint2 *>(yl + t.v[k]);
+        const uint2 v = *reinterpret_cast<const uint2 *>(yl + t.v[k + 1]);
+#if RSAMD_JUMP_XOR3
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(x0) : "v"(x0), "v"(u.x), "v"(v.x));
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(x1) : "v"(x1), "v"(u.y), "v"(v.y));
+#else
+        x0 ^= u.x ^ v.x;
+        x1 ^= u.y ^ v.y;
+#endif
+      }
+    }
+  };
+  for (int p = 0; p < ph1; ++p) {
+    if (p + 3 <= ph1 + 1) jump_gen_block(y, p + 2, tid);  // block p + 3 (the last one read: ph1 + 1)
+    if (p >= ph0 && act) {
+      const char *yl = reinterpret_cast<const char *>(y) + 8 * lt - (p >> 2) * (4 * kRing);
+      const int r0 = tab[2 * p], r1 = tab[2 * p + 1], r2 = tab[2 * p + 2];
+      run(r0, r1, yl, a0, a1);
+      run(r1, r2, yl, c0, c1);
+    }
+    __syncthreads();
+  }
+  if (act) {
+    const int w = 2 * lt;
+    if (w < kN) pe[grp][w] = a0 ^ c1;
+    if (w + 1 < kN) pe[grp][w + 1] = a1;
+    if (w >= 1 && w - 1 < kN) po[grp][w - 1] = c0;
+  }
+  __syncthreads();
   uint32_t *out = win + static_cast<size_t>(dst) * kN;
   for (int t = tid; t < kN; t += kJumpThreads) {
     uint32_t v = 0;
@@ -2403,11 +2543,36 @@ struct JumpBits {
     off.push_back(static_cast<int>(all.size()));
     const size_t n0 = all.size();
     for (int par = 0; par < 2; ++par) {
-      for (int i = par; i < kDeg; i += 2)
-        if ((p[static_cast<size_t>(i) >> 6] >> (i & 63)) & 1u) all.push_back(i);
+      for (int i = par; i < kDeg; i += 2)  // as the LDS byte offset of its aligned word pair
+        if ((p[static_cast<size_t>(i) >> 6] >> (i & 63)) & 1u) all.push_back(8 * (i >> 1));
       if (par == 0) ne.push_back(static_cast<int>(all.size() - n0));
     }
-    n.push_back(static_cast<int>(all.size() - n0));
+    const int nb = static_cast<int>(all.size() - n0), nev = ne.back();
+    n.push_back(nb);
+    // k_mt_jump_slide's section after the slice: 2 kPhases + 1 starts, then the bits again by
+    // (phase, parity) -- phase p, even; phase p, odd; phase p + 1, even ... -- each run padded to
+    // a multiple of 16 with the phase's zero offset (its reads land on zeros: an XOR of 0), so
+    // every batch of 16 is full.  Bit i is in phase i / kN <=> 8 (i >> 1) / (4 kN) (kN even).
+    const size_t tab = all.size();
+    all.resize(tab + 2 * kPhases + 1);
+    const int pad0 = static_cast<int>(all.size());
+    int ke = 0, ko = nev;
+    for (int ph = 0; ph < kPhases; ++ph) {
+      const int32_t zoff = 4 * (kRing + kMirror) + (ph >> 2) * (4 * kRing);
+      for (int par = 0; par < 2; ++par) {
+        all[tab + static_cast<size_t>(2 * ph + par)] = static_cast<int32_t>(all.size()) - pad0;
+        int &k = par ? ko : ke;
+        const int end = par ? nb : nev;
+        int cnt = 0;
+        while (k < end && all[n0 + static_cast<size_t>(k)] < 4 * (ph + 1) * kN) {
+          all.push_back(all[n0 + static_cast<size_t>(k)]);
+          ++k;
+          ++cnt;
+        }
+        for (; cnt % 16; ++cnt) all.push_back(zoff);
+      }
+    }
+    all[tab + 2 * kPhases] = static_cast<int32_t>(all.size()) - pad0;
   }
 };
 
@@ -2839,6 +3004,27 @@ int shard_layout(rs_np_shard &w, int32_t pos, int64_t count) {
   return RS_OK;
 }
 
+// the ring form of the jump (k_mt_jump_slide) unless RSAMD_JUMP_PREFIX is set (A/B: the
+// prefix form, one workgroup per CU)
+#ifndef RSAMD_JUMP_SLIDE_WG
+#define RSAMD_JUMP_SLIDE_WG 2  // ring-form jump parts per CU a level is sized for (A/B builds)
+#endif
+constexpr int kJumpSlideWg = RSAMD_JUMP_SLIDE_WG;
+bool jump_slide() {
+  static const bool v = std::getenv("RSAMD_JUMP_PREFIX") == nullptr;
+  return v;
+}
+// (levels of fewer jumps than this keep the prefix form: one round either way, and the ring
+// form's parts split by phases -- C2 level 1, 7 jumps: 16 us prefix, 22 us ring)
+constexpr int kJumpSlideMin = 32;
+void launch_jump(bool ring, unsigned grid, uint32_t *win, int half, int G, const int32_t *bits,
+                 const JumpSet &js, int S, hipStream_t s) {
+  if (ring)
+    k_mt_jump_slide<<<grid, kJumpThreads, 0, s>>>(win, half, G, bits, js, S);
+  else
+    k_mt_jump<<<grid, kJumpThreads, sizeof(uint32_t) * kPrefixAlloc, s>>>(win, half, G, bits, js, S);
+}
+
 // windows of local generators 0 .. G-1 (global g0 ..) from the stream whose block 0 is key
 int shard_windows(rs_np_shard &w, const uint32_t *key, hipStream_t s) {
   int st;
@@ -2874,8 +3060,7 @@ int shard_windows(rs_np_shard &w, const uint32_t *key, hipStream_t s) {
       js.off[0] = w.bit_off[lv];
       js.nb[0] = w.bit_n[lv];
       js.ne[0] = w.bit_ne[lv];
-      k_mt_jump<<<64, kJumpThreads, sizeof(uint32_t) * kPrefixAlloc, s>>>(
-          w.d_chain + static_cast<size_t>(j) * kN, 1, 2, w.d_bits, js, 64);
+      launch_jump(false, 64, w.d_chain + static_cast<size_t>(j) * kN, 1, 2, w.d_bits, js, 64, s);
       HIP_TRY(hipGetLastError());
       ++j;
     }
@@ -2917,23 +3102,26 @@ int shard_windows(rs_np_shard &w, const uint32_t *key, hipStream_t s) {
         js.ne[m - 1] = w.rbit_ne[x];
         jumps += std::max<int64_t>(0, std::min<int64_t>(B, w.G - m * B));
       }
-      const int S = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(64, w.cus / std::max<int64_t>(1, jumps))));
-      k_mt_jump<<<static_cast<unsigned>(js.nm * B * S), kJumpThreads, sizeof(uint32_t) * kPrefixAlloc, s>>>(
-          w.d_win, static_cast<int>(B), static_cast<int>(w.G), w.d_rbits, js, S);
+      const bool ring = jump_slide() && jumps >= kJumpSlideMin;
+      const int64_t slots = static_cast<int64_t>(w.cus) * (ring ? kJumpSlideWg : 1);  // workgroups per round
+      const int S = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(64, slots / std::max<int64_t>(1, jumps))));
+      launch_jump(ring, static_cast<unsigned>(js.nm * B * S), w.d_win, static_cast<int>(B),
+                  static_cast<int>(w.G), w.d_rbits, js, S, s);
       HIP_TRY(hipGetLastError());
     }
     return RS_OK;
   }
   for (int half = 1, lv = 0; half < w.G; half *= 2, ++lv) {
     const int jumps = static_cast<int>(std::min<int64_t>(half, w.G - half));
-    const int S = std::max(1, std::min(64, w.cus / jumps));
+    const bool ring = jump_slide() && jumps >= kJumpSlideMin;
+    const int S = std::max(1, std::min(64, w.cus * (ring ? kJumpSlideWg : 1) / jumps));
     JumpSet js{};
     js.nm = 1;
     js.off[0] = w.bit_off[lv];
     js.nb[0] = w.bit_n[lv];
     js.ne[0] = w.bit_ne[lv];
-    k_mt_jump<<<half * S, kJumpThreads, sizeof(uint32_t) * kPrefixAlloc, s>>>(
-        w.d_win, half, static_cast<int>(w.G), w.d_bits, js, S);
+    launch_jump(ring, static_cast<unsigned>(half * S), w.d_win, half, static_cast<int>(w.G), w.d_bits,
+                js, S, s);
     HIP_TRY(hipGetLastError());
   }
   return RS_OK;
