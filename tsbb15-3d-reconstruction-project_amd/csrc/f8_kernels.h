@@ -68,6 +68,7 @@ struct TailArgs {
   double *cstd, *cnorm;
   F8DevResult *res;   // HBM result (header + S_RANSAC)
   F8DevResult *hres;  // pinned host header slot (device mapping), may be null
+  int *hinl;          // pinned host S_RANSAC (int32, device mapping), may be null
 };
 
 hipError_t launch_pack_points(const double *p1, const double *p2, int n, Pt *pts,

@@ -567,7 +567,7 @@ __device__ void replay_inliers(const Pt *__restrict__ pts, int n, const int *cou
                                const double *__restrict__ Fsoa, int64_t ld, int *status,
                                double thresh, F8DevResult *__restrict__ res,
                                F8DevResult *__restrict__ hres, const int *cfast,
-                               const int *spec, const int *spec_j);
+                               const int *spec, const int *spec_j, int *__restrict__ hinl);
 
 // Candidates + their reference-order statistics, one block per slice of hypotheses:
 // every hypothesis of the slice with fast count >= max(c* - slack, 1) is appended in index
@@ -740,7 +740,7 @@ __device__ void cand_stats_block(const TailArgs &a, int bid, int nblocks) {
   __syncthreads();
   if (!last_s) return;
   replay_inliers(pts, n, counts, nblocks, per_block, bc, cand, ccount, cstd, cnorm, Fsoa, ld,
-                 status_rw, thresh, a.res, a.hres, a.cfast, a.spec, a.spec_j);
+                 status_rw, thresh, a.res, a.hres, a.cfast, a.spec, a.spec_j, a.hinl);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -767,14 +767,14 @@ __device__ void replay_inliers(const Pt *__restrict__ pts, int n, const int *cou
                                const double *__restrict__ Fsoa, int64_t ld, int *status,
                                double thresh, F8DevResult *__restrict__ res,
                                F8DevResult *__restrict__ hres, const int *cfast,
-                               const int *spec, const int *spec_j) {
+                               const int *spec, const int *spec_j, int *__restrict__ hinl) {
   int *status_out = status;
   __shared__ int pref[kSelectBlocks + 1];
   __shared__ int woff[kTailThreads / 64];
   __shared__ int base_s;
   __shared__ double fsh[9];
   __shared__ int have_s;
-  __shared__ int spec_row_s;
+  __shared__ int spec_row_s, nin_s;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // exclusive prefix of the per-block candidate counts (nb <= 256): one wave per 64 blocks,
   // then the 4 wave totals
@@ -887,13 +887,20 @@ __device__ void replay_inliers(const Pt *__restrict__ pts, int n, const int *cou
       status_out[1] = nc;
       have_s = best >= 0 ? 1 : 0;
       spec_row_s = spec_ok ? brow : -1;
+      nin_s = spec_ok ? bcount : 0;
       base_s = 0;
     }
   }
   __syncthreads();
-  // the winner's S_RANSAC is its block's speculative list (the host copies that row:
-  // rs_f8_plan_result, inl_row); otherwise extract it here
-  if (spec_row_s >= 0) return;
+  // the winner's S_RANSAC is its block's speculative list (rs_f8_plan_result reads it from
+  // hinl, or copies the row: inl_row); otherwise extract it here
+  if (spec_row_s >= 0) {
+    if (hinl) {  // the list to the pinned host buffer (no copy pass after the run)
+      const int *row = spec + static_cast<int64_t>(spec_row_s) * n;
+      for (int i = tid; i < nin_s; i += kTailThreads) hinl[i] = ld_agent(&row[i]);
+    }
+    return;
+  }
   const bool have = have_s != 0;
   double f[9];
 #pragma unroll
@@ -915,7 +922,10 @@ __device__ void replay_inliers(const Pt *__restrict__ pts, int n, const int *cou
       base_s = acc;
     }
     __syncthreads();
-    if (take) res->inliers[woff[w] + before] = i;
+    if (take) {
+      res->inliers[woff[w] + before] = i;
+      if (hinl) hinl[woff[w] + before] = i;
+    }
     __syncthreads();
   }
   if (tid == 0) {

@@ -87,6 +87,8 @@ struct rs_f8_plan {
   // last run and copies S_RANSAC on demand.
   rsd::F8DevResult *h_slot[kSlots] = {};
   rsd::F8DevResult *h_slot_dev[kSlots] = {};
+  int *h_inl[kSlots] = {};      // pinned S_RANSAC per slot (cap_n ints), written by the tail
+  int *h_inl_dev[kSlots] = {};
   hipEvent_t ring[kEvRing][4] = {};  // count start/end; tail+solve launch start/end
   bool timed[kEvRing] = {};          // whether run r % kEvRing recorded its events
   int64_t runs = 0, last_H = 0;
@@ -163,9 +165,27 @@ static void plan_free(rs_f8_plan *p) {
   if (p->ts) (void)hipStreamDestroy(p->ts);
   for (auto &h : p->h_slot)
     if (h) (void)hipHostFree(h);
+  for (auto &h : p->h_inl)
+    if (h) (void)hipHostFree(h);
   for (auto &r : p->ring)
     for (auto &e : r)
       if (e) (void)hipEventDestroy(e);
+}
+
+// the pinned S_RANSAC buffers of the result slots, cap ints each (the tail writes the winner's
+// list through the host mapping; rs_f8_plan_result reads it without a copy)
+static hipError_t alloc_h_inl(rs_f8_plan *p, int64_t cap) {
+  hipError_t e = hipSuccess;
+  for (int k = 0; k < rs_f8_plan::kSlots; ++k) {
+    if (p->h_inl[k]) (void)hipHostFree(p->h_inl[k]);
+    p->h_inl[k] = nullptr;
+    p->h_inl_dev[k] = nullptr;
+    if (e == hipSuccess)
+      e = hipHostMalloc(reinterpret_cast<void **>(&p->h_inl[k]), sizeof(int) * static_cast<size_t>(cap));
+    if (e == hipSuccess)
+      e = hipHostGetDevicePointer(reinterpret_cast<void **>(&p->h_inl_dev[k]), p->h_inl[k], 0);
+  }
+  return e;
 }
 
 extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_plan **out) {
@@ -224,6 +244,7 @@ extern "C" int rs_f8_plan_create(rs_ctx *c, int64_t n, int64_t max_hyp, rs_f8_pl
     if (e == hipSuccess)
       e = hipHostGetDevicePointer(reinterpret_cast<void **>(&p->h_slot_dev[k]), p->h_slot[k], 0);
   }
+  if (e == hipSuccess) e = alloc_h_inl(p, p->cap_n);
   for (auto &r : p->ring)
     for (auto &ev : r)
       if (e == hipSuccess) e = hipEventCreate(&ev);
@@ -285,6 +306,7 @@ static int plan_retarget(rs_f8_plan *p, int64_t n) {
       if (e == hipSuccess)
         e = hipMalloc(&b.d_res, sizeof(rsd::F8DevResult) + sizeof(int64_t) * static_cast<size_t>(cap));
     }
+    if (e == hipSuccess) e = alloc_h_inl(p, cap);
     if (e != hipSuccess) {
       // the old buffers are gone: mark the plan empty (a later retarget reallocates) and let
       // the caller drop it (rs_f8_ransac_np destroys its cached plan)
@@ -474,6 +496,7 @@ static int plan_run(rs_f8_plan *p, int64_t H, int32_t mode, uint64_t seed, uint6
   ta.cnorm = b.d_cnorm;
   ta.res = b.d_res;
   ta.hres = p->h_slot_dev[slot];
+  ta.hinl = p->h_inl_dev[slot];
   if (p->overlap) {
     // the tail on ts right after this run's count; the next run's count does not wait for it
     HIP_TRY(hipEventRecord(p->ev_count[bi], ms));
@@ -598,8 +621,10 @@ extern "C" int rs_f8_plan_result(rs_f8_plan *p, rs_f8_result *out, int64_t *inli
   }
   if (n_inliers) *n_inliers = r->n_inliers;
   const int64_t k = std::min<int64_t>(cap, r->n_inliers);
-  if (inliers && k > 0) {  // S_RANSAC stays in HBM until asked for
-    if (r->inl_row >= 0) {   // the winner's select block kept it (int32 row)
+  if (inliers && k > 0) {
+    if (const int *h = p->h_inl[(p->runs - 1) % rs_f8_plan::kSlots]) {  // written by the tail
+      for (int64_t i = 0; i < k; ++i) inliers[i] = h[i];
+    } else if (r->inl_row >= 0) {   // the winner's select block kept it (int32 row)
       std::vector<int32_t> row(static_cast<size_t>(k));
       HIP_TRY(hipMemcpy(row.data(), p->last().d_spec + r->inl_row * p->n, sizeof(int32_t) * k,
                         hipMemcpyDeviceToHost));
