@@ -712,7 +712,10 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
   __shared__ int sh_evn;
   const int tid = threadIdx.x, lane = tid & 63;
   const int n1 = a.n1, n1p = (n1 + 1) & ~1;
-  uint16_t *st = dyn, *lo = dyn + n1p, *st2 = dyn + 2 * n1p, *lo2 = dyn + 3 * n1p;
+  // the list (state, member-range start) in LDS, compacted in place (4 n1p bytes: two chunks
+  // share a CU at every N; with a second pair of arrays as the compaction target, 8 n1p
+  // bytes, N = 10 000 took 82.3 KB and one chunk per CU -- C5's entry ran in two rounds)
+  uint16_t *st = dyn, *lo = dyn + n1p;
   const int c = blockIdx.x;
   const int64_t t0 = static_cast<int64_t>(c) * a.W;
   const int T = static_cast<int>(std::min<int64_t>(a.W, a.D - t0));
@@ -1047,6 +1050,7 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
         if (tid < m) st[tid] = static_cast<uint16_t>(sv);
         __syncthreads();
         const bool keep = tid < m && static_cast<uint16_t>(sv) != st[tid == 0 ? m - 1 : tid - 1];
+        const uint16_t lv = tid < m ? lo[tid] : 0;  // read before the barrier: written in place
         const uint64_t kb = __ballot(keep);
         if (lane == 0) sh_red[tid >> 6] = __popcll(kb);
         __syncthreads();
@@ -1057,25 +1061,14 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
           base += w < (tid >> 6) ? cw : 0;
           total += cw;
         }
-        if (keep) {
+        if (keep) {  // in place: o <= tid, and every read of st / lo is behind the barrier
           const int o = base + static_cast<int>(lane_rank(kb));
-          st2[o] = static_cast<uint16_t>(sv);
-          lo2[o] = lo[tid];
+          st[o] = static_cast<uint16_t>(sv);
+          lo[o] = lv;
         }
-        if (total == 0) {  // every trajectory in one state: one survivor covering every entry
-          if (tid == 0) {
-            st2[0] = static_cast<uint16_t>(sv);
-            lo2[0] = lo[0];
-          }
-          total = 1;
-        }
+        // every trajectory in one state: one survivor covering every entry (entry 0 holds it)
+        if (total == 0) total = 1;
         __syncthreads();
-        uint16_t *x = st;
-        st = st2;
-        st2 = x;
-        x = lo;
-        lo = lo2;
-        lo2 = x;
         m = total;
         s[0] = tid < m ? st[tid] : kSentinel;
         RSD_ETICK(3, 0);
@@ -1090,33 +1083,38 @@ __global__ __launch_bounds__(kEntryThreads, 4) void k_np_entry(EntryArgs a,
         if (q < m) st[q] = static_cast<uint16_t>(s[r]);
       }
       __syncthreads();
-      const int per = (m + kEntryThreads - 1) / kEntryThreads;
+      const int per = (m + kEntryThreads - 1) / kEntryThreads;  // <= kR (m <= kMaxN1)
       const int k0 = min(m, tid * per), k1 = min(m, k0 + per);
+      // the thread's kept entries (state << 16 | lo) in registers, then written in place once
+      // the scan's barriers have ordered every read before every write (o <= p)
       int cnt = 0;
-      for (int p = k0; p < k1; ++p) cnt += st[p] != st[p == 0 ? m - 1 : p - 1] ? 1 : 0;
+      uint32_t kmask = 0u, kv[kR];
+#pragma unroll
+      for (int j = 0; j < kR; ++j) {
+        const int p = k0 + j;
+        kv[j] = 0u;
+        if (p < k1) {
+          const uint16_t x = st[p];
+          if (x != st[p == 0 ? m - 1 : p - 1]) {
+            kmask |= 1u << j;
+            kv[j] = (static_cast<uint32_t>(x) << 16) | lo[p];
+            ++cnt;
+          }
+        }
+      }
       int total;
       int o = block_excl_scan(cnt, sh_red, &total);
-      for (int p = k0; p < k1; ++p) {
-        if (st[p] != st[p == 0 ? m - 1 : p - 1]) {
-          st2[o] = st[p];
-          lo2[o] = lo[p];
+#pragma unroll
+      for (int j = 0; j < kR; ++j) {
+        if ((kmask >> j) & 1u) {
+          st[o] = static_cast<uint16_t>(kv[j] >> 16);
+          lo[o] = static_cast<uint16_t>(kv[j] & 0xffffu);
           ++o;
         }
       }
-      if (total == 0) {  // every trajectory in one state: one survivor covering every entry
-        if (tid == 0) {
-          st2[0] = st[0];
-          lo2[0] = lo[0];
-        }
-        total = 1;
-      }
+      // every trajectory in one state: one survivor covering every entry (entry 0 holds it)
+      if (total == 0) total = 1;
       __syncthreads();
-      uint16_t *x = st;
-      st = st2;
-      st2 = x;
-      x = lo;
-      lo = lo2;
-      lo2 = x;
       m = total;
 #pragma unroll
       for (int r = 0; r < kR; ++r) {
@@ -2882,7 +2880,7 @@ int shard_kernel_attrs(int n1) {
                                 static_cast<int>(sizeof(uint32_t) * kPrefixAlloc)));
     jump = true;
   }
-  const int64_t lds = 8 * static_cast<int64_t>((n1 + 1) & ~1);
+  const int64_t lds = 4 * static_cast<int64_t>((n1 + 1) & ~1);  // k_np_entry: st, lo (uint16)
   if (lds > entry_lds) {
     HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(k_np_entry<false>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
@@ -3193,7 +3191,7 @@ int shard_enqueue_parse(rs_np_shard &w) {
   if ((st = sgrow(w.d_ev, w.cap_ev, w.Cr * w.ecap))) return st;
   HIP_TRY(hipMemsetAsync(w.d_err, 0, sizeof(int), s));
   const int Cr = static_cast<int>(w.Cr), Wc = static_cast<int>(w.Wc);
-  const int64_t lds = 8 * static_cast<int64_t>((w.n1 + 1) & ~1);
+  const int64_t lds = 4 * static_cast<int64_t>((w.n1 + 1) & ~1);  // k_np_entry: st, lo (uint16)
   long long *d_stats = nullptr;
 #ifdef RSAMD_DIAG
   // RSAMD_NP_STATS=<file>: per-chunk statistics of the entry kernel appended to <file>
