@@ -1070,21 +1070,36 @@ __device__ void pnp_select_block(const int *__restrict__ counts, int H,
   __shared__ int sm[2][16], si[2][16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   int bm[2] = {0, 0}, bi[2] = {0x7fffffff, 0x7fffffff};  // front-facing, mirrored
-  // 8 loads in flight per thread before the (order-free) max / first-index comparisons
-  for (int i0 = tid; i0 < H; i0 += 8 * 1024) {
-    int c[8], f[8];
+  // 8 loads of four counts in flight per thread before the (order-free) max / first-index
+  // comparisons (C3's 5e4 counts: two rounds of loads instead of seven; the select + inliers
+  // launch measured 20.8 -> 19.5 us); counts and flags sit at 256-byte aligned scratch offsets
+  const int H4 = H >> 2;
+  const int4 *c4 = reinterpret_cast<const int4 *>(counts);
+  const uchar4 *f4 = reinterpret_cast<const uchar4 *>(mirf);
+  for (int i0 = tid; i0 < H4; i0 += 8 * 1024) {
+    int4 c[8];
+    uchar4 f[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int i = i0 + u * 1024;
-      c[u] = i < H ? counts[i] : -1;
-      f[u] = mirf && i < H ? mirf[i] : 0;
+      c[u] = i < H4 ? c4[i] : make_int4(-1, -1, -1, -1);
+      f[u] = mirf && i < H4 ? f4[i] : make_uchar4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int i = i0 + u * 1024;
-      if (f[u]) sel_better(c[u], i, bm[1], bi[1]);
-      else sel_better(c[u], i, bm[0], bi[0]);
+      const int i = 4 * (i0 + u * 1024);
+      const int cc[4] = {c[u].x, c[u].y, c[u].z, c[u].w};
+      const int ff[4] = {f[u].x, f[u].y, f[u].z, f[u].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (ff[e]) sel_better(cc[e], i + e, bm[1], bi[1]);
+        else sel_better(cc[e], i + e, bm[0], bi[0]);
+      }
     }
+  }
+  for (int i = 4 * H4 + tid; i < H; i += 1024) {  // the last H mod 4 counts
+    if (mirf && mirf[i]) sel_better(counts[i], i, bm[1], bi[1]);
+    else sel_better(counts[i], i, bm[0], bi[0]);
   }
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
