@@ -242,8 +242,8 @@ int rs_f8_plan_counts(rs_f8_plan *plan, int32_t *counts, int64_t H);
 int rs_f8_plan_models(rs_f8_plan *plan, double *F_out, int64_t H);
 /* Device time (ms, HIP events on the plan's stream) of the counting kernel, the solve kernel
  * and the whole run: of the last run, or averaged over the last `last_n` runs (<= 64).  Runs
- * may be issued back to back (each owns a result header slot; S_RANSAC stays in HBM until
- * rs_f8_plan_result copies it); rs_f8_plan_result waits for the last. */
+ * may be issued back to back (each owns a result slot in pinned host memory: the header and
+ * S_RANSAC, written by the run's last kernel); rs_f8_plan_result waits for the last. */
 int rs_f8_plan_kernel_ms(rs_f8_plan *plan, double *score_ms, double *solve_ms, double *total_ms);
 /* Timing events recorded by rs_f8_plan_run (each is a marker packet between two kernels,
  * ~3.5 us on MI355X): level 0 none, 1 around the counting kernel (default), 2 also around the
