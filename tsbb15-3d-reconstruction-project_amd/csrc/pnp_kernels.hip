@@ -1190,6 +1190,31 @@ __device__ void pnp_inliers_block(const PPt *__restrict__ med, int m_med,
   for (int q = 0; q < 9; ++q) P[q] = res->R[q];
 #pragma unroll
   for (int q = 0; q < 3; ++q) P[9 + q] = res->t[q];
+  if (m_med <= 512 && m_high <= 512 && blockDim.x == 1024) {
+    // both sets in one pass: threads 0..511 test D_med's points, 512..1023 D_high's, each half
+    // compacted in point order by its own wave prefix (one barrier pair instead of two)
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = tid >> 9, i = tid & 511;
+    const int mm = half ? m_high : m_med;
+    const PPt *src = half ? high : med;
+    const bool take = have && i < mm && pnp_inlier_ref(P, src[i], thresh);
+    const unsigned long long bal = __ballot(take);
+    const int before = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) woff[w] = __popcll(bal);
+    __syncthreads();
+    if ((tid & 511) == 0) {
+      int acc = 0;
+      for (int q = 8 * half; q < 8 * half + 8; ++q) {
+        const int tq = woff[q];
+        woff[q] = acc;
+        acc += tq;
+      }
+      if (half) res->n_high = acc;
+      else res->n_med = acc;
+    }
+    __syncthreads();
+    if (take) res->inliers[(half ? m_med : 0) + woff[w] + before] = i;
+    return;
+  }
   ordered_compact(
       m_med, [&](int i) { return pnp_inlier_ref(P, med[i], thresh); }, have, res->inliers,
       &res->n_med, woff, &base_s);
